@@ -1,0 +1,265 @@
+#!/usr/bin/env python3
+"""bench.py -- topic matches/sec at 10M filters on 1..N MI355X (BASELINE.json).
+
+One step = one batch of publish topics matched against the device-resident
+index (tokenise + trie walk + exact lookup + CSR emission of every matched
+value), inputs already resident in HBM.  Default workload: config C3 (10M
+mixed-wildcard filters incl. $share dests, $SYS filters and root globals),
+1M-topic batches per GPU.  Multi-GPU = topic-sharded weak scaling: every rank
+holds a replica of the index and matches its own batch; there is no
+data-path collective.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3]
+       torchrun ... bench.py --gpus N  (one rank per GPU)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+CONFIGS = {
+    # name: (generator cfg, default filters, description)
+    "c1": (1, 10_000, "emqx_topic_index 10k filters (70% exact, 20% '+', 10% '#'), topics depth 4-6"),
+    "c2": (2, 1_000_000, "1M 'fleet/{id}/sensor/+' + 1k global '#' rules"),
+    "c2nm": (20, 1_000_000, "1M 'fleet/{id}/sensor/+' + 1k non-matching 'rules/{k}/#' globals"),
+    "c3": (3, 10_000_000, "10M mixed-wildcard filters incl. $share groups and '$SYS' exclusion"),
+}
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    p.add_argument("--filters", type=int, default=None)
+    p.add_argument("--batch", type=int, default=1_000_000, help="topics per GPU per step")
+    p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget")
+    p.add_argument("--cpu-threads", type=int, default=16)
+    p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--latency-batches", type=int, default=20)
+    p.add_argument("--frontier-sample", type=int, default=20_000)
+    return p.parse_args()
+
+
+def main():
+    a = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl")
+    torch.cuda.set_device(local)
+    dev = torch.device(f"cuda:{local}")
+
+    from emqx_amd import _native, workload as wl
+
+    gen_cfg, default_f, desc = CONFIGS[a.config]
+    nf = a.filters or default_f
+    B = a.batch
+
+    t = time.time()
+    fs = wl.filters(gen_cfg, nf)
+    t_gen = time.time() - t
+    log(f"[rank {rank}] generated {len(fs)} filters in {t_gen:.1f}s")
+
+    t = time.time()
+    ix = _native.Index(device=local, hint_keys=len(fs))
+    chunk = 2_000_000
+    for lo in range(0, len(fs), chunk):
+        part = fs.slice(lo, min(lo + chunk, len(fs)))
+        ix.apply(np.ones(len(part), np.uint8), part.blob, part.offs, part.vals)
+    t_compile = time.time() - t
+    stream = torch.cuda.current_stream().cuda_stream
+    t = time.time()
+    ix.sync(stream)
+    torch.cuda.synchronize()
+    t_upload = time.time() - t
+    st = ix.stats()
+    log(f"[rank {rank}] index: {st['n_keys']} keys, {st['n_nodes']} nodes, {st['n_edges']} edges, "
+        f"{st['n_words']} words, {st['device_bytes'] / 2**20:.0f} MiB HBM; compile {t_compile:.1f}s upload {t_upload:.2f}s")
+
+    ts = wl.topics(gen_cfg, nf, B, first=rank * B)
+    d_blob = torch.from_numpy(ts.blob).to(dev)
+    d_offs = torch.from_numpy(ts.offs.view(np.int64)).to(dev)
+    d_hit = torch.zeros(B + 1, dtype=torch.int64, device=dev)
+    d_err = torch.zeros(B, dtype=torch.uint8, device=dev)
+    d_out = torch.zeros(1, dtype=torch.int32, device=dev)
+
+    def step(cap):
+        ix.match_batch_dev(B, d_blob.data_ptr(), d_offs.data_ptr(), d_hit.data_ptr(), d_out.data_ptr(), cap,
+                           d_err.data_ptr(), stream)
+
+    step(0)
+    torch.cuda.synchronize()
+    total_hits = int(d_hit[-1].item())
+    d_out = torch.zeros(max(total_hits, 1), dtype=torch.int32, device=dev)
+    cap = total_hits
+    for _ in range(a.warmup):
+        step(cap)
+    torch.cuda.synchronize()
+    assert int(d_hit[-1].item()) == total_hits
+    assert not bool(d_err.any().item())
+
+    ix.profile(True)
+    ix.profile_read(reset=True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step(cap)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+    walk_ms, batch_ms, nb = ix.profile_read(reset=True)
+    ix.profile(False)
+    el_t = torch.tensor([el], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
+    el_max = float(el_t.item())
+
+    value = world * B * a.steps / el_max
+    ms_per_step = el_max / a.steps * 1e3
+    walk_avg_ms = walk_ms / max(nb, 1)
+    batch_avg_ms = batch_ms / max(nb, 1)
+
+    if rank != 0:
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+
+    sys.path.insert(0, str(ROOT / "oracle"))
+    from pyoracle import Oracle, frontier
+
+    # ---- oracle over the same filter set: roofline bytes, parity sample, CPU baseline
+    t = time.time()
+    o = Oracle()
+    o.apply(np.ones(len(fs), np.uint8), fs.blob, fs.offs, fs.vals)
+    o.prepare()
+    t_oracle = time.time() - t
+    log(f"oracle built in {t_oracle:.1f}s")
+
+    host_hit = d_hit.cpu().numpy().view(np.uint64)
+    host_out = d_out.cpu().numpy().view(np.uint32)
+    rng = np.random.default_rng(0x454D5158)
+    ns = min(a.frontier_sample, B)
+    idx = np.sort(rng.choice(B, ns, replace=False))
+    sample_items = [ts.item(int(i)) for i in idx]
+    sblob, soffs = _native.pack_strings(sample_items)
+    levels, states = frontier(o, sblob, soffs, nthreads=a.cpu_threads)
+    # parity on the sample: exact CSR equality with the oracle
+    cnt, _, ohit, ovals = o.match_batch(sblob, soffs, nthreads=a.cpu_threads)
+    mism = 0
+    for j, i in enumerate(idx):
+        g = host_out[int(host_hit[i]):int(host_hit[i + 1])]
+        e = ovals[int(ohit[j]):int(ohit[j + 1])]
+        mism += int(not np.array_equal(g, e))
+    # algorithmic bytes per walk launch (SURVEY.md 8d per topic, minus the 4 H
+    # the emit kernel writes):  8 L + 32 sum|F_l| + 4
+    L_total = int(np.count_nonzero(ts.blob[: int(ts.offs[-1])] == ord("/"))) + B
+    F_total = float(states.sum()) * B / ns
+    walk_bytes = 8 * L_total + 32 * F_total + 4 * B
+    full_bytes = walk_bytes + 4 * total_hits
+    achieved = walk_bytes / (walk_avg_ms * 1e-3) / 1e9
+
+    traffic = None
+    pmc = ROOT / "profiles" / f"pmc_{a.config}.json"
+    if pmc.exists():
+        try:
+            pj = json.loads(pmc.read_text())
+            if pj.get("filters") == nf and pj.get("batch") == B:
+                traffic = pj.get("walk_hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    # ---- p50/p99 batch latency: host topics in, hit lists back in host memory
+    lat = {}
+    for lb in sorted({min(4096, B), min(65536, B)}):
+        sub = ts.slice(0, lb)
+        xs = []
+        for k in range(a.latency_batches + 2):
+            t1 = time.perf_counter()
+            ix.match_batch(sub.blob, sub.offs)
+            xs.append((time.perf_counter() - t1) * 1e3)
+        xs = np.array(xs[2:])
+        lat[str(lb)] = {"p50_ms": round(float(np.percentile(xs, 50)), 3),
+                        "p99_ms": round(float(np.percentile(xs, 99)), 3)}
+
+    # ---- CPU baseline: the oracle (restated reference walk) on host threads
+    cpu = None
+    if not a.no_cpu and world == 1:
+        n1 = min(20_000, B)
+        probe = ts.slice(0, n1)
+        t1 = time.perf_counter()
+        o.match_batch(probe.blob, probe.offs, nthreads=a.cpu_threads, with_values=False)
+        r1 = n1 / (time.perf_counter() - t1)
+        n2 = int(min(B, max(n1, r1 * a.cpu_seconds)))
+        samp = ts.slice(0, n2)
+        t1 = time.perf_counter()
+        o.match_batch(samp.blob, samp.offs, nthreads=a.cpu_threads, with_values=False)
+        el_cpu = time.perf_counter() - t1
+        cpu = {"value": round(n2 / el_cpu, 1), "unit": "topic matches/s", "cores": a.cpu_threads, "kind": "port",
+               "sample": f"first {n2} topics of the same batch vs all {len(fs)} keys; oracle/tm_oracle.c "
+                         f"seek walker (emqx_trie_search restated) over a sorted key array, "
+                         f"{a.cpu_threads} pthreads, {el_cpu:.1f}s"}
+
+    res = {
+        "metric": "topic matches/sec at 10M filters" if a.config == "c3" else f"topic matches/sec ({a.config})",
+        "value": round(value, 1),
+        "unit": "topic matches/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8/u32",
+        "data": "synthetic (emqx_amd/csrc/workload.cpp, seed 0x454D5158+cfg)",
+        "config": {"workload": f"{a.config}: {desc}", "filters": len(fs), "topics_per_gpu_step": B,
+                   "global_batch": B * world, "parallelism": f"topic-sharded x{world} (trie replicated)"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "kernel": "k_walk_fast", "kernel_avg_ms": round(walk_avg_ms, 4),
+                     "algorithmic_bytes_per_launch": int(walk_bytes)},
+        "cpu_baseline": cpu,
+        "matched_ids_per_s": round(total_hits * world * a.steps / el_max, 1),
+        "hits_per_topic": round(total_hits / B, 3),
+        "batch_device_ms": round(batch_avg_ms, 4),
+        "batch_latency_host_ms": lat,
+        "parity_sample": {"topics": ns, "mismatches": mism},
+        "build": {"generate_s": round(t_gen, 1), "compile_s": round(t_compile, 1), "upload_s": round(t_upload, 2),
+                  "device_MiB": round(st["device_bytes"] / 2**20, 1), "nodes": st["n_nodes"],
+                  "edges": st["n_edges"], "words": st["n_words"]},
+        "full_path_GBps": round(full_bytes / (batch_avg_ms * 1e-3) / 1e9, 1),
+    }
+    if cpu:
+        res["speedup_vs_cpu"] = round(value / cpu["value"], 1)
+    print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,194 @@
+"""ctypes binding of ``libtmatch.so`` (the C ABI in ``include/tmatch.h``).
+
+This is the only way the Python host layer reaches the match path.  There is
+no fallback: if the library is missing or no GPU is visible, calls raise
+:class:`NativeUnavailable` (the product path never routes through a CPU
+implementation).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from pathlib import Path
+
+import numpy as np
+
+from .build import LIB_TMATCH
+
+TM_OK, TM_EINVAL, TM_ENOMEM, TM_EDEVICE, TM_ECAP = 0, -1, -2, -3, -4
+TM_OP_DELETE, TM_OP_INSERT = 0, 1
+TM_KEY_BINARY, TM_KEY_WORDS, TM_KEY_EMPTY_LIST = 0, 1, 2
+
+# every symbol include/tmatch.h declares (tests check the export table)
+EXPORTS = ("tm_create", "tm_destroy", "tm_apply_deltas", "tm_sync", "tm_match_batch",
+           "tm_match_batch_dev", "tm_first_batch", "tm_stats", "tm_profile_enable", "tm_profile_read",
+           "tm_last_error", "tm_abi_version")
+
+
+class NativeUnavailable(RuntimeError):
+    pass
+
+
+class TmError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"tmatch error {code}: {msg}")
+        self.code = code
+
+
+class tm_options(C.Structure):
+    _fields_ = [("device", C.c_int32), ("reserved", C.c_uint32), ("hint_keys", C.c_uint64)]
+
+
+class tm_stats_t(C.Structure):
+    _fields_ = [(n, C.c_uint64) for n in ("n_keys", "n_wild_keys", "n_exact_keys", "n_dead_keys",
+                                          "n_nodes", "n_edges", "n_words", "device_bytes",
+                                          "uploads", "patch_bytes")]
+
+
+_lib = None
+
+
+def load_library(path: Path | None = None):
+    """Load libtmatch.so (does not touch the GPU)."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = Path(path) if path else LIB_TMATCH
+    if not p.exists():
+        raise NativeUnavailable(f"{p} is not built (run emqx_amd.build.build_all())")
+    lib = C.CDLL(str(p))
+    vp, u64, u32, i32 = C.c_void_p, C.c_uint64, C.c_uint32, C.c_int
+    sig = {
+        "tm_create": (i32, [C.POINTER(tm_options), C.POINTER(vp)]),
+        "tm_destroy": (i32, [vp]),
+        "tm_apply_deltas": (i32, [vp, u64, vp, vp, vp, vp, vp]),
+        "tm_sync": (i32, [vp, vp]),
+        "tm_match_batch": (i32, [vp, u64, vp, vp, vp, vp, u64, vp]),
+        "tm_match_batch_dev": (i32, [vp, u64, vp, vp, vp, vp, u64, vp, vp]),
+        "tm_first_batch": (i32, [vp, u64, vp, vp, vp, vp]),
+        "tm_stats": (i32, [vp, C.POINTER(tm_stats_t)]),
+        "tm_profile_enable": (i32, [vp, i32]),
+        "tm_profile_read": (i32, [vp, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(u64), i32]),
+        "tm_last_error": (C.c_char_p, [vp]),
+        "tm_abi_version": (u32, []),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(lib, name)
+        f.restype, f.argtypes = res, args
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def _ptr(a: np.ndarray | None):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+def _gpu_present() -> bool:
+    try:
+        import torch
+        return torch.cuda.is_available()
+    except Exception:  # pragma: no cover
+        return False
+
+
+def pack_strings(items) -> tuple[np.ndarray, np.ndarray]:
+    """bytes-likes -> (uint8 blob, uint64 offsets[n+1])."""
+    items = [bytes(x) for x in items]
+    offs = np.zeros(len(items) + 1, dtype=np.uint64)
+    if items:
+        offs[1:] = np.cumsum([len(x) for x in items], dtype=np.uint64)
+    blob = np.frombuffer(b"".join(items) + b"\0" * 16, dtype=np.uint8)
+    return blob, offs
+
+
+class Index:
+    """Owning handle of one device-resident topic index (tm_index*)."""
+
+    def __init__(self, device: int = -1, hint_keys: int = 0):
+        if not _gpu_present():
+            raise NativeUnavailable("no HIP device visible: the topic index runs on the GPU only")
+        self._lib = load_library()
+        opts = tm_options(device, 0, hint_keys)
+        h = C.c_void_p()
+        rc = self._lib.tm_create(C.byref(opts), C.byref(h))
+        if rc != TM_OK:
+            raise TmError(rc, self._lib.tm_last_error(None).decode())
+        self._h = h
+
+    def _check(self, rc):
+        if rc != TM_OK:
+            raise TmError(rc, self._lib.tm_last_error(self._h).decode())
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.tm_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- deltas
+    def apply(self, ops: np.ndarray, blob: np.ndarray, offs: np.ndarray, values: np.ndarray,
+              flags: np.ndarray | None = None):
+        ops = np.ascontiguousarray(ops, dtype=np.uint8)
+        offs = np.ascontiguousarray(offs, dtype=np.uint64)
+        values = np.ascontiguousarray(values, dtype=np.uint32)
+        blob = np.ascontiguousarray(blob, dtype=np.uint8)
+        if flags is not None:
+            flags = np.ascontiguousarray(flags, dtype=np.uint8)
+        self._check(self._lib.tm_apply_deltas(self._h, len(ops), _ptr(ops), _ptr(blob), _ptr(offs),
+                                              _ptr(values), _ptr(flags)))
+
+    def sync(self, stream: int | None = None):
+        self._check(self._lib.tm_sync(self._h, stream))
+
+    # ---- matching (host buffers)
+    def match_batch(self, blob: np.ndarray, offs: np.ndarray, cap: int | None = None):
+        """-> (hit_offsets u64[n+1], values u32[total], err u8[n]) in traversal order."""
+        n = len(offs) - 1
+        blob = np.ascontiguousarray(blob, dtype=np.uint8)
+        offs = np.ascontiguousarray(offs, dtype=np.uint64)
+        hit = np.zeros(n + 1, dtype=np.uint64)
+        err = np.zeros(max(n, 1), dtype=np.uint8)
+        if cap is None:
+            cap = max(4 * n, 1024)
+        while True:
+            out = np.empty(max(cap, 1), dtype=np.uint32)
+            rc = self._lib.tm_match_batch(self._h, n, _ptr(blob), _ptr(offs), _ptr(hit), _ptr(out), cap, _ptr(err))
+            if rc == TM_ECAP:
+                cap = int(hit[n])
+                continue
+            self._check(rc)
+            return hit, out[: int(hit[n])], err[:n]
+
+    def first_batch(self, blob: np.ndarray, offs: np.ndarray):
+        """-> (value u32[n], found u8[n]: 1 hit, 0 none, 2 badarg)."""
+        n = len(offs) - 1
+        blob = np.ascontiguousarray(blob, dtype=np.uint8)
+        offs = np.ascontiguousarray(offs, dtype=np.uint64)
+        val = np.zeros(max(n, 1), dtype=np.uint32)
+        found = np.zeros(max(n, 1), dtype=np.uint8)
+        self._check(self._lib.tm_first_batch(self._h, n, _ptr(blob), _ptr(offs), _ptr(val), _ptr(found)))
+        return val[:n], found[:n]
+
+    # ---- matching (device buffers, e.g. torch tensors' data_ptr())
+    def match_batch_dev(self, n: int, d_blob: int, d_offs: int, d_hit: int, d_out: int, cap: int, d_err: int,
+                        stream: int | None = None):
+        self._check(self._lib.tm_match_batch_dev(self._h, n, d_blob, d_offs, d_hit, d_out, cap, d_err, stream))
+
+    def profile(self, enable: bool = True):
+        self._check(self._lib.tm_profile_enable(self._h, int(enable)))
+
+    def profile_read(self, reset: bool = True):
+        """-> (walk kernel ms, whole batch ms, batches) accumulated on the device."""
+        w, b, n = C.c_double(), C.c_double(), C.c_uint64()
+        self._check(self._lib.tm_profile_read(self._h, C.byref(w), C.byref(b), C.byref(n), int(reset)))
+        return w.value, b.value, n.value
+
+    def stats(self) -> dict:
+        s = tm_stats_t()
+        self._check(self._lib.tm_stats(self._h, C.byref(s)))
+        return {k: getattr(s, k) for k, _ in tm_stats_t._fields_}

@@ -1,0 +1,59 @@
+// tm_dev.h -- what the host side hands to the gfx950 kernels (tm_kernels.hip).
+#pragma once
+#include <stdint.h>
+#include <hip/hip_runtime.h>
+#include "tm_layout.h"
+
+namespace tmx {
+
+// Read-only view of the HBM-resident index (one snapshot per batch; patches
+// are applied in stream order before the batch's kernels run).
+struct DevIndex {
+    const VocabEntry *vocab; uint32_t vmask;
+    const uint8_t *wpool;
+    const Node *nodes;
+    const Edge *edges; uint32_t emask;
+    const uint32_t *vals;
+    const ExactEntry *exact; uint32_t xmask;
+    const uint32_t *wseq;
+};
+
+constexpr int FAST_L = 8;        // levels handled by the main walk kernel (LDS frontier)
+constexpr int MID_L = 32;        // levels handled by the list kernels with an LDS frontier
+constexpr int MAX_LEVELS = 65536;// MQTT topics are <= 65535 bytes
+constexpr int RCAP = 8;          // terminal ranges kept per topic before the re-walk path
+constexpr int DEEP_LANES = 64;   // lanes of the global-scratch (deep / overflow) kernels
+
+enum { L_MID = 0, L_DEEP = 1, L_OVF_MID = 2, L_OVF_DEEP = 3, L_COUNT = 4 };
+
+// Per-batch device scratch (grow-only, owned by the index).
+struct Workspace {
+    uint32_t *cnt;        // [n] hits per topic
+    uint32_t *nr;         // [n] ranges per topic (RCAP+1 = overflow)
+    uint2 *rng;           // [n * RCAP] (value offset, count)
+    uint32_t *lists;      // [L_COUNT * n] topic lists
+    uint32_t *list_n;     // [L_COUNT] list lengths
+    uint64_t *blk;        // [n / SCAN_TILE + 2] scan block sums / prefixes
+    uint32_t *deep_wid;   // [DEEP_LANES * MAX_LEVELS]
+    uint2 *deep_stk;      // [DEEP_LANES * (MAX_LEVELS + 1)]
+    uint64_t cap_n;
+};
+
+constexpr int SCAN_TILE = 1024;
+
+// Pipeline entry points (tm_kernels.hip).  All asynchronous on `s`.
+// phase 1: tokenise + walk + scan (hit offsets and total become valid)
+// phase 2: emit the values (+ re-walk overflowing topics)
+// ev_walk0/ev_walk1 (may be null): recorded right before / after the main walk kernel
+hipError_t launch_match_phase1(const DevIndex &ix, const Workspace &ws, uint64_t n, const uint8_t *bytes,
+                               const uint64_t *offs, uint64_t *hit_offs, uint8_t *err, hipStream_t s,
+                               hipEvent_t ev_walk0 = nullptr, hipEvent_t ev_walk1 = nullptr);
+hipError_t launch_match_phase2(const DevIndex &ix, const Workspace &ws, uint64_t n, const uint8_t *bytes,
+                               const uint64_t *offs, const uint64_t *hit_offs, uint32_t *out, uint64_t cap,
+                               hipStream_t s);
+hipError_t launch_first(const DevIndex &ix, const Workspace &ws, uint64_t n, const uint8_t *bytes,
+                        const uint64_t *offs, uint32_t *out_value, uint8_t *out_found, hipStream_t s);
+// scatter patch: dst[i] (absolute device address of a u32) = val[i]
+hipError_t launch_patch(const uint64_t *d_addr, const uint32_t *d_val, uint64_t n, hipStream_t s);
+
+}  // namespace tmx

@@ -1,0 +1,939 @@
+// tm_host.cpp -- host side of libtmatch: the index compiler, the delta applier
+// that keeps an HBM mirror of it current, and the C ABI of include/tmatch.h.
+//
+// The reference stores one ETS ordered_set key per (filter, ID)
+// (apps/emqx/src/emqx_topic_index.erl:50-62, key construction
+// apps/emqx/src/emqx_trie_search.erl:115-140).  Here every insert/delete is
+// applied to host copies of the flat tables described in tm_layout.h; each
+// table records which of its 4-byte words changed, and tm_sync() ships exactly
+// those words to HBM with one pinned H2D copy + one scatter kernel, in stream
+// order before the next batch.  Tables that grow or
+// rehash are re-uploaded whole.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <unordered_set>
+#include <vector>
+
+#include "../../include/tmatch.h"
+#include "tm_dev.h"
+#include "tm_layout.h"
+
+using namespace tmx;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+// ------------------------------------------------------------ dirty words
+
+struct Dirty {
+    std::vector<std::pair<uint64_t, uint64_t>> r;   // [lo, hi) in 4-byte words
+    bool all = true;
+    void add(uint64_t lo, uint64_t hi) {
+        if (all || lo >= hi) return;
+        if (!r.empty() && lo >= r.back().first && lo <= r.back().second) {
+            r.back().second = std::max(r.back().second, hi);
+            return;
+        }
+        r.push_back({lo, hi});
+    }
+    void set_all() { all = true; r.clear(); }
+    void clear() { all = false; r.clear(); }
+};
+
+// host vector + its HBM copy
+template <class T>
+struct Mirror {
+    std::vector<T> h;
+    T *d = nullptr;
+    uint64_t dcap = 0;   // elements allocated on the device
+    Dirty dirty;
+    void touch(uint64_t i, uint64_t n = 1) {
+        uint64_t lo = i * sizeof(T), hi = (i + n) * sizeof(T);
+        dirty.add(lo / 4, (hi + 3) / 4);
+    }
+    uint64_t bytes() const { return h.size() * sizeof(T); }
+};
+
+struct NodeAux {
+    uint32_t parent = NONE, wid = NONE, nlit = 0, hash_cap = 0, exact_cap = 0;
+    uint8_t is_plus = 0;
+};
+
+struct WordRef { const uint8_t *p; uint32_t n; int kind; };   // kind: 0 binary, 1 '+', 2 '#'
+
+}  // namespace
+
+struct tm_index {
+    std::mutex mu;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+
+    Mirror<VocabEntry> vocab; uint64_t vcount = 0;
+    Mirror<uint8_t> wpool;
+    Mirror<Node> nodes; std::vector<NodeAux> aux; std::vector<uint32_t> free_nodes; uint64_t live_nodes = 0;
+    Mirror<Edge> edges; uint64_t ecount = 0;
+    Mirror<uint32_t> vals; std::vector<uint32_t> free_blocks[33];
+    Mirror<ExactEntry> exact; std::vector<uint32_t> xcap; uint64_t xcount = 0;
+    Mirror<uint32_t> wseq;
+
+    std::unordered_set<std::string> dead;
+    uint64_t n_wild = 0, n_exact = 0;
+    uint64_t uploads = 0, patch_bytes = 0;
+
+    // patch staging
+    uint64_t *pin_addr = nullptr; uint32_t *pin_val = nullptr; uint64_t pin_cap = 0;
+    uint64_t *dev_addr = nullptr; uint32_t *dev_val = nullptr; uint64_t dev_pcap = 0;
+    hipEvent_t patch_done = nullptr; bool patch_pending = false;
+
+    // per-batch workspace
+    Workspace ws{};
+    uint64_t ws_cap = 0;
+
+    // host-API staging
+    uint8_t *pin_in = nullptr; uint64_t pin_in_cap = 0;
+    uint8_t *pin_out = nullptr; uint64_t pin_out_cap = 0;
+    uint8_t *d_topics = nullptr; uint64_t d_topics_cap = 0;
+    uint64_t *d_offs = nullptr; uint64_t d_offs_cap = 0;
+    uint64_t *d_hit = nullptr; uint64_t d_hit_cap = 0;
+    uint8_t *d_err = nullptr; uint64_t d_err_cap = 0;
+    uint32_t *d_out = nullptr; uint64_t d_out_cap = 0;
+
+    // diagnostics (tm_profile_*)
+    bool prof = false;
+    struct ProfEv { hipEvent_t b0, w0, w1, b1; };
+    std::vector<ProfEv> prof_pending, prof_free;
+    double prof_walk_ms = 0, prof_batch_ms = 0;
+    uint64_t prof_batches = 0;
+};
+
+namespace {
+
+int fail(tm_index *h, int code, const std::string &msg) {
+    if (h) h->err = msg;
+    g_last_error = msg;
+    return code;
+}
+
+#define HIPCHK(h, x)                                                                    \
+    do {                                                                                \
+        hipError_t e_ = (x);                                                            \
+        if (e_ != hipSuccess)                                                           \
+            return fail(h, TM_EDEVICE, std::string(#x ": ") + hipGetErrorString(e_));   \
+    } while (0)
+
+// ---------------------------------------------------------------- hashing
+
+uint64_t word_hash(const uint8_t *p, uint32_t n) {
+    uint64_t x = FNV_OFF;
+    for (uint32_t i = 0; i < n; i++) x = (x ^ p[i]) * FNV_PRIME;
+    return word_hash_finish(x, n);
+}
+
+uint32_t pow2_at_least(uint64_t x) {
+    uint64_t c = 16;
+    while (c < x) c <<= 1;
+    return (uint32_t)c;
+}
+
+// ------------------------------------------------------------------ vocab
+
+bool vocab_eq(tm_index *ix, const VocabEntry &e, uint64_t h, const uint8_t *p, uint32_t n) {
+    if (e.h_lo != (uint32_t)h || e.h_hi != (uint32_t)(h >> 32) || e.len != n) return false;
+    if (n <= VINL) {
+        uint32_t b[4] = {0, 0, 0, 0};
+        for (uint32_t i = 0; i < n; i++) b[i / 4] |= (uint32_t)p[i] << (8 * (i % 4));
+        return !memcmp(b, e.b, 16);
+    }
+    return !memcmp(ix->wpool.h.data() + e.b[0], p, n);
+}
+
+uint32_t vocab_find(tm_index *ix, const uint8_t *p, uint32_t n) {
+    const uint64_t h = word_hash(p, n);
+    const uint32_t mask = (uint32_t)ix->vocab.h.size() - 1;
+    for (uint32_t s = (uint32_t)h & mask;; s = (s + 1) & mask) {
+        const VocabEntry &e = ix->vocab.h[s];
+        if (e.wid == NONE) return NONE;
+        if (vocab_eq(ix, e, h, p, n)) return e.wid;
+    }
+}
+
+void vocab_place(std::vector<VocabEntry> &t, const VocabEntry &e) {
+    const uint32_t mask = (uint32_t)t.size() - 1;
+    uint64_t h = ((uint64_t)e.h_hi << 32) | e.h_lo;
+    for (uint32_t s = (uint32_t)h & mask;; s = (s + 1) & mask)
+        if (t[s].wid == NONE) { t[s] = e; return; }
+}
+
+VocabEntry empty_vocab() { VocabEntry e; memset(&e, 0, sizeof e); e.wid = NONE; return e; }
+
+void vocab_grow(tm_index *ix, uint64_t need) {
+    if (need * 2 <= ix->vocab.h.size()) return;
+    std::vector<VocabEntry> nt(pow2_at_least(need * 2), empty_vocab());
+    for (const VocabEntry &e : ix->vocab.h) if (e.wid != NONE) vocab_place(nt, e);
+    ix->vocab.h.swap(nt);
+    ix->vocab.dirty.set_all();
+}
+
+uint32_t vocab_intern(tm_index *ix, const uint8_t *p, uint32_t n) {
+    uint32_t w = vocab_find(ix, p, n);
+    if (w != NONE) return w;
+    vocab_grow(ix, ix->vcount + 1);
+    VocabEntry e = empty_vocab();
+    const uint64_t h = word_hash(p, n);
+    e.h_lo = (uint32_t)h; e.h_hi = (uint32_t)(h >> 32); e.len = n; e.wid = (uint32_t)ix->vcount;
+    if (n <= VINL) {
+        for (uint32_t i = 0; i < n; i++) e.b[i / 4] |= (uint32_t)p[i] << (8 * (i % 4));
+    } else {
+        uint64_t off = ix->wpool.h.size();
+        ix->wpool.h.resize(off + ((n + 3) & ~3u), 0);
+        memcpy(ix->wpool.h.data() + off, p, n);
+        ix->wpool.touch(off, (n + 3) & ~3u);
+        e.b[0] = (uint32_t)off;
+    }
+    const uint32_t mask = (uint32_t)ix->vocab.h.size() - 1;
+    for (uint32_t s = (uint32_t)h & mask;; s = (s + 1) & mask)
+        if (ix->vocab.h[s].wid == NONE) { ix->vocab.h[s] = e; ix->vocab.touch(s); break; }
+    ix->vcount++;
+    return e.wid;
+}
+
+// ------------------------------------------------------------------ edges
+
+Edge empty_edge() { return Edge{NONE, 0, 0, 0}; }
+
+uint32_t edge_find_slot(tm_index *ix, uint32_t parent, uint32_t wid) {
+    const uint32_t mask = (uint32_t)ix->edges.h.size() - 1;
+    for (uint32_t s = edge_slot(parent, wid, mask);; s = (s + 1) & mask) {
+        const Edge &e = ix->edges.h[s];
+        if (e.parent == NONE) return NONE;
+        if (e.parent == parent && e.wid == wid) return s;
+    }
+}
+
+void edge_grow(tm_index *ix, uint64_t need) {
+    if (need * 2 <= ix->edges.h.size()) return;
+    std::vector<Edge> nt(pow2_at_least(need * 2), empty_edge());
+    const uint32_t mask = (uint32_t)nt.size() - 1;
+    for (const Edge &e : ix->edges.h) {
+        if (e.parent == NONE) continue;
+        for (uint32_t s = edge_slot(e.parent, e.wid, mask);; s = (s + 1) & mask)
+            if (nt[s].parent == NONE) { nt[s] = e; break; }
+    }
+    ix->edges.h.swap(nt);
+    ix->edges.dirty.set_all();
+}
+
+void edge_insert(tm_index *ix, uint32_t parent, uint32_t wid, uint32_t child) {
+    edge_grow(ix, ix->ecount + 1);
+    const uint32_t mask = (uint32_t)ix->edges.h.size() - 1;
+    for (uint32_t s = edge_slot(parent, wid, mask);; s = (s + 1) & mask)
+        if (ix->edges.h[s].parent == NONE) {
+            ix->edges.h[s] = Edge{parent, wid, child, 0};
+            ix->edges.touch(s);
+            break;
+        }
+    ix->ecount++;
+}
+
+// linear probing, backward-shift deletion (no tombstones on the device side)
+void edge_erase(tm_index *ix, uint32_t parent, uint32_t wid) {
+    uint32_t i = edge_find_slot(ix, parent, wid);
+    if (i == NONE) return;
+    auto &t = ix->edges.h;
+    const uint32_t mask = (uint32_t)t.size() - 1;
+    for (uint32_t j = (i + 1) & mask; t[j].parent != NONE; j = (j + 1) & mask) {
+        uint32_t k = edge_slot(t[j].parent, t[j].wid, mask);
+        bool stays = (i <= j) ? (i < k && k <= j) : (i < k || k <= j);
+        if (!stays) { t[i] = t[j]; ix->edges.touch(i); i = j; }
+    }
+    t[i] = empty_edge();
+    ix->edges.touch(i);
+    ix->ecount--;
+}
+
+// ------------------------------------------------------------- value runs
+
+uint32_t cls_of(uint32_t cap) { uint32_t c = 0; while ((1u << c) < cap) c++; return c; }
+
+uint32_t val_alloc(tm_index *ix, uint32_t cap) {
+    auto &fl = ix->free_blocks[cls_of(cap)];
+    if (!fl.empty()) { uint32_t o = fl.back(); fl.pop_back(); return o; }
+    uint64_t o = ix->vals.h.size();
+    ix->vals.h.resize(o + cap, 0);
+    return (uint32_t)o;
+}
+
+void val_free(tm_index *ix, uint32_t off, uint32_t cap) {
+    if (cap) ix->free_blocks[cls_of(cap)].push_back(off);
+}
+
+// insert v into the sorted run (off, cnt) of capacity cap; false if present
+bool run_insert(tm_index *ix, uint32_t &off, uint32_t &cnt, uint32_t &cap, uint32_t v) {
+    uint32_t *b = ix->vals.h.data() + off;
+    uint32_t pos = (uint32_t)(std::lower_bound(b, b + cnt, v) - b);
+    if (pos < cnt && b[pos] == v) return false;
+    if (cnt == cap) {
+        uint32_t ncap = cap ? cap * 2 : 1;
+        uint32_t noff = val_alloc(ix, ncap);
+        memmove(ix->vals.h.data() + noff, ix->vals.h.data() + off, sizeof(uint32_t) * cnt);
+        val_free(ix, off, cap);
+        off = noff; cap = ncap;
+        ix->vals.touch(off, cnt);
+    }
+    uint32_t *r = ix->vals.h.data() + off;
+    memmove(r + pos + 1, r + pos, sizeof(uint32_t) * (cnt - pos));
+    r[pos] = v;
+    cnt++;
+    ix->vals.touch(off + pos, cnt - pos);
+    return true;
+}
+
+bool run_erase(tm_index *ix, uint32_t &off, uint32_t &cnt, uint32_t &cap, uint32_t v) {
+    uint32_t *b = ix->vals.h.data() + off;
+    uint32_t pos = (uint32_t)(std::lower_bound(b, b + cnt, v) - b);
+    if (pos >= cnt || b[pos] != v) return false;
+    memmove(b + pos, b + pos + 1, sizeof(uint32_t) * (cnt - pos - 1));
+    cnt--;
+    if (pos < cnt) ix->vals.touch(off + pos, cnt - pos);
+    if (!cnt) { val_free(ix, off, cap); off = 0; cap = 0; }
+    return true;
+}
+
+// ------------------------------------------------------------------ nodes
+
+uint32_t node_new(tm_index *ix, uint32_t parent, uint32_t wid, bool is_plus) {
+    uint32_t id;
+    if (!ix->free_nodes.empty()) { id = ix->free_nodes.back(); ix->free_nodes.pop_back(); }
+    else { id = (uint32_t)ix->nodes.h.size(); ix->nodes.h.emplace_back(); ix->aux.emplace_back(); }
+    Node nd; memset(&nd, 0, sizeof nd); nd.plus = NONE;
+    ix->nodes.h[id] = nd;
+    ix->nodes.touch(id);
+    NodeAux a; a.parent = parent; a.wid = wid; a.is_plus = is_plus;
+    ix->aux[id] = a;
+    ix->live_nodes++;
+    return id;
+}
+
+bool node_empty(tm_index *ix, uint32_t id) {
+    const Node &n = ix->nodes.h[id];
+    return n.plus == NONE && ix->aux[id].nlit == 0 && n.hash_cnt == 0 && n.exact_cnt == 0;
+}
+
+void node_prune(tm_index *ix, uint32_t id) {
+    while (id != ROOT && node_empty(ix, id)) {
+        NodeAux a = ix->aux[id];
+        if (a.is_plus) { ix->nodes.h[a.parent].plus = NONE; ix->nodes.touch(a.parent); }
+        else { edge_erase(ix, a.parent, a.wid); ix->aux[a.parent].nlit--; }
+        ix->free_nodes.push_back(id);
+        ix->live_nodes--;
+        id = a.parent;
+    }
+}
+
+// ------------------------------------------------------------ exact table
+
+ExactEntry empty_exact() { ExactEntry e; memset(&e, 0, sizeof e); e.nlev = NONE; return e; }
+
+uint64_t seq_hash(const std::vector<uint32_t> &w) {
+    uint64_t x = FNV_OFF;
+    for (uint32_t v : w) x = seq_hash_step(x, v);
+    return seq_hash_finish(x, (uint32_t)w.size());
+}
+
+bool exact_eq(tm_index *ix, const ExactEntry &e, uint64_t h, const std::vector<uint32_t> &w) {
+    if (e.h_lo != (uint32_t)h || e.h_hi != (uint32_t)(h >> 32) || e.nlev != w.size()) return false;
+    const uint32_t *s = w.size() <= XINL ? e.wids : ix->wseq.h.data() + e.seq_off;
+    return !memcmp(s, w.data(), sizeof(uint32_t) * w.size());
+}
+
+uint32_t exact_find_slot(tm_index *ix, uint64_t h, const std::vector<uint32_t> &w) {
+    const uint32_t mask = (uint32_t)ix->exact.h.size() - 1;
+    for (uint32_t s = (uint32_t)h & mask;; s = (s + 1) & mask) {
+        const ExactEntry &e = ix->exact.h[s];
+        if (e.nlev == NONE) return NONE;
+        if (exact_eq(ix, e, h, w)) return s;
+    }
+}
+
+void exact_grow(tm_index *ix, uint64_t need) {
+    if (need * 2 <= ix->exact.h.size()) return;
+    const uint32_t ncap = pow2_at_least(need * 2);
+    std::vector<ExactEntry> nt(ncap, empty_exact());
+    std::vector<uint32_t> nc(ncap, 0);
+    const uint32_t mask = ncap - 1;
+    for (size_t i = 0; i < ix->exact.h.size(); i++) {
+        const ExactEntry &e = ix->exact.h[i];
+        if (e.nlev == NONE) continue;
+        for (uint32_t s = e.h_lo & mask;; s = (s + 1) & mask)
+            if (nt[s].nlev == NONE) { nt[s] = e; nc[s] = ix->xcap[i]; break; }
+    }
+    ix->exact.h.swap(nt);
+    ix->xcap.swap(nc);
+    ix->exact.dirty.set_all();
+}
+
+void exact_erase_slot(tm_index *ix, uint32_t i) {
+    auto &t = ix->exact.h;
+    const uint32_t mask = (uint32_t)t.size() - 1;
+    for (uint32_t j = (i + 1) & mask; t[j].nlev != NONE; j = (j + 1) & mask) {
+        uint32_t k = t[j].h_lo & mask;
+        bool stays = (i <= j) ? (i < k && k <= j) : (i < k || k <= j);
+        if (!stays) { t[i] = t[j]; ix->xcap[i] = ix->xcap[j]; ix->exact.touch(i); i = j; }
+    }
+    t[i] = empty_exact();
+    ix->xcap[i] = 0;
+    ix->exact.touch(i);
+    ix->xcount--;
+}
+
+// --------------------------------------------------------------- key ops
+
+void split_words(const uint8_t *f, uint32_t len, std::vector<WordRef> &out) {
+    out.clear();
+    uint32_t s = 0;
+    for (uint32_t i = 0; i <= len; i++) {
+        if (i == len || f[i] == '/') {
+            uint32_t n = i - s;
+            int kind = (n == 1 && f[s] == '+') ? 1 : (n == 1 && f[s] == '#') ? 2 : 0;
+            out.push_back({f + s, n, kind});
+            s = i + 1;
+        }
+    }
+}
+
+std::string dead_key(const uint8_t *f, uint32_t len, uint32_t v, uint8_t flags) {
+    std::string k;
+    k.reserve(len + 5);
+    k.push_back((char)flags);
+    k.append(reinterpret_cast<const char *>(&v), 4);
+    k.append(reinterpret_cast<const char *>(f), len);
+    return k;
+}
+
+// one insert (ins = true) or delete of the key make_key(Filter, V)
+void key_op(tm_index *ix, bool ins, const uint8_t *f, uint32_t len, uint32_t v, uint8_t flags,
+            std::vector<WordRef> &w, std::vector<uint32_t> &wids) {
+    if (flags & TM_KEY_EMPTY_LIST) {   // [] never matches a topic (topics have >= 1 level)
+        auto k = dead_key(nullptr, 0, v, TM_KEY_EMPTY_LIST);
+        if (ins) ix->dead.insert(k); else ix->dead.erase(k);
+        return;
+    }
+    split_words(f, len, w);
+    bool wild = false;
+    for (auto &x : w) wild |= x.kind != 0;
+    if (!wild && !(flags & TM_KEY_WORDS)) {
+        // binary key (emqx_trie_search.erl:121-125) -> exact table keyed by wid sequence
+        wids.clear();
+        if (ins) {
+            for (auto &x : w) wids.push_back(vocab_intern(ix, x.p, x.n));
+            exact_grow(ix, ix->xcount + 1);
+        } else {
+            for (auto &x : w) {
+                uint32_t id = vocab_find(ix, x.p, x.n);
+                if (id == NONE) return;
+                wids.push_back(id);
+            }
+        }
+        const uint64_t h = seq_hash(wids);
+        uint32_t s = exact_find_slot(ix, h, wids);
+        if (s == NONE) {
+            if (!ins) return;
+            ExactEntry e = empty_exact();
+            e.h_lo = (uint32_t)h; e.h_hi = (uint32_t)(h >> 32); e.nlev = (uint32_t)wids.size();
+            if (wids.size() <= XINL) {
+                std::copy(wids.begin(), wids.end(), e.wids);
+            } else {
+                e.seq_off = (uint32_t)ix->wseq.h.size();
+                ix->wseq.h.insert(ix->wseq.h.end(), wids.begin(), wids.end());
+                ix->wseq.touch(e.seq_off, wids.size());
+            }
+            const uint32_t mask = (uint32_t)ix->exact.h.size() - 1;
+            for (s = (uint32_t)h & mask; ix->exact.h[s].nlev != NONE; s = (s + 1) & mask) {}
+            ix->exact.h[s] = e;
+            ix->xcap[s] = 0;
+            ix->xcount++;
+        }
+        ExactEntry &e = ix->exact.h[s];
+        if (ins) { if (run_insert(ix, e.val_off, e.val_cnt, ix->xcap[s], v)) ix->n_exact++; }
+        else if (run_erase(ix, e.val_off, e.val_cnt, ix->xcap[s], v)) {
+            ix->n_exact--;
+            if (!e.val_cnt) { exact_erase_slot(ix, s); return; }
+        }
+        ix->exact.touch(s);
+        return;
+    }
+    // word-list key.  '#' anywhere but last never matches (compare/3 has no
+    // clause for it, emqx_trie_search.erl:282-290 vs :341-348; emqx_topic.erl:110)
+    for (size_t i = 0; i + 1 < w.size(); i++)
+        if (w[i].kind == 2) {
+            auto k = dead_key(f, len, v, flags & TM_KEY_WORDS);
+            if (ins) ix->dead.insert(k); else ix->dead.erase(k);
+            return;
+        }
+    const bool hash_term = w.back().kind == 2;
+    const size_t end = hash_term ? w.size() - 1 : w.size();
+    uint32_t node = ROOT;
+    for (size_t i = 0; i < end; i++) {
+        if (w[i].kind == 1) {
+            uint32_t c = ix->nodes.h[node].plus;
+            if (c == NONE) {
+                if (!ins) return;
+                c = node_new(ix, node, NONE, true);
+                ix->nodes.h[node].plus = c;
+                ix->nodes.touch(node);
+            }
+            node = c;
+        } else {
+            uint32_t wid = ins ? vocab_intern(ix, w[i].p, w[i].n) : vocab_find(ix, w[i].p, w[i].n);
+            if (wid == NONE) return;
+            uint32_t s = edge_find_slot(ix, node, wid);
+            uint32_t c;
+            if (s == NONE) {
+                if (!ins) return;
+                c = node_new(ix, node, wid, false);
+                edge_insert(ix, node, wid, c);
+                ix->aux[node].nlit++;
+            } else {
+                c = ix->edges.h[s].child;
+            }
+            node = c;
+        }
+    }
+    Node &nd = ix->nodes.h[node];
+    NodeAux &a = ix->aux[node];
+    bool changed;
+    if (ins) changed = hash_term ? run_insert(ix, nd.hash_off, nd.hash_cnt, a.hash_cap, v)
+                                 : run_insert(ix, nd.exact_off, nd.exact_cnt, a.exact_cap, v);
+    else changed = hash_term ? run_erase(ix, nd.hash_off, nd.hash_cnt, a.hash_cap, v)
+                             : run_erase(ix, nd.exact_off, nd.exact_cnt, a.exact_cap, v);
+    if (!changed) return;
+    ix->nodes.touch(node);
+    if (ins) ix->n_wild++;
+    else { ix->n_wild--; node_prune(ix, node); }
+}
+
+// ------------------------------------------------------------- device side
+
+template <class T>
+int upload_full(tm_index *ix, Mirror<T> &m) {
+    uint64_t need = std::max<uint64_t>(m.h.size(), 1);
+    // rare (first upload, growth, rehash): drain every stream that may still
+    // read the old copy before touching it
+    HIPCHK(ix, hipDeviceSynchronize());
+    if (need > m.dcap) {
+        if (m.d) HIPCHK(ix, hipFree(m.d));
+        m.d = nullptr;
+        uint64_t cap = need + need / 2 + 16;
+        HIPCHK(ix, hipMalloc(&m.d, cap * sizeof(T)));
+        m.dcap = cap;
+    }
+    if (m.bytes()) {
+        HIPCHK(ix, hipMemcpy(m.d, m.h.data(), m.bytes(), hipMemcpyHostToDevice));
+    }
+    m.dirty.clear();
+    ix->uploads++;
+    return TM_OK;
+}
+
+template <class T>
+int collect(tm_index *ix, Mirror<T> &m, std::vector<uint64_t> &addr, std::vector<uint32_t> &val) {
+    if (m.h.size() > m.dcap) m.dirty.set_all();
+    if (!m.dirty.all) {
+        uint64_t words = 0;
+        for (auto &r : m.dirty.r) words += r.second - r.first;
+        if (words * 4 > m.bytes() / 2) m.dirty.set_all();   // cheaper to ship the table
+    }
+    if (m.dirty.all) return upload_full(ix, m);
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(m.h.data());
+    const uint64_t base = reinterpret_cast<uint64_t>(m.d);
+    const uint64_t limit = (m.bytes() + 3) / 4;
+    for (auto &r : m.dirty.r)
+        for (uint64_t i = r.first; i < r.second && i < limit; i++) {
+            addr.push_back(base + 4 * i);
+            uint32_t v = 0;
+            memcpy(&v, reinterpret_cast<const uint8_t *>(src) + 4 * i, std::min<uint64_t>(4, m.bytes() - 4 * i));
+            val.push_back(v);
+        }
+    m.dirty.clear();
+    return TM_OK;
+}
+
+int sync_locked(tm_index *ix, hipStream_t s) {
+    HIPCHK(ix, hipSetDevice(ix->device));
+    if (ix->patch_pending) { HIPCHK(ix, hipEventSynchronize(ix->patch_done)); ix->patch_pending = false; }
+    std::vector<uint64_t> addr;
+    std::vector<uint32_t> val;
+    int rc;
+    if ((rc = collect(ix, ix->vocab, addr, val))) return rc;
+    if ((rc = collect(ix, ix->wpool, addr, val))) return rc;
+    if ((rc = collect(ix, ix->nodes, addr, val))) return rc;
+    if ((rc = collect(ix, ix->edges, addr, val))) return rc;
+    if ((rc = collect(ix, ix->vals, addr, val))) return rc;
+    if ((rc = collect(ix, ix->exact, addr, val))) return rc;
+    if ((rc = collect(ix, ix->wseq, addr, val))) return rc;
+    const uint64_t n = addr.size();
+    if (!n) return TM_OK;
+    if (n > ix->pin_cap) {
+        if (ix->pin_addr) HIPCHK(ix, hipHostFree(ix->pin_addr));
+        if (ix->pin_val) HIPCHK(ix, hipHostFree(ix->pin_val));
+        ix->pin_cap = n + n / 2 + 1024;
+        HIPCHK(ix, hipHostMalloc(&ix->pin_addr, ix->pin_cap * 8, hipHostMallocDefault));
+        HIPCHK(ix, hipHostMalloc(&ix->pin_val, ix->pin_cap * 4, hipHostMallocDefault));
+    }
+    if (n > ix->dev_pcap) {
+        HIPCHK(ix, hipStreamSynchronize(s));
+        if (ix->dev_addr) HIPCHK(ix, hipFree(ix->dev_addr));
+        if (ix->dev_val) HIPCHK(ix, hipFree(ix->dev_val));
+        ix->dev_pcap = n + n / 2 + 1024;
+        HIPCHK(ix, hipMalloc(&ix->dev_addr, ix->dev_pcap * 8));
+        HIPCHK(ix, hipMalloc(&ix->dev_val, ix->dev_pcap * 4));
+    }
+    memcpy(ix->pin_addr, addr.data(), n * 8);
+    memcpy(ix->pin_val, val.data(), n * 4);
+    HIPCHK(ix, hipMemcpyAsync(ix->dev_addr, ix->pin_addr, n * 8, hipMemcpyHostToDevice, s));
+    HIPCHK(ix, hipMemcpyAsync(ix->dev_val, ix->pin_val, n * 4, hipMemcpyHostToDevice, s));
+    HIPCHK(ix, launch_patch(ix->dev_addr, ix->dev_val, n, s));
+    HIPCHK(ix, hipEventRecord(ix->patch_done, s));
+    ix->patch_pending = true;
+    ix->patch_bytes += n * 4;
+    ix->uploads++;
+    return TM_OK;
+}
+
+DevIndex dev_view(tm_index *ix) {
+    DevIndex d;
+    d.vocab = ix->vocab.d; d.vmask = (uint32_t)ix->vocab.h.size() - 1;
+    d.wpool = ix->wpool.d;
+    d.nodes = ix->nodes.d;
+    d.edges = ix->edges.d; d.emask = (uint32_t)ix->edges.h.size() - 1;
+    d.vals = ix->vals.d;
+    d.exact = ix->exact.d; d.xmask = (uint32_t)ix->exact.h.size() - 1;
+    d.wseq = ix->wseq.d;
+    return d;
+}
+
+template <class T>
+int grow_dev(tm_index *ix, T *&p, uint64_t &cap, uint64_t need) {
+    if (need <= cap && p) return TM_OK;
+    HIPCHK(ix, hipDeviceSynchronize());
+    if (p) HIPCHK(ix, hipFree(p));
+    p = nullptr;
+    cap = std::max<uint64_t>(need + need / 4, 64);
+    HIPCHK(ix, hipMalloc(&p, cap * sizeof(T)));
+    return TM_OK;
+}
+
+int ensure_ws(tm_index *ix, uint64_t n, hipStream_t s) {
+    Workspace &w = ix->ws;
+    if (!w.deep_wid) {
+        HIPCHK(ix, hipMalloc(&w.deep_wid, (uint64_t)DEEP_LANES * MAX_LEVELS * 4));
+        HIPCHK(ix, hipMalloc(&w.deep_stk, (uint64_t)DEEP_LANES * (MAX_LEVELS + 1) * 8));
+        HIPCHK(ix, hipMalloc(&w.list_n, L_COUNT * 4));
+    }
+    if (n <= ix->ws_cap && w.cnt) return TM_OK;
+    (void)s;
+    HIPCHK(ix, hipDeviceSynchronize());
+    if (w.cnt) { (void)hipFree(w.cnt); (void)hipFree(w.nr); (void)hipFree(w.rng); (void)hipFree(w.lists); (void)hipFree(w.blk); }
+    uint64_t c = std::max<uint64_t>(n + n / 4, 1024);
+    HIPCHK(ix, hipMalloc(&w.cnt, c * 4));
+    HIPCHK(ix, hipMalloc(&w.nr, c * 4));
+    HIPCHK(ix, hipMalloc(&w.rng, c * RCAP * 8));
+    HIPCHK(ix, hipMalloc(&w.lists, c * L_COUNT * 4));
+    HIPCHK(ix, hipMalloc(&w.blk, (c / SCAN_TILE + 4) * 8));
+    w.cap_n = c;
+    ix->ws_cap = c;
+    return TM_OK;
+}
+
+void init_tables(tm_index *ix, uint64_t hint) {
+    ix->vocab.h.assign(pow2_at_least(std::max<uint64_t>(hint, 64)), empty_vocab());
+    ix->edges.h.assign(pow2_at_least(std::max<uint64_t>(hint * 2, 64)), empty_edge());
+    ix->exact.h.assign(pow2_at_least(std::max<uint64_t>(hint * 2, 64)), empty_exact());
+    ix->xcap.assign(ix->exact.h.size(), 0);
+    ix->nodes.h.reserve(hint + 1);
+    node_new(ix, NONE, NONE, false);   // ROOT
+    ix->vals.h.reserve(hint + 16);
+}
+
+hipStream_t pick_stream(tm_index *ix, void *s) { return s ? reinterpret_cast<hipStream_t>(s) : ix->stream; }
+
+// events of one profiled batch (null set when profiling is off)
+int prof_begin(tm_index *ix, tm_index::ProfEv &ev, hipStream_t s) {
+    ev = {nullptr, nullptr, nullptr, nullptr};
+    if (!ix->prof) return TM_OK;
+    if (!ix->prof_free.empty()) { ev = ix->prof_free.back(); ix->prof_free.pop_back(); }
+    else {
+        HIPCHK(ix, hipEventCreate(&ev.b0)); HIPCHK(ix, hipEventCreate(&ev.w0));
+        HIPCHK(ix, hipEventCreate(&ev.w1)); HIPCHK(ix, hipEventCreate(&ev.b1));
+    }
+    HIPCHK(ix, hipEventRecord(ev.b0, s));
+    return TM_OK;
+}
+
+int prof_end(tm_index *ix, tm_index::ProfEv &ev, hipStream_t s) {
+    if (!ev.b0) return TM_OK;
+    HIPCHK(ix, hipEventRecord(ev.b1, s));
+    ix->prof_pending.push_back(ev);
+    return TM_OK;
+}
+
+}  // namespace
+
+// =================================================================== C ABI
+
+extern "C" {
+
+uint32_t tm_abi_version(void) { return (1u << 16) | 0u; }
+
+const char *tm_last_error(tm_index *h) { return h ? h->err.c_str() : g_last_error.c_str(); }
+
+int tm_create(const tm_options *opts, tm_index **out) {
+    if (!out) return fail(nullptr, TM_EINVAL, "tm_create: out is NULL");
+    *out = nullptr;
+    tm_index *ix = new (std::nothrow) tm_index();
+    if (!ix) return fail(nullptr, TM_ENOMEM, "tm_create: out of host memory");
+    int dev = opts ? opts->device : -1;
+    if (dev < 0) {
+        if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    }
+    ix->device = dev;
+    hipError_t e = hipSetDevice(dev);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&ix->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ix->patch_done, hipEventDisableTiming);
+    if (e != hipSuccess) {
+        std::string m = std::string("tm_create: ") + hipGetErrorString(e);
+        delete ix;
+        return fail(nullptr, TM_EDEVICE, m);
+    }
+    init_tables(ix, opts ? opts->hint_keys : 0);
+    *out = ix;
+    return TM_OK;
+}
+
+int tm_destroy(tm_index *ix) {
+    if (!ix) return TM_EINVAL;
+    (void)hipSetDevice(ix->device);
+    (void)hipStreamSynchronize(ix->stream);
+    void *bufs[] = {ix->vocab.d, ix->wpool.d, ix->nodes.d, ix->edges.d, ix->vals.d, ix->exact.d, ix->wseq.d,
+                    ix->dev_addr, ix->dev_val, ix->ws.cnt, ix->ws.nr, ix->ws.rng, ix->ws.lists, ix->ws.list_n,
+                    ix->ws.blk, ix->ws.deep_wid, ix->ws.deep_stk, ix->d_topics, ix->d_offs, ix->d_hit,
+                    ix->d_err, ix->d_out};
+    for (void *p : bufs) if (p) (void)hipFree(p);
+    void *pins[] = {ix->pin_addr, ix->pin_val, ix->pin_in, ix->pin_out};
+    for (void *p : pins) if (p) (void)hipHostFree(p);
+    (void)hipEventDestroy(ix->patch_done);
+    (void)hipStreamDestroy(ix->stream);
+    delete ix;
+    return TM_OK;
+}
+
+int tm_apply_deltas(tm_index *ix, uint64_t n, const uint8_t *ops, const uint8_t *fb, const uint64_t *fo,
+                    const uint32_t *values, const uint8_t *key_flags) {
+    if (!ix) return fail(nullptr, TM_EINVAL, "tm_apply_deltas: null handle");
+    if (n && (!ops || !fo || !values || (!fb && fo[n] != fo[0])))
+        return fail(ix, TM_EINVAL, "tm_apply_deltas: null buffer");
+    std::lock_guard<std::mutex> g(ix->mu);
+    for (uint64_t i = 0; i < n; i++)
+        if (ops[i] > TM_OP_INSERT || fo[i + 1] < fo[i] || fo[i + 1] - fo[i] > 0xFFFFFFFFull)
+            return fail(ix, TM_EINVAL, "tm_apply_deltas: bad op or offsets at " + std::to_string(i));
+    std::vector<WordRef> w;
+    std::vector<uint32_t> wids;
+    try {
+        for (uint64_t i = 0; i < n; i++)
+            key_op(ix, ops[i] == TM_OP_INSERT, fb + fo[i], (uint32_t)(fo[i + 1] - fo[i]), values[i],
+                   key_flags ? key_flags[i] : 0, w, wids);
+    } catch (const std::bad_alloc &) {
+        return fail(ix, TM_ENOMEM, "tm_apply_deltas: out of host memory");
+    }
+    return TM_OK;
+}
+
+int tm_sync(tm_index *ix, void *stream) {
+    if (!ix) return fail(nullptr, TM_EINVAL, "tm_sync: null handle");
+    std::lock_guard<std::mutex> g(ix->mu);
+    return sync_locked(ix, pick_stream(ix, stream));
+}
+
+int tm_match_batch_dev(tm_index *ix, uint64_t n, const uint8_t *bytes, const uint64_t *offs, uint64_t *hit_offs,
+                       uint32_t *out, uint64_t cap, uint8_t *err, void *stream) {
+    if (!ix) return fail(nullptr, TM_EINVAL, "tm_match_batch_dev: null handle");
+    if (!hit_offs || (n && (!offs || !bytes || !err))) return fail(ix, TM_EINVAL, "tm_match_batch_dev: null buffer");
+    if (n >= 0xFFFFFFFFull) return fail(ix, TM_EINVAL, "tm_match_batch_dev: batch too large");
+    std::lock_guard<std::mutex> g(ix->mu);
+    hipStream_t s = pick_stream(ix, stream);
+    int rc;
+    if ((rc = sync_locked(ix, s))) return rc;
+    if ((rc = ensure_ws(ix, n, s))) return rc;
+    const DevIndex d = dev_view(ix);
+    tm_index::ProfEv ev;
+    if ((rc = prof_begin(ix, ev, s))) return rc;
+    HIPCHK(ix, launch_match_phase1(d, ix->ws, n, bytes, offs, hit_offs, err, s, ev.w0, ev.w1));
+    HIPCHK(ix, launch_match_phase2(d, ix->ws, n, bytes, offs, hit_offs, out, out ? cap : 0, s));
+    return prof_end(ix, ev, s);
+}
+
+int tm_match_batch(tm_index *ix, uint64_t n, const uint8_t *tb, const uint64_t *to, uint64_t *out_hit,
+                   uint32_t *out_vals, uint64_t cap, uint8_t *out_err) {
+    if (!ix) return fail(nullptr, TM_EINVAL, "tm_match_batch: null handle");
+    if (!to || !out_hit || (n && !tb && to[n] != to[0])) return fail(ix, TM_EINVAL, "tm_match_batch: null buffer");
+    if (n >= 0xFFFFFFFFull) return fail(ix, TM_EINVAL, "tm_match_batch: batch too large");
+    std::lock_guard<std::mutex> g(ix->mu);
+    HIPCHK(ix, hipSetDevice(ix->device));
+    hipStream_t s = ix->stream;
+    int rc;
+    if ((rc = sync_locked(ix, s))) return rc;
+    if ((rc = ensure_ws(ix, n, s))) return rc;
+    const uint64_t b0 = to[0], nbytes = to[n] - b0;
+    const uint64_t in_need = nbytes + 16 + (n + 1) * 8;
+    if (in_need > ix->pin_in_cap) {
+        HIPCHK(ix, hipStreamSynchronize(s));
+        if (ix->pin_in) HIPCHK(ix, hipHostFree(ix->pin_in));
+        ix->pin_in_cap = in_need + in_need / 4;
+        HIPCHK(ix, hipHostMalloc(&ix->pin_in, ix->pin_in_cap, hipHostMallocDefault));
+    }
+    uint64_t *pin_offs = reinterpret_cast<uint64_t *>(ix->pin_in);
+    uint8_t *pin_bytes = ix->pin_in + (n + 1) * 8;
+    for (uint64_t i = 0; i <= n; i++) pin_offs[i] = to[i] - b0;
+    if (nbytes) memcpy(pin_bytes, tb + b0, nbytes);
+    if ((rc = grow_dev(ix, ix->d_topics, ix->d_topics_cap, nbytes + 16))) return rc;
+    if ((rc = grow_dev(ix, ix->d_offs, ix->d_offs_cap, n + 1))) return rc;
+    if ((rc = grow_dev(ix, ix->d_hit, ix->d_hit_cap, n + 1))) return rc;
+    if ((rc = grow_dev(ix, ix->d_err, ix->d_err_cap, n + 1))) return rc;
+    HIPCHK(ix, hipMemcpyAsync(ix->d_offs, pin_offs, (n + 1) * 8, hipMemcpyHostToDevice, s));
+    if (nbytes) HIPCHK(ix, hipMemcpyAsync(ix->d_topics, pin_bytes, nbytes, hipMemcpyHostToDevice, s));
+    const DevIndex d = dev_view(ix);
+    HIPCHK(ix, launch_match_phase1(d, ix->ws, n, ix->d_topics, ix->d_offs, ix->d_hit, ix->d_err, s));
+    // total hits -> size the output (one small D2H + sync; the host API blocks anyway)
+    if (ix->pin_out_cap < 64) {
+        if (ix->pin_out) HIPCHK(ix, hipHostFree(ix->pin_out));
+        ix->pin_out_cap = 1 << 20;
+        HIPCHK(ix, hipHostMalloc(&ix->pin_out, ix->pin_out_cap, hipHostMallocDefault));
+    }
+    HIPCHK(ix, hipMemcpyAsync(ix->pin_out, ix->d_hit + n, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(ix, hipStreamSynchronize(s));
+    uint64_t total;
+    memcpy(&total, ix->pin_out, 8);
+    const uint64_t keep = std::min(total, out_vals ? cap : 0);
+    if ((rc = grow_dev(ix, ix->d_out, ix->d_out_cap, std::max<uint64_t>(keep, 1)))) return rc;
+    HIPCHK(ix, launch_match_phase2(d, ix->ws, n, ix->d_topics, ix->d_offs, ix->d_hit, ix->d_out, keep, s));
+    const uint64_t out_need = (n + 1) * 8 + keep * 4 + n + 16;
+    if (out_need > ix->pin_out_cap) {
+        HIPCHK(ix, hipStreamSynchronize(s));
+        HIPCHK(ix, hipHostFree(ix->pin_out));
+        ix->pin_out_cap = out_need + out_need / 4;
+        HIPCHK(ix, hipHostMalloc(&ix->pin_out, ix->pin_out_cap, hipHostMallocDefault));
+    }
+    uint8_t *po = ix->pin_out;
+    HIPCHK(ix, hipMemcpyAsync(po, ix->d_hit, (n + 1) * 8, hipMemcpyDeviceToHost, s));
+    if (keep) HIPCHK(ix, hipMemcpyAsync(po + (n + 1) * 8, ix->d_out, keep * 4, hipMemcpyDeviceToHost, s));
+    if (n) HIPCHK(ix, hipMemcpyAsync(po + (n + 1) * 8 + keep * 4, ix->d_err, n, hipMemcpyDeviceToHost, s));
+    HIPCHK(ix, hipStreamSynchronize(s));
+    memcpy(out_hit, po, (n + 1) * 8);
+    if (keep) memcpy(out_vals, po + (n + 1) * 8, keep * 4);
+    if (out_err && n) memcpy(out_err, po + (n + 1) * 8 + keep * 4, n);
+    return (out_vals && total > cap) ? TM_ECAP : TM_OK;
+}
+
+int tm_first_batch(tm_index *ix, uint64_t n, const uint8_t *tb, const uint64_t *to, uint32_t *out_value,
+                   uint8_t *out_found) {
+    if (!ix) return fail(nullptr, TM_EINVAL, "tm_first_batch: null handle");
+    if (!to || !out_value || !out_found || (n && !tb && to[n] != to[0]))
+        return fail(ix, TM_EINVAL, "tm_first_batch: null buffer");
+    if (n >= 0xFFFFFFFFull) return fail(ix, TM_EINVAL, "tm_first_batch: batch too large");
+    std::lock_guard<std::mutex> g(ix->mu);
+    HIPCHK(ix, hipSetDevice(ix->device));
+    hipStream_t s = ix->stream;
+    int rc;
+    if ((rc = sync_locked(ix, s))) return rc;
+    if ((rc = ensure_ws(ix, n, s))) return rc;
+    const uint64_t b0 = to[0], nbytes = to[n] - b0;
+    const uint64_t in_need = nbytes + 16 + (n + 1) * 8;
+    if (in_need > ix->pin_in_cap) {
+        HIPCHK(ix, hipStreamSynchronize(s));
+        if (ix->pin_in) HIPCHK(ix, hipHostFree(ix->pin_in));
+        ix->pin_in_cap = in_need + in_need / 4;
+        HIPCHK(ix, hipHostMalloc(&ix->pin_in, ix->pin_in_cap, hipHostMallocDefault));
+    }
+    uint64_t *pin_offs = reinterpret_cast<uint64_t *>(ix->pin_in);
+    uint8_t *pin_bytes = ix->pin_in + (n + 1) * 8;
+    for (uint64_t i = 0; i <= n; i++) pin_offs[i] = to[i] - b0;
+    if (nbytes) memcpy(pin_bytes, tb + b0, nbytes);
+    if ((rc = grow_dev(ix, ix->d_topics, ix->d_topics_cap, nbytes + 16))) return rc;
+    if ((rc = grow_dev(ix, ix->d_offs, ix->d_offs_cap, n + 1))) return rc;
+    if ((rc = grow_dev(ix, ix->d_out, ix->d_out_cap, n + 1))) return rc;
+    if ((rc = grow_dev(ix, ix->d_err, ix->d_err_cap, n + 1))) return rc;
+    HIPCHK(ix, hipMemcpyAsync(ix->d_offs, pin_offs, (n + 1) * 8, hipMemcpyHostToDevice, s));
+    if (nbytes) HIPCHK(ix, hipMemcpyAsync(ix->d_topics, pin_bytes, nbytes, hipMemcpyHostToDevice, s));
+    HIPCHK(ix, launch_first(dev_view(ix), ix->ws, n, ix->d_topics, ix->d_offs, ix->d_out, ix->d_err, s));
+    const uint64_t out_need = n * 5 + 16;
+    if (out_need > ix->pin_out_cap) {
+        HIPCHK(ix, hipStreamSynchronize(s));
+        if (ix->pin_out) HIPCHK(ix, hipHostFree(ix->pin_out));
+        ix->pin_out_cap = out_need + out_need / 4;
+        HIPCHK(ix, hipHostMalloc(&ix->pin_out, ix->pin_out_cap, hipHostMallocDefault));
+    }
+    if (n) {
+        HIPCHK(ix, hipMemcpyAsync(ix->pin_out, ix->d_out, n * 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(ix, hipMemcpyAsync(ix->pin_out + n * 4, ix->d_err, n, hipMemcpyDeviceToHost, s));
+    }
+    HIPCHK(ix, hipStreamSynchronize(s));
+    if (n) {
+        memcpy(out_value, ix->pin_out, n * 4);
+        memcpy(out_found, ix->pin_out + n * 4, n);
+    }
+    return TM_OK;
+}
+
+int tm_profile_enable(tm_index *ix, int enable) {
+    if (!ix) return fail(nullptr, TM_EINVAL, "tm_profile_enable: null handle");
+    std::lock_guard<std::mutex> g(ix->mu);
+    ix->prof = enable != 0;
+    return TM_OK;
+}
+
+int tm_profile_read(tm_index *ix, double *walk_ms, double *batch_ms, uint64_t *batches, int reset) {
+    if (!ix) return fail(nullptr, TM_EINVAL, "tm_profile_read: null handle");
+    std::lock_guard<std::mutex> g(ix->mu);
+    for (auto &ev : ix->prof_pending) {
+        HIPCHK(ix, hipEventSynchronize(ev.b1));
+        float w = 0, b = 0;
+        if (ev.w0) { HIPCHK(ix, hipEventElapsedTime(&w, ev.w0, ev.w1)); }
+        HIPCHK(ix, hipEventElapsedTime(&b, ev.b0, ev.b1));
+        ix->prof_walk_ms += w; ix->prof_batch_ms += b; ix->prof_batches++;
+        ix->prof_free.push_back(ev);
+    }
+    ix->prof_pending.clear();
+    if (walk_ms) *walk_ms = ix->prof_walk_ms;
+    if (batch_ms) *batch_ms = ix->prof_batch_ms;
+    if (batches) *batches = ix->prof_batches;
+    if (reset) { ix->prof_walk_ms = ix->prof_batch_ms = 0; ix->prof_batches = 0; }
+    return TM_OK;
+}
+
+int tm_stats(tm_index *ix, tm_stats_t *o) {
+    if (!ix || !o) return fail(ix, TM_EINVAL, "tm_stats: null argument");
+    std::lock_guard<std::mutex> g(ix->mu);
+    memset(o, 0, sizeof *o);
+    o->n_wild_keys = ix->n_wild;
+    o->n_exact_keys = ix->n_exact;
+    o->n_dead_keys = ix->dead.size();
+    o->n_keys = ix->n_wild + ix->n_exact + ix->dead.size();
+    o->n_nodes = ix->live_nodes;
+    o->n_edges = ix->ecount;
+    o->n_words = ix->vcount;
+    o->device_bytes = ix->vocab.dcap * sizeof(VocabEntry) + ix->wpool.dcap + ix->nodes.dcap * sizeof(Node) +
+                      ix->edges.dcap * sizeof(Edge) + ix->vals.dcap * 4 + ix->exact.dcap * sizeof(ExactEntry) +
+                      ix->wseq.dcap * 4;
+    o->uploads = ix->uploads;
+    o->patch_bytes = ix->patch_bytes;
+    return TM_OK;
+}
+
+}  // extern "C"

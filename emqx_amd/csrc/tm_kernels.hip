@@ -1,0 +1,595 @@
+// tm_kernels.hip -- gfx950 kernels of the topic-match pipeline.
+//
+// One publish topic = one unit of work (the unit of emqx_topic_index:matches/3,
+// apps/emqx/src/emqx_trie_search.erl:182-226).  A batch of topics is matched in
+// two phases on one HIP stream:
+//
+//   phase 1  k_walk_fast     one lane per topic: tokenise on '/', look every
+//                            level up in the vocab (hash + byte verification),
+//                            then walk the trie as an NFA depth first
+//                            ('#' terminal, '+' subtree, literal subtree -- the
+//                            reference's term order, so hits come out in
+//                            traversal order without a sort), then the exact
+//                            (binary-key) table.  Hits are recorded as value
+//                            ranges; the pending literal branch of every level
+//                            and the level word ids live in LDS.
+//            k_walk_list     the same for topics deeper than FAST_L (LDS, 32
+//                            levels) or MID_L (global scratch), driven by
+//                            device-side lists (no host round trip).
+//            k_scan_*        exclusive scan of per-topic hit counts -> CSR offsets.
+//   phase 2  k_emit          wave-cooperative load-balanced copy of the value
+//                            ranges into the CSR (coalesced stores).
+//            k_rewalk_list   topics with more than RCAP ranges are walked again
+//                            and write their values directly.
+//
+// Integer/byte work only; the path is HBM-latency bound, so the
+// design goal is many independent loads in flight per CU, not MFMA.
+#include "tm_dev.h"
+
+namespace tmx {
+
+// ----------------------------------------------------------------- helpers
+
+__device__ __forceinline__ uint4 ld4(const void *p) { return *reinterpret_cast<const uint4 *>(p); }
+
+struct WordAcc {
+    uint64_t h;
+    uint32_t len, b0, b1, b2, b3;
+    uint64_t start;
+    __device__ __forceinline__ void reset(uint64_t s) {
+        h = FNV_OFF; len = 0; b0 = b1 = b2 = b3 = 0; start = s;
+    }
+    __device__ __forceinline__ void push(uint32_t c) {
+        h = (h ^ c) * FNV_PRIME;
+        uint32_t v = c << ((len & 3) * 8);
+        if (len < 4) b0 |= v; else if (len < 8) b1 |= v; else if (len < 12) b2 |= v; else if (len < 16) b3 |= v;
+        len++;
+    }
+};
+
+__device__ bool bytes_eq(const uint8_t *a, const uint8_t *b, uint32_t n) {
+    for (uint32_t i = 0; i < n; i++) if (a[i] != b[i]) return false;
+    return true;
+}
+
+// vocab: word -> wid, exact by construction (64-bit hash, then length and bytes)
+__device__ uint32_t vocab_find(const DevIndex &ix, const WordAcc &w, const uint8_t *blob) {
+    const uint64_t h = word_hash_finish(w.h, w.len);
+    uint32_t slot = (uint32_t)h & ix.vmask;
+    for (;;) {
+        const uint4 *e = reinterpret_cast<const uint4 *>(ix.vocab + slot);
+        uint4 a = e[0], b = e[1];
+        if (a.z == NONE) return NONE;
+        if (a.x == (uint32_t)h && a.y == (uint32_t)(h >> 32) && a.w == w.len) {
+            if (w.len <= VINL) {
+                if (b.x == w.b0 && b.y == w.b1 && b.z == w.b2 && b.w == w.b3) return a.z;
+            } else if (bytes_eq(ix.wpool + b.x, blob + w.start, w.len)) {
+                return a.z;
+            }
+        }
+        slot = (slot + 1) & ix.vmask;
+    }
+}
+
+__device__ __forceinline__ uint32_t edge_find(const DevIndex &ix, uint32_t parent, uint32_t wid) {
+    uint32_t slot = edge_slot(parent, wid, ix.emask);
+    for (;;) {
+        uint4 e = ld4(ix.edges + slot);
+        if (e.x == parent && e.y == wid) return e.z;
+        if (e.x == NONE) return NONE;
+        slot = (slot + 1) & ix.emask;
+    }
+}
+
+// ------------------------------------------------------- frontier storage
+
+// LDS frontier: wid[level] and the pending literal child of each level,
+// laid out [level][thread] so that any mix of levels is bank-conflict free.
+template <int ML>
+struct LdsStore {
+    static constexpr uint32_t maxl = ML;
+    uint32_t *wid, *pend;
+    uint32_t stride;
+    uint64_t mask;
+    __device__ __forceinline__ uint32_t get_wid(uint32_t l) const { return wid[l * stride]; }
+    __device__ __forceinline__ void set_wid(uint32_t l, uint32_t w) { wid[l * stride] = w; }
+    __device__ __forceinline__ void reset() { mask = 0; }
+    __device__ __forceinline__ void push(uint32_t l, uint32_t node) {
+        pend[l * stride] = node; mask |= 1ull << l;
+    }
+    __device__ __forceinline__ bool pop(uint32_t &l, uint32_t &node) {
+        if (!mask) return false;
+        l = 63u - (uint32_t)__clzll(mask);
+        mask &= ~(1ull << l);
+        node = pend[l * stride];
+        return true;
+    }
+};
+
+// Global-scratch frontier for arbitrarily deep topics (one slot per lane).
+struct GlobalStore {
+    static constexpr uint32_t maxl = MAX_LEVELS;
+    uint32_t *wid;
+    uint2 *stk;
+    uint32_t top;
+    __device__ __forceinline__ uint32_t get_wid(uint32_t l) const { return wid[l]; }
+    __device__ __forceinline__ void set_wid(uint32_t l, uint32_t w) { wid[l] = w; }
+    __device__ __forceinline__ void reset() { top = 0; }
+    __device__ __forceinline__ void push(uint32_t l, uint32_t node) { stk[top++] = make_uint2(l, node); }
+    __device__ __forceinline__ bool pop(uint32_t &l, uint32_t &node) {
+        if (!top) return false;
+        uint2 e = stk[--top]; l = e.x; node = e.y;
+        return true;
+    }
+};
+
+// ---------------------------------------------------------- tokenisation
+
+enum { RC_OK = 0, RC_BADARG = 1, RC_DEEP = 2 };
+
+// topic_words/1 (emqx_trie_search.erl:369-378): split on '/', a level that is
+// exactly '+' or '#' is badarg; level words are resolved to wids.  Also
+// computes base_init's '$' flag (:160-163) and the exact-key hash.
+template <class S>
+__device__ int tokenize(const DevIndex &ix, const uint8_t *blob, uint64_t beg, uint64_t end, S &st,
+                        uint32_t &L, bool &dollar, uint64_t &xh, bool &all_found) {
+    WordAcc w; w.reset(beg);
+    uint32_t lev = 0;
+    all_found = true; dollar = false; xh = FNV_OFF;
+    auto finish = [&]() -> int {
+        if (w.len == 1 && (w.b0 == '+' || w.b0 == '#')) return RC_BADARG;
+        if (lev >= S::maxl) return RC_DEEP;
+        if (lev == 0 && w.len >= 1 && (w.b0 & 0xFF) == '$') dollar = true;
+        uint32_t wid = vocab_find(ix, w, blob);
+        st.set_wid(lev, wid);
+        all_found &= wid != NONE;
+        xh = seq_hash_step(xh, wid);
+        lev++;
+        return RC_OK;
+    };
+    for (uint64_t p = beg & ~3ull; p < end; p += 4) {
+        uint32_t word = *reinterpret_cast<const uint32_t *>(blob + p);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            uint64_t q = p + k;
+            if (q >= beg && q < end) {
+                uint32_t c = (word >> (8 * k)) & 0xFFu;
+                if (c == '/') {
+                    int rc = finish();
+                    if (rc) return rc;
+                    w.reset(q + 1);
+                } else {
+                    w.push(c);
+                }
+            }
+        }
+    }
+    int rc = finish();
+    if (rc) return rc;
+    L = lev;
+    xh = seq_hash_finish(xh, L);
+    return RC_OK;
+}
+
+__device__ uint32_t count_levels(const uint8_t *blob, uint64_t beg, uint64_t end) {
+    uint32_t n = 1;
+    for (uint64_t q = beg; q < end; q++) n += blob[q] == '/';
+    return n;
+}
+
+// match_topics/4 (emqx_trie_search.erl:381-389): binary keys equal to the topic
+template <class S>
+__device__ void exact_find(const DevIndex &ix, uint64_t xh, uint32_t L, const S &st, uint32_t &off, uint32_t &cnt) {
+    cnt = 0; off = 0;
+    uint32_t slot = (uint32_t)xh & ix.xmask;
+    for (;;) {
+        const uint4 *e = reinterpret_cast<const uint4 *>(ix.exact + slot);
+        uint4 a = e[0];
+        if (a.z == NONE) return;
+        if (a.x == (uint32_t)xh && a.y == (uint32_t)(xh >> 32) && a.z == L) {
+            uint4 b = e[1], c = e[2], d = e[3];
+            bool eq = true;
+            if (L <= XINL) {
+                const uint32_t iw[XINL] = {b.z, b.w, c.x, c.y, c.z, c.w, d.x, d.y, d.z, d.w};
+#pragma unroll
+                for (uint32_t l = 0; l < XINL; l++)
+                    if (l < L) eq &= iw[l] == st.get_wid(l);
+            } else {
+                for (uint32_t l = 0; l < L && eq; l++) eq = ix.wseq[b.y + l] == st.get_wid(l);
+            }
+            if (eq) { off = a.w; cnt = b.x; return; }
+        }
+        slot = (slot + 1) & ix.xmask;
+    }
+}
+
+// --------------------------------------------------------------- the walk
+
+// Depth-first NFA walk.  At node P on level l (P = the filter prefix matched so
+// far) the keys under P in Erlang term order are: [P] (exact terminal, only a
+// hit when l == L), [P,'#'] ('#' terminal: 'a/#' also matches 'a'), the '+'
+// subtree, then the literal subtree -- so visiting them in that order emits
+// hits in exactly the reference's traversal order (search_up, :239-253).
+// First-level '$' words skip the root's '+' and '#' (base_init, :160-163).
+// Returns false if the emitter asked to stop (match/2 first-hit mode).
+template <class S, class EM>
+__device__ bool dfs(const DevIndex &ix, uint32_t L, bool dollar, S &st, EM &em) {
+    uint32_t cur = ROOT, l = 0;
+    for (;;) {
+        const uint4 *np = reinterpret_cast<const uint4 *>(ix.nodes + cur);
+        uint4 n0 = np[0], n1 = np[1];   // plus, hash_off, hash_cnt, exact_off | exact_cnt, ...
+        const bool droot = dollar && l == 0;
+        if (l == L) {
+            if (!em(n0.w, n1.x)) return false;
+            if (!droot && !em(n0.y, n0.z)) return false;
+        } else {
+            const uint32_t w = st.get_wid(l);
+            const uint32_t lit = w != NONE ? edge_find(ix, cur, w) : NONE;
+            if (!droot && !em(n0.y, n0.z)) return false;
+            const uint32_t plus = droot ? NONE : n0.x;
+            if (plus != NONE) {
+                if (lit != NONE) st.push(l + 1, lit);
+                cur = plus; l++;
+                continue;
+            }
+            if (lit != NONE) { cur = lit; l++; continue; }
+        }
+        if (!st.pop(l, cur)) return true;
+    }
+}
+
+// ---------------------------------------------------------------- emitters
+
+struct RangeEmit {          // phase 1: count hits, keep up to RCAP value ranges
+    uint2 *rng;
+    uint32_t cnt, nr;
+    __device__ __forceinline__ bool operator()(uint32_t off, uint32_t n) {
+        if (n) {
+            if (nr < RCAP) rng[nr] = make_uint2(off, n);
+            nr++; cnt += n;
+        }
+        return true;
+    }
+};
+
+struct DirectEmit {         // re-walk: write values straight into the CSR
+    const uint32_t *vals;
+    uint32_t *out;
+    uint64_t pos, cap;
+    __device__ __forceinline__ bool operator()(uint32_t off, uint32_t n) {
+        for (uint32_t i = 0; i < n; i++, pos++)
+            if (pos < cap) out[pos] = vals[off + i];
+        return true;
+    }
+};
+
+struct FirstEmit {          // match/2: stop at the first hit
+    const uint32_t *vals;
+    uint32_t v;
+    bool found;
+    __device__ __forceinline__ bool operator()(uint32_t off, uint32_t n) {
+        if (n) { v = vals[off]; found = true; return false; }
+        return true;
+    }
+};
+
+template <class S, class EM>
+__device__ int match_topic(const DevIndex &ix, const uint8_t *blob, uint64_t beg, uint64_t end, S &st, EM &em) {
+    uint32_t L = 0; bool dollar, allf; uint64_t xh;
+    int rc = tokenize(ix, blob, beg, end, st, L, dollar, xh, allf);
+    if (rc) return rc;
+    st.reset();
+    if (!dfs(ix, L, dollar, st, em)) return RC_OK;
+    if (allf) {
+        uint32_t xoff, xcnt;
+        exact_find(ix, xh, L, st, xoff, xcnt);
+        em(xoff, xcnt);
+    }
+    return RC_OK;
+}
+
+enum { MODE_COUNT = 0, MODE_FIRST = 1 };
+
+struct Outs {               // per-mode outputs
+    uint8_t *err;
+    uint32_t *first_val;
+    uint8_t *first_found;
+};
+
+__device__ __forceinline__ void list_push(const Workspace &ws, uint64_t n, int k, uint32_t t) {
+    uint32_t i = atomicAdd(&ws.list_n[k], 1u);
+    ws.lists[(uint64_t)k * n + i] = t;
+}
+
+// one topic in phase-1 (count) or first-hit mode; returns RC_DEEP if the
+// storage is too shallow (caller routes the topic to a list kernel)
+template <int MODE, class S>
+__device__ int run_topic(const DevIndex &ix, const Workspace &ws, uint64_t n, const uint8_t *blob,
+                         const uint64_t *offs, uint64_t t, S &st, const Outs &o) {
+    const uint64_t beg = offs[t], end = offs[t + 1];
+    if (MODE == MODE_COUNT) {
+        RangeEmit em{ws.rng + t * RCAP, 0, 0};
+        int rc = match_topic(ix, blob, beg, end, st, em);
+        if (rc == RC_DEEP) return rc;
+        if (rc == RC_BADARG) { em.cnt = 0; em.nr = 0; }
+        ws.cnt[t] = em.cnt;
+        ws.nr[t] = em.nr;
+        o.err[t] = rc == RC_BADARG;
+        if (em.nr > RCAP) list_push(ws, n, S::maxl <= MID_L ? L_OVF_MID : L_OVF_DEEP, (uint32_t)t);
+        return rc;
+    } else {
+        FirstEmit em{ix.vals, 0, false};
+        int rc = match_topic(ix, blob, beg, end, st, em);
+        if (rc == RC_DEEP) return rc;
+        o.first_val[t] = em.v;
+        o.first_found[t] = rc == RC_BADARG ? 2 : (em.found ? 1 : 0);
+        return rc;
+    }
+}
+
+// ----------------------------------------------------------------- kernels
+
+constexpr int WALK_BLOCK = 256;
+
+template <int MODE>
+__global__ __launch_bounds__(WALK_BLOCK) void k_walk_fast(DevIndex ix, Workspace ws, uint64_t n,
+                                                          const uint8_t *blob, const uint64_t *offs, Outs o) {
+    __shared__ uint32_t s_wid[FAST_L * WALK_BLOCK];
+    __shared__ uint32_t s_pend[(FAST_L + 1) * WALK_BLOCK];
+    const uint64_t t = (uint64_t)blockIdx.x * WALK_BLOCK + threadIdx.x;
+    if (t >= n) return;
+    LdsStore<FAST_L> st{s_wid + threadIdx.x, s_pend + threadIdx.x, WALK_BLOCK, 0};
+    int rc = run_topic<MODE>(ix, ws, n, blob, offs, t, st, o);
+    if (rc == RC_DEEP) {
+        uint32_t nl = count_levels(blob, offs[t], offs[t + 1]);
+        list_push(ws, n, nl <= MID_L ? L_MID : L_DEEP, (uint32_t)t);
+    }
+}
+
+constexpr int MID_BLOCK = 64;
+
+template <int MODE>
+__global__ __launch_bounds__(MID_BLOCK) void k_walk_mid(DevIndex ix, Workspace ws, uint64_t n,
+                                                        const uint8_t *blob, const uint64_t *offs, Outs o) {
+    __shared__ uint32_t s_wid[MID_L * MID_BLOCK];
+    __shared__ uint32_t s_pend[(MID_L + 1) * MID_BLOCK];
+    const uint32_t cnt = ws.list_n[L_MID];
+    const uint32_t *lst = ws.lists + (uint64_t)L_MID * n;
+    LdsStore<MID_L> st{s_wid + threadIdx.x, s_pend + threadIdx.x, MID_BLOCK, 0};
+    for (uint32_t i = blockIdx.x * MID_BLOCK + threadIdx.x; i < cnt; i += gridDim.x * MID_BLOCK)
+        run_topic<MODE>(ix, ws, n, blob, offs, lst[i], st, o);
+}
+
+template <int MODE>
+__global__ __launch_bounds__(64) void k_walk_deep(DevIndex ix, Workspace ws, uint64_t n,
+                                                  const uint8_t *blob, const uint64_t *offs, Outs o) {
+    const uint32_t lane = blockIdx.x * 64 + threadIdx.x;   // < DEEP_LANES
+    const uint32_t cnt = ws.list_n[L_DEEP];
+    const uint32_t *lst = ws.lists + (uint64_t)L_DEEP * n;
+    GlobalStore st{ws.deep_wid + (uint64_t)lane * MAX_LEVELS, ws.deep_stk + (uint64_t)lane * (MAX_LEVELS + 1), 0};
+    for (uint32_t i = lane; i < cnt; i += DEEP_LANES)
+        run_topic<MODE>(ix, ws, n, blob, offs, lst[i], st, o);
+}
+
+// re-walk of topics with more than RCAP hit ranges: values go straight to the CSR
+template <class S>
+__device__ void rewalk(const DevIndex &ix, const uint8_t *blob, const uint64_t *offs, uint64_t t,
+                       const uint64_t *hit_offs, uint32_t *out, uint64_t cap, S &st) {
+    DirectEmit em{ix.vals, out, hit_offs[t], cap};
+    match_topic(ix, blob, offs[t], offs[t + 1], st, em);
+}
+
+__global__ __launch_bounds__(MID_BLOCK) void k_rewalk_mid(DevIndex ix, Workspace ws, uint64_t n, const uint8_t *blob,
+                                                          const uint64_t *offs, const uint64_t *hit_offs,
+                                                          uint32_t *out, uint64_t cap) {
+    __shared__ uint32_t s_wid[MID_L * MID_BLOCK];
+    __shared__ uint32_t s_pend[(MID_L + 1) * MID_BLOCK];
+    const uint32_t cnt = ws.list_n[L_OVF_MID];
+    const uint32_t *lst = ws.lists + (uint64_t)L_OVF_MID * n;
+    LdsStore<MID_L> st{s_wid + threadIdx.x, s_pend + threadIdx.x, MID_BLOCK, 0};
+    for (uint32_t i = blockIdx.x * MID_BLOCK + threadIdx.x; i < cnt; i += gridDim.x * MID_BLOCK)
+        rewalk(ix, blob, offs, lst[i], hit_offs, out, cap, st);
+}
+
+__global__ __launch_bounds__(64) void k_rewalk_deep(DevIndex ix, Workspace ws, uint64_t n, const uint8_t *blob,
+                                                    const uint64_t *offs, const uint64_t *hit_offs,
+                                                    uint32_t *out, uint64_t cap) {
+    const uint32_t lane = blockIdx.x * 64 + threadIdx.x;
+    const uint32_t cnt = ws.list_n[L_OVF_DEEP];
+    const uint32_t *lst = ws.lists + (uint64_t)L_OVF_DEEP * n;
+    GlobalStore st{ws.deep_wid + (uint64_t)lane * MAX_LEVELS, ws.deep_stk + (uint64_t)lane * (MAX_LEVELS + 1), 0};
+    for (uint32_t i = lane; i < cnt; i += DEEP_LANES)
+        rewalk(ix, blob, offs, lst[i], hit_offs, out, cap, st);
+}
+
+// ------------------------------------------------------------------- scan
+
+__device__ __forceinline__ uint64_t wave_incl_scan(uint64_t v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        uint64_t o = __shfl_up(v, d, 64);
+        if (lane >= d) v += o;
+    }
+    return v;
+}
+
+// block-wide exclusive scan of one value per thread (blockDim = 256)
+__device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t &total, uint64_t *s_w) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint64_t inc = wave_incl_scan(v);
+    if (lane == 63) s_w[wv] = inc;
+    __syncthreads();
+    uint64_t pre = 0;
+    total = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) { if (i < wv) pre += s_w[i]; total += s_w[i]; }
+    __syncthreads();
+    return pre + inc - v;
+}
+
+// tile of SCAN_TILE = 256 threads x 4 counts
+__global__ __launch_bounds__(256) void k_scan_reduce(const uint32_t *cnt, uint64_t n, uint64_t *blk) {
+    __shared__ uint64_t s_w[4];
+    const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE + threadIdx.x * 4;
+    uint64_t v = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) if (base + k < n) v += cnt[base + k];
+    uint64_t total;
+    block_excl_scan(v, total, s_w);
+    if (threadIdx.x == 0) blk[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(256) void k_scan_top(uint64_t *blk, uint64_t nb, uint64_t *hit_offs, uint64_t n) {
+    __shared__ uint64_t s_w[4];
+    uint64_t carry = 0;
+    for (uint64_t b0 = 0; b0 < nb; b0 += 256) {
+        const uint64_t i = b0 + threadIdx.x;
+        uint64_t v = i < nb ? blk[i] : 0, total;
+        uint64_t ex = block_excl_scan(v, total, s_w);
+        if (i < nb) blk[i] = carry + ex;
+        carry += total;
+    }
+    if (threadIdx.x == 0) hit_offs[n] = carry;
+}
+
+__global__ __launch_bounds__(256) void k_scan_apply(const uint32_t *cnt, uint64_t n, const uint64_t *blk,
+                                                    uint64_t *hit_offs) {
+    __shared__ uint64_t s_w[4];
+    const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE + threadIdx.x * 4;
+    uint32_t c[4];
+    uint64_t v = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) { c[k] = base + k < n ? cnt[base + k] : 0; v += c[k]; }
+    uint64_t total;
+    uint64_t pre = block_excl_scan(v, total, s_w) + blk[blockIdx.x];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        if (base + k < n) hit_offs[base + k] = pre;
+        pre += c[k];
+    }
+}
+
+// ------------------------------------------------------------------- emit
+
+constexpr int EMIT_BLOCK = 256;
+constexpr int EMIT_WAVES = EMIT_BLOCK / 64;
+constexpr int WR = 64 * RCAP;   // ranges per wave
+
+__device__ __forceinline__ uint32_t wave_excl_scan32(uint32_t v, uint32_t &total) {
+    const int lane = threadIdx.x & 63;
+    uint32_t inc = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        uint32_t o = __shfl_up(inc, d, 64);
+        if (lane >= d) inc += o;
+    }
+    total = __shfl(inc, 63, 64);
+    return inc - v;
+}
+
+// Each wave owns 64 consecutive topics: it flattens their value ranges into
+// LDS and then strides over the wave's hit positions, so stores are
+// contiguous whatever the per-topic hit counts are.
+__global__ __launch_bounds__(EMIT_BLOCK) void k_emit(DevIndex ix, Workspace ws, uint64_t n,
+                                                     const uint64_t *hit_offs, uint32_t *out, uint64_t cap) {
+    __shared__ uint32_t s_off[EMIT_WAVES][WR];
+    __shared__ uint32_t s_cum[EMIT_WAVES][WR];
+    __shared__ uint32_t s_rel[EMIT_WAVES][WR];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint64_t t0 = ((uint64_t)blockIdx.x * EMIT_WAVES + wv) * 64;
+    if (t0 >= n) return;   // whole wave leaves; only wave-level sync below
+    const uint64_t t = t0 + lane;
+    const bool valid = t < n;
+    uint32_t nr = valid ? ws.nr[t] : 0, c = valid ? ws.cnt[t] : 0;
+    if (nr > RCAP) { nr = 0; c = 0; }   // written by k_rewalk_*
+    const uint64_t base = hit_offs[t0];
+    const uint32_t rel = valid ? (uint32_t)(hit_offs[t] - base) : 0;
+    uint32_t R, E;
+    const uint32_t r0 = wave_excl_scan32(nr, R);
+    const uint32_t e0 = wave_excl_scan32(c, E);
+    uint32_t acc = 0;
+    for (uint32_t i = 0; i < nr; i++) {
+        uint2 g = ws.rng[t * RCAP + i];
+        s_off[wv][r0 + i] = g.x;
+        s_cum[wv][r0 + i] = e0 + acc;
+        s_rel[wv][r0 + i] = rel + acc;
+        acc += g.y;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (uint32_t e = lane; e < E; e += 64) {
+        uint32_t lo = 0, hi = R - 1;
+        while (lo < hi) {
+            uint32_t mid = (lo + hi + 1) >> 1;
+            if (s_cum[wv][mid] <= e) lo = mid; else hi = mid - 1;
+        }
+        const uint32_t k = e - s_cum[wv][lo];
+        const uint64_t pos = base + s_rel[wv][lo] + k;
+        if (pos < cap) out[pos] = ix.vals[s_off[wv][lo] + k];
+    }
+}
+
+__global__ void k_patch(const uint64_t *addr, const uint32_t *val, uint64_t n) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) *reinterpret_cast<uint32_t *>(addr[i]) = val[i];
+}
+
+// ------------------------------------------------------------ launchers
+
+static inline uint32_t blocks_for(uint64_t n, uint32_t per) { return (uint32_t)((n + per - 1) / per); }
+
+static constexpr int MID_GRID = 256;   // list kernels: fixed grids, device-side list lengths
+
+hipError_t launch_match_phase1(const DevIndex &ix, const Workspace &ws, uint64_t n, const uint8_t *bytes,
+                               const uint64_t *offs, uint64_t *hit_offs, uint8_t *err, hipStream_t s,
+                               hipEvent_t ev_walk0, hipEvent_t ev_walk1) {
+    hipError_t e = hipMemsetAsync(ws.list_n, 0, sizeof(uint32_t) * L_COUNT, s);
+    if (e != hipSuccess) return e;
+    Outs o{err, nullptr, nullptr};
+    if (n) {
+        if (ev_walk0 && (e = hipEventRecord(ev_walk0, s)) != hipSuccess) return e;
+        hipLaunchKernelGGL(k_walk_fast<MODE_COUNT>, dim3(blocks_for(n, WALK_BLOCK)), dim3(WALK_BLOCK), 0, s,
+                           ix, ws, n, bytes, offs, o);
+        if (ev_walk1 && (e = hipEventRecord(ev_walk1, s)) != hipSuccess) return e;
+        hipLaunchKernelGGL(k_walk_mid<MODE_COUNT>, dim3(MID_GRID), dim3(MID_BLOCK), 0, s, ix, ws, n, bytes, offs, o);
+        hipLaunchKernelGGL(k_walk_deep<MODE_COUNT>, dim3(DEEP_LANES / 64), dim3(64), 0, s, ix, ws, n, bytes, offs, o);
+    }
+    const uint64_t nb = (n + SCAN_TILE - 1) / SCAN_TILE;
+    if (nb) hipLaunchKernelGGL(k_scan_reduce, dim3((uint32_t)nb), dim3(256), 0, s, ws.cnt, n, ws.blk);
+    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(256), 0, s, ws.blk, nb, hit_offs, n);
+    if (nb) hipLaunchKernelGGL(k_scan_apply, dim3((uint32_t)nb), dim3(256), 0, s, ws.cnt, n, ws.blk, hit_offs);
+    return hipGetLastError();
+}
+
+hipError_t launch_match_phase2(const DevIndex &ix, const Workspace &ws, uint64_t n, const uint8_t *bytes,
+                               const uint64_t *offs, const uint64_t *hit_offs, uint32_t *out, uint64_t cap,
+                               hipStream_t s) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_emit, dim3(blocks_for(n, EMIT_BLOCK)), dim3(EMIT_BLOCK), 0, s, ix, ws, n, hit_offs, out, cap);
+    hipLaunchKernelGGL(k_rewalk_mid, dim3(MID_GRID), dim3(MID_BLOCK), 0, s, ix, ws, n, bytes, offs, hit_offs, out, cap);
+    hipLaunchKernelGGL(k_rewalk_deep, dim3(DEEP_LANES / 64), dim3(64), 0, s, ix, ws, n, bytes, offs, hit_offs, out, cap);
+    return hipGetLastError();
+}
+
+hipError_t launch_first(const DevIndex &ix, const Workspace &ws, uint64_t n, const uint8_t *bytes,
+                        const uint64_t *offs, uint32_t *out_value, uint8_t *out_found, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(ws.list_n, 0, sizeof(uint32_t) * L_COUNT, s);
+    if (e != hipSuccess) return e;
+    if (!n) return hipSuccess;
+    Outs o{nullptr, out_value, out_found};
+    hipLaunchKernelGGL(k_walk_fast<MODE_FIRST>, dim3(blocks_for(n, WALK_BLOCK)), dim3(WALK_BLOCK), 0, s,
+                       ix, ws, n, bytes, offs, o);
+    hipLaunchKernelGGL(k_walk_mid<MODE_FIRST>, dim3(MID_GRID), dim3(MID_BLOCK), 0, s, ix, ws, n, bytes, offs, o);
+    hipLaunchKernelGGL(k_walk_deep<MODE_FIRST>, dim3(DEEP_LANES / 64), dim3(64), 0, s, ix, ws, n, bytes, offs, o);
+    return hipGetLastError();
+}
+
+hipError_t launch_patch(const uint64_t *d_addr, const uint32_t *d_val, uint64_t n, hipStream_t s) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_patch, dim3(blocks_for(n, 256)), dim3(256), 0, s, d_addr, d_val, n);
+    return hipGetLastError();
+}
+
+}  // namespace tmx

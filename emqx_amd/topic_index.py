@@ -1,0 +1,184 @@
+"""Drop-in mirror of ``emqx_topic_index`` backed by the MI355X index.
+
+Same names, argument meaning and results as apps/emqx/src/emqx_topic_index.erl
+(new/0,1 :40-48, insert/4 :53-56, delete/3 :60-62, match/2 :70-72,
+matches/3 :76-78, get_id/1, get_topic/1, get_record/2 :86-106).
+
+``Tab`` plays the part of the caller-owned ETS table: it keeps the records
+(the source of truth, SURVEY.md 8b "Ownership") and interns every key
+``{Filter, {ID}}`` to a dense u32 that the device index stores.  Inserts and
+deletes are queued and shipped with one ``tm_apply_deltas`` call before the
+next match (the router-syncer batch boundary, emqx_router_syncer.erl:297-356).
+Matching always runs on the GPU through ``libtmatch``; there is no CPU path.
+
+Result order: the device returns keys in traversal order (ascending Erlang
+term order).  ``matches/3`` returns them like the reference does -- reversed,
+because match_add/2 prepends (emqx_trie_search.erl:350-356); ``[unique]``
+keeps the last key per ID (maps:values, sorted by ID as small maps are);
+``match/2`` is the first key in traversal order.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import _native
+from .trie_search import (BadArg, HASH, PLUS, get_id, get_topic, key_order, make_key,  # noqa: F401
+                          term_key, topic_words)
+
+
+class Tab:
+    """An index table: records + the device-resident mirror of its keys."""
+
+    def __init__(self, device: int = -1, hint_keys: int = 0):
+        self._index = _native.Index(device=device, hint_keys=hint_keys)
+        self._records: dict = {}        # key -> record        (the ETS rows)
+        self._kid: dict = {}            # key -> u32 value on the device
+        self._keys: list = []           # u32 -> key
+        self._free: list[int] = []
+        self._dead: set = set()         # keys that can never match (kept host-side only)
+        self._ops: list = []            # pending (op, filter_bytes, kid, flags)
+
+    # -- key <-> device encoding
+    @staticmethod
+    def _encode(key):
+        """-> (filter bytes, flags) for tm_apply_deltas, or None for a key no topic can match."""
+        f = key[0]
+        if not isinstance(f, tuple):
+            return bytes(f), _native.TM_KEY_BINARY
+        if len(f) == 0:
+            return b"", _native.TM_KEY_EMPTY_LIST
+        parts = []
+        for w in f:
+            if w == PLUS or w == HASH:
+                parts.append(w.encode())
+            elif isinstance(w, (bytes, bytearray)):
+                w = bytes(w)
+                # a binary word "+"/"#" or one containing '/' never equals a topic level
+                if w in (b"+", b"#") or b"/" in w:
+                    return None
+                parts.append(w)
+            else:
+                raise TypeError(f"bad filter word {w!r}")
+        return b"/".join(parts), _native.TM_KEY_WORDS
+
+    def _queue(self, op, key, kid):
+        enc = self._encode(key)
+        if enc is None:
+            (self._dead.add if op else self._dead.discard)(key)
+            return
+        self._ops.append((op, enc[0], kid, enc[1]))
+
+    def flush(self):
+        if not self._ops:
+            return
+        ops = np.array([o[0] for o in self._ops], dtype=np.uint8)
+        blob, offs = _native.pack_strings([o[1] for o in self._ops])
+        vals = np.array([o[2] for o in self._ops], dtype=np.uint32)
+        flags = np.array([o[3] for o in self._ops], dtype=np.uint8)
+        self._ops = []
+        self._index.apply(ops, blob, offs, vals, flags)
+
+    # -- table operations
+    def insert_key(self, key, record):
+        if key not in self._records:
+            kid = self._free.pop() if self._free else len(self._keys)
+            if kid == len(self._keys):
+                self._keys.append(key)
+            else:
+                self._keys[kid] = key
+            self._kid[key] = kid
+            self._queue(_native.TM_OP_INSERT, key, kid)
+        self._records[key] = record
+
+    def delete_key(self, key):
+        if key in self._records:
+            kid = self._kid.pop(key)
+            del self._records[key]
+            self._queue(_native.TM_OP_DELETE, key, kid)
+            self._keys[kid] = None
+            self._free.append(kid)
+
+    def size(self) -> int:
+        return len(self._records)
+
+    def keys(self):
+        return list(self._records)
+
+    def lookup(self, key):
+        return [self._records[key]] if key in self._records else []
+
+    # -- matching (batched: the unit the broker micro-batch hands over)
+    def match_kids(self, topics):
+        """-> (list of kid arrays in traversal order, badarg flags)."""
+        self.flush()
+        blob, offs = _native.pack_strings(topics)
+        hit, vals, err = self._index.match_batch(blob, offs)
+        return [vals[hit[i]:hit[i + 1]] for i in range(len(topics))], err
+
+    def stats(self) -> dict:
+        self.flush()
+        return self._index.stats()
+
+
+def new(options=None, device: int = -1) -> Tab:
+    """new/0,1: an empty index table (ETS options are accepted and ignored)."""
+    return Tab(device=device)
+
+
+def insert(filter_, ident, record, tab: Tab):
+    """insert/4: associate Filter with ID (and Record)."""
+    tab.insert_key(make_key(filter_, ident), record)
+    return True
+
+
+def delete(filter_, ident, tab: Tab):
+    """delete/3: deleting a missing entry is not an error."""
+    tab.delete_key(make_key(filter_, ident))
+    return True
+
+
+def _check_topic(topic):
+    topic_words(topic)          # raises BadArg like the reference
+    return bytes(topic)
+
+
+def matches_batch(topics, tab: Tab, opts=()):
+    """matches/3 over a batch of topics (one device launch); BadArg if any topic is bad."""
+    topics = [_check_topic(t) for t in topics]
+    kids, err = tab.match_kids(topics)
+    out = []
+    for i, ks in enumerate(kids):
+        if err[i]:
+            raise BadArg(topics[i])
+        keys = [tab._keys[k] for k in ks.tolist()]
+        out.append(_finish(keys, opts))
+    return out
+
+
+def _finish(keys, opts):
+    if "unique" in opts:
+        by_id = {}
+        for k in sorted(keys, key=key_order):      # traversal order; later keys win
+            by_id[get_id(k)] = k
+        return [by_id[i] for i in sorted(by_id, key=term_key)]
+    return sorted(keys, key=key_order, reverse=True)
+
+
+def matches(topic, tab: Tab, opts=()):
+    """matches/3."""
+    return matches_batch([topic], tab, opts)[0]
+
+
+def match(topic, tab: Tab):
+    """match/2: the first match in traversal order, or False."""
+    keys = matches_batch([topic], tab, ())[0]
+    return keys[-1] if keys else False
+
+
+def get_record(key, tab: Tab):
+    """get_record/2: [Record] or [] if the entry was deleted meanwhile."""
+    return tab.lookup(key)
+
+
+__all__ = ["new", "insert", "delete", "match", "matches", "matches_batch", "make_key", "get_id",
+           "get_topic", "get_record", "Tab", "BadArg"]

@@ -1,0 +1,135 @@
+/*
+ * tmatch.h -- C ABI of the MI355X topic-match engine (libtmatch.so).
+ *
+ * Drop-in boundary for EMQX's publish-routing match path.  Plain C types only:
+ * pointers, sizes, status codes; no exceptions cross this boundary.  What each
+ * entry point replaces in the reference (paths relative to the reference root):
+ *
+ *   tm_create / tm_destroy
+ *       emqx_topic_index:new/0,1          apps/emqx/src/emqx_topic_index.erl:40-48
+ *       (the ETS ordered_set stays the source of truth on the Erlang side; this
+ *        handle is its HBM mirror -- SURVEY.md 8b "Ownership")
+ *   tm_apply_deltas
+ *       emqx_topic_index:insert/4, delete/3 apps/emqx/src/emqx_topic_index.erl:53-62
+ *       via emqx_trie_search:make_key/2     apps/emqx/src/emqx_trie_search.erl:115-128
+ *       and the router's batched writes     apps/emqx/src/emqx_router.erl:255-273,483-509
+ *   tm_match_batch / tm_match_batch_dev
+ *       emqx_topic_index:matches/3          apps/emqx/src/emqx_topic_index.erl:76-78
+ *       = emqx_trie_search:matches/3        apps/emqx/src/emqx_trie_search.erl:182-226,381-389
+ *       called per publish by emqx_router:match_routes/1 (emqx_router.erl:205-212,511-516)
+ *   tm_first_batch
+ *       emqx_topic_index:match/2            apps/emqx/src/emqx_topic_index.erl:70-72
+ *       (first key in traversal order; emqx_trie_search.erl:171-178,350-356)
+ *   tm_stats
+ *       emqx_router:stats/1 n_routes part    apps/emqx/src/emqx_router.erl:632-635
+ *
+ * Keys.  An index entry is the pair (filter, value).  `value` is a caller-chosen
+ * u32 (the NIF interns the Erlang {ID} term, or the whole key, to a u32).
+ * Key form follows make_key/2: a binary filter with a '+'/'#' level is a word
+ * list; a binary without one is a binary key; TM_KEY_WORDS forces the
+ * word-list form (make_key(Words, ID) with a list); TM_KEY_EMPTY_LIST is the
+ * word list [] (which has no byte form).  Inserting an existing key and
+ * deleting a missing key are no-ops (ETS set semantics, emqx_topic_index.erl:58-62).
+ *
+ * Output.  For each topic the matching values are written in TRAVERSAL order:
+ * ascending Erlang term order of the keys {Filter, {Value}} -- word-list keys
+ * (by word: '#' < '+' < binary words, shorter first), then binary keys, and
+ * ascending value inside one filter.  This is exactly the order in which the
+ * reference's walk visits them; its matches/3 list is the reverse
+ * (match_add/2 prepends, emqx_trie_search.erl:353-354).
+ * A topic with a level equal to "+" or "#" is badarg (emqx_trie_search.erl:374-375):
+ * its err flag is 1 and it has no hits.
+ */
+#ifndef TMATCH_H
+#define TMATCH_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct tm_index tm_index;
+
+enum {
+    TM_OK = 0,
+    TM_EINVAL = -1,   /* bad argument (null pointer, bad op code)            */
+    TM_ENOMEM = -2,   /* host or device allocation failed                    */
+    TM_EDEVICE = -3,  /* HIP runtime error                                   */
+    TM_ECAP = -4      /* output capacity too small: offsets are valid, ids   */
+                      /* were truncated to `cap`; retry with cap >= total    */
+};
+
+enum { TM_OP_DELETE = 0, TM_OP_INSERT = 1 };
+enum { TM_KEY_BINARY = 0, TM_KEY_WORDS = 1, TM_KEY_EMPTY_LIST = 2 };
+
+typedef struct {
+    int32_t device;          /* HIP device ordinal; -1 = current device        */
+    uint32_t reserved;
+    uint64_t hint_keys;      /* expected number of keys (sizes tables up front) */
+} tm_options;
+
+typedef struct {
+    uint64_t n_keys;         /* live keys (word-list + binary + never-matching) */
+    uint64_t n_wild_keys;    /* word-list keys (trie terminals)                 */
+    uint64_t n_exact_keys;   /* binary keys                                     */
+    uint64_t n_dead_keys;    /* keys that can never match ('#' not last, [])     */
+    uint64_t n_nodes, n_edges, n_words;
+    uint64_t device_bytes;   /* HBM held by the mirror                          */
+    uint64_t uploads;        /* full + patch uploads performed                   */
+    uint64_t patch_bytes;    /* bytes moved by incremental patches              */
+} tm_stats_t;
+
+/* Create an empty index on a device.  opts may be NULL. */
+int tm_create(const tm_options *opts, tm_index **out);
+int tm_destroy(tm_index *h);
+
+/* Apply n deltas in order (a later op on the same key wins).  Host buffers:
+ * filter i is filter_bytes[filter_offsets[i] .. filter_offsets[i+1]).
+ * key_flags may be NULL (all TM_KEY_BINARY).  Device upload is deferred to the
+ * next match / tm_sync on the stream given there (patches are applied in
+ * stream order, so a batch sees exactly the deltas applied before it). */
+int tm_apply_deltas(tm_index *h, uint64_t n, const uint8_t *ops, const uint8_t *filter_bytes,
+                    const uint64_t *filter_offsets, const uint32_t *values, const uint8_t *key_flags);
+
+/* Upload pending patches on `stream` (hipStream_t; NULL = the index's own stream). */
+int tm_sync(tm_index *h, void *stream);
+
+/* Host buffers in, host buffers out (pinned staging inside).  Blocks until the
+ * hit lists are in host memory.  out_hit_offsets has n+1 entries;
+ * out_err has n entries (may be NULL). */
+int tm_match_batch(tm_index *h, uint64_t n, const uint8_t *topic_bytes, const uint64_t *topic_offsets,
+                   uint64_t *out_hit_offsets, uint32_t *out_values, uint64_t cap, uint8_t *out_err);
+
+/* Device-resident batch: every pointer is device memory; asynchronous on
+ * `stream` (hipStream_t; NULL = the index's own stream).  d_out_hit_offsets has
+ * n+1 entries and d_out_hit_offsets[n] is the total; values beyond `cap` are
+ * dropped (the caller compares the total with cap after synchronising). */
+int tm_match_batch_dev(tm_index *h, uint64_t n, const uint8_t *d_topic_bytes, const uint64_t *d_topic_offsets,
+                       uint64_t *d_out_hit_offsets, uint32_t *d_out_values, uint64_t cap,
+                       uint8_t *d_out_err, void *stream);
+
+/* match/2: first hit per topic in traversal order.  out_found[i] = 1 and
+ * out_value[i] = value if topic i has a match, 0 otherwise (2 = badarg). */
+int tm_first_batch(tm_index *h, uint64_t n, const uint8_t *topic_bytes, const uint64_t *topic_offsets,
+                   uint32_t *out_value, uint8_t *out_found);
+
+int tm_stats(tm_index *h, tm_stats_t *out);
+
+/* Diagnostics.  While enabled, every match batch records HIP events on its
+ * stream around the main walk kernel (k_walk_fast) and around the whole batch;
+ * tm_profile_read() resolves them and returns the accumulated device times
+ * (milliseconds) and the number of batches since the last reset. */
+int tm_profile_enable(tm_index *h, int enable);
+int tm_profile_read(tm_index *h, double *walk_ms, double *batch_ms, uint64_t *batches, int reset);
+
+/* Last error text for a handle (or the global one when h is NULL). */
+const char *tm_last_error(tm_index *h);
+
+/* ABI version: (major << 16) | minor. */
+uint32_t tm_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TMATCH_H */

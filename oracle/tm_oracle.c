@@ -1,0 +1,633 @@
+/*
+ * tm_oracle.c -- CPU ORACLE for the EMQX topic-match hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing in the product path (emqx_amd/, the
+ * libtmatch C-ABI) links, loads or calls this file.  It is used by tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg, and only as the
+ * checker / the timed CPU reference.
+ *
+ * It is a from-scratch C restatement of the reference algorithm, not a copy:
+ *
+ *  (1) the ordered-set seek walker of emqx_trie_search
+ *        key layout / make_key ............ apps/emqx/src/emqx_trie_search.erl:107-128
+ *        base/base_init ($-first word) .... emqx_trie_search.erl:157-163
+ *        search / search_new / search_up .. emqx_trie_search.erl:192-253
+ *        seek ............................. emqx_trie_search.erl:255-258
+ *        compare (topic mode) ............. emqx_trie_search.erl:260-348
+ *        match_add (traversal order) ...... emqx_trie_search.erl:350-356
+ *        topic_words / word (badarg) ...... emqx_trie_search.erl:369-378
+ *        match_topics (exact keys) ........ emqx_trie_search.erl:381-389
+ *      over an ordered set with "next key strictly greater than K"
+ *      (ets:next/2 on the ordered_set of emqx_topic_index.erl:41-48,108-109),
+ *      here a sorted array + binary search, ordered by Erlang term order:
+ *      word lists < binaries; inside lists '#' < '+' < binary words
+ *      (byte-lexicographic, shorter prefix first); {} < {ID}.
+ *
+ *  (2) the single-filter MQTT spec matcher emqx_topic:match/2
+ *        apps/emqx/src/emqx_topic.erl:83-116, tokens/1 :318-319
+ *      used as an independent brute-force cross-check (the reference's own
+ *      property test uses it as its oracle: emqx_topic_index_SUITE.erl:318-329).
+ *
+ * IDs are u32 values; their term order is numeric order (integer IDs).
+ * Parity pinning: tests/test_oracle_golden.py checks both oracles against the
+ * known-answer vectors transcribed from the reference suites into
+ * tests/golden/reference_vectors.json.
+ */
+#define _GNU_SOURCE
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <pthread.h>
+
+/* ------------------------------------------------------------------ keys */
+
+enum { FORM_LIST = 0, FORM_BIN = 1 };
+
+typedef struct {
+    const uint8_t *b;   /* bytes: BIN = whole binary; LIST = words joined by '/' */
+    uint32_t len;
+    uint32_t nw;        /* LIST: number of words (0 = the empty list)           */
+    uint32_t id;
+    uint8_t form;
+    uint8_t base;       /* 1 = base key {Prefix, {}} (sorts before every {ID})   */
+} okey;
+
+/* word kinds in term order: atom '#' < atom '+' < binary */
+enum { WK_HASH = 0, WK_PLUS = 1, WK_BIN = 2 };
+
+typedef struct { const uint8_t *p; uint32_t n; int kind; } oword;
+
+static int word_kind(const uint8_t *p, uint32_t n) {
+    if (n == 1 && p[0] == '#') return WK_HASH;
+    if (n == 1 && p[0] == '+') return WK_PLUS;
+    return WK_BIN;
+}
+
+/* iterate words of a LIST key: returns 1 and fills *w while words remain */
+typedef struct { const uint8_t *b; uint32_t len, pos, left; } witer;
+
+static void wit_init(witer *it, const okey *k) {
+    it->b = k->b; it->len = k->len; it->pos = 0; it->left = k->nw;
+}
+static int wit_next(witer *it, oword *w) {
+    if (!it->left) return 0;
+    uint32_t s = it->pos, e = s;
+    while (e < it->len && it->b[e] != '/') e++;
+    w->p = it->b + s; w->n = e - s; w->kind = word_kind(w->p, w->n);
+    it->pos = e + 1; it->left--;
+    return 1;
+}
+
+static int bin_cmp(const uint8_t *a, uint32_t an, const uint8_t *b, uint32_t bn) {
+    uint32_t m = an < bn ? an : bn;
+    int c = m ? memcmp(a, b, m) : 0;
+    if (c) return c < 0 ? -1 : 1;
+    return an < bn ? -1 : (an > bn ? 1 : 0);
+}
+
+static int word_cmp(const oword *a, const oword *b) {
+    if (a->kind != b->kind) return a->kind < b->kind ? -1 : 1;
+    if (a->kind != WK_BIN) return 0;
+    return bin_cmp(a->p, a->n, b->p, b->n);
+}
+
+/* Erlang term order of the filter part of two keys */
+static int filter_cmp(const okey *a, const okey *b) {
+    if (a->form != b->form) return a->form == FORM_LIST ? -1 : 1;
+    if (a->form == FORM_BIN) return bin_cmp(a->b, a->len, b->b, b->len);
+    witer ia, ib; oword wa, wb;
+    wit_init(&ia, a); wit_init(&ib, b);
+    for (;;) {
+        int ha = wit_next(&ia, &wa), hb = wit_next(&ib, &wb);
+        if (!ha || !hb) return ha == hb ? 0 : (ha ? 1 : -1); /* shorter list first */
+        int c = word_cmp(&wa, &wb);
+        if (c) return c;
+    }
+}
+
+/* full key order: {Filter, {}} < {Filter, {ID}}, IDs numeric */
+static int key_cmp(const okey *a, const okey *b) {
+    int c = filter_cmp(a, b);
+    if (c) return c;
+    if (a->base && b->base) return 0;
+    if (a->base) return -1;
+    if (b->base) return 1;
+    return a->id < b->id ? -1 : (a->id > b->id ? 1 : 0);
+}
+
+/* ------------------------------------------------------------ the index */
+
+typedef struct { okey k; uint8_t op; uint64_t seq; } pend_op; /* op 1 = insert, 0 = delete */
+
+typedef struct {
+    okey *keys; int64_t n, cap;            /* sorted, unique                       */
+    pend_op *pend; int64_t np, pcap;       /* op log not yet merged                */
+    uint8_t **chunks; int64_t nchunks, chcap; /* owned byte storage for key bytes  */
+    uint8_t *cur; uint64_t cur_left;
+    uint64_t seq;
+} oindex;
+
+static uint8_t *store_bytes(oindex *h, const char *p, uint32_t n) {
+    if (n + 1 > h->cur_left) {
+        uint64_t sz = n + 1 > (1u << 24) ? (uint64_t)n + 1 : (1u << 24);
+        if (h->nchunks == h->chcap) {
+            h->chcap = h->chcap ? h->chcap * 2 : 64;
+            h->chunks = realloc(h->chunks, sizeof(uint8_t *) * h->chcap);
+        }
+        h->cur = malloc(sz);
+        h->chunks[h->nchunks++] = h->cur;
+        h->cur_left = sz;
+    }
+    uint8_t *r = h->cur;
+    if (n) memcpy(r, p, n);
+    h->cur += n; h->cur_left -= n;
+    return r;
+}
+
+static uint32_t count_words(const char *f, uint32_t len) {
+    uint32_t nw = 1;
+    for (uint32_t i = 0; i < len; i++) nw += f[i] == '/';
+    return nw;
+}
+
+/* emqx_topic:wildcard/1 over filter_words/1 (emqx_trie_search.erl:138-140,359-366) */
+static int has_wildcard(const char *f, uint32_t len) {
+    uint32_t s = 0;
+    for (uint32_t i = 0; i <= len; i++) {
+        if (i == len || f[i] == '/') {
+            if (i - s == 1 && (f[s] == '+' || f[s] == '#')) return 1;
+            s = i + 1;
+        }
+    }
+    return 0;
+}
+
+void *orc_new(void) { return calloc(1, sizeof(oindex)); }
+
+void orc_free(void *hp) {
+    oindex *h = hp;
+    if (!h) return;
+    for (int64_t i = 0; i < h->nchunks; i++) free(h->chunks[i]);
+    free(h->chunks); free(h->keys); free(h->pend); free(h);
+}
+
+/* make_key/2 (emqx_trie_search.erl:115-128): a binary filter with a wildcard
+ * becomes a word list; a binary without one stays a binary; words_form keys
+ * (make_key(Words, ID) with a list) are always lists.  nw_override lets the
+ * caller pass the empty list ([]) which has no byte form. */
+static okey mk_key(oindex *h, const char *f, uint32_t len, uint32_t id, int words_form, int empty_list) {
+    okey k; memset(&k, 0, sizeof k);
+    k.b = store_bytes(h, f, len); k.len = len; k.id = id;
+    if (empty_list) { k.form = FORM_LIST; k.nw = 0; k.len = 0; return k; }
+    if (words_form || has_wildcard(f, len)) { k.form = FORM_LIST; k.nw = count_words(f, len); }
+    else { k.form = FORM_BIN; k.nw = 0; }
+    return k;
+}
+
+static void push_op(oindex *h, okey k, int op) {
+    if (h->np == h->pcap) {
+        h->pcap = h->pcap ? h->pcap * 2 : 1024;
+        h->pend = realloc(h->pend, sizeof(pend_op) * h->pcap);
+    }
+    h->pend[h->np].k = k; h->pend[h->np].op = (uint8_t)op; h->pend[h->np].seq = h->seq++;
+    h->np++;
+}
+
+/* flags: bit0 = words form, bit1 = empty word list ([]) */
+void orc_insert(void *hp, const char *f, uint32_t len, uint32_t id, int flags) {
+    oindex *h = hp; push_op(h, mk_key(h, f, len, id, flags & 1, flags & 2), 1);
+}
+void orc_delete(void *hp, const char *f, uint32_t len, uint32_t id, int flags) {
+    oindex *h = hp; push_op(h, mk_key(h, f, len, id, flags & 1, flags & 2), 0);
+}
+
+/* batch form: ops[i] = 1 insert / 0 delete; blob + offs (n+1) */
+void orc_apply(void *hp, int64_t n, const uint8_t *ops, const char *blob, const uint64_t *offs,
+               const uint32_t *ids, const uint8_t *flags) {
+    oindex *h = hp;
+    for (int64_t i = 0; i < n; i++) {
+        int fl = flags ? flags[i] : 0;
+        okey k = mk_key(h, blob + offs[i], (uint32_t)(offs[i + 1] - offs[i]), ids[i], fl & 1, fl & 2);
+        push_op(h, k, ops[i]);
+    }
+}
+
+/* ---- parallel merge sort (pthreads) for bulk builds ---- */
+
+typedef int (*cmpf)(const void *, const void *);
+static int pend_cmp(const void *a, const void *b) {
+    const pend_op *x = a, *y = b;
+    int c = key_cmp(&x->k, &y->k);
+    if (c) return c;
+    return x->seq < y->seq ? -1 : (x->seq > y->seq ? 1 : 0);
+}
+
+typedef struct { pend_op *a; int64_t n; } sort_job;
+static void *sort_worker(void *p) { sort_job *j = p; qsort(j->a, j->n, sizeof(pend_op), pend_cmp); return 0; }
+
+static void merge_runs(pend_op *src, pend_op *dst, int64_t lo, int64_t mid, int64_t hi) {
+    int64_t i = lo, j = mid, o = lo;
+    while (i < mid && j < hi) dst[o++] = pend_cmp(&src[j], &src[i]) < 0 ? src[j++] : src[i++];
+    while (i < mid) dst[o++] = src[i++];
+    while (j < hi) dst[o++] = src[j++];
+}
+typedef struct { pend_op *src, *dst; int64_t lo, mid, hi; } merge_job;
+static void *merge_worker(void *p) { merge_job *j = p; merge_runs(j->src, j->dst, j->lo, j->mid, j->hi); return 0; }
+
+static void psort(pend_op *a, int64_t n) {
+    int T = 1;
+    if (n > (1 << 16)) T = 8;
+    if (T == 1) { qsort(a, n, sizeof(pend_op), pend_cmp); return; }
+    int64_t bounds[9];
+    for (int t = 0; t <= T; t++) bounds[t] = n * t / T;
+    pthread_t th[8]; sort_job sj[8];
+    for (int t = 0; t < T; t++) { sj[t].a = a + bounds[t]; sj[t].n = bounds[t + 1] - bounds[t]; pthread_create(&th[t], 0, sort_worker, &sj[t]); }
+    for (int t = 0; t < T; t++) pthread_join(th[t], 0);
+    pend_op *tmp = malloc(sizeof(pend_op) * n), *src = a, *dst = tmp;
+    for (int w = 1; w < T; w *= 2) {
+        merge_job mj[8]; int nj = 0;
+        for (int t = 0; t < T; t += 2 * w) {
+            int64_t lo = bounds[t], mid = bounds[t + w < T ? t + w : T], hi = bounds[t + 2 * w < T ? t + 2 * w : T];
+            mj[nj].src = src; mj[nj].dst = dst; mj[nj].lo = lo; mj[nj].mid = mid; mj[nj].hi = hi; nj++;
+        }
+        for (int t = 0; t < nj; t++) pthread_create(&th[t], 0, merge_worker, &mj[t]);
+        for (int t = 0; t < nj; t++) pthread_join(th[t], 0);
+        pend_op *s = src; src = dst; dst = s;
+    }
+    if (src != a) memcpy(a, src, sizeof(pend_op) * n);
+    free(tmp);
+}
+
+/* merge the op log into the sorted key array (last op per key wins) */
+static void flush(oindex *h) {
+    if (!h->np) return;
+    psort(h->pend, h->np);
+    int64_t m = 0;                      /* collapse to final op per key */
+    for (int64_t i = 0; i < h->np; i++) {
+        if (m && key_cmp(&h->pend[m - 1].k, &h->pend[i].k) == 0) h->pend[m - 1] = h->pend[i];
+        else h->pend[m++] = h->pend[i];
+    }
+    okey *out = malloc(sizeof(okey) * (h->n + m + 1));
+    int64_t i = 0, j = 0, o = 0;
+    while (i < h->n || j < m) {
+        int c = (i < h->n && j < m) ? key_cmp(&h->keys[i], &h->pend[j].k) : (i < h->n ? -1 : 1);
+        if (c < 0) out[o++] = h->keys[i++];
+        else {
+            if (h->pend[j].op) out[o++] = h->pend[j].k;   /* insert (or overwrite) */
+            if (c == 0) i++;
+            j++;
+        }
+    }
+    free(h->keys);
+    h->keys = out; h->n = o; h->cap = h->n + m + 1;
+    h->np = 0;
+}
+
+int64_t orc_size(void *hp) { oindex *h = hp; flush(h); return h->n; }
+
+void orc_prepare(void *hp) { flush((oindex *)hp); }
+
+/* NextF: ets:next/2 -- first key strictly greater than k, or -1 ('$end_of_table') */
+static int64_t next_key(const oindex *h, const okey *k) {
+    int64_t lo = 0, hi = h->n;
+    while (lo < hi) {
+        int64_t mid = (lo + hi) >> 1;
+        if (key_cmp(&h->keys[mid], k) <= 0) lo = mid + 1; else hi = mid;
+    }
+    return lo < h->n ? lo : -1;
+}
+
+/* ------------------------------------------------------------ the walk */
+
+#define MAXW 65536
+
+typedef struct {
+    const uint8_t *p[MAXW];
+    uint32_t n[MAXW];
+    uint32_t nw;
+} twords;
+
+/* topic_words/1 + word/2: split on '/', a level equal to '+' or '#' -> badarg */
+static int topic_words(const uint8_t *t, uint32_t len, twords *w) {
+    uint32_t s = 0; w->nw = 0;
+    for (uint32_t i = 0; i <= len; i++) {
+        if (i == len || t[i] == '/') {
+            uint32_t n = i - s;
+            if (n == 1 && (t[s] == '+' || t[s] == '#')) return -1;
+            w->p[w->nw] = t + s; w->n[w->nw] = n; w->nw++;
+            s = i + 1;
+        }
+    }
+    return 0;
+}
+
+enum { C_FULL = -1, C_PREFIX = -2, C_LOWER = -3 };  /* >= 0: seek position */
+
+/* compare/3 in topic mode (emqx_trie_search.erl:260-348), iterative form.
+ * Returns C_FULL/C_PREFIX/C_LOWER or the seek Pos (seek word = topic word Pos). */
+static int64_t compare(const okey *k, const twords *tw) {
+    if (k->form == FORM_BIN) return C_LOWER;                /* :260-261 */
+    witer it; oword fw; wit_init(&it, k);
+    int64_t lastplus = -1;
+    uint32_t i = 0;
+    for (;; i++) {
+        int hf = wit_next(&it, &fw);
+        if (!hf) return i == tw->nw ? C_FULL : C_PREFIX;      /* :262-281 */
+        if (fw.kind == WK_HASH && it.left == 0) return C_FULL;/* :282-290 */
+        if (i == tw->nw) break;                               /* :333-340 lower */
+        if (fw.kind == WK_PLUS) { lastplus = i; continue; }   /* :302-320 */
+        if (fw.kind == WK_BIN) {
+            int c = bin_cmp(fw.p, fw.n, tw->p[i], tw->n[i]);
+            if (c == 0) continue;                             /* :321-324 */
+            if (c > 0) break;                                 /* :325-332 lower */
+        }
+        return (int64_t)i;                                    /* :341-348 seek */
+    }
+    return lastplus >= 0 ? lastplus : C_LOWER;                /* '+' frame converts lower */
+}
+
+typedef struct {
+    uint32_t *ids; int64_t n, cap;  /* output (traversal order) */
+    uint8_t *scratch; uint32_t scap;
+} oacc;
+
+static void acc_add(oacc *a, uint32_t id) {
+    if (a->ids && a->n < a->cap) a->ids[a->n] = id;
+    a->n++;
+}
+
+/* base(seek(Pos, W, Filter)) -- Filter[0..Pos) ++ [W] as a LIST base key */
+static okey seek_key(const okey *k, uint32_t pos, const uint8_t *w, uint32_t wn, oacc *a) {
+    uint32_t plen = 0, cnt = 0;
+    if (pos) {
+        for (plen = 0; plen < k->len; plen++)
+            if (k->b[plen] == '/' && ++cnt == pos) break;
+    }
+    uint32_t need = plen + (pos ? 1 : 0) + wn;
+    if (need > a->scap) { a->scap = need * 2 + 64; a->scratch = realloc(a->scratch, a->scap); }
+    if (plen) memcpy(a->scratch, k->b, plen);
+    uint32_t o = plen;
+    if (pos) a->scratch[o++] = '/';
+    if (wn) memcpy(a->scratch + o, w, wn);
+    okey s; memset(&s, 0, sizeof s);
+    s.b = a->scratch; s.len = need; s.nw = pos + 1; s.form = FORM_LIST; s.base = 1;
+    return s;
+}
+
+/* search/3 + match_topics/4.  mode: 0 = all (traversal order), 1 = first only.
+ * returns number of matches, or -1 on badarg. */
+static int64_t walk(const oindex *h, const uint8_t *t, uint32_t tl, twords *tw, oacc *a, int first_only) {
+    if (topic_words(t, tl, tw) < 0) return -1;
+    okey base; memset(&base, 0, sizeof base);
+    base.form = FORM_LIST; base.base = 1;
+    if (tw->n[0] >= 1 && tw->p[0][0] == '$') {               /* base_init :160-163 */
+        base.b = tw->p[0]; base.len = tw->n[0]; base.nw = 1;
+    } else { base.b = (const uint8_t *)""; base.len = 0; base.nw = 0; }
+    int64_t cur = next_key(h, &base);
+    for (;;) {                                                /* search_new/search_up */
+        if (cur < 0) return a->n;                             /* '$end_of_table' */
+        const okey *k = &h->keys[cur];
+        int64_t c = compare(k, tw);
+        if (c == C_FULL) {
+            acc_add(a, k->id);
+            if (first_only) return a->n;
+            cur = next_key(h, k);
+        } else if (c == C_PREFIX) {
+            cur = next_key(h, k);
+        } else if (c == C_LOWER) {
+            break;
+        } else {
+            okey s = seek_key(k, (uint32_t)c, tw->p[c], tw->n[c], a);
+            cur = next_key(h, &s);
+        }
+    }
+    /* match_topics/4 (:381-389) */
+    okey tb; memset(&tb, 0, sizeof tb);
+    tb.b = t; tb.len = tl; tb.form = FORM_BIN; tb.base = 1;
+    for (;;) {
+        if (cur < 0) return a->n;
+        const okey *k = &h->keys[cur];
+        if (k->form == FORM_BIN && bin_cmp(k->b, k->len, t, tl) == 0) {
+            acc_add(a, k->id);
+            if (first_only) return a->n;
+            cur = next_key(h, k);
+        } else if (filter_cmp(k, &tb) < 0) {
+            cur = next_key(h, &tb);
+        } else return a->n;
+    }
+}
+
+static __thread twords *tls_tw;
+static twords *get_tw(void) { if (!tls_tw) tls_tw = malloc(sizeof(twords)); return tls_tw; }
+
+/* emqx_topic_index:matches/3 with [] opts, but in TRAVERSAL order (ascending
+ * term order); the reference's list is the reverse (match_add prepends). */
+int64_t orc_matches(void *hp, const char *t, uint32_t tl, uint32_t *out, int64_t cap) {
+    oindex *h = hp; flush(h);
+    oacc a = {out, 0, cap, 0, 0};
+    int64_t r = walk(h, (const uint8_t *)t, tl, get_tw(), &a, 0);
+    free(a.scratch);
+    return r;
+}
+
+/* emqx_topic_index:match/2: first key in traversal order. returns 1 + id in *out,
+ * 0 for false, -1 for badarg */
+int orc_first(void *hp, const char *t, uint32_t tl, uint32_t *out) {
+    oindex *h = hp; flush(h);
+    uint32_t id = 0;
+    oacc a = {&id, 0, 1, 0, 0};
+    int64_t r = walk(h, (const uint8_t *)t, tl, get_tw(), &a, 1);
+    free(a.scratch);
+    if (r < 0) return -1;
+    if (r == 0) return 0;
+    *out = id; return 1;
+}
+
+/* ---- batch (multithreaded, static topic partitioning) ---- */
+
+typedef struct {
+    const oindex *h; const char *blob; const uint64_t *offs;
+    int64_t lo, hi;
+    int64_t *counts; uint64_t *hashes;          /* per topic */
+    const int64_t *out_offs; uint32_t *out_ids; /* optional fill pass */
+    int64_t total;
+} batch_job;
+
+static void *batch_worker(void *p) {
+    batch_job *j = p;
+    twords *tw = malloc(sizeof(twords));
+    oacc a; memset(&a, 0, sizeof a);
+    uint32_t *tmp = 0; int64_t tcap = 0;
+    for (int64_t i = j->lo; i < j->hi; i++) {
+        const uint8_t *t = (const uint8_t *)j->blob + j->offs[i];
+        uint32_t tl = (uint32_t)(j->offs[i + 1] - j->offs[i]);
+        if (j->out_ids) { a.ids = j->out_ids + j->out_offs[i]; a.cap = j->out_offs[i + 1] - j->out_offs[i]; }
+        else { a.ids = tmp; a.cap = tcap; }
+        a.n = 0;
+        int64_t r = walk(j->h, t, tl, tw, &a, 0);
+        if (!j->out_ids && r > tcap) {           /* re-run into a big enough buffer for the hash */
+            tcap = r * 2 + 16; tmp = realloc(tmp, sizeof(uint32_t) * tcap);
+            a.ids = tmp; a.cap = tcap; a.n = 0;
+            r = walk(j->h, t, tl, tw, &a, 0);
+        }
+        if (j->counts) j->counts[i] = r;
+        if (j->hashes) {
+            uint64_t x = 0xcbf29ce484222325ull;
+            const uint32_t *ids = a.ids;
+            for (int64_t q = 0; q < (r > 0 ? r : 0); q++) { x ^= ids[q]; x *= 0x100000001b3ull; }
+            j->hashes[i] = r < 0 ? 0 : x;
+        }
+        if (r > 0) j->total += r;
+    }
+    free(a.scratch); free(tmp); free(tw);
+    return 0;
+}
+
+/* counts[i] = number of matches (-1 = badarg); hashes[i] = FNV-1a over the id
+ * sequence in traversal order.  If out_offs/out_ids are given, the ids are
+ * written there (out_offs from a prior counting call).  Returns total matches. */
+int64_t orc_match_batch(void *hp, const char *blob, const uint64_t *offs, int64_t n,
+                        int64_t *counts, uint64_t *hashes, const int64_t *out_offs,
+                        uint32_t *out_ids, int nthreads) {
+    oindex *h = hp; flush(h);
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    pthread_t th[256]; batch_job jb[256];
+    for (int t = 0; t < nthreads; t++) {
+        memset(&jb[t], 0, sizeof jb[t]);
+        jb[t].h = h; jb[t].blob = blob; jb[t].offs = offs;
+        jb[t].lo = n * t / nthreads; jb[t].hi = n * (t + 1) / nthreads;
+        jb[t].counts = counts; jb[t].hashes = hashes; jb[t].out_offs = out_offs; jb[t].out_ids = out_ids;
+        pthread_create(&th[t], 0, batch_worker, &jb[t]);
+    }
+    int64_t tot = 0;
+    for (int t = 0; t < nthreads; t++) { pthread_join(th[t], 0); tot += jb[t].total; }
+    return tot;
+}
+
+/* ---------------------------------------------- brute-force spec matcher */
+
+/* emqx_topic:match/2 (emqx_topic.erl:83-116) for a topic name and a filter.
+ * filter_words_form: the filter is a word list (no binary first-byte clause).
+ * Returns 1/0. Topic levels are assumed valid (no '+'/'#' levels). */
+int orc_spec_match(const char *t, uint32_t tl, const char *f, uint32_t fl, int filter_words_form) {
+    if (!filter_words_form && tl && fl && t[0] == '$' && (f[0] == '+' || f[0] == '#')) return 0; /* :83-86 */
+    uint32_t ti = 0, fi = 0, level = 0;
+    int tdone = 0, fdone = 0;
+    for (;; level++) {
+        /* next name word */
+        uint32_t ts = ti, te = ti; while (!tdone && te < tl && t[te] != '/') te++;
+        uint32_t fs = fi, fe = fi; while (!fdone && fe < fl && f[fe] != '/') fe++;
+        int fw_hash = !fdone && fe - fs == 1 && f[fs] == '#';
+        int fw_plus = !fdone && fe - fs == 1 && f[fs] == '+';
+        int f_last = !fdone && fe >= fl;
+        if (level == 0 && !tdone && te > ts && t[ts] == '$' && (fw_hash || fw_plus)) return 0; /* match_words :101-102 */
+        if (tdone && fdone) return 1;                                 /* [] [] */
+        if (fw_hash && f_last) return 1;                              /* _ ['#'] */
+        if (tdone || fdone) return 0;
+        if (!fw_plus) {
+            if (fw_hash) return 0;                                     /* '#' not last */
+            if (te - ts != fe - fs || memcmp(t + ts, f + fs, te - ts)) return 0;
+        }
+        if (te >= tl) tdone = 1; else ti = te + 1;
+        if (fe >= fl) fdone = 1; else fi = fe + 1;
+    }
+}
+
+/* ------------------------------------------ NFA frontier (roofline bytes) */
+
+/* A(topic) = 8 L + sum_{l<L} 32 |F_l| + 4 H + 4, where F_l are
+ * the live trie states entering level l (root = 1; the literal path and every
+ * live '+' branch).  A state is a word-list prefix P such that some word-list
+ * key starts with P (contiguous in term order from base(P)); the first-level
+ * '$' rule removes the root's '+' (base_init, emqx_trie_search.erl:160-163). */
+typedef struct { uint8_t *b; uint32_t len, nw; } pfx;
+
+static int prefix_exists(const oindex *h, const pfx *p) {
+    okey k; memset(&k, 0, sizeof k);
+    k.b = p->b; k.len = p->len; k.nw = p->nw; k.form = FORM_LIST; k.base = 1;
+    int64_t i = next_key(h, &k);
+    if (i < 0) return 0;
+    const okey *x = &h->keys[i];
+    if (x->form != FORM_LIST || x->nw < p->nw) return 0;
+    witer a, b; oword wa, wb;
+    wit_init(&a, &k); wit_init(&b, x);
+    for (uint32_t q = 0; q < p->nw; q++) {
+        wit_next(&a, &wa); wit_next(&b, &wb);
+        if (word_cmp(&wa, &wb)) return 0;
+    }
+    return 1;
+}
+
+static pfx pfx_ext(const pfx *p, const uint8_t *w, uint32_t wn) {
+    pfx r;
+    r.len = p->len + (p->nw ? 1 : 0) + wn; r.nw = p->nw + 1;
+    r.b = malloc(r.len + 1);
+    uint32_t o = 0;
+    if (p->len) { memcpy(r.b, p->b, p->len); o = p->len; }
+    if (p->nw) r.b[o++] = '/';
+    if (wn) memcpy(r.b + o, w, wn);
+    return r;
+}
+
+/* returns sum_{l<L} |F_l| (-1 on badarg); *levels = L */
+static int64_t frontier(const oindex *h, const uint8_t *t, uint32_t tl, twords *tw, uint32_t *levels) {
+    if (topic_words(t, tl, tw) < 0) return -1;
+    *levels = tw->nw;
+    int dollar = tw->n[0] >= 1 && tw->p[0][0] == '$';
+    int64_t cap = 16, n = 1, sum = 1;
+    pfx *cur = malloc(sizeof(pfx) * cap);
+    cur[0].b = malloc(1); cur[0].len = 0; cur[0].nw = 0;
+    for (uint32_t l = 0; l < tw->nw && n; l++) {
+        int64_t m = 0, mcap = 2 * n + 2;
+        pfx *nx = malloc(sizeof(pfx) * mcap);
+        for (int64_t i = 0; i < n; i++) {
+            if (!(l == 0 && dollar)) {
+                pfx c = pfx_ext(&cur[i], (const uint8_t *)"+", 1);
+                if (prefix_exists(h, &c)) nx[m++] = c; else free(c.b);
+            }
+            pfx c = pfx_ext(&cur[i], tw->p[l], tw->n[l]);
+            if (prefix_exists(h, &c)) nx[m++] = c; else free(c.b);
+        }
+        for (int64_t i = 0; i < n; i++) free(cur[i].b);
+        free(cur);
+        cur = nx; n = m;
+        if (l + 1 < tw->nw) sum += n;
+    }
+    for (int64_t i = 0; i < n; i++) free(cur[i].b);
+    free(cur);
+    return sum;
+}
+
+typedef struct {
+    const oindex *h; const char *blob; const uint64_t *offs; int64_t lo, hi;
+    uint32_t *levels; int64_t *states;
+} fr_job;
+
+static void *fr_worker(void *p) {
+    fr_job *j = p;
+    twords *tw = malloc(sizeof(twords));
+    for (int64_t i = j->lo; i < j->hi; i++) {
+        uint32_t L = 0;
+        j->states[i] = frontier(j->h, (const uint8_t *)j->blob + j->offs[i],
+                                (uint32_t)(j->offs[i + 1] - j->offs[i]), tw, &L);
+        j->levels[i] = L;
+    }
+    free(tw);
+    return 0;
+}
+
+void orc_frontier_batch(void *hp, const char *blob, const uint64_t *offs, int64_t n, uint32_t *levels,
+                        int64_t *states, int nthreads) {
+    oindex *h = hp; flush(h);
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    pthread_t th[256]; fr_job jb[256];
+    for (int t = 0; t < nthreads; t++) {
+        jb[t].h = h; jb[t].blob = blob; jb[t].offs = offs;
+        jb[t].lo = n * t / nthreads; jb[t].hi = n * (t + 1) / nthreads;
+        jb[t].levels = levels; jb[t].states = states;
+        pthread_create(&th[t], 0, fr_worker, &jb[t]);
+    }
+    for (int t = 0; t < nthreads; t++) pthread_join(th[t], 0);
+}

@@ -1,0 +1,90 @@
+"""Shared test harness: runs the golden known-answer cases against a backend.
+
+A backend turns (inserts, topic) into the matched keys in TRAVERSAL order
+(ascending Erlang term order), or raises BadArg.  Two backends exist:
+the CPU oracle (OracleBackend, here) and the GPU product path
+(emqx_amd.topic_index.Tab, in the gpu tests).
+"""
+from __future__ import annotations
+
+import json
+from pathlib import Path
+
+from emqx_amd.trie_search import BadArg, get_id, get_topic, key_order, make_key, term_key
+from emqx_amd.topic_index import _finish
+
+GOLDEN = json.loads((Path(__file__).parent / "golden" / "reference_vectors.json").read_text())
+
+
+def case_keys(case):
+    """keys of a case, and u32 values assigned in (ID, filter) term order so the
+    value order inside one filter is the ID term order."""
+    keys = []
+    for ins in case["inserts"]:
+        f, ident = ins[0].encode(), ins[1]
+        opts = ins[2] if len(ins) > 2 else {}
+        if opts.get("words"):
+            from emqx_amd.trie_search import filter as tfilter
+            k = make_key(tfilter(f), ident)
+        else:
+            k = make_key(f, ident)
+        if k not in keys:
+            keys.append(k)
+    ordered = sorted(keys, key=lambda k: (term_key(get_id(k)), key_order(k)))
+    return keys, {k: i for i, k in enumerate(ordered)}
+
+
+def encode_key(k):
+    f = k[0]
+    if isinstance(f, tuple):
+        if not f:
+            return b"", 2
+        return b"/".join(w.encode() if isinstance(w, str) else w for w in f), 1
+    return f, 0
+
+
+class OracleBackend:
+    def __init__(self, keys, kid):
+        from pyoracle import Oracle
+        self.o = Oracle()
+        self.by_kid = {v: k for k, v in kid.items()}
+        for k in keys:
+            f, fl = encode_key(k)
+            self.o.insert(f, kid[k], fl)
+
+    def traversal(self, topic: bytes):
+        r = self.o.matches(topic)
+        if r is None:
+            raise BadArg(topic)
+        return [self.by_kid[v] for v in r]
+
+
+def run_checks(case, traversal_fn):
+    """traversal_fn(topic) -> keys in traversal order.  Asserts every check."""
+    for chk in case["checks"]:
+        t = chk["topic"].encode()
+        kind = chk["kind"]
+        if kind == "badarg":
+            try:
+                traversal_fn(t)
+            except BadArg:
+                continue
+            raise AssertionError(f"{case['name']}: {t!r} should be badarg")
+        keys = traversal_fn(t)
+        assert keys == sorted(keys, key=key_order), f"{case['name']}: not in traversal order"
+        if kind == "match":
+            exp = chk["expect"]
+            got = False if not keys else [get_topic(keys[0]).decode(), get_id(keys[0])]
+            assert got == exp, (case["name"], t, got, exp)
+        elif kind == "match_id":
+            assert keys and get_id(keys[0]) == chk["expect"], (case["name"], t, keys)
+        elif kind == "sorted_topics":
+            got = [get_topic(k).decode() for k in keys]
+            assert got == chk["expect"], (case["name"], t, got)
+        elif kind == "ids":
+            got = [get_id(k) for k in _finish(keys, chk["opts"])]
+            assert got == chk["expect"], (case["name"], t, got, chk["expect"])
+        elif kind == "count":
+            assert len(keys) == chk["expect"], (case["name"], t, keys)
+        else:
+            raise AssertionError(kind)

@@ -1,0 +1,341 @@
+"""GPU parity: the MI355X path (libtmatch through its C ABI) against the CPU
+oracle (the reference's walk restated) and the reference's known answers.
+
+Integer/byte work: the bar is bit-exact -- the same values per topic in the
+same (traversal) order, the same badarg flags.
+"""
+import random
+
+import numpy as np
+import pytest
+
+from emqx_amd import _native, router as rt, topic_index as ti, workload as wl
+from emqx_amd.trie_search import BadArg, get_id, get_topic, topic_words
+from harness import GOLDEN, case_keys, encode_key, run_checks
+from pyoracle import Oracle
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch_dev():
+    import torch
+    assert torch.cuda.is_available(), "gpu tests need a HIP device"
+    return torch
+
+
+def gpu_index(items: wl.ItemSet | None = None, flags=None) -> _native.Index:
+    ix = _native.Index()
+    if items is not None and len(items):
+        ix.apply(np.ones(len(items), np.uint8), items.blob, items.offs, items.vals, flags)
+    return ix
+
+
+def oracle_of(items: wl.ItemSet, flags=None) -> Oracle:
+    o = Oracle()
+    o.apply(np.ones(len(items), np.uint8), items.blob, items.offs, items.vals, flags)
+    o.prepare()
+    return o
+
+
+def assert_same(ix: _native.Index, o: Oracle, topics: wl.ItemSet):
+    hit, vals, err = ix.match_batch(topics.blob, topics.offs)
+    cnt, _, ohit, ovals = o.match_batch(topics.blob, topics.offs)
+    assert np.array_equal(err.astype(bool), cnt < 0), "badarg flags differ"
+    gcnt = np.diff(hit.astype(np.int64))
+    bad = np.nonzero(gcnt != np.maximum(cnt, 0))[0]
+    assert len(bad) == 0, f"{len(bad)} topics differ in hit count, first {topics.item(int(bad[0]))!r}: " \
+                          f"gpu {gcnt[bad[0]]} oracle {cnt[bad[0]]}"
+    assert np.array_equal(vals, ovals), "hit values / order differ"
+    return hit, vals
+
+
+def items_of(strings, vals=None) -> wl.ItemSet:
+    blob, offs = _native.pack_strings(strings)
+    v = np.arange(len(strings), dtype=np.uint32) if vals is None else np.asarray(vals, np.uint32)
+    return wl.ItemSet(blob, offs, v, np.zeros(len(strings), np.uint8))
+
+
+# ------------------------------------------------------------ known answers
+
+@pytest.mark.parametrize("case", GOLDEN["index_cases"], ids=lambda c: c["name"])
+def test_golden_native(torch_dev, case):
+    keys, kid = case_keys(case)
+    ix = _native.Index()
+    by_kid = {v: k for k, v in kid.items()}
+    if keys:
+        enc = [encode_key(k) for k in keys]
+        blob, offs = _native.pack_strings([e[0] for e in enc])
+        ix.apply(np.ones(len(keys), np.uint8), blob, offs, np.array([kid[k] for k in keys], np.uint32),
+                 np.array([e[1] for e in enc], np.uint8))
+
+    def traversal(t):
+        blob, offs = _native.pack_strings([t])
+        hit, vals, err = ix.match_batch(blob, offs)
+        if err[0]:
+            raise BadArg(t)
+        return [by_kid[int(v)] for v in vals]
+
+    run_checks(case, traversal)
+
+
+@pytest.mark.parametrize("case", GOLDEN["index_cases"], ids=lambda c: c["name"])
+def test_golden_topic_index_api(torch_dev, case):
+    tab = ti.new()
+    from emqx_amd.trie_search import filter as tfilter
+    for ins in case["inserts"]:
+        f = ins[0].encode()
+        words = len(ins) > 2 and ins[2].get("words")
+        ti.insert(tfilter(f) if words else f, ins[1], b"", tab)
+    for chk in case["checks"]:
+        t = chk["topic"].encode()
+        if chk["kind"] == "badarg":
+            with pytest.raises(BadArg):
+                ti.match(t, tab)
+            continue
+        if chk["kind"] == "match":
+            m = ti.match(t, tab)
+            got = False if m is False else [get_topic(m).decode(), get_id(m)]
+            assert got == chk["expect"]
+        elif chk["kind"] == "match_id":
+            assert get_id(ti.match(t, tab)) == chk["expect"]
+        elif chk["kind"] == "sorted_topics":
+            ms = sorted(ti.matches(t, tab, []), key=ti.key_order)
+            assert [get_topic(k).decode() for k in ms] == chk["expect"]
+        elif chk["kind"] == "ids":
+            assert [get_id(k) for k in ti.matches(t, tab, chk["opts"])] == chk["expect"]
+        elif chk["kind"] == "count":
+            assert len(ti.matches(t, tab, [])) == chk["expect"]
+
+
+@pytest.mark.parametrize("case", GOLDEN["router_cases"], ids=lambda c: c["name"])
+def test_router_known_answers(torch_dev, case):
+    r = rt.Router(node="node")
+    for st in case["steps"]:
+        if "add" in st:
+            r.add_route(st["add"][0].encode(), st["add"][1])
+        elif "delete" in st:
+            r.delete_route(st["delete"][0].encode(), st["delete"][1])
+        elif "match_routes_sorted" in st:
+            got = sorted(r.match_routes(st["match_routes_sorted"].encode()), key=rt.route_order)
+            assert [[x.topic.decode(), x.dest] for x in got] == st["expect"]
+        elif "topics_sorted" in st:
+            assert sorted(t.decode() for t in r.topics()) == st["topics_sorted"]
+
+
+# ---------------------------------------------------------- random vs oracle
+
+def _rand_level(r):
+    c = r.random()
+    if c < 0.15:
+        return r.choice([b"foo", b"bar", b"baz", b"xyzzy"])
+    if c < 0.22:
+        return b""
+    if c < 0.27:
+        return b"$" + r.choice([b"SYS", b"a", b""])
+    if c < 0.30:
+        return r.choice([b"b+", b"c#", b"+x", b"#y", b"a-very-long-level-word-over-16-bytes"])
+    return ("%X" % r.randint(1, 16)).encode()
+
+
+def _rand_filter(r, levels):
+    out = []
+    for lvl in levels:
+        p = r.choices(["level", "+", "#"], [5, 2, 1])[0]
+        if p == "#":
+            out.append(b"#")
+            break
+        out.append(b"+" if p == "+" else lvl)
+    return b"/".join(out)
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_random_sets_vs_oracle(torch_dev, seed):
+    r = random.Random(0x454D5158 + 100 + seed)
+    topics = [b"/".join(_rand_level(r) for _ in range(r.randint(1, 12))) for _ in range(400)]
+    topics += [b"a/+/b", b"#", b"", b"/", b"$SYS", b"$"]
+    filters = []
+    for _ in range(500):
+        base = r.choice(topics).split(b"/")
+        filters.append(_rand_filter(r, [_rand_level(r) if r.random() < 0.3 else w for w in base]))
+    flags = np.array([r.random() < 0.2 for _ in filters], np.uint8)   # some word-list keys
+    fs = items_of(filters)
+    ix = gpu_index(fs, flags)
+    o = oracle_of(fs, flags)
+    ts = items_of(topics)
+    assert_same(ix, o, ts)
+    # deletes (and re-inserts) as deltas, then match again
+    dele = sorted(r.sample(range(len(filters)), 150))
+    ops = np.zeros(len(dele), np.uint8)
+    d = items_of([filters[i] for i in dele], dele)
+    ix.apply(ops, d.blob, d.offs, d.vals, flags[dele])
+    o.apply(ops, d.blob, d.offs, d.vals, flags[dele])
+    assert_same(ix, o, ts)
+    back = dele[::3]
+    d2 = items_of([filters[i] for i in back], back)
+    ix.apply(np.ones(len(back), np.uint8), d2.blob, d2.offs, d2.vals, flags[back])
+    o.apply(np.ones(len(back), np.uint8), d2.blob, d2.offs, d2.vals, flags[back])
+    assert_same(ix, o, ts)
+
+
+# ------------------------------------------------------------- configs
+
+def test_c1_full_vs_oracle(torch_dev):
+    fs = wl.filters(1, 10_000)
+    ts = wl.topics(1, 10_000, 100_000)
+    hit, _ = assert_same(gpu_index(fs), oracle_of(fs), ts)
+    assert hit[-1] > 100_000  # instantiated topics all hit at least once
+
+
+@pytest.mark.parametrize("cfg", [2, 20])
+def test_c2_reduced_vs_oracle(torch_dev, cfg):
+    fs = wl.filters(cfg, 50_000)
+    ts = wl.topics(cfg, 50_000, 50_000)
+    hit, _ = assert_same(gpu_index(fs), oracle_of(fs), ts)
+    per = np.diff(hit.astype(np.int64))
+    if cfg == 2:
+        assert per.min() >= 1000 and per.max() == 1001
+    else:
+        assert per.max() <= 1
+
+
+def test_c3_reduced_vs_oracle(torch_dev):
+    fs = wl.filters(3, 200_000)
+    ts = wl.topics(3, 200_000, 100_000)
+    assert_same(gpu_index(fs), oracle_of(fs), ts)
+
+
+def test_c5_churn_replay_vs_oracle(torch_dev):
+    nf = 20_000
+    fs = wl.filters(5, nf)
+    ix, o = gpu_index(fs), oracle_of(fs)
+    ts = wl.topics(5, nf, 20_000)
+    step = 2_000
+    for k in range(5):
+        d = wl.deltas(nf, k * step, step)
+        ix.apply(d.flags, d.blob, d.offs, d.vals)
+        o.apply(d.flags, d.blob, d.offs, d.vals)
+        assert_same(ix, o, ts)
+
+
+# ------------------------------------------------------------- edge cases
+
+def test_deep_topics_and_overflow(torch_dev):
+    letters = [chr(ord("a") + i).encode() for i in range(26)]
+    T = b"/".join(letters)                                  # 26 levels (mid path)
+    deep = b"/".join(b"l%d" % i for i in range(300))        # deep path
+    filters = [b"#", T + b"/#", T + b"/+", b"+/" * 26 + b"#", b"a/+/c/+/e/+/g/+/i/+/k/+/m/+/o/+/q/+/s/+/u/+/w/+/y/+/#",
+               deep, deep + b"/#", b"l0/+/#", b"+/l1/#", deep.rsplit(b"/", 1)[0] + b"/+",
+               b"a/#", b"+/#", b"+/+/#", b"a/b/#", b"+/b/#", b"a/+/#", b"a/b/+", b"+/+", b"a/+", b"+/b",
+               b"a/b", b"#", b"+/+/+/#"]
+    topics = [T, T + b"/1", deep, deep + b"/x", b"a/b", b"a/b/c", b"l0/l1", b"/".join([b"w"] * 1000),
+              b"/".join([b"+"] * 40), T + b"/#"]
+    fs = items_of(filters)
+    ix, o = gpu_index(fs), oracle_of(fs)
+    hit, _ = assert_same(ix, o, items_of(topics))
+    assert np.diff(hit.astype(np.int64))[4] > 8      # 'a/b' overflows the RCAP ranges
+
+
+def test_edge_topics(torch_dev):
+    long_word = b"x" * 40
+    filters = [b"", b"/", b"+", b"#", b"$SYS/#", b"$/+", b"+/+", long_word, long_word + b"/+",
+               b"/".join([b"e"] * 12), b"/".join([b"e"] * 12) + b"/#", b"\xff\x00/+", b"a/b\x00c",
+               b"$share/g/t/+", b"t/+"]
+    topics = [b"", b"/", b"//", b"$", b"$SYS", b"$SYS/x", b"$/a", long_word, long_word + b"/y",
+              b"/".join([b"e"] * 12), b"\xff\x00/z", b"a/b\x00c", b"a/b", b"+", b"a/#", b"t/1",
+              b"$share/g/t/1"]
+    fs = items_of(filters)
+    fl = np.array([0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 0, 0], np.uint8)
+    assert_same(gpu_index(fs, fl), oracle_of(fs, fl), items_of(topics))
+
+
+def test_empty_batch_and_index(torch_dev):
+    ix = gpu_index()
+    hit, vals, err = ix.match_batch(*_native.pack_strings([]))
+    assert hit.tolist() == [0] and len(vals) == 0
+    hit, vals, err = ix.match_batch(*_native.pack_strings([b"a/b", b"#"]))
+    assert hit.tolist() == [0, 0, 0] and err.tolist() == [0, 1]
+
+
+def test_first_batch_vs_oracle(torch_dev):
+    fs = wl.filters(3, 50_000)
+    ts = wl.topics(3, 50_000, 20_000)
+    ix, o = gpu_index(fs), oracle_of(fs)
+    val, found = ix.first_batch(ts.blob, ts.offs)
+    for i in range(0, len(ts), 7):
+        r, v = o.first(ts.item(i))
+        exp = {-1: 2, 0: 0, 1: 1}[r]
+        assert found[i] == exp, ts.item(i)
+        if r == 1:
+            assert val[i] == v
+
+
+def test_device_api_with_torch_stream(torch_dev):
+    torch = torch_dev
+    fs = wl.filters(3, 50_000)
+    ts = wl.topics(3, 50_000, 30_000)
+    ix = gpu_index(fs)
+    ref_hit, ref_vals, _ = ix.match_batch(ts.blob, ts.offs)
+    dev = torch.device("cuda:0")
+    blob = torch.from_numpy(ts.blob).to(dev)
+    offs = torch.from_numpy(ts.offs.view(np.int64)).to(dev)
+    n = len(ts)
+    hit = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    cap = int(ref_hit[-1])
+    out = torch.zeros(cap, dtype=torch.int32, device=dev)
+    err = torch.zeros(n, dtype=torch.uint8, device=dev)
+    s = torch.cuda.current_stream().cuda_stream
+    ix.match_batch_dev(n, blob.data_ptr(), offs.data_ptr(), hit.data_ptr(), out.data_ptr(), cap, err.data_ptr(), s)
+    torch.cuda.synchronize()
+    assert np.array_equal(hit.cpu().numpy().view(np.uint64), ref_hit)
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), ref_vals)
+    # capacity too small: values beyond cap are dropped, total still reported
+    out2 = torch.zeros(10, dtype=torch.int32, device=dev)
+    ix.match_batch_dev(n, blob.data_ptr(), offs.data_ptr(), hit.data_ptr(), out2.data_ptr(), 10, err.data_ptr(), s)
+    torch.cuda.synchronize()
+    assert int(hit[-1]) == cap
+    assert np.array_equal(out2.cpu().numpy().view(np.uint32), ref_vals[:10])
+
+
+def test_stats_and_idempotence(torch_dev):
+    ix = gpu_index()
+    d = items_of([b"a/+", b"a/+", b"a/b", b"a/#/b", b"x"], [1, 1, 2, 3, 4])
+    ix.apply(np.ones(5, np.uint8), d.blob, d.offs, d.vals)
+    st = ix.stats()
+    assert (st["n_wild_keys"], st["n_exact_keys"], st["n_dead_keys"]) == (1, 2, 1)
+    ix.apply(np.zeros(5, np.uint8), d.blob, d.offs, d.vals)
+    missing = items_of([b"never/there", b"never/+"])
+    ix.apply(np.zeros(2, np.uint8), missing.blob, missing.offs, missing.vals)   # not an error
+    st = ix.stats()
+    assert st["n_keys"] == 0 and st["n_nodes"] == 1 and st["n_edges"] == 0
+    hit, vals, err = ix.match_batch(*_native.pack_strings([b"a/b", b"x"]))
+    assert hit.tolist() == [0, 0, 0]
+
+
+def test_c3_scale_properties(torch_dev):
+    """2M filters, 1M topics: exact CSR vs the oracle on a 20k-topic sample, plus
+    size-independent properties over the whole batch."""
+    nf = 2_000_000
+    fs = wl.filters(3, nf)
+    ts = wl.topics(3, nf, 1_000_000)
+    ix = gpu_index(fs)
+    hit, vals, err = ix.match_batch(ts.blob, ts.offs)
+    hit2, vals2, _ = ix.match_batch(ts.blob, ts.offs)
+    assert np.array_equal(hit, hit2) and np.array_equal(vals, vals2)           # deterministic
+    assert not err.any()
+    per = np.diff(hit.astype(np.int64))
+    assert (per >= 0).all()
+    o = oracle_of(fs)
+    idx = np.random.default_rng(7).choice(len(ts), 20_000, replace=False)
+    sample = items_of([ts.item(int(i)) for i in idx])
+    cnt, _, ohit, ovals = o.match_batch(sample.blob, sample.offs)
+    for j, i in enumerate(idx):
+        g = vals[int(hit[i]):int(hit[i + 1])]
+        e = ovals[int(ohit[j]):int(ohit[j + 1])]
+        assert np.array_equal(g, e), ts.item(int(i))
+    # '$SYS' topics never hit the root globals '#' (value nf) / '+/#' (value nf + 1)
+    sys_rows = [i for i in range(0, len(ts), 97) if ts.item(i).startswith(b"$")]
+    assert sys_rows
+    for i in sys_rows:
+        g = vals[int(hit[i]):int(hit[i + 1])]
+        assert nf not in g and nf + 1 not in g

@@ -1,0 +1,82 @@
+"""Host-side logic that needs no GPU: key helpers, term order, workloads."""
+import numpy as np
+
+from emqx_amd import workload as wl
+from emqx_amd.topic_index import Tab, _finish
+from emqx_amd.trie_search import (HASH, PLUS, BadArg, filter as tfilter, get_id, get_topic, key_order,
+                                  make_key, term_key, topic_words)
+
+
+def test_make_key_forms():
+    assert make_key(b"a/b", 1) == (b"a/b", (1,))
+    assert make_key(b"a/+/#", 1) == ((b"a", PLUS, HASH), (1,))
+    assert make_key([b"a", b"b"], 1) == ((b"a", b"b"), (1,))
+    assert get_topic(make_key(b"sensor/+/metric//#", 3)) == b"sensor/+/metric//#"
+    assert tfilter(b"") is False
+
+
+def test_topic_words_badarg():
+    for t in (b"+", b"#", b"a/+/b", b"a/b/#"):
+        try:
+            topic_words(t)
+        except BadArg:
+            continue
+        raise AssertionError(t)
+    assert topic_words(b"a/b/b+") == [b"a", b"b", b"b+"]
+
+
+def test_term_order():
+    # numbers < atoms < tuples < lists < binaries; '#' < '+' < binary words
+    xs = [b"a", [1], ("x",), "atom", 5]
+    assert sorted(xs, key=term_key) == [5, "atom", ("x",), [1], b"a"]
+    k1, k2, k3 = make_key(b"a/#", 1), make_key(b"a/+", 1), make_key(b"a/b/+", 1)
+    k4 = make_key(b"a/b", 1)
+    assert sorted([k4, k3, k2, k1], key=key_order) == [k1, k2, k3, k4]
+
+
+def test_finish_orders_like_reference():
+    keys = [make_key(b"a/+/#", 8), make_key(b"a/+/+", 7), make_key(b"a/b/#", 2), make_key(b"a/b/#", 3),
+            make_key(b"a/b/+", 5), make_key(b"a/b/c", 4)]
+    assert [get_id(k) for k in _finish(keys, ["unique"])] == [2, 3, 4, 5, 7, 8]
+    assert _finish(keys, [])[0] == make_key(b"a/b/c", 4)
+
+
+def test_encode_dead_word_lists():
+    assert Tab._encode(((b"a/b", PLUS), (1,))) is None
+    assert Tab._encode(((b"+",), (1,))) is None
+    assert Tab._encode(((), (1,))) == (b"", 2)
+    assert Tab._encode(((b"a", PLUS), (1,))) == (b"a/+", 1)
+
+
+def test_workload_deterministic_and_sharded():
+    a = wl.filters(3, 5000)
+    b = wl.filters(3, 5000)
+    assert a.items() == b.items()
+    assert len(a) == 5002  # + the '#' and '+/#' globals
+    parts = [wl.filters(3, 5000, shard=s, nshards=4) for s in range(4)]
+    merged = sorted(sum((list(zip(p.vals.tolist(), p.items())) for p in parts), []))
+    assert merged == sorted(zip(a.vals.tolist(), a.items()))
+    t = wl.topics(3, 5000, 2000)
+    assert len(t) == 2000
+    assert any(x.startswith(b"$SYS/") for x in t.items())
+
+
+def test_workload_c2_shape():
+    f = wl.filters(2, 1000)
+    items = f.items()
+    assert items[0] == b"fleet/0/sensor/+" and items[999] == b"fleet/999/sensor/+"
+    assert items[1000:1250] == [b"#"] * 250 and items[1250] == b"fleet/#"
+    t = wl.topics(2, 1000, 100).items()
+    assert all(x.startswith(b"fleet/") and x.split(b"/")[2] == b"sensor" for x in t)
+
+
+def test_workload_deltas_remove_live_keys_once():
+    d = wl.deltas(1000, 0, 2000)
+    subs = d.flags == 1
+    assert subs.sum() == 1000
+    dels = d.vals[~subs]
+    assert len(set(dels.tolist())) == len(dels) and dels.max() < 1000
+    base = wl.filters(5, 1000)
+    base_keys = set(zip(base.items(), base.vals.tolist()))
+    for i in np.nonzero(~subs)[0][:50]:
+        assert (d.item(i), int(d.vals[i])) in base_keys
