@@ -12,7 +12,7 @@ struct DevIndex {
     const VocabEntry *vocab; uint32_t vmask;
     const uint8_t *wpool;
     const Node *nodes;
-    const Edge *edges; uint32_t emask;
+    const CSlot *ctab;
     const uint32_t *vals;
     const ExactEntry *exact; uint32_t xmask;
     const uint32_t *wseq;

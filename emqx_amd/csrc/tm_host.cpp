@@ -61,7 +61,7 @@ struct Mirror {
 };
 
 struct NodeAux {
-    uint32_t parent = NONE, wid = NONE, nlit = 0, hash_cap = 0, exact_cap = 0;
+    uint32_t parent = NONE, wid = NONE, hash_cap = 0, exact_cap = 0;
     uint8_t is_plus = 0;
 };
 
@@ -78,7 +78,7 @@ struct tm_index {
     Mirror<VocabEntry> vocab; uint64_t vcount = 0;
     Mirror<uint8_t> wpool;
     Mirror<Node> nodes; std::vector<NodeAux> aux; std::vector<uint32_t> free_nodes; uint64_t live_nodes = 0;
-    Mirror<Edge> edges; uint64_t ecount = 0;
+    Mirror<CSlot> ctab; std::vector<uint32_t> free_ctab[33]; uint64_t nlinks = 0, ntables = 0;
     Mirror<uint32_t> vals; std::vector<uint32_t> free_blocks[33];
     Mirror<ExactEntry> exact; std::vector<uint32_t> xcap; uint64_t xcount = 0;
     Mirror<uint32_t> wseq;
@@ -144,14 +144,19 @@ uint32_t pow2_at_least(uint64_t x) {
 
 // ------------------------------------------------------------------ vocab
 
+void pack8(const uint8_t *p, uint32_t n, uint32_t &b0, uint32_t &b1) {
+    b0 = b1 = 0;
+    for (uint32_t i = 0; i < n && i < 8; i++) (i < 4 ? b0 : b1) |= (uint32_t)p[i] << (8 * (i % 4));
+}
+
 bool vocab_eq(tm_index *ix, const VocabEntry &e, uint64_t h, const uint8_t *p, uint32_t n) {
-    if (e.h_lo != (uint32_t)h || e.h_hi != (uint32_t)(h >> 32) || e.len != n) return false;
+    if (e.tag != vocab_tag(h, n)) return false;
     if (n <= VINL) {
-        uint32_t b[4] = {0, 0, 0, 0};
-        for (uint32_t i = 0; i < n; i++) b[i / 4] |= (uint32_t)p[i] << (8 * (i % 4));
-        return !memcmp(b, e.b, 16);
+        uint32_t b0, b1;
+        pack8(p, n, b0, b1);
+        return e.b0 == b0 && e.b1 == b1;
     }
-    return !memcmp(ix->wpool.h.data() + e.b[0], p, n);
+    return e.b1 == n && !memcmp(ix->wpool.h.data() + e.b0, p, n);
 }
 
 uint32_t vocab_find(tm_index *ix, const uint8_t *p, uint32_t n) {
@@ -164,19 +169,31 @@ uint32_t vocab_find(tm_index *ix, const uint8_t *p, uint32_t n) {
     }
 }
 
-void vocab_place(std::vector<VocabEntry> &t, const VocabEntry &e) {
-    const uint32_t mask = (uint32_t)t.size() - 1;
-    uint64_t h = ((uint64_t)e.h_hi << 32) | e.h_lo;
-    for (uint32_t s = (uint32_t)h & mask;; s = (s + 1) & mask)
-        if (t[s].wid == NONE) { t[s] = e; return; }
-}
-
 VocabEntry empty_vocab() { VocabEntry e; memset(&e, 0, sizeof e); e.wid = NONE; return e; }
+
+// the word bytes of an entry (for rehashing)
+void vocab_bytes(tm_index *ix, const VocabEntry &e, std::string &out) {
+    uint32_t n = e.tag & 0xFF;
+    if (n < VINL + 1) {
+        out.resize(n);
+        for (uint32_t i = 0; i < n; i++) out[i] = (char)(((i < 4 ? e.b0 : e.b1) >> (8 * (i % 4))) & 0xFF);
+    } else {
+        out.assign(reinterpret_cast<const char *>(ix->wpool.h.data() + e.b0), e.b1);
+    }
+}
 
 void vocab_grow(tm_index *ix, uint64_t need) {
     if (need * 2 <= ix->vocab.h.size()) return;
     std::vector<VocabEntry> nt(pow2_at_least(need * 2), empty_vocab());
-    for (const VocabEntry &e : ix->vocab.h) if (e.wid != NONE) vocab_place(nt, e);
+    const uint32_t mask = (uint32_t)nt.size() - 1;
+    std::string w;
+    for (const VocabEntry &e : ix->vocab.h) {
+        if (e.wid == NONE) continue;
+        vocab_bytes(ix, e, w);
+        const uint64_t h = word_hash(reinterpret_cast<const uint8_t *>(w.data()), (uint32_t)w.size());
+        for (uint32_t s = (uint32_t)h & mask;; s = (s + 1) & mask)
+            if (nt[s].wid == NONE) { nt[s] = e; break; }
+    }
     ix->vocab.h.swap(nt);
     ix->vocab.dirty.set_all();
 }
@@ -187,15 +204,17 @@ uint32_t vocab_intern(tm_index *ix, const uint8_t *p, uint32_t n) {
     vocab_grow(ix, ix->vcount + 1);
     VocabEntry e = empty_vocab();
     const uint64_t h = word_hash(p, n);
-    e.h_lo = (uint32_t)h; e.h_hi = (uint32_t)(h >> 32); e.len = n; e.wid = (uint32_t)ix->vcount;
+    e.tag = vocab_tag(h, n);
+    e.wid = (uint32_t)ix->vcount;
     if (n <= VINL) {
-        for (uint32_t i = 0; i < n; i++) e.b[i / 4] |= (uint32_t)p[i] << (8 * (i % 4));
+        pack8(p, n, e.b0, e.b1);
     } else {
         uint64_t off = ix->wpool.h.size();
         ix->wpool.h.resize(off + ((n + 3) & ~3u), 0);
         memcpy(ix->wpool.h.data() + off, p, n);
         ix->wpool.touch(off, (n + 3) & ~3u);
-        e.b[0] = (uint32_t)off;
+        e.b0 = (uint32_t)off;
+        e.b1 = n;
     }
     const uint32_t mask = (uint32_t)ix->vocab.h.size() - 1;
     for (uint32_t s = (uint32_t)h & mask;; s = (s + 1) & mask)
@@ -204,58 +223,51 @@ uint32_t vocab_intern(tm_index *ix, const uint8_t *p, uint32_t n) {
     return e.wid;
 }
 
-// ------------------------------------------------------------------ edges
+// ------------------------------------------------- private child tables
 
-Edge empty_edge() { return Edge{NONE, 0, 0, 0}; }
+uint32_t cls_of(uint32_t cap);
 
-uint32_t edge_find_slot(tm_index *ix, uint32_t parent, uint32_t wid) {
-    const uint32_t mask = (uint32_t)ix->edges.h.size() - 1;
-    for (uint32_t s = edge_slot(parent, wid, mask);; s = (s + 1) & mask) {
-        const Edge &e = ix->edges.h[s];
-        if (e.parent == NONE) return NONE;
-        if (e.parent == parent && e.wid == wid) return s;
+uint32_t ctab_alloc(tm_index *ix, uint32_t cap) {
+    auto &fl = ix->free_ctab[cls_of(cap)];
+    uint32_t o;
+    if (!fl.empty()) { o = fl.back(); fl.pop_back(); }
+    else { o = (uint32_t)ix->ctab.h.size(); ix->ctab.h.resize(o + cap); }
+    for (uint32_t i = 0; i < cap; i++) ix->ctab.h[o + i] = CSlot{NONE, NONE};
+    ix->ctab.touch(o, cap);
+    ix->ntables++;
+    return o;
+}
+
+void ctab_free(tm_index *ix, uint32_t off, uint32_t cap) {
+    ix->free_ctab[cls_of(cap)].push_back(off);
+    ix->ntables--;
+}
+
+void ctab_put(tm_index *ix, uint32_t off, uint32_t mask, uint32_t wid, uint32_t child) {
+    for (uint32_t s = child_hash(wid) & mask;; s = (s + 1) & mask)
+        if (ix->ctab.h[off + s].wid == NONE) { ix->ctab.h[off + s] = CSlot{wid, child}; ix->ctab.touch(off + s); return; }
+}
+
+uint32_t ctab_find(tm_index *ix, uint32_t off, uint32_t mask, uint32_t wid) {
+    for (uint32_t s = child_hash(wid) & mask;; s = (s + 1) & mask) {
+        const CSlot &c = ix->ctab.h[off + s];
+        if (c.wid == NONE) return NONE;
+        if (c.wid == wid) return s;
     }
 }
 
-void edge_grow(tm_index *ix, uint64_t need) {
-    if (need * 2 <= ix->edges.h.size()) return;
-    std::vector<Edge> nt(pow2_at_least(need * 2), empty_edge());
-    const uint32_t mask = (uint32_t)nt.size() - 1;
-    for (const Edge &e : ix->edges.h) {
-        if (e.parent == NONE) continue;
-        for (uint32_t s = edge_slot(e.parent, e.wid, mask);; s = (s + 1) & mask)
-            if (nt[s].parent == NONE) { nt[s] = e; break; }
-    }
-    ix->edges.h.swap(nt);
-    ix->edges.dirty.set_all();
-}
-
-void edge_insert(tm_index *ix, uint32_t parent, uint32_t wid, uint32_t child) {
-    edge_grow(ix, ix->ecount + 1);
-    const uint32_t mask = (uint32_t)ix->edges.h.size() - 1;
-    for (uint32_t s = edge_slot(parent, wid, mask);; s = (s + 1) & mask)
-        if (ix->edges.h[s].parent == NONE) {
-            ix->edges.h[s] = Edge{parent, wid, child, 0};
-            ix->edges.touch(s);
-            break;
-        }
-    ix->ecount++;
-}
-
-// linear probing, backward-shift deletion (no tombstones on the device side)
-void edge_erase(tm_index *ix, uint32_t parent, uint32_t wid) {
-    uint32_t i = edge_find_slot(ix, parent, wid);
+// backward-shift deletion inside one private table
+void ctab_erase(tm_index *ix, uint32_t off, uint32_t mask, uint32_t wid) {
+    uint32_t i = ctab_find(ix, off, mask, wid);
     if (i == NONE) return;
-    auto &t = ix->edges.h;
-    const uint32_t mask = (uint32_t)t.size() - 1;
-    for (uint32_t j = (i + 1) & mask; t[j].parent != NONE; j = (j + 1) & mask) {
-        uint32_t k = edge_slot(t[j].parent, t[j].wid, mask);
+    CSlot *t = ix->ctab.h.data() + off;
+    for (uint32_t j = (i + 1) & mask; t[j].wid != NONE; j = (j + 1) & mask) {
+        uint32_t k = child_hash(t[j].wid) & mask;
         bool stays = (i <= j) ? (i < k && k <= j) : (i < k || k <= j);
-        if (!stays) { t[i] = t[j]; ix->edges.touch(i); i = j; }
+        if (!stays) { t[i] = t[j]; ix->ctab.touch(off + i); i = j; }
     }
-    t[i] = empty_edge();
-    ix->edges.touch(i);
-    ix->ecount--;
+    t[i] = CSlot{NONE, NONE};
+    ix->ctab.touch(off + i);
 }
 
 // ------------------------------------------------------------- value runs
@@ -313,6 +325,7 @@ uint32_t node_new(tm_index *ix, uint32_t parent, uint32_t wid, bool is_plus) {
     if (!ix->free_nodes.empty()) { id = ix->free_nodes.back(); ix->free_nodes.pop_back(); }
     else { id = (uint32_t)ix->nodes.h.size(); ix->nodes.h.emplace_back(); ix->aux.emplace_back(); }
     Node nd; memset(&nd, 0, sizeof nd); nd.plus = NONE;
+    for (uint32_t k = 0; k < KINL; k++) { nd.kw[k] = NONE; nd.kc[k] = NONE; }
     ix->nodes.h[id] = nd;
     ix->nodes.touch(id);
     NodeAux a; a.parent = parent; a.wid = wid; a.is_plus = is_plus;
@@ -321,16 +334,88 @@ uint32_t node_new(tm_index *ix, uint32_t parent, uint32_t wid, bool is_plus) {
     return id;
 }
 
+// literal child of `node` for word `wid`
+uint32_t child_find(tm_index *ix, uint32_t node, uint32_t wid) {
+    const Node &n = ix->nodes.h[node];
+    if (n.nlit <= KINL) {
+        for (uint32_t k = 0; k < KINL; k++) if (n.kw[k] == wid) return n.kc[k];
+        return NONE;
+    }
+    uint32_t s = ctab_find(ix, n.kw[0], n.kw[1], wid);
+    return s == NONE ? NONE : ix->ctab.h[n.kw[0] + s].child;
+}
+
+void set_bloom(Node &n, uint32_t wid) {
+    uint32_t b = child_bit(child_hash(wid));
+    if (b < 32) n.mask_lo |= 1u << b; else n.mask_hi |= 1u << (b - 32);
+}
+
+// move a node's children into a private table of `cap` slots (cap = pow2)
+void to_table(tm_index *ix, uint32_t node, uint32_t cap) {
+    Node &n = ix->nodes.h[node];
+    std::vector<CSlot> kids;
+    if (n.nlit <= KINL) {
+        for (uint32_t k = 0; k < KINL; k++) if (n.kw[k] != NONE) kids.push_back({n.kw[k], n.kc[k]});
+    } else {
+        for (uint32_t i = 0; i <= n.kw[1]; i++) if (ix->ctab.h[n.kw[0] + i].wid != NONE) kids.push_back(ix->ctab.h[n.kw[0] + i]);
+        ctab_free(ix, n.kw[0], n.kw[1] + 1);
+    }
+    uint32_t off = ctab_alloc(ix, cap);
+    Node &m = ix->nodes.h[node];
+    m.mask_lo = m.mask_hi = 0;
+    for (auto &c : kids) { ctab_put(ix, off, cap - 1, c.wid, c.child); set_bloom(m, c.wid); }
+    for (uint32_t k = 0; k < KINL; k++) { m.kw[k] = NONE; m.kc[k] = NONE; }
+    m.kw[0] = off; m.kw[1] = cap - 1;
+}
+
+void child_add(tm_index *ix, uint32_t node, uint32_t wid, uint32_t child) {
+    ix->nlinks++;
+    Node *n = &ix->nodes.h[node];
+    if (n->nlit < KINL) {
+        for (uint32_t k = 0; k < KINL; k++)
+            if (n->kw[k] == NONE) { n->kw[k] = wid; n->kc[k] = child; break; }
+    } else {
+        if (n->nlit == KINL) to_table(ix, node, 16);
+        else if ((n->nlit + 1) * 2 > n->kw[1] + 1) to_table(ix, node, (n->kw[1] + 1) * 2);
+        n = &ix->nodes.h[node];
+        ctab_put(ix, n->kw[0], n->kw[1], wid, child);
+        set_bloom(*n, wid);
+    }
+    n->nlit++;
+    ix->nodes.touch(node);
+}
+
+void child_remove(tm_index *ix, uint32_t node, uint32_t wid) {
+    ix->nlinks--;
+    Node &n = ix->nodes.h[node];
+    if (n.nlit <= KINL) {
+        for (uint32_t k = 0; k < KINL; k++)
+            if (n.kw[k] == wid) { n.kw[k] = NONE; n.kc[k] = NONE; break; }
+        n.nlit--;
+    } else {
+        ctab_erase(ix, n.kw[0], n.kw[1], wid);
+        n.nlit--;
+        if (n.nlit == KINL) {   // back to inline mode
+            std::vector<CSlot> kids;
+            for (uint32_t i = 0; i <= n.kw[1]; i++) if (ix->ctab.h[n.kw[0] + i].wid != NONE) kids.push_back(ix->ctab.h[n.kw[0] + i]);
+            ctab_free(ix, n.kw[0], n.kw[1] + 1);
+            for (uint32_t k = 0; k < KINL; k++) { n.kw[k] = kids[k].wid; n.kc[k] = kids[k].child; }
+            n.mask_lo = n.mask_hi = 0;
+        }
+    }
+    ix->nodes.touch(node);
+}
+
 bool node_empty(tm_index *ix, uint32_t id) {
     const Node &n = ix->nodes.h[id];
-    return n.plus == NONE && ix->aux[id].nlit == 0 && n.hash_cnt == 0 && n.exact_cnt == 0;
+    return n.plus == NONE && n.nlit == 0 && n.hash_cnt == 0 && n.exact_cnt == 0;
 }
 
 void node_prune(tm_index *ix, uint32_t id) {
     while (id != ROOT && node_empty(ix, id)) {
         NodeAux a = ix->aux[id];
         if (a.is_plus) { ix->nodes.h[a.parent].plus = NONE; ix->nodes.touch(a.parent); }
-        else { edge_erase(ix, a.parent, a.wid); ix->aux[a.parent].nlit--; }
+        else child_remove(ix, a.parent, a.wid);
         ix->free_nodes.push_back(id);
         ix->live_nodes--;
         id = a.parent;
@@ -493,15 +578,11 @@ void key_op(tm_index *ix, bool ins, const uint8_t *f, uint32_t len, uint32_t v, 
         } else {
             uint32_t wid = ins ? vocab_intern(ix, w[i].p, w[i].n) : vocab_find(ix, w[i].p, w[i].n);
             if (wid == NONE) return;
-            uint32_t s = edge_find_slot(ix, node, wid);
-            uint32_t c;
-            if (s == NONE) {
+            uint32_t c = child_find(ix, node, wid);
+            if (c == NONE) {
                 if (!ins) return;
                 c = node_new(ix, node, wid, false);
-                edge_insert(ix, node, wid, c);
-                ix->aux[node].nlit++;
-            } else {
-                c = ix->edges.h[s].child;
+                child_add(ix, node, wid, c);
             }
             node = c;
         }
@@ -574,7 +655,7 @@ int sync_locked(tm_index *ix, hipStream_t s) {
     if ((rc = collect(ix, ix->vocab, addr, val))) return rc;
     if ((rc = collect(ix, ix->wpool, addr, val))) return rc;
     if ((rc = collect(ix, ix->nodes, addr, val))) return rc;
-    if ((rc = collect(ix, ix->edges, addr, val))) return rc;
+    if ((rc = collect(ix, ix->ctab, addr, val))) return rc;
     if ((rc = collect(ix, ix->vals, addr, val))) return rc;
     if ((rc = collect(ix, ix->exact, addr, val))) return rc;
     if ((rc = collect(ix, ix->wseq, addr, val))) return rc;
@@ -612,7 +693,7 @@ DevIndex dev_view(tm_index *ix) {
     d.vocab = ix->vocab.d; d.vmask = (uint32_t)ix->vocab.h.size() - 1;
     d.wpool = ix->wpool.d;
     d.nodes = ix->nodes.d;
-    d.edges = ix->edges.d; d.emask = (uint32_t)ix->edges.h.size() - 1;
+    d.ctab = ix->ctab.d;
     d.vals = ix->vals.d;
     d.exact = ix->exact.d; d.xmask = (uint32_t)ix->exact.h.size() - 1;
     d.wseq = ix->wseq.d;
@@ -653,11 +734,13 @@ int ensure_ws(tm_index *ix, uint64_t n, hipStream_t s) {
 }
 
 void init_tables(tm_index *ix, uint64_t hint) {
-    ix->vocab.h.assign(pow2_at_least(std::max<uint64_t>(hint, 64)), empty_vocab());
-    ix->edges.h.assign(pow2_at_least(std::max<uint64_t>(hint * 2, 64)), empty_edge());
-    ix->exact.h.assign(pow2_at_least(std::max<uint64_t>(hint * 2, 64)), empty_exact());
+    // tables start small and double at load 1/2: their size follows the live
+    // key set, so hot entries stay dense (vocab / top trie levels in L2)
+    ix->vocab.h.assign(1024, empty_vocab());
+    ix->exact.h.assign(1024, empty_exact());
     ix->xcap.assign(ix->exact.h.size(), 0);
-    ix->nodes.h.reserve(hint + 1);
+    ix->nodes.h.reserve(hint / 2 + 1);
+    ix->aux.reserve(hint / 2 + 1);
     node_new(ix, NONE, NONE, false);   // ROOT
     ix->vals.h.reserve(hint + 16);
 }
@@ -721,7 +804,7 @@ int tm_destroy(tm_index *ix) {
     if (!ix) return TM_EINVAL;
     (void)hipSetDevice(ix->device);
     (void)hipStreamSynchronize(ix->stream);
-    void *bufs[] = {ix->vocab.d, ix->wpool.d, ix->nodes.d, ix->edges.d, ix->vals.d, ix->exact.d, ix->wseq.d,
+    void *bufs[] = {ix->vocab.d, ix->wpool.d, ix->nodes.d, ix->ctab.d, ix->vals.d, ix->exact.d, ix->wseq.d,
                     ix->dev_addr, ix->dev_val, ix->ws.cnt, ix->ws.nr, ix->ws.rng, ix->ws.lists, ix->ws.list_n,
                     ix->ws.blk, ix->ws.deep_wid, ix->ws.deep_stk, ix->d_topics, ix->d_offs, ix->d_hit,
                     ix->d_err, ix->d_out};
@@ -926,10 +1009,10 @@ int tm_stats(tm_index *ix, tm_stats_t *o) {
     o->n_dead_keys = ix->dead.size();
     o->n_keys = ix->n_wild + ix->n_exact + ix->dead.size();
     o->n_nodes = ix->live_nodes;
-    o->n_edges = ix->ecount;
+    o->n_edges = ix->nlinks;
     o->n_words = ix->vcount;
     o->device_bytes = ix->vocab.dcap * sizeof(VocabEntry) + ix->wpool.dcap + ix->nodes.dcap * sizeof(Node) +
-                      ix->edges.dcap * sizeof(Edge) + ix->vals.dcap * 4 + ix->exact.dcap * sizeof(ExactEntry) +
+                      ix->ctab.dcap * sizeof(CSlot) + ix->vals.dcap * 4 + ix->exact.dcap * sizeof(ExactEntry) +
                       ix->wseq.dcap * 4;
     o->uploads = ix->uploads;
     o->patch_bytes = ix->patch_bytes;

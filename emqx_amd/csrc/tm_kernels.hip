@@ -34,15 +34,15 @@ __device__ __forceinline__ uint4 ld4(const void *p) { return *reinterpret_cast<c
 
 struct WordAcc {
     uint64_t h;
-    uint32_t len, b0, b1, b2, b3;
+    uint32_t len, b0, b1;
     uint64_t start;
     __device__ __forceinline__ void reset(uint64_t s) {
-        h = FNV_OFF; len = 0; b0 = b1 = b2 = b3 = 0; start = s;
+        h = FNV_OFF; len = 0; b0 = b1 = 0; start = s;
     }
     __device__ __forceinline__ void push(uint32_t c) {
         h = (h ^ c) * FNV_PRIME;
         uint32_t v = c << ((len & 3) * 8);
-        if (len < 4) b0 |= v; else if (len < 8) b1 |= v; else if (len < 12) b2 |= v; else if (len < 16) b3 |= v;
+        if (len < 4) b0 |= v; else if (len < 8) b1 |= v;
         len++;
     }
 };
@@ -52,32 +52,32 @@ __device__ bool bytes_eq(const uint8_t *a, const uint8_t *b, uint32_t n) {
     return true;
 }
 
-// vocab: word -> wid, exact by construction (64-bit hash, then length and bytes)
+// vocab: word -> wid, exact by construction (hash tag, then length and bytes)
 __device__ uint32_t vocab_find(const DevIndex &ix, const WordAcc &w, const uint8_t *blob) {
     const uint64_t h = word_hash_finish(w.h, w.len);
+    const uint32_t tag = vocab_tag(h, w.len);
     uint32_t slot = (uint32_t)h & ix.vmask;
     for (;;) {
-        const uint4 *e = reinterpret_cast<const uint4 *>(ix.vocab + slot);
-        uint4 a = e[0], b = e[1];
-        if (a.z == NONE) return NONE;
-        if (a.x == (uint32_t)h && a.y == (uint32_t)(h >> 32) && a.w == w.len) {
+        const uint4 e = ld4(ix.vocab + slot);   // tag, wid, b0, b1
+        if (e.y == NONE) return NONE;
+        if (e.x == tag) {
             if (w.len <= VINL) {
-                if (b.x == w.b0 && b.y == w.b1 && b.z == w.b2 && b.w == w.b3) return a.z;
-            } else if (bytes_eq(ix.wpool + b.x, blob + w.start, w.len)) {
-                return a.z;
+                if (e.z == w.b0 && e.w == w.b1) return e.y;
+            } else if (e.w == w.len && bytes_eq(ix.wpool + e.z, blob + w.start, w.len)) {
+                return e.y;
             }
         }
         slot = (slot + 1) & ix.vmask;
     }
 }
 
-__device__ __forceinline__ uint32_t edge_find(const DevIndex &ix, uint32_t parent, uint32_t wid) {
-    uint32_t slot = edge_slot(parent, wid, ix.emask);
-    for (;;) {
-        uint4 e = ld4(ix.edges + slot);
-        if (e.x == parent && e.y == wid) return e.z;
+// literal child in a node's private table (table mode, nlit > KINL)
+__device__ __forceinline__ uint32_t ctab_find(const DevIndex &ix, uint32_t off, uint32_t mask, uint32_t wid,
+                                              uint32_t h) {
+    for (uint32_t s = h & mask;; s = (s + 1) & mask) {
+        const uint2 e = *reinterpret_cast<const uint2 *>(ix.ctab + off + s);
+        if (e.x == wid) return e.y;
         if (e.x == NONE) return NONE;
-        slot = (slot + 1) & ix.emask;
     }
 }
 
@@ -147,20 +147,21 @@ __device__ int tokenize(const DevIndex &ix, const uint8_t *blob, uint64_t beg, u
         lev++;
         return RC_OK;
     };
-    for (uint64_t p = beg & ~3ull; p < end; p += 4) {
-        uint32_t word = *reinterpret_cast<const uint32_t *>(blob + p);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            uint64_t q = p + k;
-            if (q >= beg && q < end) {
-                uint32_t c = (word >> (8 * k)) & 0xFFu;
-                if (c == '/') {
-                    int rc = finish();
-                    if (rc) return rc;
-                    w.reset(q + 1);
-                } else {
-                    w.push(c);
-                }
+    for (uint64_t p = beg & ~15ull; p < end; p += 16) {
+        // aligned 16-byte loads: the chunk shares its 16-byte granule with a
+        // valid byte, so it never crosses a page the caller does not own
+        const uint4 v = ld4(blob + p);
+        const uint32_t k0 = p < beg ? (uint32_t)(beg - p) : 0;
+        const uint32_t k1 = end - p < 16 ? (uint32_t)(end - p) : 16;
+        for (uint32_t k = k0; k < k1; k++) {
+            const uint32_t word = k < 4 ? v.x : k < 8 ? v.y : k < 12 ? v.z : v.w;
+            const uint32_t c = (word >> ((k & 3) * 8)) & 0xFFu;
+            if (c == '/') {
+                int rc = finish();
+                if (rc) return rc;
+                w.reset(p + k + 1);
+            } else {
+                w.push(c);
             }
         }
     }
@@ -216,15 +217,28 @@ template <class S, class EM>
 __device__ bool dfs(const DevIndex &ix, uint32_t L, bool dollar, S &st, EM &em) {
     uint32_t cur = ROOT, l = 0;
     for (;;) {
+        // the whole state is one 64-byte line (tm_layout.h Node)
         const uint4 *np = reinterpret_cast<const uint4 *>(ix.nodes + cur);
-        uint4 n0 = np[0], n1 = np[1];   // plus, hash_off, hash_cnt, exact_off | exact_cnt, ...
+        const uint4 n0 = np[0];   // plus, hash_off, hash_cnt, exact_off
+        const uint4 n1 = np[1];   // exact_cnt, nlit, mask_lo, mask_hi
+        const uint4 n2 = np[2];   // kw[0..3] (table mode: offset, size-1)
+        const uint4 n3 = np[3];   // kc[0..3]
         const bool droot = dollar && l == 0;
         if (l == L) {
             if (!em(n0.w, n1.x)) return false;
             if (!droot && !em(n0.y, n0.z)) return false;
         } else {
             const uint32_t w = st.get_wid(l);
-            const uint32_t lit = w != NONE ? edge_find(ix, cur, w) : NONE;
+            uint32_t lit = NONE;
+            if (w != NONE) {
+                if (n1.y <= KINL) {
+                    lit = n2.x == w ? n3.x : n2.y == w ? n3.y : n2.z == w ? n3.z : n2.w == w ? n3.w : NONE;
+                } else {
+                    const uint32_t h = child_hash(w), b = child_bit(h);
+                    const uint32_t m = b < 32 ? n1.z >> b : n1.w >> (b - 32);
+                    if (m & 1u) lit = ctab_find(ix, n2.x, n2.y, w, h);
+                }
+            }
             if (!droot && !em(n0.y, n0.z)) return false;
             const uint32_t plus = droot ? NONE : n0.x;
             if (plus != NONE) {
@@ -488,46 +502,70 @@ __device__ __forceinline__ uint32_t wave_excl_scan32(uint32_t v, uint32_t &total
     return inc - v;
 }
 
-// Each wave owns 64 consecutive topics: it flattens their value ranges into
-// LDS and then strides over the wave's hit positions, so stores are
-// contiguous whatever the per-topic hit counts are.
+// Each wave owns 64 consecutive topics.  It flattens their value ranges into
+// LDS (sorted by output position), then every lane produces whole aligned
+// quads of the wave's CSR span: one LDS binary search per quad, four value
+// reads, one 16-byte store -- so a wave writes 1 KiB per store instruction
+// whatever the per-topic hit counts are.  Positions of topics that overflowed
+// RCAP ranges are skipped (k_rewalk_* writes them).
 __global__ __launch_bounds__(EMIT_BLOCK) void k_emit(DevIndex ix, Workspace ws, uint64_t n,
                                                      const uint64_t *hit_offs, uint32_t *out, uint64_t cap) {
     __shared__ uint32_t s_off[EMIT_WAVES][WR];
-    __shared__ uint32_t s_cum[EMIT_WAVES][WR];
     __shared__ uint32_t s_rel[EMIT_WAVES][WR];
+    __shared__ uint32_t s_cnt[EMIT_WAVES][WR];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint64_t t0 = ((uint64_t)blockIdx.x * EMIT_WAVES + wv) * 64;
     if (t0 >= n) return;   // whole wave leaves; only wave-level sync below
     const uint64_t t = t0 + lane;
     const bool valid = t < n;
-    uint32_t nr = valid ? ws.nr[t] : 0, c = valid ? ws.cnt[t] : 0;
-    if (nr > RCAP) { nr = 0; c = 0; }   // written by k_rewalk_*
+    uint32_t nr = valid ? ws.nr[t] : 0;
+    if (nr > RCAP) nr = 0;   // written by k_rewalk_*
     const uint64_t base = hit_offs[t0];
+    const uint64_t endp = hit_offs[t0 + 64 < n ? t0 + 64 : n];
     const uint32_t rel = valid ? (uint32_t)(hit_offs[t] - base) : 0;
-    uint32_t R, E;
+    uint32_t R;
     const uint32_t r0 = wave_excl_scan32(nr, R);
-    const uint32_t e0 = wave_excl_scan32(c, E);
     uint32_t acc = 0;
     for (uint32_t i = 0; i < nr; i++) {
-        uint2 g = ws.rng[t * RCAP + i];
+        const uint2 g = ws.rng[t * RCAP + i];
         s_off[wv][r0 + i] = g.x;
-        s_cum[wv][r0 + i] = e0 + acc;
         s_rel[wv][r0 + i] = rel + acc;
+        s_cnt[wv][r0 + i] = g.y;
         acc += g.y;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    for (uint32_t e = lane; e < E; e += 64) {
-        uint32_t lo = 0, hi = R - 1;
+    if (!R) return;
+    const bool vec = (reinterpret_cast<uintptr_t>(out) & 15) == 0;
+    const uint64_t q1 = (endp + 3) >> 2;
+    for (uint64_t q = (base >> 2) + lane; q < q1; q += 64) {
+        const uint64_t p0 = q << 2;
+        const uint32_t first = (uint32_t)((p0 > base ? p0 : base) - base);
+        uint32_t lo = 0, hi = R - 1;            // last range starting at or before `first`
         while (lo < hi) {
-            uint32_t mid = (lo + hi + 1) >> 1;
-            if (s_cum[wv][mid] <= e) lo = mid; else hi = mid - 1;
+            const uint32_t mid = (lo + hi + 1) >> 1;
+            if (s_rel[wv][mid] <= first) lo = mid; else hi = mid - 1;
         }
-        const uint32_t k = e - s_cum[wv][lo];
-        const uint64_t pos = base + s_rel[wv][lo] + k;
-        if (pos < cap) out[pos] = ix.vals[s_off[wv][lo] + k];
+        uint32_t r = lo, v[4];
+        bool ok[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint64_t p = p0 + k;
+            ok[k] = false; v[k] = 0;
+            if (p < base || p >= endp) continue;
+            const uint32_t x = (uint32_t)(p - base);
+            while (r + 1 < R && s_rel[wv][r + 1] <= x) r++;
+            const uint32_t rs = s_rel[wv][r];
+            if (x >= rs && x - rs < s_cnt[wv][r]) { v[k] = ix.vals[s_off[wv][r] + (x - rs)]; ok[k] = true; }
+        }
+        if (vec && ok[0] && ok[1] && ok[2] && ok[3] && p0 + 3 < cap) {
+            *reinterpret_cast<uint4 *>(out + p0) = make_uint4(v[0], v[1], v[2], v[3]);
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                if (ok[k] && p0 + k < cap) out[p0 + k] = v[k];
+        }
     }
 }
 

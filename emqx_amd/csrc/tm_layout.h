@@ -7,13 +7,14 @@
 // open-addressing tables + two pools, all flat arrays of 4-byte words so the
 // host can patch them in place and mirror the patches to HBM:
 //
-//   vocab  : word bytes  -> word id (wid)       32 B/entry, verified by bytes
-//   edges  : (node, wid) -> child node           16 B/entry   (literal levels)
+//   vocab  : word bytes  -> word id (wid)       16 B/entry, verified by bytes
+//   ctab   : private child tables (wid -> child) of nodes with more than 4
+//            literal children                    8 B/slot
 //   nodes  : per trie node: '+' child, '#'-terminal and exact-terminal value
-//            ranges                              32 B/node
+//            ranges, up to 4 inline literal children  64 B/node (one line)
 //   exact  : wid sequence -> value range         64 B/entry   (binary keys)
 //   vals   : u32 values (caller IDs), one sorted run per terminal
-//   wpool  : bytes of words longer than 16 B; wseq: wid runs of exact keys
+//   wpool  : bytes of words longer than 8 B; wseq: wid runs of exact keys
 //            longer than XINL levels
 //
 // A word-list key (wildcard filter, or make_key(Words, ID)) is a path in the
@@ -33,29 +34,38 @@ namespace tmx {
 
 constexpr uint32_t NONE = 0xFFFFFFFFu;
 constexpr uint32_t ROOT = 0;
-constexpr uint32_t VINL = 16;   // inline word bytes in a vocab entry
+constexpr uint32_t VINL = 8;    // inline word bytes in a vocab entry
 constexpr uint32_t XINL = 10;   // inline wids in an exact entry
 
-struct alignas(16) VocabEntry {   // 32 B
-    uint32_t h_lo, h_hi;           // 64-bit word hash
+struct alignas(16) VocabEntry {   // 16 B
+    uint32_t tag;                  // hash bits 32..55 | min(len, 255); 0 with wid NONE = empty
     uint32_t wid;                  // NONE = empty slot
-    uint32_t len;                  // word length in bytes
-    uint32_t b[4];                 // len <= 16: the bytes, little endian, zero padded
-                                   // len  > 16: b[0] = offset of the word in wpool
+    uint32_t b0, b1;               // len <= 8: the bytes, little endian, zero padded
+                                   // len  > 8: b0 = offset of the word in wpool, b1 = len
 };
 
-struct alignas(16) Edge {          // 16 B
-    uint32_t parent;               // NONE = empty slot
-    uint32_t wid;
+struct CSlot {                     // 8 B: one literal child in a node's private table
+    uint32_t wid;                  // NONE = empty slot
     uint32_t child;
-    uint32_t pad;
 };
 
-struct alignas(16) Node {          // 32 B
+constexpr uint32_t KINL = 4;     // literal children kept inside the node's line
+
+// One 64-byte line per trie state: everything a walk step needs -- the '+'
+// child, both terminals and, for nodes with <= KINL literal children (almost
+// every node below the top levels), the literal children themselves.  A node
+// with more children keeps them in a private open-addressing table of CSlots
+// (contiguous, so the hot top of the trie packs densely in L2), and `mask` (a
+// 64-bit Bloom of its child wids) lets the walk skip probes that cannot hit.
+struct alignas(64) Node {          // 64 B
     uint32_t plus;                 // '+' child or NONE
     uint32_t hash_off, hash_cnt;   // values of filter <path>/#
     uint32_t exact_off, exact_cnt; // values of filter <path> (word-list form)
-    uint32_t pad[3];
+    uint32_t nlit;                 // literal children; > KINL: table mode
+    uint32_t mask_lo, mask_hi;     // table mode: Bloom bits of the child wids
+    uint32_t kw[KINL];             // inline: child wids (NONE = free); table mode: kw[0] = table
+                                   // offset (CSlots), kw[1] = table size - 1
+    uint32_t kc[KINL];             // inline: child node ids
 };
 
 struct alignas(16) ExactEntry {    // 64 B
@@ -66,9 +76,9 @@ struct alignas(16) ExactEntry {    // 64 B
     uint32_t wids[XINL];
 };
 
-static_assert(sizeof(VocabEntry) == 32, "vocab entry");
-static_assert(sizeof(Edge) == 16, "edge");
-static_assert(sizeof(Node) == 32, "node");
+static_assert(sizeof(VocabEntry) == 16, "vocab entry");
+static_assert(sizeof(CSlot) == 8, "child slot");
+static_assert(sizeof(Node) == 64, "node");
 static_assert(sizeof(ExactEntry) == 64, "exact entry");
 
 // ---- hashing (identical on host and device) -------------------------------
@@ -85,9 +95,13 @@ constexpr uint64_t FNV_PRIME = 0x100000001b3ull;
 
 TM_HD uint64_t word_hash_finish(uint64_t fnv, uint32_t len) { return mix64(fnv ^ ((uint64_t)len << 56)); }
 
-TM_HD uint32_t edge_slot(uint32_t parent, uint32_t wid, uint32_t mask) {
-    return (uint32_t)mix64(((uint64_t)parent << 32) | wid) & mask;
+TM_HD uint32_t vocab_tag(uint64_t h, uint32_t len) {
+    return ((uint32_t)(h >> 32) & 0xFFFFFF00u) | (len < 255 ? len : 255);
 }
+
+// child table hash: low bits pick the slot, the top 6 bits the Bloom bit
+TM_HD uint32_t child_hash(uint32_t wid) { return (uint32_t)mix64((uint64_t)wid * 0x9e3779b97f4a7c15ull + 1); }
+TM_HD uint32_t child_bit(uint32_t h) { return h >> 26; }
 
 TM_HD uint64_t seq_hash_step(uint64_t h, uint32_t wid) { return (h ^ wid) * FNV_PRIME; }
 TM_HD uint64_t seq_hash_finish(uint64_t h, uint32_t nlev) { return mix64(h + 0x9e3779b97f4a7c15ull * (nlev + 1)); }

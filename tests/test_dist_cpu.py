@@ -1,0 +1,100 @@
+"""world_size-2 gloo tests of the multi-GPU modes on CPU.
+
+The filter-sharded exchange (allgather of counts + allgatherv of values +
+merge) runs exactly as on GPUs, only over gloo; the per-shard hit lists come
+from the CPU oracle here (the test's stand-in for each rank's GPU shard), and
+the merged result must equal the oracle over the unsharded filter set.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parent.parent
+    sys.path.insert(0, str(root))
+    sys.path.insert(0, str(root / "oracle"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        _body(rank, world, q)
+    except BaseException as e:  # surface worker failures instead of a queue timeout
+        q.put((rank, "error", repr(e), None, None))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def _body(rank, world, q):
+    from emqx_amd import shard, workload as wl
+    from pyoracle import Oracle
+    nf = 20_000
+    fs = wl.filters(3, nf, shard=rank, nshards=world)
+    ts = wl.topics(3, nf, 3_000)
+    o = Oracle()
+    o.apply(np.ones(len(fs), np.uint8), fs.blob, fs.offs, fs.vals)
+    cnt, _, hit, vals = o.match_batch(ts.blob, ts.offs)
+    m_offs, m_vals = shard.allgatherv_hits(torch.from_numpy(hit.astype(np.int64)),
+                                           torch.from_numpy(vals.view(np.int32)))
+    # topic-sharded slices partition the stream
+    first, n = shard.topic_slice(rank, world, 1000)
+    t = torch.tensor([first, n], dtype=torch.int64)
+    g = [torch.zeros(2, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(g, t)
+    # max-over-ranks timing reduction used by bench.py
+    el = torch.tensor([0.5 + rank], dtype=torch.float64)
+    dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    q.put((rank, m_offs.numpy(), m_vals.numpy(), [x.tolist() for x in g], float(el)))
+
+
+@pytest.mark.timeout(300)
+def test_filter_sharded_exchange_gloo():
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parent.parent
+    sys.path.insert(0, str(root / "oracle"))
+    from emqx_amd import workload as wl
+    from pyoracle import Oracle
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(world)]
+    for p in ps:
+        p.join(timeout=60)
+    res.sort(key=lambda x: x[0])
+    for r in res:
+        assert not (isinstance(r[1], str) and r[1] == "error"), r
+    # every rank ends with the same merged CSR
+    assert np.array_equal(res[0][1], res[1][1]) and np.array_equal(res[0][2], res[1][2])
+    # ... equal to the unsharded oracle, per topic as sorted sets
+    nf = 20_000
+    fs = wl.filters(3, nf)
+    ts = wl.topics(3, nf, 3_000)
+    o = Oracle()
+    o.apply(np.ones(len(fs), np.uint8), fs.blob, fs.offs, fs.vals)
+    cnt, _, hit, vals = o.match_batch(ts.blob, ts.offs)
+    m_offs, m_vals = res[0][1], res[0][2].view(np.uint32)
+    assert np.array_equal(m_offs, hit.astype(np.int64))
+    for i in range(len(ts)):
+        assert np.array_equal(np.sort(vals[hit[i]:hit[i + 1]]), m_vals[m_offs[i]:m_offs[i + 1]])
+    assert res[0][3] == [[0, 1000], [1000, 1000]]
+    assert res[0][4] == 1.5

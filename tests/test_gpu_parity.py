@@ -339,3 +339,28 @@ def test_c3_scale_properties(torch_dev):
     for i in sys_rows:
         g = vals[int(hit[i]):int(hit[i + 1])]
         assert nf not in g and nf + 1 not in g
+
+
+def test_child_table_grow_and_shrink(torch_dev):
+    """A node going inline (<= 4 children) -> private table -> bigger tables ->
+    back to inline, with matches checked against the oracle at every stage."""
+    ix = gpu_index()
+    o = Oracle()
+    topics = items_of([b"a/%d/x" % i for i in range(200)] + [b"a/%d" % i for i in range(200)] + [b"b/1/x"])
+    live = []
+    r = random.Random(5)
+    for stage in [3, 5, 6, 17, 33, 130, 200]:
+        add = [i for i in range(stage) if i not in live]
+        d = items_of([b"a/%d/+" % i for i in add] + [b"a/%d/#" % i for i in add], add + [1000 + i for i in add])
+        ix.apply(np.ones(len(d), np.uint8), d.blob, d.offs, d.vals)
+        o.apply(np.ones(len(d), np.uint8), d.blob, d.offs, d.vals)
+        live += add
+        assert_same(ix, o, topics)
+    for keep in [120, 40, 9, 5, 4, 2, 0]:
+        drop = r.sample(live, len(live) - keep)
+        live = [i for i in live if i not in drop]
+        d = items_of([b"a/%d/+" % i for i in drop] + [b"a/%d/#" % i for i in drop], drop + [1000 + i for i in drop])
+        ix.apply(np.zeros(len(d), np.uint8), d.blob, d.offs, d.vals)
+        o.apply(np.zeros(len(d), np.uint8), d.blob, d.offs, d.vals)
+        assert_same(ix, o, topics)
+    assert ix.stats()["n_nodes"] == 1

@@ -1,0 +1,58 @@
+#!/usr/bin/env python3
+"""Minimal profiling driver: build a config's index, then run --batches
+device-resident match batches (no oracle, no CPU work) so rocprofv3 passes
+(kernel trace or PMC counters) see only the match kernels."""
+import argparse
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--config", default="c3")
+    p.add_argument("--filters", type=int, default=None)
+    p.add_argument("--batch", type=int, default=1_000_000)
+    p.add_argument("--batches", type=int, default=5)
+    a = p.parse_args()
+    import torch
+    from bench import CONFIGS
+    from emqx_amd import _native, workload as wl
+    gen, nf0, _ = CONFIGS[a.config]
+    nf = a.filters or nf0
+    fs = wl.filters(gen, nf)
+    ix = _native.Index(device=0)
+    for lo in range(0, len(fs), 2_000_000):
+        part = fs.slice(lo, min(lo + 2_000_000, len(fs)))
+        ix.apply(np.ones(len(part), np.uint8), part.blob, part.offs, part.vals)
+    ts = wl.topics(gen, nf, a.batch)
+    dev = torch.device("cuda:0")
+    d_blob = torch.from_numpy(ts.blob).to(dev)
+    d_offs = torch.from_numpy(ts.offs.view(np.int64)).to(dev)
+    d_hit = torch.zeros(a.batch + 1, dtype=torch.int64, device=dev)
+    d_err = torch.zeros(a.batch, dtype=torch.uint8, device=dev)
+    s = torch.cuda.current_stream().cuda_stream
+    ix.match_batch_dev(a.batch, d_blob.data_ptr(), d_offs.data_ptr(), d_hit.data_ptr(), 0, 0, d_err.data_ptr(), s)
+    torch.cuda.synchronize()
+    tot = int(d_hit[-1])
+    d_out = torch.zeros(max(tot, 1), dtype=torch.int32, device=dev)
+    ix.profile(True)
+    t = time.perf_counter()
+    for _ in range(a.batches):
+        ix.match_batch_dev(a.batch, d_blob.data_ptr(), d_offs.data_ptr(), d_hit.data_ptr(), d_out.data_ptr(), tot,
+                           d_err.data_ptr(), s)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t
+    w, b, n = ix.profile_read()
+    st = ix.stats()
+    print(f"{a.config} filters={len(fs)} batch={a.batch} hits={tot} wall/batch={el / a.batches * 1e3:.3f}ms "
+          f"walk={w / n:.4f}ms batch_dev={b / n:.4f}ms rate={a.batch * a.batches / el / 1e9:.3f}G/s "
+          f"device_MiB={st['device_bytes'] / 2**20:.0f}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
