@@ -32,24 +32,25 @@ struct Workspace {
     uint32_t *nr;         // [n] ranges per topic (RCAP+1 = overflow)
     uint2 *rng;           // [n * RCAP] (value offset, count)
     uint32_t *lists;      // [L_COUNT * n] topic lists
-    uint32_t *list_n;     // [L_COUNT] list lengths
-    uint64_t *blk;        // [n / SCAN_TILE + 2] scan block sums / prefixes
+    uint32_t *list_n;     // [L_COUNT] list lengths + [L_COUNT] reset ticket (zero between batches)
+    uint64_t *blk;        // [n / TILE + 2] tile hit totals -> exclusive tile prefixes
     uint32_t *deep_wid;   // [DEEP_LANES * MAX_LEVELS]
     uint2 *deep_stk;      // [DEEP_LANES * (MAX_LEVELS + 1)]
     uint64_t cap_n;
 };
 
-constexpr int SCAN_TILE = 1024;
+constexpr int TILE = 256;    // topics per walk block = per scan tile = per emit block
 
 // Pipeline entry points (tm_kernels.hip).  All asynchronous on `s`.
-// phase 1: tokenise + walk + scan (hit offsets and total become valid)
-// phase 2: emit the values (+ re-walk overflowing topics)
+// phase 1: tokenise + walk + tile totals (hit_offs[n] = total becomes valid)
+// phase 2: finish the scan (hit_offs[0..n)), emit the values, re-walk
+//          overflowing topics, reset the device-side list counters
 // ev_walk0/ev_walk1 (may be null): recorded right before / after the main walk kernel
 hipError_t launch_match_phase1(const DevIndex &ix, const Workspace &ws, uint64_t n, const uint8_t *bytes,
                                const uint64_t *offs, uint64_t *hit_offs, uint8_t *err, hipStream_t s,
                                hipEvent_t ev_walk0 = nullptr, hipEvent_t ev_walk1 = nullptr);
 hipError_t launch_match_phase2(const DevIndex &ix, const Workspace &ws, uint64_t n, const uint8_t *bytes,
-                               const uint64_t *offs, const uint64_t *hit_offs, uint32_t *out, uint64_t cap,
+                               const uint64_t *offs, uint64_t *hit_offs, uint32_t *out, uint64_t cap,
                                hipStream_t s);
 hipError_t launch_first(const DevIndex &ix, const Workspace &ws, uint64_t n, const uint8_t *bytes,
                         const uint64_t *offs, uint32_t *out_value, uint8_t *out_found, hipStream_t s);

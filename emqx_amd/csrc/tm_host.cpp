@@ -104,6 +104,7 @@ struct tm_index {
     uint64_t *d_hit = nullptr; uint64_t d_hit_cap = 0;
     uint8_t *d_err = nullptr; uint64_t d_err_cap = 0;
     uint32_t *d_out = nullptr; uint64_t d_out_cap = 0;
+    uint32_t *pin_vals = nullptr, *pin_vals_dev = nullptr; uint64_t pin_vals_cap = 0;
 
     // diagnostics (tm_profile_*)
     bool prof = false;
@@ -716,7 +717,8 @@ int ensure_ws(tm_index *ix, uint64_t n, hipStream_t s) {
     if (!w.deep_wid) {
         HIPCHK(ix, hipMalloc(&w.deep_wid, (uint64_t)DEEP_LANES * MAX_LEVELS * 4));
         HIPCHK(ix, hipMalloc(&w.deep_stk, (uint64_t)DEEP_LANES * (MAX_LEVELS + 1) * 8));
-        HIPCHK(ix, hipMalloc(&w.list_n, L_COUNT * 4));
+        HIPCHK(ix, hipMalloc(&w.list_n, (L_COUNT + 1) * 4));
+        HIPCHK(ix, hipMemset(w.list_n, 0, (L_COUNT + 1) * 4));
     }
     if (n <= ix->ws_cap && w.cnt) return TM_OK;
     (void)s;
@@ -727,7 +729,7 @@ int ensure_ws(tm_index *ix, uint64_t n, hipStream_t s) {
     HIPCHK(ix, hipMalloc(&w.nr, c * 4));
     HIPCHK(ix, hipMalloc(&w.rng, c * RCAP * 8));
     HIPCHK(ix, hipMalloc(&w.lists, c * L_COUNT * 4));
-    HIPCHK(ix, hipMalloc(&w.blk, (c / SCAN_TILE + 4) * 8));
+    HIPCHK(ix, hipMalloc(&w.blk, (c / TILE + 4) * 8));
     w.cap_n = c;
     ix->ws_cap = c;
     return TM_OK;
@@ -809,7 +811,7 @@ int tm_destroy(tm_index *ix) {
                     ix->ws.blk, ix->ws.deep_wid, ix->ws.deep_stk, ix->d_topics, ix->d_offs, ix->d_hit,
                     ix->d_err, ix->d_out};
     for (void *p : bufs) if (p) (void)hipFree(p);
-    void *pins[] = {ix->pin_addr, ix->pin_val, ix->pin_in, ix->pin_out};
+    void *pins[] = {ix->pin_addr, ix->pin_val, ix->pin_in, ix->pin_out, ix->pin_vals};
     for (void *p : pins) if (p) (void)hipHostFree(p);
     (void)hipEventDestroy(ix->patch_done);
     (void)hipStreamDestroy(ix->stream);
@@ -889,38 +891,44 @@ int tm_match_batch(tm_index *ix, uint64_t n, const uint8_t *tb, const uint64_t *
     if ((rc = grow_dev(ix, ix->d_offs, ix->d_offs_cap, n + 1))) return rc;
     if ((rc = grow_dev(ix, ix->d_hit, ix->d_hit_cap, n + 1))) return rc;
     if ((rc = grow_dev(ix, ix->d_err, ix->d_err_cap, n + 1))) return rc;
+    // small outputs (offsets, err flags) come back by DMA; the values are
+    // written by k_emit straight into mapped pinned memory, so the batch costs
+    // one host synchronisation (a second one only when that buffer must grow)
+    const uint64_t small = (n + 1) * 8 + n + 16;
+    if (small > ix->pin_out_cap) {
+        HIPCHK(ix, hipStreamSynchronize(s));
+        if (ix->pin_out) HIPCHK(ix, hipHostFree(ix->pin_out));
+        ix->pin_out_cap = small + small / 4;
+        HIPCHK(ix, hipHostMalloc(&ix->pin_out, ix->pin_out_cap, hipHostMallocDefault));
+    }
     HIPCHK(ix, hipMemcpyAsync(ix->d_offs, pin_offs, (n + 1) * 8, hipMemcpyHostToDevice, s));
     if (nbytes) HIPCHK(ix, hipMemcpyAsync(ix->d_topics, pin_bytes, nbytes, hipMemcpyHostToDevice, s));
     const DevIndex d = dev_view(ix);
-    HIPCHK(ix, launch_match_phase1(d, ix->ws, n, ix->d_topics, ix->d_offs, ix->d_hit, ix->d_err, s));
-    // total hits -> size the output (one small D2H + sync; the host API blocks anyway)
-    if (ix->pin_out_cap < 64) {
-        if (ix->pin_out) HIPCHK(ix, hipHostFree(ix->pin_out));
-        ix->pin_out_cap = 1 << 20;
-        HIPCHK(ix, hipHostMalloc(&ix->pin_out, ix->pin_out_cap, hipHostMallocDefault));
-    }
-    HIPCHK(ix, hipMemcpyAsync(ix->pin_out, ix->d_hit + n, 8, hipMemcpyDeviceToHost, s));
-    HIPCHK(ix, hipStreamSynchronize(s));
-    uint64_t total;
-    memcpy(&total, ix->pin_out, 8);
-    const uint64_t keep = std::min(total, out_vals ? cap : 0);
-    if ((rc = grow_dev(ix, ix->d_out, ix->d_out_cap, std::max<uint64_t>(keep, 1)))) return rc;
-    HIPCHK(ix, launch_match_phase2(d, ix->ws, n, ix->d_topics, ix->d_offs, ix->d_hit, ix->d_out, keep, s));
-    const uint64_t out_need = (n + 1) * 8 + keep * 4 + n + 16;
-    if (out_need > ix->pin_out_cap) {
+    uint64_t total = 0;
+    for (int attempt = 0; attempt < 2; attempt++) {
+        if (!ix->pin_vals) {
+            ix->pin_vals_cap = std::max<uint64_t>(ix->pin_vals_cap, 1 << 16);
+            HIPCHK(ix, hipHostMalloc(&ix->pin_vals, ix->pin_vals_cap * 4, hipHostMallocMapped));
+            HIPCHK(ix, hipHostGetDevicePointer(reinterpret_cast<void **>(&ix->pin_vals_dev), ix->pin_vals, 0));
+        }
+        HIPCHK(ix, launch_match_phase1(d, ix->ws, n, ix->d_topics, ix->d_offs, ix->d_hit, ix->d_err, s));
+        HIPCHK(ix, launch_match_phase2(d, ix->ws, n, ix->d_topics, ix->d_offs, ix->d_hit, ix->pin_vals_dev,
+                                       ix->pin_vals_cap, s));
+        uint8_t *po = ix->pin_out;
+        HIPCHK(ix, hipMemcpyAsync(po, ix->d_hit, (n + 1) * 8, hipMemcpyDeviceToHost, s));
+        if (n) HIPCHK(ix, hipMemcpyAsync(po + (n + 1) * 8, ix->d_err, n, hipMemcpyDeviceToHost, s));
         HIPCHK(ix, hipStreamSynchronize(s));
-        HIPCHK(ix, hipHostFree(ix->pin_out));
-        ix->pin_out_cap = out_need + out_need / 4;
-        HIPCHK(ix, hipHostMalloc(&ix->pin_out, ix->pin_out_cap, hipHostMallocDefault));
+        memcpy(&total, po + n * 8, 8);
+        if (total <= ix->pin_vals_cap || !out_vals || total <= 0) break;
+        // grow the mapped buffer and run the batch again (rare: sizes are sticky)
+        HIPCHK(ix, hipHostFree(ix->pin_vals));
+        ix->pin_vals = nullptr;
+        ix->pin_vals_cap = total + total / 4;
     }
-    uint8_t *po = ix->pin_out;
-    HIPCHK(ix, hipMemcpyAsync(po, ix->d_hit, (n + 1) * 8, hipMemcpyDeviceToHost, s));
-    if (keep) HIPCHK(ix, hipMemcpyAsync(po + (n + 1) * 8, ix->d_out, keep * 4, hipMemcpyDeviceToHost, s));
-    if (n) HIPCHK(ix, hipMemcpyAsync(po + (n + 1) * 8 + keep * 4, ix->d_err, n, hipMemcpyDeviceToHost, s));
-    HIPCHK(ix, hipStreamSynchronize(s));
-    memcpy(out_hit, po, (n + 1) * 8);
-    if (keep) memcpy(out_vals, po + (n + 1) * 8, keep * 4);
-    if (out_err && n) memcpy(out_err, po + (n + 1) * 8 + keep * 4, n);
+    memcpy(out_hit, ix->pin_out, (n + 1) * 8);
+    if (out_err && n) memcpy(out_err, ix->pin_out + (n + 1) * 8, n);
+    const uint64_t keep = std::min(total, out_vals ? cap : 0);
+    if (keep) memcpy(out_vals, ix->pin_vals, keep * 4);
     return (out_vals && total > cap) ? TM_ECAP : TM_OK;
 }
 

@@ -316,10 +316,11 @@ __device__ __forceinline__ void list_push(const Workspace &ws, uint64_t n, int k
 }
 
 // one topic in phase-1 (count) or first-hit mode; returns RC_DEEP if the
-// storage is too shallow (caller routes the topic to a list kernel)
+// storage is too shallow (caller routes the topic to a list kernel).  *hits
+// receives the topic's hit count (count mode).
 template <int MODE, class S>
 __device__ int run_topic(const DevIndex &ix, const Workspace &ws, uint64_t n, const uint8_t *blob,
-                         const uint64_t *offs, uint64_t t, S &st, const Outs &o) {
+                         const uint64_t *offs, uint64_t t, S &st, const Outs &o, uint32_t *hits) {
     const uint64_t beg = offs[t], end = offs[t + 1];
     if (MODE == MODE_COUNT) {
         RangeEmit em{ws.rng + t * RCAP, 0, 0};
@@ -330,6 +331,7 @@ __device__ int run_topic(const DevIndex &ix, const Workspace &ws, uint64_t n, co
         ws.nr[t] = em.nr;
         o.err[t] = rc == RC_BADARG;
         if (em.nr > RCAP) list_push(ws, n, S::maxl <= MID_L ? L_OVF_MID : L_OVF_DEEP, (uint32_t)t);
+        *hits = em.cnt;
         return rc;
     } else {
         FirstEmit em{ix.vals, 0, false};
@@ -337,86 +339,12 @@ __device__ int run_topic(const DevIndex &ix, const Workspace &ws, uint64_t n, co
         if (rc == RC_DEEP) return rc;
         o.first_val[t] = em.v;
         o.first_found[t] = rc == RC_BADARG ? 2 : (em.found ? 1 : 0);
+        *hits = 0;
         return rc;
     }
 }
 
-// ----------------------------------------------------------------- kernels
-
-constexpr int WALK_BLOCK = 256;
-
-template <int MODE>
-__global__ __launch_bounds__(WALK_BLOCK) void k_walk_fast(DevIndex ix, Workspace ws, uint64_t n,
-                                                          const uint8_t *blob, const uint64_t *offs, Outs o) {
-    __shared__ uint32_t s_wid[FAST_L * WALK_BLOCK];
-    __shared__ uint32_t s_pend[(FAST_L + 1) * WALK_BLOCK];
-    const uint64_t t = (uint64_t)blockIdx.x * WALK_BLOCK + threadIdx.x;
-    if (t >= n) return;
-    LdsStore<FAST_L> st{s_wid + threadIdx.x, s_pend + threadIdx.x, WALK_BLOCK, 0};
-    int rc = run_topic<MODE>(ix, ws, n, blob, offs, t, st, o);
-    if (rc == RC_DEEP) {
-        uint32_t nl = count_levels(blob, offs[t], offs[t + 1]);
-        list_push(ws, n, nl <= MID_L ? L_MID : L_DEEP, (uint32_t)t);
-    }
-}
-
-constexpr int MID_BLOCK = 64;
-
-template <int MODE>
-__global__ __launch_bounds__(MID_BLOCK) void k_walk_mid(DevIndex ix, Workspace ws, uint64_t n,
-                                                        const uint8_t *blob, const uint64_t *offs, Outs o) {
-    __shared__ uint32_t s_wid[MID_L * MID_BLOCK];
-    __shared__ uint32_t s_pend[(MID_L + 1) * MID_BLOCK];
-    const uint32_t cnt = ws.list_n[L_MID];
-    const uint32_t *lst = ws.lists + (uint64_t)L_MID * n;
-    LdsStore<MID_L> st{s_wid + threadIdx.x, s_pend + threadIdx.x, MID_BLOCK, 0};
-    for (uint32_t i = blockIdx.x * MID_BLOCK + threadIdx.x; i < cnt; i += gridDim.x * MID_BLOCK)
-        run_topic<MODE>(ix, ws, n, blob, offs, lst[i], st, o);
-}
-
-template <int MODE>
-__global__ __launch_bounds__(64) void k_walk_deep(DevIndex ix, Workspace ws, uint64_t n,
-                                                  const uint8_t *blob, const uint64_t *offs, Outs o) {
-    const uint32_t lane = blockIdx.x * 64 + threadIdx.x;   // < DEEP_LANES
-    const uint32_t cnt = ws.list_n[L_DEEP];
-    const uint32_t *lst = ws.lists + (uint64_t)L_DEEP * n;
-    GlobalStore st{ws.deep_wid + (uint64_t)lane * MAX_LEVELS, ws.deep_stk + (uint64_t)lane * (MAX_LEVELS + 1), 0};
-    for (uint32_t i = lane; i < cnt; i += DEEP_LANES)
-        run_topic<MODE>(ix, ws, n, blob, offs, lst[i], st, o);
-}
-
-// re-walk of topics with more than RCAP hit ranges: values go straight to the CSR
-template <class S>
-__device__ void rewalk(const DevIndex &ix, const uint8_t *blob, const uint64_t *offs, uint64_t t,
-                       const uint64_t *hit_offs, uint32_t *out, uint64_t cap, S &st) {
-    DirectEmit em{ix.vals, out, hit_offs[t], cap};
-    match_topic(ix, blob, offs[t], offs[t + 1], st, em);
-}
-
-__global__ __launch_bounds__(MID_BLOCK) void k_rewalk_mid(DevIndex ix, Workspace ws, uint64_t n, const uint8_t *blob,
-                                                          const uint64_t *offs, const uint64_t *hit_offs,
-                                                          uint32_t *out, uint64_t cap) {
-    __shared__ uint32_t s_wid[MID_L * MID_BLOCK];
-    __shared__ uint32_t s_pend[(MID_L + 1) * MID_BLOCK];
-    const uint32_t cnt = ws.list_n[L_OVF_MID];
-    const uint32_t *lst = ws.lists + (uint64_t)L_OVF_MID * n;
-    LdsStore<MID_L> st{s_wid + threadIdx.x, s_pend + threadIdx.x, MID_BLOCK, 0};
-    for (uint32_t i = blockIdx.x * MID_BLOCK + threadIdx.x; i < cnt; i += gridDim.x * MID_BLOCK)
-        rewalk(ix, blob, offs, lst[i], hit_offs, out, cap, st);
-}
-
-__global__ __launch_bounds__(64) void k_rewalk_deep(DevIndex ix, Workspace ws, uint64_t n, const uint8_t *blob,
-                                                    const uint64_t *offs, const uint64_t *hit_offs,
-                                                    uint32_t *out, uint64_t cap) {
-    const uint32_t lane = blockIdx.x * 64 + threadIdx.x;
-    const uint32_t cnt = ws.list_n[L_OVF_DEEP];
-    const uint32_t *lst = ws.lists + (uint64_t)L_OVF_DEEP * n;
-    GlobalStore st{ws.deep_wid + (uint64_t)lane * MAX_LEVELS, ws.deep_stk + (uint64_t)lane * (MAX_LEVELS + 1), 0};
-    for (uint32_t i = lane; i < cnt; i += DEEP_LANES)
-        rewalk(ix, blob, offs, lst[i], hit_offs, out, cap, st);
-}
-
-// ------------------------------------------------------------------- scan
+// ------------------------------------------------------------ wave / block scans
 
 __device__ __forceinline__ uint64_t wave_incl_scan(uint64_t v) {
     const int lane = threadIdx.x & 63;
@@ -426,6 +354,18 @@ __device__ __forceinline__ uint64_t wave_incl_scan(uint64_t v) {
         if (lane >= d) v += o;
     }
     return v;
+}
+
+__device__ __forceinline__ uint32_t wave_excl_scan32(uint32_t v, uint32_t &total) {
+    const int lane = threadIdx.x & 63;
+    uint32_t inc = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        uint32_t o = __shfl_up(inc, d, 64);
+        if (lane >= d) inc += o;
+    }
+    total = __shfl(inc, 63, 64);
+    return inc - v;
 }
 
 // block-wide exclusive scan of one value per thread (blockDim = 256)
@@ -442,18 +382,117 @@ __device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t &total,
     return pre + inc - v;
 }
 
-// tile of SCAN_TILE = 256 threads x 4 counts
-__global__ __launch_bounds__(256) void k_scan_reduce(const uint32_t *cnt, uint64_t n, uint64_t *blk) {
+// ----------------------------------------------------------------- kernels
+//
+// Per batch: phase 1 = k_walk_fast, k_walk_tail, k_scan_top; phase 2 =
+// k_emit, k_rewalk_tail.  Tiles of TILE = 256 topics line up across kernels:
+// the walk writes each tile's hit total into ws.blk, k_scan_top turns those
+// into tile prefixes, k_emit finishes the scan inside its tile.
+
+constexpr int WALK_BLOCK = 256;
+static_assert(WALK_BLOCK == TILE, "walk blocks are scan tiles");
+
+template <int MODE>
+__global__ __launch_bounds__(WALK_BLOCK) void k_walk_fast(DevIndex ix, Workspace ws, uint64_t n,
+                                                          const uint8_t *blob, const uint64_t *offs, Outs o) {
+    __shared__ uint32_t s_wid[FAST_L * WALK_BLOCK];
+    __shared__ uint32_t s_pend[(FAST_L + 1) * WALK_BLOCK];
     __shared__ uint64_t s_w[4];
-    const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE + threadIdx.x * 4;
-    uint64_t v = 0;
-#pragma unroll
-    for (int k = 0; k < 4; k++) if (base + k < n) v += cnt[base + k];
-    uint64_t total;
-    block_excl_scan(v, total, s_w);
-    if (threadIdx.x == 0) blk[blockIdx.x] = total;
+    const uint64_t t = (uint64_t)blockIdx.x * WALK_BLOCK + threadIdx.x;
+    uint32_t hits = 0;
+    if (t < n) {
+        LdsStore<FAST_L> st{s_wid + threadIdx.x, s_pend + threadIdx.x, WALK_BLOCK, 0};
+        int rc = run_topic<MODE>(ix, ws, n, blob, offs, t, st, o, &hits);
+        if (rc == RC_DEEP) {
+            hits = 0;   // counted by k_walk_tail (atomically added to this tile)
+            uint32_t nl = count_levels(blob, offs[t], offs[t + 1]);
+            list_push(ws, n, nl <= MID_L ? L_MID : L_DEEP, (uint32_t)t);
+        }
+    }
+    if (MODE == MODE_COUNT) {
+        uint64_t total;
+        block_excl_scan(hits, total, s_w);
+        if (threadIdx.x == 0) ws.blk[blockIdx.x] = total;
+    }
 }
 
+constexpr int MID_BLOCK = 64;
+constexpr int MID_GRID = 256;                         // LDS-frontier blocks of the tail kernels
+constexpr int TAIL_GRID = MID_GRID + DEEP_LANES / 64; // + global-scratch blocks
+
+// last block of a grid (atomic ticket) resets the list counters for the next batch
+__device__ __forceinline__ void reset_lists_if_last(const Workspace &ws) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        const uint32_t ticket = atomicAdd(&ws.list_n[L_COUNT], 1u);
+        if (ticket == gridDim.x - 1) {
+            for (int k = 0; k < L_COUNT; k++) atomicExch(&ws.list_n[k], 0u);
+            atomicExch(&ws.list_n[L_COUNT], 0u);
+        }
+    }
+}
+
+// topics deeper than FAST_L: blocks < MID_GRID take the MID list (LDS frontier,
+// <= MID_L levels), the rest take the DEEP list (global scratch, any depth)
+template <int MODE>
+__global__ __launch_bounds__(MID_BLOCK) void k_walk_tail(DevIndex ix, Workspace ws, uint64_t n,
+                                                         const uint8_t *blob, const uint64_t *offs, Outs o) {
+    __shared__ uint32_t s_wid[MID_L * MID_BLOCK];
+    __shared__ uint32_t s_pend[(MID_L + 1) * MID_BLOCK];
+    uint32_t hits = 0;
+    if (blockIdx.x < MID_GRID) {
+        const uint32_t cnt = ws.list_n[L_MID];
+        const uint32_t *lst = ws.lists + (uint64_t)L_MID * n;
+        LdsStore<MID_L> st{s_wid + threadIdx.x, s_pend + threadIdx.x, MID_BLOCK, 0};
+        for (uint32_t i = blockIdx.x * MID_BLOCK + threadIdx.x; i < cnt; i += MID_GRID * MID_BLOCK) {
+            run_topic<MODE>(ix, ws, n, blob, offs, lst[i], st, o, &hits);
+            if (MODE == MODE_COUNT && hits) atomicAdd((unsigned long long *)&ws.blk[lst[i] / TILE], hits);
+        }
+    } else {
+        const uint32_t lane = (blockIdx.x - MID_GRID) * 64 + threadIdx.x;   // < DEEP_LANES
+        const uint32_t cnt = ws.list_n[L_DEEP];
+        const uint32_t *lst = ws.lists + (uint64_t)L_DEEP * n;
+        GlobalStore st{ws.deep_wid + (uint64_t)lane * MAX_LEVELS, ws.deep_stk + (uint64_t)lane * (MAX_LEVELS + 1), 0};
+        for (uint32_t i = lane; i < cnt; i += DEEP_LANES) {
+            run_topic<MODE>(ix, ws, n, blob, offs, lst[i], st, o, &hits);
+            if (MODE == MODE_COUNT && hits) atomicAdd((unsigned long long *)&ws.blk[lst[i] / TILE], hits);
+        }
+    }
+    if (MODE == MODE_FIRST) reset_lists_if_last(ws);   // count mode: k_rewalk_tail resets
+}
+
+// re-walk of topics with more than RCAP hit ranges: values go straight to the CSR
+template <class S>
+__device__ void rewalk(const DevIndex &ix, const uint8_t *blob, const uint64_t *offs, uint64_t t,
+                       const uint64_t *hit_offs, uint32_t *out, uint64_t cap, S &st) {
+    DirectEmit em{ix.vals, out, hit_offs[t], cap};
+    match_topic(ix, blob, offs[t], offs[t + 1], st, em);
+}
+
+__global__ __launch_bounds__(MID_BLOCK) void k_rewalk_tail(DevIndex ix, Workspace ws, uint64_t n, const uint8_t *blob,
+                                                           const uint64_t *offs, const uint64_t *hit_offs,
+                                                           uint32_t *out, uint64_t cap) {
+    __shared__ uint32_t s_wid[MID_L * MID_BLOCK];
+    __shared__ uint32_t s_pend[(MID_L + 1) * MID_BLOCK];
+    if (blockIdx.x < MID_GRID) {
+        const uint32_t cnt = ws.list_n[L_OVF_MID];
+        const uint32_t *lst = ws.lists + (uint64_t)L_OVF_MID * n;
+        LdsStore<MID_L> st{s_wid + threadIdx.x, s_pend + threadIdx.x, MID_BLOCK, 0};
+        for (uint32_t i = blockIdx.x * MID_BLOCK + threadIdx.x; i < cnt; i += MID_GRID * MID_BLOCK)
+            rewalk(ix, blob, offs, lst[i], hit_offs, out, cap, st);
+    } else {
+        const uint32_t lane = (blockIdx.x - MID_GRID) * 64 + threadIdx.x;
+        const uint32_t cnt = ws.list_n[L_OVF_DEEP];
+        const uint32_t *lst = ws.lists + (uint64_t)L_OVF_DEEP * n;
+        GlobalStore st{ws.deep_wid + (uint64_t)lane * MAX_LEVELS, ws.deep_stk + (uint64_t)lane * (MAX_LEVELS + 1), 0};
+        for (uint32_t i = lane; i < cnt; i += DEEP_LANES)
+            rewalk(ix, blob, offs, lst[i], hit_offs, out, cap, st);
+    }
+    reset_lists_if_last(ws);
+}
+
+// tile totals -> exclusive tile prefixes; hit_offs[n] = grand total
 __global__ __launch_bounds__(256) void k_scan_top(uint64_t *blk, uint64_t nb, uint64_t *hit_offs, uint64_t n) {
     __shared__ uint64_t s_w[4];
     uint64_t carry = 0;
@@ -467,62 +506,42 @@ __global__ __launch_bounds__(256) void k_scan_top(uint64_t *blk, uint64_t nb, ui
     if (threadIdx.x == 0) hit_offs[n] = carry;
 }
 
-__global__ __launch_bounds__(256) void k_scan_apply(const uint32_t *cnt, uint64_t n, const uint64_t *blk,
-                                                    uint64_t *hit_offs) {
-    __shared__ uint64_t s_w[4];
-    const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE + threadIdx.x * 4;
-    uint32_t c[4];
-    uint64_t v = 0;
-#pragma unroll
-    for (int k = 0; k < 4; k++) { c[k] = base + k < n ? cnt[base + k] : 0; v += c[k]; }
-    uint64_t total;
-    uint64_t pre = block_excl_scan(v, total, s_w) + blk[blockIdx.x];
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        if (base + k < n) hit_offs[base + k] = pre;
-        pre += c[k];
-    }
-}
-
 // ------------------------------------------------------------------- emit
 
-constexpr int EMIT_BLOCK = 256;
+constexpr int EMIT_BLOCK = TILE;
 constexpr int EMIT_WAVES = EMIT_BLOCK / 64;
 constexpr int WR = 64 * RCAP;   // ranges per wave
 
-__device__ __forceinline__ uint32_t wave_excl_scan32(uint32_t v, uint32_t &total) {
-    const int lane = threadIdx.x & 63;
-    uint32_t inc = v;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        uint32_t o = __shfl_up(inc, d, 64);
-        if (lane >= d) inc += o;
-    }
-    total = __shfl(inc, 63, 64);
-    return inc - v;
-}
-
-// Each wave owns 64 consecutive topics.  It flattens their value ranges into
-// LDS (sorted by output position), then every lane produces whole aligned
-// quads of the wave's CSR span: one LDS binary search per quad, four value
-// reads, one 16-byte store -- so a wave writes 1 KiB per store instruction
+// One block = one tile of 256 topics: finishes the scan (tile prefix + local
+// exclusive scan -> hit_offs), then each wave flattens its 64 topics' value
+// ranges into LDS (sorted by output position) and every lane produces whole
+// aligned quads of the wave's CSR span: one LDS binary search per quad, four
+// value reads, one 16-byte store -- a wave writes 1 KiB per store instruction
 // whatever the per-topic hit counts are.  Positions of topics that overflowed
-// RCAP ranges are skipped (k_rewalk_* writes them).
+// RCAP ranges are skipped (k_rewalk_tail writes them).
 __global__ __launch_bounds__(EMIT_BLOCK) void k_emit(DevIndex ix, Workspace ws, uint64_t n,
-                                                     const uint64_t *hit_offs, uint32_t *out, uint64_t cap) {
+                                                     uint64_t *hit_offs, uint32_t *out, uint64_t cap) {
     __shared__ uint32_t s_off[EMIT_WAVES][WR];
     __shared__ uint32_t s_rel[EMIT_WAVES][WR];
     __shared__ uint32_t s_cnt[EMIT_WAVES][WR];
+    __shared__ uint64_t s_w[4];
+    __shared__ uint64_t s_end[EMIT_WAVES];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const uint64_t t0 = ((uint64_t)blockIdx.x * EMIT_WAVES + wv) * 64;
-    if (t0 >= n) return;   // whole wave leaves; only wave-level sync below
-    const uint64_t t = t0 + lane;
+    const uint64_t t = (uint64_t)blockIdx.x * EMIT_BLOCK + threadIdx.x;
     const bool valid = t < n;
+    const uint32_t c = valid ? ws.cnt[t] : 0;
+    uint64_t total;
+    const uint64_t my = ws.blk[blockIdx.x] + block_excl_scan(c, total, s_w);
+    if (valid) hit_offs[t] = my;
+    if (lane == 63) s_end[wv] = my + c;
+    __syncthreads();
+    const uint64_t t0 = t - lane;
+    if (t0 >= n) return;   // whole wave leaves; only wave-level sync below
+    const uint64_t base = __shfl(my, 0, 64);
+    const uint64_t endp = s_end[wv];
     uint32_t nr = valid ? ws.nr[t] : 0;
-    if (nr > RCAP) nr = 0;   // written by k_rewalk_*
-    const uint64_t base = hit_offs[t0];
-    const uint64_t endp = hit_offs[t0 + 64 < n ? t0 + 64 : n];
-    const uint32_t rel = valid ? (uint32_t)(hit_offs[t] - base) : 0;
+    if (nr > RCAP) nr = 0;   // written by k_rewalk_tail
+    const uint32_t rel = (uint32_t)(my - base);
     uint32_t R;
     const uint32_t r0 = wave_excl_scan32(nr, R);
     uint32_t acc = 0;
@@ -578,49 +597,38 @@ __global__ void k_patch(const uint64_t *addr, const uint32_t *val, uint64_t n) {
 
 static inline uint32_t blocks_for(uint64_t n, uint32_t per) { return (uint32_t)((n + per - 1) / per); }
 
-static constexpr int MID_GRID = 256;   // list kernels: fixed grids, device-side list lengths
-
 hipError_t launch_match_phase1(const DevIndex &ix, const Workspace &ws, uint64_t n, const uint8_t *bytes,
                                const uint64_t *offs, uint64_t *hit_offs, uint8_t *err, hipStream_t s,
                                hipEvent_t ev_walk0, hipEvent_t ev_walk1) {
-    hipError_t e = hipMemsetAsync(ws.list_n, 0, sizeof(uint32_t) * L_COUNT, s);
-    if (e != hipSuccess) return e;
+    hipError_t e;
     Outs o{err, nullptr, nullptr};
+    const uint32_t nb = blocks_for(n, TILE);
     if (n) {
         if (ev_walk0 && (e = hipEventRecord(ev_walk0, s)) != hipSuccess) return e;
-        hipLaunchKernelGGL(k_walk_fast<MODE_COUNT>, dim3(blocks_for(n, WALK_BLOCK)), dim3(WALK_BLOCK), 0, s,
-                           ix, ws, n, bytes, offs, o);
+        hipLaunchKernelGGL(k_walk_fast<MODE_COUNT>, dim3(nb), dim3(WALK_BLOCK), 0, s, ix, ws, n, bytes, offs, o);
         if (ev_walk1 && (e = hipEventRecord(ev_walk1, s)) != hipSuccess) return e;
-        hipLaunchKernelGGL(k_walk_mid<MODE_COUNT>, dim3(MID_GRID), dim3(MID_BLOCK), 0, s, ix, ws, n, bytes, offs, o);
-        hipLaunchKernelGGL(k_walk_deep<MODE_COUNT>, dim3(DEEP_LANES / 64), dim3(64), 0, s, ix, ws, n, bytes, offs, o);
+        hipLaunchKernelGGL(k_walk_tail<MODE_COUNT>, dim3(TAIL_GRID), dim3(MID_BLOCK), 0, s, ix, ws, n, bytes, offs, o);
     }
-    const uint64_t nb = (n + SCAN_TILE - 1) / SCAN_TILE;
-    if (nb) hipLaunchKernelGGL(k_scan_reduce, dim3((uint32_t)nb), dim3(256), 0, s, ws.cnt, n, ws.blk);
-    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(256), 0, s, ws.blk, nb, hit_offs, n);
-    if (nb) hipLaunchKernelGGL(k_scan_apply, dim3((uint32_t)nb), dim3(256), 0, s, ws.cnt, n, ws.blk, hit_offs);
+    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(256), 0, s, ws.blk, (uint64_t)nb, hit_offs, n);
     return hipGetLastError();
 }
 
 hipError_t launch_match_phase2(const DevIndex &ix, const Workspace &ws, uint64_t n, const uint8_t *bytes,
-                               const uint64_t *offs, const uint64_t *hit_offs, uint32_t *out, uint64_t cap,
+                               const uint64_t *offs, uint64_t *hit_offs, uint32_t *out, uint64_t cap,
                                hipStream_t s) {
     if (!n) return hipSuccess;
-    hipLaunchKernelGGL(k_emit, dim3(blocks_for(n, EMIT_BLOCK)), dim3(EMIT_BLOCK), 0, s, ix, ws, n, hit_offs, out, cap);
-    hipLaunchKernelGGL(k_rewalk_mid, dim3(MID_GRID), dim3(MID_BLOCK), 0, s, ix, ws, n, bytes, offs, hit_offs, out, cap);
-    hipLaunchKernelGGL(k_rewalk_deep, dim3(DEEP_LANES / 64), dim3(64), 0, s, ix, ws, n, bytes, offs, hit_offs, out, cap);
+    hipLaunchKernelGGL(k_emit, dim3(blocks_for(n, TILE)), dim3(EMIT_BLOCK), 0, s, ix, ws, n, hit_offs, out, cap);
+    hipLaunchKernelGGL(k_rewalk_tail, dim3(TAIL_GRID), dim3(MID_BLOCK), 0, s, ix, ws, n, bytes, offs, hit_offs, out, cap);
     return hipGetLastError();
 }
 
 hipError_t launch_first(const DevIndex &ix, const Workspace &ws, uint64_t n, const uint8_t *bytes,
                         const uint64_t *offs, uint32_t *out_value, uint8_t *out_found, hipStream_t s) {
-    hipError_t e = hipMemsetAsync(ws.list_n, 0, sizeof(uint32_t) * L_COUNT, s);
-    if (e != hipSuccess) return e;
     if (!n) return hipSuccess;
     Outs o{nullptr, out_value, out_found};
     hipLaunchKernelGGL(k_walk_fast<MODE_FIRST>, dim3(blocks_for(n, WALK_BLOCK)), dim3(WALK_BLOCK), 0, s,
                        ix, ws, n, bytes, offs, o);
-    hipLaunchKernelGGL(k_walk_mid<MODE_FIRST>, dim3(MID_GRID), dim3(MID_BLOCK), 0, s, ix, ws, n, bytes, offs, o);
-    hipLaunchKernelGGL(k_walk_deep<MODE_FIRST>, dim3(DEEP_LANES / 64), dim3(64), 0, s, ix, ws, n, bytes, offs, o);
+    hipLaunchKernelGGL(k_walk_tail<MODE_FIRST>, dim3(TAIL_GRID), dim3(MID_BLOCK), 0, s, ix, ws, n, bytes, offs, o);
     return hipGetLastError();
 }
 
