@@ -213,15 +213,20 @@ def main():
         t1 = time.perf_counter()
         o.match_batch(probe.blob, probe.offs, nthreads=a.cpu_threads, with_values=False)
         r1 = n1 / (time.perf_counter() - t1)
-        n2 = int(min(B, max(n1, r1 * a.cpu_seconds)))
+        # a bounded sample of about cpu_seconds of CPU work: whole passes over
+        # the batch when it is shorter than that, else its first n2 topics
+        want = int(max(n1, r1 * a.cpu_seconds))
+        passes, n2 = (max(1, round(want / B)), B) if want >= B else (1, want)
         samp = ts.slice(0, n2)
         t1 = time.perf_counter()
-        o.match_batch(samp.blob, samp.offs, nthreads=a.cpu_threads, with_values=False)
+        for _ in range(passes):
+            o.match_batch(samp.blob, samp.offs, nthreads=a.cpu_threads, with_values=False)
         el_cpu = time.perf_counter() - t1
-        cpu = {"value": round(n2 / el_cpu, 1), "unit": "topic matches/s", "cores": a.cpu_threads, "kind": "port",
-               "sample": f"first {n2} topics of the same batch vs all {len(fs)} keys; oracle/tm_oracle.c "
-                         f"seek walker (emqx_trie_search restated) over a sorted key array, "
-                         f"{a.cpu_threads} pthreads, {el_cpu:.1f}s"}
+        what = f"{passes} passes over the {B}-topic batch" if passes > 1 else f"first {n2} topics of the batch"
+        cpu = {"value": round(passes * n2 / el_cpu, 1), "unit": "topic matches/s", "cores": a.cpu_threads,
+               "kind": "port",
+               "sample": f"{what} vs all {len(fs)} keys; oracle/tm_oracle.c seek walker (emqx_trie_search "
+                         f"restated) over a sorted key array, {a.cpu_threads} pthreads, {el_cpu:.1f}s"}
 
     res = {
         "metric": "topic matches/sec at 10M filters" if a.config == "c3" else f"topic matches/sec ({a.config})",

@@ -1,0 +1,134 @@
+#!/usr/bin/env python3
+"""Turn one tools/gpu_prof.sh output directory into the committed evidence
+under profiles/:
+
+  profiles/<round>_<tag>.md            kernel-trace summary per kernel and grid
+                                       (bench command + profiling driver) and
+                                       the PMC counters of the full-grid match
+                                       kernels with the derived figures
+  profiles/<round>_<tag>_*_stats.csv   rocprofv3 --stats summaries, verbatim
+  profiles/pmc_<config>.json           walk-kernel HBM bytes per launch, read by
+                                       bench.py for roofline.traffic
+
+HBM bytes: FETCH_SIZE and WRITE_SIZE are reported by rocprofv3 in KiB.
+FETCH_SIZE = TCC_EA0_RDREQ x 64 B (MI355X_MICROARCH.md, HBM section); the
+walk's reads are 16-B-per-lane loads of scattered 64-B lines, not the wide
+streaming reads the guide's x2 correction was calibrated on, so the value is
+taken as is (the memory-side request count x 64 B) and labelled uncalibrated.
+It also counts Infinity-Cache (MALL) hits, so it is an upper bound on HBM.
+
+usage: prof_report.py <prof_dir> <round> <tag> <config> <filters> <batch>
+"""
+import csv
+import json
+import os
+import shutil
+import sys
+from collections import defaultdict
+
+
+def short(name):
+    n = name.split("(")[0].replace("void ", "")
+    return n
+
+
+def trace_table(path):
+    rows = list(csv.DictReader(open(path)))
+    agg = defaultdict(list)
+    for r in rows:
+        grid = int(r.get("Grid_Size_X") or r.get("Grid_Size") or 0)
+        agg[(short(r["Kernel_Name"]), grid)].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    out = ["| kernel | grid (threads) | calls | avg us | min us | max us |", "|---|---|---|---|---|---|"]
+    for (name, grid), d in sorted(agg.items(), key=lambda kv: -sum(kv[1])):
+        if "tmx::" not in name:
+            continue
+        out.append(f"| {name} | {grid} | {len(d)} | {sum(d) / len(d) / 1e3:.2f} | {min(d) / 1e3:.2f} | {max(d) / 1e3:.2f} |")
+    return out, agg
+
+
+def pmc_values(prof, grid):
+    vals = defaultdict(lambda: defaultdict(list))
+    for d in sorted(os.listdir(prof)):
+        p = os.path.join(prof, d, "run_counter_collection.csv")
+        if not (d.startswith("pmc") and os.path.isfile(p)):
+            continue
+        for r in csv.DictReader(open(p)):
+            if int(r["Grid_Size"]) != grid or "tmx::" not in r["Kernel_Name"]:
+                continue
+            vals[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in vals.items()}
+
+
+def main(prof, rnd, tag, config, filters, batch):
+    filters, batch = int(filters), int(batch)
+    grid = (batch + 255) // 256 * 256
+    lines = [f"# Profile {rnd}/{tag}: config {config}, {filters} filters, {batch}-topic batches", ""]
+    bench_json = os.path.join(prof, "bench.json")
+    if os.path.isfile(bench_json) and os.path.getsize(bench_json):
+        lines += ["## bench.py line (run under rocprofv3 --kernel-trace --stats)", "", "```",
+                  open(bench_json).read().strip(), "```", ""]
+    durations = {}
+    for sub, title in (("bench", "bench.py --steps 10 --warmup 2 (includes the 4k/64k latency batches)"),
+                       ("trace", "tools/profile_walk.py (full batches only)")):
+        p = os.path.join(prof, sub, "run_kernel_trace.csv")
+        if not os.path.isfile(p):
+            continue
+        tab, agg = trace_table(p)
+        lines += [f"## Kernel trace: {title}", ""] + tab + [""]
+        for (name, g), d in agg.items():
+            if g == grid:
+                durations.setdefault(name, []).extend(d)
+        st = os.path.join(prof, sub, "run_kernel_stats.csv")
+        if os.path.isfile(st):
+            shutil.copy(st, os.path.join("profiles", f"{rnd}_{tag}_{sub}_kernel_stats.csv"))
+    pm = pmc_values(prof, grid)
+    walk = [k for k in pm if "k_walk_fast" in k]
+    res = {"config": config, "filters": filters, "batch": batch, "grid": grid}
+    if pm:
+        lines += [f"## PMC counters per launch (grid {grid}, mean over launches; one rocprofv3 --pmc pass per group)", ""]
+        names = sorted({c for k in pm for c in pm[k]})
+        lines.append("| counter | " + " | ".join(sorted(pm)) + " |")
+        lines.append("|---|" + "---|" * len(pm))
+        for c in names:
+            lines.append(f"| {c} | " + " | ".join(f"{pm[k].get(c, float('nan')):.6g}" for k in sorted(pm)) + " |")
+        lines.append("")
+        lines += ["## Derived", ""]
+        for k in sorted(pm):
+            c = pm[k]
+            d = durations.get(k)
+            dur = sum(d) / len(d) * 1e-9 if d else None
+            fb = c.get("FETCH_SIZE", 0) * 1024
+            wb = c.get("WRITE_SIZE", 0) * 1024
+            hit = c.get("TCC_HIT_sum"), c.get("TCC_MISS_sum")
+            lines.append(f"* **{k}**: avg {dur * 1e6:.1f} us; " if dur else f"* **{k}**: ")
+            lines[-1] += (f"memory-side reads {fb / 1e6:.1f} MB ({fb / batch:.0f} B/topic), writes {wb / 1e6:.1f} MB "
+                          f"({wb / batch:.0f} B/topic)")
+            if dur:
+                lines[-1] += f", {(fb + wb) / dur / 1e9:.0f} GB/s"
+            if hit[0] is not None and hit[1] is not None and hit[0] + hit[1] > 0:
+                lines[-1] += f"; L2 hit {hit[0] / (hit[0] + hit[1]) * 100:.1f}%"
+            if c.get("TCP_TCC_READ_REQ_sum"):
+                lines[-1] += (f"; L1->L2 read requests {c['TCP_TCC_READ_REQ_sum'] / batch:.1f}/topic, "
+                              f"mean L2 latency {c.get('TCP_TCC_READ_REQ_LATENCY_sum', 0) / c['TCP_TCC_READ_REQ_sum']:.0f} cycles")
+            if c.get("SQ_WAVE_CYCLES"):
+                lines[-1] += (f"; waves parked on waitcnt {c.get('SQ_WAIT_ANY', 0) / c['SQ_WAVE_CYCLES'] * 100:.0f}% "
+                              f"of wave-cycles, VMEM reads {c.get('SQ_INSTS_VMEM_RD', 0) / c.get('SQ_WAVES', 1):.0f}/wave")
+            if dur and c.get("GRBM_GUI_ACTIVE"):
+                lines[-1] += f"; clock ~{c['GRBM_GUI_ACTIVE'] / 8 / dur / 1e9:.2f} GHz"
+        lines.append("")
+        if walk:
+            c = pm[walk[0]]
+            res["walk_kernel"] = walk[0]
+            res["walk_fetch_bytes_per_launch"] = int(c.get("FETCH_SIZE", 0) * 1024)
+            res["walk_write_bytes_per_launch"] = int(c.get("WRITE_SIZE", 0) * 1024)
+            res["walk_hbm_bytes_per_launch"] = res["walk_fetch_bytes_per_launch"] + res["walk_write_bytes_per_launch"]
+            res["note"] = ("FETCH_SIZE (memory-side 64-B read requests, MALL hits included) + WRITE_SIZE, "
+                           "uncalibrated for 16-B scattered line reads")
+            res["source"] = f"profiles/{rnd}_{tag}.md"
+            json.dump(res, open(os.path.join("profiles", f"pmc_{config}.json"), "w"), indent=1)
+    open(os.path.join("profiles", f"{rnd}_{tag}.md"), "w").write("\n".join(lines) + "\n")
+    print("\n".join(lines))
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:])
