@@ -21,7 +21,10 @@ struct DevIndex {
 constexpr int FAST_L = 8;        // levels handled by the main walk kernel (LDS frontier)
 constexpr int MID_L = 32;        // levels handled by the list kernels with an LDS frontier
 constexpr int MAX_LEVELS = 65536;// MQTT topics are <= 65535 bytes
-constexpr int RCAP = 8;          // terminal ranges kept per topic before the re-walk path
+#ifndef RCAP_N
+#define RCAP_N 8
+#endif
+constexpr int RCAP = RCAP_N;          // terminal ranges kept per topic before the re-walk path
 constexpr int DEEP_LANES = 64;   // lanes of the global-scratch (deep / overflow) kernels
 
 enum { L_MID = 0, L_DEEP = 1, L_OVF_MID = 2, L_OVF_DEEP = 3, L_COUNT = 4 };

@@ -131,7 +131,14 @@ int fail(tm_index *h, int code, const std::string &msg) {
 
 // ---------------------------------------------------------------- hashing
 
+void pack8(const uint8_t *p, uint32_t n, uint32_t &b0, uint32_t &b1);
+
 uint64_t word_hash(const uint8_t *p, uint32_t n) {
+    if (n <= VINL) {
+        uint32_t b0, b1;
+        pack8(p, n, b0, b1);
+        return word_hash_short(b0, b1, n);
+    }
     uint64_t x = FNV_OFF;
     for (uint32_t i = 0; i < n; i++) x = (x ^ p[i]) * FNV_PRIME;
     return word_hash_finish(x, n);
@@ -184,8 +191,10 @@ void vocab_bytes(tm_index *ix, const VocabEntry &e, std::string &out) {
 }
 
 void vocab_grow(tm_index *ix, uint64_t need) {
-    if (need * 2 <= ix->vocab.h.size()) return;
-    std::vector<VocabEntry> nt(pow2_at_least(need * 2), empty_vocab());
+    // load <= 1/4: the walk's deferred probes resolve on the first slot
+    // almost always (one round trip per topic for all its levels)
+    if (need * 4 <= ix->vocab.h.size()) return;
+    std::vector<VocabEntry> nt(pow2_at_least(need * 4), empty_vocab());
     const uint32_t mask = (uint32_t)nt.size() - 1;
     std::string w;
     for (const VocabEntry &e : ix->vocab.h) {

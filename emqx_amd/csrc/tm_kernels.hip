@@ -33,8 +33,8 @@ namespace tmx {
 __device__ __forceinline__ uint4 ld4(const void *p) { return *reinterpret_cast<const uint4 *>(p); }
 
 struct WordAcc {
-    uint64_t h;
-    uint32_t len, b0, b1;
+    uint64_t h;                 // FNV-1a over the bytes (used for words > VINL bytes)
+    uint32_t len, b0, b1;       // length, first 8 bytes packed little endian
     uint64_t start;
     __device__ __forceinline__ void reset(uint64_t s) {
         h = FNV_OFF; len = 0; b0 = b1 = 0; start = s;
@@ -52,23 +52,31 @@ __device__ bool bytes_eq(const uint8_t *a, const uint8_t *b, uint32_t n) {
     return true;
 }
 
-// vocab: word -> wid, exact by construction (hash tag, then length and bytes)
-__device__ uint32_t vocab_find(const DevIndex &ix, const WordAcc &w, const uint8_t *blob) {
-    const uint64_t h = word_hash_finish(w.h, w.len);
-    const uint32_t tag = vocab_tag(h, w.len);
-    uint32_t slot = (uint32_t)h & ix.vmask;
+__device__ __forceinline__ uint64_t word_hash_dev(const WordAcc &w) {
+    return w.len <= VINL ? word_hash_short(w.b0, w.b1, w.len) : word_hash_finish(w.h, w.len);
+}
+
+// continue a vocab probe sequence from `slot` (exact: tag, then bytes)
+__device__ uint32_t vocab_probe(const DevIndex &ix, uint32_t slot, uint32_t tag, uint32_t len, uint32_t b0,
+                                uint32_t b1, const uint8_t *bytes) {
     for (;;) {
         const uint4 e = ld4(ix.vocab + slot);   // tag, wid, b0, b1
         if (e.y == NONE) return NONE;
         if (e.x == tag) {
-            if (w.len <= VINL) {
-                if (e.z == w.b0 && e.w == w.b1) return e.y;
-            } else if (e.w == w.len && bytes_eq(ix.wpool + e.z, blob + w.start, w.len)) {
+            if (len <= VINL) {
+                if (e.z == b0 && e.w == b1) return e.y;
+            } else if (e.w == len && bytes_eq(ix.wpool + e.z, bytes, len)) {
                 return e.y;
             }
         }
         slot = (slot + 1) & ix.vmask;
     }
+}
+
+// vocab: word -> wid, exact by construction (hash tag, then length and bytes)
+__device__ uint32_t vocab_find(const DevIndex &ix, const WordAcc &w, const uint8_t *blob) {
+    const uint64_t h = word_hash_dev(w);
+    return vocab_probe(ix, (uint32_t)h & ix.vmask, vocab_tag(h, w.len), w.len, w.b0, w.b1, blob + w.start);
 }
 
 // literal child in a node's private table (table mode, nlit > KINL)
@@ -88,12 +96,22 @@ __device__ __forceinline__ uint32_t ctab_find(const DevIndex &ix, uint32_t off, 
 template <int ML>
 struct LdsStore {
     static constexpr uint32_t maxl = ML;
+    static constexpr bool deferred = true;   // vocab probes of short words after tokenisation
     uint32_t *wid, *pend;
+    uint8_t *len8;                           // [level][thread] word lengths (deferred probes)
     uint32_t stride;
     uint64_t mask;
     __device__ __forceinline__ uint32_t get_wid(uint32_t l) const { return wid[l * stride]; }
     __device__ __forceinline__ void set_wid(uint32_t l, uint32_t w) { wid[l * stride] = w; }
     __device__ __forceinline__ void reset() { mask = 0; }
+    // deferred vocab probes: a short word's packed bytes + length, parked in
+    // the wid / pend slots of its level until the probe resolves it
+    __device__ __forceinline__ void put_word(uint32_t l, uint32_t b0, uint32_t b1, uint32_t len) {
+        wid[l * stride] = b0; pend[l * stride] = b1; len8[l * stride] = (uint8_t)len;
+    }
+    __device__ __forceinline__ uint32_t word_b0(uint32_t l) const { return wid[l * stride]; }
+    __device__ __forceinline__ uint32_t word_b1(uint32_t l) const { return pend[l * stride]; }
+    __device__ __forceinline__ uint32_t word_len(uint32_t l) const { return len8[l * stride]; }
     __device__ __forceinline__ void push(uint32_t l, uint32_t node) {
         pend[l * stride] = node; mask |= 1ull << l;
     }
@@ -109,6 +127,7 @@ struct LdsStore {
 // Global-scratch frontier for arbitrarily deep topics (one slot per lane).
 struct GlobalStore {
     static constexpr uint32_t maxl = MAX_LEVELS;
+    static constexpr bool deferred = false;
     uint32_t *wid;
     uint2 *stk;
     uint32_t top;
@@ -127,30 +146,56 @@ struct GlobalStore {
 
 enum { RC_OK = 0, RC_BADARG = 1, RC_DEEP = 2 };
 
+// levels whose vocab probes are in flight together (6 covers MQTT's usual
+// topic depths in one round trip and keeps k_walk_fast within 64 VGPRs, i.e.
+// 8 waves per SIMD)
+#ifndef VGROUP
+#define VGROUP 6
+#endif
+
 // topic_words/1 (emqx_trie_search.erl:369-378): split on '/', a level that is
 // exactly '+' or '#' is badarg; level words are resolved to wids.  Also
 // computes base_init's '$' flag (:160-163) and the exact-key hash.
+//
+// Two passes.  The scan (ALU only once the first two 16-byte chunks of the
+// topic are in) keeps each short word's packed bytes and length in the
+// frontier's LDS slots; words longer than VINL bytes are looked up on the spot.
+// Then the vocab probes of up to VGROUP levels are issued together, so a topic's
+// words cost one memory round trip instead of one per level, and the lanes of a
+// wave no longer serialise on the byte position where each of their words ends.
 template <class S>
 __device__ int tokenize(const DevIndex &ix, const uint8_t *blob, uint64_t beg, uint64_t end, S &st,
                         uint32_t &L, bool &dollar, uint64_t &xh, bool &all_found) {
     WordAcc w; w.reset(beg);
     uint32_t lev = 0;
+    uint64_t longmask = 0;   // levels resolved during the scan (deferred stores)
     all_found = true; dollar = false; xh = FNV_OFF;
     auto finish = [&]() -> int {
         if (w.len == 1 && (w.b0 == '+' || w.b0 == '#')) return RC_BADARG;
         if (lev >= S::maxl) return RC_DEEP;
         if (lev == 0 && w.len >= 1 && (w.b0 & 0xFF) == '$') dollar = true;
-        uint32_t wid = vocab_find(ix, w, blob);
-        st.set_wid(lev, wid);
-        all_found &= wid != NONE;
-        xh = seq_hash_step(xh, wid);
+        if constexpr (S::deferred) {
+            if (w.len <= VINL) {
+                st.put_word(lev, w.b0, w.b1, w.len);
+            } else {
+                st.set_wid(lev, vocab_find(ix, w, blob));
+                longmask |= 1ull << lev;
+            }
+        } else {
+            st.set_wid(lev, vocab_find(ix, w, blob));
+        }
         lev++;
         return RC_OK;
     };
-    for (uint64_t p = beg & ~15ull; p < end; p += 16) {
-        // aligned 16-byte loads: the chunk shares its 16-byte granule with a
-        // valid byte, so it never crosses a page the caller does not own
-        const uint4 v = ld4(blob + p);
+    const uint64_t p0 = beg & ~15ull;
+    // aligned 16-byte loads (the first two issued together): a chunk shares its 16-byte granule with a valid
+    // byte, so it never crosses a page the caller does not own
+    const uint4 z = make_uint4(0, 0, 0, 0);
+    const uint4 c0 = p0 < end ? ld4(blob + p0) : z;
+    const uint4 c1 = p0 + 16 < end ? ld4(blob + p0 + 16) : z;
+    uint32_t ci = 0;
+    for (uint64_t p = p0; p < end; p += 16, ci++) {
+        const uint4 v = ci == 0 ? c0 : ci == 1 ? c1 : ld4(blob + p);
         const uint32_t k0 = p < beg ? (uint32_t)(beg - p) : 0;
         const uint32_t k1 = end - p < 16 ? (uint32_t)(end - p) : 16;
         for (uint32_t k = k0; k < k1; k++) {
@@ -168,6 +213,44 @@ __device__ int tokenize(const DevIndex &ix, const uint8_t *blob, uint64_t beg, u
     int rc = finish();
     if (rc) return rc;
     L = lev;
+    if constexpr (S::deferred) {
+        for (uint32_t base = 0; base < L; base += VGROUP) {
+            uint4 e[VGROUP];
+            uint32_t tg[VGROUP];
+#pragma unroll
+            for (uint32_t k = 0; k < VGROUP; k++) {
+                const uint32_t l = base + k;
+                tg[k] = 0;
+                if (l < L && !((longmask >> l) & 1)) {
+                    const uint32_t len = st.word_len(l);
+                    const uint64_t h = word_hash_short(st.word_b0(l), st.word_b1(l), len);
+                    tg[k] = vocab_tag(h, len);
+                    e[k] = ld4(ix.vocab + ((uint32_t)h & ix.vmask));
+                }
+            }
+#pragma unroll
+            for (uint32_t k = 0; k < VGROUP; k++) {
+                const uint32_t l = base + k;
+                if (l < L && !((longmask >> l) & 1)) {
+                    const uint32_t b0 = st.word_b0(l), b1 = st.word_b1(l);
+                    uint32_t wid;
+                    if (e[k].y == NONE) wid = NONE;
+                    else if (e[k].x == tg[k] && e[k].z == b0 && e[k].w == b1) wid = e[k].y;
+                    else {   // rare at load <= 1/4: walk the probe sequence on
+                        const uint32_t len = st.word_len(l);
+                        const uint64_t h = word_hash_short(b0, b1, len);
+                        wid = vocab_probe(ix, ((uint32_t)h + 1) & ix.vmask, tg[k], len, b0, b1, nullptr);
+                    }
+                    st.set_wid(l, wid);
+                }
+            }
+        }
+    }
+    for (uint32_t l = 0; l < L; l++) {
+        const uint32_t wid = st.get_wid(l);
+        all_found &= wid != NONE;
+        xh = seq_hash_step(xh, wid);
+    }
     xh = seq_hash_finish(xh, L);
     return RC_OK;
 }
@@ -178,14 +261,15 @@ __device__ uint32_t count_levels(const uint8_t *blob, uint64_t beg, uint64_t end
     return n;
 }
 
-// match_topics/4 (emqx_trie_search.erl:381-389): binary keys equal to the topic
+// match_topics/4 (emqx_trie_search.erl:381-389): binary keys equal to the topic.
+// The first 16 bytes of the home slot (`a`) are loaded before the trie walk so
+// their latency hides behind it; later probes are rare.
 template <class S>
-__device__ void exact_find(const DevIndex &ix, uint64_t xh, uint32_t L, const S &st, uint32_t &off, uint32_t &cnt) {
+__device__ void exact_find(const DevIndex &ix, uint64_t xh, uint32_t L, const S &st, uint32_t slot, uint4 a,
+                           uint32_t &off, uint32_t &cnt) {
     cnt = 0; off = 0;
-    uint32_t slot = (uint32_t)xh & ix.xmask;
     for (;;) {
         const uint4 *e = reinterpret_cast<const uint4 *>(ix.exact + slot);
-        uint4 a = e[0];
         if (a.z == NONE) return;
         if (a.x == (uint32_t)xh && a.y == (uint32_t)(xh >> 32) && a.z == L) {
             uint4 b = e[1], c = e[2], d = e[3];
@@ -201,6 +285,7 @@ __device__ void exact_find(const DevIndex &ix, uint64_t xh, uint32_t L, const S 
             if (eq) { off = a.w; cnt = b.x; return; }
         }
         slot = (slot + 1) & ix.xmask;
+        a = ld4(ix.exact + slot);
     }
 }
 
@@ -254,15 +339,24 @@ __device__ bool dfs(const DevIndex &ix, uint32_t L, bool dollar, S &st, EM &em) 
 
 // ---------------------------------------------------------------- emitters
 
-struct RangeEmit {          // phase 1: count hits, keep up to RCAP value ranges
-    uint2 *rng;
+struct RangeEmit {          // phase 1: count hits, keep up to RCAP value ranges in registers
+    uint2 r[RCAP];
     uint32_t cnt, nr;
     __device__ __forceinline__ bool operator()(uint32_t off, uint32_t n) {
         if (n) {
-            if (nr < RCAP) rng[nr] = make_uint2(off, n);
+#pragma unroll
+            for (uint32_t i = 0; i < RCAP; i++)
+                if (nr == i) r[i] = make_uint2(off, n);
             nr++; cnt += n;
         }
         return true;
+    }
+    // ranges are stored rank-major (rng[i * n + t]): lanes of a wave write and
+    // k_emit reads them coalesced
+    __device__ __forceinline__ void store(uint2 *rng, uint64_t n, uint64_t t) const {
+#pragma unroll
+        for (uint32_t i = 0; i < RCAP; i++)
+            if (i < nr) rng[(uint64_t)i * n + t] = r[i];
     }
 };
 
@@ -293,10 +387,12 @@ __device__ int match_topic(const DevIndex &ix, const uint8_t *blob, uint64_t beg
     int rc = tokenize(ix, blob, beg, end, st, L, dollar, xh, allf);
     if (rc) return rc;
     st.reset();
+    const uint32_t xslot = (uint32_t)xh & ix.xmask;
+    const uint4 xa = allf ? ld4(ix.exact + xslot) : make_uint4(0, 0, NONE, 0);
     if (!dfs(ix, L, dollar, st, em)) return RC_OK;
     if (allf) {
         uint32_t xoff, xcnt;
-        exact_find(ix, xh, L, st, xoff, xcnt);
+        exact_find(ix, xh, L, st, xslot, xa, xoff, xcnt);
         em(xoff, xcnt);
     }
     return RC_OK;
@@ -323,12 +419,14 @@ __device__ int run_topic(const DevIndex &ix, const Workspace &ws, uint64_t n, co
                          const uint64_t *offs, uint64_t t, S &st, const Outs &o, uint32_t *hits) {
     const uint64_t beg = offs[t], end = offs[t + 1];
     if (MODE == MODE_COUNT) {
-        RangeEmit em{ws.rng + t * RCAP, 0, 0};
+        RangeEmit em;
+        em.cnt = 0; em.nr = 0;
         int rc = match_topic(ix, blob, beg, end, st, em);
         if (rc == RC_DEEP) return rc;
         if (rc == RC_BADARG) { em.cnt = 0; em.nr = 0; }
         ws.cnt[t] = em.cnt;
         ws.nr[t] = em.nr;
+        em.store(ws.rng, n, t);
         o.err[t] = rc == RC_BADARG;
         if (em.nr > RCAP) list_push(ws, n, S::maxl <= MID_L ? L_OVF_MID : L_OVF_DEEP, (uint32_t)t);
         *hits = em.cnt;
@@ -393,15 +491,16 @@ constexpr int WALK_BLOCK = 256;
 static_assert(WALK_BLOCK == TILE, "walk blocks are scan tiles");
 
 template <int MODE>
-__global__ __launch_bounds__(WALK_BLOCK) void k_walk_fast(DevIndex ix, Workspace ws, uint64_t n,
+__global__ __launch_bounds__(WALK_BLOCK, 8) void k_walk_fast(DevIndex ix, Workspace ws, uint64_t n,
                                                           const uint8_t *blob, const uint64_t *offs, Outs o) {
     __shared__ uint32_t s_wid[FAST_L * WALK_BLOCK];
     __shared__ uint32_t s_pend[(FAST_L + 1) * WALK_BLOCK];
+    __shared__ uint8_t s_len[FAST_L * WALK_BLOCK];
     __shared__ uint64_t s_w[4];
     const uint64_t t = (uint64_t)blockIdx.x * WALK_BLOCK + threadIdx.x;
     uint32_t hits = 0;
     if (t < n) {
-        LdsStore<FAST_L> st{s_wid + threadIdx.x, s_pend + threadIdx.x, WALK_BLOCK, 0};
+        LdsStore<FAST_L> st{s_wid + threadIdx.x, s_pend + threadIdx.x, s_len + threadIdx.x, WALK_BLOCK, 0};
         int rc = run_topic<MODE>(ix, ws, n, blob, offs, t, st, o, &hits);
         if (rc == RC_DEEP) {
             hits = 0;   // counted by k_walk_tail (atomically added to this tile)
@@ -440,11 +539,12 @@ __global__ __launch_bounds__(MID_BLOCK) void k_walk_tail(DevIndex ix, Workspace 
                                                          const uint8_t *blob, const uint64_t *offs, Outs o) {
     __shared__ uint32_t s_wid[MID_L * MID_BLOCK];
     __shared__ uint32_t s_pend[(MID_L + 1) * MID_BLOCK];
+    __shared__ uint8_t s_len[MID_L * MID_BLOCK];
     uint32_t hits = 0;
     if (blockIdx.x < MID_GRID) {
         const uint32_t cnt = ws.list_n[L_MID];
         const uint32_t *lst = ws.lists + (uint64_t)L_MID * n;
-        LdsStore<MID_L> st{s_wid + threadIdx.x, s_pend + threadIdx.x, MID_BLOCK, 0};
+        LdsStore<MID_L> st{s_wid + threadIdx.x, s_pend + threadIdx.x, s_len + threadIdx.x, MID_BLOCK, 0};
         for (uint32_t i = blockIdx.x * MID_BLOCK + threadIdx.x; i < cnt; i += MID_GRID * MID_BLOCK) {
             run_topic<MODE>(ix, ws, n, blob, offs, lst[i], st, o, &hits);
             if (MODE == MODE_COUNT && hits) atomicAdd((unsigned long long *)&ws.blk[lst[i] / TILE], hits);
@@ -475,10 +575,11 @@ __global__ __launch_bounds__(MID_BLOCK) void k_rewalk_tail(DevIndex ix, Workspac
                                                            uint32_t *out, uint64_t cap) {
     __shared__ uint32_t s_wid[MID_L * MID_BLOCK];
     __shared__ uint32_t s_pend[(MID_L + 1) * MID_BLOCK];
+    __shared__ uint8_t s_len[MID_L * MID_BLOCK];
     if (blockIdx.x < MID_GRID) {
         const uint32_t cnt = ws.list_n[L_OVF_MID];
         const uint32_t *lst = ws.lists + (uint64_t)L_OVF_MID * n;
-        LdsStore<MID_L> st{s_wid + threadIdx.x, s_pend + threadIdx.x, MID_BLOCK, 0};
+        LdsStore<MID_L> st{s_wid + threadIdx.x, s_pend + threadIdx.x, s_len + threadIdx.x, MID_BLOCK, 0};
         for (uint32_t i = blockIdx.x * MID_BLOCK + threadIdx.x; i < cnt; i += MID_GRID * MID_BLOCK)
             rewalk(ix, blob, offs, lst[i], hit_offs, out, cap, st);
     } else {
@@ -546,7 +647,7 @@ __global__ __launch_bounds__(EMIT_BLOCK) void k_emit(DevIndex ix, Workspace ws, 
     const uint32_t r0 = wave_excl_scan32(nr, R);
     uint32_t acc = 0;
     for (uint32_t i = 0; i < nr; i++) {
-        const uint2 g = ws.rng[t * RCAP + i];
+        const uint2 g = ws.rng[(uint64_t)i * n + t];
         s_off[wv][r0 + i] = g.x;
         s_rel[wv][r0 + i] = rel + acc;
         s_cnt[wv][r0 + i] = g.y;

@@ -93,6 +93,13 @@ TM_HD uint64_t mix64(uint64_t x) {          // splitmix64 finaliser
 constexpr uint64_t FNV_OFF = 0xcbf29ce484222325ull;
 constexpr uint64_t FNV_PRIME = 0x100000001b3ull;
 
+// Word hash.  A word of <= VINL bytes is hashed from its packed little-endian
+// bytes (b0 = bytes 0..3, b1 = bytes 4..7, zero padded) and its length, so the
+// walk kernel can defer its vocab probe to after tokenisation with nothing but
+// (b0, b1, len) kept per level; a longer word is FNV-1a over its bytes.
+TM_HD uint64_t word_hash_short(uint32_t b0, uint32_t b1, uint32_t len) {
+    return mix64((((uint64_t)b1 << 32) | b0) + 0x9e3779b97f4a7c15ull * (len + 1));
+}
 TM_HD uint64_t word_hash_finish(uint64_t fnv, uint32_t len) { return mix64(fnv ^ ((uint64_t)len << 56)); }
 
 TM_HD uint32_t vocab_tag(uint64_t h, uint32_t len) {
