@@ -9,6 +9,15 @@ mixed-wildcard filters incl. $share dests, $SYS filters and root globals),
 holds a replica of the index and matches its own batch; there is no
 data-path collective.
 
+Other modes (not the headline line):
+  --config c4   filter-sharded (100M filters split over the ranks, each rank
+                matches the SAME batch against its shard, the hit lists are
+                allgathered over RCCL and merged on the device): strong scaling
+  --config c5   churn: every step first applies --deltas subscribe/unsubscribe
+                ops (one router-syncer batch) to the replicated index, then
+                matches the batch; reports deltas/s beside topics/s
+  --config c1 / c2 / c2nm   the other BASELINE.json configs, topic-sharded
+
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3]
        torchrun ... bench.py --gpus N  (one rank per GPU)
 """
@@ -32,6 +41,8 @@ CONFIGS = {
     "c2": (2, 1_000_000, "1M 'fleet/{id}/sensor/+' + 1k global '#' rules"),
     "c2nm": (20, 1_000_000, "1M 'fleet/{id}/sensor/+' + 1k non-matching 'rules/{k}/#' globals"),
     "c3": (3, 10_000_000, "10M mixed-wildcard filters incl. $share groups and '$SYS' exclusion"),
+    "c4": (4, 100_000_000, "100M mixed filters filter-sharded over the ranks, RCCL allgatherv of hit lists"),
+    "c5": (5, 10_000_000, "churn: 10M mixed filters, subscribe/unsubscribe deltas interleaved with match batches"),
 }
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
@@ -48,9 +59,11 @@ def parse():
     p.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     p.add_argument("--filters", type=int, default=None)
     p.add_argument("--batch", type=int, default=1_000_000, help="topics per GPU per step")
-    p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget")
+    p.add_argument("--deltas", type=int, default=1000, help="c5: deltas applied per step")
+    p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     p.add_argument("--cpu-threads", type=int, default=16)
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--no-parity", action="store_true")
     p.add_argument("--latency-batches", type=int, default=20)
     p.add_argument("--frontier-sample", type=int, default=20_000)
     return p.parse_args()
@@ -64,19 +77,20 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        dist.init_process_group("nccl")
     torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
     dev = torch.device(f"cuda:{local}")
 
-    from emqx_amd import _native, workload as wl
+    from emqx_amd import _native, shard, workload as wl
 
     gen_cfg, default_f, desc = CONFIGS[a.config]
+    filter_sharded = a.config == "c4"
     nf = a.filters or default_f
     B = a.batch
 
     t = time.time()
-    fs = wl.filters(gen_cfg, nf)
+    fs = wl.filters(gen_cfg, nf, shard=rank, nshards=world) if filter_sharded else wl.filters(gen_cfg, nf)
     t_gen = time.time() - t
     log(f"[rank {rank}] generated {len(fs)} filters in {t_gen:.1f}s")
 
@@ -96,26 +110,47 @@ def main():
     log(f"[rank {rank}] index: {st['n_keys']} keys, {st['n_nodes']} nodes, {st['n_edges']} edges, "
         f"{st['n_words']} words, {st['device_bytes'] / 2**20:.0f} MiB HBM; compile {t_compile:.1f}s upload {t_upload:.2f}s")
 
-    ts = wl.topics(gen_cfg, nf, B, first=rank * B)
+    # topic-sharded: rank r matches topics [r B, (r+1) B); filter-sharded: all ranks the same batch
+    first = 0 if filter_sharded else rank * B
+    ts = wl.topics(gen_cfg, nf, B, first=first)
     d_blob = torch.from_numpy(ts.blob).to(dev)
     d_offs = torch.from_numpy(ts.offs.view(np.int64)).to(dev)
     d_hit = torch.zeros(B + 1, dtype=torch.int64, device=dev)
     d_err = torch.zeros(B, dtype=torch.uint8, device=dev)
     d_out = torch.zeros(1, dtype=torch.int32, device=dev)
 
+    # c5: the delta stream, generated up front (host buffers, as the syncer hands them over)
+    dchunks = []
+    if a.config == "c5":
+        nd = a.deltas * (a.steps + a.warmup + 1)
+        dl = wl.deltas(nf, 0, nd)
+        dchunks = [dl.slice(k * a.deltas, (k + 1) * a.deltas) for k in range(a.steps + a.warmup + 1)]
+    dpos = [0]
+
     def step(cap):
+        if dchunks:
+            d = dchunks[dpos[0]]
+            dpos[0] += 1
+            ix.apply(d.flags, d.blob, d.offs, d.vals)
         ix.match_batch_dev(B, d_blob.data_ptr(), d_offs.data_ptr(), d_hit.data_ptr(), d_out.data_ptr(), cap,
                            d_err.data_ptr(), stream)
+        if filter_sharded:
+            if world == 1:   # one shard: the merge alone (the exchange is the identity)
+                return shard.merge(d_hit.view(1, B + 1), d_out.view(1, -1), d_out.numel(), stream)
+            return shard.allgatherv_hits(d_hit, d_out, stream=stream)
+        return None
 
-    step(0)
+    # sizing pass (no values written), then the output buffer
+    ix.match_batch_dev(B, d_blob.data_ptr(), d_offs.data_ptr(), d_hit.data_ptr(), d_out.data_ptr(), 0,
+                       d_err.data_ptr(), stream)
     torch.cuda.synchronize()
     total_hits = int(d_hit[-1].item())
-    d_out = torch.zeros(max(total_hits, 1), dtype=torch.int32, device=dev)
-    cap = total_hits
+    slack = a.deltas * (a.steps + a.warmup) * 64 if dchunks else 0   # churn may add hits
+    d_out = torch.zeros(max(total_hits + slack, 1), dtype=torch.int32, device=dev)
+    cap = total_hits + slack
     for _ in range(a.warmup):
         step(cap)
     torch.cuda.synchronize()
-    assert int(d_hit[-1].item()) == total_hits
     assert not bool(d_err.any().item())
 
     ix.profile(True)
@@ -124,8 +159,9 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    merged = None
     for _ in range(a.steps):
-        step(cap)
+        merged = step(cap)
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     if world > 1:
@@ -136,11 +172,37 @@ def main():
     if world > 1:
         dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
     el_max = float(el_t.item())
+    last_hits = int(d_hit[-1].item())
+    assert last_hits <= cap
+    merged_total = int(merged[0][-1].item()) if merged is not None else None
 
-    value = world * B * a.steps / el_max
+    # whole-job topics/s: topic-sharded = every rank's own batch; filter-sharded = the one shared batch
+    topics_per_step = B if filter_sharded else world * B
+    value = topics_per_step * a.steps / el_max
     ms_per_step = el_max / a.steps * 1e3
     walk_avg_ms = walk_ms / max(nb, 1)
     batch_avg_ms = batch_ms / max(nb, 1)
+
+    # p50/p99 batch latency: host topics in, hit lists back in host memory (every rank)
+    lat = {}
+    if not filter_sharded:
+        for lb in sorted({min(4096, B), min(65536, B)}):
+            sub = ts.slice(0, lb)
+            xs = []
+            for k in range(a.latency_batches + 2):
+                t1 = time.perf_counter()
+                ix.match_batch(sub.blob, sub.offs)
+                xs.append((time.perf_counter() - t1) * 1e3)
+            xs = np.array(xs[2:])
+            lat[str(lb)] = {"p50_ms": float(np.percentile(xs, 50)), "p99_ms": float(np.percentile(xs, 99))}
+    if world > 1 and lat:
+        # the slowest rank's percentiles (max over ranks)
+        keys = sorted(lat)
+        v = torch.tensor([lat[k][q] for k in keys for q in ("p50_ms", "p99_ms")], dtype=torch.float64, device=dev)
+        dist.all_reduce(v, op=dist.ReduceOp.MAX)
+        v = v.tolist()
+        lat = {k: {"p50_ms": v[2 * i], "p99_ms": v[2 * i + 1]} for i, k in enumerate(keys)}
+    lat = {k: {q: round(x, 3) for q, x in d.items()} for k, d in lat.items()}
 
     if rank != 0:
         if world > 1:
@@ -151,85 +213,80 @@ def main():
     sys.path.insert(0, str(ROOT / "oracle"))
     from pyoracle import Oracle, frontier
 
-    # ---- oracle over the same filter set: roofline bytes, parity sample, CPU baseline
-    t = time.time()
-    o = Oracle()
-    o.apply(np.ones(len(fs), np.uint8), fs.blob, fs.offs, fs.vals)
-    o.prepare()
-    t_oracle = time.time() - t
-    log(f"oracle built in {t_oracle:.1f}s")
-
-    host_hit = d_hit.cpu().numpy().view(np.uint64)
-    host_out = d_out.cpu().numpy().view(np.uint32)
-    rng = np.random.default_rng(0x454D5158)
+    res_extra = {}
+    mism = None
     ns = min(a.frontier_sample, B)
-    idx = np.sort(rng.choice(B, ns, replace=False))
-    sample_items = [ts.item(int(i)) for i in idx]
-    sblob, soffs = _native.pack_strings(sample_items)
-    levels, states = frontier(o, sblob, soffs, nthreads=a.cpu_threads)
-    # parity on the sample: exact CSR equality with the oracle
-    cnt, _, ohit, ovals = o.match_batch(sblob, soffs, nthreads=a.cpu_threads)
-    mism = 0
-    for j, i in enumerate(idx):
-        g = host_out[int(host_hit[i]):int(host_hit[i + 1])]
-        e = ovals[int(ohit[j]):int(ohit[j + 1])]
-        mism += int(not np.array_equal(g, e))
-    # algorithmic bytes per walk launch (SURVEY.md 8d per topic, minus the 4 H
-    # the emit kernel writes):  8 L + 32 sum|F_l| + 4
-    L_total = int(np.count_nonzero(ts.blob[: int(ts.offs[-1])] == ord("/"))) + B
-    F_total = float(states.sum()) * B / ns
-    walk_bytes = 8 * L_total + 32 * F_total + 4 * B
-    full_bytes = walk_bytes + 4 * total_hits
-    achieved = walk_bytes / (walk_avg_ms * 1e-3) / 1e9
+    achieved = walk_bytes = None
+    cpu = None
+    if not a.no_parity:
+        # ---- oracle over this rank's key set (after the churn, for c5): roofline
+        # bytes, parity sample, CPU baseline
+        t = time.time()
+        o = Oracle()
+        o.apply(np.ones(len(fs), np.uint8), fs.blob, fs.offs, fs.vals)
+        for k in range(dpos[0]):
+            d = dchunks[k]
+            o.apply(d.flags, d.blob, d.offs, d.vals)
+        o.prepare()
+        log(f"oracle built in {time.time() - t:.1f}s")
+        # the last step's output of this rank (its own shard's lists for c4)
+        host_hit = d_hit.cpu().numpy().view(np.uint64)
+        host_out = d_out.cpu().numpy().view(np.uint32)
+        rng = np.random.default_rng(0x454D5158)
+        idx = np.sort(rng.choice(B, ns, replace=False))
+        sblob, soffs = _native.pack_strings([ts.item(int(i)) for i in idx])
+        levels, states = frontier(o, sblob, soffs, nthreads=a.cpu_threads)
+        cnt, _, ohit, ovals = o.match_batch(sblob, soffs, nthreads=a.cpu_threads)
+        mism = 0
+        for j, i in enumerate(idx):
+            g = host_out[int(host_hit[i]):int(host_hit[i + 1])]
+            e = ovals[int(ohit[j]):int(ohit[j + 1])]
+            mism += int(not np.array_equal(g, e))
+        # algorithmic bytes per walk launch (SURVEY.md 8d per topic, minus the
+        # 4 H the emit kernel writes):  8 L + 32 sum|F_l| + 4
+        L_total = int(np.count_nonzero(ts.blob[: int(ts.offs[-1])] == ord("/"))) + B
+        F_total = float(states.sum()) * B / ns
+        walk_bytes = 8 * L_total + 32 * F_total + 4 * B
+        achieved = walk_bytes / (walk_avg_ms * 1e-3) / 1e9
+        res_extra["full_path_GBps"] = round((walk_bytes + 4 * last_hits) / (batch_avg_ms * 1e-3) / 1e9, 1)
+
+        # ---- CPU baseline: the oracle (restated reference walk) on host threads
+        if not a.no_cpu and world == 1 and a.config in ("c1", "c2", "c2nm", "c3"):
+            n1 = min(20_000, B)
+            probe = ts.slice(0, n1)
+            t1 = time.perf_counter()
+            o.match_batch(probe.blob, probe.offs, nthreads=a.cpu_threads, with_values=False)
+            r1 = n1 / (time.perf_counter() - t1)
+            # a bounded sample of about cpu_seconds of CPU work: whole passes over
+            # the batch when it is shorter than that, else its first n2 topics
+            want = int(max(n1, r1 * a.cpu_seconds))
+            passes, n2 = (max(1, round(want / B)), B) if want >= B else (1, want)
+            samp = ts.slice(0, n2)
+            t1 = time.perf_counter()
+            for _ in range(passes):
+                o.match_batch(samp.blob, samp.offs, nthreads=a.cpu_threads, with_values=False)
+            el_cpu = time.perf_counter() - t1
+            what = f"{passes} passes over the {B}-topic batch" if passes > 1 else f"first {n2} topics of the batch"
+            cpu = {"value": round(passes * n2 / el_cpu, 1), "unit": "topic matches/s", "cores": a.cpu_threads,
+                   "kind": "port",
+                   "sample": f"{what} vs all {len(fs)} keys; oracle/tm_oracle.c seek walker (emqx_trie_search "
+                             f"restated) over a sorted key array, {a.cpu_threads} pthreads, {el_cpu:.1f}s"}
 
     traffic = None
     pmc = ROOT / "profiles" / f"pmc_{a.config}.json"
     if pmc.exists():
         try:
             pj = json.loads(pmc.read_text())
-            if pj.get("filters") == nf and pj.get("batch") == B:
+            if pj.get("filters") == len(fs) and pj.get("batch") == B:
                 traffic = pj.get("walk_hbm_bytes_per_launch")
         except Exception:
             traffic = None
 
-    # ---- p50/p99 batch latency: host topics in, hit lists back in host memory
-    lat = {}
-    for lb in sorted({min(4096, B), min(65536, B)}):
-        sub = ts.slice(0, lb)
-        xs = []
-        for k in range(a.latency_batches + 2):
-            t1 = time.perf_counter()
-            ix.match_batch(sub.blob, sub.offs)
-            xs.append((time.perf_counter() - t1) * 1e3)
-        xs = np.array(xs[2:])
-        lat[str(lb)] = {"p50_ms": round(float(np.percentile(xs, 50)), 3),
-                        "p99_ms": round(float(np.percentile(xs, 99)), 3)}
-
-    # ---- CPU baseline: the oracle (restated reference walk) on host threads
-    cpu = None
-    if not a.no_cpu and world == 1:
-        n1 = min(20_000, B)
-        probe = ts.slice(0, n1)
-        t1 = time.perf_counter()
-        o.match_batch(probe.blob, probe.offs, nthreads=a.cpu_threads, with_values=False)
-        r1 = n1 / (time.perf_counter() - t1)
-        # a bounded sample of about cpu_seconds of CPU work: whole passes over
-        # the batch when it is shorter than that, else its first n2 topics
-        want = int(max(n1, r1 * a.cpu_seconds))
-        passes, n2 = (max(1, round(want / B)), B) if want >= B else (1, want)
-        samp = ts.slice(0, n2)
-        t1 = time.perf_counter()
-        for _ in range(passes):
-            o.match_batch(samp.blob, samp.offs, nthreads=a.cpu_threads, with_values=False)
-        el_cpu = time.perf_counter() - t1
-        what = f"{passes} passes over the {B}-topic batch" if passes > 1 else f"first {n2} topics of the batch"
-        cpu = {"value": round(passes * n2 / el_cpu, 1), "unit": "topic matches/s", "cores": a.cpu_threads,
-               "kind": "port",
-               "sample": f"{what} vs all {len(fs)} keys; oracle/tm_oracle.c seek walker (emqx_trie_search "
-                         f"restated) over a sorted key array, {a.cpu_threads} pthreads, {el_cpu:.1f}s"}
-
+    metric = {"c3": "topic matches/sec at 10M filters"}.get(a.config, f"topic matches/sec ({a.config})")
+    par = (f"filter-sharded x{world} (RCCL allgatherv of hit lists)" if filter_sharded
+           else f"topic-sharded x{world} (trie replicated)")
     res = {
-        "metric": "topic matches/sec at 10M filters" if a.config == "c3" else f"topic matches/sec ({a.config})",
+        "metric": metric,
         "value": round(value, 1),
         "unit": "topic matches/s",
         "n_gpus": world,
@@ -237,27 +294,34 @@ def main():
         "warmup": a.warmup,
         "ms_per_step": round(ms_per_step, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if filter_sharded else "weak",
         "vs_baseline": None,
         "dtype": "u8/u32",
         "data": "synthetic (emqx_amd/csrc/workload.cpp, seed 0x454D5158+cfg)",
-        "config": {"workload": f"{a.config}: {desc}", "filters": len(fs), "topics_per_gpu_step": B,
-                   "global_batch": B * world, "parallelism": f"topic-sharded x{world} (trie replicated)"},
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+        "config": {"workload": f"{a.config}: {desc}", "filters": nf if filter_sharded else len(fs),
+                   "topics_per_gpu_step": B, "global_batch": topics_per_step, "parallelism": par},
+        "roofline": {"bound": "hbm", "achieved": None if achieved is None else round(achieved, 1),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": None if achieved is None else round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "kernel": "k_walk_fast", "kernel_avg_ms": round(walk_avg_ms, 4),
-                     "algorithmic_bytes_per_launch": int(walk_bytes)},
+                     "algorithmic_bytes_per_launch": None if walk_bytes is None else int(walk_bytes)},
         "cpu_baseline": cpu,
-        "matched_ids_per_s": round(total_hits * world * a.steps / el_max, 1),
-        "hits_per_topic": round(total_hits / B, 3),
+        "matched_ids_per_s": round(last_hits * (1 if filter_sharded else world) * a.steps / el_max, 1),
+        "hits_per_topic": round((merged_total if merged_total is not None else last_hits) / B, 3),
         "batch_device_ms": round(batch_avg_ms, 4),
         "batch_latency_host_ms": lat,
-        "parity_sample": {"topics": ns, "mismatches": mism},
+        "parity_sample": None if mism is None else {"topics": ns, "mismatches": mism,
+                                                    "against": "oracle over this rank's keys"},
         "build": {"generate_s": round(t_gen, 1), "compile_s": round(t_compile, 1), "upload_s": round(t_upload, 2),
                   "device_MiB": round(st["device_bytes"] / 2**20, 1), "nodes": st["n_nodes"],
-                  "edges": st["n_edges"], "words": st["n_words"]},
-        "full_path_GBps": round(full_bytes / (batch_avg_ms * 1e-3) / 1e9, 1),
+                  "edges": st["n_edges"], "words": st["n_words"], "keys_this_rank": st["n_keys"]},
     }
+    res.update(res_extra)
+    if dchunks:
+        res["deltas_per_step"] = a.deltas
+        res["deltas_per_s"] = round(a.deltas * a.steps / el_max, 1)
+    if filter_sharded:
+        res["merged_hits_per_step"] = merged_total
     if cpu:
         res["speedup_vs_cpu"] = round(value / cpu["value"], 1)
     print(json.dumps(res), flush=True)

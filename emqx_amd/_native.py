@@ -21,7 +21,7 @@ TM_KEY_BINARY, TM_KEY_WORDS, TM_KEY_EMPTY_LIST = 0, 1, 2
 # every symbol include/tmatch.h declares (tests check the export table)
 EXPORTS = ("tm_create", "tm_destroy", "tm_apply_deltas", "tm_sync", "tm_match_batch",
            "tm_match_batch_dev", "tm_first_batch", "tm_stats", "tm_profile_enable", "tm_profile_read",
-           "tm_last_error", "tm_abi_version")
+           "tm_last_error", "tm_abi_version", "tm_merge_shards")
 
 
 class NativeUnavailable(RuntimeError):
@@ -70,6 +70,7 @@ def load_library(path: Path | None = None):
         "tm_profile_read": (i32, [vp, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(u64), i32]),
         "tm_last_error": (C.c_char_p, [vp]),
         "tm_abi_version": (u32, []),
+        "tm_merge_shards": (i32, [u32, u64, vp, vp, u64, vp, vp, u64, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -89,6 +90,17 @@ def _gpu_present() -> bool:
         return torch.cuda.is_available()
     except Exception:  # pragma: no cover
         return False
+
+
+def merge_shards(world: int, n: int, d_shard_hit: int, d_shard_vals: int, stride: int, d_out_hit: int,
+                 d_out_vals: int, cap: int, stream: int | None = None):
+    """tm_merge_shards on device pointers (filter-sharded mode)."""
+    if not _gpu_present():
+        raise NativeUnavailable("no HIP device visible: the shard merge runs on the GPU only")
+    lib = load_library()
+    rc = lib.tm_merge_shards(world, n, d_shard_hit, d_shard_vals, stride, d_out_hit, d_out_vals, cap, stream)
+    if rc != TM_OK:
+        raise TmError(rc, lib.tm_last_error(None).decode())
 
 
 def pack_strings(items) -> tuple[np.ndarray, np.ndarray]:

@@ -57,6 +57,9 @@ hipError_t launch_match_phase2(const DevIndex &ix, const Workspace &ws, uint64_t
                                hipStream_t s);
 hipError_t launch_first(const DevIndex &ix, const Workspace &ws, uint64_t n, const uint8_t *bytes,
                         const uint64_t *offs, uint32_t *out_value, uint8_t *out_found, hipStream_t s);
+// filter-sharded merge of allgathered per-shard CSR hit lists (k_merge_shards)
+hipError_t launch_merge_shards(uint32_t world, uint64_t n, const uint64_t *shard_hit, const uint32_t *shard_vals,
+                               uint64_t stride, uint64_t *out_hit, uint32_t *out, uint64_t cap, hipStream_t s);
 // scatter patch: dst[i] (absolute device address of a u32) = val[i]
 hipError_t launch_patch(const uint64_t *d_addr, const uint32_t *d_val, uint64_t n, hipStream_t s);
 

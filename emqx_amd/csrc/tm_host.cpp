@@ -784,7 +784,7 @@ int prof_end(tm_index *ix, tm_index::ProfEv &ev, hipStream_t s) {
 
 extern "C" {
 
-uint32_t tm_abi_version(void) { return (1u << 16) | 0u; }
+uint32_t tm_abi_version(void) { return (1u << 16) | 1u; }
 
 const char *tm_last_error(tm_index *h) { return h ? h->err.c_str() : g_last_error.c_str(); }
 
@@ -988,6 +988,16 @@ int tm_first_batch(tm_index *ix, uint64_t n, const uint8_t *tb, const uint64_t *
         memcpy(out_value, ix->pin_out, n * 4);
         memcpy(out_found, ix->pin_out + n * 4, n);
     }
+    return TM_OK;
+}
+
+int tm_merge_shards(uint32_t world, uint64_t n, const uint64_t *shard_hit, const uint32_t *shard_vals,
+                    uint64_t stride, uint64_t *out_hit, uint32_t *out, uint64_t cap, void *stream) {
+    if (!world || !shard_hit || !out_hit || (cap && !out) || (n && !shard_vals))
+        return fail(nullptr, TM_EINVAL, "tm_merge_shards: bad argument");
+    hipError_t e = launch_merge_shards(world, n, shard_hit, shard_vals, stride, out_hit, out, cap,
+                                       reinterpret_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return fail(nullptr, TM_EDEVICE, std::string("tm_merge_shards: ") + hipGetErrorString(e));
     return TM_OK;
 }
 

@@ -694,6 +694,39 @@ __global__ void k_patch(const uint64_t *addr, const uint32_t *val, uint64_t n) {
     if (i < n) *reinterpret_cast<uint32_t *>(addr[i]) = val[i];
 }
 
+// ------------------------------------------------------ filter-sharded merge
+
+// Filter-sharded mode: `world` shards matched the same n topics
+// against disjoint key sets; their CSR hit lists were allgathered (RCCL) into
+// shard_hit [world][n+1] and shard_vals [world][stride].  Topic t's merged list
+// is shard 0's list, then shard 1's, ... -- the union of disjoint key sets, so
+// the same value set as one index holding every key.  Merged offsets are the
+// sums of the shards' offsets (a sum of exclusive prefix sums is the prefix sum
+// of the summed counts): no scan needed.  One thread per (shard, topic), shard
+// major, so neighbouring lanes read neighbouring source runs.
+__global__ __launch_bounds__(256) void k_merge_shards(uint32_t world, uint64_t n, const uint64_t *shard_hit,
+                                                      const uint32_t *shard_vals, uint64_t stride,
+                                                      uint64_t *out_hit, uint32_t *out, uint64_t cap) {
+    const uint64_t id = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (id >= (uint64_t)world * (n + 1)) return;
+    const uint32_t r = (uint32_t)(id / (n + 1));
+    const uint64_t t = id % (n + 1);
+    uint64_t base = 0, before = 0;
+    for (uint32_t q = 0; q < world; q++) {
+        const uint64_t o = shard_hit[(uint64_t)q * (n + 1) + t];
+        base += o;
+        if (q < r && t < n) before += shard_hit[(uint64_t)q * (n + 1) + t + 1] - o;
+    }
+    if (r == 0) out_hit[t] = base;
+    if (t == n) return;
+    const uint64_t *h = shard_hit + (uint64_t)r * (n + 1);
+    const uint64_t s0 = h[t], s1 = h[t + 1];
+    const uint32_t *src = shard_vals + (uint64_t)r * stride;
+    uint64_t d = base + before;
+    for (uint64_t i = s0; i < s1; i++, d++)
+        if (d < cap) out[d] = src[i];
+}
+
 // ------------------------------------------------------------ launchers
 
 static inline uint32_t blocks_for(uint64_t n, uint32_t per) { return (uint32_t)((n + per - 1) / per); }
@@ -730,6 +763,14 @@ hipError_t launch_first(const DevIndex &ix, const Workspace &ws, uint64_t n, con
     hipLaunchKernelGGL(k_walk_fast<MODE_FIRST>, dim3(blocks_for(n, WALK_BLOCK)), dim3(WALK_BLOCK), 0, s,
                        ix, ws, n, bytes, offs, o);
     hipLaunchKernelGGL(k_walk_tail<MODE_FIRST>, dim3(TAIL_GRID), dim3(MID_BLOCK), 0, s, ix, ws, n, bytes, offs, o);
+    return hipGetLastError();
+}
+
+hipError_t launch_merge_shards(uint32_t world, uint64_t n, const uint64_t *shard_hit, const uint32_t *shard_vals,
+                               uint64_t stride, uint64_t *out_hit, uint32_t *out, uint64_t cap, hipStream_t s) {
+    const uint64_t threads = (uint64_t)world * (n + 1);
+    hipLaunchKernelGGL(k_merge_shards, dim3(blocks_for(threads, 256)), dim3(256), 0, s, world, n, shard_hit,
+                       shard_vals, stride, out_hit, out, cap);
     return hipGetLastError();
 }
 

@@ -22,6 +22,12 @@
  *       (first key in traversal order; emqx_trie_search.erl:171-178,350-356)
  *   tm_stats
  *       emqx_router:stats/1 n_routes part    apps/emqx/src/emqx_router.erl:632-635
+ *   tm_merge_shards
+ *       no reference counterpart: the reference holds every route on every
+ *       node (mria-replicated emqx_route_filters, emqx_router.erl:105-108);
+ *       filter sets beyond one GPU are split into shards and the
+ *       shards' hit lists, allgathered over RCCL, are merged by this call so
+ *       the result equals emqx_topic_index:matches/3 over the whole set
  *
  * Keys.  An index entry is the pair (filter, value).  `value` is a caller-chosen
  * u32 (the NIF interns the Erlang {ID} term, or the whole key, to a u32).
@@ -115,6 +121,17 @@ int tm_first_batch(tm_index *h, uint64_t n, const uint8_t *topic_bytes, const ui
                    uint32_t *out_value, uint8_t *out_found);
 
 int tm_stats(tm_index *h, tm_stats_t *out);
+
+/* Filter-sharded merge (device buffers, asynchronous on `stream`; runs on the
+ * current HIP device).  `world` shards matched the same n topics;
+ * d_shard_hit_offsets is [world][n+1] (each shard's CSR offsets, starting at
+ * 0), d_shard_values is [world][stride] (shard r's values at r*stride).  Writes
+ * the merged CSR: d_out_hit_offsets[n+1] and, up to `cap`, d_out_values --
+ * topic t's values of shard 0, then shard 1, ..., each in that shard's
+ * traversal order (the same value set as one index holding all the keys). */
+int tm_merge_shards(uint32_t world, uint64_t n, const uint64_t *d_shard_hit_offsets, const uint32_t *d_shard_values,
+                    uint64_t stride, uint64_t *d_out_hit_offsets, uint32_t *d_out_values, uint64_t cap,
+                    void *stream);
 
 /* Diagnostics.  While enabled, every match batch records HIP events on its
  * stream around the main walk kernel (k_walk_fast) and around the whole batch;

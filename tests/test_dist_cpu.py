@@ -1,9 +1,12 @@
 """world_size-2 gloo tests of the multi-GPU modes on CPU.
 
-The filter-sharded exchange (allgather of counts + allgatherv of values +
-merge) runs exactly as on GPUs, only over gloo; the per-shard hit lists come
-from the CPU oracle here (the test's stand-in for each rank's GPU shard), and
-the merged result must equal the oracle over the unsharded filter set.
+The filter-sharded exchange (allgather of the CSR offsets + allgatherv of the
+values, emqx_amd.shard.exchange) runs exactly as on GPUs, only over gloo; the
+per-shard hit lists come from the CPU oracle here (the test's stand-in for each
+rank's GPU shard) and the device merge (tm_merge_shards) is restated in numpy
+(`_merge_ref`, the kernel's contract; the kernel itself is checked against it in
+tests/test_gpu_parity.py).  The merged result must equal the oracle over the
+unsharded filter set, as per-topic value sets.
 """
 import os
 import socket
@@ -40,6 +43,18 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
+def _merge_ref(all_offs, all_vals):
+    """numpy restatement of tm_merge_shards: per topic, shard 0's values, then shard 1's, ..."""
+    world, n1 = all_offs.shape
+    n = n1 - 1
+    out_hit = all_offs.sum(axis=0)
+    out = []
+    for t in range(n):
+        for r in range(world):
+            out.append(all_vals[r, all_offs[r, t]:all_offs[r, t + 1]])
+    return out_hit, (np.concatenate(out) if out else np.zeros(0, np.int32))
+
+
 def _body(rank, world, q):
     from emqx_amd import shard, workload as wl
     from pyoracle import Oracle
@@ -49,8 +64,10 @@ def _body(rank, world, q):
     o = Oracle()
     o.apply(np.ones(len(fs), np.uint8), fs.blob, fs.offs, fs.vals)
     cnt, _, hit, vals = o.match_batch(ts.blob, ts.offs)
-    m_offs, m_vals = shard.allgatherv_hits(torch.from_numpy(hit.astype(np.int64)),
-                                           torch.from_numpy(vals.view(np.int32)))
+    all_offs, all_vals, stride = shard.exchange(torch.from_numpy(hit.astype(np.int64)),
+                                                torch.from_numpy(vals.view(np.int32)))
+    assert all_vals.shape == (world, stride)
+    m_offs, m_vals = _merge_ref(all_offs.numpy(), all_vals.numpy())
     # topic-sharded slices partition the stream
     first, n = shard.topic_slice(rank, world, 1000)
     t = torch.tensor([first, n], dtype=torch.int64)
@@ -59,7 +76,7 @@ def _body(rank, world, q):
     # max-over-ranks timing reduction used by bench.py
     el = torch.tensor([0.5 + rank], dtype=torch.float64)
     dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    q.put((rank, m_offs.numpy(), m_vals.numpy(), [x.tolist() for x in g], float(el)))
+    q.put((rank, m_offs, m_vals, [x.tolist() for x in g], float(el)))
 
 
 @pytest.mark.timeout(300)
@@ -95,6 +112,6 @@ def test_filter_sharded_exchange_gloo():
     m_offs, m_vals = res[0][1], res[0][2].view(np.uint32)
     assert np.array_equal(m_offs, hit.astype(np.int64))
     for i in range(len(ts)):
-        assert np.array_equal(np.sort(vals[hit[i]:hit[i + 1]]), m_vals[m_offs[i]:m_offs[i + 1]])
+        assert np.array_equal(np.sort(vals[hit[i]:hit[i + 1]]), np.sort(m_vals[m_offs[i]:m_offs[i + 1]]))
     assert res[0][3] == [[0, 1000], [1000, 1000]]
     assert res[0][4] == 1.5

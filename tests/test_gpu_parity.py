@@ -364,3 +364,46 @@ def test_child_table_grow_and_shrink(torch_dev):
         o.apply(np.zeros(len(d), np.uint8), d.blob, d.offs, d.vals)
         assert_same(ix, o, topics)
     assert ix.stats()["n_nodes"] == 1
+
+
+# ------------------------------------------------------------- filter-sharded
+
+def _merge_ref(all_offs, all_vals):
+    """numpy restatement of tm_merge_shards (the kernel's contract)."""
+    world, n1 = all_offs.shape
+    out = [all_vals[r, all_offs[r, t]:all_offs[r, t + 1]] for t in range(n1 - 1) for r in range(world)]
+    return all_offs.sum(axis=0), (np.concatenate(out) if out else np.zeros(0, np.int32))
+
+
+@pytest.mark.parametrize("world", [1, 3])
+def test_filter_sharded_merge_vs_oracle(torch_dev, world):
+    """C4 in one process: `world` shard indexes on one GPU, the same topic batch
+    on each, the gathered CSR lists merged by tm_merge_shards == the unsharded
+    oracle (per-topic value sets) and == the kernel contract (exact order)."""
+    import torch
+    from emqx_amd import shard
+    nf = 60_000
+    ts = wl.topics(3, nf, 20_000)
+    dev = torch.device("cuda:0")
+    offs, vals = [], []
+    for r in range(world):
+        part = wl.filters(3, nf, shard=r, nshards=world)
+        hit, v, err = gpu_index(part).match_batch(ts.blob, ts.offs)
+        offs.append(hit.astype(np.int64))
+        vals.append(v.view(np.int32))
+    stride = max(max(len(v) for v in vals), 1)
+    all_offs = np.stack(offs)
+    all_vals = np.zeros((world, stride), np.int32)
+    for r, v in enumerate(vals):
+        all_vals[r, :len(v)] = v
+    m_hit, m_vals = shard.merge(torch.from_numpy(all_offs).to(dev), torch.from_numpy(all_vals).to(dev), stride)
+    torch.cuda.synchronize()
+    m_hit, m_vals = m_hit.cpu().numpy(), m_vals.cpu().numpy()
+    r_hit, r_vals = _merge_ref(all_offs, all_vals)
+    assert np.array_equal(m_hit, r_hit) and np.array_equal(m_vals, r_vals)
+    fs = wl.filters(3, nf)
+    cnt, _, ohit, ovals = oracle_of(fs).match_batch(ts.blob, ts.offs)
+    assert np.array_equal(m_hit.astype(np.uint64), ohit.astype(np.uint64))
+    mv = m_vals.view(np.uint32)
+    for i in range(len(ts)):
+        assert np.array_equal(np.sort(mv[m_hit[i]:m_hit[i + 1]]), np.sort(ovals[ohit[i]:ohit[i + 1]])), i
