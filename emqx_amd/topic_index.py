@@ -158,10 +158,10 @@ def matches_batch(topics, tab: Tab, opts=()):
 def _finish(keys, opts):
     if "unique" in opts:
         by_id = {}
-        for k in sorted(keys, key=key_order):      # traversal order; later keys win
+        for k in keys:                             # traversal order (device); later keys win
             by_id[get_id(k)] = k
         return [by_id[i] for i in sorted(by_id, key=term_key)]
-    return sorted(keys, key=key_order, reverse=True)
+    return keys[::-1]          # the device emits traversal order; matches/3 is its reverse
 
 
 def matches(topic, tab: Tab, opts=()):

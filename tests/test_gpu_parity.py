@@ -407,3 +407,88 @@ def test_filter_sharded_merge_vs_oracle(torch_dev, world):
     mv = m_vals.view(np.uint32)
     for i in range(len(ts)):
         assert np.array_equal(np.sort(mv[m_hit[i]:m_hit[i + 1]]), np.sort(ovals[ohit[i]:ohit[i + 1]])), i
+
+
+# ------------------------------------------------- router / syncer / broker
+
+def test_router_exact_bag_on_device(torch_dev):
+    """Exact routes live in the device index's exact table; match_routes puts
+    them first, in bag insertion order, then the filter matches in matches/3
+    order (emqx_router.erl:511-516)."""
+    r = rt.Router(node="n1")
+    for topic, dest in [(b"a/b", "n2"), (b"a/+", "n1"), (b"a/b", "n1"), (b"#", "n3"), (b"a/b", (b"g", "n4"))]:
+        r.add_route(topic, dest)
+    r.delete_route(b"a/b", "n2")
+    r.add_route(b"a/b", "n2")                      # re-added: goes to the end of the bag
+    exp = [(b"a/b", "n1"), (b"a/b", (b"g", "n4")), (b"a/b", "n2"), (b"a/+", "n1"), (b"#", "n3")]
+    assert [tuple(x) for x in r.match_routes(b"a/b")] == exp
+    assert r.lookup_routes(b"a/b") == [rt.Route(b"a/b", d) for d in ("n1", (b"g", "n4"), "n2")]
+    assert r.has_route(b"a/+", "n1") and not r.has_route(b"a/+", "n2") and r.has_route(b"a/b", "n2")
+    assert r.stats_n_routes() == 5
+    assert [tuple(x) for x in r.match_routes(b"a/c")] == [(b"a/+", "n1"), (b"#", "n3")]
+    assert [tuple(x) for x in r.match_routes(b"$SYS/x")] == []
+
+
+def test_router_cleanup_and_replicated_events(torch_dev):
+    rnd = random.Random(7)
+    ops = []
+    for i in range(400):
+        t = b"/".join(rnd.choice([b"a", b"b", b"c", b"+"]) for _ in range(rnd.randint(1, 3)))
+        if rnd.random() < 0.1:
+            t += b"/#"
+        d = rnd.choice(["n1", "n2", "n3", (b"g", "n2"), (b"h", "n3")])
+        ops.append(("add" if rnd.random() < 0.75 else "delete", t, d))
+    a, b = rt.Router(node="n1"), rt.Router(node="n1")
+    for op, t, d in ops:
+        (a.add_route if op == "add" else a.delete_route)(t, d)
+        # the same writes as mria would replicate them into another node's tables
+        from emqx_amd.trie_search import filter as tfilter
+        rec = rt.RouteIdx(ti.make_key(t, d)) if tfilter(t) is not False else rt.Route(t, d)
+        b.on_table_event(("write" if op == "add" else "delete", rec))
+    topics = [b"/".join(rnd.choice([b"a", b"b", b"c", b"d"]) for _ in range(rnd.randint(1, 4))) for _ in range(300)]
+    assert a.match_routes_batch(topics) == b.match_routes_batch(topics)
+    a.cleanup_routes("n2")
+    left = [x for rs in a.match_routes_batch(topics) for x in rs]
+    assert left and all(rt.get_dest_node(x.dest) != "n2" for x in left)
+    full = [x for rs in b.match_routes_batch(topics) for x in rs]
+    assert sorted((x for x in full if rt.get_dest_node(x.dest) != "n2"), key=rt.route_order) == \
+        sorted(left, key=rt.route_order)
+
+
+def test_syncer_batches_reach_the_device(torch_dev):
+    from emqx_amd import syncer as sy
+    direct, synced = rt.Router(node="n1"), rt.Router(node="n1")
+    s = sy.Syncer(synced, max_batch_size=100)
+    refs = []
+    for i in range(600):
+        t = f"dev/{i % 150}/+/x".encode() if i % 3 else f"dev/{i % 150}/y".encode()
+        op = "delete" if i % 7 == 0 else "add"
+        (direct.add_route if op == "add" else direct.delete_route)(t, "n1")
+        refs.append(s.push(op, t, "n1", {"reply": True}))
+    assert s.run_once() > 0 and s.batches >= 2
+    assert all(x.wait(0) == "ok" for x in refs)
+    topics = [f"dev/{i}/{j}/x".encode() for i in range(150) for j in ("q", "y")] + \
+             [f"dev/{i}/y".encode() for i in range(150)]
+    assert direct.match_routes_batch(topics) == synced.match_routes_batch(topics)
+
+
+def test_broker_micro_batch_equals_per_message_publish(torch_dev):
+    from emqx_amd import broker as bk
+    r = rt.Router(node="n1")
+    fs = wl.filters(1, 2_000)
+    for i in range(len(fs)):
+        r.add_route(fs.item(i), ["n1", "n2", (b"grp", "n3")][i % 3])
+    ts = wl.topics(1, 2_000, 3_000)
+    msgs = [bk.Message(ts.item(i), i) for i in range(len(ts))]
+    b = bk.Broker(r, max_batch=1024, max_wait_ms=50, start=True)
+    try:
+        futs = [b.publish(m) for m in msgs]
+        batched = [f.result(timeout=60) for f in futs]
+    finally:
+        b.close()
+    assert b.batches < len(msgs) / 100       # micro-batched: few device launches
+    single = bk.Broker(r)
+    for m, got in zip(msgs[:300], batched[:300]):
+        routes = bk.aggre(r.match_routes(m.topic))
+        assert got[0] == routes
+        assert got == single.publish_batch([m])[0]
