@@ -52,7 +52,9 @@ def load_library(path: Path | None = None):
     global _lib
     if _lib is not None and path is None:
         return _lib
-    p = Path(path) if path else LIB_TMATCH
+    import os
+    # TM_LIB: an experimental build of the same library (emqx_amd.build.build_variant)
+    p = Path(path) if path else Path(os.environ.get("TM_LIB", LIB_TMATCH))
     if not p.exists():
         raise NativeUnavailable(f"{p} is not built (run emqx_amd.build.build_all())")
     lib = C.CDLL(str(p))

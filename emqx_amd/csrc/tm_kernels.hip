@@ -101,6 +101,9 @@ struct LdsStore {
     uint8_t *len8;                           // [level][thread] word lengths (deferred probes)
     uint32_t stride;
     uint64_t mask;
+#ifdef TM_STUDY
+    uint32_t n_steps = 0, n_probe = 0;   // study build: node visits, child-table probes
+#endif
     __device__ __forceinline__ uint32_t get_wid(uint32_t l) const { return wid[l * stride]; }
     __device__ __forceinline__ void set_wid(uint32_t l, uint32_t w) { wid[l * stride] = w; }
     __device__ __forceinline__ void reset() { mask = 0; }
@@ -302,6 +305,9 @@ template <class S, class EM>
 __device__ bool dfs(const DevIndex &ix, uint32_t L, bool dollar, S &st, EM &em) {
     uint32_t cur = ROOT, l = 0;
     for (;;) {
+#ifdef TM_STUDY
+        if constexpr (S::deferred) st.n_steps++;
+#endif
         // the whole state is one 64-byte line (tm_layout.h Node)
         const uint4 *np = reinterpret_cast<const uint4 *>(ix.nodes + cur);
         const uint4 n0 = np[0];   // plus, hash_off, hash_cnt, exact_off
@@ -321,6 +327,9 @@ __device__ bool dfs(const DevIndex &ix, uint32_t L, bool dollar, S &st, EM &em) 
                 } else {
                     const uint32_t h = child_hash(w), b = child_bit(h);
                     const uint32_t m = b < 32 ? n1.z >> b : n1.w >> (b - 32);
+#ifdef TM_STUDY
+                    if constexpr (S::deferred) st.n_probe += m & 1u;
+#endif
                     if (m & 1u) lit = ctab_find(ix, n2.x, n2.y, w, h);
                 }
             }
@@ -427,7 +436,14 @@ __device__ int run_topic(const DevIndex &ix, const Workspace &ws, uint64_t n, co
         ws.cnt[t] = em.cnt;
         ws.nr[t] = em.nr;
         em.store(ws.rng, n, t);
+#ifdef TM_STUDY   // study build (tools/study_steps.py): visits and probes in the err byte
+        if constexpr (S::maxl == FAST_L)
+            o.err[t] = (uint8_t)((st.n_steps < 31 ? st.n_steps : 31) | ((st.n_probe < 7 ? st.n_probe : 7) << 5));
+        else
+            o.err[t] = rc == RC_BADARG;
+#else
         o.err[t] = rc == RC_BADARG;
+#endif
         if (em.nr > RCAP) list_push(ws, n, S::maxl <= MID_L ? L_OVF_MID : L_OVF_DEEP, (uint32_t)t);
         *hits = em.cnt;
         return rc;

@@ -1,0 +1,32 @@
+#!/usr/bin/env python3
+"""Study build (TM_STUDY): per-topic DFS node visits and child-table probes,
+packed into the err byte by the instrumented k_walk_fast (TM_LIB=...study.so)."""
+import sys
+from pathlib import Path
+import numpy as np
+sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+
+
+def main():
+    import torch
+    from bench import CONFIGS
+    from emqx_amd import _native, workload as wl
+    cfg = sys.argv[1] if len(sys.argv) > 1 else "c3"
+    gen, nf, _ = CONFIGS[cfg]
+    fs = wl.filters(gen, nf)
+    ix = _native.Index(device=0)
+    for lo in range(0, len(fs), 2_000_000):
+        p = fs.slice(lo, min(lo + 2_000_000, len(fs)))
+        ix.apply(np.ones(len(p), np.uint8), p.blob, p.offs, p.vals)
+    ts = wl.topics(gen, nf, 200_000)
+    hit, vals, err = ix.match_batch(ts.blob, ts.offs)
+    steps = (err & 31).astype(np.int64)
+    probes = (err >> 5).astype(np.int64)
+    w = steps.reshape(-1, 64)
+    print(f"{cfg}: steps mean {steps.mean():.2f} p50 {np.median(steps)} p99 {np.percentile(steps, 99)} "
+          f"wave-max mean {w.max(1).mean():.2f}; ctab probes mean {probes.mean():.2f} "
+          f"wave-max mean {probes.reshape(-1, 64).max(1).mean():.2f}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
