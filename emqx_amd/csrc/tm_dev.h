@@ -15,6 +15,7 @@ struct DevIndex {
     const CSlot *ctab;
     const uint32_t *vals;
     const ExactEntry *exact; uint32_t xmask;
+    const uint16_t *xfp;
     const uint32_t *wseq;
 };
 
@@ -43,6 +44,7 @@ struct Workspace {
 };
 
 constexpr int TILE = 256;    // topics per walk block = per scan tile = per emit block
+
 
 // Pipeline entry points (tm_kernels.hip).  All asynchronous on `s`.
 // phase 1: tokenise + walk + tile totals (hit_offs[n] = total becomes valid)

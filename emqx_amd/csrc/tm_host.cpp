@@ -81,6 +81,7 @@ struct tm_index {
     Mirror<CSlot> ctab; std::vector<uint32_t> free_ctab[33]; uint64_t nlinks = 0, ntables = 0;
     Mirror<uint32_t> vals; std::vector<uint32_t> free_blocks[33];
     Mirror<ExactEntry> exact; std::vector<uint32_t> xcap; uint64_t xcount = 0;
+    Mirror<uint16_t> xfp;   // exact-table fingerprints, slot for slot (0 = empty)
     Mirror<uint32_t> wseq;
 
     std::unordered_set<std::string> dead;
@@ -462,16 +463,19 @@ void exact_grow(tm_index *ix, uint64_t need) {
     const uint32_t ncap = pow2_at_least(need * 2);
     std::vector<ExactEntry> nt(ncap, empty_exact());
     std::vector<uint32_t> nc(ncap, 0);
+    std::vector<uint16_t> nf(ncap, 0);
     const uint32_t mask = ncap - 1;
     for (size_t i = 0; i < ix->exact.h.size(); i++) {
         const ExactEntry &e = ix->exact.h[i];
         if (e.nlev == NONE) continue;
         for (uint32_t s = e.h_lo & mask;; s = (s + 1) & mask)
-            if (nt[s].nlev == NONE) { nt[s] = e; nc[s] = ix->xcap[i]; break; }
+            if (nt[s].nlev == NONE) { nt[s] = e; nc[s] = ix->xcap[i]; nf[s] = ix->xfp.h[i]; break; }
     }
     ix->exact.h.swap(nt);
     ix->xcap.swap(nc);
+    ix->xfp.h.swap(nf);
     ix->exact.dirty.set_all();
+    ix->xfp.dirty.set_all();
 }
 
 void exact_erase_slot(tm_index *ix, uint32_t i) {
@@ -480,11 +484,17 @@ void exact_erase_slot(tm_index *ix, uint32_t i) {
     for (uint32_t j = (i + 1) & mask; t[j].nlev != NONE; j = (j + 1) & mask) {
         uint32_t k = t[j].h_lo & mask;
         bool stays = (i <= j) ? (i < k && k <= j) : (i < k || k <= j);
-        if (!stays) { t[i] = t[j]; ix->xcap[i] = ix->xcap[j]; ix->exact.touch(i); i = j; }
+        if (!stays) {
+            t[i] = t[j]; ix->xcap[i] = ix->xcap[j]; ix->xfp.h[i] = ix->xfp.h[j];
+            ix->exact.touch(i); ix->xfp.touch(i);
+            i = j;
+        }
     }
     t[i] = empty_exact();
     ix->xcap[i] = 0;
+    ix->xfp.h[i] = 0;
     ix->exact.touch(i);
+    ix->xfp.touch(i);
     ix->xcount--;
 }
 
@@ -553,6 +563,8 @@ void key_op(tm_index *ix, bool ins, const uint8_t *f, uint32_t len, uint32_t v, 
             for (s = (uint32_t)h & mask; ix->exact.h[s].nlev != NONE; s = (s + 1) & mask) {}
             ix->exact.h[s] = e;
             ix->xcap[s] = 0;
+            ix->xfp.h[s] = exact_fp(h);
+            ix->xfp.touch(s);
             ix->xcount++;
         }
         ExactEntry &e = ix->exact.h[s];
@@ -668,6 +680,7 @@ int sync_locked(tm_index *ix, hipStream_t s) {
     if ((rc = collect(ix, ix->ctab, addr, val))) return rc;
     if ((rc = collect(ix, ix->vals, addr, val))) return rc;
     if ((rc = collect(ix, ix->exact, addr, val))) return rc;
+    if ((rc = collect(ix, ix->xfp, addr, val))) return rc;
     if ((rc = collect(ix, ix->wseq, addr, val))) return rc;
     const uint64_t n = addr.size();
     if (!n) return TM_OK;
@@ -706,6 +719,7 @@ DevIndex dev_view(tm_index *ix) {
     d.ctab = ix->ctab.d;
     d.vals = ix->vals.d;
     d.exact = ix->exact.d; d.xmask = (uint32_t)ix->exact.h.size() - 1;
+    d.xfp = ix->xfp.d;
     d.wseq = ix->wseq.d;
     return d;
 }
@@ -749,6 +763,7 @@ void init_tables(tm_index *ix, uint64_t hint) {
     // key set, so hot entries stay dense (vocab / top trie levels in L2)
     ix->vocab.h.assign(1024, empty_vocab());
     ix->exact.h.assign(1024, empty_exact());
+    ix->xfp.h.assign(1024, 0);
     ix->xcap.assign(ix->exact.h.size(), 0);
     ix->nodes.h.reserve(hint / 2 + 1);
     ix->aux.reserve(hint / 2 + 1);
@@ -815,9 +830,10 @@ int tm_destroy(tm_index *ix) {
     if (!ix) return TM_EINVAL;
     (void)hipSetDevice(ix->device);
     (void)hipStreamSynchronize(ix->stream);
-    void *bufs[] = {ix->vocab.d, ix->wpool.d, ix->nodes.d, ix->ctab.d, ix->vals.d, ix->exact.d, ix->wseq.d,
+    void *bufs[] = {ix->vocab.d, ix->wpool.d, ix->nodes.d, ix->ctab.d, ix->vals.d, ix->exact.d, ix->xfp.d, ix->wseq.d,
                     ix->dev_addr, ix->dev_val, ix->ws.cnt, ix->ws.nr, ix->ws.rng, ix->ws.lists, ix->ws.list_n,
-                    ix->ws.blk, ix->ws.deep_wid, ix->ws.deep_stk, ix->d_topics, ix->d_offs, ix->d_hit,
+                    ix->ws.blk, ix->ws.deep_wid, ix->ws.deep_stk,
+                    ix->d_topics, ix->d_offs, ix->d_hit,
                     ix->d_err, ix->d_out};
     for (void *p : bufs) if (p) (void)hipFree(p);
     void *pins[] = {ix->pin_addr, ix->pin_val, ix->pin_in, ix->pin_out, ix->pin_vals};
@@ -1039,7 +1055,7 @@ int tm_stats(tm_index *ix, tm_stats_t *o) {
     o->n_edges = ix->nlinks;
     o->n_words = ix->vcount;
     o->device_bytes = ix->vocab.dcap * sizeof(VocabEntry) + ix->wpool.dcap + ix->nodes.dcap * sizeof(Node) +
-                      ix->ctab.dcap * sizeof(CSlot) + ix->vals.dcap * 4 + ix->exact.dcap * sizeof(ExactEntry) +
+                      ix->ctab.dcap * sizeof(CSlot) + ix->vals.dcap * 4 + ix->exact.dcap * sizeof(ExactEntry) + ix->xfp.dcap * 2 +
                       ix->wseq.dcap * 4;
     o->uploads = ix->uploads;
     o->patch_bytes = ix->patch_bytes;

@@ -265,30 +265,35 @@ __device__ uint32_t count_levels(const uint8_t *blob, uint64_t beg, uint64_t end
 }
 
 // match_topics/4 (emqx_trie_search.erl:381-389): binary keys equal to the topic.
-// The first 16 bytes of the home slot (`a`) are loaded before the trie walk so
-// their latency hides behind it; later probes are rare.
+// The probe walks the 2-byte fingerprint array (`f` = the home slot's, loaded
+// before the trie walk so its latency hides behind it) and reads a 64-byte
+// entry only where the fingerprint matches; the entry is then verified
+// exactly (hash, level count, every wid).
 template <class S>
-__device__ void exact_find(const DevIndex &ix, uint64_t xh, uint32_t L, const S &st, uint32_t slot, uint4 a,
+__device__ void exact_find(const DevIndex &ix, uint64_t xh, uint32_t L, const S &st, uint32_t slot, uint32_t f,
                            uint32_t &off, uint32_t &cnt) {
     cnt = 0; off = 0;
+    const uint32_t fp = exact_fp(xh);
     for (;;) {
-        const uint4 *e = reinterpret_cast<const uint4 *>(ix.exact + slot);
-        if (a.z == NONE) return;
-        if (a.x == (uint32_t)xh && a.y == (uint32_t)(xh >> 32) && a.z == L) {
-            uint4 b = e[1], c = e[2], d = e[3];
-            bool eq = true;
-            if (L <= XINL) {
-                const uint32_t iw[XINL] = {b.z, b.w, c.x, c.y, c.z, c.w, d.x, d.y, d.z, d.w};
+        if (f == 0) return;
+        if (f == fp) {
+            const uint4 *e = reinterpret_cast<const uint4 *>(ix.exact + slot);
+            const uint4 a = e[0], b = e[1], c = e[2], d = e[3];
+            if (a.x == (uint32_t)xh && a.y == (uint32_t)(xh >> 32) && a.z == L) {
+                bool eq = true;
+                if (L <= XINL) {
+                    const uint32_t iw[XINL] = {b.z, b.w, c.x, c.y, c.z, c.w, d.x, d.y, d.z, d.w};
 #pragma unroll
-                for (uint32_t l = 0; l < XINL; l++)
-                    if (l < L) eq &= iw[l] == st.get_wid(l);
-            } else {
-                for (uint32_t l = 0; l < L && eq; l++) eq = ix.wseq[b.y + l] == st.get_wid(l);
+                    for (uint32_t l = 0; l < XINL; l++)
+                        if (l < L) eq &= iw[l] == st.get_wid(l);
+                } else {
+                    for (uint32_t l = 0; l < L && eq; l++) eq = ix.wseq[b.y + l] == st.get_wid(l);
+                }
+                if (eq) { off = a.w; cnt = b.x; return; }
             }
-            if (eq) { off = a.w; cnt = b.x; return; }
         }
         slot = (slot + 1) & ix.xmask;
-        a = ld4(ix.exact + slot);
+        f = ix.xfp[slot];
     }
 }
 
@@ -397,11 +402,14 @@ __device__ int match_topic(const DevIndex &ix, const uint8_t *blob, uint64_t beg
     if (rc) return rc;
     st.reset();
     const uint32_t xslot = (uint32_t)xh & ix.xmask;
-    const uint4 xa = allf ? ld4(ix.exact + xslot) : make_uint4(0, 0, NONE, 0);
+#ifdef TM_STUDY_NOEXACT
+    allf = false;   // timing study only: the exact-table probe skipped (wrong results)
+#endif
+    const uint32_t xf = allf ? ix.xfp[xslot] : 0;
     if (!dfs(ix, L, dollar, st, em)) return RC_OK;
     if (allf) {
         uint32_t xoff, xcnt;
-        exact_find(ix, xh, L, st, xslot, xa, xoff, xcnt);
+        exact_find(ix, xh, L, st, xslot, xf, xoff, xcnt);
         em(xoff, xcnt);
     }
     return RC_OK;

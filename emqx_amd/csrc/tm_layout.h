@@ -13,6 +13,9 @@
 //   nodes  : per trie node: '+' child, '#'-terminal and exact-terminal value
 //            ranges, up to 4 inline literal children  64 B/node (one line)
 //   exact  : wid sequence -> value range         64 B/entry   (binary keys)
+//   xfp    : 16-bit fingerprint per exact slot   2 B/slot: the walk probes
+//            this compact array first and reads a 64-byte entry only on a
+//            fingerprint match (most topics have no binary key)
 //   vals   : u32 values (caller IDs), one sorted run per terminal
 //   wpool  : bytes of words longer than 8 B; wseq: wid runs of exact keys
 //            longer than XINL levels
@@ -109,6 +112,9 @@ TM_HD uint32_t vocab_tag(uint64_t h, uint32_t len) {
 // child table hash: low bits pick the slot, the top 6 bits the Bloom bit
 TM_HD uint32_t child_hash(uint32_t wid) { return (uint32_t)mix64((uint64_t)wid * 0x9e3779b97f4a7c15ull + 1); }
 TM_HD uint32_t child_bit(uint32_t h) { return h >> 26; }
+
+// exact-table fingerprint of a wid-sequence hash (never 0: 0 marks an empty slot)
+TM_HD uint16_t exact_fp(uint64_t h) { return (uint16_t)((h >> 48) | 1u); }
 
 TM_HD uint64_t seq_hash_step(uint64_t h, uint32_t wid) { return (h ^ wid) * FNV_PRIME; }
 TM_HD uint64_t seq_hash_finish(uint64_t h, uint32_t nlev) { return mix64(h + 0x9e3779b97f4a7c15ull * (nlev + 1)); }

@@ -18,6 +18,9 @@ def main():
     p.add_argument("--filters", type=int, default=None)
     p.add_argument("--batch", type=int, default=1_000_000)
     p.add_argument("--batches", type=int, default=5)
+    p.add_argument("--order", default="stream", choices=["stream", "sorted", "bucket"],
+                   help="topic order in the batch: generator stream, byte-sorted, or bucketed "
+                        "by the hash of the first two levels (locality study)")
     a = p.parse_args()
     import torch
     from bench import CONFIGS
@@ -30,6 +33,14 @@ def main():
         part = fs.slice(lo, min(lo + 2_000_000, len(fs)))
         ix.apply(np.ones(len(part), np.uint8), part.blob, part.offs, part.vals)
     ts = wl.topics(gen, nf, a.batch)
+    if a.order != "stream":
+        items = ts.items()
+        if a.order == "sorted":
+            items = sorted(items)
+        else:
+            items = sorted(items, key=lambda t: hash(b"/".join(t.split(b"/")[:2])) & 0xFFFF)
+        blob, offs = _native.pack_strings(items)
+        ts = wl.ItemSet(blob, offs, np.zeros(len(items), np.uint32), np.zeros(len(items), np.uint8))
     dev = torch.device("cuda:0")
     d_blob = torch.from_numpy(ts.blob).to(dev)
     d_offs = torch.from_numpy(ts.offs.view(np.int64)).to(dev)
@@ -49,7 +60,7 @@ def main():
     el = time.perf_counter() - t
     w, b, n = ix.profile_read()
     st = ix.stats()
-    print(f"{a.config} filters={len(fs)} batch={a.batch} hits={tot} wall/batch={el / a.batches * 1e3:.3f}ms "
+    print(f"{a.config}/{a.order} filters={len(fs)} batch={a.batch} hits={tot} wall/batch={el / a.batches * 1e3:.3f}ms "
           f"walk={w / n:.4f}ms batch_dev={b / n:.4f}ms rate={a.batch * a.batches / el / 1e9:.3f}G/s "
           f"device_MiB={st['device_bytes'] / 2**20:.0f}", flush=True)
 
