@@ -93,9 +93,11 @@ struct tm_index {
     uint64_t *dev_addr = nullptr; uint32_t *dev_val = nullptr; uint64_t dev_pcap = 0;
     hipEvent_t patch_done = nullptr; bool patch_pending = false;
 
-    // per-batch workspace
-    Workspace ws{};
-    uint64_t ws_cap = 0;
+    // per-batch workspaces, one per stream that has run a batch: batches on
+    // different streams may overlap (a broker pipelines micro-batches)
+    struct WsSlot { hipStream_t s; Workspace w; hipEvent_t done; bool used; };
+    std::vector<WsSlot> wss;
+    bool patched = false;   // patch_done has been recorded at least once
 
     // host-API staging
     uint8_t *pin_in = nullptr; uint64_t pin_in_cap = 0;
@@ -668,6 +670,13 @@ int collect(tm_index *ix, Mirror<T> &m, std::vector<uint64_t> &addr, std::vector
     return TM_OK;
 }
 
+// a batch on stream s is done with the index: later patches (on any stream) wait for it
+int batch_done(tm_index *ix, hipStream_t s) {
+    for (auto &e : ix->wss)
+        if (e.s == s) { HIPCHK(ix, hipEventRecord(e.done, s)); e.used = true; }
+    return TM_OK;
+}
+
 int sync_locked(tm_index *ix, hipStream_t s) {
     HIPCHK(ix, hipSetDevice(ix->device));
     if (ix->patch_pending) { HIPCHK(ix, hipEventSynchronize(ix->patch_done)); ix->patch_pending = false; }
@@ -701,11 +710,16 @@ int sync_locked(tm_index *ix, hipStream_t s) {
     }
     memcpy(ix->pin_addr, addr.data(), n * 8);
     memcpy(ix->pin_val, val.data(), n * 4);
+    // patches rewrite the tables in place: wait for batches still reading them
+    // on other streams (a batch sees exactly the deltas applied before it)
+    for (auto &e : ix->wss)
+        if (e.used && e.s != s) HIPCHK(ix, hipStreamWaitEvent(s, e.done, 0));
     HIPCHK(ix, hipMemcpyAsync(ix->dev_addr, ix->pin_addr, n * 8, hipMemcpyHostToDevice, s));
     HIPCHK(ix, hipMemcpyAsync(ix->dev_val, ix->pin_val, n * 4, hipMemcpyHostToDevice, s));
     HIPCHK(ix, launch_patch(ix->dev_addr, ix->dev_val, n, s));
     HIPCHK(ix, hipEventRecord(ix->patch_done, s));
     ix->patch_pending = true;
+    ix->patched = true;
     ix->patch_bytes += n * 4;
     ix->uploads++;
     return TM_OK;
@@ -735,16 +749,26 @@ int grow_dev(tm_index *ix, T *&p, uint64_t &cap, uint64_t need) {
     return TM_OK;
 }
 
-int ensure_ws(tm_index *ix, uint64_t n, hipStream_t s) {
-    Workspace &w = ix->ws;
+int ensure_ws(tm_index *ix, uint64_t n, hipStream_t s, Workspace *&out) {
+    Workspace *wp = nullptr;
+    for (auto &e : ix->wss) if (e.s == s) wp = &e.w;
+    if (!wp) {
+        hipEvent_t ev;
+        HIPCHK(ix, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        ix->wss.push_back({s, Workspace{}, ev, false});
+        wp = &ix->wss.back().w;
+    }
+    Workspace &w = *wp;
+    out = wp;
     if (!w.deep_wid) {
         HIPCHK(ix, hipMalloc(&w.deep_wid, (uint64_t)DEEP_LANES * MAX_LEVELS * 4));
         HIPCHK(ix, hipMalloc(&w.deep_stk, (uint64_t)DEEP_LANES * (MAX_LEVELS + 1) * 8));
         HIPCHK(ix, hipMalloc(&w.list_n, (L_COUNT + 1) * 4));
         HIPCHK(ix, hipMemset(w.list_n, 0, (L_COUNT + 1) * 4));
     }
-    if (n <= ix->ws_cap && w.cnt) return TM_OK;
-    (void)s;
+    // the batch must see every patch shipped so far, whichever stream it went on
+    if (ix->patched) HIPCHK(ix, hipStreamWaitEvent(s, ix->patch_done, 0));
+    if (n <= w.cap_n && w.cnt) return TM_OK;
     HIPCHK(ix, hipDeviceSynchronize());
     if (w.cnt) { (void)hipFree(w.cnt); (void)hipFree(w.nr); (void)hipFree(w.rng); (void)hipFree(w.lists); (void)hipFree(w.blk); }
     uint64_t c = std::max<uint64_t>(n + n / 4, 1024);
@@ -754,7 +778,6 @@ int ensure_ws(tm_index *ix, uint64_t n, hipStream_t s) {
     HIPCHK(ix, hipMalloc(&w.lists, c * L_COUNT * 4));
     HIPCHK(ix, hipMalloc(&w.blk, (c / TILE + 4) * 8));
     w.cap_n = c;
-    ix->ws_cap = c;
     return TM_OK;
 }
 
@@ -831,11 +854,16 @@ int tm_destroy(tm_index *ix) {
     (void)hipSetDevice(ix->device);
     (void)hipStreamSynchronize(ix->stream);
     void *bufs[] = {ix->vocab.d, ix->wpool.d, ix->nodes.d, ix->ctab.d, ix->vals.d, ix->exact.d, ix->xfp.d, ix->wseq.d,
-                    ix->dev_addr, ix->dev_val, ix->ws.cnt, ix->ws.nr, ix->ws.rng, ix->ws.lists, ix->ws.list_n,
-                    ix->ws.blk, ix->ws.deep_wid, ix->ws.deep_stk,
+                    ix->dev_addr, ix->dev_val,
                     ix->d_topics, ix->d_offs, ix->d_hit,
                     ix->d_err, ix->d_out};
     for (void *p : bufs) if (p) (void)hipFree(p);
+    for (auto &e : ix->wss) {
+        (void)hipEventDestroy(e.done);
+        const Workspace &w = e.w;
+        void *wb[] = {w.cnt, w.nr, w.rng, w.lists, w.list_n, w.blk, w.deep_wid, w.deep_stk};
+        for (void *p : wb) if (p) (void)hipFree(p);
+    }
     void *pins[] = {ix->pin_addr, ix->pin_val, ix->pin_in, ix->pin_out, ix->pin_vals};
     for (void *p : pins) if (p) (void)hipHostFree(p);
     (void)hipEventDestroy(ix->patch_done);
@@ -880,12 +908,14 @@ int tm_match_batch_dev(tm_index *ix, uint64_t n, const uint8_t *bytes, const uin
     hipStream_t s = pick_stream(ix, stream);
     int rc;
     if ((rc = sync_locked(ix, s))) return rc;
-    if ((rc = ensure_ws(ix, n, s))) return rc;
+    Workspace *ws;
+    if ((rc = ensure_ws(ix, n, s, ws))) return rc;
     const DevIndex d = dev_view(ix);
     tm_index::ProfEv ev;
     if ((rc = prof_begin(ix, ev, s))) return rc;
-    HIPCHK(ix, launch_match_phase1(d, ix->ws, n, bytes, offs, hit_offs, err, s, ev.w0, ev.w1));
-    HIPCHK(ix, launch_match_phase2(d, ix->ws, n, bytes, offs, hit_offs, out, out ? cap : 0, s));
+    HIPCHK(ix, launch_match_phase1(d, *ws, n, bytes, offs, hit_offs, err, s, ev.w0, ev.w1));
+    HIPCHK(ix, launch_match_phase2(d, *ws, n, bytes, offs, hit_offs, out, out ? cap : 0, s));
+    if ((rc = batch_done(ix, s))) return rc;
     return prof_end(ix, ev, s);
 }
 
@@ -899,7 +929,8 @@ int tm_match_batch(tm_index *ix, uint64_t n, const uint8_t *tb, const uint64_t *
     hipStream_t s = ix->stream;
     int rc;
     if ((rc = sync_locked(ix, s))) return rc;
-    if ((rc = ensure_ws(ix, n, s))) return rc;
+    Workspace *ws;
+    if ((rc = ensure_ws(ix, n, s, ws))) return rc;
     const uint64_t b0 = to[0], nbytes = to[n] - b0;
     const uint64_t in_need = nbytes + 16 + (n + 1) * 8;
     if (in_need > ix->pin_in_cap) {
@@ -936,8 +967,8 @@ int tm_match_batch(tm_index *ix, uint64_t n, const uint8_t *tb, const uint64_t *
             HIPCHK(ix, hipHostMalloc(&ix->pin_vals, ix->pin_vals_cap * 4, hipHostMallocMapped));
             HIPCHK(ix, hipHostGetDevicePointer(reinterpret_cast<void **>(&ix->pin_vals_dev), ix->pin_vals, 0));
         }
-        HIPCHK(ix, launch_match_phase1(d, ix->ws, n, ix->d_topics, ix->d_offs, ix->d_hit, ix->d_err, s));
-        HIPCHK(ix, launch_match_phase2(d, ix->ws, n, ix->d_topics, ix->d_offs, ix->d_hit, ix->pin_vals_dev,
+        HIPCHK(ix, launch_match_phase1(d, *ws, n, ix->d_topics, ix->d_offs, ix->d_hit, ix->d_err, s));
+        HIPCHK(ix, launch_match_phase2(d, *ws, n, ix->d_topics, ix->d_offs, ix->d_hit, ix->pin_vals_dev,
                                        ix->pin_vals_cap, s));
         uint8_t *po = ix->pin_out;
         HIPCHK(ix, hipMemcpyAsync(po, ix->d_hit, (n + 1) * 8, hipMemcpyDeviceToHost, s));
@@ -968,7 +999,8 @@ int tm_first_batch(tm_index *ix, uint64_t n, const uint8_t *tb, const uint64_t *
     hipStream_t s = ix->stream;
     int rc;
     if ((rc = sync_locked(ix, s))) return rc;
-    if ((rc = ensure_ws(ix, n, s))) return rc;
+    Workspace *ws;
+    if ((rc = ensure_ws(ix, n, s, ws))) return rc;
     const uint64_t b0 = to[0], nbytes = to[n] - b0;
     const uint64_t in_need = nbytes + 16 + (n + 1) * 8;
     if (in_need > ix->pin_in_cap) {
@@ -987,7 +1019,7 @@ int tm_first_batch(tm_index *ix, uint64_t n, const uint8_t *tb, const uint64_t *
     if ((rc = grow_dev(ix, ix->d_err, ix->d_err_cap, n + 1))) return rc;
     HIPCHK(ix, hipMemcpyAsync(ix->d_offs, pin_offs, (n + 1) * 8, hipMemcpyHostToDevice, s));
     if (nbytes) HIPCHK(ix, hipMemcpyAsync(ix->d_topics, pin_bytes, nbytes, hipMemcpyHostToDevice, s));
-    HIPCHK(ix, launch_first(dev_view(ix), ix->ws, n, ix->d_topics, ix->d_offs, ix->d_out, ix->d_err, s));
+    HIPCHK(ix, launch_first(dev_view(ix), *ws, n, ix->d_topics, ix->d_offs, ix->d_out, ix->d_err, s));
     const uint64_t out_need = n * 5 + 16;
     if (out_need > ix->pin_out_cap) {
         HIPCHK(ix, hipStreamSynchronize(s));

@@ -492,3 +492,37 @@ def test_broker_micro_batch_equals_per_message_publish(torch_dev):
         routes = bk.aggre(r.match_routes(m.topic))
         assert got[0] == routes
         assert got == single.publish_batch([m])[0]
+
+
+def test_batches_on_two_streams_see_patches_in_order(torch_dev):
+    """Per-stream workspaces: batches on two streams may overlap; a batch sees
+    every delta applied before it, whichever stream shipped the patch."""
+    import torch
+    nf = 30_000
+    fs = wl.filters(5, nf)
+    ix, o = gpu_index(fs), oracle_of(fs)
+    ts = wl.topics(5, nf, 40_000)
+    dev = torch.device("cuda:0")
+    d_blob = torch.from_numpy(ts.blob.copy()).to(dev)
+    d_offs = torch.from_numpy(ts.offs.view(np.int64).copy()).to(dev)
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    n = len(ts)
+    results = []
+    for k in range(4):
+        d = wl.deltas(nf, k * 3_000, 3_000)
+        ix.apply(d.flags, d.blob, d.offs, d.vals)
+        o.apply(d.flags, d.blob, d.offs, d.vals)
+        o.prepare()
+        _, _, ohit, ovals = o.match_batch(ts.blob, ts.offs)
+        s = streams[k % 2]
+        hit = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+        err = torch.zeros(n, dtype=torch.uint8, device=dev)
+        out = torch.zeros(int(ohit[-1]) + 1, dtype=torch.int32, device=dev)
+        ix.match_batch_dev(n, d_blob.data_ptr(), d_offs.data_ptr(), hit.data_ptr(), out.data_ptr(), out.numel(),
+                           err.data_ptr(), s.cuda_stream)
+        results.append((hit, out, ohit, ovals))
+    torch.cuda.synchronize()
+    for hit, out, ohit, ovals in results:
+        h = hit.cpu().numpy().view(np.uint64)
+        assert np.array_equal(h, ohit.astype(np.uint64))
+        assert np.array_equal(out.cpu().numpy().view(np.uint32)[: int(h[-1])], ovals)
