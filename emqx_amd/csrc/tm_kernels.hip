@@ -618,17 +618,27 @@ __global__ __launch_bounds__(MID_BLOCK) void k_rewalk_tail(DevIndex ix, Workspac
 }
 
 // tile totals -> exclusive tile prefixes; hit_offs[n] = grand total
-__global__ __launch_bounds__(256) void k_scan_top(uint64_t *blk, uint64_t nb, uint64_t *hit_offs, uint64_t n) {
-    __shared__ uint64_t s_w[4];
-    uint64_t carry = 0;
-    for (uint64_t b0 = 0; b0 < nb; b0 += 256) {
-        const uint64_t i = b0 + threadIdx.x;
-        uint64_t v = i < nb ? blk[i] : 0, total;
-        uint64_t ex = block_excl_scan(v, total, s_w);
-        if (i < nb) blk[i] = carry + ex;
-        carry += total;
+__global__ __launch_bounds__(1024) void k_scan_top(uint64_t *blk, uint64_t nb, uint64_t *hit_offs, uint64_t n) {
+    // one block: thread j owns a contiguous run of ceil(nb / 1024) tiles (one
+    // pass over the totals instead of nb / 256 dependent block scans)
+    __shared__ uint64_t s_w[16];
+    const uint64_t per = (nb + 1023) / 1024;
+    const uint64_t b0 = threadIdx.x * per, b1 = b0 + per < nb ? b0 + per : nb;
+    uint64_t sum = 0;
+    for (uint64_t i = b0; i < b1; i++) sum += blk[i];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint64_t inc = wave_incl_scan(sum);
+    if (lane == 63) s_w[wv] = inc;
+    __syncthreads();
+    uint64_t pre = 0, total = 0;
+    for (int k = 0; k < 16; k++) { if (k < wv) pre += s_w[k]; total += s_w[k]; }
+    uint64_t run = pre + inc - sum;
+    for (uint64_t i = b0; i < b1; i++) {
+        const uint64_t v = blk[i];
+        blk[i] = run;
+        run += v;
     }
-    if (threadIdx.x == 0) hit_offs[n] = carry;
+    if (threadIdx.x == 0) hit_offs[n] = total;
 }
 
 // ------------------------------------------------------------------- emit
@@ -767,7 +777,7 @@ hipError_t launch_match_phase1(const DevIndex &ix, const Workspace &ws, uint64_t
         if (ev_walk1 && (e = hipEventRecord(ev_walk1, s)) != hipSuccess) return e;
         hipLaunchKernelGGL(k_walk_tail<MODE_COUNT>, dim3(TAIL_GRID), dim3(MID_BLOCK), 0, s, ix, ws, n, bytes, offs, o);
     }
-    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(256), 0, s, ws.blk, (uint64_t)nb, hit_offs, n);
+    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(1024), 0, s, ws.blk, (uint64_t)nb, hit_offs, n);
     return hipGetLastError();
 }
 
