@@ -45,6 +45,7 @@ CONFIGS = {
     "c5": (5, 10_000_000, "churn: 10M mixed filters, subscribe/unsubscribe deltas interleaved with match batches"),
 }
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
+RANDOM_REQ_CEILING = 5.5e10   # measured random 64-B request rate beyond L2 (profiles/r1_gather.md)
 
 
 def log(*a):
@@ -293,14 +294,24 @@ def main():
                              f"restated) over a sorted key array, {a.cpu_threads} pthreads, {el_cpu:.1f}s"}
 
     traffic = None
+    mem_req = None
     pmc = ROOT / "profiles" / f"pmc_{a.config}.json"
     if pmc.exists():
         try:
             pj = json.loads(pmc.read_text())
             if pj.get("filters") == len(fs) and pj.get("batch") == B:
                 traffic = pj.get("walk_hbm_bytes_per_launch")
+                mem_req = pj.get("walk_mem_requests_per_launch")
         except Exception:
             traffic = None
+    # practical roofline of a pointer-chasing walk: the measured memory-side
+    # random-request rate (tools/gather_bench.hip, profiles/r1_gather.md)
+    req_ceiling = None
+    if mem_req and walk_avg_ms:
+        rate = mem_req / (walk_avg_ms * 1e-3)
+        req_ceiling = {"requests_per_launch": mem_req, "requests_per_s": round(rate, 1),
+                       "ceiling_per_s": RANDOM_REQ_CEILING, "frac": round(rate / RANDOM_REQ_CEILING, 4),
+                       "source": "profiles/r1_gather.md (64-B random requests beyond L2, 256 MiB-2 GiB tables)"}
 
     metric = {"c3": "topic matches/sec at 10M filters"}.get(a.config, f"topic matches/sec ({a.config})")
     par = (f"filter-sharded x{world} (RCCL allgatherv of hit lists)" if filter_sharded
@@ -325,7 +336,8 @@ def main():
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": None if achieved is None else round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "kernel": "k_walk_fast", "kernel_avg_ms": round(walk_avg_ms, 4),
-                     "algorithmic_bytes_per_launch": None if walk_bytes is None else int(walk_bytes)},
+                     "algorithmic_bytes_per_launch": None if walk_bytes is None else int(walk_bytes),
+                     "random_request_roofline": req_ceiling},
         "cpu_baseline": cpu,
         "matched_ids_per_s": round(last_hits * (1 if filter_sharded else world) * a.steps / el_max, 1),
         "hits_per_topic": round((merged_total if merged_total is not None else last_hits) / B, 3),

@@ -32,6 +32,15 @@ namespace tmx {
 
 __device__ __forceinline__ uint4 ld4(const void *p) { return *reinterpret_cast<const uint4 *>(p); }
 
+// Empty asm "uses": pin a loaded value at this point on every path.  Without
+// them the compiler sinks loads into the branches that read each field (one
+// dependent round trip per field: the exact entry took three, a child slot
+// two), and a load left pending on a skipped branch makes it drain vmcnt(0)
+// before the next reuse of its registers.
+__device__ __forceinline__ void pin(uint32_t &v) { asm volatile("" : "+v"(v)); }
+__device__ __forceinline__ void pin(uint2 &v) { pin(v.x); pin(v.y); }
+__device__ __forceinline__ void pin(uint4 &v) { pin(v.x); pin(v.y); pin(v.z); pin(v.w); }
+
 struct WordAcc {
     uint64_t h;                 // FNV-1a over the bytes (used for words > VINL bytes)
     uint32_t len, b0, b1;       // length, first 8 bytes packed little endian
@@ -83,7 +92,8 @@ __device__ uint32_t vocab_find(const DevIndex &ix, const WordAcc &w, const uint8
 __device__ __forceinline__ uint32_t ctab_find(const DevIndex &ix, uint32_t off, uint32_t mask, uint32_t wid,
                                               uint32_t h) {
     for (uint32_t s = h & mask;; s = (s + 1) & mask) {
-        const uint2 e = *reinterpret_cast<const uint2 *>(ix.ctab + off + s);
+        uint2 e = *reinterpret_cast<const uint2 *>(ix.ctab + off + s);
+        pin(e);
         if (e.x == wid) return e.y;
         if (e.x == NONE) return NONE;
     }
@@ -217,29 +227,33 @@ __device__ int tokenize(const DevIndex &ix, const uint8_t *blob, uint64_t beg, u
     if (rc) return rc;
     L = lev;
     if constexpr (S::deferred) {
+        // Branch-free issue and consumption: every lane issues VGROUP loads
+        // (unused levels read slot 0) and consumes all of them, so no load is
+        // left pending on a skipped branch -- the compiler would otherwise drain
+        // vmcnt(0) before reusing its registers and serialise the probes.
         for (uint32_t base = 0; base < L; base += VGROUP) {
             uint4 e[VGROUP];
             uint32_t tg[VGROUP];
+            bool use[VGROUP];
 #pragma unroll
             for (uint32_t k = 0; k < VGROUP; k++) {
                 const uint32_t l = base + k;
-                tg[k] = 0;
-                if (l < L && !((longmask >> l) & 1)) {
-                    const uint32_t len = st.word_len(l);
-                    const uint64_t h = word_hash_short(st.word_b0(l), st.word_b1(l), len);
-                    tg[k] = vocab_tag(h, len);
-                    e[k] = ld4(ix.vocab + ((uint32_t)h & ix.vmask));
-                }
+                use[k] = l < L && !((longmask >> l) & 1);
+                const uint32_t ls = use[k] ? l : 0;
+                const uint32_t len = st.word_len(ls);
+                const uint64_t h = word_hash_short(st.word_b0(ls), st.word_b1(ls), len);
+                tg[k] = vocab_tag(h, len);
+                e[k] = ld4(ix.vocab + (use[k] ? ((uint32_t)h & ix.vmask) : 0u));
             }
 #pragma unroll
             for (uint32_t k = 0; k < VGROUP; k++) {
-                const uint32_t l = base + k;
-                if (l < L && !((longmask >> l) & 1)) {
-                    const uint32_t b0 = st.word_b0(l), b1 = st.word_b1(l);
-                    uint32_t wid;
-                    if (e[k].y == NONE) wid = NONE;
-                    else if (e[k].x == tg[k] && e[k].z == b0 && e[k].w == b1) wid = e[k].y;
-                    else {   // rare at load <= 1/4: walk the probe sequence on
+                const uint32_t l = use[k] ? base + k : 0;
+                const uint32_t b0 = st.word_b0(l), b1 = st.word_b1(l);
+                const bool hit = e[k].x == tg[k] && e[k].z == b0 && e[k].w == b1;
+                uint32_t wid = e[k].y == NONE ? NONE : hit ? e[k].y : NONE - 1;
+                pin(wid);   // consume e[k] here on every path
+                if (use[k]) {
+                    if (wid == NONE - 1) {   // rare at load <= 1/2: walk the probe sequence on
                         const uint32_t len = st.word_len(l);
                         const uint64_t h = word_hash_short(b0, b1, len);
                         wid = vocab_probe(ix, ((uint32_t)h + 1) & ix.vmask, tg[k], len, b0, b1, nullptr);
@@ -278,7 +292,8 @@ __device__ void exact_find(const DevIndex &ix, uint64_t xh, uint32_t L, const S 
         if (f == 0) return;
         if (f == fp) {
             const uint4 *e = reinterpret_cast<const uint4 *>(ix.exact + slot);
-            const uint4 a = e[0], b = e[1], c = e[2], d = e[3];
+            uint4 a = e[0], b = e[1], c = e[2], d = e[3];
+            pin(a); pin(b); pin(c); pin(d);
             if (a.x == (uint32_t)xh && a.y == (uint32_t)(xh >> 32) && a.z == L) {
                 bool eq = true;
                 if (L <= XINL) {
@@ -320,15 +335,22 @@ __device__ bool dfs(const DevIndex &ix, uint32_t L, bool dollar, S &st, EM &em) 
         const uint4 n2 = np[2];   // kw[0..3] (table mode: offset, size-1)
         const uint4 n3 = np[3];   // kc[0..3]
         const bool droot = dollar && l == 0;
+        // The inline-child match reads n2/n3 on every path (pinned): a line
+        // load left pending on a skipped branch would make the compiler drain
+        // vmcnt(0) at the top of the next step, before its loads are issued --
+        // serialising them behind the exact-table fingerprint load that is
+        // meant to overlap the walk.
+        const uint32_t w = l < L ? st.get_wid(l) : NONE;
+        uint32_t inl = n2.x == w ? n3.x : n2.y == w ? n3.y : n2.z == w ? n3.z : n2.w == w ? n3.w : NONE;
+        pin(inl);
         if (l == L) {
             if (!em(n0.w, n1.x)) return false;
             if (!droot && !em(n0.y, n0.z)) return false;
         } else {
-            const uint32_t w = st.get_wid(l);
             uint32_t lit = NONE;
             if (w != NONE) {
                 if (n1.y <= KINL) {
-                    lit = n2.x == w ? n3.x : n2.y == w ? n3.y : n2.z == w ? n3.z : n2.w == w ? n3.w : NONE;
+                    lit = inl;
                 } else {
                     const uint32_t h = child_hash(w), b = child_bit(h);
                     const uint32_t m = b < 32 ? n1.z >> b : n1.w >> (b - 32);

@@ -13,8 +13,10 @@ under profiles/:
 HBM bytes: FETCH_SIZE and WRITE_SIZE are reported by rocprofv3 in KiB.
 FETCH_SIZE = TCC_EA0_RDREQ x 64 B (MI355X_MICROARCH.md, HBM section); the
 walk's reads are 16-B-per-lane loads of scattered 64-B lines, not the wide
-streaming reads the guide's x2 correction was calibrated on, so the value is
-taken as is (the memory-side request count x 64 B) and labelled uncalibrated.
+streaming reads the guide's x2 correction was calibrated on.  Calibrated with
+tools/gather_bench.hip on a known request count (profiles/r1_gather.md): for
+scattered 16-B and 64-B reads FETCH_SIZE counts exactly 64 B per memory-side
+request, so the value is taken as is (no x2).
 It also counts Infinity-Cache (MALL) hits, so it is an upper bound on HBM.
 
 usage: prof_report.py <prof_dir> <round> <tag> <config> <filters> <batch>
@@ -122,8 +124,9 @@ def main(prof, rnd, tag, config, filters, batch):
             res["walk_fetch_bytes_per_launch"] = int(c.get("FETCH_SIZE", 0) * 1024)
             res["walk_write_bytes_per_launch"] = int(c.get("WRITE_SIZE", 0) * 1024)
             res["walk_hbm_bytes_per_launch"] = res["walk_fetch_bytes_per_launch"] + res["walk_write_bytes_per_launch"]
-            res["note"] = ("FETCH_SIZE (memory-side 64-B read requests, MALL hits included) + WRITE_SIZE, "
-                           "uncalibrated for 16-B scattered line reads")
+            res["walk_mem_requests_per_launch"] = round(res["walk_fetch_bytes_per_launch"] / 64)
+            res["note"] = ("FETCH_SIZE (memory-side 64-B read requests, MALL hits included; calibrated at 64 B "
+                           "per scattered request, profiles/r1_gather.md) + WRITE_SIZE")
             res["source"] = f"profiles/{rnd}_{tag}.md"
             json.dump(res, open(os.path.join("profiles", f"pmc_{config}.json"), "w"), indent=1)
     open(os.path.join("profiles", f"{rnd}_{tag}.md"), "w").write("\n".join(lines) + "\n")
