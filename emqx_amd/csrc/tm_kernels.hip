@@ -354,10 +354,12 @@ __device__ bool dfs(const DevIndex &ix, uint32_t L, bool dollar, S &st, EM &em) 
                 } else {
                     const uint32_t h = child_hash(w), b = child_bit(h);
                     const uint32_t m = b < 32 ? n1.z >> b : n1.w >> (b - 32);
-#ifdef TM_STUDY
-                    if constexpr (S::deferred) st.n_probe += m & 1u;
-#endif
                     if (m & 1u) lit = ctab_find(ix, n2.x, n2.y, w, h);
+#ifdef TM_STUDY
+                    if constexpr (S::deferred) {
+                        if (m & 1u) { if (lit != NONE) st.n_steps += 1u << 16; else st.n_probe++; }
+                    }
+#endif
                 }
             }
             if (!droot && !em(n0.y, n0.z)) return false;
@@ -468,7 +470,15 @@ __device__ int run_topic(const DevIndex &ix, const Workspace &ws, uint64_t n, co
         em.store(ws.rng, n, t);
 #ifdef TM_STUDY   // study build (tools/study_steps.py): visits and probes in the err byte
         if constexpr (S::maxl == FAST_L)
-            o.err[t] = (uint8_t)((st.n_steps < 31 ? st.n_steps : 31) | ((st.n_probe < 7 ? st.n_probe : 7) << 5));
+        {   // TM_STUDY_HITS: ctab probes that found the child (low nibble) / missed (high nibble)
+#ifdef TM_STUDY_HITS
+            const uint32_t hit = st.n_steps >> 16;
+            o.err[t] = (uint8_t)((hit < 15 ? hit : 15) | ((st.n_probe < 15 ? st.n_probe : 15) << 4));
+#else
+            const uint32_t vis = st.n_steps & 0xFFFF, pr = (st.n_steps >> 16) + st.n_probe;
+            o.err[t] = (uint8_t)((vis < 31 ? vis : 31) | ((pr < 7 ? pr : 7) << 5));
+#endif
+        }
         else
             o.err[t] = rc == RC_BADARG;
 #else

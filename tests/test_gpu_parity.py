@@ -366,6 +366,53 @@ def test_child_table_grow_and_shrink(torch_dev):
     assert ix.stats()["n_nodes"] == 1
 
 
+def test_chains_cut_and_healed_under_deltas(torch_dev):
+    """Long single-child chains made, cut in the middle (a terminal, a literal
+    sibling, a '+' sibling), healed and removed again, with matches checked
+    against the oracle at every stage: chains of 3 to 24 levels through literal
+    and '+' edges, ending in exact and '#' terminals."""
+    def chain(tag, n, plus_at=()):
+        return b"/".join(b"+" if i in plus_at else b"%s%d" % (tag, i) for i in range(n))
+
+    base = [chain(b"a", 3), chain(b"b", 11), chain(b"c", 12) + b"/#", chain(b"d", 24),
+            chain(b"e", 14, plus_at=(3, 4, 9)), chain(b"f", 6, plus_at=(1,)) + b"/#", b"g/+/+/+/+/h"]
+    cuts = [chain(b"b", 5), chain(b"b", 6) + b"/#", chain(b"d", 8) + b"/zz", chain(b"d", 15) + b"/+",
+            chain(b"e", 7) + b"/x", chain(b"c", 2) + b"/+/#", b"g/+/+/q"]
+
+    def topics_for(fs):
+        out = []
+        for f in fs:
+            ws = [w if w not in (b"+", b"#") else b"w" for w in f.split(b"/")]
+            for n in range(1, len(ws) + 3):
+                out.append(b"/".join((ws + [b"t", b"u"])[:n]))
+            for i in range(len(ws)):   # deviate at every level
+                out.append(b"/".join(ws[:i] + [b"zz"] + ws[i + 1:]))
+        return out
+
+    ts = items_of(sorted(set(topics_for(base + cuts))))
+    ix, o = gpu_index(), Oracle()
+
+    def apply(fs, vals, ins):
+        d = items_of(fs, vals)
+        op = np.full(len(fs), 1 if ins else 0, np.uint8)
+        ix.apply(op, d.blob, d.offs, d.vals)
+        o.apply(op, d.blob, d.offs, d.vals)
+
+    apply(base, range(len(base)), True)
+    assert_same(ix, o, ts)
+    apply(cuts, range(100, 100 + len(cuts)), True)
+    assert_same(ix, o, ts)
+    apply(cuts[::2], range(100, 100 + len(cuts), 2), False)
+    assert_same(ix, o, ts)
+    apply(cuts[1::2], range(101, 100 + len(cuts), 2), False)
+    assert_same(ix, o, ts)
+    apply(base[::2], range(0, len(base), 2), False)
+    assert_same(ix, o, ts)
+    apply(base[1::2], range(1, len(base), 2), False)
+    assert_same(ix, o, ts)
+    assert ix.stats()["n_nodes"] == 1
+
+
 # ------------------------------------------------------------- filter-sharded
 
 def _merge_ref(all_offs, all_vals):

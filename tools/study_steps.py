@@ -18,8 +18,16 @@ def main():
     for lo in range(0, len(fs), 2_000_000):
         p = fs.slice(lo, min(lo + 2_000_000, len(fs)))
         ix.apply(np.ones(len(p), np.uint8), p.blob, p.offs, p.vals)
+    st = ix.stats()
+    print(f"{cfg}: nodes {st['n_nodes']} edges {st['n_edges']}", flush=True)
     ts = wl.topics(gen, nf, 200_000)
     hit, vals, err = ix.match_batch(ts.blob, ts.offs)
+    import os
+    if os.environ.get("TM_STUDY_HITS"):
+        hits_, miss_ = (err & 15).astype(np.int64), (err >> 4).astype(np.int64)
+        print(f"{cfg}: child-table probes that found the child mean {hits_.mean():.2f}, "
+              f"that missed mean {miss_.mean():.2f} (each capped at 15)", flush=True)
+        return
     steps = (err & 31).astype(np.int64)
     probes = (err >> 5).astype(np.int64)
     w = steps.reshape(-1, 64)
