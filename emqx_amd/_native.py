@@ -160,11 +160,24 @@ class Index:
         self._check(self._lib.tm_sync(self._h, stream))
 
     # ---- matching (host buffers)
-    def match_batch(self, blob: np.ndarray, offs: np.ndarray, cap: int | None = None):
-        """-> (hit_offsets u64[n+1], values u32[total], err u8[n]) in traversal order."""
+    def match_batch(self, blob: np.ndarray, offs: np.ndarray, cap: int | None = None, out=None):
+        """-> (hit_offsets u64[n+1], values u32[total], err u8[n]) in traversal order.
+
+        `out` = (hit u64[>= n+1], values u32[cap], err u8[>= n]): caller-owned
+        buffers reused across batches (what a NIF keeps per scheduler); the
+        results are views into them.  Without it fresh arrays are allocated."""
         n = len(offs) - 1
         blob = np.ascontiguousarray(blob, dtype=np.uint8)
         offs = np.ascontiguousarray(offs, dtype=np.uint64)
+        if out is not None:
+            hit, vals, err = out
+            if len(hit) < n + 1 or len(err) < n or hit.dtype != np.uint64 or vals.dtype != np.uint32 \
+                    or err.dtype != np.uint8:
+                raise ValueError("match_batch: out buffers too small or of the wrong dtype")
+            rc = self._lib.tm_match_batch(self._h, n, _ptr(blob), _ptr(offs), _ptr(hit), _ptr(vals), len(vals),
+                                          _ptr(err))
+            self._check(rc)
+            return hit[: n + 1], vals[: int(hit[n])], err[:n]
         hit = np.zeros(n + 1, dtype=np.uint64)
         err = np.zeros(max(n, 1), dtype=np.uint8)
         if cap is None:

@@ -12,6 +12,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -100,13 +102,12 @@ struct tm_index {
     bool patched = false;   // patch_done has been recorded at least once
 
     // host-API staging
-    uint8_t *pin_in = nullptr; uint64_t pin_in_cap = 0;
-    uint8_t *pin_out = nullptr; uint64_t pin_out_cap = 0;
-    uint8_t *d_topics = nullptr; uint64_t d_topics_cap = 0;
-    uint64_t *d_offs = nullptr; uint64_t d_offs_cap = 0;
-    uint64_t *d_hit = nullptr; uint64_t d_hit_cap = 0;
-    uint8_t *d_err = nullptr; uint64_t d_err_cap = 0;
-    uint32_t *d_out = nullptr; uint64_t d_out_cap = 0;
+    // host-API staging: mapped pinned buffers (pin_*_dev = their device
+    // addresses) and the HBM copies used for batches above ZC_TOPICS
+    uint8_t *pin_in = nullptr, *pin_in_dev = nullptr; uint64_t pin_in_cap = 0;
+    uint8_t *pin_out = nullptr, *pin_out_dev = nullptr; uint64_t pin_out_cap = 0;
+    uint8_t *d_in = nullptr; uint64_t d_in_cap = 0;
+    uint8_t *d_res = nullptr; uint64_t d_res_cap = 0;
     uint32_t *pin_vals = nullptr, *pin_vals_dev = nullptr; uint64_t pin_vals_cap = 0;
 
     // diagnostics (tm_profile_*)
@@ -855,8 +856,7 @@ int tm_destroy(tm_index *ix) {
     (void)hipStreamSynchronize(ix->stream);
     void *bufs[] = {ix->vocab.d, ix->wpool.d, ix->nodes.d, ix->ctab.d, ix->vals.d, ix->exact.d, ix->xfp.d, ix->wseq.d,
                     ix->dev_addr, ix->dev_val,
-                    ix->d_topics, ix->d_offs, ix->d_hit,
-                    ix->d_err, ix->d_out};
+                    ix->d_in, ix->d_res};
     for (void *p : bufs) if (p) (void)hipFree(p);
     for (auto &e : ix->wss) {
         (void)hipEventDestroy(e.done);
@@ -919,8 +919,78 @@ int tm_match_batch_dev(tm_index *ix, uint64_t n, const uint8_t *bytes, const uin
     return prof_end(ix, ev, s);
 }
 
+namespace {
+
+// Batches of up to ZC_TOPICS topics are staged zero-copy: the kernels read the
+// topics from, and write offsets / flags / values into, mapped pinned host
+// memory over PCIe.  A small batch then costs its kernels plus one host
+// synchronisation -- no copy commands and no gaps between them.  Larger
+// batches move in one H2D and one D2H transfer.
+constexpr uint64_t ZC_TOPICS = 65536;
+
+int pin_mapped(tm_index *ix, hipStream_t s, uint8_t *&host, uint8_t *&dev, uint64_t &cap, uint64_t need) {
+    if (need <= cap) return TM_OK;
+    HIPCHK(ix, hipStreamSynchronize(s));
+    if (host) HIPCHK(ix, hipHostFree(host));
+    host = dev = nullptr;
+    cap = need + need / 4;
+    HIPCHK(ix, hipHostMalloc(&host, cap, hipHostMallocMapped));
+    HIPCHK(ix, hipHostGetDevicePointer(reinterpret_cast<void **>(&dev), host, 0));
+    return TM_OK;
+}
+
+// a host topic batch -> what the kernels read: rebased offsets, then the bytes
+// (16-aligned: the walk's aligned 16-byte loads), in one buffer
+int stage_in(tm_index *ix, uint64_t n, const uint8_t *tb, const uint64_t *to, hipStream_t s,
+             const uint8_t *&dbytes, const uint64_t *&doffs) {
+    const uint64_t b0 = to[0], nbytes = to[n] - b0;
+    const uint64_t boff = ((n + 1) * 8 + 15) & ~15ull;
+    const uint64_t need = boff + nbytes + 16;
+    int rc;
+    if ((rc = pin_mapped(ix, s, ix->pin_in, ix->pin_in_dev, ix->pin_in_cap, need))) return rc;
+    uint64_t *po = reinterpret_cast<uint64_t *>(ix->pin_in);
+    for (uint64_t i = 0; i <= n; i++) po[i] = to[i] - b0;
+    if (nbytes) memcpy(ix->pin_in + boff, tb + b0, nbytes);
+    const uint8_t *base = ix->pin_in_dev;
+    if (n > ZC_TOPICS) {
+        if ((rc = grow_dev(ix, ix->d_in, ix->d_in_cap, need))) return rc;
+        HIPCHK(ix, hipMemcpyAsync(ix->d_in, ix->pin_in, boff + nbytes, hipMemcpyHostToDevice, s));
+        base = ix->d_in;
+    }
+    doffs = reinterpret_cast<const uint64_t *>(base);
+    dbytes = base + boff;
+    return TM_OK;
+}
+
+// where the kernels write `bytes` of per-topic results (read back by fetch_out)
+int stage_out(tm_index *ix, uint64_t n, uint64_t bytes, hipStream_t s, uint8_t *&dout) {
+    int rc;
+    if ((rc = pin_mapped(ix, s, ix->pin_out, ix->pin_out_dev, ix->pin_out_cap, bytes + 16))) return rc;
+    dout = ix->pin_out_dev;
+    if (n > ZC_TOPICS) {
+        if ((rc = grow_dev(ix, ix->d_res, ix->d_res_cap, bytes + 16))) return rc;
+        dout = ix->d_res;
+    }
+    return TM_OK;
+}
+
+int fetch_out(tm_index *ix, uint64_t n, uint64_t bytes, hipStream_t s) {
+    if (n > ZC_TOPICS && bytes) HIPCHK(ix, hipMemcpyAsync(ix->pin_out, ix->d_res, bytes, hipMemcpyDeviceToHost, s));
+    return TM_OK;
+}
+
+}  // namespace
+
+// TM_HOST_TIMING=1: per-phase host timings of tm_match_batch on stderr (diagnostics)
+static double now_us() {
+    return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 int tm_match_batch(tm_index *ix, uint64_t n, const uint8_t *tb, const uint64_t *to, uint64_t *out_hit,
                    uint32_t *out_vals, uint64_t cap, uint8_t *out_err) {
+    static const bool timing = getenv("TM_HOST_TIMING") != nullptr;
+    double tt[8]; int nt = 0;
+    if (timing) tt[nt++] = now_us();
     if (!ix) return fail(nullptr, TM_EINVAL, "tm_match_batch: null handle");
     if (!to || !out_hit || (n && !tb && to[n] != to[0])) return fail(ix, TM_EINVAL, "tm_match_batch: null buffer");
     if (n >= 0xFFFFFFFFull) return fail(ix, TM_EINVAL, "tm_match_batch: batch too large");
@@ -931,34 +1001,19 @@ int tm_match_batch(tm_index *ix, uint64_t n, const uint8_t *tb, const uint64_t *
     if ((rc = sync_locked(ix, s))) return rc;
     Workspace *ws;
     if ((rc = ensure_ws(ix, n, s, ws))) return rc;
-    const uint64_t b0 = to[0], nbytes = to[n] - b0;
-    const uint64_t in_need = nbytes + 16 + (n + 1) * 8;
-    if (in_need > ix->pin_in_cap) {
-        HIPCHK(ix, hipStreamSynchronize(s));
-        if (ix->pin_in) HIPCHK(ix, hipHostFree(ix->pin_in));
-        ix->pin_in_cap = in_need + in_need / 4;
-        HIPCHK(ix, hipHostMalloc(&ix->pin_in, ix->pin_in_cap, hipHostMallocDefault));
-    }
-    uint64_t *pin_offs = reinterpret_cast<uint64_t *>(ix->pin_in);
-    uint8_t *pin_bytes = ix->pin_in + (n + 1) * 8;
-    for (uint64_t i = 0; i <= n; i++) pin_offs[i] = to[i] - b0;
-    if (nbytes) memcpy(pin_bytes, tb + b0, nbytes);
-    if ((rc = grow_dev(ix, ix->d_topics, ix->d_topics_cap, nbytes + 16))) return rc;
-    if ((rc = grow_dev(ix, ix->d_offs, ix->d_offs_cap, n + 1))) return rc;
-    if ((rc = grow_dev(ix, ix->d_hit, ix->d_hit_cap, n + 1))) return rc;
-    if ((rc = grow_dev(ix, ix->d_err, ix->d_err_cap, n + 1))) return rc;
-    // small outputs (offsets, err flags) come back by DMA; the values are
+    if (timing) tt[nt++] = now_us();
+    const uint8_t *dbytes;
+    const uint64_t *doffs;
+    if ((rc = stage_in(ix, n, tb, to, s, dbytes, doffs))) return rc;
+    if (timing) tt[nt++] = now_us();
+    // results: hit offsets (n + 1) x u64, then the badarg flags; the values are
     // written by k_emit straight into mapped pinned memory, so the batch costs
     // one host synchronisation (a second one only when that buffer must grow)
-    const uint64_t small = (n + 1) * 8 + n + 16;
-    if (small > ix->pin_out_cap) {
-        HIPCHK(ix, hipStreamSynchronize(s));
-        if (ix->pin_out) HIPCHK(ix, hipHostFree(ix->pin_out));
-        ix->pin_out_cap = small + small / 4;
-        HIPCHK(ix, hipHostMalloc(&ix->pin_out, ix->pin_out_cap, hipHostMallocDefault));
-    }
-    HIPCHK(ix, hipMemcpyAsync(ix->d_offs, pin_offs, (n + 1) * 8, hipMemcpyHostToDevice, s));
-    if (nbytes) HIPCHK(ix, hipMemcpyAsync(ix->d_topics, pin_bytes, nbytes, hipMemcpyHostToDevice, s));
+    const uint64_t rbytes = (n + 1) * 8 + n;
+    uint8_t *dres;
+    if ((rc = stage_out(ix, n, rbytes, s, dres))) return rc;
+    uint64_t *dhit = reinterpret_cast<uint64_t *>(dres);
+    uint8_t *derr = dres + (n + 1) * 8;
     const DevIndex d = dev_view(ix);
     uint64_t total = 0;
     for (int attempt = 0; attempt < 2; attempt++) {
@@ -967,14 +1022,13 @@ int tm_match_batch(tm_index *ix, uint64_t n, const uint8_t *tb, const uint64_t *
             HIPCHK(ix, hipHostMalloc(&ix->pin_vals, ix->pin_vals_cap * 4, hipHostMallocMapped));
             HIPCHK(ix, hipHostGetDevicePointer(reinterpret_cast<void **>(&ix->pin_vals_dev), ix->pin_vals, 0));
         }
-        HIPCHK(ix, launch_match_phase1(d, *ws, n, ix->d_topics, ix->d_offs, ix->d_hit, ix->d_err, s));
-        HIPCHK(ix, launch_match_phase2(d, *ws, n, ix->d_topics, ix->d_offs, ix->d_hit, ix->pin_vals_dev,
-                                       ix->pin_vals_cap, s));
-        uint8_t *po = ix->pin_out;
-        HIPCHK(ix, hipMemcpyAsync(po, ix->d_hit, (n + 1) * 8, hipMemcpyDeviceToHost, s));
-        if (n) HIPCHK(ix, hipMemcpyAsync(po + (n + 1) * 8, ix->d_err, n, hipMemcpyDeviceToHost, s));
+        HIPCHK(ix, launch_match_phase1(d, *ws, n, dbytes, doffs, dhit, derr, s));
+        HIPCHK(ix, launch_match_phase2(d, *ws, n, dbytes, doffs, dhit, ix->pin_vals_dev, ix->pin_vals_cap, s));
+        if ((rc = fetch_out(ix, n, rbytes, s))) return rc;
+        if (timing && nt < 5) tt[nt++] = now_us();
         HIPCHK(ix, hipStreamSynchronize(s));
-        memcpy(&total, po + n * 8, 8);
+        if (timing && nt < 6) tt[nt++] = now_us();
+        memcpy(&total, ix->pin_out + n * 8, 8);
         if (total <= ix->pin_vals_cap || !out_vals || total <= 0) break;
         // grow the mapped buffer and run the batch again (rare: sizes are sticky)
         HIPCHK(ix, hipHostFree(ix->pin_vals));
@@ -985,6 +1039,11 @@ int tm_match_batch(tm_index *ix, uint64_t n, const uint8_t *tb, const uint64_t *
     if (out_err && n) memcpy(out_err, ix->pin_out + (n + 1) * 8, n);
     const uint64_t keep = std::min(total, out_vals ? cap : 0);
     if (keep) memcpy(out_vals, ix->pin_vals, keep * 4);
+    if (timing) {
+        tt[nt++] = now_us();
+        fprintf(stderr, "tm_match_batch n=%lu: sync %.1f stage %.1f launch %.1f wait %.1f copy-out %.1f us\n",
+                (unsigned long)n, tt[1] - tt[0], tt[2] - tt[1], tt[3] - tt[2], tt[4] - tt[3], tt[nt - 1] - tt[4]);
+    }
     return (out_vals && total > cap) ? TM_ECAP : TM_OK;
 }
 
@@ -1001,36 +1060,14 @@ int tm_first_batch(tm_index *ix, uint64_t n, const uint8_t *tb, const uint64_t *
     if ((rc = sync_locked(ix, s))) return rc;
     Workspace *ws;
     if ((rc = ensure_ws(ix, n, s, ws))) return rc;
-    const uint64_t b0 = to[0], nbytes = to[n] - b0;
-    const uint64_t in_need = nbytes + 16 + (n + 1) * 8;
-    if (in_need > ix->pin_in_cap) {
-        HIPCHK(ix, hipStreamSynchronize(s));
-        if (ix->pin_in) HIPCHK(ix, hipHostFree(ix->pin_in));
-        ix->pin_in_cap = in_need + in_need / 4;
-        HIPCHK(ix, hipHostMalloc(&ix->pin_in, ix->pin_in_cap, hipHostMallocDefault));
-    }
-    uint64_t *pin_offs = reinterpret_cast<uint64_t *>(ix->pin_in);
-    uint8_t *pin_bytes = ix->pin_in + (n + 1) * 8;
-    for (uint64_t i = 0; i <= n; i++) pin_offs[i] = to[i] - b0;
-    if (nbytes) memcpy(pin_bytes, tb + b0, nbytes);
-    if ((rc = grow_dev(ix, ix->d_topics, ix->d_topics_cap, nbytes + 16))) return rc;
-    if ((rc = grow_dev(ix, ix->d_offs, ix->d_offs_cap, n + 1))) return rc;
-    if ((rc = grow_dev(ix, ix->d_out, ix->d_out_cap, n + 1))) return rc;
-    if ((rc = grow_dev(ix, ix->d_err, ix->d_err_cap, n + 1))) return rc;
-    HIPCHK(ix, hipMemcpyAsync(ix->d_offs, pin_offs, (n + 1) * 8, hipMemcpyHostToDevice, s));
-    if (nbytes) HIPCHK(ix, hipMemcpyAsync(ix->d_topics, pin_bytes, nbytes, hipMemcpyHostToDevice, s));
-    HIPCHK(ix, launch_first(dev_view(ix), *ws, n, ix->d_topics, ix->d_offs, ix->d_out, ix->d_err, s));
-    const uint64_t out_need = n * 5 + 16;
-    if (out_need > ix->pin_out_cap) {
-        HIPCHK(ix, hipStreamSynchronize(s));
-        if (ix->pin_out) HIPCHK(ix, hipHostFree(ix->pin_out));
-        ix->pin_out_cap = out_need + out_need / 4;
-        HIPCHK(ix, hipHostMalloc(&ix->pin_out, ix->pin_out_cap, hipHostMallocDefault));
-    }
-    if (n) {
-        HIPCHK(ix, hipMemcpyAsync(ix->pin_out, ix->d_out, n * 4, hipMemcpyDeviceToHost, s));
-        HIPCHK(ix, hipMemcpyAsync(ix->pin_out + n * 4, ix->d_err, n, hipMemcpyDeviceToHost, s));
-    }
+    const uint8_t *dbytes;
+    const uint64_t *doffs;
+    if ((rc = stage_in(ix, n, tb, to, s, dbytes, doffs))) return rc;
+    const uint64_t rbytes = n * 5;   // first value u32 per topic, then the found flags
+    uint8_t *dres;
+    if ((rc = stage_out(ix, n, rbytes, s, dres))) return rc;
+    HIPCHK(ix, launch_first(dev_view(ix), *ws, n, dbytes, doffs, reinterpret_cast<uint32_t *>(dres), dres + n * 4, s));
+    if ((rc = fetch_out(ix, n, rbytes, s))) return rc;
     HIPCHK(ix, hipStreamSynchronize(s));
     if (n) {
         memcpy(out_value, ix->pin_out, n * 4);

@@ -413,6 +413,21 @@ def test_chains_cut_and_healed_under_deltas(torch_dev):
     assert ix.stats()["n_nodes"] == 1
 
 
+def test_host_batches_zero_copy_and_staged_agree(torch_dev):
+    """Batches up to 65536 topics are staged zero-copy (kernels read and write
+    mapped host memory), larger ones through HBM copies; caller-owned output
+    buffers are reused across batches.  All paths give the oracle's results."""
+    fs = wl.filters(1, 10_000)
+    ix, o = gpu_index(fs), oracle_of(fs)
+    for nt in (1, 4096, 65536, 65537, 150_000):
+        ts = wl.topics(1, 10_000, nt)
+        hit, vals = assert_same(ix, o, ts)
+        bufs = (np.zeros(nt + 1, np.uint64), np.zeros(len(vals) + 7, np.uint32), np.zeros(nt, np.uint8))
+        for _ in range(2):
+            h2, v2, e2 = ix.match_batch(ts.blob, ts.offs, out=bufs)
+            assert np.array_equal(h2, hit) and np.array_equal(v2, vals) and not e2.any()
+
+
 # ------------------------------------------------------------- filter-sharded
 
 def _merge_ref(all_offs, all_vals):
