@@ -571,15 +571,198 @@ __global__ __launch_bounds__(WALK_BLOCK, 8) void k_walk_fast(DevIndex ix, Worksp
     }
 }
 
+// ------------------------------------------------------ wave per topic
+//
+// Small batches (latency).  One wavefront per topic: the lanes split the topic
+// on '/' together (ballot over 64-byte windows), look its levels up in the
+// vocab at once (lane l = level l), then walk the trie breadth first -- the
+// live '+'/literal frontier of a level is one state per lane, compacted into
+// LDS with ballot + prefix count, so every state of a level is one request in
+// the same round trip.  Hits carry their traversal rank as a 64-bit path code
+// (2 bits per level, MSB first: '#'-terminal 0 < '+' subtree 1 < literal
+// subtree 2; at the topic's last level exact terminal 0 < '#'-terminal 1;
+// binary key all ones), and are sorted by it before they are written: the same
+// (cnt, nr, ranges) a lane walk produces, in the same order.  A topic deeper
+// than WV_MAXL levels, whose frontier outgrows the wave, or with more than
+// WV_HITS ranges goes to the lane-walk tail lists instead.
+constexpr int WV_BLOCK = 256;   // 4 waves = 4 topics per block
+constexpr int WV_WAVES = WV_BLOCK / 64;
+constexpr uint32_t WV_MAXL = 31;   // 2 code bits per level + 1 for the exact/'#' digit at level L
+constexpr uint32_t WV_HITS = 64;
+
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ uint32_t lane_rank(uint64_t m) {   // set bits of m below this lane
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+template <int MODE>
+__global__ __launch_bounds__(WV_BLOCK) void k_walk_wave(DevIndex ix, Workspace ws, uint64_t n,
+                                                        const uint8_t *blob, const uint64_t *offs, Outs o) {
+    __shared__ uint32_t s_slash[WV_WAVES][64];
+    __shared__ uint32_t s_node[WV_WAVES][64];
+    __shared__ uint64_t s_code[WV_WAVES][64];
+    __shared__ uint64_t s_hcode[WV_WAVES][WV_HITS];
+    __shared__ uint32_t s_hoff[WV_WAVES][WV_HITS], s_hcnt[WV_WAVES][WV_HITS];
+    const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint64_t t = (uint64_t)blockIdx.x * WV_WAVES + wv;
+    if (t >= n) return;                       // whole wave
+    const uint64_t beg = offs[t], end = offs[t + 1], len = end - beg;
+
+    // ---- topic_words/1: level boundaries by ballot over 64-byte windows
+    uint32_t nsl = 0;
+    for (uint64_t p = 0; p < len; p += 64) {
+        const bool sl = p + lane < len && blob[beg + p + lane] == '/';
+        const uint64_t m = __ballot(sl);
+        if (sl) {
+            const uint32_t k = nsl + lane_rank(m);
+            if (k < 64) s_slash[wv][k] = (uint32_t)(p + lane);
+        }
+        nsl += (uint32_t)__popcll(m);
+    }
+    const uint32_t L = nsl + 1;
+    wave_sync();
+    auto to_lists = [&](uint32_t lists_mid, uint32_t lists_deep) {
+        if (lane == 0) {
+            const uint32_t nl = count_levels(blob, beg, end);
+            list_push(ws, n, nl <= MID_L ? lists_mid : lists_deep, (uint32_t)t);
+        }
+    };
+    if (L > WV_MAXL) { to_lists(L_MID, L_DEEP); return; }
+
+    // ---- this lane's level: bytes, badarg check, vocab lookup
+    const bool mine = lane < L;
+    const uint32_t ws0 = !mine || lane == 0 ? 0 : s_slash[wv][lane - 1] + 1;
+    const uint32_t we0 = !mine ? 0 : lane == L - 1 ? (uint32_t)len : s_slash[wv][lane];
+    const uint32_t wl = we0 - ws0;
+    const uint8_t *wp = blob + beg + ws0;
+    WordAcc w; w.reset(beg + ws0);
+    if (mine) for (uint32_t i = 0; i < wl; i++) w.push(wp[i]);
+    const bool bad = mine && wl == 1 && (w.b0 == '+' || w.b0 == '#');
+    const bool badarg = __ballot(bad) != 0;
+    const bool dollar = __shfl(mine && wl >= 1 && (w.b0 & 0xFFu) == '$' ? 1 : 0, 0, 64) != 0;
+    uint32_t wid = mine && !badarg ? vocab_find(ix, w, blob) : NONE;
+    const bool allf = __ballot(mine && wid == NONE) == 0;
+    uint64_t xh = FNV_OFF;
+    for (uint32_t l = 0; l < L; l++) xh = seq_hash_step(xh, (uint32_t)__shfl((int)wid, (int)l, 64));
+    xh = seq_hash_finish(xh, L);
+    const uint32_t xslot = (uint32_t)xh & ix.xmask;
+    const uint32_t xf = allf && !badarg ? ix.xfp[xslot] : 0;   // in flight during the walk
+
+    // ---- breadth-first walk: one frontier state per lane
+    uint32_t nst = badarg ? 0 : 1, nh = 0;
+    uint32_t node = ROOT;
+    uint64_t code = 0;
+    bool ovf = false;
+    auto add_hits = [&](bool h, uint64_t c, uint32_t off, uint32_t cnt) {
+        const uint64_t m = __ballot(h);
+        if (h) {
+            const uint32_t k = nh + lane_rank(m);
+            if (k < WV_HITS) { s_hcode[wv][k] = c; s_hoff[wv][k] = off; s_hcnt[wv][k] = cnt; }
+        }
+        nh += (uint32_t)__popcll(m);
+    };
+    for (uint32_t l = 0; nst; l++) {
+        const bool act = lane < nst;
+        uint4 n0 = make_uint4(NONE, 0, 0, 0), n1 = make_uint4(0, 0, 0, 0), n2 = n1, n3 = n1;
+        if (act) {
+            const uint4 *np = reinterpret_cast<const uint4 *>(ix.nodes + node);
+            n0 = np[0]; n1 = np[1]; n2 = np[2]; n3 = np[3];
+        }
+        pin(n0); pin(n1); pin(n2); pin(n3);
+        const bool droot = dollar && l == 0;
+        const uint32_t sh = 62 - 2 * l;
+        if (l == L) {
+            add_hits(act && n1.x, code, n0.w, n1.x);                              // exact terminal: digit 0
+            add_hits(act && !droot && n0.z, code | (1ull << sh), n0.y, n0.z);     // '#' terminal: digit 1
+            break;
+        }
+        add_hits(act && !droot && n0.z, code, n0.y, n0.z);                       // '#' terminal: digit 0
+        const uint32_t wl_ = (uint32_t)__shfl((int)wid, (int)l, 64);
+        uint32_t lit = NONE;
+        if (act && wl_ != NONE) {
+            if (n1.y <= KINL) {
+                lit = n2.x == wl_ ? n3.x : n2.y == wl_ ? n3.y : n2.z == wl_ ? n3.z : n2.w == wl_ ? n3.w : NONE;
+            } else {
+                const uint32_t h = child_hash(wl_), b = child_bit(h);
+                const uint32_t mb = b < 32 ? n1.z >> b : n1.w >> (b - 32);
+                if (mb & 1u) lit = ctab_find(ix, n2.x, n2.y, wl_, h);
+            }
+        }
+        const uint32_t plus = act && !droot ? n0.x : NONE;
+        const uint64_t mp = __ballot(plus != NONE), ml = __ballot(lit != NONE);
+        const uint32_t np_ = (uint32_t)__popcll(mp), nn = np_ + (uint32_t)__popcll(ml);
+        if (nn > 64) { ovf = true; break; }
+        wave_sync();   // every lane has read its state before the slots are reused
+        if (plus != NONE) { const uint32_t k = lane_rank(mp); s_node[wv][k] = plus; s_code[wv][k] = code | (1ull << sh); }
+        if (lit != NONE) { const uint32_t k = np_ + lane_rank(ml); s_node[wv][k] = lit; s_code[wv][k] = code | (2ull << sh); }
+        wave_sync();
+        nst = nn;
+        if (lane < nst) { node = s_node[wv][lane]; code = s_code[wv][lane]; }
+    }
+
+    // ---- match_topics/4: the binary key equal to the topic, after every list key
+    if (!ovf && allf && !badarg) {
+        uint32_t slot = xslot, f = xf, xoff = 0, xcnt = 0;
+        const uint32_t fp = exact_fp(xh);
+        for (;;) {
+            if (f == 0) break;
+            if (f == fp) {
+                const uint32_t *e = reinterpret_cast<const uint32_t *>(ix.exact + slot);
+                const bool keyok = e[0] == (uint32_t)xh && e[1] == (uint32_t)(xh >> 32) && e[2] == L;
+                if (keyok) {
+                    const uint32_t ew = !mine ? wid : L <= XINL ? e[6 + lane] : ix.wseq[e[5] + lane];
+                    if (__ballot(mine && ew != wid) == 0) { xoff = e[3]; xcnt = e[4]; break; }
+                }
+            }
+            slot = (slot + 1) & ix.xmask;
+            f = ix.xfp[slot];
+        }
+        add_hits(lane == 0 && xcnt, ~0ull, xoff, xcnt);
+    }
+    if (ovf || nh > WV_HITS) { to_lists(L_MID, L_DEEP); return; }
+
+    // ---- rank the hits by path code (traversal order) and write them out
+    wave_sync();
+    const bool hv = lane < nh;
+    const uint64_t my = hv ? s_hcode[wv][lane] : 0;
+    uint32_t rank = 0, total = 0;
+    for (uint32_t j = 0; j < nh; j++) {
+        rank += s_hcode[wv][j] < my;
+        total += s_hcnt[wv][j];
+    }
+    if (MODE == MODE_COUNT) {
+        if (hv && rank < RCAP) ws.rng[(uint64_t)rank * n + t] = make_uint2(s_hoff[wv][lane], s_hcnt[wv][lane]);
+        if (lane == 0) {
+            ws.cnt[t] = total;
+            ws.nr[t] = nh;
+            o.err[t] = badarg;
+            if (total) atomicAdd((unsigned long long *)&ws.blk[t / TILE], (unsigned long long)total);
+            if (nh > RCAP) list_push(ws, n, L_OVF_MID, (uint32_t)t);
+        }
+    } else {
+        if (hv && rank == 0) o.first_val[t] = ix.vals[s_hoff[wv][lane]];
+        if (lane == 0) {
+            if (!nh) o.first_val[t] = 0;
+            o.first_found[t] = badarg ? 2 : (nh ? 1 : 0);
+        }
+    }
+}
+
 constexpr int MID_BLOCK = 64;
 constexpr int MID_GRID = 256;                         // LDS-frontier blocks of the tail kernels
 constexpr int TAIL_GRID = MID_GRID + DEEP_LANES / 64; // + global-scratch blocks
 
 // last block of a grid (atomic ticket) resets the list counters for the next batch
+// (no fence: a block only READ the list counters, and those loads completed
+// before its ticket was taken, so the reset cannot overtake them)
 __device__ __forceinline__ void reset_lists_if_last(const Workspace &ws) {
     __syncthreads();
     if (threadIdx.x == 0) {
-        __threadfence();
         const uint32_t ticket = atomicAdd(&ws.list_n[L_COUNT], 1u);
         if (ticket == gridDim.x - 1) {
             for (int k = 0; k < L_COUNT; k++) atomicExch(&ws.list_n[k], 0u);
@@ -797,6 +980,10 @@ __global__ __launch_bounds__(256) void k_merge_shards(uint32_t world, uint64_t n
 
 static inline uint32_t blocks_for(uint64_t n, uint32_t per) { return (uint32_t)((n + per - 1) / per); }
 
+#ifndef WAVE_TOPICS
+#define WAVE_TOPICS 4096   // batches of up to this many topics take the wave-per-topic walk (latency)
+#endif
+
 hipError_t launch_match_phase1(const DevIndex &ix, const Workspace &ws, uint64_t n, const uint8_t *bytes,
                                const uint64_t *offs, uint64_t *hit_offs, uint8_t *err, hipStream_t s,
                                hipEvent_t ev_walk0, hipEvent_t ev_walk1) {
@@ -804,8 +991,15 @@ hipError_t launch_match_phase1(const DevIndex &ix, const Workspace &ws, uint64_t
     Outs o{err, nullptr, nullptr};
     const uint32_t nb = blocks_for(n, TILE);
     if (n) {
+        const bool wave = n <= WAVE_TOPICS;
+        // the wave walk adds its topics' hits into the tile totals
+        if (wave && (e = hipMemsetAsync(ws.blk, 0, (uint64_t)nb * 8, s)) != hipSuccess) return e;
         if (ev_walk0 && (e = hipEventRecord(ev_walk0, s)) != hipSuccess) return e;
-        hipLaunchKernelGGL(k_walk_fast<MODE_COUNT>, dim3(nb), dim3(WALK_BLOCK), 0, s, ix, ws, n, bytes, offs, o);
+        if (wave)
+            hipLaunchKernelGGL(k_walk_wave<MODE_COUNT>, dim3(blocks_for(n, WV_WAVES)), dim3(WV_BLOCK), 0, s, ix, ws, n,
+                               bytes, offs, o);
+        else
+            hipLaunchKernelGGL(k_walk_fast<MODE_COUNT>, dim3(nb), dim3(WALK_BLOCK), 0, s, ix, ws, n, bytes, offs, o);
         if (ev_walk1 && (e = hipEventRecord(ev_walk1, s)) != hipSuccess) return e;
         hipLaunchKernelGGL(k_walk_tail<MODE_COUNT>, dim3(TAIL_GRID), dim3(MID_BLOCK), 0, s, ix, ws, n, bytes, offs, o);
     }
@@ -826,8 +1020,12 @@ hipError_t launch_first(const DevIndex &ix, const Workspace &ws, uint64_t n, con
                         const uint64_t *offs, uint32_t *out_value, uint8_t *out_found, hipStream_t s) {
     if (!n) return hipSuccess;
     Outs o{nullptr, out_value, out_found};
-    hipLaunchKernelGGL(k_walk_fast<MODE_FIRST>, dim3(blocks_for(n, WALK_BLOCK)), dim3(WALK_BLOCK), 0, s,
-                       ix, ws, n, bytes, offs, o);
+    if (n <= WAVE_TOPICS)
+        hipLaunchKernelGGL(k_walk_wave<MODE_FIRST>, dim3(blocks_for(n, WV_WAVES)), dim3(WV_BLOCK), 0, s, ix, ws, n,
+                           bytes, offs, o);
+    else
+        hipLaunchKernelGGL(k_walk_fast<MODE_FIRST>, dim3(blocks_for(n, WALK_BLOCK)), dim3(WALK_BLOCK), 0, s,
+                           ix, ws, n, bytes, offs, o);
     hipLaunchKernelGGL(k_walk_tail<MODE_FIRST>, dim3(TAIL_GRID), dim3(MID_BLOCK), 0, s, ix, ws, n, bytes, offs, o);
     return hipGetLastError();
 }

@@ -428,6 +428,40 @@ def test_host_batches_zero_copy_and_staged_agree(torch_dev):
             assert np.array_equal(h2, hit) and np.array_equal(v2, vals) and not e2.any()
 
 
+def test_wave_walk_limits_fall_back_exactly(torch_dev):
+    """Batches of <= 4096 topics take the wave-per-topic walk; its limits (a
+    frontier wider than the wave, more than 64 hit ranges, more than 31 levels)
+    hand the topic to the lane walk.  Small (wave) and large (lane) batches of
+    the same topics must both equal the oracle."""
+    import itertools
+    words = [b"a", b"b", b"c", b"d", b"e", b"f", b"g"]
+    fl = []
+    for k in range(1, 8):   # every '+' pattern of every prefix: frontier 2^k at level k
+        for pat in itertools.product([0, 1], repeat=k):
+            ws_ = [b"+" if p else w for p, w in zip(pat, words)]
+            fl.append(b"/".join(ws_))
+            fl.append(b"/".join(ws_) + b"/#")
+    deep = b"/".join(b"l%d" % i for i in range(40))
+    for L in (30, 31, 32, 33, 40):
+        fl.append(b"/".join(deep.split(b"/")[:L]))
+        fl.append(b"/".join(deep.split(b"/")[:L - 1] + [b"+"]))
+        fl.append(b"/".join(deep.split(b"/")[:L - 2] + [b"#"]))
+    fs = items_of(fl)
+    ix, o = gpu_index(fs), oracle_of(fs)
+    tl = [b"/".join(words[:k]) for k in range(1, 8)] + [b"a/b/c/x/e/f/g", b"x/b/c/d/e/f/g/h"]
+    tl += [b"/".join(deep.split(b"/")[:L]) for L in range(28, 41)]
+    small = items_of(tl)
+    assert_same(ix, o, small)                                  # wave walk (+ fallbacks)
+    big = items_of(tl * 400)                                   # > 4096 topics: lane walk
+    assert_same(ix, o, big)
+    first, found = ix.first_batch(small.blob, small.offs)
+    cnt, _, ohit, ovals = o.match_batch(small.blob, small.offs)
+    for i in range(len(small)):
+        assert bool(found[i]) == (cnt[i] > 0)
+        if cnt[i] > 0:
+            assert first[i] == ovals[ohit[i]]
+
+
 # ------------------------------------------------------------- filter-sharded
 
 def _merge_ref(all_offs, all_vals):
