@@ -360,8 +360,8 @@ uint32_t child_find(tm_index *ix, uint32_t node, uint32_t wid) {
 }
 
 void set_bloom(Node &n, uint32_t wid) {
-    uint32_t b = child_bit(child_hash(wid));
-    if (b < 32) n.mask_lo |= 1u << b; else n.mask_hi |= 1u << (b - 32);
+    const uint32_t b = child_bit(child_hash(wid));
+    bloom_word(n, b >> 5) |= 1u << (b & 31);
 }
 
 // move a node's children into a private table of `cap` slots (cap = pow2)
@@ -376,9 +376,8 @@ void to_table(tm_index *ix, uint32_t node, uint32_t cap) {
     }
     uint32_t off = ctab_alloc(ix, cap);
     Node &m = ix->nodes.h[node];
-    m.mask_lo = m.mask_hi = 0;
+    for (uint32_t j = 0; j < 8; j++) bloom_word(m, j) = 0;
     for (auto &c : kids) { ctab_put(ix, off, cap - 1, c.wid, c.child); set_bloom(m, c.wid); }
-    for (uint32_t k = 0; k < KINL; k++) { m.kw[k] = NONE; m.kc[k] = NONE; }
     m.kw[0] = off; m.kw[1] = cap - 1;
 }
 

@@ -32,6 +32,14 @@ namespace tmx {
 
 __device__ __forceinline__ uint4 ld4(const void *p) { return *reinterpret_cast<const uint4 *>(p); }
 
+// bit b (0..255) of a table-mode node's Bloom: words mask_lo, mask_hi, kw[2..3], kc[0..3]
+__device__ __forceinline__ uint32_t bloom_bit(const uint4 &n1, const uint4 &n2, const uint4 &n3, uint32_t b) {
+    const uint32_t j = b >> 5;
+    const uint32_t w = j == 0 ? n1.z : j == 1 ? n1.w : j == 2 ? n2.z : j == 3 ? n2.w
+                     : j == 4 ? n3.x : j == 5 ? n3.y : j == 6 ? n3.z : n3.w;
+    return (w >> (b & 31)) & 1u;
+}
+
 // Empty asm "uses": pin a loaded value at this point on every path.  Without
 // them the compiler sinks loads into the branches that read each field (one
 // dependent round trip per field: the exact entry took three, a child slot
@@ -352,8 +360,8 @@ __device__ bool dfs(const DevIndex &ix, uint32_t L, bool dollar, S &st, EM &em) 
                 if (n1.y <= KINL) {
                     lit = inl;
                 } else {
-                    const uint32_t h = child_hash(w), b = child_bit(h);
-                    const uint32_t m = b < 32 ? n1.z >> b : n1.w >> (b - 32);
+                    const uint32_t h = child_hash(w);
+                    const uint32_t m = bloom_bit(n1, n2, n3, child_bit(h));
                     if (m & 1u) lit = ctab_find(ix, n2.x, n2.y, w, h);
 #ifdef TM_STUDY
                     if constexpr (S::deferred) {
@@ -688,8 +696,8 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_wave(DevIndex ix, Workspace w
             if (n1.y <= KINL) {
                 lit = n2.x == wl_ ? n3.x : n2.y == wl_ ? n3.y : n2.z == wl_ ? n3.z : n2.w == wl_ ? n3.w : NONE;
             } else {
-                const uint32_t h = child_hash(wl_), b = child_bit(h);
-                const uint32_t mb = b < 32 ? n1.z >> b : n1.w >> (b - 32);
+                const uint32_t h = child_hash(wl_);
+                const uint32_t mb = bloom_bit(n1, n2, n3, child_bit(h));
                 if (mb & 1u) lit = ctab_find(ix, n2.x, n2.y, wl_, h);
             }
         }
