@@ -590,13 +590,12 @@ __global__ __launch_bounds__(WALK_BLOCK, 8) void k_walk_fast(DevIndex ix, Worksp
 // (2 bits per level, MSB first: '#'-terminal 0 < '+' subtree 1 < literal
 // subtree 2; at the topic's last level exact terminal 0 < '#'-terminal 1;
 // binary key all ones), and are sorted by it before they are written: the same
-// (cnt, nr, ranges) a lane walk produces, in the same order.  A topic deeper
-// than WV_MAXL levels, whose frontier outgrows the wave, or with more than
-// WV_HITS ranges goes to the lane-walk tail lists instead.
-constexpr int WV_BLOCK = 256;   // 4 waves = 4 topics per block
+// (cnt, nr, ranges) a lane walk produces, in the same order.  The "wave" is a
+// group of WAVE_W lanes (16: four topics per wavefront); a topic deeper than
+// the group, whose frontier outgrows it, or with more hit ranges than lanes
+// goes to the lane-walk tail lists instead.
+constexpr int WV_BLOCK = 256;   // 4 waves per block
 constexpr int WV_WAVES = WV_BLOCK / 64;
-constexpr uint32_t WV_MAXL = 31;   // 2 code bits per level + 1 for the exact/'#' digit at level L
-constexpr uint32_t WV_HITS = 64;
 
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -604,59 +603,81 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-__device__ __forceinline__ uint32_t lane_rank(uint64_t m) {   // set bits of m below this lane
-    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-}
+// A group of W lanes (W = 16, 32 or 64) of a wavefront working on one topic:
+// ballots, ranks and broadcasts restricted to the group.
+template <int W>
+struct Group {
+    uint32_t g, gl;   // group within the wave, lane within the group
+    __device__ __forceinline__ Group() : g((threadIdx.x & 63) / W), gl((threadIdx.x & 63) % W) {}
+    __device__ __forceinline__ uint64_t ballot(bool p) const {
+        const uint64_t m = __ballot(p);
+        return W == 64 ? m : (m >> (g * W)) & ((1ull << (W & 63)) - 1);
+    }
+    __device__ __forceinline__ uint32_t rank(uint64_t gm) const {   // set bits of gm below this lane
+        return (uint32_t)__popcll(gm & ((1ull << gl) - 1));
+    }
+    __device__ __forceinline__ uint32_t bcast(uint32_t v, uint32_t src) const {
+        return (uint32_t)__shfl((int)v, (int)src, W);
+    }
+};
 
-template <int MODE>
+// W lanes per topic: W <= 31 levels (one level per lane; 2 code bits per level
+// plus the digit at level L fit 64 bits up to 31), at most W frontier states
+// and W hit ranges; anything larger goes to the lane walk's lists.
+template <int MODE, int W>
 __global__ __launch_bounds__(WV_BLOCK) void k_walk_wave(DevIndex ix, Workspace ws, uint64_t n,
                                                         const uint8_t *blob, const uint64_t *offs, Outs o) {
+    constexpr uint32_t G = 64 / W;                        // topics per wave
+    constexpr uint32_t MAXL = W < 31 ? W : 31;
     __shared__ uint32_t s_slash[WV_WAVES][64];
     __shared__ uint32_t s_node[WV_WAVES][64];
     __shared__ uint64_t s_code[WV_WAVES][64];
-    __shared__ uint64_t s_hcode[WV_WAVES][WV_HITS];
-    __shared__ uint32_t s_hoff[WV_WAVES][WV_HITS], s_hcnt[WV_WAVES][WV_HITS];
-    const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const uint64_t t = (uint64_t)blockIdx.x * WV_WAVES + wv;
-    if (t >= n) return;                       // whole wave
+    __shared__ uint64_t s_hcode[WV_WAVES][64];
+    __shared__ uint32_t s_hoff[WV_WAVES][64], s_hcnt[WV_WAVES][64];
+    const Group<W> grp;
+    const uint32_t wv = threadIdx.x >> 6, gl = grp.gl, base = grp.g * W;
+    const uint64_t t = ((uint64_t)blockIdx.x * WV_WAVES + wv) * G + grp.g;
+    if (t >= n) return;                       // the whole group
+    uint32_t *sl_ = s_slash[wv] + base, *sn_ = s_node[wv] + base, *hoff = s_hoff[wv] + base, *hcnt = s_hcnt[wv] + base;
+    uint64_t *sc_ = s_code[wv] + base, *hcode = s_hcode[wv] + base;
     const uint64_t beg = offs[t], end = offs[t + 1], len = end - beg;
 
-    // ---- topic_words/1: level boundaries by ballot over 64-byte windows
+    // ---- topic_words/1: level boundaries by ballot over W-byte windows
     uint32_t nsl = 0;
-    for (uint64_t p = 0; p < len; p += 64) {
-        const bool sl = p + lane < len && blob[beg + p + lane] == '/';
-        const uint64_t m = __ballot(sl);
+    for (uint64_t p = 0; p < len; p += W) {
+        const bool sl = p + gl < len && blob[beg + p + gl] == '/';
+        const uint64_t m = grp.ballot(sl);
         if (sl) {
-            const uint32_t k = nsl + lane_rank(m);
-            if (k < 64) s_slash[wv][k] = (uint32_t)(p + lane);
+            const uint32_t k = nsl + grp.rank(m);
+            if (k < W) sl_[k] = (uint32_t)(p + gl);
         }
         nsl += (uint32_t)__popcll(m);
     }
     const uint32_t L = nsl + 1;
     wave_sync();
-    auto to_lists = [&](uint32_t lists_mid, uint32_t lists_deep) {
-        if (lane == 0) {
+    auto to_lists = [&]() {
+        if (gl == 0) {
             const uint32_t nl = count_levels(blob, beg, end);
-            list_push(ws, n, nl <= MID_L ? lists_mid : lists_deep, (uint32_t)t);
+            list_push(ws, n, nl <= MID_L ? L_MID : L_DEEP, (uint32_t)t);
         }
     };
-    if (L > WV_MAXL) { to_lists(L_MID, L_DEEP); return; }
+    if (L > MAXL) { to_lists(); return; }
 
     // ---- this lane's level: bytes, badarg check, vocab lookup
-    const bool mine = lane < L;
-    const uint32_t ws0 = !mine || lane == 0 ? 0 : s_slash[wv][lane - 1] + 1;
-    const uint32_t we0 = !mine ? 0 : lane == L - 1 ? (uint32_t)len : s_slash[wv][lane];
+    const bool mine = gl < L;
+    const uint32_t ws0 = !mine || gl == 0 ? 0 : sl_[gl - 1] + 1;
+    const uint32_t we0 = !mine ? 0 : gl == L - 1 ? (uint32_t)len : sl_[gl];
     const uint32_t wl = we0 - ws0;
     const uint8_t *wp = blob + beg + ws0;
     WordAcc w; w.reset(beg + ws0);
     if (mine) for (uint32_t i = 0; i < wl; i++) w.push(wp[i]);
     const bool bad = mine && wl == 1 && (w.b0 == '+' || w.b0 == '#');
-    const bool badarg = __ballot(bad) != 0;
-    const bool dollar = __shfl(mine && wl >= 1 && (w.b0 & 0xFFu) == '$' ? 1 : 0, 0, 64) != 0;
+    const bool badarg = grp.ballot(bad) != 0;
+    const bool dollar = grp.bcast(mine && wl >= 1 && (w.b0 & 0xFFu) == '$' ? 1u : 0u, 0) != 0;
     uint32_t wid = mine && !badarg ? vocab_find(ix, w, blob) : NONE;
-    const bool allf = __ballot(mine && wid == NONE) == 0;
+    const bool allf = grp.ballot(mine && wid == NONE) == 0;
     uint64_t xh = FNV_OFF;
-    for (uint32_t l = 0; l < L; l++) xh = seq_hash_step(xh, (uint32_t)__shfl((int)wid, (int)l, 64));
+    for (uint32_t l = 0; l < L; l++) xh = seq_hash_step(xh, grp.bcast(wid, l));
     xh = seq_hash_finish(xh, L);
     const uint32_t xslot = (uint32_t)xh & ix.xmask;
     const uint32_t xf = allf && !badarg ? ix.xfp[xslot] : 0;   // in flight during the walk
@@ -667,15 +688,15 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_wave(DevIndex ix, Workspace w
     uint64_t code = 0;
     bool ovf = false;
     auto add_hits = [&](bool h, uint64_t c, uint32_t off, uint32_t cnt) {
-        const uint64_t m = __ballot(h);
+        const uint64_t m = grp.ballot(h);
         if (h) {
-            const uint32_t k = nh + lane_rank(m);
-            if (k < WV_HITS) { s_hcode[wv][k] = c; s_hoff[wv][k] = off; s_hcnt[wv][k] = cnt; }
+            const uint32_t k = nh + grp.rank(m);
+            if (k < W) { hcode[k] = c; hoff[k] = off; hcnt[k] = cnt; }
         }
         nh += (uint32_t)__popcll(m);
     };
     for (uint32_t l = 0; nst; l++) {
-        const bool act = lane < nst;
+        const bool act = gl < nst;
         uint4 n0 = make_uint4(NONE, 0, 0, 0), n1 = make_uint4(0, 0, 0, 0), n2 = n1, n3 = n1;
         if (act) {
             const uint4 *np = reinterpret_cast<const uint4 *>(ix.nodes + node);
@@ -690,7 +711,7 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_wave(DevIndex ix, Workspace w
             break;
         }
         add_hits(act && !droot && n0.z, code, n0.y, n0.z);                       // '#' terminal: digit 0
-        const uint32_t wl_ = (uint32_t)__shfl((int)wid, (int)l, 64);
+        const uint32_t wl_ = grp.bcast(wid, l);
         uint32_t lit = NONE;
         if (act && wl_ != NONE) {
             if (n1.y <= KINL) {
@@ -702,15 +723,15 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_wave(DevIndex ix, Workspace w
             }
         }
         const uint32_t plus = act && !droot ? n0.x : NONE;
-        const uint64_t mp = __ballot(plus != NONE), ml = __ballot(lit != NONE);
+        const uint64_t mp = grp.ballot(plus != NONE), ml = grp.ballot(lit != NONE);
         const uint32_t np_ = (uint32_t)__popcll(mp), nn = np_ + (uint32_t)__popcll(ml);
-        if (nn > 64) { ovf = true; break; }
+        if (nn > W) { ovf = true; break; }
         wave_sync();   // every lane has read its state before the slots are reused
-        if (plus != NONE) { const uint32_t k = lane_rank(mp); s_node[wv][k] = plus; s_code[wv][k] = code | (1ull << sh); }
-        if (lit != NONE) { const uint32_t k = np_ + lane_rank(ml); s_node[wv][k] = lit; s_code[wv][k] = code | (2ull << sh); }
+        if (plus != NONE) { const uint32_t k = grp.rank(mp); sn_[k] = plus; sc_[k] = code | (1ull << sh); }
+        if (lit != NONE) { const uint32_t k = np_ + grp.rank(ml); sn_[k] = lit; sc_[k] = code | (2ull << sh); }
         wave_sync();
         nst = nn;
-        if (lane < nst) { node = s_node[wv][lane]; code = s_code[wv][lane]; }
+        if (gl < nst) { node = sn_[gl]; code = sc_[gl]; }
     }
 
     // ---- match_topics/4: the binary key equal to the topic, after every list key
@@ -723,29 +744,29 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_wave(DevIndex ix, Workspace w
                 const uint32_t *e = reinterpret_cast<const uint32_t *>(ix.exact + slot);
                 const bool keyok = e[0] == (uint32_t)xh && e[1] == (uint32_t)(xh >> 32) && e[2] == L;
                 if (keyok) {
-                    const uint32_t ew = !mine ? wid : L <= XINL ? e[6 + lane] : ix.wseq[e[5] + lane];
-                    if (__ballot(mine && ew != wid) == 0) { xoff = e[3]; xcnt = e[4]; break; }
+                    const uint32_t ew = !mine ? wid : L <= XINL ? e[6 + gl] : ix.wseq[e[5] + gl];
+                    if (grp.ballot(mine && ew != wid) == 0) { xoff = e[3]; xcnt = e[4]; break; }
                 }
             }
             slot = (slot + 1) & ix.xmask;
             f = ix.xfp[slot];
         }
-        add_hits(lane == 0 && xcnt, ~0ull, xoff, xcnt);
+        add_hits(gl == 0 && xcnt, ~0ull, xoff, xcnt);
     }
-    if (ovf || nh > WV_HITS) { to_lists(L_MID, L_DEEP); return; }
+    if (ovf || nh > W) { to_lists(); return; }
 
     // ---- rank the hits by path code (traversal order) and write them out
     wave_sync();
-    const bool hv = lane < nh;
-    const uint64_t my = hv ? s_hcode[wv][lane] : 0;
+    const bool hv = gl < nh;
+    const uint64_t my = hv ? hcode[gl] : 0;
     uint32_t rank = 0, total = 0;
     for (uint32_t j = 0; j < nh; j++) {
-        rank += s_hcode[wv][j] < my;
-        total += s_hcnt[wv][j];
+        rank += hcode[j] < my;
+        total += hcnt[j];
     }
     if (MODE == MODE_COUNT) {
-        if (hv && rank < RCAP) ws.rng[(uint64_t)rank * n + t] = make_uint2(s_hoff[wv][lane], s_hcnt[wv][lane]);
-        if (lane == 0) {
+        if (hv && rank < RCAP) ws.rng[(uint64_t)rank * n + t] = make_uint2(hoff[gl], hcnt[gl]);
+        if (gl == 0) {
             ws.cnt[t] = total;
             ws.nr[t] = nh;
             o.err[t] = badarg;
@@ -753,8 +774,8 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_wave(DevIndex ix, Workspace w
             if (nh > RCAP) list_push(ws, n, L_OVF_MID, (uint32_t)t);
         }
     } else {
-        if (hv && rank == 0) o.first_val[t] = ix.vals[s_hoff[wv][lane]];
-        if (lane == 0) {
+        if (hv && rank == 0) o.first_val[t] = ix.vals[hoff[gl]];
+        if (gl == 0) {
             if (!nh) o.first_val[t] = 0;
             o.first_found[t] = badarg ? 2 : (nh ? 1 : 0);
         }
@@ -989,8 +1010,12 @@ __global__ __launch_bounds__(256) void k_merge_shards(uint32_t world, uint64_t n
 static inline uint32_t blocks_for(uint64_t n, uint32_t per) { return (uint32_t)((n + per - 1) / per); }
 
 #ifndef WAVE_TOPICS
-#define WAVE_TOPICS 4096   // batches of up to this many topics take the wave-per-topic walk (latency)
+#define WAVE_TOPICS 8192   // batches of up to this many topics take the wave-per-topic walk (latency)
 #endif
+#ifndef WAVE_W
+#define WAVE_W 16          // lanes per topic in the wave walk
+#endif
+constexpr uint32_t WV_TOPICS_PER_BLOCK = WV_WAVES * (64 / WAVE_W);
 
 hipError_t launch_match_phase1(const DevIndex &ix, const Workspace &ws, uint64_t n, const uint8_t *bytes,
                                const uint64_t *offs, uint64_t *hit_offs, uint8_t *err, hipStream_t s,
@@ -1004,8 +1029,8 @@ hipError_t launch_match_phase1(const DevIndex &ix, const Workspace &ws, uint64_t
         if (wave && (e = hipMemsetAsync(ws.blk, 0, (uint64_t)nb * 8, s)) != hipSuccess) return e;
         if (ev_walk0 && (e = hipEventRecord(ev_walk0, s)) != hipSuccess) return e;
         if (wave)
-            hipLaunchKernelGGL(k_walk_wave<MODE_COUNT>, dim3(blocks_for(n, WV_WAVES)), dim3(WV_BLOCK), 0, s, ix, ws, n,
-                               bytes, offs, o);
+            hipLaunchKernelGGL((k_walk_wave<MODE_COUNT, WAVE_W>), dim3(blocks_for(n, WV_TOPICS_PER_BLOCK)),
+                               dim3(WV_BLOCK), 0, s, ix, ws, n, bytes, offs, o);
         else
             hipLaunchKernelGGL(k_walk_fast<MODE_COUNT>, dim3(nb), dim3(WALK_BLOCK), 0, s, ix, ws, n, bytes, offs, o);
         if (ev_walk1 && (e = hipEventRecord(ev_walk1, s)) != hipSuccess) return e;
@@ -1029,8 +1054,8 @@ hipError_t launch_first(const DevIndex &ix, const Workspace &ws, uint64_t n, con
     if (!n) return hipSuccess;
     Outs o{nullptr, out_value, out_found};
     if (n <= WAVE_TOPICS)
-        hipLaunchKernelGGL(k_walk_wave<MODE_FIRST>, dim3(blocks_for(n, WV_WAVES)), dim3(WV_BLOCK), 0, s, ix, ws, n,
-                           bytes, offs, o);
+        hipLaunchKernelGGL((k_walk_wave<MODE_FIRST, WAVE_W>), dim3(blocks_for(n, WV_TOPICS_PER_BLOCK)),
+                           dim3(WV_BLOCK), 0, s, ix, ws, n, bytes, offs, o);
     else
         hipLaunchKernelGGL(k_walk_fast<MODE_FIRST>, dim3(blocks_for(n, WALK_BLOCK)), dim3(WALK_BLOCK), 0, s,
                            ix, ws, n, bytes, offs, o);

@@ -429,9 +429,9 @@ def test_host_batches_zero_copy_and_staged_agree(torch_dev):
 
 
 def test_wave_walk_limits_fall_back_exactly(torch_dev):
-    """Batches of <= 4096 topics take the wave-per-topic walk; its limits (a
-    frontier wider than the wave, more than 64 hit ranges, more than 31 levels)
-    hand the topic to the lane walk.  Small (wave) and large (lane) batches of
+    """Batches of <= 8192 topics take the wave-per-topic walk (16 lanes per
+    topic); its limits (a frontier wider than the group, more hit ranges than
+    lanes, more levels than lanes) hand the topic to the lane walk.  Small (wave) and large (lane) batches of
     the same topics must both equal the oracle."""
     import itertools
     words = [b"a", b"b", b"c", b"d", b"e", b"f", b"g"]
@@ -452,7 +452,7 @@ def test_wave_walk_limits_fall_back_exactly(torch_dev):
     tl += [b"/".join(deep.split(b"/")[:L]) for L in range(28, 41)]
     small = items_of(tl)
     assert_same(ix, o, small)                                  # wave walk (+ fallbacks)
-    big = items_of(tl * 400)                                   # > 4096 topics: lane walk
+    big = items_of(tl * 400)                                   # > 8192 topics: lane walk
     assert_same(ix, o, big)
     first, found = ix.first_batch(small.blob, small.offs)
     cnt, _, ohit, ovals = o.match_batch(small.blob, small.offs)
