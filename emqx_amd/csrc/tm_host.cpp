@@ -64,6 +64,7 @@ struct Mirror {
 
 struct NodeAux {
     uint32_t parent = NONE, wid = NONE, hash_cap = 0, exact_cap = 0;
+    uint32_t hash_roff = 0, exact_roff = 0;   // the runs' offsets in vals (the line may hold an inline value)
     uint8_t is_plus = 0;
 };
 
@@ -82,7 +83,7 @@ struct tm_index {
     Mirror<Node> nodes; std::vector<NodeAux> aux; std::vector<uint32_t> free_nodes; uint64_t live_nodes = 0;
     Mirror<CSlot> ctab; std::vector<uint32_t> free_ctab[33]; uint64_t nlinks = 0, ntables = 0;
     Mirror<uint32_t> vals; std::vector<uint32_t> free_blocks[33];
-    Mirror<ExactEntry> exact; std::vector<uint32_t> xcap; uint64_t xcount = 0;
+    Mirror<ExactEntry> exact; std::vector<uint32_t> xcap, xroff; uint64_t xcount = 0;
     Mirror<uint16_t> xfp;   // exact-table fingerprints, slot for slot (0 = empty)
     Mirror<uint32_t> wseq;
 
@@ -332,6 +333,17 @@ bool run_erase(tm_index *ix, uint32_t &off, uint32_t &cnt, uint32_t &cap, uint32
     return true;
 }
 
+// Insert or erase v in a run kept at host offset roff (capacity cap), then
+// write the run's device encoding into (doff, dcnt): a single value inline.
+bool run_op(tm_index *ix, bool ins, uint32_t &roff, uint32_t &cap, uint32_t &doff, uint32_t &dcnt, uint32_t v) {
+    uint32_t off = roff, cnt = dcnt & RUN_CNT;
+    const bool changed = ins ? run_insert(ix, off, cnt, cap, v) : run_erase(ix, off, cnt, cap, v);
+    roff = off;
+    if (cnt == 1) { doff = ix->vals.h[off]; dcnt = 1u | RUN_INLINE; }
+    else { doff = off; dcnt = cnt; }
+    return changed;
+}
+
 // ------------------------------------------------------------------ nodes
 
 uint32_t node_new(tm_index *ix, uint32_t parent, uint32_t wid, bool is_plus) {
@@ -464,17 +476,18 @@ void exact_grow(tm_index *ix, uint64_t need) {
     if (need * 2 <= ix->exact.h.size()) return;
     const uint32_t ncap = pow2_at_least(need * 2);
     std::vector<ExactEntry> nt(ncap, empty_exact());
-    std::vector<uint32_t> nc(ncap, 0);
+    std::vector<uint32_t> nc(ncap, 0), nr(ncap, 0);
     std::vector<uint16_t> nf(ncap, 0);
     const uint32_t mask = ncap - 1;
     for (size_t i = 0; i < ix->exact.h.size(); i++) {
         const ExactEntry &e = ix->exact.h[i];
         if (e.nlev == NONE) continue;
         for (uint32_t s = e.h_lo & mask;; s = (s + 1) & mask)
-            if (nt[s].nlev == NONE) { nt[s] = e; nc[s] = ix->xcap[i]; nf[s] = ix->xfp.h[i]; break; }
+            if (nt[s].nlev == NONE) { nt[s] = e; nc[s] = ix->xcap[i]; nr[s] = ix->xroff[i]; nf[s] = ix->xfp.h[i]; break; }
     }
     ix->exact.h.swap(nt);
     ix->xcap.swap(nc);
+    ix->xroff.swap(nr);
     ix->xfp.h.swap(nf);
     ix->exact.dirty.set_all();
     ix->xfp.dirty.set_all();
@@ -487,13 +500,14 @@ void exact_erase_slot(tm_index *ix, uint32_t i) {
         uint32_t k = t[j].h_lo & mask;
         bool stays = (i <= j) ? (i < k && k <= j) : (i < k || k <= j);
         if (!stays) {
-            t[i] = t[j]; ix->xcap[i] = ix->xcap[j]; ix->xfp.h[i] = ix->xfp.h[j];
+            t[i] = t[j]; ix->xcap[i] = ix->xcap[j]; ix->xroff[i] = ix->xroff[j]; ix->xfp.h[i] = ix->xfp.h[j];
             ix->exact.touch(i); ix->xfp.touch(i);
             i = j;
         }
     }
     t[i] = empty_exact();
     ix->xcap[i] = 0;
+    ix->xroff[i] = 0;
     ix->xfp.h[i] = 0;
     ix->exact.touch(i);
     ix->xfp.touch(i);
@@ -565,15 +579,16 @@ void key_op(tm_index *ix, bool ins, const uint8_t *f, uint32_t len, uint32_t v, 
             for (s = (uint32_t)h & mask; ix->exact.h[s].nlev != NONE; s = (s + 1) & mask) {}
             ix->exact.h[s] = e;
             ix->xcap[s] = 0;
+            ix->xroff[s] = 0;
             ix->xfp.h[s] = exact_fp(h);
             ix->xfp.touch(s);
             ix->xcount++;
         }
         ExactEntry &e = ix->exact.h[s];
-        if (ins) { if (run_insert(ix, e.val_off, e.val_cnt, ix->xcap[s], v)) ix->n_exact++; }
-        else if (run_erase(ix, e.val_off, e.val_cnt, ix->xcap[s], v)) {
+        if (ins) { if (run_op(ix, true, ix->xroff[s], ix->xcap[s], e.val_off, e.val_cnt, v)) ix->n_exact++; }
+        else if (run_op(ix, false, ix->xroff[s], ix->xcap[s], e.val_off, e.val_cnt, v)) {
             ix->n_exact--;
-            if (!e.val_cnt) { exact_erase_slot(ix, s); return; }
+            if (!(e.val_cnt & RUN_CNT)) { exact_erase_slot(ix, s); return; }
         }
         ix->exact.touch(s);
         return;
@@ -614,10 +629,8 @@ void key_op(tm_index *ix, bool ins, const uint8_t *f, uint32_t len, uint32_t v, 
     Node &nd = ix->nodes.h[node];
     NodeAux &a = ix->aux[node];
     bool changed;
-    if (ins) changed = hash_term ? run_insert(ix, nd.hash_off, nd.hash_cnt, a.hash_cap, v)
-                                 : run_insert(ix, nd.exact_off, nd.exact_cnt, a.exact_cap, v);
-    else changed = hash_term ? run_erase(ix, nd.hash_off, nd.hash_cnt, a.hash_cap, v)
-                             : run_erase(ix, nd.exact_off, nd.exact_cnt, a.exact_cap, v);
+    changed = hash_term ? run_op(ix, ins, a.hash_roff, a.hash_cap, nd.hash_off, nd.hash_cnt, v)
+                        : run_op(ix, ins, a.exact_roff, a.exact_cap, nd.exact_off, nd.exact_cnt, v);
     if (!changed) return;
     ix->nodes.touch(node);
     if (ins) ix->n_wild++;
@@ -788,6 +801,7 @@ void init_tables(tm_index *ix, uint64_t hint) {
     ix->exact.h.assign(1024, empty_exact());
     ix->xfp.h.assign(1024, 0);
     ix->xcap.assign(ix->exact.h.size(), 0);
+    ix->xroff.assign(ix->exact.h.size(), 0);
     ix->nodes.h.reserve(hint / 2 + 1);
     ix->aux.reserve(hint / 2 + 1);
     node_new(ix, NONE, NONE, false);   // ROOT

@@ -388,12 +388,12 @@ __device__ bool dfs(const DevIndex &ix, uint32_t L, bool dollar, S &st, EM &em) 
 struct RangeEmit {          // phase 1: count hits, keep up to RCAP value ranges in registers
     uint2 r[RCAP];
     uint32_t cnt, nr;
-    __device__ __forceinline__ bool operator()(uint32_t off, uint32_t n) {
+    __device__ __forceinline__ bool operator()(uint32_t off, uint32_t n) {   // n: a run's device count
         if (n) {
 #pragma unroll
             for (uint32_t i = 0; i < RCAP; i++)
                 if (nr == i) r[i] = make_uint2(off, n);
-            nr++; cnt += n;
+            nr++; cnt += n & RUN_CNT;
         }
         return true;
     }
@@ -411,8 +411,9 @@ struct DirectEmit {         // re-walk: write values straight into the CSR
     uint32_t *out;
     uint64_t pos, cap;
     __device__ __forceinline__ bool operator()(uint32_t off, uint32_t n) {
-        for (uint32_t i = 0; i < n; i++, pos++)
-            if (pos < cap) out[pos] = vals[off + i];
+        const uint32_t c = n & RUN_CNT;
+        for (uint32_t i = 0; i < c; i++, pos++)
+            if (pos < cap) out[pos] = (n & RUN_INLINE) ? off : vals[off + i];
         return true;
     }
 };
@@ -422,7 +423,7 @@ struct FirstEmit {          // match/2: stop at the first hit
     uint32_t v;
     bool found;
     __device__ __forceinline__ bool operator()(uint32_t off, uint32_t n) {
-        if (n) { v = vals[off]; found = true; return false; }
+        if (n) { v = (n & RUN_INLINE) ? off : vals[off]; found = true; return false; }
         return true;
     }
 };
@@ -762,7 +763,7 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_wave(DevIndex ix, Workspace w
     uint32_t rank = 0, total = 0;
     for (uint32_t j = 0; j < nh; j++) {
         rank += hcode[j] < my;
-        total += hcnt[j];
+        total += hcnt[j] & RUN_CNT;
     }
     if (MODE == MODE_COUNT) {
         if (hv && rank < RCAP) ws.rng[(uint64_t)rank * n + t] = make_uint2(hoff[gl], hcnt[gl]);
@@ -774,7 +775,7 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_wave(DevIndex ix, Workspace w
             if (nh > RCAP) list_push(ws, n, L_OVF_MID, (uint32_t)t);
         }
     } else {
-        if (hv && rank == 0) o.first_val[t] = ix.vals[hoff[gl]];
+        if (hv && rank == 0) o.first_val[t] = (hcnt[gl] & RUN_INLINE) ? hoff[gl] : ix.vals[hoff[gl]];
         if (gl == 0) {
             if (!nh) o.first_val[t] = 0;
             o.first_found[t] = badarg ? 2 : (nh ? 1 : 0);
@@ -928,8 +929,8 @@ __global__ __launch_bounds__(EMIT_BLOCK) void k_emit(DevIndex ix, Workspace ws, 
         const uint2 g = ws.rng[(uint64_t)i * n + t];
         s_off[wv][r0 + i] = g.x;
         s_rel[wv][r0 + i] = rel + acc;
-        s_cnt[wv][r0 + i] = g.y;
-        acc += g.y;
+        s_cnt[wv][r0 + i] = g.y;          // device count (RUN_INLINE: g.x is the value)
+        acc += g.y & RUN_CNT;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -955,7 +956,11 @@ __global__ __launch_bounds__(EMIT_BLOCK) void k_emit(DevIndex ix, Workspace ws, 
             const uint32_t x = (uint32_t)(p - base);
             while (r + 1 < R && s_rel[wv][r + 1] <= x) r++;
             const uint32_t rs = s_rel[wv][r];
-            if (x >= rs && x - rs < s_cnt[wv][r]) { v[k] = ix.vals[s_off[wv][r] + (x - rs)]; ok[k] = true; }
+            const uint32_t rc = s_cnt[wv][r];
+            if (x >= rs && x - rs < (rc & RUN_CNT)) {
+                v[k] = (rc & RUN_INLINE) ? s_off[wv][r] : ix.vals[s_off[wv][r] + (x - rs)];
+                ok[k] = true;
+            }
         }
         if (vec && ok[0] && ok[1] && ok[2] && ok[3] && p0 + 3 < cap) {
             *reinterpret_cast<uint4 *>(out + p0) = make_uint4(v[0], v[1], v[2], v[3]);

@@ -80,6 +80,13 @@ struct alignas(16) ExactEntry {    // 64 B
     uint32_t wids[XINL];
 };
 
+// Value runs as the device sees them (Node hash_/exact_ fields, ExactEntry
+// val_*): (offset into vals, count), except that a run of exactly ONE value is
+// stored inline -- off = the value itself, cnt = 1 | RUN_INLINE -- so emitting
+// the (common) single-subscriber filter reads no `vals` line.
+constexpr uint32_t RUN_INLINE = 0x80000000u;
+constexpr uint32_t RUN_CNT = 0x7FFFFFFFu;
+
 static_assert(sizeof(VocabEntry) == 16, "vocab entry");
 static_assert(sizeof(CSlot) == 8, "child slot");
 static_assert(sizeof(Node) == 64, "node");
