@@ -376,6 +376,35 @@ void set_bloom(Node &n, uint32_t wid) {
     bloom_word(n, b >> 5) |= 1u << (b & 31);
 }
 
+// summary of node q as its parent's psum (tm_layout.h): terminals, '+' child,
+// 61-bit Bloom of the literal child wids (all ones past 61 children)
+uint64_t node_psum(tm_index *ix, uint32_t q) {
+    const Node &n = ix->nodes.h[q];
+    uint64_t m = (n.hash_cnt ? PSUM_HASH : 0) | (n.exact_cnt ? PSUM_EXACT : 0) | (n.plus != NONE ? PSUM_PLUS : 0);
+    auto add = [&](uint32_t wid) { m |= 1ull << psum_bit(child_hash(wid)); };
+    if (n.nlit <= KINL) {
+        for (uint32_t k = 0; k < KINL; k++) if (n.kw[k] != NONE) add(n.kw[k]);
+    } else if (n.nlit > 61) {
+        m |= ~7ull;
+    } else {
+        for (uint32_t i = 0; i <= n.kw[1]; i++) if (ix->ctab.h[n.kw[0] + i].wid != NONE) add(ix->ctab.h[n.kw[0] + i].wid);
+    }
+    return m;
+}
+
+// node x changed: if it is a '+' child, refresh its parent's summary of it
+void psum_refresh(tm_index *ix, uint32_t x) {
+    if (x == ROOT || !ix->aux[x].is_plus) return;
+    const uint32_t p = ix->aux[x].parent;
+    Node &pn = ix->nodes.h[p];
+    if (pn.plus != x) return;
+    const uint64_t m = node_psum(ix, x);
+    if (pn.psum_lo != (uint32_t)m || pn.psum_hi != (uint32_t)(m >> 32)) {
+        pn.psum_lo = (uint32_t)m; pn.psum_hi = (uint32_t)(m >> 32);
+        ix->nodes.touch(p);
+    }
+}
+
 // move a node's children into a private table of `cap` slots (cap = pow2)
 void to_table(tm_index *ix, uint32_t node, uint32_t cap) {
     Node &n = ix->nodes.h[node];
@@ -388,7 +417,7 @@ void to_table(tm_index *ix, uint32_t node, uint32_t cap) {
     }
     uint32_t off = ctab_alloc(ix, cap);
     Node &m = ix->nodes.h[node];
-    for (uint32_t j = 0; j < 8; j++) bloom_word(m, j) = 0;
+    for (uint32_t j = 0; j < 6; j++) bloom_word(m, j) = 0;
     for (auto &c : kids) { ctab_put(ix, off, cap - 1, c.wid, c.child); set_bloom(m, c.wid); }
     m.kw[0] = off; m.kw[1] = cap - 1;
 }
@@ -408,6 +437,7 @@ void child_add(tm_index *ix, uint32_t node, uint32_t wid, uint32_t child) {
     }
     n->nlit++;
     ix->nodes.touch(node);
+    psum_refresh(ix, node);
 }
 
 void child_remove(tm_index *ix, uint32_t node, uint32_t wid) {
@@ -425,10 +455,10 @@ void child_remove(tm_index *ix, uint32_t node, uint32_t wid) {
             for (uint32_t i = 0; i <= n.kw[1]; i++) if (ix->ctab.h[n.kw[0] + i].wid != NONE) kids.push_back(ix->ctab.h[n.kw[0] + i]);
             ctab_free(ix, n.kw[0], n.kw[1] + 1);
             for (uint32_t k = 0; k < KINL; k++) { n.kw[k] = kids[k].wid; n.kc[k] = kids[k].child; }
-            n.mask_lo = n.mask_hi = 0;
         }
     }
     ix->nodes.touch(node);
+    psum_refresh(ix, node);
 }
 
 bool node_empty(tm_index *ix, uint32_t id) {
@@ -439,8 +469,14 @@ bool node_empty(tm_index *ix, uint32_t id) {
 void node_prune(tm_index *ix, uint32_t id) {
     while (id != ROOT && node_empty(ix, id)) {
         NodeAux a = ix->aux[id];
-        if (a.is_plus) { ix->nodes.h[a.parent].plus = NONE; ix->nodes.touch(a.parent); }
-        else child_remove(ix, a.parent, a.wid);
+        if (a.is_plus) {
+            Node &pn = ix->nodes.h[a.parent];
+            pn.plus = NONE; pn.psum_lo = pn.psum_hi = 0;
+            ix->nodes.touch(a.parent);
+            psum_refresh(ix, a.parent);
+        } else {
+            child_remove(ix, a.parent, a.wid);
+        }
         ix->free_nodes.push_back(id);
         ix->live_nodes--;
         id = a.parent;
@@ -612,6 +648,8 @@ void key_op(tm_index *ix, bool ins, const uint8_t *f, uint32_t len, uint32_t v, 
                 c = node_new(ix, node, NONE, true);
                 ix->nodes.h[node].plus = c;
                 ix->nodes.touch(node);
+                psum_refresh(ix, node);   // node gained a '+' child
+                psum_refresh(ix, c);
             }
             node = c;
         } else {
@@ -633,6 +671,7 @@ void key_op(tm_index *ix, bool ins, const uint8_t *f, uint32_t len, uint32_t v, 
                         : run_op(ix, ins, a.exact_roff, a.exact_cap, nd.exact_off, nd.exact_cnt, v);
     if (!changed) return;
     ix->nodes.touch(node);
+    psum_refresh(ix, node);
     if (ins) ix->n_wild++;
     else { ix->n_wild--; node_prune(ix, node); }
 }

@@ -32,12 +32,22 @@ namespace tmx {
 
 __device__ __forceinline__ uint4 ld4(const void *p) { return *reinterpret_cast<const uint4 *>(p); }
 
-// bit b (0..255) of a table-mode node's Bloom: words mask_lo, mask_hi, kw[2..3], kc[0..3]
-__device__ __forceinline__ uint32_t bloom_bit(const uint4 &n1, const uint4 &n2, const uint4 &n3, uint32_t b) {
+// bit b (0..191) of a table-mode node's Bloom: words kw[2..3], kc[0..3]
+__device__ __forceinline__ uint32_t bloom_bit(const uint4 &n2, const uint4 &n3, uint32_t b) {
     const uint32_t j = b >> 5;
-    const uint32_t w = j == 0 ? n1.z : j == 1 ? n1.w : j == 2 ? n2.z : j == 3 ? n2.w
-                     : j == 4 ? n3.x : j == 5 ? n3.y : j == 6 ? n3.z : n3.w;
+    const uint32_t w = j == 0 ? n2.z : j == 1 ? n2.w : j == 2 ? n3.x : j == 3 ? n3.y : j == 4 ? n3.z : n3.w;
     return (w >> (b & 31)) & 1u;
+}
+
+// can the '+' child (summarised by psum = n1.z | n1.w << 32) contribute to a
+// topic of L levels when entered at level lq?  (emit at lq == L, or emit / go
+// on below it: '#' terminal, '+' child, or a literal child for word wq)
+__device__ __forceinline__ bool plus_alive(uint32_t plo, uint32_t phi, uint32_t lq, uint32_t L, uint32_t wq) {
+    if (lq == L) return (plo & (PSUM_HASH | PSUM_EXACT)) != 0;
+    if (plo & (PSUM_HASH | PSUM_PLUS)) return true;
+    if (wq == NONE) return false;
+    const uint32_t b = psum_bit(child_hash(wq));
+    return (((b < 32 ? plo : phi) >> (b & 31)) & 1u) != 0;
 }
 
 // Empty asm "uses": pin a loaded value at this point on every path.  Without
@@ -332,6 +342,9 @@ __device__ void exact_find(const DevIndex &ix, uint64_t xh, uint32_t L, const S 
 template <class S, class EM>
 __device__ bool dfs(const DevIndex &ix, uint32_t L, bool dollar, S &st, EM &em) {
     uint32_t cur = ROOT, l = 0;
+#ifdef TM_STUDY_DEAD
+    bool via_plus = false;   // study: how the current node was reached
+#endif
     for (;;) {
 #ifdef TM_STUDY
         if constexpr (S::deferred) st.n_steps++;
@@ -339,7 +352,7 @@ __device__ bool dfs(const DevIndex &ix, uint32_t L, bool dollar, S &st, EM &em) 
         // the whole state is one 64-byte line (tm_layout.h Node)
         const uint4 *np = reinterpret_cast<const uint4 *>(ix.nodes + cur);
         const uint4 n0 = np[0];   // plus, hash_off, hash_cnt, exact_off
-        const uint4 n1 = np[1];   // exact_cnt, nlit, mask_lo, mask_hi
+        const uint4 n1 = np[1];   // exact_cnt, nlit, psum_lo, psum_hi
         const uint4 n2 = np[2];   // kw[0..3] (table mode: offset, size-1)
         const uint4 n3 = np[3];   // kc[0..3]
         const bool droot = dollar && l == 0;
@@ -361,9 +374,9 @@ __device__ bool dfs(const DevIndex &ix, uint32_t L, bool dollar, S &st, EM &em) 
                     lit = inl;
                 } else {
                     const uint32_t h = child_hash(w);
-                    const uint32_t m = bloom_bit(n1, n2, n3, child_bit(h));
+                    const uint32_t m = bloom_bit(n2, n3, child_bit(h));
                     if (m & 1u) lit = ctab_find(ix, n2.x, n2.y, w, h);
-#ifdef TM_STUDY
+#if defined(TM_STUDY) && !defined(TM_STUDY_DEAD)
                     if constexpr (S::deferred) {
                         if (m & 1u) { if (lit != NONE) st.n_steps += 1u << 16; else st.n_probe++; }
                     }
@@ -371,14 +384,36 @@ __device__ bool dfs(const DevIndex &ix, uint32_t L, bool dollar, S &st, EM &em) 
                 }
             }
             if (!droot && !em(n0.y, n0.z)) return false;
-            const uint32_t plus = droot ? NONE : n0.x;
+            uint32_t plus = droot ? NONE : n0.x;
+#ifndef TM_NO_PSUM
+            if (plus != NONE && !plus_alive(n1.z, n1.w, l + 1, L, l + 1 < L ? st.get_wid(l + 1) : NONE)) plus = NONE;
+#endif
+#ifdef TM_STUDY_DEAD
+            if constexpr (S::deferred) {   // a visit that emits nothing and leads nowhere
+                if (plus == NONE && lit == NONE && (droot || !n0.z)) {
+                    if (via_plus) st.n_steps += 1u << 16; else st.n_probe++;
+                }
+            }
+#endif
             if (plus != NONE) {
                 if (lit != NONE) st.push(l + 1, lit);
                 cur = plus; l++;
+#ifdef TM_STUDY_DEAD
+                via_plus = true;
+#endif
                 continue;
             }
-            if (lit != NONE) { cur = lit; l++; continue; }
+            if (lit != NONE) {
+                cur = lit; l++;
+#ifdef TM_STUDY_DEAD
+                via_plus = false;
+#endif
+                continue;
+            }
         }
+#ifdef TM_STUDY_DEAD
+        via_plus = false;
+#endif
         if (!st.pop(l, cur)) return true;
     }
 }
@@ -719,11 +754,15 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_wave(DevIndex ix, Workspace w
                 lit = n2.x == wl_ ? n3.x : n2.y == wl_ ? n3.y : n2.z == wl_ ? n3.z : n2.w == wl_ ? n3.w : NONE;
             } else {
                 const uint32_t h = child_hash(wl_);
-                const uint32_t mb = bloom_bit(n1, n2, n3, child_bit(h));
+                const uint32_t mb = bloom_bit(n2, n3, child_bit(h));
                 if (mb & 1u) lit = ctab_find(ix, n2.x, n2.y, wl_, h);
             }
         }
-        const uint32_t plus = act && !droot ? n0.x : NONE;
+        uint32_t plus = act && !droot ? n0.x : NONE;
+#ifndef TM_NO_PSUM
+        const uint32_t wnext = l + 1 < L ? grp.bcast(wid, l + 1) : NONE;
+        if (plus != NONE && !plus_alive(n1.z, n1.w, l + 1, L, wnext)) plus = NONE;
+#endif
         const uint64_t mp = grp.ballot(plus != NONE), ml = grp.ballot(lit != NONE);
         const uint32_t np_ = (uint32_t)__popcll(mp), nn = np_ + (uint32_t)__popcll(ml);
         if (nn > W) { ovf = true; break; }

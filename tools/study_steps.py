@@ -23,6 +23,11 @@ def main():
     ts = wl.topics(gen, nf, 200_000)
     hit, vals, err = ix.match_batch(ts.blob, ts.offs)
     import os
+    if os.environ.get("TM_STUDY_DEAD"):
+        dp, dl = (err & 15).astype(np.int64), (err >> 4).astype(np.int64)
+        print(f"{cfg}: dead-end visits (emit nothing, lead nowhere) reached via '+' mean {dp.mean():.2f}, "
+              f"via a literal edge or a pop mean {dl.mean():.2f} (each capped at 15)", flush=True)
+        return
     if os.environ.get("TM_STUDY_HITS"):
         hits_, miss_ = (err & 15).astype(np.int64), (err >> 4).astype(np.int64)
         print(f"{cfg}: child-table probes that found the child mean {hits_.mean():.2f}, "
