@@ -247,7 +247,7 @@ uint32_t ctab_alloc(tm_index *ix, uint32_t cap) {
     uint32_t o;
     if (!fl.empty()) { o = fl.back(); fl.pop_back(); }
     else { o = (uint32_t)ix->ctab.h.size(); ix->ctab.h.resize(o + cap); }
-    for (uint32_t i = 0; i < cap; i++) ix->ctab.h[o + i] = CSlot{NONE, NONE};
+    for (uint32_t i = 0; i < cap; i++) ix->ctab.h[o + i] = CSlot{NONE, NONE, 0, 0};
     ix->ctab.touch(o, cap);
     ix->ntables++;
     return o;
@@ -258,9 +258,13 @@ void ctab_free(tm_index *ix, uint32_t off, uint32_t cap) {
     ix->ntables--;
 }
 
-void ctab_put(tm_index *ix, uint32_t off, uint32_t mask, uint32_t wid, uint32_t child) {
+void ctab_put(tm_index *ix, uint32_t off, uint32_t mask, uint32_t wid, uint32_t child, uint64_t sum) {
     for (uint32_t s = child_hash(wid) & mask;; s = (s + 1) & mask)
-        if (ix->ctab.h[off + s].wid == NONE) { ix->ctab.h[off + s] = CSlot{wid, child}; ix->ctab.touch(off + s); return; }
+        if (ix->ctab.h[off + s].wid == NONE) {
+            ix->ctab.h[off + s] = CSlot{wid, child, (uint32_t)sum, (uint32_t)(sum >> 32)};
+            ix->ctab.touch(off + s);
+            return;
+        }
 }
 
 uint32_t ctab_find(tm_index *ix, uint32_t off, uint32_t mask, uint32_t wid) {
@@ -281,7 +285,7 @@ void ctab_erase(tm_index *ix, uint32_t off, uint32_t mask, uint32_t wid) {
         bool stays = (i <= j) ? (i < k && k <= j) : (i < k || k <= j);
         if (!stays) { t[i] = t[j]; ix->ctab.touch(off + i); i = j; }
     }
-    t[i] = CSlot{NONE, NONE};
+    t[i] = CSlot{NONE, NONE, 0, 0};
     ix->ctab.touch(off + i);
 }
 
@@ -392,16 +396,32 @@ uint64_t node_psum(tm_index *ix, uint32_t q) {
     return m;
 }
 
-// node x changed: if it is a '+' child, refresh its parent's summary of it
-void psum_refresh(tm_index *ix, uint32_t x) {
-    if (x == ROOT || !ix->aux[x].is_plus) return;
-    const uint32_t p = ix->aux[x].parent;
+// node x changed: refresh its parent's summary of it -- the parent line's psum
+// for a '+' child, the child-table slot for a literal child of a table-mode
+// parent (inline-mode parents keep no per-child summary)
+void summary_refresh(tm_index *ix, uint32_t x) {
+    if (x == ROOT) return;
+    const NodeAux &a = ix->aux[x];
+    const uint32_t p = a.parent;
     Node &pn = ix->nodes.h[p];
-    if (pn.plus != x) return;
+    if (a.is_plus) {
+        if (pn.plus != x) return;
+        const uint64_t m = node_psum(ix, x);
+        if (pn.psum_lo != (uint32_t)m || pn.psum_hi != (uint32_t)(m >> 32)) {
+            pn.psum_lo = (uint32_t)m; pn.psum_hi = (uint32_t)(m >> 32);
+            ix->nodes.touch(p);
+        }
+        return;
+    }
+    if (pn.nlit <= KINL) return;
+    const uint32_t sl = ctab_find(ix, pn.kw[0], pn.kw[1], a.wid);
+    if (sl == NONE) return;
+    CSlot &c = ix->ctab.h[pn.kw[0] + sl];
+    if (c.child != x) return;
     const uint64_t m = node_psum(ix, x);
-    if (pn.psum_lo != (uint32_t)m || pn.psum_hi != (uint32_t)(m >> 32)) {
-        pn.psum_lo = (uint32_t)m; pn.psum_hi = (uint32_t)(m >> 32);
-        ix->nodes.touch(p);
+    if (c.sum_lo != (uint32_t)m || c.sum_hi != (uint32_t)(m >> 32)) {
+        c.sum_lo = (uint32_t)m; c.sum_hi = (uint32_t)(m >> 32);
+        ix->ctab.touch(pn.kw[0] + sl);
     }
 }
 
@@ -410,7 +430,11 @@ void to_table(tm_index *ix, uint32_t node, uint32_t cap) {
     Node &n = ix->nodes.h[node];
     std::vector<CSlot> kids;
     if (n.nlit <= KINL) {
-        for (uint32_t k = 0; k < KINL; k++) if (n.kw[k] != NONE) kids.push_back({n.kw[k], n.kc[k]});
+        for (uint32_t k = 0; k < KINL; k++)
+            if (n.kw[k] != NONE) {
+                const uint64_t m = node_psum(ix, n.kc[k]);
+                kids.push_back({n.kw[k], n.kc[k], (uint32_t)m, (uint32_t)(m >> 32)});
+            }
     } else {
         for (uint32_t i = 0; i <= n.kw[1]; i++) if (ix->ctab.h[n.kw[0] + i].wid != NONE) kids.push_back(ix->ctab.h[n.kw[0] + i]);
         ctab_free(ix, n.kw[0], n.kw[1] + 1);
@@ -418,7 +442,10 @@ void to_table(tm_index *ix, uint32_t node, uint32_t cap) {
     uint32_t off = ctab_alloc(ix, cap);
     Node &m = ix->nodes.h[node];
     for (uint32_t j = 0; j < 6; j++) bloom_word(m, j) = 0;
-    for (auto &c : kids) { ctab_put(ix, off, cap - 1, c.wid, c.child); set_bloom(m, c.wid); }
+    for (auto &c : kids) {
+        ctab_put(ix, off, cap - 1, c.wid, c.child, (uint64_t)c.sum_hi << 32 | c.sum_lo);
+        set_bloom(m, c.wid);
+    }
     m.kw[0] = off; m.kw[1] = cap - 1;
 }
 
@@ -432,12 +459,12 @@ void child_add(tm_index *ix, uint32_t node, uint32_t wid, uint32_t child) {
         if (n->nlit == KINL) to_table(ix, node, 16);
         else if ((n->nlit + 1) * 2 > n->kw[1] + 1) to_table(ix, node, (n->kw[1] + 1) * 2);
         n = &ix->nodes.h[node];
-        ctab_put(ix, n->kw[0], n->kw[1], wid, child);
+        ctab_put(ix, n->kw[0], n->kw[1], wid, child, node_psum(ix, child));
         set_bloom(*n, wid);
     }
     n->nlit++;
     ix->nodes.touch(node);
-    psum_refresh(ix, node);
+    summary_refresh(ix, node);
 }
 
 void child_remove(tm_index *ix, uint32_t node, uint32_t wid) {
@@ -458,7 +485,7 @@ void child_remove(tm_index *ix, uint32_t node, uint32_t wid) {
         }
     }
     ix->nodes.touch(node);
-    psum_refresh(ix, node);
+    summary_refresh(ix, node);
 }
 
 bool node_empty(tm_index *ix, uint32_t id) {
@@ -473,7 +500,7 @@ void node_prune(tm_index *ix, uint32_t id) {
             Node &pn = ix->nodes.h[a.parent];
             pn.plus = NONE; pn.psum_lo = pn.psum_hi = 0;
             ix->nodes.touch(a.parent);
-            psum_refresh(ix, a.parent);
+            summary_refresh(ix, a.parent);
         } else {
             child_remove(ix, a.parent, a.wid);
         }
@@ -648,8 +675,8 @@ void key_op(tm_index *ix, bool ins, const uint8_t *f, uint32_t len, uint32_t v, 
                 c = node_new(ix, node, NONE, true);
                 ix->nodes.h[node].plus = c;
                 ix->nodes.touch(node);
-                psum_refresh(ix, node);   // node gained a '+' child
-                psum_refresh(ix, c);
+                summary_refresh(ix, node);   // node gained a '+' child
+                summary_refresh(ix, c);
             }
             node = c;
         } else {
@@ -671,7 +698,7 @@ void key_op(tm_index *ix, bool ins, const uint8_t *f, uint32_t len, uint32_t v, 
                         : run_op(ix, ins, a.exact_roff, a.exact_cap, nd.exact_off, nd.exact_cnt, v);
     if (!changed) return;
     ix->nodes.touch(node);
-    psum_refresh(ix, node);
+    summary_refresh(ix, node);
     if (ins) ix->n_wild++;
     else { ix->n_wild--; node_prune(ix, node); }
 }

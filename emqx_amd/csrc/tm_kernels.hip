@@ -39,10 +39,10 @@ __device__ __forceinline__ uint32_t bloom_bit(const uint4 &n2, const uint4 &n3, 
     return (w >> (b & 31)) & 1u;
 }
 
-// can the '+' child (summarised by psum = n1.z | n1.w << 32) contribute to a
-// topic of L levels when entered at level lq?  (emit at lq == L, or emit / go
+// can a child (summarised as Node.psum / CSlot.sum) contribute to a topic of
+// L levels when entered at level lq?  (emit at lq == L, or emit / go
 // on below it: '#' terminal, '+' child, or a literal child for word wq)
-__device__ __forceinline__ bool plus_alive(uint32_t plo, uint32_t phi, uint32_t lq, uint32_t L, uint32_t wq) {
+__device__ __forceinline__ bool child_alive(uint32_t plo, uint32_t phi, uint32_t lq, uint32_t L, uint32_t wq) {
     if (lq == L) return (plo & (PSUM_HASH | PSUM_EXACT)) != 0;
     if (plo & (PSUM_HASH | PSUM_PLUS)) return true;
     if (wq == NONE) return false;
@@ -106,13 +106,14 @@ __device__ uint32_t vocab_find(const DevIndex &ix, const WordAcc &w, const uint8
     return vocab_probe(ix, (uint32_t)h & ix.vmask, vocab_tag(h, w.len), w.len, w.b0, w.b1, blob + w.start);
 }
 
-// literal child in a node's private table (table mode, nlit > KINL)
+// literal child in a node's private table (table mode, nlit > KINL), with the
+// slot's summary of the child
 __device__ __forceinline__ uint32_t ctab_find(const DevIndex &ix, uint32_t off, uint32_t mask, uint32_t wid,
-                                              uint32_t h) {
+                                              uint32_t h, uint32_t &slo, uint32_t &shi) {
     for (uint32_t s = h & mask;; s = (s + 1) & mask) {
-        uint2 e = *reinterpret_cast<const uint2 *>(ix.ctab + off + s);
+        uint4 e = ld4(ix.ctab + off + s);
         pin(e);
-        if (e.x == wid) return e.y;
+        if (e.x == wid) { slo = e.z; shi = e.w; return e.y; }
         if (e.x == NONE) return NONE;
     }
 }
@@ -375,7 +376,14 @@ __device__ bool dfs(const DevIndex &ix, uint32_t L, bool dollar, S &st, EM &em) 
                 } else {
                     const uint32_t h = child_hash(w);
                     const uint32_t m = bloom_bit(n2, n3, child_bit(h));
-                    if (m & 1u) lit = ctab_find(ix, n2.x, n2.y, w, h);
+                    if (m & 1u) {
+                        uint32_t slo, shi;
+                        lit = ctab_find(ix, n2.x, n2.y, w, h, slo, shi);
+#ifndef TM_NO_PSUM
+                        if (lit != NONE && !child_alive(slo, shi, l + 1, L, l + 1 < L ? st.get_wid(l + 1) : NONE))
+                            lit = NONE;
+#endif
+                    }
 #if defined(TM_STUDY) && !defined(TM_STUDY_DEAD)
                     if constexpr (S::deferred) {
                         if (m & 1u) { if (lit != NONE) st.n_steps += 1u << 16; else st.n_probe++; }
@@ -386,7 +394,7 @@ __device__ bool dfs(const DevIndex &ix, uint32_t L, bool dollar, S &st, EM &em) 
             if (!droot && !em(n0.y, n0.z)) return false;
             uint32_t plus = droot ? NONE : n0.x;
 #ifndef TM_NO_PSUM
-            if (plus != NONE && !plus_alive(n1.z, n1.w, l + 1, L, l + 1 < L ? st.get_wid(l + 1) : NONE)) plus = NONE;
+            if (plus != NONE && !child_alive(n1.z, n1.w, l + 1, L, l + 1 < L ? st.get_wid(l + 1) : NONE)) plus = NONE;
 #endif
 #ifdef TM_STUDY_DEAD
             if constexpr (S::deferred) {   // a visit that emits nothing and leads nowhere
@@ -748,6 +756,7 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_wave(DevIndex ix, Workspace w
         }
         add_hits(act && !droot && n0.z, code, n0.y, n0.z);                       // '#' terminal: digit 0
         const uint32_t wl_ = grp.bcast(wid, l);
+        const uint32_t wnext = l + 1 < L ? grp.bcast(wid, l + 1) : NONE;
         uint32_t lit = NONE;
         if (act && wl_ != NONE) {
             if (n1.y <= KINL) {
@@ -755,13 +764,18 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_wave(DevIndex ix, Workspace w
             } else {
                 const uint32_t h = child_hash(wl_);
                 const uint32_t mb = bloom_bit(n2, n3, child_bit(h));
-                if (mb & 1u) lit = ctab_find(ix, n2.x, n2.y, wl_, h);
+                if (mb & 1u) {
+                    uint32_t slo, shi;
+                    lit = ctab_find(ix, n2.x, n2.y, wl_, h, slo, shi);
+#ifndef TM_NO_PSUM
+                    if (lit != NONE && !child_alive(slo, shi, l + 1, L, wnext)) lit = NONE;
+#endif
+                }
             }
         }
         uint32_t plus = act && !droot ? n0.x : NONE;
 #ifndef TM_NO_PSUM
-        const uint32_t wnext = l + 1 < L ? grp.bcast(wid, l + 1) : NONE;
-        if (plus != NONE && !plus_alive(n1.z, n1.w, l + 1, L, wnext)) plus = NONE;
+        if (plus != NONE && !child_alive(n1.z, n1.w, l + 1, L, wnext)) plus = NONE;
 #endif
         const uint64_t mp = grp.ballot(plus != NONE), ml = grp.ballot(lit != NONE);
         const uint32_t np_ = (uint32_t)__popcll(mp), nn = np_ + (uint32_t)__popcll(ml);

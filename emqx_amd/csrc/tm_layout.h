@@ -47,9 +47,11 @@ struct alignas(16) VocabEntry {   // 16 B
                                    // len  > 8: b0 = offset of the word in wpool, b1 = len
 };
 
-struct CSlot {                     // 8 B: one literal child in a node's private table
+struct alignas(16) CSlot {          // 16 B: one literal child in a node's private table
     uint32_t wid;                  // NONE = empty slot
     uint32_t child;
+    uint32_t sum_lo, sum_hi;       // summary of the child (PSUM_* bits + Bloom, as Node.psum):
+                                   // the probe that finds a child also says if visiting it can matter
 };
 
 constexpr uint32_t KINL = 4;     // literal children kept inside the node's line
@@ -96,7 +98,7 @@ constexpr uint32_t RUN_INLINE = 0x80000000u;
 constexpr uint32_t RUN_CNT = 0x7FFFFFFFu;
 
 static_assert(sizeof(VocabEntry) == 16, "vocab entry");
-static_assert(sizeof(CSlot) == 8, "child slot");
+static_assert(sizeof(CSlot) == 16, "child slot");
 static_assert(sizeof(Node) == 64, "node");
 static_assert(sizeof(ExactEntry) == 64, "exact entry");
 
