@@ -382,24 +382,45 @@ void set_bloom(Node &n, uint32_t wid) {
 
 // summary of node q as its parent's psum (tm_layout.h): terminals, '+' child,
 // 61-bit Bloom of the literal child wids (all ones past 61 children)
-uint64_t node_psum(tm_index *ix, uint32_t q) {
+// literal-children Bloom of node q (29 bits), all ones past 29 children
+uint64_t lit_bloom(tm_index *ix, uint32_t q) {
     const Node &n = ix->nodes.h[q];
-    uint64_t m = (n.hash_cnt ? PSUM_HASH : 0) | (n.exact_cnt ? PSUM_EXACT : 0) | (n.plus != NONE ? PSUM_PLUS : 0);
+    uint64_t m = 0;
     auto add = [&](uint32_t wid) { m |= 1ull << psum_bit(child_hash(wid)); };
     if (n.nlit <= KINL) {
         for (uint32_t k = 0; k < KINL; k++) if (n.kw[k] != NONE) add(n.kw[k]);
-    } else if (n.nlit > 61) {
-        m |= ~7ull;
+    } else if (n.nlit > 29) {
+        m = (1ull << 29) - 1;
     } else {
         for (uint32_t i = 0; i <= n.kw[1]; i++) if (ix->ctab.h[n.kw[0] + i].wid != NONE) add(ix->ctab.h[n.kw[0] + i].wid);
     }
     return m;
 }
 
+uint64_t node_flags(const Node &n) {
+    return (n.hash_cnt ? PSUM_HASH : 0) | (n.exact_cnt ? PSUM_EXACT : 0) | (n.plus != NONE ? PSUM_PLUS : 0);
+}
+
+// summary of node q as its parent keeps it (tm_layout.h PSUM_*)
+uint64_t node_psum(tm_index *ix, uint32_t q) {
+    const Node &n = ix->nodes.h[q];
+    uint64_t m = node_flags(n) | lit_bloom(ix, q) << 6;
+    if (n.plus != NONE) m |= node_flags(ix->nodes.h[n.plus]) << 3 | lit_bloom(ix, n.plus) << 35;
+    return m;
+}
+
 // node x changed: refresh its parent's summary of it -- the parent line's psum
 // for a '+' child, the child-table slot for a literal child of a table-mode
 // parent (inline-mode parents keep no per-child summary)
+void summary_refresh1(tm_index *ix, uint32_t x);
 void summary_refresh(tm_index *ix, uint32_t x) {
+    // x's summary sits in its parent; the parent's own summary (in the
+    // grandparent) covers x too when x is the parent's '+' child
+    summary_refresh1(ix, x);
+    if (x != ROOT && ix->aux[x].is_plus) summary_refresh1(ix, ix->aux[x].parent);
+}
+
+void summary_refresh1(tm_index *ix, uint32_t x) {
     if (x == ROOT) return;
     const NodeAux &a = ix->aux[x];
     const uint32_t p = a.parent;

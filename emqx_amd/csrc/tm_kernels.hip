@@ -39,15 +39,21 @@ __device__ __forceinline__ uint32_t bloom_bit(const uint4 &n2, const uint4 &n3, 
     return (w >> (b & 31)) & 1u;
 }
 
-// can a child (summarised as Node.psum / CSlot.sum) contribute to a topic of
-// L levels when entered at level lq?  (emit at lq == L, or emit / go
-// on below it: '#' terminal, '+' child, or a literal child for word wq)
-__device__ __forceinline__ bool child_alive(uint32_t plo, uint32_t phi, uint32_t lq, uint32_t L, uint32_t wq) {
-    if (lq == L) return (plo & (PSUM_HASH | PSUM_EXACT)) != 0;
-    if (plo & (PSUM_HASH | PSUM_PLUS)) return true;
-    if (wq == NONE) return false;
-    const uint32_t b = psum_bit(child_hash(wq));
-    return (((b < 32 ? plo : phi) >> (b & 31)) & 1u) != 0;
+// can a child Q (summarised as Node.psum / CSlot.sum, tm_layout.h) contribute
+// to a topic of L levels when entered at level lq?  Q must emit at lq == L, or
+// below it emit ('#' terminal) or go on: a literal child for word wq, or its
+// '+' child QQ, which in turn must be able to contribute at lq + 1 (word wq2)
+__device__ __forceinline__ bool child_alive(uint32_t lo, uint32_t hi, uint32_t lq, uint32_t L, uint32_t wq,
+                                            uint32_t wq2) {
+    const uint64_t m = (uint64_t)hi << 32 | lo;
+    if (lq == L) return (m & (PSUM_HASH | PSUM_EXACT)) != 0;
+    if (m & PSUM_HASH) return true;
+    if (wq != NONE && ((m >> (6 + psum_bit(child_hash(wq)))) & 1u)) return true;
+    if (!(m & PSUM_PLUS)) return false;
+    const uint32_t qq = (uint32_t)(m >> 3) & 7u;
+    if (lq + 1 == L) return (qq & (PSUM_HASH | PSUM_EXACT)) != 0;
+    if (qq & (PSUM_HASH | PSUM_PLUS)) return true;
+    return wq2 != NONE && ((m >> (35 + psum_bit(child_hash(wq2)))) & 1u);
 }
 
 // Empty asm "uses": pin a loaded value at this point on every path.  Without
@@ -380,7 +386,8 @@ __device__ bool dfs(const DevIndex &ix, uint32_t L, bool dollar, S &st, EM &em) 
                         uint32_t slo, shi;
                         lit = ctab_find(ix, n2.x, n2.y, w, h, slo, shi);
 #ifndef TM_NO_PSUM
-                        if (lit != NONE && !child_alive(slo, shi, l + 1, L, l + 1 < L ? st.get_wid(l + 1) : NONE))
+                        if (lit != NONE && !child_alive(slo, shi, l + 1, L, l + 1 < L ? st.get_wid(l + 1) : NONE,
+                                                        l + 2 < L ? st.get_wid(l + 2) : NONE))
                             lit = NONE;
 #endif
                     }
@@ -394,7 +401,9 @@ __device__ bool dfs(const DevIndex &ix, uint32_t L, bool dollar, S &st, EM &em) 
             if (!droot && !em(n0.y, n0.z)) return false;
             uint32_t plus = droot ? NONE : n0.x;
 #ifndef TM_NO_PSUM
-            if (plus != NONE && !child_alive(n1.z, n1.w, l + 1, L, l + 1 < L ? st.get_wid(l + 1) : NONE)) plus = NONE;
+            if (plus != NONE && !child_alive(n1.z, n1.w, l + 1, L, l + 1 < L ? st.get_wid(l + 1) : NONE,
+                                             l + 2 < L ? st.get_wid(l + 2) : NONE))
+                plus = NONE;
 #endif
 #ifdef TM_STUDY_DEAD
             if constexpr (S::deferred) {   // a visit that emits nothing and leads nowhere
@@ -757,6 +766,7 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_wave(DevIndex ix, Workspace w
         add_hits(act && !droot && n0.z, code, n0.y, n0.z);                       // '#' terminal: digit 0
         const uint32_t wl_ = grp.bcast(wid, l);
         const uint32_t wnext = l + 1 < L ? grp.bcast(wid, l + 1) : NONE;
+        const uint32_t wnext2 = l + 2 < L ? grp.bcast(wid, l + 2) : NONE;
         uint32_t lit = NONE;
         if (act && wl_ != NONE) {
             if (n1.y <= KINL) {
@@ -768,14 +778,14 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_wave(DevIndex ix, Workspace w
                     uint32_t slo, shi;
                     lit = ctab_find(ix, n2.x, n2.y, wl_, h, slo, shi);
 #ifndef TM_NO_PSUM
-                    if (lit != NONE && !child_alive(slo, shi, l + 1, L, wnext)) lit = NONE;
+                    if (lit != NONE && !child_alive(slo, shi, l + 1, L, wnext, wnext2)) lit = NONE;
 #endif
                 }
             }
         }
         uint32_t plus = act && !droot ? n0.x : NONE;
 #ifndef TM_NO_PSUM
-        if (plus != NONE && !child_alive(n1.z, n1.w, l + 1, L, wnext)) plus = NONE;
+        if (plus != NONE && !child_alive(n1.z, n1.w, l + 1, L, wnext, wnext2)) plus = NONE;
 #endif
         const uint64_t mp = grp.ballot(plus != NONE), ml = grp.ballot(lit != NONE);
         const uint32_t np_ = (uint32_t)__popcll(mp), nn = np_ + (uint32_t)__popcll(ml);

@@ -80,7 +80,13 @@ struct alignas(64) Node {          // 64 B
     uint32_t kc[KINL];             // inline: child node ids; table mode: Bloom bits 64-191
 };
 
-constexpr uint32_t PSUM_HASH = 1u, PSUM_EXACT = 2u, PSUM_PLUS = 4u;   // bits of psum_lo
+// Summary of a child Q (Node.psum for the '+' child, CSlot.sum for a literal
+// child), two levels deep so a '+' chain that dies one level down is skipped too:
+//   bits 0-2  Q has a '#' terminal / an exact terminal / a '+' child (QQ)
+//   bits 3-5  the same for QQ (0 if Q has no '+' child)
+//   bits 6-34  29-bit Bloom of Q's literal child wids  (all ones past 29 children)
+//   bits 35-63 29-bit Bloom of QQ's literal child wids
+constexpr uint32_t PSUM_HASH = 1u, PSUM_EXACT = 2u, PSUM_PLUS = 4u;   // bits of psum_lo (<< 3: QQ's)
 
 struct alignas(16) ExactEntry {    // 64 B
     uint32_t h_lo, h_hi;           // hash of the wid sequence
@@ -130,7 +136,7 @@ TM_HD uint32_t vocab_tag(uint64_t h, uint32_t len) {
 // child table hash: low bits pick the slot, the high 16 bits the Bloom bits
 TM_HD uint32_t child_hash(uint32_t wid) { return (uint32_t)mix64((uint64_t)wid * 0x9e3779b97f4a7c15ull + 1); }
 TM_HD uint32_t child_bit(uint32_t h) { return ((h >> 16) * 192u) >> 16; }      // 0..191, table-mode Bloom
-TM_HD uint32_t psum_bit(uint32_t h) { return 3u + (((h >> 16) * 61u) >> 16); }  // 3..63, '+'-child summary
+TM_HD uint32_t psum_bit(uint32_t h) { return ((h >> 16) * 29u) >> 16; }      // 0..28, + 6 (Q) or + 35 (QQ)
 // Bloom word j (bits 32j .. 32j+31) of a table-mode node line
 TM_HD uint32_t &bloom_word(Node &n, uint32_t j) { return j < 2 ? n.kw[2 + j] : n.kc[j - 2]; }
 
