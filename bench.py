@@ -208,7 +208,8 @@ def main():
             sub = ts.slice(0, lb)
             # caller-owned result buffers reused across batches (the C ABI's
             # contract; a NIF keeps them per scheduler)
-            bufs = (np.zeros(lb + 1, np.uint64), np.zeros(64 * lb + 1024, np.uint32), np.zeros(lb, np.uint8))
+            _, v0, _ = ix.match_batch(sub.blob, sub.offs)          # sizes the value buffer
+            bufs = (np.zeros(lb + 1, np.uint64), np.zeros(len(v0) + 1024, np.uint32), np.zeros(lb, np.uint8))
             xs = []
             for k in range(a.latency_batches + 2):
                 t1 = time.perf_counter()
