@@ -22,8 +22,8 @@ from __future__ import annotations
 import numpy as np
 
 from . import _native
-from .trie_search import (BadArg, HASH, PLUS, get_id, get_topic, key_order, make_key,  # noqa: F401
-                          term_key, topic_words)
+from .trie_search import (BadArg, HASH, PLUS, filter_words, get_id, get_topic, key_order,  # noqa: F401
+                          make_key, search_filter, term_key, topic_words)
 
 
 class Tab:
@@ -37,6 +37,7 @@ class Tab:
         self._free: list[int] = []
         self._dead: set = set()         # keys that can never match (kept host-side only)
         self._ops: list = []            # pending (op, filter_bytes, kid, flags)
+        self._sorted = None             # (keys, order keys) in term order, for matches_filter/3
 
     # -- key <-> device encoding
     @staticmethod
@@ -81,6 +82,7 @@ class Tab:
     # -- table operations
     def insert_key(self, key, record):
         if key not in self._records:
+            self._sorted = None
             kid = self._free.pop() if self._free else len(self._keys)
             if kid == len(self._keys):
                 self._keys.append(key)
@@ -92,6 +94,7 @@ class Tab:
 
     def delete_key(self, key):
         if key in self._records:
+            self._sorted = None
             kid = self._kid.pop(key)
             del self._records[key]
             self._queue(_native.TM_OP_DELETE, key, kid)
@@ -103,6 +106,13 @@ class Tab:
 
     def keys(self):
         return list(self._records)
+
+    def sorted_keys(self):
+        """every key of the table in Erlang term order (the ordered_set view)"""
+        if self._sorted is None:
+            keys = sorted(self._records, key=key_order)
+            self._sorted = (keys, [key_order(k) for k in keys])
+        return self._sorted
 
     def lookup(self, key):
         return [self._records[key]] if key in self._records else []
@@ -175,10 +185,25 @@ def match(topic, tab: Tab):
     return keys[-1] if keys else False
 
 
+def matches_filter(filter_, tab: Tab, opts=()):
+    """matches_filter/3 (emqx_topic_index.erl:82-84 -> emqx_trie_search.erl:186-189):
+    the index keys a subscription to `filter_` covers, by the reference's
+    ordered search (filter_words/1, base_init/1, compare/3 with the filter
+    clauses :291-300, no match_topics phase -- binary keys never match).
+
+    A host-side call over the table's ordered key set, not the publish path:
+    its result depends on where the ordered walk stops (a stored key below the
+    query at a query '+' ends the whole search), which the device NFA walk has
+    no notion of.  Callers are control-plane (durable-storage stream
+    discovery, emqx_ds_new_streams.erl:325)."""
+    keys, order = tab.sorted_keys()
+    return _finish(search_filter(keys, order, filter_words(filter_)), opts)
+
+
 def get_record(key, tab: Tab):
     """get_record/2: [Record] or [] if the entry was deleted meanwhile."""
     return tab.lookup(key)
 
 
-__all__ = ["new", "insert", "delete", "match", "matches", "matches_batch", "make_key", "get_id",
+__all__ = ["new", "insert", "delete", "match", "matches", "matches_batch", "matches_filter", "make_key", "get_id",
            "get_topic", "get_record", "Tab", "BadArg"]

@@ -32,6 +32,8 @@ def load():
         lib.orc_prepare.argtypes = [vp]
         lib.orc_matches.argtypes = [vp, C.c_char_p, u32, vp, i64]
         lib.orc_matches.restype = i64
+        lib.orc_matches_filter.argtypes = [vp, C.c_char_p, u32, vp, i64]
+        lib.orc_matches_filter.restype = i64
         lib.orc_first.argtypes = [vp, C.c_char_p, u32, vp]
         lib.orc_first.restype = C.c_int
         lib.orc_match_batch.argtypes = [vp, vp, vp, i64, vp, vp, vp, vp, C.c_int]
@@ -88,6 +90,16 @@ class Oracle:
             r = self._l.orc_matches(self._h, topic, len(topic), _p(out), cap)
             if r < 0:
                 return None
+            if r <= cap:
+                return out[:r].tolist()
+            cap = int(r)
+
+    def matches_filter(self, flt: bytes):
+        """matches_filter/3 values in traversal order (the query split by filter_words/1)"""
+        cap = 64
+        while True:
+            out = np.empty(cap, np.uint32)
+            r = self._l.orc_matches_filter(self._h, flt, len(flt), _p(out), cap)
             if r <= cap:
                 return out[:r].tolist()
             cap = int(r)

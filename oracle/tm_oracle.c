@@ -17,6 +17,7 @@
  *        match_add (traversal order) ...... emqx_trie_search.erl:350-356
  *        topic_words / word (badarg) ...... emqx_trie_search.erl:369-378
  *        match_topics (exact keys) ........ emqx_trie_search.erl:381-389
+ *        matches_filter / filter clauses .. emqx_trie_search.erl:186-189, 291-300, 358-366
  *      over an ordered set with "next key strictly greater than K"
  *      (ets:next/2 on the ordered_set of emqx_topic_index.erl:41-48,108-109),
  *      here a sorted array + binary search, ordered by Erlang term order:
@@ -415,6 +416,65 @@ static int64_t walk(const oindex *h, const uint8_t *t, uint32_t tl, twords *tw, 
             cur = next_key(h, &tb);
         } else return a->n;
     }
+}
+
+/* ------------------------------------------------- matches_filter/3 */
+
+/* compare/3 with a FILTER as the query (emqx_trie_search.erl:260-348 incl.
+ * the filter clauses :291-300): query words may be the atoms '+' / '#'.
+ * Clause order decides: [] / ['#'] stored first, then a query ['#'] matches
+ * anything, a query '+' passes the stored word over (and does NOT turn a
+ * 'lower' into a seek), a stored '+' does (seek to the query word there). */
+static int64_t compare_filter(const okey *k, const oword *qw, uint32_t nq) {
+    if (k->form == FORM_BIN) return C_LOWER;                  /* :260-261 */
+    witer it; oword fw; wit_init(&it, k);
+    int64_t lastplus = -1;
+    for (uint32_t i = 0;; i++) {
+        int hf = wit_next(&it, &fw);
+        if (!hf) return i == nq ? C_FULL : C_PREFIX;          /* :262-281 */
+        if (fw.kind == WK_HASH && it.left == 0) return C_FULL;/* :282-290 */
+        if (i < nq && qw[i].kind == WK_HASH && i == nq - 1) return C_FULL; /* :292-293 */
+        if (i == nq) break;                                   /* :333-340 lower */
+        if (qw[i].kind == WK_PLUS) continue;                  /* :294-300 */
+        if (fw.kind == WK_PLUS) { lastplus = i; continue; }   /* :302-320 */
+        int c = word_cmp(&fw, &qw[i]);
+        if (c == 0) continue;                                 /* :321-324 */
+        if (c > 0) break;                                     /* :325-332 lower */
+        return (int64_t)i;                                    /* :341-348 seek */
+    }
+    return lastplus >= 0 ? lastplus : C_LOWER;
+}
+
+/* emqx_topic_index:matches_filter/3 (search with [topic_filter], no
+ * match_topics phase): ids in traversal order.  The query is a binary split
+ * by filter_words/1 ('+' / '#' levels become the atoms). */
+int64_t orc_matches_filter(void *hp, const char *f, uint32_t fl, uint32_t *out, int64_t cap) {
+    oindex *h = hp; flush(h);
+    uint32_t nq = count_words(f, fl);
+    oword *qw = malloc(sizeof(oword) * nq);
+    uint32_t s0 = 0, q = 0;
+    for (uint32_t i = 0; i <= fl; i++)
+        if (i == fl || f[i] == '/') {
+            qw[q].p = (const uint8_t *)f + s0; qw[q].n = i - s0; qw[q].kind = word_kind(qw[q].p, qw[q].n);
+            q++; s0 = i + 1;
+        }
+    oacc a = {out, 0, cap, 0, 0};
+    okey base; memset(&base, 0, sizeof base);
+    base.form = FORM_LIST; base.base = 1;
+    if (qw[0].kind == WK_BIN && qw[0].n >= 1 && qw[0].p[0] == '$') {   /* base_init :160-163 */
+        base.b = qw[0].p; base.len = qw[0].n; base.nw = 1;
+    } else { base.b = (const uint8_t *)""; base.len = 0; base.nw = 0; }
+    int64_t cur = next_key(h, &base);
+    while (cur >= 0) {
+        const okey *k = &h->keys[cur];
+        int64_t c = compare_filter(k, qw, nq);
+        if (c == C_FULL) { acc_add(&a, k->id); cur = next_key(h, k); }
+        else if (c == C_PREFIX) cur = next_key(h, k);
+        else if (c == C_LOWER) break;
+        else { okey sk = seek_key(k, (uint32_t)c, qw[c].p, qw[c].n, &a); cur = next_key(h, &sk); }
+    }
+    free(a.scratch); free(qw);
+    return a.n;
 }
 
 static __thread twords *tls_tw;

@@ -622,3 +622,27 @@ def test_batches_on_two_streams_see_patches_in_order(torch_dev):
         h = hit.cpu().numpy().view(np.uint64)
         assert np.array_equal(h, ohit.astype(np.uint64))
         assert np.array_equal(out.cpu().numpy().view(np.uint32)[: int(h[-1])], ovals)
+
+
+def test_topic_index_matches_filter(torch_dev):
+    """matches_filter/3 through the topic_index API (emqx_topic_index.erl:82-84)
+    on a device-backed table after inserts and deletes: the reverse of the
+    oracle's traversal order, and publishes still match on the same table."""
+    r = random.Random(0x454D5158 + 900)
+    tab = ti.new()
+    o = Oracle()
+    rf = lambda: _rand_filter(r, [_rand_level(r) for _ in range(r.randint(1, 4))])   # noqa: E731
+    filters = [rf() for _ in range(400)]
+    for i, f in enumerate(filters):
+        ti.insert(f, i, b"", tab)
+        o.insert(f, i, 0)
+    for i in r.sample(range(len(filters)), 80):
+        ti.delete(filters[i], i, tab)
+        o.delete(filters[i], i, 0)
+    for q in [b"#", b"+/#", b"foo/+", b"$SYS/#", b"+/+/+"] + [rf() for _ in range(40)]:
+        got = [get_id(k) for k in ti.matches_filter(q, tab)]
+        assert got == o.matches_filter(q)[::-1], q
+        uniq = [get_id(k) for k in ti.matches_filter(q, tab, ["unique"])]
+        assert uniq == sorted(set(got)), q
+    t = b"foo/bar/1"
+    assert sorted(get_id(k) for k in ti.matches(t, tab, [])) == sorted(o.matches(t))
