@@ -21,7 +21,7 @@ TM_KEY_BINARY, TM_KEY_WORDS, TM_KEY_EMPTY_LIST = 0, 1, 2
 # every symbol include/tmatch.h declares (tests check the export table)
 EXPORTS = ("tm_create", "tm_destroy", "tm_apply_deltas", "tm_sync", "tm_match_batch",
            "tm_match_batch_dev", "tm_first_batch", "tm_stats", "tm_profile_enable", "tm_profile_read",
-           "tm_last_error", "tm_abi_version", "tm_merge_shards")
+           "tm_last_error", "tm_abi_version", "tm_merge_shards", "tm_host_alloc", "tm_host_free")
 
 
 class NativeUnavailable(RuntimeError):
@@ -73,6 +73,8 @@ def load_library(path: Path | None = None):
         "tm_last_error": (C.c_char_p, [vp]),
         "tm_abi_version": (u32, []),
         "tm_merge_shards": (i32, [u32, u64, vp, vp, u64, vp, vp, u64, vp]),
+        "tm_host_alloc": (i32, [vp, u64, C.POINTER(vp)]),
+        "tm_host_free": (i32, [vp, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -135,6 +137,7 @@ class Index:
 
     def close(self):
         if getattr(self, "_h", None):
+            self._pinned = []   # tm_destroy frees the tm_host_alloc buffers
             self._lib.tm_destroy(self._h)
             self._h = None
 
@@ -158,6 +161,28 @@ class Index:
 
     def sync(self, stream: int | None = None):
         self._check(self._lib.tm_sync(self._h, stream))
+
+    # ---- pinned host buffers (tm_host_alloc)
+    def host_array(self, n: int, dtype) -> np.ndarray:
+        """A numpy array in pinned host memory mapped into the device.  Batches
+        whose buffers (topics 16-byte aligned, offsets, outputs) all come from
+        here run in place, without staging copies (include/tmatch.h).  Valid
+        until host_free() or close()."""
+        dtype = np.dtype(dtype)
+        nbytes = max(int(n), 1) * dtype.itemsize
+        p = C.c_void_p()
+        self._check(self._lib.tm_host_alloc(self._h, nbytes, C.byref(p)))
+        buf = (C.c_uint8 * nbytes).from_address(p.value)
+        a = np.frombuffer(buf, dtype=dtype, count=max(int(n), 1))
+        if not hasattr(self, "_pinned"):
+            self._pinned = []
+        self._pinned.append(p.value)
+        return a
+
+    def host_free(self, a: np.ndarray):
+        addr = a.__array_interface__["data"][0]
+        self._check(self._lib.tm_host_free(self._h, C.c_void_p(addr)))
+        self._pinned.remove(addr)
 
     # ---- matching (host buffers)
     def match_batch(self, blob: np.ndarray, offs: np.ndarray, cap: int | None = None, out=None):

@@ -110,6 +110,9 @@ struct tm_index {
     uint8_t *d_in = nullptr; uint64_t d_in_cap = 0;
     uint8_t *d_res = nullptr; uint64_t d_res_cap = 0;
     uint32_t *pin_vals = nullptr, *pin_vals_dev = nullptr; uint64_t pin_vals_cap = 0;
+    // caller buffers from tm_host_alloc (host address -> size, device address)
+    struct Pinned { uint8_t *host, *dev; uint64_t size; };
+    std::vector<Pinned> pinned;
 
     // diagnostics (tm_profile_*)
     bool prof = false;
@@ -923,7 +926,7 @@ int prof_end(tm_index *ix, tm_index::ProfEv &ev, hipStream_t s) {
 
 extern "C" {
 
-uint32_t tm_abi_version(void) { return (1u << 16) | 1u; }
+uint32_t tm_abi_version(void) { return (1u << 16) | 2u; }
 
 const char *tm_last_error(tm_index *h) { return h ? h->err.c_str() : g_last_error.c_str(); }
 
@@ -966,6 +969,7 @@ int tm_destroy(tm_index *ix) {
     }
     void *pins[] = {ix->pin_addr, ix->pin_val, ix->pin_in, ix->pin_out, ix->pin_vals};
     for (void *p : pins) if (p) (void)hipHostFree(p);
+    for (auto &b : ix->pinned) (void)hipHostFree(b.host);
     (void)hipEventDestroy(ix->patch_done);
     (void)hipStreamDestroy(ix->stream);
     delete ix;
@@ -1026,7 +1030,9 @@ namespace {
 // memory over PCIe.  A small batch then costs its kernels plus one host
 // synchronisation -- no copy commands and no gaps between them.  Larger
 // batches move in one H2D and one D2H transfer.
-constexpr uint64_t ZC_TOPICS = 65536;
+#ifndef ZC_TOPICS
+#define ZC_TOPICS 65536
+#endif
 
 int pin_mapped(tm_index *ix, hipStream_t s, uint8_t *&host, uint8_t *&dev, uint64_t &cap, uint64_t need) {
     if (need <= cap) return TM_OK;
@@ -1081,6 +1087,43 @@ int fetch_out(tm_index *ix, uint64_t n, uint64_t bytes, hipStream_t s) {
 
 }  // namespace
 
+// device address of [p, p + bytes) if the range lies in one tm_host_alloc buffer
+static uint8_t *pinned_dev(tm_index *ix, const void *p, uint64_t bytes) {
+    const uint8_t *q = static_cast<const uint8_t *>(p);
+    for (const auto &b : ix->pinned)
+        if (q >= b.host && bytes <= b.size && q - b.host <= (ptrdiff_t)(b.size - bytes)) return b.dev + (q - b.host);
+    return nullptr;
+}
+
+int tm_host_alloc(tm_index *ix, uint64_t bytes, void **out) {
+    if (!ix || !out) return fail(ix, TM_EINVAL, "tm_host_alloc: null argument");
+    *out = nullptr;
+    std::lock_guard<std::mutex> g(ix->mu);
+    HIPCHK(ix, hipSetDevice(ix->device));
+    void *h = nullptr, *d = nullptr;
+    if (hipHostMalloc(&h, bytes ? bytes : 1, hipHostMallocMapped) != hipSuccess || !h)
+        return fail(ix, TM_ENOMEM, "tm_host_alloc: hipHostMalloc failed");
+    HIPCHK(ix, hipHostGetDevicePointer(&d, h, 0));
+    ix->pinned.push_back({static_cast<uint8_t *>(h), static_cast<uint8_t *>(d), bytes});
+    *out = h;
+    return TM_OK;
+}
+
+int tm_host_free(tm_index *ix, void *p) {
+    if (!ix) return fail(nullptr, TM_EINVAL, "tm_host_free: null handle");
+    if (!p) return TM_OK;
+    std::lock_guard<std::mutex> g(ix->mu);
+    for (size_t i = 0; i < ix->pinned.size(); i++) {
+        if (ix->pinned[i].host != p) continue;
+        HIPCHK(ix, hipSetDevice(ix->device));
+        HIPCHK(ix, hipStreamSynchronize(ix->stream));   // no batch may still write it
+        HIPCHK(ix, hipHostFree(p));
+        ix->pinned.erase(ix->pinned.begin() + i);
+        return TM_OK;
+    }
+    return fail(ix, TM_EINVAL, "tm_host_free: not a tm_host_alloc buffer of this index");
+}
+
 // TM_HOST_TIMING=1: per-phase host timings of tm_match_batch on stderr (diagnostics)
 static double now_us() {
     return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
@@ -1102,6 +1145,36 @@ int tm_match_batch(tm_index *ix, uint64_t n, const uint8_t *tb, const uint64_t *
     Workspace *ws;
     if ((rc = ensure_ws(ix, n, s, ws))) return rc;
     if (timing) tt[nt++] = now_us();
+    if (n && n <= ZC_TOPICS) {
+        // every buffer from tm_host_alloc: the kernels read the topics and
+        // write the hit lists in place (no staging copy in, no copy out)
+        const uint64_t nbytes = to[n];
+        uint8_t *db = nbytes ? pinned_dev(ix, tb, nbytes) : nullptr;
+        uint8_t *dof = pinned_dev(ix, to, (n + 1) * 8);
+        uint8_t *dh = pinned_dev(ix, out_hit, (n + 1) * 8);
+        uint8_t *dv = out_vals ? pinned_dev(ix, out_vals, cap * 4) : nullptr;
+        uint8_t *de = out_err ? pinned_dev(ix, out_err, n) : nullptr;
+        const bool aligned = ((uintptr_t)tb & 15) == 0;
+        if ((db || !nbytes) && aligned && dof && dh && (dv || !out_vals) && (de || !out_err)) {
+            if (!de) {   // flags nobody reads still need a home
+                if ((rc = stage_out(ix, n, n, s, de))) return rc;
+            }
+            const DevIndex d = dev_view(ix);
+            const uint8_t *dbytes = db ? db : dof;   // no bytes: any valid address
+            uint64_t *dhit = reinterpret_cast<uint64_t *>(dh);
+            HIPCHK(ix, launch_match_phase1(d, *ws, n, dbytes, reinterpret_cast<const uint64_t *>(dof), dhit, de, s));
+            HIPCHK(ix, launch_match_phase2(d, *ws, n, dbytes, reinterpret_cast<const uint64_t *>(dof), dhit,
+                                           reinterpret_cast<uint32_t *>(dv), dv ? cap : 0, s));
+            if (timing) tt[nt++] = now_us();
+            HIPCHK(ix, hipStreamSynchronize(s));
+            if (timing) {
+                tt[nt++] = now_us();
+                fprintf(stderr, "tm_match_batch n=%lu (in place): sync %.1f launch %.1f wait %.1f us\n",
+                        (unsigned long)n, tt[1] - tt[0], tt[2] - tt[1], tt[3] - tt[2]);
+            }
+            return (out_vals && out_hit[n] > cap) ? TM_ECAP : TM_OK;
+        }
+    }
     const uint8_t *dbytes;
     const uint64_t *doffs;
     if ((rc = stage_in(ix, n, tb, to, s, dbytes, doffs))) return rc;

@@ -352,6 +352,10 @@ __device__ bool dfs(const DevIndex &ix, uint32_t L, bool dollar, S &st, EM &em) 
 #ifdef TM_STUDY_DEAD
     bool via_plus = false;   // study: how the current node was reached
 #endif
+#ifdef TM_STUDY_LEAF
+    uint32_t via = 2;        // study: 0 '+', 1 child table, 2 inline child
+    uint64_t via_ct = 0;     // study: pushed literal branches that came from a child table
+#endif
     for (;;) {
 #ifdef TM_STUDY
         if constexpr (S::deferred) st.n_steps++;
@@ -372,6 +376,9 @@ __device__ bool dfs(const DevIndex &ix, uint32_t L, bool dollar, S &st, EM &em) 
         uint32_t inl = n2.x == w ? n3.x : n2.y == w ? n3.y : n2.z == w ? n3.z : n2.w == w ? n3.w : NONE;
         pin(inl);
         if (l == L) {
+#ifdef TM_STUDY_LEAF
+            if constexpr (S::deferred) { if (via == 1) st.n_steps += 1u << 16; else st.n_probe++; }
+#endif
             if (!em(n0.w, n1.x)) return false;
             if (!droot && !em(n0.y, n0.z)) return false;
         } else {
@@ -391,7 +398,7 @@ __device__ bool dfs(const DevIndex &ix, uint32_t L, bool dollar, S &st, EM &em) 
                             lit = NONE;
 #endif
                     }
-#if defined(TM_STUDY) && !defined(TM_STUDY_DEAD)
+#if defined(TM_STUDY) && !defined(TM_STUDY_DEAD) && !defined(TM_STUDY_LEAF)
                     if constexpr (S::deferred) {
                         if (m & 1u) { if (lit != NONE) st.n_steps += 1u << 16; else st.n_probe++; }
                     }
@@ -413,8 +420,14 @@ __device__ bool dfs(const DevIndex &ix, uint32_t L, bool dollar, S &st, EM &em) 
             }
 #endif
             if (plus != NONE) {
+#ifdef TM_STUDY_LEAF
+                if (lit != NONE) via_ct = (via_ct & ~(1ull << (l + 1))) | ((uint64_t)(n1.y > KINL) << (l + 1));
+#endif
                 if (lit != NONE) st.push(l + 1, lit);
                 cur = plus; l++;
+#ifdef TM_STUDY_LEAF
+                via = 0;
+#endif
 #ifdef TM_STUDY_DEAD
                 via_plus = true;
 #endif
@@ -422,6 +435,9 @@ __device__ bool dfs(const DevIndex &ix, uint32_t L, bool dollar, S &st, EM &em) 
             }
             if (lit != NONE) {
                 cur = lit; l++;
+#ifdef TM_STUDY_LEAF
+                via = n1.y <= KINL ? 2 : 1;
+#endif
 #ifdef TM_STUDY_DEAD
                 via_plus = false;
 #endif
@@ -432,6 +448,9 @@ __device__ bool dfs(const DevIndex &ix, uint32_t L, bool dollar, S &st, EM &em) 
         via_plus = false;
 #endif
         if (!st.pop(l, cur)) return true;
+#ifdef TM_STUDY_LEAF
+        via = ((via_ct >> l) & 1) ? 1 : 2;
+#endif
     }
 }
 

@@ -107,6 +107,16 @@ int tm_sync(tm_index *h, void *stream);
 int tm_match_batch(tm_index *h, uint64_t n, const uint8_t *topic_bytes, const uint64_t *topic_offsets,
                    uint64_t *out_hit_offsets, uint32_t *out_values, uint64_t cap, uint8_t *out_err);
 
+/* Pinned host buffers, mapped into the index's device.  A NIF keeps its
+ * per-scheduler batch buffers here: when every buffer given to tm_match_batch
+ * (topic bytes -- 16-byte aligned --, offsets, hit offsets, values and err if
+ * not NULL) lies in tm_host_alloc memory of the same index and n <= 65536, the
+ * kernels read the topics and write the hit lists in place: no staging copy
+ * in, no copy out.  Other batches take the staged path; results are the same.
+ * tm_host_free waits for the index's batches to finish first. */
+int tm_host_alloc(tm_index *h, uint64_t bytes, void **out);
+int tm_host_free(tm_index *h, void *p);
+
 /* Device-resident batch: every pointer is device memory; asynchronous on
  * `stream` (hipStream_t; NULL = the index's own stream).  d_out_hit_offsets has
  * n+1 entries and d_out_hit_offsets[n] is the total; values beyond `cap` are

@@ -46,3 +46,5 @@ def test_null_handle_is_einval():
     assert lib.tm_destroy(None) == _native.TM_EINVAL
     assert lib.tm_apply_deltas(None, 0, None, None, None, None, None) == _native.TM_EINVAL
     assert lib.tm_match_batch(None, 0, None, None, None, None, 0, None) == _native.TM_EINVAL
+    assert lib.tm_host_alloc(None, 16, None) == _native.TM_EINVAL
+    assert lib.tm_host_free(None, None) == _native.TM_EINVAL

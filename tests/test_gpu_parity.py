@@ -428,6 +428,47 @@ def test_host_batches_zero_copy_and_staged_agree(torch_dev):
             assert np.array_equal(h2, hit) and np.array_equal(v2, vals) and not e2.any()
 
 
+def test_host_batches_in_place_pinned_buffers(torch_dev):
+    """Buffers from tm_host_alloc: batches <= 65536 topics run in place (the
+    kernels read the caller's topics and write its hit lists), others take the
+    staged path; a misaligned topic blob falls back to staging; a short value
+    buffer gives TM_ECAP with complete offsets and the first `cap` values.
+    Every case gives the oracle's results."""
+    fs = wl.filters(3, 20_000)
+    ix, o = gpu_index(fs), oracle_of(fs)
+    for nt in (1, 4096, 65536, 65537):
+        ts = wl.topics(3, 20_000, nt)
+        hit, vals = assert_same(ix, o, ts)
+        nb = int(ts.offs[-1])
+        pb = ix.host_array(nb + 32, np.uint8)
+        po = ix.host_array(nt + 1, np.uint64)
+        ph = ix.host_array(nt + 1, np.uint64)
+        pv = ix.host_array(len(vals) + 5, np.uint32)
+        pe = ix.host_array(nt, np.uint8)
+        pb[:nb] = ts.blob[:nb]
+        po[:] = ts.offs
+        for _ in range(2):
+            ph[:] = 0
+            pe[:] = 7
+            h2, v2, e2 = ix.match_batch(pb, po, out=(ph, pv, pe))
+            assert np.array_equal(h2, hit) and np.array_equal(v2, vals) and not e2.any()
+        # misaligned blob (offsets shifted by one byte): staged, same results
+        pb[1:nb + 1] = ts.blob[:nb]
+        h3, v3, _ = ix.match_batch(pb[1:], po, out=(ph, pv, pe))
+        assert np.array_equal(h3, hit) and np.array_equal(v3, vals)
+        # too small a value buffer
+        if len(vals) > 3:
+            pb[:nb] = ts.blob[:nb]
+            rc = ix._lib.tm_match_batch(ix._h, nt, _native._ptr(pb), _native._ptr(po), _native._ptr(ph),
+                                        _native._ptr(pv), 3, _native._ptr(pe))
+            assert rc == _native.TM_ECAP
+            assert np.array_equal(ph, hit) and np.array_equal(pv[:3], vals[:3])
+        for a in (pb, po, ph, pv, pe):
+            ix.host_free(a)
+    with pytest.raises(_native.TmError):
+        ix.host_free(np.zeros(4, np.uint8))
+
+
 def test_wave_walk_limits_fall_back_exactly(torch_dev):
     """Batches of <= 8192 topics take the wave-per-topic walk (16 lanes per
     topic); its limits (a frontier wider than the group, more hit ranges than

@@ -54,6 +54,19 @@ def main():
         ix._lib.tm_match_batch(*args)
         xs.append((time.perf_counter() - t1) * 1e3)
     report("tm_match_batch (reused outputs)", xs)
+    # every buffer from tm_host_alloc: the batch runs in place
+    nb = int(offs[-1] - offs[0])
+    pb, po = ix.host_array(nb + 16, np.uint8), ix.host_array(n + 1, np.uint64)
+    pb[:nb] = blob[int(offs[0]):int(offs[-1])]
+    po[:] = offs - offs[0]
+    ph, pv, pe = ix.host_array(n + 1, np.uint64), ix.host_array(cap, np.uint32), ix.host_array(n, np.uint8)
+    args = (ix._h, n, _ptr(pb), _ptr(po), _ptr(ph), _ptr(pv), cap, _ptr(pe))
+    xs = []
+    for _ in range(a.reps):
+        t1 = time.perf_counter()
+        ix._lib.tm_match_batch(*args)
+        xs.append((time.perf_counter() - t1) * 1e3)
+    report("tm_match_batch (tm_host_alloc buffers, in place)", xs)
 
 
 if __name__ == "__main__":

@@ -28,6 +28,11 @@ def main():
         print(f"{cfg}: dead-end visits (emit nothing, lead nowhere) reached via '+' mean {dp.mean():.2f}, "
               f"via a literal edge or a pop mean {dl.mean():.2f} (each capped at 15)", flush=True)
         return
+    if os.environ.get("TM_STUDY_LEAF"):
+        ct, other = (err & 15).astype(np.int64), (err >> 4).astype(np.int64)
+        print(f"{cfg}: visits at the topic's last level (emit only) reached through a child table mean "
+              f"{ct.mean():.2f}, through '+' or an inline child mean {other.mean():.2f} (each capped at 15)", flush=True)
+        return
     if os.environ.get("TM_STUDY_HITS"):
         hits_, miss_ = (err & 15).astype(np.int64), (err >> 4).astype(np.int64)
         print(f"{cfg}: child-table probes that found the child mean {hits_.mean():.2f}, "
