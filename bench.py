@@ -55,14 +55,14 @@ def log(*a):
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--steps", type=int, default=100)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     p.add_argument("--filters", type=int, default=None)
     p.add_argument("--batch", type=int, default=1_000_000, help="topics per GPU per step")
     p.add_argument("--deltas", type=int, default=100,
                    help="c5: deltas applied per step (100 x ~2.5k steps/s = 2.5x the configured 100k deltas/s)")
-    p.add_argument("--streams", type=int, default=2,
+    p.add_argument("--streams", type=int, default=3,
                    help="HIP streams the steps rotate over (batch k+1's walk overlaps batch k's scan/emit)")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     p.add_argument("--cpu-threads", type=int, default=16)

@@ -392,13 +392,27 @@ __device__ bool dfs(const DevIndex &ix, uint32_t L, bool dollar, S &st, EM &em) 
                     if (m & 1u) {
                         uint32_t slo, shi;
                         lit = ctab_find(ix, n2.x, n2.y, w, h, slo, shi);
+#ifdef TM_STUDY_MISS   // study: probes that find no child, by level (1), or at l >= 3 / found but dead (2)
+                        if constexpr (S::deferred) {
+                            const bool absent = lit == NONE;
+                            const bool dead = !absent && !child_alive(slo, shi, l + 1, L,
+                                l + 1 < L ? st.get_wid(l + 1) : NONE, l + 2 < L ? st.get_wid(l + 2) : NONE);
+                            if (TM_STUDY_MISS == 1) {
+                                if (absent && l <= 1) st.n_steps += 1u << 16;
+                                if (absent && l == 2) st.n_probe++;
+                            } else {
+                                if (absent && l >= 3) st.n_steps += 1u << 16;
+                                if (dead) st.n_probe++;
+                            }
+                        }
+#endif
 #ifndef TM_NO_PSUM
                         if (lit != NONE && !child_alive(slo, shi, l + 1, L, l + 1 < L ? st.get_wid(l + 1) : NONE,
                                                         l + 2 < L ? st.get_wid(l + 2) : NONE))
                             lit = NONE;
 #endif
                     }
-#if defined(TM_STUDY) && !defined(TM_STUDY_DEAD) && !defined(TM_STUDY_LEAF)
+#if defined(TM_STUDY) && !defined(TM_STUDY_DEAD) && !defined(TM_STUDY_LEAF) && !defined(TM_STUDY_MISS)
                     if constexpr (S::deferred) {
                         if (m & 1u) { if (lit != NONE) st.n_steps += 1u << 16; else st.n_probe++; }
                     }

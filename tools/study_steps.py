@@ -28,6 +28,13 @@ def main():
         print(f"{cfg}: dead-end visits (emit nothing, lead nowhere) reached via '+' mean {dp.mean():.2f}, "
               f"via a literal edge or a pop mean {dl.mean():.2f} (each capped at 15)", flush=True)
         return
+    if os.environ.get("TM_STUDY_MISS"):
+        a, b = (err & 15).astype(np.int64), (err >> 4).astype(np.int64)
+        what = (("absent at levels 0-1", "absent at level 2") if os.environ["TM_STUDY_MISS"] == "1"
+                else ("absent at levels >= 3", "found but dead (any level)"))
+        print(f"{cfg}: child-table probes {what[0]} mean {a.mean():.2f}, {what[1]} mean {b.mean():.2f} "
+              f"(each capped at 15)", flush=True)
+        return
     if os.environ.get("TM_STUDY_LEAF"):
         ct, other = (err & 15).astype(np.int64), (err >> 4).astype(np.int64)
         print(f"{cfg}: visits at the topic's last level (emit only) reached through a child table mean "
