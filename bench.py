@@ -183,6 +183,14 @@ def main():
     if world > 1:
         dist.barrier()
     walk_ms, batch_ms, nb = ix.profile_read(reset=True)
+    # the same kernel alone: a few batches on one stream, one after another
+    # (with several streams a launch's duration includes the GPU time it
+    # shares with the other streams' kernels)
+    for _ in range(5):
+        ix.match_batch_dev(B, d_blob.data_ptr(), d_offs.data_ptr(), outs[0]["hit"].data_ptr(),
+                           outs[0]["out"].data_ptr(), cap, outs[0]["err"].data_ptr(), stream)
+        torch.cuda.synchronize()
+    iso_walk_ms, _, iso_nb = ix.profile_read(reset=True)
     ix.profile(False)
     el_t = torch.tensor([el], dtype=torch.float64, device=dev)
     if world > 1:
@@ -284,6 +292,11 @@ def main():
         F_total = float(states.sum()) * B / ns
         walk_bytes = 8 * L_total + 32 * F_total + 4 * B
         achieved = walk_bytes / (walk_avg_ms * 1e-3) / 1e9
+        iso_ms = iso_walk_ms / max(iso_nb, 1)
+        res_extra["walk_isolated"] = {"kernel_avg_ms": round(iso_ms, 4),
+                                      "achieved_GBps": round(walk_bytes / (iso_ms * 1e-3) / 1e9, 1),
+                                      "frac": round(walk_bytes / (iso_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                                      "note": "k_walk_fast alone: 5 batches on one stream after the timed region"}
         res_extra["full_path_GBps"] = round((walk_bytes + 4 * last_hits) / (batch_avg_ms * 1e-3) / 1e9, 1)
         # the walk's algorithmic bytes over the wall time of a step: with steps
         # overlapping on several streams a launch's own duration overstates its

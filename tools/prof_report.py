@@ -70,16 +70,17 @@ def main(prof, rnd, tag, config, filters, batch):
         lines += ["## bench.py line (run under rocprofv3 --kernel-trace --stats)", "", "```",
                   open(bench_json).read().strip(), "```", ""]
     durations = {}
-    for sub, title in (("bench", "bench.py --steps 10 --warmup 2 (includes the 4k/64k latency batches)"),
+    for sub, title in (("bench", "bench.py with its defaults (includes the 4k/64k latency batches and the isolated walk batches)"),
                        ("trace", "tools/profile_walk.py (full batches only)")):
         p = os.path.join(prof, sub, "run_kernel_trace.csv")
         if not os.path.isfile(p):
             continue
         tab, agg = trace_table(p)
         lines += [f"## Kernel trace: {title}", ""] + tab + [""]
-        for (name, g), d in agg.items():
-            if g == grid:
-                durations.setdefault(name, []).extend(d)
+        if sub == "trace":   # the driver the PMC passes ran: kernels alone on one stream
+            for (name, g), d in agg.items():
+                if g == grid:
+                    durations.setdefault(name, []).extend(d)
         st = os.path.join(prof, sub, "run_kernel_stats.csv")
         if os.path.isfile(st):
             shutil.copy(st, os.path.join("profiles", f"{rnd}_{tag}_{sub}_kernel_stats.csv"))
@@ -116,7 +117,9 @@ def main(prof, rnd, tag, config, filters, batch):
                 lines[-1] += (f"; waves parked on waitcnt {c.get('SQ_WAIT_ANY', 0) / c['SQ_WAVE_CYCLES'] * 100:.0f}% "
                               f"of wave-cycles, VMEM reads {c.get('SQ_INSTS_VMEM_RD', 0) / c.get('SQ_WAVES', 1):.0f}/wave")
             if dur and c.get("GRBM_GUI_ACTIVE"):
-                lines[-1] += f"; clock ~{c['GRBM_GUI_ACTIVE'] / 8 / dur / 1e9:.2f} GHz"
+                # the PMC passes run the kernel slower than the trace run, so
+                # GRBM cycles over the trace duration is not the clock
+                lines[-1] += f"; {c['GRBM_GUI_ACTIVE'] / 8 / 1e6:.2f} M GPU-busy cycles per XCD in the PMC pass"
         lines.append("")
         if walk:
             c = pm[walk[0]]
