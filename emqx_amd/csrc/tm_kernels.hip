@@ -991,8 +991,9 @@ constexpr int WR = 64 * RCAP;   // ranges per wave
 // One block = one tile of 256 topics: finishes the scan (tile prefix + local
 // exclusive scan -> hit_offs), then each wave flattens its 64 topics' value
 // ranges into LDS (sorted by output position) and every lane produces whole
-// aligned quads of the wave's CSR span: one LDS binary search per quad, four
-// value reads, one 16-byte store -- a wave writes 1 KiB per store instruction
+// aligned quads of the wave's CSR span: the quad's range found from the lane's
+// previous one (a few steps, else a binary search), four value reads, one
+// 16-byte store -- a wave writes 1 KiB per store instruction
 // whatever the per-topic hit counts are.  Positions of topics that overflowed
 // RCAP ranges are skipped (k_rewalk_tail writes them).
 __global__ __launch_bounds__(EMIT_BLOCK) void k_emit(DevIndex ix, Workspace ws, uint64_t n,
@@ -1034,15 +1035,23 @@ __global__ __launch_bounds__(EMIT_BLOCK) void k_emit(DevIndex ix, Workspace ws, 
     if (!R) return;
     const bool vec = (reinterpret_cast<uintptr_t>(out) & 15) == 0;
     const uint64_t q1 = (endp + 3) >> 2;
+    uint32_t r = 0;   // last range starting at or before the lane's position (positions only grow)
     for (uint64_t q = (base >> 2) + lane; q < q1; q += 64) {
         const uint64_t p0 = q << 2;
         const uint32_t first = (uint32_t)((p0 > base ? p0 : base) - base);
-        uint32_t lo = 0, hi = R - 1;            // last range starting at or before `first`
-        while (lo < hi) {
-            const uint32_t mid = (lo + hi + 1) >> 1;
-            if (s_rel[wv][mid] <= first) lo = mid; else hi = mid - 1;
+        // a lane moves 256 positions per iteration: a few steps forward cover
+        // long ranges (C2: 250 values), a binary search the rest
+        uint32_t k = 0;
+        while (k < 2 && r + 1 < R && s_rel[wv][r + 1] <= first) { r++; k++; }
+        if (r + 1 < R && s_rel[wv][r + 1] <= first) {
+            uint32_t lo = r + 1, hi = R - 1;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi + 1) >> 1;
+                if (s_rel[wv][mid] <= first) lo = mid; else hi = mid - 1;
+            }
+            r = lo;
         }
-        uint32_t r = lo, v[4];
+        uint32_t v[4];
         bool ok[4];
 #pragma unroll
         for (int k = 0; k < 4; k++) {
