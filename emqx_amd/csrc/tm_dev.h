@@ -36,8 +36,8 @@ struct Workspace {
     uint32_t *nr;         // [n] ranges per topic (RCAP+1 = overflow)
     uint2 *rng;           // [n * RCAP] (value offset, count)
     uint32_t *lists;      // [L_COUNT * n] topic lists
-    uint32_t *list_n;     // [L_COUNT] list lengths + [L_COUNT] reset ticket (zero between batches)
-    uint64_t *blk;        // [n / TILE + 2] tile hit totals -> exclusive tile prefixes
+    uint32_t *list_n;     // [L_COUNT] list lengths, [L_COUNT] reset ticket, [L_COUNT + 1] scan ticket (zero between batches)
+    uint64_t *blk;        // [n / TILE + 2] tile hit totals -> exclusive tile prefixes (zero between batches)
     uint32_t *deep_wid;   // [DEEP_LANES * MAX_LEVELS]
     uint2 *deep_stk;      // [DEEP_LANES * (MAX_LEVELS + 1)]
     uint64_t cap_n;

@@ -866,8 +866,8 @@ int ensure_ws(tm_index *ix, uint64_t n, hipStream_t s, Workspace *&out) {
     if (!w.deep_wid) {
         HIPCHK(ix, hipMalloc(&w.deep_wid, (uint64_t)DEEP_LANES * MAX_LEVELS * 4));
         HIPCHK(ix, hipMalloc(&w.deep_stk, (uint64_t)DEEP_LANES * (MAX_LEVELS + 1) * 8));
-        HIPCHK(ix, hipMalloc(&w.list_n, (L_COUNT + 1) * 4));
-        HIPCHK(ix, hipMemset(w.list_n, 0, (L_COUNT + 1) * 4));
+        HIPCHK(ix, hipMalloc(&w.list_n, (L_COUNT + 2) * 4));
+        HIPCHK(ix, hipMemset(w.list_n, 0, (L_COUNT + 2) * 4));
     }
     // the batch must see every patch shipped so far, whichever stream it went on
     if (ix->patched) HIPCHK(ix, hipStreamWaitEvent(s, ix->patch_done, 0));
@@ -880,6 +880,7 @@ int ensure_ws(tm_index *ix, uint64_t n, hipStream_t s, Workspace *&out) {
     HIPCHK(ix, hipMalloc(&w.rng, c * RCAP * 8));
     HIPCHK(ix, hipMalloc(&w.lists, c * L_COUNT * 4));
     HIPCHK(ix, hipMalloc(&w.blk, (c / TILE + 4) * 8));
+    HIPCHK(ix, hipMemset(w.blk, 0, (c / TILE + 4) * 8));   // zero between batches (k_emit)
     w.cap_n = c;
     return TM_OK;
 }

@@ -899,9 +899,14 @@ __device__ __forceinline__ void reset_lists_if_last(const Workspace &ws) {
 
 // topics deeper than FAST_L: blocks < MID_GRID take the MID list (LDS frontier,
 // <= MID_L levels), the rest take the DEEP list (global scratch, any depth)
+//
+// scan_hit != null (count mode, small batches): the grid's last block also
+// turns the nb tile totals into exclusive tile prefixes and writes the grand
+// total to scan_hit[n] -- k_scan_top's job, without its own launch.
 template <int MODE>
 __global__ __launch_bounds__(MID_BLOCK) void k_walk_tail(DevIndex ix, Workspace ws, uint64_t n,
-                                                         const uint8_t *blob, const uint64_t *offs, Outs o) {
+                                                         const uint8_t *blob, const uint64_t *offs, Outs o,
+                                                         uint64_t nb, uint64_t *scan_hit) {
     __shared__ uint32_t s_wid[MID_L * MID_BLOCK];
     __shared__ uint32_t s_pend[(MID_L + 1) * MID_BLOCK];
     __shared__ uint8_t s_len[MID_L * MID_BLOCK];
@@ -925,6 +930,29 @@ __global__ __launch_bounds__(MID_BLOCK) void k_walk_tail(DevIndex ix, Workspace 
         }
     }
     if (MODE == MODE_FIRST) reset_lists_if_last(ws);   // count mode: k_rewalk_tail resets
+    if (MODE == MODE_COUNT && scan_hit) {
+        __shared__ uint32_t s_last;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __threadfence();   // this block's tile additions before its ticket
+            s_last = atomicAdd(&ws.list_n[L_COUNT + 1], 1u) == gridDim.x - 1;
+        }
+        __syncthreads();
+        if (!s_last) return;
+        __threadfence();
+        uint64_t carry = 0;
+        for (uint64_t b0 = 0; b0 < nb; b0 += MID_BLOCK) {
+            const uint64_t i = b0 + threadIdx.x;
+            const uint64_t v = i < nb ? __hip_atomic_load(&ws.blk[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+            const uint64_t inc = wave_incl_scan(v);
+            if (i < nb) ws.blk[i] = carry + inc - v;
+            carry += __shfl(inc, 63, 64);
+        }
+        if (threadIdx.x == 0) {
+            scan_hit[n] = carry;
+            atomicExch(&ws.list_n[L_COUNT + 1], 0u);
+        }
+    }
 }
 
 // re-walk of topics with more than RCAP hit ranges: values go straight to the CSR
@@ -1012,6 +1040,9 @@ __global__ __launch_bounds__(EMIT_BLOCK) void k_emit(DevIndex ix, Workspace ws, 
     if (valid) hit_offs[t] = my;
     if (lane == 63) s_end[wv] = my + c;
     __syncthreads();
+    // every thread has read its tile prefix: leave the tile total zero for the
+    // next batch (the wave walk adds into it)
+    if (threadIdx.x == 0) ws.blk[blockIdx.x] = 0;
     const uint64_t t0 = t - lane;
     if (t0 >= n) return;   // whole wave leaves; only wave-level sync below
     const uint64_t base = __shfl(my, 0, 64);
@@ -1133,10 +1164,10 @@ hipError_t launch_match_phase1(const DevIndex &ix, const Workspace &ws, uint64_t
     hipError_t e;
     Outs o{err, nullptr, nullptr};
     const uint32_t nb = blocks_for(n, TILE);
+    // tile totals are zero between batches (k_emit leaves them so): the wave
+    // walk adds its topics' hits into them, the lane walk overwrites them
+    const bool wave = n && n <= WAVE_TOPICS;
     if (n) {
-        const bool wave = n <= WAVE_TOPICS;
-        // the wave walk adds its topics' hits into the tile totals
-        if (wave && (e = hipMemsetAsync(ws.blk, 0, (uint64_t)nb * 8, s)) != hipSuccess) return e;
         if (ev_walk0 && (e = hipEventRecord(ev_walk0, s)) != hipSuccess) return e;
         if (wave)
             hipLaunchKernelGGL((k_walk_wave<MODE_COUNT, WAVE_W>), dim3(blocks_for(n, WV_TOPICS_PER_BLOCK)),
@@ -1144,9 +1175,11 @@ hipError_t launch_match_phase1(const DevIndex &ix, const Workspace &ws, uint64_t
         else
             hipLaunchKernelGGL(k_walk_fast<MODE_COUNT>, dim3(nb), dim3(WALK_BLOCK), 0, s, ix, ws, n, bytes, offs, o);
         if (ev_walk1 && (e = hipEventRecord(ev_walk1, s)) != hipSuccess) return e;
-        hipLaunchKernelGGL(k_walk_tail<MODE_COUNT>, dim3(TAIL_GRID), dim3(MID_BLOCK), 0, s, ix, ws, n, bytes, offs, o);
+        // small batches: the tail kernel's last block also scans the (few) tile totals
+        hipLaunchKernelGGL(k_walk_tail<MODE_COUNT>, dim3(TAIL_GRID), dim3(MID_BLOCK), 0, s, ix, ws, n, bytes, offs, o,
+                           (uint64_t)nb, wave ? hit_offs : nullptr);
     }
-    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(1024), 0, s, ws.blk, (uint64_t)nb, hit_offs, n);
+    if (!wave) hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(1024), 0, s, ws.blk, (uint64_t)nb, hit_offs, n);
     return hipGetLastError();
 }
 
@@ -1169,7 +1202,8 @@ hipError_t launch_first(const DevIndex &ix, const Workspace &ws, uint64_t n, con
     else
         hipLaunchKernelGGL(k_walk_fast<MODE_FIRST>, dim3(blocks_for(n, WALK_BLOCK)), dim3(WALK_BLOCK), 0, s,
                            ix, ws, n, bytes, offs, o);
-    hipLaunchKernelGGL(k_walk_tail<MODE_FIRST>, dim3(TAIL_GRID), dim3(MID_BLOCK), 0, s, ix, ws, n, bytes, offs, o);
+    hipLaunchKernelGGL(k_walk_tail<MODE_FIRST>, dim3(TAIL_GRID), dim3(MID_BLOCK), 0, s, ix, ws, n, bytes, offs, o,
+                       (uint64_t)0, nullptr);
     return hipGetLastError();
 }
 
