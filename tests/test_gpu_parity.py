@@ -469,6 +469,27 @@ def test_host_batches_in_place_pinned_buffers(torch_dev):
         ix.host_free(np.zeros(4, np.uint8))
 
 
+def test_mixed_batch_sizes_and_modes_in_sequence(torch_dev):
+    """Tile totals stay zero between batches (k_emit clears them; the wave walk
+    adds into them, the lane walk overwrites them, the small-batch tail kernel
+    scans them): wave-walk, lane-walk, first-hit and deep-topic batches in any
+    order on one index all give the oracle's results."""
+    fs = wl.filters(1, 10_000)
+    ix, o = gpu_index(fs), oracle_of(fs)
+    deep = items_of([b"/".join([b"a"] * 40), b"/".join([b"+x"] * 12) + b"/y"] * 3)
+    seq = [5, 9000, 3000, 1, 20_000, 8192, 8193, 2]
+    for k, nt in enumerate(seq):
+        ts = wl.topics(1, 10_000, nt, first=k * 7)
+        hit, vals = assert_same(ix, o, ts)
+        if k % 3 == 1:   # match/2: the first value in traversal order
+            v, f = ix.first_batch(ts.blob, ts.offs)
+            has = np.diff(hit.astype(np.int64)) > 0
+            assert np.array_equal(f == 1, has)
+            assert np.array_equal(v[has], vals[hit[:-1][has].astype(np.int64)])
+        if k % 2 == 0:
+            assert_same(ix, o, deep)
+
+
 def test_wave_walk_limits_fall_back_exactly(torch_dev):
     """Batches of <= 8192 topics take the wave-per-topic walk (16 lanes per
     topic); its limits (a frontier wider than the group, more hit ranges than
