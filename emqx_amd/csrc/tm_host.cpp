@@ -1234,6 +1234,18 @@ int tm_first_batch(tm_index *ix, uint64_t n, const uint8_t *tb, const uint64_t *
     if ((rc = sync_locked(ix, s))) return rc;
     Workspace *ws;
     if ((rc = ensure_ws(ix, n, s, ws))) return rc;
+    if (n && n <= ZC_TOPICS) {   // tm_host_alloc buffers: in place, as tm_match_batch
+        const uint64_t nbytes = to[n];
+        uint8_t *db = nbytes ? pinned_dev(ix, tb, nbytes) : nullptr;
+        uint8_t *dof = pinned_dev(ix, to, (n + 1) * 8);
+        uint8_t *dv = pinned_dev(ix, out_value, n * 4), *df = pinned_dev(ix, out_found, n);
+        if ((db || !nbytes) && ((uintptr_t)tb & 15) == 0 && dof && dv && df) {
+            HIPCHK(ix, launch_first(dev_view(ix), *ws, n, db ? db : dof, reinterpret_cast<const uint64_t *>(dof),
+                                    reinterpret_cast<uint32_t *>(dv), df, s));
+            HIPCHK(ix, hipStreamSynchronize(s));
+            return TM_OK;
+        }
+    }
     const uint8_t *dbytes;
     const uint64_t *doffs;
     if ((rc = stage_in(ix, n, tb, to, s, dbytes, doffs))) return rc;

@@ -112,7 +112,8 @@ int tm_match_batch(tm_index *h, uint64_t n, const uint8_t *topic_bytes, const ui
  * (topic bytes -- 16-byte aligned --, offsets, hit offsets, values and err if
  * not NULL) lies in tm_host_alloc memory of the same index and n <= 65536, the
  * kernels read the topics and write the hit lists in place: no staging copy
- * in, no copy out.  Other batches take the staged path; results are the same.
+ * in, no copy out.  The same holds for tm_first_batch (out_value, out_found).
+ * Other batches take the staged path; results are the same.
  * tm_host_free waits for the index's batches to finish first. */
 int tm_host_alloc(tm_index *h, uint64_t bytes, void **out);
 int tm_host_free(tm_index *h, void *p);

@@ -452,6 +452,14 @@ def test_host_batches_in_place_pinned_buffers(torch_dev):
             pe[:] = 7
             h2, v2, e2 = ix.match_batch(pb, po, out=(ph, pv, pe))
             assert np.array_equal(h2, hit) and np.array_equal(v2, vals) and not e2.any()
+        # match/2 in place: the same first hits as the staged call
+        fv, ff = ix.host_array(nt, np.uint32), ix.host_array(nt, np.uint8)
+        assert ix._lib.tm_first_batch(ix._h, nt, _native._ptr(pb), _native._ptr(po), _native._ptr(fv),
+                                      _native._ptr(ff)) == _native.TM_OK
+        sv, sf = ix.first_batch(ts.blob, ts.offs)
+        assert np.array_equal(ff, sf) and np.array_equal(fv[sf == 1], sv[sf == 1])
+        ix.host_free(fv)
+        ix.host_free(ff)
         # misaligned blob (offsets shifted by one byte): staged, same results
         pb[1:nb + 1] = ts.blob[:nb]
         h3, v3, _ = ix.match_batch(pb[1:], po, out=(ph, pv, pe))
