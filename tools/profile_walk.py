@@ -21,6 +21,9 @@ def main():
     p.add_argument("--order", default="stream", choices=["stream", "sorted", "bucket"],
                    help="topic order in the batch: generator stream, byte-sorted, or bucketed "
                         "by the hash of the first two levels (locality study)")
+    p.add_argument("--filter-order", default="stream", choices=["stream", "sorted"],
+                   help="insertion order of the filters (node ids follow it): generator stream or "
+                        "byte-sorted, i.e. trie nodes numbered depth first (layout study)")
     a = p.parse_args()
     import torch
     from bench import CONFIGS
@@ -28,6 +31,12 @@ def main():
     gen, nf0, _ = CONFIGS[a.config]
     nf = a.filters or nf0
     fs = wl.filters(gen, nf)
+    if a.filter_order == "sorted":
+        items = fs.items()
+        order = sorted(range(len(items)), key=items.__getitem__)
+        blob, offs = _native.pack_strings([items[i] for i in order])
+        fs = wl.ItemSet(blob, offs, fs.vals[np.array(order)], fs.flags[np.array(order)])
+        del items, order
     ix = _native.Index(device=0)
     for lo in range(0, len(fs), 2_000_000):
         part = fs.slice(lo, min(lo + 2_000_000, len(fs)))
@@ -60,7 +69,7 @@ def main():
     el = time.perf_counter() - t
     w, b, n = ix.profile_read()
     st = ix.stats()
-    print(f"{a.config}/{a.order} filters={len(fs)} batch={a.batch} hits={tot} wall/batch={el / a.batches * 1e3:.3f}ms "
+    print(f"{a.config}/{a.order}/filters-{a.filter_order} filters={len(fs)} batch={a.batch} hits={tot} wall/batch={el / a.batches * 1e3:.3f}ms "
           f"walk={w / n:.4f}ms batch_dev={b / n:.4f}ms rate={a.batch * a.batches / el / 1e9:.3f}G/s "
           f"device_MiB={st['device_bytes'] / 2**20:.0f}", flush=True)
 
