@@ -65,15 +65,16 @@ __device__ __forceinline__ void pin(uint32_t &v) { asm volatile("" : "+v"(v)); }
 __device__ __forceinline__ void pin(uint2 &v) { pin(v.x); pin(v.y); }
 __device__ __forceinline__ void pin(uint4 &v) { pin(v.x); pin(v.y); pin(v.z); pin(v.w); }
 
+// A word being scanned: its length and first 8 bytes.  Words longer than VINL
+// bytes (rare) are hashed from their bytes in memory when they end, so the
+// per-byte loop carries no 64-bit FNV multiply.
 struct WordAcc {
-    uint64_t h;                 // FNV-1a over the bytes (used for words > VINL bytes)
     uint32_t len, b0, b1;       // length, first 8 bytes packed little endian
     uint64_t start;
     __device__ __forceinline__ void reset(uint64_t s) {
-        h = FNV_OFF; len = 0; b0 = b1 = 0; start = s;
+        len = 0; b0 = b1 = 0; start = s;
     }
     __device__ __forceinline__ void push(uint32_t c) {
-        h = (h ^ c) * FNV_PRIME;
         uint32_t v = c << ((len & 3) * 8);
         if (len < 4) b0 |= v; else if (len < 8) b1 |= v;
         len++;
@@ -85,8 +86,11 @@ __device__ bool bytes_eq(const uint8_t *a, const uint8_t *b, uint32_t n) {
     return true;
 }
 
-__device__ __forceinline__ uint64_t word_hash_dev(const WordAcc &w) {
-    return w.len <= VINL ? word_hash_short(w.b0, w.b1, w.len) : word_hash_finish(w.h, w.len);
+__device__ __forceinline__ uint64_t word_hash_dev(const WordAcc &w, const uint8_t *blob) {
+    if (w.len <= VINL) return word_hash_short(w.b0, w.b1, w.len);
+    uint64_t h = FNV_OFF;   // FNV-1a, as the host's word_hash (tm_host.cpp)
+    for (uint32_t i = 0; i < w.len; i++) h = (h ^ blob[w.start + i]) * FNV_PRIME;
+    return word_hash_finish(h, w.len);
 }
 
 // continue a vocab probe sequence from `slot` (exact: tag, then bytes)
@@ -108,7 +112,7 @@ __device__ uint32_t vocab_probe(const DevIndex &ix, uint32_t slot, uint32_t tag,
 
 // vocab: word -> wid, exact by construction (hash tag, then length and bytes)
 __device__ uint32_t vocab_find(const DevIndex &ix, const WordAcc &w, const uint8_t *blob) {
-    const uint64_t h = word_hash_dev(w);
+    const uint64_t h = word_hash_dev(w, blob);
     return vocab_probe(ix, (uint32_t)h & ix.vmask, vocab_tag(h, w.len), w.len, w.b0, w.b1, blob + w.start);
 }
 
@@ -196,61 +200,110 @@ enum { RC_OK = 0, RC_BADARG = 1, RC_DEEP = 2 };
 // computes base_init's '$' flag (:160-163) and the exact-key hash.
 //
 // Two passes.  The scan (ALU only once the first two 16-byte chunks of the
-// topic are in) keeps each short word's packed bytes and length in the
-// frontier's LDS slots; words longer than VINL bytes are looked up on the spot.
+// topic are in) keeps each word's packed bytes and length in the frontier's
+// LDS slots; words longer than VINL bytes are looked up after it.
 // Then the vocab probes of up to VGROUP levels are issued together, so a topic's
 // words cost one memory round trip instead of one per level, and the lanes of a
 // wave no longer serialise on the byte position where each of their words ends.
 template <class S>
 __device__ int tokenize(const DevIndex &ix, const uint8_t *blob, uint64_t beg, uint64_t end, S &st,
                         uint32_t &L, bool &dollar, uint64_t &xh, bool &all_found) {
-    WordAcc w; w.reset(beg);
-    uint32_t lev = 0;
-    uint64_t longmask = 0;   // levels resolved during the scan (deferred stores)
+    uint64_t longmask = 0;   // levels resolved before the deferred probes
     all_found = true; dollar = false; xh = FNV_OFF;
-    auto finish = [&]() -> int {
-        if (w.len == 1 && (w.b0 == '+' || w.b0 == '#')) return RC_BADARG;
-        if (lev >= S::maxl) return RC_DEEP;
-        if (lev == 0 && w.len >= 1 && (w.b0 & 0xFF) == '$') dollar = true;
-        if constexpr (S::deferred) {
-            if (w.len <= VINL) {
-                st.put_word(lev, w.b0, w.b1, w.len);
-            } else {
-                st.set_wid(lev, vocab_find(ix, w, blob));
-                longmask |= 1ull << lev;
-            }
-        } else {
-            st.set_wid(lev, vocab_find(ix, w, blob));
-        }
-        lev++;
-        return RC_OK;
-    };
     const uint64_t p0 = beg & ~15ull;
     // aligned 16-byte loads (the first two issued together): a chunk shares its 16-byte granule with a valid
     // byte, so it never crosses a page the caller does not own
     const uint4 z = make_uint4(0, 0, 0, 0);
     const uint4 c0 = p0 < end ? ld4(blob + p0) : z;
     const uint4 c1 = p0 + 16 < end ? ld4(blob + p0 + 16) : z;
-    uint32_t ci = 0;
-    for (uint64_t p = p0; p < end; p += 16, ci++) {
-        const uint4 v = ci == 0 ? c0 : ci == 1 ? c1 : ld4(blob + p);
-        const uint32_t k0 = p < beg ? (uint32_t)(beg - p) : 0;
-        const uint32_t k1 = end - p < 16 ? (uint32_t)(end - p) : 16;
-        for (uint32_t k = k0; k < k1; k++) {
-            const uint32_t word = k < 4 ? v.x : k < 8 ? v.y : k < 12 ? v.z : v.w;
-            const uint32_t c = (word >> ((k & 3) * 8)) & 0xFFu;
-            if (c == '/') {
-                int rc = finish();
-                if (rc) return rc;
-                w.reset(p + k + 1);
-            } else {
-                w.push(c);
+    if constexpr (S::deferred) {
+        // The scan keeps only (first 8 bytes, length) per word and parks them in
+        // the level's LDS slots when a '/' ends it; the checks (badarg, depth,
+        // '$', long words) run per level afterwards, so the divergent work at a
+        // word end is three LDS stores.  A word longer than VINL bytes parks
+        // its length and start instead (len8 = 255), resolved below.
+        uint32_t lev = 0, len = 0, b0 = 0, b1 = 0;
+        uint64_t ws = beg;
+        auto park = [&]() {
+            if (lev < S::maxl) {
+                if (len <= VINL) st.put_word(lev, b0, b1, len);
+                else st.put_word(lev, len, (uint32_t)(ws - beg), 255);
+            }
+            lev++;
+        };
+        uint32_t ci = 0;
+        for (uint64_t p = p0; p < end; p += 16, ci++) {
+            const uint4 v = ci == 0 ? c0 : ci == 1 ? c1 : ld4(blob + p);
+            const uint32_t k0 = p < beg ? (uint32_t)(beg - p) : 0;
+            const uint32_t k1 = end - p < 16 ? (uint32_t)(end - p) : 16;
+#pragma unroll
+            for (uint32_t k = 0; k < 16; k++) {
+                if (k < k0 || k >= k1) continue;
+                const uint32_t word = k < 4 ? v.x : k < 8 ? v.y : k < 12 ? v.z : v.w;
+                const uint32_t c = (word >> ((k & 3) * 8)) & 0xFFu;
+                if (c == '/') {
+                    park();
+                    len = 0; b0 = 0; b1 = 0; ws = p + k + 1;
+                } else {
+                    const uint32_t sh = (len & 3) * 8;
+                    b0 |= len < 4 ? c << sh : 0u;
+                    b1 |= len - 4 < 4 ? c << sh : 0u;
+                    len++;
+                }
             }
         }
+        park();
+        if (lev > S::maxl) return RC_DEEP;
+        L = lev;
+        for (uint32_t l = 0; l < L; l++) {   // a level exactly '+' or '#' is badarg (:374-375)
+            const uint32_t n = st.word_len(l), c = st.word_b0(l) & 0xFFu;
+            if (n == 1 && (c == '+' || c == '#')) return RC_BADARG;
+        }
+        // base_init (:160-163): the first level starts with '$'
+        dollar = st.word_len(0) == 255 ? blob[beg] == '$' : st.word_len(0) >= 1 && (st.word_b0(0) & 0xFFu) == '$';
+        for (uint32_t l = 0; l < L; l++) {
+            if (st.word_len(l) != 255) continue;
+            WordAcc w; w.reset(beg + st.word_b1(l)); w.len = st.word_b0(l);
+            st.set_wid(l, vocab_find(ix, w, blob));
+            longmask |= 1ull << l;
+        }
+    } else {
+        WordAcc w; w.reset(beg);
+        uint32_t lev = 0;
+        auto finish = [&]() -> int {
+            if (w.len == 1 && (w.b0 == '+' || w.b0 == '#')) return RC_BADARG;
+            if (lev >= S::maxl) return RC_DEEP;
+            if (lev == 0 && w.len >= 1 && (w.b0 & 0xFF) == '$') dollar = true;
+            st.set_wid(lev, vocab_find(ix, w, blob));
+            lev++;
+            return RC_OK;
+        };
+        uint32_t ci = 0;
+        for (uint64_t p = p0; p < end; p += 16, ci++) {
+            const uint4 v = ci == 0 ? c0 : ci == 1 ? c1 : ld4(blob + p);
+            const uint32_t k0 = p < beg ? (uint32_t)(beg - p) : 0;
+            const uint32_t k1 = end - p < 16 ? (uint32_t)(end - p) : 16;
+            for (uint32_t k = k0; k < k1; k++) {
+                const uint32_t word = k < 4 ? v.x : k < 8 ? v.y : k < 12 ? v.z : v.w;
+                const uint32_t c = (word >> ((k & 3) * 8)) & 0xFFu;
+                if (c == '/') {
+                    int rc = finish();
+                    if (rc) return rc;
+                    w.reset(p + k + 1);
+                } else {
+                    w.push(c);
+                }
+            }
+        }
+        int rc = finish();
+        if (rc) return rc;
+        L = lev;
     }
-    int rc = finish();
-    if (rc) return rc;
-    L = lev;
+#ifdef TM_STUDY_SCANONLY   // timing study: no vocab probes (wrong results)
+    if constexpr (S::deferred) {
+        for (uint32_t l = 0; l < L; l++) if (!((longmask >> l) & 1)) st.set_wid(l, st.word_b0(l) ^ st.word_b1(l));
+    } else
+#endif
     if constexpr (S::deferred) {
         // Branch-free issue and consumption: every lane issues VGROUP loads
         // (unused levels read slot 0) and consumes all of them, so no load is
@@ -518,6 +571,10 @@ __device__ int match_topic(const DevIndex &ix, const uint8_t *blob, uint64_t beg
     uint32_t L = 0; bool dollar, allf; uint64_t xh;
     int rc = tokenize(ix, blob, beg, end, st, L, dollar, xh, allf);
     if (rc) return rc;
+#ifdef TM_STUDY_TOKONLY   // timing study: tokenise + vocab only (wrong results)
+    if (xh == 42) em(0, 1);   // keep the tokeniser's outputs live
+    return RC_OK;
+#endif
     st.reset();
     const uint32_t xslot = (uint32_t)xh & ix.xmask;
 #ifdef TM_STUDY_NOEXACT
