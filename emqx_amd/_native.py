@@ -217,7 +217,7 @@ class Index:
             return hit, out[: int(hit[n])], err[:n]
 
     def first_batch(self, blob: np.ndarray, offs: np.ndarray):
-        """-> (value u32[n], found u8[n]: 1 hit, 0 none, 2 badarg)."""
+        """-> (value u32[n], found u8[n]: 1 hit, 0 none, 2 badarg, 3 > 65536 levels)."""
         n = len(offs) - 1
         blob = np.ascontiguousarray(blob, dtype=np.uint8)
         offs = np.ascontiguousarray(offs, dtype=np.uint64)

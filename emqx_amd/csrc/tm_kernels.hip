@@ -614,8 +614,11 @@ __device__ int run_topic(const DevIndex &ix, const Workspace &ws, uint64_t n, co
         RangeEmit em;
         em.cnt = 0; em.nr = 0;
         int rc = match_topic(ix, blob, beg, end, st, em);
-        if (rc == RC_DEEP) return rc;
-        if (rc == RC_BADARG) { em.cnt = 0; em.nr = 0; }
+        // more levels than the global scratch holds (> 65536: longer than any
+        // MQTT topic, emqx_mqtt.hrl:44): flagged err 2, no hits
+        const bool toolong = rc == RC_DEEP && S::maxl == MAX_LEVELS;
+        if (rc == RC_DEEP && !toolong) return rc;
+        if (rc != RC_OK) { em.cnt = 0; em.nr = 0; }
         ws.cnt[t] = em.cnt;
         ws.nr[t] = em.nr;
         em.store(ws.rng, n, t);
@@ -631,9 +634,9 @@ __device__ int run_topic(const DevIndex &ix, const Workspace &ws, uint64_t n, co
 #endif
         }
         else
-            o.err[t] = rc == RC_BADARG;
+            o.err[t] = rc == RC_BADARG ? 1 : (toolong ? 2 : 0);
 #else
-        o.err[t] = rc == RC_BADARG;
+        o.err[t] = rc == RC_BADARG ? 1 : (toolong ? 2 : 0);
 #endif
         if (em.nr > RCAP) list_push(ws, n, S::maxl <= MID_L ? L_OVF_MID : L_OVF_DEEP, (uint32_t)t);
         *hits = em.cnt;
@@ -641,9 +644,10 @@ __device__ int run_topic(const DevIndex &ix, const Workspace &ws, uint64_t n, co
     } else {
         FirstEmit em{ix.vals, 0, false};
         int rc = match_topic(ix, blob, beg, end, st, em);
-        if (rc == RC_DEEP) return rc;
-        o.first_val[t] = em.v;
-        o.first_found[t] = rc == RC_BADARG ? 2 : (em.found ? 1 : 0);
+        const bool toolong = rc == RC_DEEP && S::maxl == MAX_LEVELS;
+        if (rc == RC_DEEP && !toolong) return rc;
+        o.first_val[t] = toolong ? 0 : em.v;
+        o.first_found[t] = rc == RC_BADARG ? 2 : (toolong ? 3 : (em.found ? 1 : 0));
         *hits = 0;
         return rc;
     }

@@ -147,6 +147,12 @@ def delete(filter_, ident, tab: Tab):
     return True
 
 
+class TopicTooDeep(ValueError):
+    """A topic of more than 65536 levels: longer than MQTT's 65535-byte
+    maximum (emqx_mqtt.hrl:44), so no client can publish it; the device walk's
+    scratch ends there (include/tmatch.h, err flag 2)."""
+
+
 def _check_topic(topic):
     topic_words(topic)          # raises BadArg like the reference
     return bytes(topic)
@@ -158,6 +164,8 @@ def matches_batch(topics, tab: Tab, opts=()):
     kids, err = tab.match_kids(topics)
     out = []
     for i, ks in enumerate(kids):
+        if err[i] == 2:
+            raise TopicTooDeep(len(topics[i]))
         if err[i]:
             raise BadArg(topics[i])
         keys = [tab._keys[k] for k in ks.tolist()]
@@ -206,4 +214,4 @@ def get_record(key, tab: Tab):
 
 
 __all__ = ["new", "insert", "delete", "match", "matches", "matches_batch", "matches_filter", "make_key", "get_id",
-           "get_topic", "get_record", "Tab", "BadArg"]
+           "get_topic", "get_record", "Tab", "BadArg", "TopicTooDeep"]

@@ -45,6 +45,9 @@
  * (match_add/2 prepends, emqx_trie_search.erl:353-354).
  * A topic with a level equal to "+" or "#" is badarg (emqx_trie_search.erl:374-375):
  * its err flag is 1 and it has no hits.
+ * A topic of more than 65536 levels (longer than MQTT's 65535-byte maximum,
+ * emqx_mqtt.hrl:44, so never seen from a client) is not matched: err flag 2,
+ * no hits.
  */
 #ifndef TMATCH_H
 #define TMATCH_H
@@ -127,7 +130,8 @@ int tm_match_batch_dev(tm_index *h, uint64_t n, const uint8_t *d_topic_bytes, co
                        uint8_t *d_out_err, void *stream);
 
 /* match/2: first hit per topic in traversal order.  out_found[i] = 1 and
- * out_value[i] = value if topic i has a match, 0 otherwise (2 = badarg). */
+ * out_value[i] = value if topic i has a match, 0 otherwise (2 = badarg,
+ * 3 = more than 65536 levels). */
 int tm_first_batch(tm_index *h, uint64_t n, const uint8_t *topic_bytes, const uint64_t *topic_offsets,
                    uint32_t *out_value, uint8_t *out_found);
 

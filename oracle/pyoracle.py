@@ -105,13 +105,13 @@ class Oracle:
             cap = int(r)
 
     def first(self, topic: bytes):
-        """(found, value); found = -1 badarg, 0 false, 1 hit"""
+        """(found, value); found = -1 badarg, -2 more than 65536 levels, 0 false, 1 hit"""
         v = np.zeros(1, np.uint32)
         r = self._l.orc_first(self._h, topic, len(topic), _p(v))
         return r, int(v[0])
 
     def match_batch(self, blob, offs, nthreads: int = 8, with_values: bool = True):
-        """-> (counts i64[n] (-1 badarg), hashes u64[n], hit_offs u64[n+1] | None, values | None)"""
+        """-> (counts i64[n] (-1 badarg, -2 more than 65536 levels), hashes u64[n], hit_offs u64[n+1] | None, values | None)"""
         n = len(offs) - 1
         blob = np.ascontiguousarray(blob, np.uint8)
         offs = np.ascontiguousarray(offs, np.uint64)

@@ -308,13 +308,17 @@ typedef struct {
     uint32_t nw;
 } twords;
 
-/* topic_words/1 + word/2: split on '/', a level equal to '+' or '#' -> badarg */
+/* topic_words/1 + word/2: split on '/', a level equal to '+' or '#' -> badarg (-1).
+ * More than MAXW levels (a topic longer than MQTT's 65535 bytes, emqx_mqtt.hrl:44)
+ * -> -2: outside the device's domain (include/tmatch.h, err flag 2); the
+ * reference's index itself has no such limit. */
 static int topic_words(const uint8_t *t, uint32_t len, twords *w) {
     uint32_t s = 0; w->nw = 0;
     for (uint32_t i = 0; i <= len; i++) {
         if (i == len || t[i] == '/') {
             uint32_t n = i - s;
             if (n == 1 && (t[s] == '+' || t[s] == '#')) return -1;
+            if (w->nw == MAXW) return -2;
             w->p[w->nw] = t + s; w->n[w->nw] = n; w->nw++;
             s = i + 1;
         }
@@ -376,9 +380,10 @@ static okey seek_key(const okey *k, uint32_t pos, const uint8_t *w, uint32_t wn,
 }
 
 /* search/3 + match_topics/4.  mode: 0 = all (traversal order), 1 = first only.
- * returns number of matches, or -1 on badarg. */
+ * returns number of matches, or -1 on badarg (-2: more than MAXW levels). */
 static int64_t walk(const oindex *h, const uint8_t *t, uint32_t tl, twords *tw, oacc *a, int first_only) {
-    if (topic_words(t, tl, tw) < 0) return -1;
+    int rc = topic_words(t, tl, tw);
+    if (rc < 0) return rc;
     okey base; memset(&base, 0, sizeof base);
     base.form = FORM_LIST; base.base = 1;
     if (tw->n[0] >= 1 && tw->p[0][0] == '$') {               /* base_init :160-163 */
@@ -498,7 +503,7 @@ int orc_first(void *hp, const char *t, uint32_t tl, uint32_t *out) {
     oacc a = {&id, 0, 1, 0, 0};
     int64_t r = walk(h, (const uint8_t *)t, tl, get_tw(), &a, 1);
     free(a.scratch);
-    if (r < 0) return -1;
+    if (r < 0) return (int)r;
     if (r == 0) return 0;
     *out = id; return 1;
 }

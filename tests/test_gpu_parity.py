@@ -41,7 +41,7 @@ def oracle_of(items: wl.ItemSet, flags=None) -> Oracle:
 def assert_same(ix: _native.Index, o: Oracle, topics: wl.ItemSet):
     hit, vals, err = ix.match_batch(topics.blob, topics.offs)
     cnt, _, ohit, ovals = o.match_batch(topics.blob, topics.offs)
-    assert np.array_equal(err.astype(bool), cnt < 0), "badarg flags differ"
+    assert np.array_equal(err.astype(np.int64), np.where(cnt < 0, -cnt, 0)), "badarg / too-deep flags differ"
     gcnt = np.diff(hit.astype(np.int64))
     bad = np.nonzero(gcnt != np.maximum(cnt, 0))[0]
     assert len(bad) == 0, f"{len(bad)} topics differ in hit count, first {topics.item(int(bad[0]))!r}: " \
@@ -234,6 +234,35 @@ def test_deep_topics_and_overflow(torch_dev):
     ix, o = gpu_index(fs), oracle_of(fs)
     hit, _ = assert_same(ix, o, items_of(topics))
     assert np.diff(hit.astype(np.int64))[4] > 8      # 'a/b' overflows the RCAP ranges
+
+
+def test_maximum_size_topics(torch_dev):
+    """Topics at MQTT's 65535-byte maximum (emqx_mqtt.hrl:44): one 65535-byte
+    word, 32768 one-byte levels, 65536 empty levels (the walk's scratch depth),
+    and one level more than that -- err flag 2 / found 3 on the device, -2 in
+    the oracle, TopicTooDeep from the mirror (include/tmatch.h)."""
+    big = b"x" * 65535
+    many = b"/".join([b"a"] * 32768)                       # 65535 bytes, 32768 levels
+    empty = b"/" * 65535                                    # 65536 empty levels
+    over = b"/" * 65536                                     # 65537 levels
+    filters = [big, big + b"/#", b"+", b"#", b"+/#", b"a/#", many, b"/".join([b"+"] * 32768),
+               b"/".join([b"+"] * 32767) + b"/#", empty, b"/#", b"+/+/#", many[:-2] + b"/+", b"x/#"]
+    topics = [big, big[:-1], many, many[:-2], empty, over, over + b"a", b"+/" + over, over + b"/+",
+              b"/".join([b"a"] * 40000)]
+    fs = items_of(filters)
+    ix, o = gpu_index(fs), oracle_of(fs)
+    assert_same(ix, o, items_of(topics))
+    hit, vals, err = ix.match_batch(*_native.pack_strings(topics))
+    assert err.tolist() == [0, 0, 0, 0, 0, 2, 2, 1, 2, 0]
+    assert hit[6] == hit[5] and hit[9] == hit[8]
+    val, found = ix.first_batch(*_native.pack_strings(topics))
+    assert found.tolist()[5:9] == [3, 3, 2, 3]
+    tab = ti.new()
+    for i, f in enumerate(filters):
+        ti.insert(f, i, None, tab)
+    assert ti.matches(big, tab) and ti.matches(empty, tab)
+    with pytest.raises(ti.TopicTooDeep):
+        ti.matches(over, tab)
 
 
 def test_edge_topics(torch_dev):

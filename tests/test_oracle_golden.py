@@ -100,6 +100,21 @@ def test_badarg_and_first():
     assert o.first(b"b/b")[0] == 0
 
 
+def test_oracle_depth_domain():
+    """65536 levels (65535 bytes of '/') is the deepest topic the device walks;
+    one level more is outside its domain (-2), a '+' level before that point
+    is still badarg (-1)."""
+    o = Oracle()
+    o.insert(b"#", 1)
+    o.insert(b"/" * 65535, 2)
+    assert o.first(b"/" * 65535) == (1, 1)
+    assert o.matches(b"/" * 65535) is not None
+    assert o.first(b"/" * 65536)[0] == -2
+    assert o.first(b"+" + b"/" * 65536)[0] == -1
+    assert o.first(b"/" * 65536 + b"+")[0] == -1     # the 65537th level is "+"
+    assert o.first(b"/" * 65537 + b"+")[0] == -2
+
+
 def test_words_form_keys_distinct():
     """t_insert_filter: binary and word-list keys with the same id are two keys."""
     o = Oracle()
