@@ -1076,6 +1076,11 @@ __global__ __launch_bounds__(1024) void k_scan_top(uint64_t *blk, uint64_t nb, u
 constexpr int EMIT_BLOCK = TILE;
 constexpr int EMIT_WAVES = EMIT_BLOCK / 64;
 constexpr int WR = 64 * RCAP;   // ranges per wave
+#ifndef TM_EMIT_Q
+#define TM_EMIT_Q 1
+#endif
+typedef uint4 __attribute__((aligned(4))) uint4u;   // dword-aligned 16-B load (global_load_dwordx4)
+constexpr int EMIT_Q = TM_EMIT_Q;   // quads per lane per iteration (loads in flight before the stores)
 
 // One block = one tile of 256 topics: finishes the scan (tile prefix + local
 // exclusive scan -> hit_offs), then each wave flattens its 64 topics' value
@@ -1128,11 +1133,13 @@ __global__ __launch_bounds__(EMIT_BLOCK) void k_emit(DevIndex ix, Workspace ws, 
     const bool vec = (reinterpret_cast<uintptr_t>(out) & 15) == 0;
     const uint64_t q1 = (endp + 3) >> 2;
     uint32_t r = 0;   // last range starting at or before the lane's position (positions only grow)
-    for (uint64_t q = (base >> 2) + lane; q < q1; q += 64) {
+    // one quad: its range found from the lane's previous one (positions only
+    // grow; a lane moves 256 positions per quad, so a few steps forward cover
+    // long ranges -- C2: 250 values -- and a binary search the rest), then its
+    // four values
+    auto fetch = [&](uint64_t q, uint32_t (&v)[4], bool (&ok)[4]) {
         const uint64_t p0 = q << 2;
         const uint32_t first = (uint32_t)((p0 > base ? p0 : base) - base);
-        // a lane moves 256 positions per iteration: a few steps forward cover
-        // long ranges (C2: 250 values), a binary search the rest
         uint32_t k = 0;
         while (k < 2 && r + 1 < R && s_rel[wv][r + 1] <= first) { r++; k++; }
         if (r + 1 < R && s_rel[wv][r + 1] <= first) {
@@ -1143,13 +1150,24 @@ __global__ __launch_bounds__(EMIT_BLOCK) void k_emit(DevIndex ix, Workspace ws, 
             }
             r = lo;
         }
-        uint32_t v[4];
-        bool ok[4];
+        if (q < q1 && p0 >= base && p0 + 3 < endp) {   // whole quad inside one run: one 16-B load
+            const uint32_t rs = s_rel[wv][r], rc = s_cnt[wv][r];
+            if (!(rc & RUN_INLINE) && first >= rs && first + 3 - rs < (rc & RUN_CNT)) {
+#ifdef TM_STUDY_EMIT_NOREAD   // study: store-only bound of the emit (wrong values)
+                const uint4 a = make_uint4(first, rs, rc, 0);
+#else
+                const uint4 a = *reinterpret_cast<const uint4u *>(ix.vals + s_off[wv][r] + (first - rs));
+#endif
+                v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+                ok[0] = ok[1] = ok[2] = ok[3] = true;
+                return;
+            }
+        }
 #pragma unroll
         for (int k = 0; k < 4; k++) {
             const uint64_t p = p0 + k;
             ok[k] = false; v[k] = 0;
-            if (p < base || p >= endp) continue;
+            if (q >= q1 || p < base || p >= endp) continue;
             const uint32_t x = (uint32_t)(p - base);
             while (r + 1 < R && s_rel[wv][r + 1] <= x) r++;
             const uint32_t rs = s_rel[wv][r];
@@ -1159,6 +1177,9 @@ __global__ __launch_bounds__(EMIT_BLOCK) void k_emit(DevIndex ix, Workspace ws, 
                 ok[k] = true;
             }
         }
+    };
+    auto put = [&](uint64_t q, const uint32_t (&v)[4], const bool (&ok)[4]) {
+        const uint64_t p0 = q << 2;
         if (vec && ok[0] && ok[1] && ok[2] && ok[3] && p0 + 3 < cap) {
             *reinterpret_cast<uint4 *>(out + p0) = make_uint4(v[0], v[1], v[2], v[3]);
         } else {
@@ -1166,6 +1187,16 @@ __global__ __launch_bounds__(EMIT_BLOCK) void k_emit(DevIndex ix, Workspace ws, 
             for (int k = 0; k < 4; k++)
                 if (ok[k] && p0 + k < cap) out[p0 + k] = v[k];
         }
+    };
+    // EMIT_Q quads per iteration, all their value loads issued before any
+    // store (the compiler cannot move a vals load above a store to out)
+    for (uint64_t q = (base >> 2) + lane; q < q1; q += 64 * EMIT_Q) {
+        uint32_t v[EMIT_Q][4];
+        bool ok[EMIT_Q][4];
+#pragma unroll
+        for (int j = 0; j < EMIT_Q; j++) fetch(q + 64 * j, v[j], ok[j]);
+#pragma unroll
+        for (int j = 0; j < EMIT_Q; j++) put(q + 64 * j, v[j], ok[j]);
     }
 }
 
