@@ -1181,7 +1181,12 @@ __global__ __launch_bounds__(EMIT_BLOCK) void k_emit(DevIndex ix, Workspace ws, 
     auto put = [&](uint64_t q, const uint32_t (&v)[4], const bool (&ok)[4]) {
         const uint64_t p0 = q << 2;
         if (vec && ok[0] && ok[1] && ok[2] && ok[3] && p0 + 3 < cap) {
-            *reinterpret_cast<uint4 *>(out + p0) = make_uint4(v[0], v[1], v[2], v[3]);
+            // non-temporal: the hit lists are not read back by the GPU, and
+            // dirty output lines left in L2 slow the next batch's walk (C2
+            // walk 0.150 -> 0.124 ms, C3 batch -1 %)
+            typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+            const u32x4 x = {v[0], v[1], v[2], v[3]};
+            __builtin_nontemporal_store(x, reinterpret_cast<u32x4 *>(out + p0));
         } else {
 #pragma unroll
             for (int k = 0; k < 4; k++)
