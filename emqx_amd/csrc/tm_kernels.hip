@@ -547,7 +547,8 @@ struct RangeEmit {          // phase 1: count hits, keep up to RCAP value ranges
     __device__ __forceinline__ void store(uint2 *rng, uint64_t n, uint64_t t) const {
 #pragma unroll
         for (uint32_t i = 0; i < RCAP; i++)
-            if (i < nr) rng[(uint64_t)i * n + t] = r[i];
+            if (i < nr) __builtin_nontemporal_store((uint64_t)r[i].x | ((uint64_t)r[i].y << 32),
+                                                    reinterpret_cast<uint64_t *>(rng) + (uint64_t)i * n + t);
     }
 };
 
@@ -626,8 +627,9 @@ __device__ int run_topic(const DevIndex &ix, const Workspace &ws, uint64_t n, co
         const bool toolong = rc == RC_DEEP && S::maxl == MAX_LEVELS;
         if (rc == RC_DEEP && !toolong) return rc;
         if (rc != RC_OK) { em.cnt = 0; em.nr = 0; }
-        ws.cnt[t] = em.cnt;
-        ws.nr[t] = em.nr;
+        // per-topic outputs, read once by k_emit: non-temporal (bench +1.6 %)
+        __builtin_nontemporal_store(em.cnt, ws.cnt + t);
+        __builtin_nontemporal_store(em.nr, ws.nr + t);
         em.store(ws.rng, n, t);
 #ifdef TM_STUDY   // study build (tools/study_steps.py): visits and probes in the err byte
         if constexpr (S::maxl == FAST_L)
