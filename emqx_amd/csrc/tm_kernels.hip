@@ -645,7 +645,7 @@ __device__ int run_topic(const DevIndex &ix, const Workspace &ws, uint64_t n, co
         else
             o.err[t] = rc == RC_BADARG ? 1 : (toolong ? 2 : 0);
 #else
-        o.err[t] = rc == RC_BADARG ? 1 : (toolong ? 2 : 0);
+        __builtin_nontemporal_store((uint8_t)(rc == RC_BADARG ? 1 : (toolong ? 2 : 0)), o.err + t);
 #endif
         if (em.nr > RCAP) list_push(ws, n, S::maxl <= MID_L ? L_OVF_MID : L_OVF_DEEP, (uint32_t)t);
         *hits = em.cnt;
@@ -1114,7 +1114,8 @@ __global__ __launch_bounds__(EMIT_BLOCK) void k_emit(DevIndex ix, Workspace ws, 
     const uint32_t c = valid ? __builtin_nontemporal_load(ws.cnt + t) : 0;
     uint64_t total;
     const uint64_t my = ws.blk[blockIdx.x] + block_excl_scan(c, total, s_w);
-    if (valid) hit_offs[t] = my;
+    // the GPU never reads the offsets (or the err flags) back: non-temporal
+    if (valid) __builtin_nontemporal_store(my, hit_offs + t);
     if (lane == 63) s_end[wv] = my + c;
     __syncthreads();
     // every thread has read its tile prefix: leave the tile total zero for the
