@@ -5,18 +5,22 @@ One step = one batch of publish topics matched against the device-resident
 index (tokenise + trie walk + exact lookup + CSR emission of every matched
 value), inputs already resident in HBM.  Default workload: config C3 (10M
 mixed-wildcard filters incl. $share dests, $SYS filters and root globals),
-1M-topic batches per GPU.  Multi-GPU = topic-sharded weak scaling: every rank
-holds a replica of the index and matches its own batch; there is no
-data-path collective.
+1M-topic batches per GPU.  The timed steps rotate over --rotate distinct
+1M-topic batches (default 4, 4M different topics), so no step re-matches the
+batch the step before it left in the 256 MB Infinity Cache.  Multi-GPU =
+topic-sharded weak scaling: every rank holds a replica of the index and
+matches its own batches; there is no data-path collective.
 
 Other modes (not the headline line):
   --config c4   filter-sharded (100M filters split over the ranks, each rank
-                matches the SAME batch against its shard, the hit lists are
-                allgathered over RCCL and merged on the device): strong scaling
+                matches the SAME batch against its shard, per-topic hit counts
+                and the hit lists are allgathered over RCCL and merged on the
+                device): strong scaling
   --config c5   churn: every step first applies --deltas subscribe/unsubscribe
                 ops (one router-syncer batch) to the replicated index, then
                 matches the batch; reports deltas/s beside topics/s
-  --config c1 / c2 / c2nm   the other BASELINE.json configs, topic-sharded
+  --config c1 / c2 / c2nm / c3deep   the other BASELINE.json configs (and C3
+                with 10 % of the topics 33-64 levels deep), topic-sharded
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3]
        torchrun ... bench.py --gpus N  (one rank per GPU)
@@ -25,8 +29,10 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
+import threading
 import time
 from pathlib import Path
 
@@ -41,6 +47,7 @@ CONFIGS = {
     "c2": (2, 1_000_000, "1M 'fleet/{id}/sensor/+' + 1k global '#' rules"),
     "c2nm": (20, 1_000_000, "1M 'fleet/{id}/sensor/+' + 1k non-matching 'rules/{k}/#' globals"),
     "c3": (3, 10_000_000, "10M mixed-wildcard filters incl. $share groups and '$SYS' exclusion"),
+    "c3deep": (30, 10_000_000, "C3 filters; 10% of the topics 33-64 levels deep"),
     "c4": (4, 100_000_000, "100M mixed filters filter-sharded over the ranks, RCCL allgatherv of hit lists"),
     "c5": (5, 10_000_000, "churn: 10M mixed filters, subscribe/unsubscribe deltas interleaved with match batches"),
 }
@@ -60,17 +67,45 @@ def parse():
     p.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     p.add_argument("--filters", type=int, default=None)
     p.add_argument("--batch", type=int, default=1_000_000, help="topics per GPU per step")
+    p.add_argument("--rotate", type=int, default=4, help="distinct topic batches the steps rotate over")
     p.add_argument("--deltas", type=int, default=100,
                    help="c5: deltas applied per step (100 x ~2.5k steps/s = 2.5x the configured 100k deltas/s)")
     p.add_argument("--streams", type=int, default=3,
                    help="HIP streams the steps rotate over (batch k+1's walk overlaps batch k's scan/emit)")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
-    p.add_argument("--cpu-threads", type=int, default=16)
+    p.add_argument("--cpu-threads", type=int, default=None,
+                   help="CPU baseline threads (default: the CPUs this process may use)")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-parity", action="store_true")
     p.add_argument("--latency-batches", type=int, default=20)
+    p.add_argument("--concurrency", type=int, default=8,
+                   help="host threads of the concurrent-caller latency leg (0 = skip)")
     p.add_argument("--frontier-sample", type=int, default=20_000)
     return p.parse_args()
+
+
+def host_cpus():
+    """CPUs this process may use: its affinity set, capped by a cgroup CPU
+    quota if one is set (the GPU box gives a process a share of the machine),
+    and the CPU model."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    threads = aff if quota is None else max(1, min(aff, math.floor(quota)))
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return threads, {"cpu_model": model, "affinity_cpus": aff, "cgroup_cpu_quota": quota}
 
 
 def main():
@@ -87,11 +122,13 @@ def main():
     dev = torch.device(f"cuda:{local}")
 
     from emqx_amd import _native, shard, workload as wl
+    from emqx_amd.build import source_hash
 
     gen_cfg, default_f, desc = CONFIGS[a.config]
     filter_sharded = a.config == "c4"
     nf = a.filters or default_f
     B = a.batch
+    R = max(1, a.rotate)
 
     t = time.time()
     fs = wl.filters(gen_cfg, nf, shard=rank, nshards=world) if filter_sharded else wl.filters(gen_cfg, nf)
@@ -114,11 +151,12 @@ def main():
     log(f"[rank {rank}] index: {st['n_keys']} keys, {st['n_nodes']} nodes, {st['n_edges']} edges, "
         f"{st['n_words']} words, {st['device_bytes'] / 2**20:.0f} MiB HBM; compile {t_compile:.1f}s upload {t_upload:.2f}s")
 
-    # topic-sharded: rank r matches topics [r B, (r+1) B); filter-sharded: all ranks the same batch
-    first = 0 if filter_sharded else rank * B
-    ts = wl.topics(gen_cfg, nf, B, first=first)
-    d_blob = torch.from_numpy(ts.blob).to(dev)
-    d_offs = torch.from_numpy(ts.offs.view(np.int64)).to(dev)
+    # R distinct batches per rank.  Topic-sharded: rank r owns topics
+    # [(r R + k) B, (r R + k + 1) B) of the stream; filter-sharded: every rank
+    # matches the same R batches against its shard.
+    base = 0 if filter_sharded else rank * R
+    tsets = [wl.topics(gen_cfg, nf, B, first=(base + k) * B) for k in range(R)]
+    d_in = [(torch.from_numpy(ts.blob).to(dev), torch.from_numpy(ts.offs.view(np.int64)).to(dev)) for ts in tsets]
     # one output set per stream: consecutive steps rotate over the streams, so
     # step k+1's walk overlaps step k's scan / emit (the library keeps one
     # workspace per stream and orders index patches across streams)
@@ -127,7 +165,6 @@ def main():
     outs = [{"hit": torch.zeros(B + 1, dtype=torch.int64, device=dev),
              "err": torch.zeros(B, dtype=torch.uint8, device=dev),
              "out": torch.zeros(1, dtype=torch.int32, device=dev)} for _ in range(nstreams)]
-    d_hit, d_err = outs[0]["hit"], outs[0]["err"]
 
     # c5: the delta stream, generated up front (host buffers, as the syncer hands them over)
     dchunks = []
@@ -137,12 +174,14 @@ def main():
         dchunks = [dl.slice(k * a.deltas, (k + 1) * a.deltas) for k in range(a.steps + a.warmup + 1)]
     dpos = [0]
     kstep = [0]
+    xch = shard.Exchange(B, dev) if filter_sharded and world > 1 else None
 
     def step(cap):
-        k = kstep[0] % nstreams
+        k = kstep[0]
         kstep[0] += 1
-        o = outs[k]
-        sid = streams[k].cuda_stream
+        o = outs[k % nstreams]
+        d_blob, d_offs = d_in[k % R]
+        sid = streams[k % nstreams].cuda_stream
         if dchunks:
             d = dchunks[dpos[0]]
             dpos[0] += 1
@@ -151,15 +190,19 @@ def main():
                            o["err"].data_ptr(), sid)
         if filter_sharded:
             if world == 1:   # one shard: the merge alone (the exchange is the identity)
-                return shard.merge(o["hit"].view(1, B + 1), o["out"].view(1, -1), o["out"].numel(), sid)
-            return shard.allgatherv_hits(o["hit"], o["out"], stream=sid)
+                return shard.merge_local(o["hit"], o["out"], sid)
+            return xch.run(o["hit"], o["out"], stream=sid)
         return None
 
-    # sizing pass (no values written), then the output buffers
-    ix.match_batch_dev(B, d_blob.data_ptr(), d_offs.data_ptr(), d_hit.data_ptr(), outs[0]["out"].data_ptr(), 0,
-                       d_err.data_ptr(), stream)
-    torch.cuda.synchronize()
-    total_hits = int(d_hit[-1].item())
+    # sizing pass (no values written) over every batch, then the output buffers
+    total_hits = 0
+    for d_blob, d_offs in d_in:
+        ix.match_batch_dev(B, d_blob.data_ptr(), d_offs.data_ptr(), outs[0]["hit"].data_ptr(),
+                           outs[0]["out"].data_ptr(), 0, outs[0]["err"].data_ptr(), stream)
+        torch.cuda.synchronize()
+        total_hits = max(total_hits, int(outs[0]["hit"][-1].item()))
+        if xch is not None:
+            xch.size_from(outs[0]["hit"])   # per-peer exchange capacity: setup, not the data path
     slack = a.deltas * (a.steps + a.warmup) * 64 if dchunks else 0   # churn may add hits
     cap = total_hits + slack
     for o in outs:
@@ -183,24 +226,46 @@ def main():
     if world > 1:
         dist.barrier()
     walk_ms, batch_ms, nb = ix.profile_read(reset=True)
-    # the same kernel alone: a few batches on one stream, one after another
-    # (with several streams a launch's duration includes the GPU time it
-    # shares with the other streams' kernels)
-    for _ in range(5):
-        ix.match_batch_dev(B, d_blob.data_ptr(), d_offs.data_ptr(), outs[0]["hit"].data_ptr(),
-                           outs[0]["out"].data_ptr(), cap, outs[0]["err"].data_ptr(), stream)
-        torch.cuda.synchronize()
-    iso_walk_ms, _, iso_nb = ix.profile_read(reset=True)
+    if xch is not None:   # the on-device high-water mark: did any timed batch overflow the capacity?
+        assert xch.check(), "filter-sharded exchange capacity overflowed during the timed steps"
+    last_k = kstep[0] - 1
+    last = outs[last_k % nstreams]
+    last_batch = last_k % R
+    d_hit, d_out = last["hit"], last["out"]
+    last_hits = int(d_hit[-1].item())
+    assert last_hits <= cap
+    merged_total = int(merged[0][-1].item()) if merged is not None else None
+    merged_topics = merged[0].numel() - 1 if merged is not None else None
+    # The walk kernel alone: two passes over the R batches, back to back on
+    # one stream (so no other kernel runs beside a walk), waited for once at
+    # the end.  An event recorded on an idle stream is stamped before the
+    # host has enqueued the kernel behind it, so one unprofiled batch goes
+    # first and every profiled launch is enqueued while the stream is busy:
+    # the events then bracket the kernel alone, as rocprof does.  This is the
+    # duration roofline.kernel_avg_ms reports; rocprof sees these launches as
+    # the last 2 R full-grid k_walk_fast launches of the run
+    # (tools/prof_report.py splits them out).
+    iso_passes = 2
+    spare = outs[0]
+
+    def iso_launch(d_blob, d_offs):
+        ix.match_batch_dev(B, d_blob.data_ptr(), d_offs.data_ptr(), spare["hit"].data_ptr(),
+                           spare["out"].data_ptr(), cap, spare["err"].data_ptr(), stream)
+
+    ix.profile(False)
+    torch.cuda.synchronize()
+    iso_launch(*d_in[0])
+    ix.profile(True)
+    for _ in range(iso_passes):
+        for d_blob, d_offs in d_in:
+            iso_launch(d_blob, d_offs)
+    torch.cuda.synchronize()
+    iso_walk_ms, iso_batch_ms, iso_nb = ix.profile_read(reset=True)
     ix.profile(False)
     el_t = torch.tensor([el], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
     el_max = float(el_t.item())
-    last = outs[(kstep[0] - 1) % nstreams]
-    d_hit, d_out = last["hit"], last["out"]
-    last_hits = int(d_hit[-1].item())
-    assert last_hits <= cap
-    merged_total = int(merged[0][-1].item()) if merged is not None else None
 
     # whole-job topics/s: topic-sharded = every rank's own batch; filter-sharded = the one shared batch
     topics_per_step = B if filter_sharded else world * B
@@ -208,21 +273,25 @@ def main():
     ms_per_step = el_max / a.steps * 1e3
     walk_avg_ms = walk_ms / max(nb, 1)
     batch_avg_ms = batch_ms / max(nb, 1)
+    iso_ms = iso_walk_ms / max(iso_nb, 1)
+    iso_batch = iso_batch_ms / max(iso_nb, 1)
 
     # p50/p99 batch latency: host topics in, hit lists back in host memory
     # (every rank).  "pinned": the caller's buffers come from tm_host_alloc
     # (what a NIF keeps per scheduler), so the kernels read the topics and
     # write the hit lists in place; "pageable": ordinary caller buffers,
     # staged through the library's pinned buffers (one copy in, one out).
+    ts = tsets[0]
     lat = {}
+    conc = None
     if not filter_sharded:
         for lb in sorted({min(4096, B), min(65536, B)}):
             sub = ts.slice(0, lb)
             _, v0, _ = ix.match_batch(sub.blob, sub.offs)          # sizes the value buffer
-            nb = int(sub.offs[-1] - sub.offs[0])
-            pb = ix.host_array(nb + 16, np.uint8)
+            nbytes = int(sub.offs[-1] - sub.offs[0])
+            pb = ix.host_array(nbytes + 16, np.uint8)
             po = ix.host_array(lb + 1, np.uint64)
-            pb[:nb] = sub.blob[int(sub.offs[0]):int(sub.offs[-1])]
+            pb[:nbytes] = sub.blob[int(sub.offs[0]):int(sub.offs[-1])]
             po[:] = sub.offs - sub.offs[0]
             kinds = {"pinned": (pb, po, (ix.host_array(lb + 1, np.uint64), ix.host_array(len(v0) + 1024, np.uint32),
                                          ix.host_array(lb, np.uint8))),
@@ -236,6 +305,8 @@ def main():
                     xs.append((time.perf_counter() - t1) * 1e3)
                 xs = np.array(xs[2:])
                 lat[f"{kind}/{lb}"] = {"p50_ms": float(np.percentile(xs, 50)), "p99_ms": float(np.percentile(xs, 99))}
+        if a.concurrency > 0 and hasattr(ix, "host_array"):
+            conc = concurrent_latency(ix, ts, a.concurrency, min(4096, B))
     if world > 1 and lat:
         # the slowest rank's percentiles (max over ranks)
         keys = sorted(lat)
@@ -257,6 +328,9 @@ def main():
     sys.path.insert(0, str(ROOT / "oracle"))
     from pyoracle import Oracle, frontier
 
+    cpu_threads, cpu_info = host_cpus()
+    if a.cpu_threads:
+        cpu_threads = a.cpu_threads
     res_extra = {}
     mism = None
     ns = min(a.frontier_sample, B)
@@ -273,42 +347,41 @@ def main():
             o.apply(d.flags, d.blob, d.offs, d.vals)
         o.prepare()
         log(f"oracle built in {time.time() - t:.1f}s")
-        # the last step's output of this rank (its own shard's lists for c4)
+        # the last timed step's output of this rank (its own shard's lists for c4)
         host_hit = d_hit.cpu().numpy().view(np.uint64)
         host_out = d_out.cpu().numpy().view(np.uint32)
         rng = np.random.default_rng(0x454D5158)
         idx = np.sort(rng.choice(B, ns, replace=False))
-        sblob, soffs = _native.pack_strings([ts.item(int(i)) for i in idx])
-        levels, states = frontier(o, sblob, soffs, nthreads=a.cpu_threads)
-        cnt, _, ohit, ovals = o.match_batch(sblob, soffs, nthreads=a.cpu_threads)
+        lts = tsets[last_batch]
+        sblob, soffs = _native.pack_strings([lts.item(int(i)) for i in idx])
+        cnt, _, ohit, ovals = o.match_batch(sblob, soffs, nthreads=cpu_threads)
         mism = 0
         for j, i in enumerate(idx):
             g = host_out[int(host_hit[i]):int(host_hit[i + 1])]
             e = ovals[int(ohit[j]):int(ohit[j + 1])]
             mism += int(not np.array_equal(g, e))
         # algorithmic bytes per walk launch (SURVEY.md 8d per topic, minus the
-        # 4 H the emit kernel writes):  8 L + 32 sum|F_l| + 4
-        L_total = int(np.count_nonzero(ts.blob[: int(ts.offs[-1])] == ord("/"))) + B
-        F_total = float(states.sum()) * B / ns
-        walk_bytes = 8 * L_total + 32 * F_total + 4 * B
-        achieved = walk_bytes / (walk_avg_ms * 1e-3) / 1e9
-        iso_ms = iso_walk_ms / max(iso_nb, 1)
-        res_extra["walk_isolated"] = {"kernel_avg_ms": round(iso_ms, 4),
-                                      "achieved_GBps": round(walk_bytes / (iso_ms * 1e-3) / 1e9, 1),
-                                      "frac": round(walk_bytes / (iso_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                                      "note": "k_walk_fast alone: 5 batches on one stream after the timed region"}
-        res_extra["full_path_GBps"] = round((walk_bytes + 4 * last_hits) / (batch_avg_ms * 1e-3) / 1e9, 1)
-        # the walk's algorithmic bytes over the wall time of a step: with steps
-        # overlapping on several streams a launch's own duration overstates its
-        # share of the GPU, so this is the effective rate beside roofline.achieved
-        res_extra["walk_effective_GBps"] = round(walk_bytes / (ms_per_step * 1e-3) / 1e9, 1)
+        # 4 H the emit kernel writes):  8 L + 32 sum|F_l| + 4, averaged over
+        # the R batches (L exact, sum|F_l| from an ns / R sample of each)
+        per = max(1, ns // R)
+        wb = []
+        for k, tk in enumerate(tsets):
+            kidx = np.sort(rng.choice(B, per, replace=False))
+            fb, fo = _native.pack_strings([tk.item(int(i)) for i in kidx])
+            _, states = frontier(o, fb, fo, nthreads=cpu_threads)
+            L_total = int(np.count_nonzero(tk.blob[: int(tk.offs[-1])] == ord("/"))) + B
+            F_total = float(states.sum()) * B / per
+            wb.append(8 * L_total + 32 * F_total + 4 * B)
+        walk_bytes = float(np.mean(wb))
+        achieved = walk_bytes / (iso_ms * 1e-3) / 1e9
+        res_extra["full_path_GBps"] = round((walk_bytes + 4 * last_hits) / (iso_batch * 1e-3) / 1e9, 1)
 
-        # ---- CPU baseline: the oracle (restated reference walk) on host threads
-        if not a.no_cpu and world == 1 and a.config in ("c1", "c2", "c2nm", "c3"):
+        # ---- CPU baseline: the oracle (restated reference walk) on the host's CPUs
+        if not a.no_cpu and world == 1 and a.config in ("c1", "c2", "c2nm", "c3", "c3deep"):
             n1 = min(20_000, B)
             probe = ts.slice(0, n1)
             t1 = time.perf_counter()
-            o.match_batch(probe.blob, probe.offs, nthreads=a.cpu_threads, with_values=False)
+            o.match_batch(probe.blob, probe.offs, nthreads=cpu_threads, with_values=False)
             r1 = n1 / (time.perf_counter() - t1)
             # a bounded sample of about cpu_seconds of CPU work: whole passes over
             # the batch when it is shorter than that, else its first n2 topics
@@ -317,36 +390,47 @@ def main():
             samp = ts.slice(0, n2)
             t1 = time.perf_counter()
             for _ in range(passes):
-                o.match_batch(samp.blob, samp.offs, nthreads=a.cpu_threads, with_values=False)
+                o.match_batch(samp.blob, samp.offs, nthreads=cpu_threads, with_values=False)
             el_cpu = time.perf_counter() - t1
             what = f"{passes} passes over the {B}-topic batch" if passes > 1 else f"first {n2} topics of the batch"
-            cpu = {"value": round(passes * n2 / el_cpu, 1), "unit": "topic matches/s", "cores": a.cpu_threads,
-                   "kind": "port",
+            cpu = {"value": round(passes * n2 / el_cpu, 1), "unit": "topic matches/s", "cores": cpu_threads,
+                   "kind": "port", **cpu_info,
                    "sample": f"{what} vs all {len(fs)} keys; oracle/tm_oracle.c seek walker (emqx_trie_search "
-                             f"restated) over a sorted key array, {a.cpu_threads} pthreads, {el_cpu:.1f}s"}
+                             f"restated) over a sorted key array, {cpu_threads} pthreads (one per CPU this "
+                             f"process may use), {el_cpu:.1f}s"}
 
-    traffic = None
-    mem_req = None
+    # memory-side traffic of the walk: PMC counters cannot be read inside this
+    # process, so they come from profiles/pmc_<config>.json -- used only if it
+    # was measured on the kernels this tree builds (source hash) and the same
+    # workload shape
+    traffic = mem_req = None
+    traffic_note = "no profiles/pmc_{}.json".format(a.config)
     pmc = ROOT / "profiles" / f"pmc_{a.config}.json"
     if pmc.exists():
         try:
             pj = json.loads(pmc.read_text())
-            if pj.get("filters") == len(fs) and pj.get("batch") == B:
+            same = (pj.get("filters") == len(fs) and pj.get("batch") == B and pj.get("rotate") == R)
+            fresh = pj.get("source_hash") == source_hash()
+            if same and fresh:
                 traffic = pj.get("walk_hbm_bytes_per_launch")
                 mem_req = pj.get("walk_mem_requests_per_launch")
-        except Exception:
-            traffic = None
+                traffic_note = f"{pj.get('source')} (kernel sources {pj['source_hash']}, this tree)"
+            else:
+                traffic_note = ("refused: " + ("stale (measured on other kernel sources)" if not fresh
+                                              else "different workload shape") + f" -- {pj.get('source')}")
+        except (ValueError, KeyError, OSError) as e:
+            traffic_note = f"unreadable: {e!r}"
     # practical roofline of a pointer-chasing walk: the measured memory-side
     # random-request rate (tools/gather_bench.hip, profiles/r1_gather.md)
     req_ceiling = None
-    if mem_req and walk_avg_ms:
-        rate = mem_req / (walk_avg_ms * 1e-3)
+    if mem_req and iso_ms:
+        rate = mem_req / (iso_ms * 1e-3)
         req_ceiling = {"requests_per_launch": mem_req, "requests_per_s": round(rate, 1),
                        "ceiling_per_s": RANDOM_REQ_CEILING, "frac": round(rate / RANDOM_REQ_CEILING, 4),
                        "source": "profiles/r1_gather.md (64-B random requests beyond L2, 256 MiB-2 GiB tables)"}
 
     metric = {"c3": "topic matches/sec at 10M filters"}.get(a.config, f"topic matches/sec ({a.config})")
-    par = (f"filter-sharded x{world} (RCCL allgatherv of hit lists)" if filter_sharded
+    par = (f"filter-sharded x{world} (RCCL allgather of counts + allgatherv of hit lists)" if filter_sharded
            else f"topic-sharded x{world} (trie replicated)")
     res = {
         "metric": metric,
@@ -363,37 +447,114 @@ def main():
         "data": "synthetic (emqx_amd/csrc/workload.cpp, seed 0x454D5158+cfg)",
         "config": {"workload": f"{a.config}: {desc}", "filters": nf if filter_sharded else len(fs),
                    "topics_per_gpu_step": B, "global_batch": topics_per_step, "parallelism": par,
-                   "streams": nstreams},
+                   "streams": nstreams, "distinct_batches": R},
         "roofline": {"bound": "hbm", "achieved": None if achieved is None else round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": None if achieved is None else round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "kernel": "k_walk_fast", "kernel_avg_ms": round(walk_avg_ms, 4),
+                     "traffic_source": traffic_note,
+                     "kernel": "k_walk_fast", "kernel_avg_ms": round(iso_ms, 4),
+                     "kernel_launches": int(iso_nb),
+                     "kernel_timing": (f"HIP events on the launch stream around k_walk_fast, {iso_passes} passes over "
+                                       f"the {R} batches back to back on one stream after the timed region"),
                      "algorithmic_bytes_per_launch": None if walk_bytes is None else int(walk_bytes),
-                     "random_request_roofline": req_ceiling},
+                     "random_request_roofline": req_ceiling,
+                     "effective": {"walk_avg_ms_overlapped": round(walk_avg_ms, 4),
+                                   "walk_GBps_per_step": None if walk_bytes is None
+                                   else round(walk_bytes / (ms_per_step * 1e-3) / 1e9, 1),
+                                   "note": f"the timed region's walks, overlapping the other {nstreams - 1} streams' "
+                                           f"kernels; GBps_per_step = algorithmic bytes / ms_per_step"}},
+        "checks": {"walk_isolated_le_ms_per_step": bool(iso_ms <= ms_per_step)},
         "cpu_baseline": cpu,
         "matched_ids_per_s": round(last_hits * (1 if filter_sharded else world) * a.steps / el_max, 1),
-        "hits_per_topic": round((merged_total if merged_total is not None else last_hits) / B, 3),
+        "hits_per_topic": round(merged_total / max(merged_topics, 1) if merged_total is not None else last_hits / B, 3),
         "batch_device_ms": round(batch_avg_ms, 4),
+        "batch_device_isolated_ms": round(iso_batch, 4),
         "batch_latency_host_ms": lat_pinned,
         "batch_latency_host_pageable_ms": lat_pageable,
+        "concurrent_callers": conc,
         "parity_sample": None if mism is None else {"topics": ns, "mismatches": mism,
                                                     "against": "oracle over this rank's keys"},
         "build": {"generate_s": round(t_gen, 1), "compile_s": round(t_compile, 1), "upload_s": round(t_upload, 2),
                   "device_MiB": round(st["device_bytes"] / 2**20, 1), "nodes": st["n_nodes"],
-                  "edges": st["n_edges"], "words": st["n_words"], "keys_this_rank": st["n_keys"]},
+                  "edges": st["n_edges"], "words": st["n_words"], "keys_this_rank": st["n_keys"],
+                  "kernel_source_hash": source_hash()},
     }
     res.update(res_extra)
     if dchunks:
         res["deltas_per_step"] = a.deltas
         res["deltas_per_s"] = round(a.deltas * a.steps / el_max, 1)
     if filter_sharded:
-        res["merged_hits_per_step"] = merged_total
+        res["merged_hits_this_rank_slice"] = merged_total
+        res["merged_topics_this_rank_slice"] = merged_topics
+        if xch is not None:
+            res["exchange"] = {"per_peer_capacity": xch.per_peer, "slice": xch.s,
+                               "collectives": "all_to_all_single of u32 counts + padded u32 values (RCCL)"}
     if cpu:
         res["speedup_vs_cpu"] = round(value / cpu["value"], 1)
+    if not res["checks"]["walk_isolated_le_ms_per_step"]:
+        log(f"WARNING: isolated walk {iso_ms:.4f} ms > ms_per_step {ms_per_step:.4f} ms")
     print(json.dumps(res), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def concurrent_latency(ix, ts, nthreads: int, lb: int, seconds: float = 1.5):
+    """Concurrent callers (SURVEY.md 8b Threading: every client process calls
+    matches/3 at once): `nthreads` host threads each submit lb-topic batches
+    through tm_match_batch with their own tm_host_alloc buffers while one more
+    thread applies subscribe/unsubscribe deltas; ctypes drops the GIL for the
+    call, so the batches overlap inside the library.  -> per-batch p50/p99 and
+    the aggregate rate."""
+    from emqx_amd import _native
+    subs = []
+    for k in range(nthreads):
+        sub = ts.slice(k * lb, (k + 1) * lb)
+        nbytes = int(sub.offs[-1])
+        pb = ix.host_array(nbytes + 16, np.uint8)
+        po = ix.host_array(lb + 1, np.uint64)
+        pb[:nbytes] = sub.blob[:nbytes]
+        po[:] = sub.offs
+        _, v0, _ = ix.match_batch(sub.blob, sub.offs)
+        bufs = (ix.host_array(lb + 1, np.uint64), ix.host_array(len(v0) + 4096, np.uint32), ix.host_array(lb, np.uint8))
+        subs.append((pb, po, bufs))
+    stop = threading.Event()
+    lat = [[] for _ in range(nthreads)]
+
+    def caller(k):
+        pb, po, bufs = subs[k]
+        while not stop.is_set():
+            t1 = time.perf_counter()
+            ix.match_batch(pb, po, out=bufs)
+            lat[k].append((time.perf_counter() - t1) * 1e3)
+
+    nd = [0]
+
+    def churn():
+        d = _native.pack_strings([b"bench/concurrent/%d/+" % i for i in range(256)])
+        vals = np.arange(256, dtype=np.uint32) + np.uint32(0xF0000000)
+        op = 1
+        while not stop.is_set():
+            ix.apply(np.full(256, op, np.uint8), d[0], d[1], vals)
+            nd[0] += 256
+            op ^= 1
+            time.sleep(0.001)
+
+    th = [threading.Thread(target=caller, args=(k,)) for k in range(nthreads)] + [threading.Thread(target=churn)]
+    t0 = time.perf_counter()
+    for x in th:
+        x.start()
+    time.sleep(seconds)
+    stop.set()
+    for x in th:
+        x.join()
+    el = time.perf_counter() - t0
+    xs = np.concatenate([np.array(v[2:]) for v in lat if len(v) > 2])
+    nbatches = sum(len(v) for v in lat)
+    return {"threads": nthreads, "topics_per_batch": lb, "batches": int(nbatches),
+            "p50_ms": round(float(np.percentile(xs, 50)), 3), "p99_ms": round(float(np.percentile(xs, 99)), 3),
+            "topics_per_s": round(nbatches * lb / el, 1), "deltas_per_s": round(nd[0] / el, 1),
+            "buffers": "tm_host_alloc per thread (in place)"}
 
 
 if __name__ == "__main__":

@@ -21,7 +21,8 @@ TM_KEY_BINARY, TM_KEY_WORDS, TM_KEY_EMPTY_LIST = 0, 1, 2
 # every symbol include/tmatch.h declares (tests check the export table)
 EXPORTS = ("tm_create", "tm_destroy", "tm_apply_deltas", "tm_sync", "tm_match_batch",
            "tm_match_batch_dev", "tm_first_batch", "tm_stats", "tm_profile_enable", "tm_profile_read",
-           "tm_last_error", "tm_abi_version", "tm_merge_shards", "tm_host_alloc", "tm_host_free")
+           "tm_last_error", "tm_abi_version", "tm_merge_shards", "tm_host_alloc", "tm_host_free",
+           "tm_stream_release")
 
 
 class NativeUnavailable(RuntimeError):
@@ -75,6 +76,7 @@ def load_library(path: Path | None = None):
         "tm_merge_shards": (i32, [u32, u64, vp, vp, u64, vp, vp, u64, vp]),
         "tm_host_alloc": (i32, [vp, u64, C.POINTER(vp)]),
         "tm_host_free": (i32, [vp, vp]),
+        "tm_stream_release": (i32, [vp, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -230,6 +232,10 @@ class Index:
     def match_batch_dev(self, n: int, d_blob: int, d_offs: int, d_hit: int, d_out: int, cap: int, d_err: int,
                         stream: int | None = None):
         self._check(self._lib.tm_match_batch_dev(self._h, n, d_blob, d_offs, d_hit, d_out, cap, d_err, stream))
+
+    def release_stream(self, stream: int | None):
+        """Drop the batch scratch the library keeps for `stream`."""
+        self._check(self._lib.tm_stream_release(self._h, stream))
 
     def profile(self, enable: bool = True):
         self._check(self._lib.tm_profile_enable(self._h, int(enable)))

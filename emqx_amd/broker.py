@@ -81,13 +81,19 @@ class Broker:
 
     def publish_batch(self, msgs):
         """do_publish/1 for every message of a batch, with one device match.
-        -> per message: (routes after aggre, route results)."""
+        -> per message: (routes after aggre, route results), or the exception
+        of a message whose topic is invalid (badarg): it fails alone, the
+        other messages of the batch are routed (emqx_trie_search.erl:374-375
+        raises in the one publishing process)."""
         if not msgs:
             return []
-        all_routes = self.router.match_routes_batch([m.topic for m in msgs])
+        all_routes = self.router.match_routes_batch([m.topic for m in msgs], errors="return")
         self.batches += 1
         out = []
         for m, routes in zip(msgs, all_routes):
+            if isinstance(routes, Exception):
+                out.append(routes)
+                continue
             agg = aggre(routes)
             out.append((agg, [self._route2(r, m) for r in agg]))
         return out
@@ -116,8 +122,11 @@ class Broker:
         try:
             res = self.publish_batch([m for m, _ in batch])
             for (_, fut), r in zip(batch, res):
-                fut.set_result(r)
-        except BaseException as e:   # the batch's callers see the error (e.g. badarg)
+                if isinstance(r, Exception):
+                    fut.set_exception(r)        # this message only (badarg)
+                else:
+                    fut.set_result(r)
+        except BaseException as e:   # a failure of the whole batch (device error): every caller sees it
             for _, fut in batch:
                 if not fut.done():
                     fut.set_exception(e)

@@ -22,6 +22,22 @@ LIB_ORACLE = ROOT / "oracle" / "liboracle.so"
 ARCH = os.environ.get("TM_OFFLOAD_ARCH", "gfx950")
 
 
+KERNEL_SOURCES = ("tm_kernels.hip", "tm_host.cpp", "tm_layout.h", "tm_dev.h")
+
+
+def source_hash() -> str:
+    """Hash of the sources the match kernels are built from.  Measurements
+    that cannot be taken inside bench.py itself (rocprofv3 PMC counters,
+    profiles/pmc_<config>.json) are stamped with it, and bench.py refuses a
+    stamp that does not match the tree it runs."""
+    import hashlib
+    h = hashlib.sha256()
+    for name in KERNEL_SOURCES:
+        h.update(name.encode())
+        h.update((CSRC / name).read_bytes())
+    return h.hexdigest()[:16]
+
+
 def _stale(out: Path, deps) -> bool:
     if not out.exists():
         return True

@@ -16,6 +16,8 @@
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
+#include <condition_variable>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <unordered_set>
@@ -72,11 +74,47 @@ struct WordRef { const uint8_t *p; uint32_t n; int kind; };   // kind: 0 binary,
 
 }  // namespace
 
+// Per-caller execution context.  Host-API callers (tm_match_batch /
+// tm_first_batch) check one out of a pool, so concurrent callers -- every
+// client process calls matches/3 at once in the reference, on a shared
+// read_concurrency table (emqx_topic_index.erl:41-48) -- run their batches on
+// their own streams with their own scratch and staging buffers, and wait for
+// the GPU without holding the index lock.  Device-API callers
+// (tm_match_batch_dev) get one per stream they pass, in a bounded LRU pool.
+struct Lane {
+    hipStream_t s = nullptr;
+    bool owned = false;       // stream created by the library (host-API lane)
+    bool busy = false;        // checked out by a host-API caller
+    bool used = false;        // `done` has been recorded
+    hipEvent_t done = nullptr;   // after the lane's last batch: later patches wait for it
+    uint64_t tick = 0;        // last use (LRU of device-API lanes)
+    Workspace w{};
+    // host-API staging: mapped pinned buffers (*_dev = their device
+    // addresses) and the HBM copies used for batches above ZC_TOPICS
+    uint8_t *pin_in = nullptr, *pin_in_dev = nullptr; uint64_t pin_in_cap = 0;
+    uint8_t *pin_out = nullptr, *pin_out_dev = nullptr; uint64_t pin_out_cap = 0;
+    uint8_t *d_in = nullptr; uint64_t d_in_cap = 0;
+    uint8_t *d_res = nullptr; uint64_t d_res_cap = 0;
+    uint32_t *pin_vals = nullptr, *pin_vals_dev = nullptr; uint64_t pin_vals_cap = 0;
+};
+
+// Patch staging: a small ring, so shipping a patch waits on the host only for
+// the patch PATCH_RING before it, not for the one just enqueued.
+constexpr int PATCH_RING = 4;
+struct PatchSlot {
+    uint64_t *pin_addr = nullptr; uint32_t *pin_val = nullptr; uint64_t pin_cap = 0;
+    uint64_t *dev_addr = nullptr; uint32_t *dev_val = nullptr; uint64_t dev_cap = 0;
+    hipEvent_t done = nullptr; bool pending = false;
+};
+
+constexpr int MAX_HOST_LANES = 16;   // concurrent host-API batches in flight
+constexpr int MAX_DEV_LANES = 16;    // device-API streams with a workspace kept
+
 struct tm_index {
     std::mutex mu;
+    std::condition_variable cv;      // a host lane was released
     int device = 0;
-    hipStream_t stream = nullptr;
-    std::string err;
+    hipStream_t stream = nullptr;    // the index's own stream (tm_sync, device API with stream NULL)
 
     Mirror<VocabEntry> vocab; uint64_t vcount = 0;
     Mirror<uint8_t> wpool;
@@ -91,25 +129,12 @@ struct tm_index {
     uint64_t n_wild = 0, n_exact = 0;
     uint64_t uploads = 0, patch_bytes = 0;
 
-    // patch staging
-    uint64_t *pin_addr = nullptr; uint32_t *pin_val = nullptr; uint64_t pin_cap = 0;
-    uint64_t *dev_addr = nullptr; uint32_t *dev_val = nullptr; uint64_t dev_pcap = 0;
-    hipEvent_t patch_done = nullptr; bool patch_pending = false;
+    PatchSlot patch[PATCH_RING]; uint32_t patch_head = 0;
+    hipEvent_t last_patch = nullptr;   // event of the latest patch (every batch waits for it)
 
-    // per-batch workspaces, one per stream that has run a batch: batches on
-    // different streams may overlap (a broker pipelines micro-batches)
-    struct WsSlot { hipStream_t s; Workspace w; hipEvent_t done; bool used; };
-    std::vector<WsSlot> wss;
-    bool patched = false;   // patch_done has been recorded at least once
+    std::vector<std::unique_ptr<Lane>> lanes;
+    uint64_t tick = 0;
 
-    // host-API staging
-    // host-API staging: mapped pinned buffers (pin_*_dev = their device
-    // addresses) and the HBM copies used for batches above ZC_TOPICS
-    uint8_t *pin_in = nullptr, *pin_in_dev = nullptr; uint64_t pin_in_cap = 0;
-    uint8_t *pin_out = nullptr, *pin_out_dev = nullptr; uint64_t pin_out_cap = 0;
-    uint8_t *d_in = nullptr; uint64_t d_in_cap = 0;
-    uint8_t *d_res = nullptr; uint64_t d_res_cap = 0;
-    uint32_t *pin_vals = nullptr, *pin_vals_dev = nullptr; uint64_t pin_vals_cap = 0;
     // caller buffers from tm_host_alloc (host address -> size, device address)
     struct Pinned { uint8_t *host, *dev; uint64_t size; };
     std::vector<Pinned> pinned;
@@ -124,8 +149,9 @@ struct tm_index {
 
 namespace {
 
-int fail(tm_index *h, int code, const std::string &msg) {
-    if (h) h->err = msg;
+// errors are kept per calling thread (tm_last_error): concurrent callers of
+// one index each see their own
+int fail(tm_index *, int code, const std::string &msg) {
     g_last_error = msg;
     return code;
 }
@@ -773,16 +799,20 @@ int collect(tm_index *ix, Mirror<T> &m, std::vector<uint64_t> &addr, std::vector
     return TM_OK;
 }
 
-// a batch on stream s is done with the index: later patches (on any stream) wait for it
-int batch_done(tm_index *ix, hipStream_t s) {
-    for (auto &e : ix->wss)
-        if (e.s == s) { HIPCHK(ix, hipEventRecord(e.done, s)); e.used = true; }
+// the lane's batch is done with the index: later patches (on any stream) wait for it
+int batch_done(tm_index *ix, Lane &ln) {
+    HIPCHK(ix, hipEventRecord(ln.done, ln.s));
+    ln.used = true;
     return TM_OK;
 }
 
+// Ship every dirty word to HBM on stream s (caller holds ix->mu).  Patches
+// rewrite the tables in place, so a patch first waits for every batch still
+// reading them (each lane's `done`) and for the patch before it; every later
+// batch waits for this one (`last_patch`, ensure_ws): a batch sees exactly the
+// deltas applied before it (C5), whichever stream either ran on.
 int sync_locked(tm_index *ix, hipStream_t s) {
     HIPCHK(ix, hipSetDevice(ix->device));
-    if (ix->patch_pending) { HIPCHK(ix, hipEventSynchronize(ix->patch_done)); ix->patch_pending = false; }
     std::vector<uint64_t> addr;
     std::vector<uint32_t> val;
     int rc;
@@ -796,33 +826,36 @@ int sync_locked(tm_index *ix, hipStream_t s) {
     if ((rc = collect(ix, ix->wseq, addr, val))) return rc;
     const uint64_t n = addr.size();
     if (!n) return TM_OK;
-    if (n > ix->pin_cap) {
-        if (ix->pin_addr) HIPCHK(ix, hipHostFree(ix->pin_addr));
-        if (ix->pin_val) HIPCHK(ix, hipHostFree(ix->pin_val));
-        ix->pin_cap = n + n / 2 + 1024;
-        HIPCHK(ix, hipHostMalloc(&ix->pin_addr, ix->pin_cap * 8, hipHostMallocDefault));
-        HIPCHK(ix, hipHostMalloc(&ix->pin_val, ix->pin_cap * 4, hipHostMallocDefault));
+    PatchSlot &p = ix->patch[ix->patch_head % PATCH_RING];
+    ix->patch_head++;
+    if (p.pending) { HIPCHK(ix, hipEventSynchronize(p.done)); p.pending = false; }
+    if (n > p.pin_cap) {
+        if (p.pin_addr) HIPCHK(ix, hipHostFree(p.pin_addr));
+        if (p.pin_val) HIPCHK(ix, hipHostFree(p.pin_val));
+        p.pin_addr = nullptr; p.pin_val = nullptr;
+        p.pin_cap = n + n / 2 + 1024;
+        HIPCHK(ix, hipHostMalloc(&p.pin_addr, p.pin_cap * 8, hipHostMallocDefault));
+        HIPCHK(ix, hipHostMalloc(&p.pin_val, p.pin_cap * 4, hipHostMallocDefault));
     }
-    if (n > ix->dev_pcap) {
-        HIPCHK(ix, hipStreamSynchronize(s));
-        if (ix->dev_addr) HIPCHK(ix, hipFree(ix->dev_addr));
-        if (ix->dev_val) HIPCHK(ix, hipFree(ix->dev_val));
-        ix->dev_pcap = n + n / 2 + 1024;
-        HIPCHK(ix, hipMalloc(&ix->dev_addr, ix->dev_pcap * 8));
-        HIPCHK(ix, hipMalloc(&ix->dev_val, ix->dev_pcap * 4));
+    if (n > p.dev_cap) {   // the slot's previous patch has completed (p.done above)
+        if (p.dev_addr) HIPCHK(ix, hipFree(p.dev_addr));
+        if (p.dev_val) HIPCHK(ix, hipFree(p.dev_val));
+        p.dev_addr = nullptr; p.dev_val = nullptr;
+        p.dev_cap = n + n / 2 + 1024;
+        HIPCHK(ix, hipMalloc(&p.dev_addr, p.dev_cap * 8));
+        HIPCHK(ix, hipMalloc(&p.dev_val, p.dev_cap * 4));
     }
-    memcpy(ix->pin_addr, addr.data(), n * 8);
-    memcpy(ix->pin_val, val.data(), n * 4);
-    // patches rewrite the tables in place: wait for batches still reading them
-    // on other streams (a batch sees exactly the deltas applied before it)
-    for (auto &e : ix->wss)
-        if (e.used && e.s != s) HIPCHK(ix, hipStreamWaitEvent(s, e.done, 0));
-    HIPCHK(ix, hipMemcpyAsync(ix->dev_addr, ix->pin_addr, n * 8, hipMemcpyHostToDevice, s));
-    HIPCHK(ix, hipMemcpyAsync(ix->dev_val, ix->pin_val, n * 4, hipMemcpyHostToDevice, s));
-    HIPCHK(ix, launch_patch(ix->dev_addr, ix->dev_val, n, s));
-    HIPCHK(ix, hipEventRecord(ix->patch_done, s));
-    ix->patch_pending = true;
-    ix->patched = true;
+    memcpy(p.pin_addr, addr.data(), n * 8);
+    memcpy(p.pin_val, val.data(), n * 4);
+    for (auto &l : ix->lanes)
+        if (l->used && l->s != s) HIPCHK(ix, hipStreamWaitEvent(s, l->done, 0));
+    if (ix->last_patch) HIPCHK(ix, hipStreamWaitEvent(s, ix->last_patch, 0));
+    HIPCHK(ix, hipMemcpyAsync(p.dev_addr, p.pin_addr, n * 8, hipMemcpyHostToDevice, s));
+    HIPCHK(ix, hipMemcpyAsync(p.dev_val, p.pin_val, n * 4, hipMemcpyHostToDevice, s));
+    HIPCHK(ix, launch_patch(p.dev_addr, p.dev_val, n, s));
+    HIPCHK(ix, hipEventRecord(p.done, s));
+    p.pending = true;
+    ix->last_patch = p.done;
     ix->patch_bytes += n * 4;
     ix->uploads++;
     return TM_OK;
@@ -841,10 +874,96 @@ DevIndex dev_view(tm_index *ix) {
     return d;
 }
 
+// ------------------------------------------------------------------ lanes
+
+void free_workspace(Workspace &w) {
+    void *wb[] = {w.cnt, w.nr, w.rng, w.lists, w.list_n, w.blk, w.deep_wid, w.deep_stk};
+    for (void *p : wb) if (p) (void)hipFree(p);
+    w = Workspace{};
+}
+
+void free_lane(Lane &l) {
+    free_workspace(l.w);
+    void *dv[] = {l.d_in, l.d_res};
+    for (void *p : dv) if (p) (void)hipFree(p);
+    void *pins[] = {l.pin_in, l.pin_out, l.pin_vals};
+    for (void *p : pins) if (p) (void)hipHostFree(p);
+    if (l.done) (void)hipEventDestroy(l.done);
+    if (l.owned && l.s) (void)hipStreamDestroy(l.s);
+}
+
+int make_lane(tm_index *ix, hipStream_t s, bool owned, Lane *&out) {
+    auto l = std::make_unique<Lane>();
+    l->owned = owned;
+    if (owned) HIPCHK(ix, hipStreamCreateWithFlags(&l->s, hipStreamNonBlocking));
+    else l->s = s;
+    HIPCHK(ix, hipEventCreateWithFlags(&l->done, hipEventDisableTiming));
+    out = l.get();
+    ix->lanes.push_back(std::move(l));
+    return TM_OK;
+}
+
+// a host-API lane for this caller (waits while MAX_HOST_LANES are in use)
+int host_lane(tm_index *ix, std::unique_lock<std::mutex> &g, Lane *&out) {
+    for (;;) {
+        int owned = 0;
+        for (auto &l : ix->lanes) {
+            if (!l->owned) continue;
+            owned++;
+            if (!l->busy) { l->busy = true; out = l.get(); return TM_OK; }
+        }
+        if (owned < MAX_HOST_LANES) {
+            int rc = make_lane(ix, nullptr, true, out);
+            if (rc) return rc;
+            out->busy = true;
+            return TM_OK;
+        }
+        ix->cv.wait(g);
+    }
+}
+
+// releases a checked-out host lane on every exit path (retaking the lock if
+// the caller dropped it to wait for the GPU)
+struct LaneLease {
+    tm_index *ix;
+    std::unique_lock<std::mutex> &g;
+    Lane *ln = nullptr;
+    ~LaneLease() {
+        if (!ln) return;
+        if (!g.owns_lock()) g.lock();
+        ln->busy = false;
+        ix->cv.notify_one();
+    }
+};
+
+// the device-API lane of stream s; the least recently used one is retired
+// (after its batches finish) when MAX_DEV_LANES streams hold a workspace
+int dev_lane(tm_index *ix, hipStream_t s, Lane *&out) {
+    int n = 0;
+    size_t lru = SIZE_MAX;
+    for (size_t i = 0; i < ix->lanes.size(); i++) {
+        Lane &l = *ix->lanes[i];
+        if (l.owned) continue;
+        if (l.s == s) { l.tick = ++ix->tick; out = &l; return TM_OK; }
+        n++;
+        if (lru == SIZE_MAX || l.tick < ix->lanes[lru]->tick) lru = i;
+    }
+    if (n >= MAX_DEV_LANES && lru != SIZE_MAX) {
+        Lane &l = *ix->lanes[lru];
+        if (l.used) HIPCHK(ix, hipEventSynchronize(l.done));
+        free_lane(l);
+        ix->lanes.erase(ix->lanes.begin() + lru);
+    }
+    int rc = make_lane(ix, s, false, out);
+    if (rc) return rc;
+    out->tick = ++ix->tick;
+    return TM_OK;
+}
+
 template <class T>
-int grow_dev(tm_index *ix, T *&p, uint64_t &cap, uint64_t need) {
+int grow_dev(tm_index *ix, hipStream_t s, T *&p, uint64_t &cap, uint64_t need) {
     if (need <= cap && p) return TM_OK;
-    HIPCHK(ix, hipDeviceSynchronize());
+    HIPCHK(ix, hipStreamSynchronize(s));   // only this lane's stream uses its buffers
     if (p) HIPCHK(ix, hipFree(p));
     p = nullptr;
     cap = std::max<uint64_t>(need + need / 4, 64);
@@ -852,27 +971,18 @@ int grow_dev(tm_index *ix, T *&p, uint64_t &cap, uint64_t need) {
     return TM_OK;
 }
 
-int ensure_ws(tm_index *ix, uint64_t n, hipStream_t s, Workspace *&out) {
-    Workspace *wp = nullptr;
-    for (auto &e : ix->wss) if (e.s == s) wp = &e.w;
-    if (!wp) {
-        hipEvent_t ev;
-        HIPCHK(ix, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-        ix->wss.push_back({s, Workspace{}, ev, false});
-        wp = &ix->wss.back().w;
-    }
-    Workspace &w = *wp;
-    out = wp;
+int ensure_ws(tm_index *ix, uint64_t n, Lane &ln) {
+    Workspace &w = ln.w;
     if (!w.deep_wid) {
         HIPCHK(ix, hipMalloc(&w.deep_wid, (uint64_t)DEEP_LANES * MAX_LEVELS * 4));
         HIPCHK(ix, hipMalloc(&w.deep_stk, (uint64_t)DEEP_LANES * (MAX_LEVELS + 1) * 8));
         HIPCHK(ix, hipMalloc(&w.list_n, (L_COUNT + 2) * 4));
-        HIPCHK(ix, hipMemset(w.list_n, 0, (L_COUNT + 2) * 4));
+        HIPCHK(ix, hipMemsetAsync(w.list_n, 0, (L_COUNT + 2) * 4, ln.s));
     }
     // the batch must see every patch shipped so far, whichever stream it went on
-    if (ix->patched) HIPCHK(ix, hipStreamWaitEvent(s, ix->patch_done, 0));
+    if (ix->last_patch) HIPCHK(ix, hipStreamWaitEvent(ln.s, ix->last_patch, 0));
     if (n <= w.cap_n && w.cnt) return TM_OK;
-    HIPCHK(ix, hipDeviceSynchronize());
+    HIPCHK(ix, hipStreamSynchronize(ln.s));
     if (w.cnt) { (void)hipFree(w.cnt); (void)hipFree(w.nr); (void)hipFree(w.rng); (void)hipFree(w.lists); (void)hipFree(w.blk); }
     uint64_t c = std::max<uint64_t>(n + n / 4, 1024);
     HIPCHK(ix, hipMalloc(&w.cnt, c * 4));
@@ -880,7 +990,7 @@ int ensure_ws(tm_index *ix, uint64_t n, hipStream_t s, Workspace *&out) {
     HIPCHK(ix, hipMalloc(&w.rng, c * RCAP * 8));
     HIPCHK(ix, hipMalloc(&w.lists, c * L_COUNT * 4));
     HIPCHK(ix, hipMalloc(&w.blk, (c / TILE + 4) * 8));
-    HIPCHK(ix, hipMemset(w.blk, 0, (c / TILE + 4) * 8));   // zero between batches (k_emit)
+    HIPCHK(ix, hipMemsetAsync(w.blk, 0, (c / TILE + 4) * 8, ln.s));   // zero between batches (k_emit)
     w.cap_n = c;
     return TM_OK;
 }
@@ -921,15 +1031,22 @@ int prof_end(tm_index *ix, tm_index::ProfEv &ev, hipStream_t s) {
     return TM_OK;
 }
 
+// wait for every batch of every lane (caller holds ix->mu)
+int drain_lanes(tm_index *ix) {
+    for (auto &l : ix->lanes)
+        if (l->used) HIPCHK(ix, hipEventSynchronize(l->done));
+    return TM_OK;
+}
+
 }  // namespace
 
 // =================================================================== C ABI
 
 extern "C" {
 
-uint32_t tm_abi_version(void) { return (1u << 16) | 2u; }
+uint32_t tm_abi_version(void) { return (1u << 16) | 3u; }
 
-const char *tm_last_error(tm_index *h) { return h ? h->err.c_str() : g_last_error.c_str(); }
+const char *tm_last_error(tm_index *) { return g_last_error.c_str(); }
 
 int tm_create(const tm_options *opts, tm_index **out) {
     if (!out) return fail(nullptr, TM_EINVAL, "tm_create: out is NULL");
@@ -943,7 +1060,8 @@ int tm_create(const tm_options *opts, tm_index **out) {
     ix->device = dev;
     hipError_t e = hipSetDevice(dev);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&ix->stream, hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&ix->patch_done, hipEventDisableTiming);
+    for (int i = 0; i < PATCH_RING && e == hipSuccess; i++)
+        e = hipEventCreateWithFlags(&ix->patch[i].done, hipEventDisableTiming);
     if (e != hipSuccess) {
         std::string m = std::string("tm_create: ") + hipGetErrorString(e);
         delete ix;
@@ -957,21 +1075,20 @@ int tm_create(const tm_options *opts, tm_index **out) {
 int tm_destroy(tm_index *ix) {
     if (!ix) return TM_EINVAL;
     (void)hipSetDevice(ix->device);
-    (void)hipStreamSynchronize(ix->stream);
-    void *bufs[] = {ix->vocab.d, ix->wpool.d, ix->nodes.d, ix->ctab.d, ix->vals.d, ix->exact.d, ix->xfp.d, ix->wseq.d,
-                    ix->dev_addr, ix->dev_val,
-                    ix->d_in, ix->d_res};
+    (void)hipDeviceSynchronize();
+    void *bufs[] = {ix->vocab.d, ix->wpool.d, ix->nodes.d, ix->ctab.d, ix->vals.d, ix->exact.d, ix->xfp.d, ix->wseq.d};
     for (void *p : bufs) if (p) (void)hipFree(p);
-    for (auto &e : ix->wss) {
-        (void)hipEventDestroy(e.done);
-        const Workspace &w = e.w;
-        void *wb[] = {w.cnt, w.nr, w.rng, w.lists, w.list_n, w.blk, w.deep_wid, w.deep_stk};
-        for (void *p : wb) if (p) (void)hipFree(p);
+    for (auto &l : ix->lanes) free_lane(*l);
+    for (auto &p : ix->patch) {
+        void *dv[] = {p.dev_addr, p.dev_val};
+        for (void *q : dv) if (q) (void)hipFree(q);
+        void *pins[] = {p.pin_addr, p.pin_val};
+        for (void *q : pins) if (q) (void)hipHostFree(q);
+        if (p.done) (void)hipEventDestroy(p.done);
     }
-    void *pins[] = {ix->pin_addr, ix->pin_val, ix->pin_in, ix->pin_out, ix->pin_vals};
-    for (void *p : pins) if (p) (void)hipHostFree(p);
     for (auto &b : ix->pinned) (void)hipHostFree(b.host);
-    (void)hipEventDestroy(ix->patch_done);
+    for (auto &ev : ix->prof_pending) { (void)hipEventDestroy(ev.b0); (void)hipEventDestroy(ev.w0); (void)hipEventDestroy(ev.w1); (void)hipEventDestroy(ev.b1); }
+    for (auto &ev : ix->prof_free) { (void)hipEventDestroy(ev.b0); (void)hipEventDestroy(ev.w0); (void)hipEventDestroy(ev.w1); (void)hipEventDestroy(ev.b1); }
     (void)hipStreamDestroy(ix->stream);
     delete ix;
     return TM_OK;
@@ -982,10 +1099,10 @@ int tm_apply_deltas(tm_index *ix, uint64_t n, const uint8_t *ops, const uint8_t 
     if (!ix) return fail(nullptr, TM_EINVAL, "tm_apply_deltas: null handle");
     if (n && (!ops || !fo || !values || (!fb && fo[n] != fo[0])))
         return fail(ix, TM_EINVAL, "tm_apply_deltas: null buffer");
-    std::lock_guard<std::mutex> g(ix->mu);
     for (uint64_t i = 0; i < n; i++)
         if (ops[i] > TM_OP_INSERT || fo[i + 1] < fo[i] || fo[i + 1] - fo[i] > 0xFFFFFFFFull)
             return fail(ix, TM_EINVAL, "tm_apply_deltas: bad op or offsets at " + std::to_string(i));
+    std::lock_guard<std::mutex> g(ix->mu);
     std::vector<WordRef> w;
     std::vector<uint32_t> wids;
     try {
@@ -1013,15 +1130,31 @@ int tm_match_batch_dev(tm_index *ix, uint64_t n, const uint8_t *bytes, const uin
     hipStream_t s = pick_stream(ix, stream);
     int rc;
     if ((rc = sync_locked(ix, s))) return rc;
-    Workspace *ws;
-    if ((rc = ensure_ws(ix, n, s, ws))) return rc;
+    Lane *ln;
+    if ((rc = dev_lane(ix, s, ln))) return rc;
+    if ((rc = ensure_ws(ix, n, *ln))) return rc;
     const DevIndex d = dev_view(ix);
     tm_index::ProfEv ev;
     if ((rc = prof_begin(ix, ev, s))) return rc;
-    HIPCHK(ix, launch_match_phase1(d, *ws, n, bytes, offs, hit_offs, err, s, ev.w0, ev.w1));
-    HIPCHK(ix, launch_match_phase2(d, *ws, n, bytes, offs, hit_offs, out, out ? cap : 0, s));
-    if ((rc = batch_done(ix, s))) return rc;
+    HIPCHK(ix, launch_match_phase1(d, ln->w, n, bytes, offs, hit_offs, err, s, ev.w0, ev.w1));
+    HIPCHK(ix, launch_match_phase2(d, ln->w, n, bytes, offs, hit_offs, out, out ? cap : 0, s));
+    if ((rc = batch_done(ix, *ln))) return rc;
     return prof_end(ix, ev, s);
+}
+
+int tm_stream_release(tm_index *ix, void *stream) {
+    if (!ix) return fail(nullptr, TM_EINVAL, "tm_stream_release: null handle");
+    std::lock_guard<std::mutex> g(ix->mu);
+    hipStream_t s = pick_stream(ix, stream);
+    for (size_t i = 0; i < ix->lanes.size(); i++) {
+        Lane &l = *ix->lanes[i];
+        if (l.owned || l.s != s) continue;
+        if (l.used) HIPCHK(ix, hipEventSynchronize(l.done));
+        free_lane(l);
+        ix->lanes.erase(ix->lanes.begin() + i);
+        break;
+    }
+    return TM_OK;
 }
 
 namespace {
@@ -1047,22 +1180,22 @@ int pin_mapped(tm_index *ix, hipStream_t s, uint8_t *&host, uint8_t *&dev, uint6
 }
 
 // a host topic batch -> what the kernels read: rebased offsets, then the bytes
-// (16-aligned: the walk's aligned 16-byte loads), in one buffer
-int stage_in(tm_index *ix, uint64_t n, const uint8_t *tb, const uint64_t *to, hipStream_t s,
+// (16-aligned: the walk's aligned 16-byte loads), in one buffer of the lane
+int stage_in(tm_index *ix, Lane &ln, uint64_t n, const uint8_t *tb, const uint64_t *to,
              const uint8_t *&dbytes, const uint64_t *&doffs) {
     const uint64_t b0 = to[0], nbytes = to[n] - b0;
     const uint64_t boff = ((n + 1) * 8 + 15) & ~15ull;
     const uint64_t need = boff + nbytes + 16;
     int rc;
-    if ((rc = pin_mapped(ix, s, ix->pin_in, ix->pin_in_dev, ix->pin_in_cap, need))) return rc;
-    uint64_t *po = reinterpret_cast<uint64_t *>(ix->pin_in);
+    if ((rc = pin_mapped(ix, ln.s, ln.pin_in, ln.pin_in_dev, ln.pin_in_cap, need))) return rc;
+    uint64_t *po = reinterpret_cast<uint64_t *>(ln.pin_in);
     for (uint64_t i = 0; i <= n; i++) po[i] = to[i] - b0;
-    if (nbytes) memcpy(ix->pin_in + boff, tb + b0, nbytes);
-    const uint8_t *base = ix->pin_in_dev;
+    if (nbytes) memcpy(ln.pin_in + boff, tb + b0, nbytes);
+    const uint8_t *base = ln.pin_in_dev;
     if (n > ZC_TOPICS) {
-        if ((rc = grow_dev(ix, ix->d_in, ix->d_in_cap, need))) return rc;
-        HIPCHK(ix, hipMemcpyAsync(ix->d_in, ix->pin_in, boff + nbytes, hipMemcpyHostToDevice, s));
-        base = ix->d_in;
+        if ((rc = grow_dev(ix, ln.s, ln.d_in, ln.d_in_cap, need))) return rc;
+        HIPCHK(ix, hipMemcpyAsync(ln.d_in, ln.pin_in, boff + nbytes, hipMemcpyHostToDevice, ln.s));
+        base = ln.d_in;
     }
     doffs = reinterpret_cast<const uint64_t *>(base);
     dbytes = base + boff;
@@ -1070,19 +1203,19 @@ int stage_in(tm_index *ix, uint64_t n, const uint8_t *tb, const uint64_t *to, hi
 }
 
 // where the kernels write `bytes` of per-topic results (read back by fetch_out)
-int stage_out(tm_index *ix, uint64_t n, uint64_t bytes, hipStream_t s, uint8_t *&dout) {
+int stage_out(tm_index *ix, Lane &ln, uint64_t n, uint64_t bytes, uint8_t *&dout) {
     int rc;
-    if ((rc = pin_mapped(ix, s, ix->pin_out, ix->pin_out_dev, ix->pin_out_cap, bytes + 16))) return rc;
-    dout = ix->pin_out_dev;
+    if ((rc = pin_mapped(ix, ln.s, ln.pin_out, ln.pin_out_dev, ln.pin_out_cap, bytes + 16))) return rc;
+    dout = ln.pin_out_dev;
     if (n > ZC_TOPICS) {
-        if ((rc = grow_dev(ix, ix->d_res, ix->d_res_cap, bytes + 16))) return rc;
-        dout = ix->d_res;
+        if ((rc = grow_dev(ix, ln.s, ln.d_res, ln.d_res_cap, bytes + 16))) return rc;
+        dout = ln.d_res;
     }
     return TM_OK;
 }
 
-int fetch_out(tm_index *ix, uint64_t n, uint64_t bytes, hipStream_t s) {
-    if (n > ZC_TOPICS && bytes) HIPCHK(ix, hipMemcpyAsync(ix->pin_out, ix->d_res, bytes, hipMemcpyDeviceToHost, s));
+int fetch_out(tm_index *ix, Lane &ln, uint64_t n, uint64_t bytes) {
+    if (n > ZC_TOPICS && bytes) HIPCHK(ix, hipMemcpyAsync(ln.pin_out, ln.d_res, bytes, hipMemcpyDeviceToHost, ln.s));
     return TM_OK;
 }
 
@@ -1117,7 +1250,8 @@ int tm_host_free(tm_index *ix, void *p) {
     for (size_t i = 0; i < ix->pinned.size(); i++) {
         if (ix->pinned[i].host != p) continue;
         HIPCHK(ix, hipSetDevice(ix->device));
-        HIPCHK(ix, hipStreamSynchronize(ix->stream));   // no batch may still write it
+        int rc = drain_lanes(ix);   // no batch may still read or write it
+        if (rc) return rc;
         HIPCHK(ix, hipHostFree(p));
         ix->pinned.erase(ix->pinned.begin() + i);
         return TM_OK;
@@ -1130,6 +1264,10 @@ static double now_us() {
     return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
+// Host-API batches hold the index lock only to ship pending patches, pick up
+// the index's current device view and queue the kernels on the caller's lane;
+// they wait for the GPU and copy results out without it, so concurrent callers
+// overlap on the device (each lane is its own stream) and deltas keep flowing.
 int tm_match_batch(tm_index *ix, uint64_t n, const uint8_t *tb, const uint64_t *to, uint64_t *out_hit,
                    uint32_t *out_vals, uint64_t cap, uint8_t *out_err) {
     static const bool timing = getenv("TM_HOST_TIMING") != nullptr;
@@ -1138,13 +1276,15 @@ int tm_match_batch(tm_index *ix, uint64_t n, const uint8_t *tb, const uint64_t *
     if (!ix) return fail(nullptr, TM_EINVAL, "tm_match_batch: null handle");
     if (!to || !out_hit || (n && !tb && to[n] != to[0])) return fail(ix, TM_EINVAL, "tm_match_batch: null buffer");
     if (n >= 0xFFFFFFFFull) return fail(ix, TM_EINVAL, "tm_match_batch: batch too large");
-    std::lock_guard<std::mutex> g(ix->mu);
+    std::unique_lock<std::mutex> g(ix->mu);
     HIPCHK(ix, hipSetDevice(ix->device));
-    hipStream_t s = ix->stream;
+    LaneLease lease{ix, g};
     int rc;
+    if ((rc = host_lane(ix, g, lease.ln))) return rc;
+    Lane &ln = *lease.ln;
+    const hipStream_t s = ln.s;
     if ((rc = sync_locked(ix, s))) return rc;
-    Workspace *ws;
-    if ((rc = ensure_ws(ix, n, s, ws))) return rc;
+    if ((rc = ensure_ws(ix, n, ln))) return rc;
     if (timing) tt[nt++] = now_us();
     if (n && n <= ZC_TOPICS) {
         // every buffer from tm_host_alloc: the kernels read the topics and
@@ -1158,14 +1298,16 @@ int tm_match_batch(tm_index *ix, uint64_t n, const uint8_t *tb, const uint64_t *
         const bool aligned = ((uintptr_t)tb & 15) == 0;
         if ((db || !nbytes) && aligned && dof && dh && (dv || !out_vals) && (de || !out_err)) {
             if (!de) {   // flags nobody reads still need a home
-                if ((rc = stage_out(ix, n, n, s, de))) return rc;
+                if ((rc = stage_out(ix, ln, n, n, de))) return rc;
             }
             const DevIndex d = dev_view(ix);
             const uint8_t *dbytes = db ? db : dof;   // no bytes: any valid address
             uint64_t *dhit = reinterpret_cast<uint64_t *>(dh);
-            HIPCHK(ix, launch_match_phase1(d, *ws, n, dbytes, reinterpret_cast<const uint64_t *>(dof), dhit, de, s));
-            HIPCHK(ix, launch_match_phase2(d, *ws, n, dbytes, reinterpret_cast<const uint64_t *>(dof), dhit,
+            HIPCHK(ix, launch_match_phase1(d, ln.w, n, dbytes, reinterpret_cast<const uint64_t *>(dof), dhit, de, s));
+            HIPCHK(ix, launch_match_phase2(d, ln.w, n, dbytes, reinterpret_cast<const uint64_t *>(dof), dhit,
                                            reinterpret_cast<uint32_t *>(dv), dv ? cap : 0, s));
+            if ((rc = batch_done(ix, ln))) return rc;
+            g.unlock();
             if (timing) tt[nt++] = now_us();
             HIPCHK(ix, hipStreamSynchronize(s));
             if (timing) {
@@ -1178,41 +1320,46 @@ int tm_match_batch(tm_index *ix, uint64_t n, const uint8_t *tb, const uint64_t *
     }
     const uint8_t *dbytes;
     const uint64_t *doffs;
-    if ((rc = stage_in(ix, n, tb, to, s, dbytes, doffs))) return rc;
+    if ((rc = stage_in(ix, ln, n, tb, to, dbytes, doffs))) return rc;
     if (timing) tt[nt++] = now_us();
     // results: hit offsets (n + 1) x u64, then the badarg flags; the values are
     // written by k_emit straight into mapped pinned memory, so the batch costs
     // one host synchronisation (a second one only when that buffer must grow)
     const uint64_t rbytes = (n + 1) * 8 + n;
     uint8_t *dres;
-    if ((rc = stage_out(ix, n, rbytes, s, dres))) return rc;
+    if ((rc = stage_out(ix, ln, n, rbytes, dres))) return rc;
     uint64_t *dhit = reinterpret_cast<uint64_t *>(dres);
     uint8_t *derr = dres + (n + 1) * 8;
-    const DevIndex d = dev_view(ix);
     uint64_t total = 0;
     for (int attempt = 0; attempt < 2; attempt++) {
-        if (!ix->pin_vals) {
-            ix->pin_vals_cap = std::max<uint64_t>(ix->pin_vals_cap, 1 << 16);
-            HIPCHK(ix, hipHostMalloc(&ix->pin_vals, ix->pin_vals_cap * 4, hipHostMallocMapped));
-            HIPCHK(ix, hipHostGetDevicePointer(reinterpret_cast<void **>(&ix->pin_vals_dev), ix->pin_vals, 0));
+        if (!ln.pin_vals) {
+            ln.pin_vals_cap = std::max<uint64_t>(ln.pin_vals_cap, 1 << 16);
+            HIPCHK(ix, hipHostMalloc(&ln.pin_vals, ln.pin_vals_cap * 4, hipHostMallocMapped));
+            HIPCHK(ix, hipHostGetDevicePointer(reinterpret_cast<void **>(&ln.pin_vals_dev), ln.pin_vals, 0));
         }
-        HIPCHK(ix, launch_match_phase1(d, *ws, n, dbytes, doffs, dhit, derr, s));
-        HIPCHK(ix, launch_match_phase2(d, *ws, n, dbytes, doffs, dhit, ix->pin_vals_dev, ix->pin_vals_cap, s));
-        if ((rc = fetch_out(ix, n, rbytes, s))) return rc;
+        const DevIndex d = dev_view(ix);
+        HIPCHK(ix, launch_match_phase1(d, ln.w, n, dbytes, doffs, dhit, derr, s));
+        HIPCHK(ix, launch_match_phase2(d, ln.w, n, dbytes, doffs, dhit, ln.pin_vals_dev, ln.pin_vals_cap, s));
+        if ((rc = fetch_out(ix, ln, n, rbytes))) return rc;
+        if ((rc = batch_done(ix, ln))) return rc;
+        g.unlock();
         if (timing && nt < 5) tt[nt++] = now_us();
         HIPCHK(ix, hipStreamSynchronize(s));
         if (timing && nt < 6) tt[nt++] = now_us();
-        memcpy(&total, ix->pin_out + n * 8, 8);
-        if (total <= ix->pin_vals_cap || !out_vals || total <= 0) break;
+        memcpy(&total, ln.pin_out + n * 8, 8);
+        if (total <= ln.pin_vals_cap || !out_vals || total <= 0) break;
         // grow the mapped buffer and run the batch again (rare: sizes are sticky)
-        HIPCHK(ix, hipHostFree(ix->pin_vals));
-        ix->pin_vals = nullptr;
-        ix->pin_vals_cap = total + total / 4;
+        g.lock();
+        HIPCHK(ix, hipHostFree(ln.pin_vals));
+        ln.pin_vals = nullptr;
+        ln.pin_vals_cap = total + total / 4;
+        if ((rc = sync_locked(ix, s))) return rc;
+        if ((rc = ensure_ws(ix, n, ln))) return rc;
     }
-    memcpy(out_hit, ix->pin_out, (n + 1) * 8);
-    if (out_err && n) memcpy(out_err, ix->pin_out + (n + 1) * 8, n);
+    memcpy(out_hit, ln.pin_out, (n + 1) * 8);
+    if (out_err && n) memcpy(out_err, ln.pin_out + (n + 1) * 8, n);
     const uint64_t keep = std::min(total, out_vals ? cap : 0);
-    if (keep) memcpy(out_vals, ix->pin_vals, keep * 4);
+    if (keep) memcpy(out_vals, ln.pin_vals, keep * 4);
     if (timing) {
         tt[nt++] = now_us();
         fprintf(stderr, "tm_match_batch n=%lu: sync %.1f stage %.1f launch %.1f wait %.1f copy-out %.1f us\n",
@@ -1227,37 +1374,43 @@ int tm_first_batch(tm_index *ix, uint64_t n, const uint8_t *tb, const uint64_t *
     if (!to || !out_value || !out_found || (n && !tb && to[n] != to[0]))
         return fail(ix, TM_EINVAL, "tm_first_batch: null buffer");
     if (n >= 0xFFFFFFFFull) return fail(ix, TM_EINVAL, "tm_first_batch: batch too large");
-    std::lock_guard<std::mutex> g(ix->mu);
+    std::unique_lock<std::mutex> g(ix->mu);
     HIPCHK(ix, hipSetDevice(ix->device));
-    hipStream_t s = ix->stream;
+    LaneLease lease{ix, g};
     int rc;
+    if ((rc = host_lane(ix, g, lease.ln))) return rc;
+    Lane &ln = *lease.ln;
+    const hipStream_t s = ln.s;
     if ((rc = sync_locked(ix, s))) return rc;
-    Workspace *ws;
-    if ((rc = ensure_ws(ix, n, s, ws))) return rc;
+    if ((rc = ensure_ws(ix, n, ln))) return rc;
     if (n && n <= ZC_TOPICS) {   // tm_host_alloc buffers: in place, as tm_match_batch
         const uint64_t nbytes = to[n];
         uint8_t *db = nbytes ? pinned_dev(ix, tb, nbytes) : nullptr;
         uint8_t *dof = pinned_dev(ix, to, (n + 1) * 8);
         uint8_t *dv = pinned_dev(ix, out_value, n * 4), *df = pinned_dev(ix, out_found, n);
         if ((db || !nbytes) && ((uintptr_t)tb & 15) == 0 && dof && dv && df) {
-            HIPCHK(ix, launch_first(dev_view(ix), *ws, n, db ? db : dof, reinterpret_cast<const uint64_t *>(dof),
+            HIPCHK(ix, launch_first(dev_view(ix), ln.w, n, db ? db : dof, reinterpret_cast<const uint64_t *>(dof),
                                     reinterpret_cast<uint32_t *>(dv), df, s));
+            if ((rc = batch_done(ix, ln))) return rc;
+            g.unlock();
             HIPCHK(ix, hipStreamSynchronize(s));
             return TM_OK;
         }
     }
     const uint8_t *dbytes;
     const uint64_t *doffs;
-    if ((rc = stage_in(ix, n, tb, to, s, dbytes, doffs))) return rc;
+    if ((rc = stage_in(ix, ln, n, tb, to, dbytes, doffs))) return rc;
     const uint64_t rbytes = n * 5;   // first value u32 per topic, then the found flags
     uint8_t *dres;
-    if ((rc = stage_out(ix, n, rbytes, s, dres))) return rc;
-    HIPCHK(ix, launch_first(dev_view(ix), *ws, n, dbytes, doffs, reinterpret_cast<uint32_t *>(dres), dres + n * 4, s));
-    if ((rc = fetch_out(ix, n, rbytes, s))) return rc;
+    if ((rc = stage_out(ix, ln, n, rbytes, dres))) return rc;
+    HIPCHK(ix, launch_first(dev_view(ix), ln.w, n, dbytes, doffs, reinterpret_cast<uint32_t *>(dres), dres + n * 4, s));
+    if ((rc = fetch_out(ix, ln, n, rbytes))) return rc;
+    if ((rc = batch_done(ix, ln))) return rc;
+    g.unlock();
     HIPCHK(ix, hipStreamSynchronize(s));
     if (n) {
-        memcpy(out_value, ix->pin_out, n * 4);
-        memcpy(out_found, ix->pin_out + n * 4, n);
+        memcpy(out_value, ln.pin_out, n * 4);
+        memcpy(out_found, ln.pin_out + n * 4, n);
     }
     return TM_OK;
 }

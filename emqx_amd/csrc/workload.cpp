@@ -21,6 +21,8 @@
 //      topics must not hit.  Vocabularies 16/4096/65536/65536/1024/256.
 //      Topics: 2% '$SYS/...', 49% instantiate a filter, 49% random.
 //  C4  = C3 at 100M, sharded by filter index mod N.
+//  C3deep (cfg 30) = C3 filters; C3 topics of which 10% are extended with
+//      random words to 33-64 levels (the deep-topic path).
 //  C5  = C3 base + deltas: even delta k subscribes new filter F + k/2, odd
 //      delta unsubscribes base filter (k/2 * P) mod F (P coprime to F), so
 //      every unsubscribe removes a live key exactly once.
@@ -223,7 +225,7 @@ static void put(Out &o, const std::string &s, uint32_t v, uint8_t f) {
     o.flags.push_back(f);
 }
 
-// cfg: 1, 2 (C2), 20 (C2 non-matching globals), 3 (C3/C4/C5 base).
+// cfg: 1, 2 (C2), 20 (C2 non-matching globals), 3 (C3/C4/C5 base; topics: 30 = C3deep).
 // Filters [lo, hi) of the config's full filter list, keeping index % nshards == shard.
 int tmw_filters(int cfg, uint64_t seed, uint64_t nf, uint64_t shard, uint64_t nshards, tmw_set *out) {
     if (!out || nshards == 0) return -1;
@@ -256,8 +258,16 @@ int tmw_topics(int cfg, uint64_t seed, uint64_t nf, uint64_t first, uint64_t n, 
         std::vector<std::string> w;
         std::string s;
         for (uint64_t j = first + lo; j < first + hi; j++) {
-            if (cfg == 1 || cfg == 3) mixed_topic(cfg == 1 ? C1 : C3, seed, nf, j, s, w);
+            if (cfg == 1 || cfg == 3 || cfg == 30) mixed_topic(cfg == 1 ? C1 : C3, seed, nf, j, s, w);
             else c2_topic(seed, nf, j, s);
+            if (cfg == 30) {   // C3 topics, 10% of them extended to 33-64 levels
+                Rng r(mix64(seed ^ 0x44454550ull ^ (j * 0x9e3779b97f4a7c15ull)));
+                if (r.below(10) == 0) {
+                    const size_t L = 33 + (size_t)r.below(32);
+                    while (w.size() < L) w.push_back(level_word(seed, (int)(w.size() % 6), r.below(256)));
+                    join(w, s);
+                }
+            }
             put(o, s, 0, 0);
         }
     }, parts);

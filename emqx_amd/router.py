@@ -153,12 +153,17 @@ class Router:
             return make_key(topic, dest) in self._filters._records
         return dest in self._bag.get(topic, {})
 
-    def match_routes_batch(self, topics):
-        """match_routes/1 over a batch of publish topics: one device launch."""
+    def match_routes_batch(self, topics, errors: str = "raise"):
+        """match_routes/1 over a batch of publish topics: one device launch.
+        errors="return": a bad topic's slot holds its BadArg instead of
+        failing the batch (topic_index.matches_batch)."""
         topics = [bytes(t) for t in topics]
-        matched = ti.matches_batch(topics, self._filters, ())
+        matched = ti.matches_batch(topics, self._filters, (), errors=errors)
         out = []
         for t, ms in zip(topics, matched):
+            if isinstance(ms, Exception):
+                out.append(ms)
+                continue
             exact, wild = [], []
             for m in ms:
                 (wild if isinstance(m[0], tuple) else exact).append(m)

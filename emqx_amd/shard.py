@@ -4,15 +4,25 @@ Topic-sharded (C1-C3, C5): every rank holds a replica of the index and matches
 its own contiguous slice of the topic stream; no data-path collective.
 
 Filter-sharded (C4, filter sets beyond one GPU): rank r holds the keys whose
-index is r mod N; every rank matches the same topic batch against its shard;
-then the per-shard CSR hit lists are exchanged -- one allgather of the CSR
-offsets (n+1 x u64 per rank) and one allgather of the values, each rank's
-payload padded to the largest (an allgatherv; shards are balanced, so the
-padding is a few percent) -- over RCCL/xGMI on GPUs (gloo on CPU), and merged
-on the device by ``tm_merge_shards``: per topic, shard 0's values, then shard
-1's, ...  Shards hold disjoint keys, so the merged list is the union: the same
-value set as one index holding every key (the parity criterion of
-BASELINE.json: "same filter-ID set per topic").
+index is r mod N, and every rank matches the same topic batch against its
+shard.  Topic slice q of the batch (topics [q s, (q+1) s), s = ceil(n / N))
+belongs to rank q -- the publisher that handed those topics in -- so each
+rank needs, for its own slice only, the hit lists of every shard:
+
+  1. counts: all_to_all of per-topic hit counts (s x u32 per peer),
+  2. values: all_to_all of each slice's values, padded to a per-peer capacity
+     taken from the high-water mark of earlier batches (no host read of the
+     sizes on the data path: an on-device running maximum says afterwards
+     whether any slice overflowed the capacity, and the caller re-runs such a
+     batch with a larger one),
+  3. merge: per topic of the slice, shard 0's values, then shard 1's, ...
+     (``tm_merge_shards`` on the device).
+
+Over RCCL/xGMI on GPUs, gloo on CPU (tests).  Shards hold disjoint keys, so
+the merged list is the union: the same value set as one index holding every
+key (the parity criterion of BASELINE.json: "same filter-ID set per topic").
+Every rank receives only its slice, so each value crosses xGMI once, not N-1
+times as with an allgather of whole lists.
 """
 from __future__ import annotations
 
@@ -25,45 +35,128 @@ def topic_slice(rank: int, world: int, batch: int) -> tuple[int, int]:
     return rank * batch, batch
 
 
-def exchange(hit_offs: torch.Tensor, vals: torch.Tensor, group=None):
-    """The collective half of the filter-sharded exchange.
-
-    hit_offs: int64 [n+1] (this rank's CSR offsets, hit_offs[0] == 0),
-    vals: int32 [>= hit_offs[n]].  Returns (all_offs int64 [world, n+1],
-    all_vals int32 [world, stride], stride) identical on every rank.
-    """
-    world = dist.get_world_size(group)
-    n1 = hit_offs.numel()
-    dev = hit_offs.device
-    all_offs = torch.empty(world * n1, dtype=torch.int64, device=dev)
-    dist.all_gather_into_tensor(all_offs, hit_offs.contiguous(), group=group)
-    all_offs = all_offs.view(world, n1)
-    stride = max(int(all_offs[:, -1].max().item()), 1)
-    total = int(hit_offs[-1].item())
-    if vals.numel() >= stride:
-        send = vals[:stride].contiguous()
-    else:
-        send = torch.zeros(stride, dtype=torch.int32, device=dev)
-        send[:total] = vals[:total]
-    all_vals = torch.empty(world * stride, dtype=torch.int32, device=dev)
-    dist.all_gather_into_tensor(all_vals, send, group=group)
-    return all_offs, all_vals.view(world, stride), stride
+def slice_bounds(n: int, world: int) -> tuple[int, list[tuple[int, int]]]:
+    """Filter-sharded mode: the slice length s and [lo, hi) of each rank's topic slice."""
+    s = (n + world - 1) // world if n else 0
+    return s, [(min(q * s, n), min((q + 1) * s, n)) for q in range(world)]
 
 
-def merge(all_offs: torch.Tensor, all_vals: torch.Tensor, stride: int, stream: int | None = None):
-    """The device half: tm_merge_shards on the gathered buffers (GPU only)."""
+def pack_slices(hit: torch.Tensor, vals: torch.Tensor, world: int, per_peer: int):
+    """Send side of the exchange (device ops only, no host read).
+
+    hit: int64 [n+1] CSR offsets (hit[0] == 0), vals: int32 [>= hit[n]].
+    -> (counts int32 [world, s], values int32 [world, per_peer], largest
+    slice value count as a 0-d int64 tensor)."""
+    n = hit.numel() - 1
+    s, _ = slice_bounds(n, world)
+    dev = hit.device
+    counts = torch.zeros(world * s, dtype=torch.int32, device=dev)
+    counts[:n] = (hit[1:] - hit[:-1]).to(torch.int32)
+    edges = torch.clamp(torch.arange(world + 1, device=dev, dtype=torch.int64) * s, max=n)
+    bounds = hit[edges]                                    # slice q = vals[bounds[q] : bounds[q+1]]
+    lens = bounds[1:] - bounds[:-1]
+    idx = bounds[:-1, None] + torch.arange(per_peer, device=dev, dtype=torch.int64)[None, :]
+    ok = idx < bounds[1:, None]
+    src = vals[torch.clamp(idx, max=max(vals.numel() - 1, 0))] if vals.numel() else torch.zeros_like(idx, dtype=torch.int32)
+    packed = torch.where(ok, src, torch.zeros((), dtype=torch.int32, device=dev))
+    return counts.view(world, s), packed, lens.max()
+
+
+def exchange_slices(counts: torch.Tensor, packed: torch.Tensor, group=None):
+    """The collective half: all_to_all of counts and padded values.
+    -> (recv_counts int32 [world, s]: shard q's counts for this rank's slice,
+        recv_vals int32 [world, per_peer]: shard q's values for it)."""
+    rc = torch.empty_like(counts)
+    rv = torch.empty_like(packed)
+    dist.all_to_all_single(rc.view(-1), counts.contiguous().view(-1), group=group)
+    dist.all_to_all_single(rv.view(-1), packed.contiguous().view(-1), group=group)
+    return rc, rv
+
+
+def shard_offsets(recv_counts: torch.Tensor) -> torch.Tensor:
+    """[world, s] counts -> [world, s+1] per-shard CSR offsets (device scan)."""
+    w, s = recv_counts.shape
+    offs = torch.zeros(w, s + 1, dtype=torch.int64, device=recv_counts.device)
+    torch.cumsum(recv_counts.to(torch.int64), dim=1, out=offs[:, 1:])
+    return offs
+
+
+def merge(all_offs: torch.Tensor, all_vals: torch.Tensor, stride: int, cap: int | None = None,
+          stream: int | None = None):
+    """The device half: tm_merge_shards on the gathered buffers (GPU only).
+    cap defaults to every value the shards could hold (no host read)."""
     from . import _native
     world, n1 = all_offs.shape
     n = n1 - 1
     out_hit = torch.empty(n1, dtype=torch.int64, device=all_offs.device)
-    total = int(all_offs[:, -1].sum().item())
-    out_vals = torch.empty(max(total, 1), dtype=torch.int32, device=all_offs.device)
+    if cap is None:
+        cap = world * stride
+    out_vals = torch.empty(max(cap, 1), dtype=torch.int32, device=all_offs.device)
     _native.merge_shards(world, n, all_offs.data_ptr(), all_vals.data_ptr(), stride, out_hit.data_ptr(),
-                         out_vals.data_ptr(), total, stream)
-    return out_hit, out_vals[:total]
+                         out_vals.data_ptr(), cap, stream)
+    return out_hit, out_vals
 
 
-def allgatherv_hits(hit_offs: torch.Tensor, vals: torch.Tensor, group=None, stream: int | None = None):
-    """Exchange one rank's CSR hit lists with every rank and merge them on the device."""
-    all_offs, all_vals, stride = exchange(hit_offs, vals, group)
-    return merge(all_offs, all_vals, stride, stream)
+def merge_local(hit: torch.Tensor, vals: torch.Tensor, stream: int | None = None):
+    """One shard (world 1): the exchange is the identity, the merge still runs."""
+    return merge(hit.view(1, -1), vals.view(1, -1), vals.numel(), vals.numel(), stream)
+
+
+class Exchange:
+    """Filter-sharded exchange of one rank for batches of n topics.
+
+    ``run(hit, vals)`` packs this shard's lists by destination slice, swaps
+    them with every rank and merges this rank's slice on the device; the
+    per-peer value capacity starts at ``per_peer`` (or is sized by the first
+    batch) and ``check()`` -- one host read, off the data path -- reports
+    whether any batch since the last check overflowed it and grows it."""
+
+    def __init__(self, n: int, device, per_peer: int = 0, group=None, headroom: float = 1.25):
+        self.n = n
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.s, self.bounds = slice_bounds(n, self.world)
+        self.per_peer = per_peer
+        self.headroom = headroom
+        self.peak = torch.zeros((), dtype=torch.int64, device=device)
+
+    def size_from(self, hit: torch.Tensor):
+        """Size the capacity from one batch's offsets (one host read; setup only)."""
+        edges = torch.clamp(torch.arange(self.world + 1, device=hit.device, dtype=torch.int64) * self.s, max=self.n)
+        b = hit[edges]
+        m = (b[1:] - b[:-1]).max().view(1)
+        if self.world > 1:
+            dist.all_reduce(m, op=dist.ReduceOp.MAX, group=self.group)
+        self.per_peer = max(int(int(m.item()) * self.headroom), self.per_peer, 1)
+
+    def swap(self, hit: torch.Tensor, vals: torch.Tensor):
+        """Pack + all_to_all (any device): -> (per-shard offsets int64 [world,
+        s+1] and values int32 [world, per_peer] of this rank's slice)."""
+        if self.per_peer <= 0:
+            self.size_from(hit)
+        counts, packed, mx = pack_slices(hit, vals, self.world, self.per_peer)
+        torch.maximum(self.peak, mx, out=self.peak)
+        rc, rv = exchange_slices(counts, packed, self.group)
+        return shard_offsets(rc), rv
+
+    def run(self, hit: torch.Tensor, vals: torch.Tensor, stream: int | None = None):
+        """swap + the device merge of this rank's slice: -> (offsets int64
+        [slice + 1], values int32) of topics [lo, hi) of the batch."""
+        offs, rv = self.swap(hit, vals)
+        lo, hi = self.bounds[self.rank]
+        out_hit, out_vals = merge(offs, rv, self.per_peer, self.world * self.per_peer, stream)
+        return out_hit[: hi - lo + 1], out_vals
+
+    def check(self) -> bool:
+        """True if every batch since the last check fitted; otherwise grow the
+        capacity (the caller re-runs the batches it has not consumed)."""
+        m = self.peak.view(1).clone()
+        if self.world > 1:
+            dist.all_reduce(m, op=dist.ReduceOp.MAX, group=self.group)
+        peak = int(m.item())
+        ok = peak <= self.per_peer
+        if not ok:
+            self.per_peer = int(peak * self.headroom) + 1
+        self.peak.zero_()
+        return ok

@@ -153,33 +153,62 @@ class TopicTooDeep(ValueError):
     scratch ends there (include/tmatch.h, err flag 2)."""
 
 
-def _check_topic(topic):
-    topic_words(topic)          # raises BadArg like the reference
-    return bytes(topic)
+def matches_batch(topics, tab: Tab, opts=(), errors: str = "raise"):
+    """matches/3 over a batch of topics (one device launch).
 
-
-def matches_batch(topics, tab: Tab, opts=()):
-    """matches/3 over a batch of topics (one device launch); BadArg if any topic is bad."""
-    topics = [_check_topic(t) for t in topics]
+    A topic with a '+'/'#' level is badarg (emqx_trie_search.erl:374-375) and
+    one of more than 65536 levels is TopicTooDeep; the device flags each topic
+    on its own.  errors="raise" raises for the first such topic (one call, one
+    topic: the reference's behaviour); errors="return" puts the exception in
+    that topic's slot and still returns every other topic's matches -- a
+    micro-batch of many publishers fails only the bad publish, as each
+    publishing process does in the reference."""
+    topics = [bytes(t) for t in topics]
     kids, err = tab.match_kids(topics)
     out = []
     for i, ks in enumerate(kids):
-        if err[i] == 2:
-            raise TopicTooDeep(len(topics[i]))
         if err[i]:
-            raise BadArg(topics[i])
+            e = TopicTooDeep(len(topics[i])) if err[i] == 2 else BadArg(topics[i])
+            if errors == "raise":
+                raise e
+            out.append(e)
+            continue
         keys = [tab._keys[k] for k in ks.tolist()]
         out.append(_finish(keys, opts))
     return out
 
 
+def traversal_order(keys):
+    """Device order -> the reference's traversal order.  The device emits keys
+    in ascending Erlang term order of their filters, but the keys of ONE
+    filter (several IDs on one filter: $share groups, many subscribers of a
+    rule topic) come in the order of their u32 values, which Tab hands out by
+    insertion (and reuses).  The reference orders them by {ID}
+    (emqx_trie_search.erl:107-111: {Filter, {ID}} in an ordered_set), so each
+    run of equal filters is sorted by the ID's term order."""
+    out = []
+    i, n = 0, len(keys)
+    while i < n:
+        j = i + 1
+        f = keys[i][0]
+        while j < n and keys[j][0] == f:
+            j += 1
+        if j - i > 1:
+            out.extend(sorted(keys[i:j], key=lambda k: term_key(k[1][0])))
+        else:
+            out.append(keys[i])
+        i = j
+    return out
+
+
 def _finish(keys, opts):
+    keys = traversal_order(keys)
     if "unique" in opts:
         by_id = {}
-        for k in keys:                             # traversal order (device); later keys win
+        for k in keys:                             # traversal order; later keys win
             by_id[get_id(k)] = k
         return [by_id[i] for i in sorted(by_id, key=term_key)]
-    return keys[::-1]          # the device emits traversal order; matches/3 is its reverse
+    return keys[::-1]          # matches/3 is the reverse of the traversal order (match_add/2 prepends)
 
 
 def matches(topic, tab: Tab, opts=()):

@@ -74,13 +74,13 @@ def _take(s: _Set) -> ItemSet:
 
 
 def config_seed(cfg: int) -> int:
-    return SEED_BASE + {1: 0, 2: 1, 20: 1, 3: 2, 4: 3, 5: 4}[cfg]
+    return SEED_BASE + {1: 0, 2: 1, 20: 1, 3: 2, 30: 2, 4: 3, 5: 4}[cfg]
 
 
 def filters(cfg: int, n: int, seed: int | None = None, shard: int = 0, nshards: int = 1) -> ItemSet:
-    """cfg 1, 2, 20 (C2 with non-matching globals) or 3 (also the C4/C5 base)."""
+    """cfg 1, 2, 20 (C2 with non-matching globals) or 3 (also the C3deep/C4/C5 base)."""
     s = _Set()
-    gen_cfg = 3 if cfg in (4, 5) else cfg
+    gen_cfg = 3 if cfg in (4, 5, 30) else cfg
     rc = _load().tmw_filters(gen_cfg, config_seed(cfg) if seed is None else seed, n, shard, nshards, C.byref(s))
     if rc:
         raise ValueError("tmw_filters failed")

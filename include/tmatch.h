@@ -106,7 +106,15 @@ int tm_sync(tm_index *h, void *stream);
 
 /* Host buffers in, host buffers out (pinned staging inside).  Blocks until the
  * hit lists are in host memory.  out_hit_offsets has n+1 entries;
- * out_err has n entries (may be NULL). */
+ * out_err has n entries (may be NULL).
+ * Thread safety: any number of threads may call tm_match_batch,
+ * tm_first_batch and tm_apply_deltas on one index at once (the reference's
+ * readers run concurrently on a read_concurrency ETS table,
+ * emqx_topic_index.erl:41-48).  Each host-API batch runs on its own stream
+ * with its own scratch (up to 16 in flight; more callers wait for one), and
+ * the index lock is held only while pending deltas are shipped and the
+ * kernels are queued, never while waiting for the GPU.  A batch sees every
+ * delta applied before it was queued. */
 int tm_match_batch(tm_index *h, uint64_t n, const uint8_t *topic_bytes, const uint64_t *topic_offsets,
                    uint64_t *out_hit_offsets, uint32_t *out_values, uint64_t cap, uint8_t *out_err);
 
@@ -124,10 +132,16 @@ int tm_host_free(tm_index *h, void *p);
 /* Device-resident batch: every pointer is device memory; asynchronous on
  * `stream` (hipStream_t; NULL = the index's own stream).  d_out_hit_offsets has
  * n+1 entries and d_out_hit_offsets[n] is the total; values beyond `cap` are
- * dropped (the caller compares the total with cap after synchronising). */
+ * dropped (the caller compares the total with cap after synchronising).
+ * The library keeps batch scratch for the 16 most recently used streams (an
+ * older stream's is released after its batches finish). */
 int tm_match_batch_dev(tm_index *h, uint64_t n, const uint8_t *d_topic_bytes, const uint64_t *d_topic_offsets,
                        uint64_t *d_out_hit_offsets, uint32_t *d_out_values, uint64_t cap,
                        uint8_t *d_out_err, void *stream);
+
+/* Release the batch scratch kept for `stream` (after its batches finish);
+ * a caller that retires a stream calls this.  No reference counterpart. */
+int tm_stream_release(tm_index *h, void *stream);
 
 /* match/2: first hit per topic in traversal order.  out_found[i] = 1 and
  * out_value[i] = value if topic i has a match, 0 otherwise (2 = badarg,
@@ -155,7 +169,7 @@ int tm_merge_shards(uint32_t world, uint64_t n, const uint64_t *d_shard_hit_offs
 int tm_profile_enable(tm_index *h, int enable);
 int tm_profile_read(tm_index *h, double *walk_ms, double *batch_ms, uint64_t *batches, int reset);
 
-/* Last error text for a handle (or the global one when h is NULL). */
+/* Last error text of the calling thread (h is ignored; kept for the ABI). */
 const char *tm_last_error(tm_index *h);
 
 /* ABI version: (major << 16) | minor. */

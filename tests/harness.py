@@ -88,3 +88,53 @@ def run_checks(case, traversal_fn):
             assert len(keys) == chk["expect"], (case["name"], t, keys)
         else:
             raise AssertionError(kind)
+
+
+class RouterModel:
+    """The route tables of emqx_router's v2 schema restated for tests
+    (emqx_router.erl:483-516): wildcard routes are index keys
+    make_key(Topic, Dest); exact routes are rows of a bag in insertion order.
+    expected() answers match_routes/1 with the CPU oracle for the wildcard
+    part -- an independent expectation for the GPU router, syncer and broker."""
+
+    def __init__(self):
+        self.wild = set()
+        self.bag = {}
+
+    def add(self, topic, dest):
+        from emqx_amd.trie_search import filter as tfilter
+        if tfilter(topic) is not False:
+            self.wild.add(make_key(topic, dest))
+        else:
+            row = self.bag.setdefault(topic, [])
+            if dest not in row:
+                row.append(dest)
+
+    def delete(self, topic, dest):
+        from emqx_amd.trie_search import filter as tfilter
+        if tfilter(topic) is not False:
+            self.wild.discard(make_key(topic, dest))
+        elif dest in self.bag.get(topic, []):
+            self.bag[topic].remove(dest)
+            if not self.bag[topic]:
+                del self.bag[topic]
+
+    def expected(self, topics):
+        """-> per topic: [Route] as match_routes/1 returns them, or BadArg."""
+        from pyoracle import Oracle
+        from emqx_amd.router import Route
+        keys = sorted(self.wild, key=key_order)          # values in term order: a filter's IDs ascend
+        o = Oracle()
+        for i, k in enumerate(keys):
+            f, fl = encode_key(k)
+            o.insert(f, i, fl)
+        out = []
+        for t in topics:
+            tr = o.matches(bytes(t))
+            if tr is None:
+                out.append(BadArg(t))
+                continue
+            ws = [keys[v] for v in tr]
+            out.append([Route(t, d) for d in self.bag.get(t, [])] +
+                       [Route(get_topic(k), get_id(k)) for k in reversed(ws)])
+        return out

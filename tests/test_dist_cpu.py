@@ -1,12 +1,13 @@
 """world_size-2 gloo tests of the multi-GPU modes on CPU.
 
-The filter-sharded exchange (allgather of the CSR offsets + allgatherv of the
-values, emqx_amd.shard.exchange) runs exactly as on GPUs, only over gloo; the
-per-shard hit lists come from the CPU oracle here (the test's stand-in for each
-rank's GPU shard) and the device merge (tm_merge_shards) is restated in numpy
-(`_merge_ref`, the kernel's contract; the kernel itself is checked against it in
-tests/test_gpu_parity.py).  The merged result must equal the oracle over the
-unsharded filter set, as per-topic value sets.
+The filter-sharded exchange (emqx_amd.shard.Exchange.swap: all_to_all of the
+per-topic u32 counts and of each topic slice's values, padded to a per-peer
+capacity with an on-device overflow check) runs exactly as on GPUs, only over
+gloo; the per-shard hit lists come from the CPU oracle here (the test's
+stand-in for each rank's GPU shard) and the device merge (tm_merge_shards) is
+restated in numpy (`_merge_ref`, the kernel's contract; the kernel itself is
+checked against it in tests/test_gpu_parity.py).  Each rank's merged slice
+must equal the oracle over the unsharded filter set, as per-topic value sets.
 """
 import os
 import socket
@@ -59,24 +60,31 @@ def _body(rank, world, q):
     from emqx_amd import shard, workload as wl
     from pyoracle import Oracle
     nf = 20_000
+    n = 3_001                       # not a multiple of the world: a short last slice
     fs = wl.filters(3, nf, shard=rank, nshards=world)
-    ts = wl.topics(3, nf, 3_000)
+    ts = wl.topics(3, nf, n)
     o = Oracle()
     o.apply(np.ones(len(fs), np.uint8), fs.blob, fs.offs, fs.vals)
     cnt, _, hit, vals = o.match_batch(ts.blob, ts.offs)
-    all_offs, all_vals, stride = shard.exchange(torch.from_numpy(hit.astype(np.int64)),
-                                                torch.from_numpy(vals.view(np.int32)))
-    assert all_vals.shape == (world, stride)
-    m_offs, m_vals = _merge_ref(all_offs.numpy(), all_vals.numpy())
+    hit_t = torch.from_numpy(hit.astype(np.int64))
+    vals_t = torch.from_numpy(vals.view(np.int32).copy())
+    # a capacity far too small first: the overflow check must catch it and grow
+    xch = shard.Exchange(n, "cpu", per_peer=8)
+    xch.swap(hit_t, vals_t)
+    overflowed = not xch.check()
+    offs, rv = xch.swap(hit_t, vals_t)
+    fitted = xch.check()
+    m_offs, m_vals = _merge_ref(offs.numpy(), rv.numpy())
+    lo, hi = xch.bounds[rank]
     # topic-sharded slices partition the stream
-    first, n = shard.topic_slice(rank, world, 1000)
-    t = torch.tensor([first, n], dtype=torch.int64)
+    first, nn = shard.topic_slice(rank, world, 1000)
+    t = torch.tensor([first, nn], dtype=torch.int64)
     g = [torch.zeros(2, dtype=torch.int64) for _ in range(world)]
     dist.all_gather(g, t)
     # max-over-ranks timing reduction used by bench.py
     el = torch.tensor([0.5 + rank], dtype=torch.float64)
     dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    q.put((rank, m_offs, m_vals, [x.tolist() for x in g], float(el)))
+    q.put((rank, m_offs[: hi - lo + 1], m_vals, [x.tolist() for x in g], float(el), (lo, hi), overflowed, fitted))
 
 
 @pytest.mark.timeout(300)
@@ -100,18 +108,23 @@ def test_filter_sharded_exchange_gloo():
     res.sort(key=lambda x: x[0])
     for r in res:
         assert not (isinstance(r[1], str) and r[1] == "error"), r
-    # every rank ends with the same merged CSR
-    assert np.array_equal(res[0][1], res[1][1]) and np.array_equal(res[0][2], res[1][2])
-    # ... equal to the unsharded oracle, per topic as sorted sets
+    # the slices partition the batch; capacity overflow detected, then fitted
+    n = 3_001
+    assert [r[5] for r in res] == [(0, 1501), (1501, 3001)]
+    assert all(r[6] and r[7] for r in res)
+    # each rank's merged slice == the unsharded oracle, per topic as sorted sets
     nf = 20_000
     fs = wl.filters(3, nf)
-    ts = wl.topics(3, nf, 3_000)
+    ts = wl.topics(3, nf, n)
     o = Oracle()
     o.apply(np.ones(len(fs), np.uint8), fs.blob, fs.offs, fs.vals)
     cnt, _, hit, vals = o.match_batch(ts.blob, ts.offs)
-    m_offs, m_vals = res[0][1], res[0][2].view(np.uint32)
-    assert np.array_equal(m_offs, hit.astype(np.int64))
-    for i in range(len(ts)):
-        assert np.array_equal(np.sort(vals[hit[i]:hit[i + 1]]), np.sort(m_vals[m_offs[i]:m_offs[i + 1]]))
+    for r in res:
+        lo, hi = r[5]
+        m_offs, m_vals = r[1], r[2].view(np.uint32)
+        assert np.array_equal(m_offs, hit[lo:hi + 1].astype(np.int64) - int(hit[lo]))
+        for i in range(lo, hi):
+            assert np.array_equal(np.sort(vals[hit[i]:hit[i + 1]]),
+                                  np.sort(m_vals[m_offs[i - lo]:m_offs[i - lo + 1]]))
     assert res[0][3] == [[0, 1000], [1000, 1000]]
     assert res[0][4] == 1.5

@@ -11,7 +11,7 @@ import pytest
 
 from emqx_amd import _native, router as rt, topic_index as ti, workload as wl
 from emqx_amd.trie_search import BadArg, get_id, get_topic, topic_words
-from harness import GOLDEN, case_keys, encode_key, run_checks
+from harness import GOLDEN, RouterModel, case_keys, encode_key, run_checks
 from pyoracle import Oracle
 
 pytestmark = pytest.mark.gpu
@@ -594,6 +594,7 @@ def test_filter_sharded_merge_vs_oracle(torch_dev, world):
     m_hit, m_vals = shard.merge(torch.from_numpy(all_offs).to(dev), torch.from_numpy(all_vals).to(dev), stride)
     torch.cuda.synchronize()
     m_hit, m_vals = m_hit.cpu().numpy(), m_vals.cpu().numpy()
+    m_vals = m_vals[: int(m_hit[-1])]
     r_hit, r_vals = _merge_ref(all_offs, all_vals)
     assert np.array_equal(m_hit, r_hit) and np.array_equal(m_vals, r_vals)
     fs = wl.filters(3, nf)
@@ -651,29 +652,43 @@ def test_router_cleanup_and_replicated_events(torch_dev):
 
 
 def test_syncer_batches_reach_the_device(torch_dev):
+    """Route ops pushed through the syncer (batches of <= 100, one
+    tm_apply_deltas each) give the routes the reference's tables would hold:
+    match_routes equals the CPU model + oracle (harness.RouterModel)."""
     from emqx_amd import syncer as sy
-    direct, synced = rt.Router(node="n1"), rt.Router(node="n1")
+    synced = rt.Router(node="n1")
+    model = RouterModel()
     s = sy.Syncer(synced, max_batch_size=100)
     refs = []
     for i in range(600):
         t = f"dev/{i % 150}/+/x".encode() if i % 3 else f"dev/{i % 150}/y".encode()
         op = "delete" if i % 7 == 0 else "add"
-        (direct.add_route if op == "add" else direct.delete_route)(t, "n1")
+        (model.add if op == "add" else model.delete)(t, "n1")
         refs.append(s.push(op, t, "n1", {"reply": True}))
     assert s.run_once() > 0 and s.batches >= 2
     assert all(x.wait(0) == "ok" for x in refs)
     topics = [f"dev/{i}/{j}/x".encode() for i in range(150) for j in ("q", "y")] + \
              [f"dev/{i}/y".encode() for i in range(150)]
-    assert direct.match_routes_batch(topics) == synced.match_routes_batch(topics)
+    assert synced.match_routes_batch(topics) == model.expected(topics)
 
 
-def test_broker_micro_batch_equals_per_message_publish(torch_dev):
-    from emqx_amd import broker as bk
+def _broker_fixture(n_filters, n_topics):
     r = rt.Router(node="n1")
-    fs = wl.filters(1, 2_000)
+    model = RouterModel()
+    fs = wl.filters(1, n_filters)
     for i in range(len(fs)):
-        r.add_route(fs.item(i), ["n1", "n2", (b"grp", "n3")][i % 3])
-    ts = wl.topics(1, 2_000, 3_000)
+        d = ["n1", "n2", (b"grp", "n3")][i % 3]
+        r.add_route(fs.item(i), d)
+        model.add(fs.item(i), d)
+    ts = wl.topics(1, n_filters, n_topics)
+    return r, model, ts
+
+
+def test_broker_micro_batch_matches_the_reference_routes(torch_dev):
+    """Publishes micro-batched into few device launches; every message gets
+    aggre/1 of the routes the reference would find (CPU model + oracle)."""
+    from emqx_amd import broker as bk
+    r, model, ts = _broker_fixture(2_000, 3_000)
     msgs = [bk.Message(ts.item(i), i) for i in range(len(ts))]
     b = bk.Broker(r, max_batch=1024, max_wait_ms=50, start=True)
     try:
@@ -682,11 +697,85 @@ def test_broker_micro_batch_equals_per_message_publish(torch_dev):
     finally:
         b.close()
     assert b.batches < len(msgs) / 100       # micro-batched: few device launches
-    single = bk.Broker(r)
-    for m, got in zip(msgs[:300], batched[:300]):
-        routes = bk.aggre(r.match_routes(m.topic))
-        assert got[0] == routes
-        assert got == single.publish_batch([m])[0]
+    exp = model.expected([m.topic for m in msgs])
+    for got, routes in zip(batched, exp):
+        assert got[0] == bk.aggre(routes)
+
+
+def test_broker_badarg_fails_only_its_message(torch_dev):
+    """One 'a/+/b' publish inside a 1k micro-batch: 999 messages routed as the
+    reference would route them, one BadArg (emqx_trie_search.erl:374-375 fails
+    only the publishing process)."""
+    from emqx_amd import broker as bk
+    r, model, ts = _broker_fixture(2_000, 999)
+    msgs = [bk.Message(ts.item(i), i) for i in range(500)] + [bk.Message(b"a/+/b", -1)] + \
+           [bk.Message(ts.item(i), i) for i in range(500, 999)]
+    b = bk.Broker(r, max_batch=1000, max_wait_ms=1000)
+    futs = [b.publish(m) for m in msgs]
+    b.flush()
+    assert b.batches == 1
+    exp = model.expected([m.topic for m in msgs])
+    bad = [i for i, f in enumerate(futs) if f.exception(0) is not None]
+    assert bad == [500] and isinstance(futs[500].exception(0), BadArg)
+    for i, f in enumerate(futs):
+        if i != 500:
+            assert f.result(0)[0] == bk.aggre(exp[i])
+
+
+def test_ids_of_one_filter_follow_term_order(torch_dev):
+    """Several IDs on one filter come back in the ID's term order whatever
+    order they were inserted in and whichever u32 kid they got (freed kids are
+    reused): match/2 is the smallest key, matches/3 the reverse traversal."""
+    tab = ti.new()
+    ti.insert(b"a/+", 2, None, tab)
+    ti.insert(b"a/+", 1, None, tab)
+    ti.insert(b"a/+", "node", None, tab)
+    ti.insert(b"a/#", 7, None, tab)
+    assert ti.match(b"a/b", tab) == ti.make_key(b"a/#", 7)
+    assert [get_id(k) for k in ti.matches(b"a/b", tab)] == ["node", 2, 1, 7]
+    ti.delete(b"a/#", 7, tab)
+    assert ti.match(b"a/b", tab) == ti.make_key(b"a/+", 1)
+    ti.delete(b"a/+", 2, tab)                  # its kid is freed ...
+    ti.insert(b"a/+", 0, None, tab)            # ... and reused by a smaller ID
+    assert ti.match(b"a/b", tab) == ti.make_key(b"a/+", 0)
+    assert [get_id(k) for k in ti.matches(b"a/b", tab)] == ["node", 1, 0]
+    assert [get_id(k) for k in ti.matches(b"a/b", tab, ["unique"])] == [0, 1, "node"]
+
+
+def test_c2_full_size_sample_vs_oracle(torch_dev):
+    """C2 at full size (1M 'fleet/{id}/sensor/+' + 1k globals, one 1M-topic
+    batch, ~1e9 values on the device): offsets of every topic and the values
+    of a 20k-topic sample equal the oracle's (traversal order)."""
+    import torch
+    nf = 1_000_000
+    fs = wl.filters(2, nf)
+    ts = wl.topics(2, nf, 1_000_000)
+    ix = gpu_index(fs)
+    dev = torch.device("cuda:0")
+    n = len(ts)
+    blob = torch.from_numpy(ts.blob).to(dev)
+    offs = torch.from_numpy(ts.offs.view(np.int64)).to(dev)
+    hit = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    err = torch.zeros(n, dtype=torch.uint8, device=dev)
+    s = torch.cuda.current_stream().cuda_stream
+    ix.match_batch_dev(n, blob.data_ptr(), offs.data_ptr(), hit.data_ptr(), 0, 0, err.data_ptr(), s)
+    torch.cuda.synchronize()
+    total = int(hit[-1])
+    out = torch.zeros(total, dtype=torch.int32, device=dev)
+    ix.match_batch_dev(n, blob.data_ptr(), offs.data_ptr(), hit.data_ptr(), out.data_ptr(), total, err.data_ptr(), s)
+    torch.cuda.synchronize()
+    assert not bool(err.any())
+    h = hit.cpu().numpy()
+    per = np.diff(h)
+    assert per.min() >= 1000 and per.max() == 1001
+    idx = np.sort(np.random.default_rng(11).choice(n, 20_000, replace=False))
+    sample = items_of([ts.item(int(i)) for i in idx])
+    o = oracle_of(fs)
+    _, _, ohit, ovals = o.match_batch(sample.blob, sample.offs)
+    assert np.array_equal(per[idx], np.diff(ohit.astype(np.int64)))
+    rows = torch.from_numpy(np.concatenate([np.arange(h[i], h[i + 1]) for i in idx])).to(dev)
+    got = out[rows].cpu().numpy().view(np.uint32)
+    assert np.array_equal(got, ovals)
 
 
 def test_batches_on_two_streams_see_patches_in_order(torch_dev):
@@ -745,3 +834,105 @@ def test_topic_index_matches_filter(torch_dev):
         assert uniq == sorted(set(got)), q
     t = b"foo/bar/1"
     assert sorted(get_id(k) for k in ti.matches(t, tab, [])) == sorted(o.matches(t))
+
+
+# ------------------------------------------------------ concurrent callers
+
+def test_concurrent_callers_see_consistent_snapshots(torch_dev):
+    """12 host threads submit 4k-topic batches through tm_match_batch at once
+    (half with tm_host_alloc buffers, half pageable) while the main thread
+    applies 16 epochs of subscribe/unsubscribe deltas.  Each epoch is one
+    tm_apply_deltas call that also inserts a marker key 'probe/+' -> 900000+e,
+    so the probe topic of a batch says how many epochs it saw; every batch
+    must equal the oracle after exactly that many epochs, and a thread's
+    batches never go back in time (SURVEY.md 8b Threading: a batch sees a
+    consistent prefix of the deltas)."""
+    import threading
+    import time
+    nf, nthreads, lb, epochs = 10_000, 12, 4096, 16
+    fs = wl.filters(1, nf)
+    ix, o = gpu_index(fs), oracle_of(fs)
+    r = random.Random(0x454D5158 + 77)
+    tsets = []
+    for t in range(nthreads):
+        ts = wl.topics(1, nf, lb, first=t * lb)
+        tsets.append(items_of(ts.items() + [b"probe/x"]))
+    ep_ops = []
+    for e in range(epochs):
+        fl, vals, ops = [b"probe/+"], [900_000 + e], [1]
+        for i in range(60):   # new filters that match some batch topics
+            words = tsets[r.randrange(nthreads)].item(r.randrange(lb)).split(b"/")
+            k = r.randrange(len(words))
+            words[k] = b"+" if r.random() < 0.5 else words[k]
+            fl.append(b"/".join(words[: k + 1]) + (b"/#" if r.random() < 0.3 else b""))
+            vals.append(100_000 + e * 1000 + i)
+            ops.append(1)
+        for _ in range(60):   # unsubscribe base filters
+            i = r.randrange(len(fs))
+            fl.append(fs.item(i))
+            vals.append(int(fs.vals[i]))
+            ops.append(0)
+        ep_ops.append((np.array(ops, np.uint8), items_of(fl, vals)))
+    # the oracle after e epochs, for every thread's topics
+    expected = []
+    for e in range(epochs + 1):
+        if e:
+            ops, d = ep_ops[e - 1]
+            o.apply(ops, d.blob, d.offs, d.vals)
+        o.prepare()
+        expected.append([o.match_batch(ts.blob, ts.offs)[2:] for ts in tsets])
+    results = [[] for _ in range(nthreads)]
+    stop = threading.Event()
+    errors = []
+
+    def caller(t):
+        try:
+            ts = tsets[t]
+            n = len(ts)
+            if t % 2:   # pageable caller buffers
+                bufs = (np.zeros(n + 1, np.uint64), np.zeros(200_000, np.uint32), np.zeros(n, np.uint8))
+                blob, offs = ts.blob, ts.offs
+            else:       # tm_host_alloc buffers: in place
+                nb = int(ts.offs[-1])
+                blob = ix.host_array(nb + 16, np.uint8)
+                blob[:nb] = ts.blob[:nb]
+                offs = ix.host_array(n + 1, np.uint64)
+                offs[:] = ts.offs
+                bufs = (ix.host_array(n + 1, np.uint64), ix.host_array(200_000, np.uint32), ix.host_array(n, np.uint8))
+            while not stop.is_set() or len(results[t]) < 3:
+                t0 = time.perf_counter()
+                hit, vals, err = ix.match_batch(blob, offs, out=bufs)
+                results[t].append((time.perf_counter() - t0, hit.copy(), vals.copy(), err.copy()))
+        except BaseException as e:   # noqa: BLE001 - reported below
+            errors.append(repr(e))
+
+    th = [threading.Thread(target=caller, args=(t,)) for t in range(nthreads)]
+    for x in th:
+        x.start()
+    for ops, d in ep_ops:
+        time.sleep(0.02)
+        ix.apply(ops, d.blob, d.offs, d.vals)
+    time.sleep(0.05)
+    stop.set()
+    for x in th:
+        x.join(timeout=60)
+    assert not errors, errors
+    seen = set()
+    lat = []
+    for t in range(nthreads):
+        last = -1
+        for dt, hit, vals, err in results[t]:
+            lat.append(dt)
+            assert not err.any()
+            probe = vals[int(hit[-2]):int(hit[-1])]
+            e = len(probe)
+            assert sorted(probe.tolist()) == [900_000 + k for k in range(e)], "a batch saw part of an epoch"
+            assert e >= last, "a thread's batches went back in time"
+            last = e
+            seen.add(e)
+            ohit, ovals = expected[e][t]
+            assert np.array_equal(hit, ohit) and np.array_equal(vals, ovals), (t, e)
+    assert len(seen) >= 4, seen          # the batches did interleave with the epochs
+    lat = np.array(lat) * 1e3
+    print(f"concurrent callers: {len(lat)} batches, epochs seen {sorted(seen)}, "
+          f"p50 {np.percentile(lat, 50):.3f} ms p99 {np.percentile(lat, 99):.3f} ms")

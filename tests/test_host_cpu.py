@@ -80,3 +80,42 @@ def test_workload_deltas_remove_live_keys_once():
     base_keys = set(zip(base.items(), base.vals.tolist()))
     for i in np.nonzero(~subs)[0][:50]:
         assert (d.item(i), int(d.vals[i])) in base_keys
+
+
+def test_ids_of_one_filter_in_term_order():
+    """The device orders the values of one filter by u32 kid (insertion order,
+    reused kids); the reference orders the keys {Filter, {ID}} of one filter
+    by the ID's term order (advisor finding, emqx_trie_search.erl:107-111).
+    traversal_order re-sorts each run of equal filters."""
+    from emqx_amd.topic_index import traversal_order
+    a2, a1, a_atom = make_key(b"a/+", 2), make_key(b"a/+", 1), make_key(b"a/+", "node1")
+    h9 = make_key(b"a/#", 9)
+    dev_order = [h9, a_atom, a2, a1, make_key(b"a/b", 5), make_key(b"a/b", 0)]
+    got = traversal_order(dev_order)
+    assert got == sorted(dev_order, key=key_order)
+    assert got == [h9, a1, a2, a_atom, make_key(b"a/b", 0), make_key(b"a/b", 5)]
+    # match/2 = first in traversal order; matches/3 = its reverse
+    assert _finish(dev_order, [])[-1] == h9
+    assert _finish([a2, a1], [])[-1] == a1
+
+
+def test_broker_badarg_fails_only_that_message():
+    """A micro-batch with one '+'-level topic: that message's result is its
+    BadArg, every other message is routed (no GPU: a stub router)."""
+    from emqx_amd import broker as bk
+    from emqx_amd.router import Route
+
+    class StubRouter:
+        node = "n1"
+
+        def match_routes_batch(self, topics, errors="raise"):
+            assert errors == "return"
+            return [BadArg(t) if b"+" in t.split(b"/") else [Route(t, "n1")] for t in topics]
+
+    b = bk.Broker(StubRouter())
+    msgs = [bk.Message(b"a/%d" % i, i) for i in range(10)] + [bk.Message(b"a/+/b", 99)]
+    futs = [b.publish(m) for m in msgs]
+    b.flush()
+    for f in futs[:10]:
+        assert f.result(0)[0] == [(f.result(0)[0][0][0], "n1")]
+    assert isinstance(futs[10].exception(0), BadArg)

@@ -157,7 +157,7 @@ class _StubMatchRouter:
     def __init__(self):
         self.calls = []
 
-    def match_routes_batch(self, topics):
+    def match_routes_batch(self, topics, errors="raise"):
         self.calls.append(len(topics))
         return [[Route(t, "n1"), Route(b"#", "n2"), Route(b"+/x", (b"g", "n3"))] for t in topics]
 
@@ -199,7 +199,7 @@ def test_broker_micro_batches_by_size_and_time():
 
 def test_broker_error_reaches_callers():
     class Bad(_StubMatchRouter):
-        def match_routes_batch(self, topics):
+        def match_routes_batch(self, topics, errors="raise"):
             raise ValueError("badarg")
     b = bk.Broker(Bad(), max_batch=2)
     f1, f2 = b.publish(bk.Message(b"a", 0)), b.publish(bk.Message(b"b", 0))

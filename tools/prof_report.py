@@ -19,7 +19,14 @@ scattered 16-B and 64-B reads FETCH_SIZE counts exactly 64 B per memory-side
 request, so the value is taken as is (no x2).
 It also counts Infinity-Cache (MALL) hits, so it is an upper bound on HBM.
 
-usage: prof_report.py <prof_dir> <round> <tag> <config> <filters> <batch>
+The bench run's kernel trace is split by phase: its last 2 x rotate
+full-grid k_walk_fast launches are the isolated pass bench.py times for
+roofline.kernel_avg_ms (one stream, back to back), the launches before them
+ran overlapped on three streams.  pmc_<config>.json is stamped with the
+kernel-source hash (emqx_amd.build.source_hash) and the workload shape;
+bench.py refuses it for any other tree or shape.
+
+usage: prof_report.py <prof_dir> <round> <tag> <config> <filters> <batch> [rotate] [batches]
 """
 import csv
 import json
@@ -48,8 +55,11 @@ def trace_table(path):
     return out, agg
 
 
-def pmc_values(prof, grid):
-    vals = defaultdict(lambda: defaultdict(list))
+def pmc_values(prof, grid, last):
+    """mean counter value per launch over the LAST `last` launches of each
+    kernel at this grid (the profiling driver's timed launches; its sizing
+    launches, which write no values, come first)"""
+    vals = defaultdict(lambda: defaultdict(dict))
     for d in sorted(os.listdir(prof)):
         p = os.path.join(prof, d, "run_counter_collection.csv")
         if not (d.startswith("pmc") and os.path.isfile(p)):
@@ -57,12 +67,31 @@ def pmc_values(prof, grid):
         for r in csv.DictReader(open(p)):
             if int(r["Grid_Size"]) != grid or "tmx::" not in r["Kernel_Name"]:
                 continue
-            vals[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
-    return {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in vals.items()}
+            k, c, disp = short(r["Kernel_Name"]), r["Counter_Name"], int(r["Dispatch_Id"])
+            vals[k][c][disp] = vals[k][c].get(disp, 0.0) + float(r["Counter_Value"])
+    out = {}
+    for k, cs in vals.items():
+        out[k] = {}
+        for c, per in cs.items():
+            v = [per[d] for d in sorted(per)[-last:]]
+            out[k][c] = sum(v) / len(v)
+    return out
 
 
-def main(prof, rnd, tag, config, filters, batch):
-    filters, batch = int(filters), int(batch)
+def split_phases(path, grid, n_iso):
+    """k_walk_fast full-grid launches of the bench run in time order -> (timed
+    region + warmup, isolated pass) durations in ns"""
+    rows = [r for r in csv.DictReader(open(path)) if "k_walk_fast" in r["Kernel_Name"]
+            and int(r.get("Grid_Size_X") or r.get("Grid_Size") or 0) == grid]
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    d = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows]
+    return d[:-n_iso], d[-n_iso:]
+
+
+def main(prof, rnd, tag, config, filters, batch, rotate=4, batches=8):
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+    from emqx_amd.build import source_hash
+    filters, batch, rotate, batches = int(filters), int(batch), int(rotate), int(batches)
     grid = (batch + 255) // 256 * 256
     lines = [f"# Profile {rnd}/{tag}: config {config}, {filters} filters, {batch}-topic batches", ""]
     bench_json = os.path.join(prof, "bench.json")
@@ -77,6 +106,14 @@ def main(prof, rnd, tag, config, filters, batch):
             continue
         tab, agg = trace_table(p)
         lines += [f"## Kernel trace: {title}", ""] + tab + [""]
+        if sub == "bench":
+            timed, iso = split_phases(p, grid, 2 * rotate)
+            if iso:
+                lines += [f"k_walk_fast (grid {grid}) by phase of the bench run: the last {len(iso)} launches "
+                          f"(bench.py's isolated pass, one stream, back to back) avg {sum(iso) / len(iso) / 1e3:.2f} us "
+                          f"(min {min(iso) / 1e3:.2f}, max {max(iso) / 1e3:.2f}); the {len(timed)} before them "
+                          f"(sizing, warmup, timed steps on three streams) avg {sum(timed) / max(len(timed), 1) / 1e3:.2f} us.",
+                          ""]
         if sub == "trace":   # the driver the PMC passes ran: kernels alone on one stream
             for (name, g), d in agg.items():
                 if g == grid:
@@ -84,9 +121,10 @@ def main(prof, rnd, tag, config, filters, batch):
         st = os.path.join(prof, sub, "run_kernel_stats.csv")
         if os.path.isfile(st):
             shutil.copy(st, os.path.join("profiles", f"{rnd}_{tag}_{sub}_kernel_stats.csv"))
-    pm = pmc_values(prof, grid)
+    pm = pmc_values(prof, grid, batches)
     walk = [k for k in pm if "k_walk_fast" in k]
-    res = {"config": config, "filters": filters, "batch": batch, "grid": grid}
+    res = {"config": config, "filters": filters, "batch": batch, "rotate": rotate, "grid": grid,
+           "source_hash": source_hash()}
     if pm:
         lines += [f"## PMC counters per launch (grid {grid}, mean over launches; one rocprofv3 --pmc pass per group)", ""]
         names = sorted({c for k in pm for c in pm[k]})

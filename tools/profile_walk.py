@@ -17,7 +17,8 @@ def main():
     p.add_argument("--config", default="c3")
     p.add_argument("--filters", type=int, default=None)
     p.add_argument("--batch", type=int, default=1_000_000)
-    p.add_argument("--batches", type=int, default=5)
+    p.add_argument("--batches", type=int, default=8)
+    p.add_argument("--rotate", type=int, default=4, help="distinct batches the launches cycle over (as bench.py)")
     p.add_argument("--order", default="stream", choices=["stream", "sorted", "bucket"],
                    help="topic order in the batch: generator stream, byte-sorted, or bucketed "
                         "by the hash of the first two levels (locality study)")
@@ -41,37 +42,47 @@ def main():
     for lo in range(0, len(fs), 2_000_000):
         part = fs.slice(lo, min(lo + 2_000_000, len(fs)))
         ix.apply(np.ones(len(part), np.uint8), part.blob, part.offs, part.vals)
-    ts = wl.topics(gen, nf, a.batch)
-    if a.order != "stream":
-        items = ts.items()
-        if a.order == "sorted":
-            items = sorted(items)
-        else:
-            items = sorted(items, key=lambda t: hash(b"/".join(t.split(b"/")[:2])) & 0xFFFF)
-        blob, offs = _native.pack_strings(items)
-        ts = wl.ItemSet(blob, offs, np.zeros(len(items), np.uint32), np.zeros(len(items), np.uint8))
     dev = torch.device("cuda:0")
-    d_blob = torch.from_numpy(ts.blob).to(dev)
-    d_offs = torch.from_numpy(ts.offs.view(np.int64)).to(dev)
+    R = max(1, a.rotate)
+    d_in = []
+    for k in range(R):
+        ts = wl.topics(gen, nf, a.batch, first=k * a.batch)
+        if a.order != "stream":
+            items = ts.items()
+            if a.order == "sorted":
+                items = sorted(items)
+            else:
+                items = sorted(items, key=lambda t: hash(b"/".join(t.split(b"/")[:2])) & 0xFFFF)
+            blob, offs = _native.pack_strings(items)
+            ts = wl.ItemSet(blob, offs, np.zeros(len(items), np.uint32), np.zeros(len(items), np.uint8))
+        d_in.append((torch.from_numpy(ts.blob).to(dev), torch.from_numpy(ts.offs.view(np.int64)).to(dev)))
     d_hit = torch.zeros(a.batch + 1, dtype=torch.int64, device=dev)
     d_err = torch.zeros(a.batch, dtype=torch.uint8, device=dev)
     s = torch.cuda.current_stream().cuda_stream
-    ix.match_batch_dev(a.batch, d_blob.data_ptr(), d_offs.data_ptr(), d_hit.data_ptr(), 0, 0, d_err.data_ptr(), s)
-    torch.cuda.synchronize()
-    tot = int(d_hit[-1])
+    tot = 0
+    for d_blob, d_offs in d_in:
+        ix.match_batch_dev(a.batch, d_blob.data_ptr(), d_offs.data_ptr(), d_hit.data_ptr(), 0, 0, d_err.data_ptr(), s)
+        torch.cuda.synchronize()
+        tot = max(tot, int(d_hit[-1]))
     d_out = torch.zeros(max(tot, 1), dtype=torch.int32, device=dev)
-    ix.profile(True)
-    t = time.perf_counter()
-    for _ in range(a.batches):
+
+    def launch(k):
+        d_blob, d_offs = d_in[k % R]
         ix.match_batch_dev(a.batch, d_blob.data_ptr(), d_offs.data_ptr(), d_hit.data_ptr(), d_out.data_ptr(), tot,
                            d_err.data_ptr(), s)
+
+    launch(0)   # unprofiled: the profiled launches are enqueued behind a busy stream
+    ix.profile(True)
+    t = time.perf_counter()
+    for k in range(a.batches):
+        launch(k)
     torch.cuda.synchronize()
     el = time.perf_counter() - t
     w, b, n = ix.profile_read()
     st = ix.stats()
-    print(f"{a.config}/{a.order}/filters-{a.filter_order} filters={len(fs)} batch={a.batch} hits={tot} wall/batch={el / a.batches * 1e3:.3f}ms "
-          f"walk={w / n:.4f}ms batch_dev={b / n:.4f}ms rate={a.batch * a.batches / el / 1e9:.3f}G/s "
-          f"device_MiB={st['device_bytes'] / 2**20:.0f}", flush=True)
+    print(f"{a.config}/{a.order}/filters-{a.filter_order} filters={len(fs)} batch={a.batch} rotate={R} hits<={tot} "
+          f"wall/batch={el / a.batches * 1e3:.3f}ms walk={w / n:.4f}ms batch_dev={b / n:.4f}ms "
+          f"rate={a.batch * a.batches / el / 1e9:.3f}G/s device_MiB={st['device_bytes'] / 2**20:.0f}", flush=True)
 
 
 if __name__ == "__main__":
