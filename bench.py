@@ -246,7 +246,9 @@ def main():
     # the last 2 R full-grid k_walk_fast launches of the run
     # (tools/prof_report.py splits them out).
     iso_passes = 2
-    spare = outs[0]
+    spare = {"hit": torch.zeros(B + 1, dtype=torch.int64, device=dev),
+             "err": torch.zeros(B, dtype=torch.uint8, device=dev),
+             "out": torch.zeros(max(cap, 1), dtype=torch.int32, device=dev)}   # the timed steps' outputs stay intact
 
     def iso_launch(d_blob, d_offs):
         ix.match_batch_dev(B, d_blob.data_ptr(), d_offs.data_ptr(), spare["hit"].data_ptr(),
@@ -499,7 +501,7 @@ def main():
         dist.destroy_process_group()
 
 
-def concurrent_latency(ix, ts, nthreads: int, lb: int, seconds: float = 1.5):
+def concurrent_latency(ix, ts, nthreads: int, lb: int, seconds: float = 1.0):
     """Concurrent callers (SURVEY.md 8b Threading: every client process calls
     matches/3 at once): `nthreads` host threads each submit lb-topic batches
     through tm_match_batch with their own tm_host_alloc buffers while one more

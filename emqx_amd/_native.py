@@ -17,12 +17,13 @@ from .build import LIB_TMATCH
 TM_OK, TM_EINVAL, TM_ENOMEM, TM_EDEVICE, TM_ECAP = 0, -1, -2, -3, -4
 TM_OP_DELETE, TM_OP_INSERT = 0, 1
 TM_KEY_BINARY, TM_KEY_WORDS, TM_KEY_EMPTY_LIST = 0, 1, 2
+TM_ORDER_TRAVERSAL, TM_ORDER_SORTED, TM_ORDER_UNIQUE = 0, 1, 2
 
 # every symbol include/tmatch.h declares (tests check the export table)
 EXPORTS = ("tm_create", "tm_destroy", "tm_apply_deltas", "tm_sync", "tm_match_batch",
            "tm_match_batch_dev", "tm_first_batch", "tm_stats", "tm_profile_enable", "tm_profile_read",
            "tm_last_error", "tm_abi_version", "tm_merge_shards", "tm_host_alloc", "tm_host_free",
-           "tm_stream_release")
+           "tm_stream_release", "tm_match_batch_ex", "tm_match_batch_dev_ex", "tm_sort_segments")
 
 
 class NativeUnavailable(RuntimeError):
@@ -77,6 +78,9 @@ def load_library(path: Path | None = None):
         "tm_host_alloc": (i32, [vp, u64, C.POINTER(vp)]),
         "tm_host_free": (i32, [vp, vp]),
         "tm_stream_release": (i32, [vp, vp]),
+        "tm_match_batch_ex": (i32, [vp, u64, vp, vp, vp, vp, u64, vp, u32, vp]),
+        "tm_match_batch_dev_ex": (i32, [vp, u64, vp, vp, vp, vp, u64, vp, u32, vp, vp]),
+        "tm_sort_segments": (i32, [vp, u64, vp, vp, u64, u32, vp, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -187,8 +191,12 @@ class Index:
         self._pinned.remove(addr)
 
     # ---- matching (host buffers)
-    def match_batch(self, blob: np.ndarray, offs: np.ndarray, cap: int | None = None, out=None):
-        """-> (hit_offsets u64[n+1], values u32[total], err u8[n]) in traversal order.
+    def match_batch(self, blob: np.ndarray, offs: np.ndarray, cap: int | None = None, out=None,
+                    order: int = TM_ORDER_TRAVERSAL, unique_counts: np.ndarray | None = None):
+        """-> (hit_offsets u64[n+1], values u32[total], err u8[n]), each topic's
+        values in `order` (traversal by default; TM_ORDER_SORTED ascending;
+        TM_ORDER_UNIQUE ascending distinct values first, padded with
+        0xFFFFFFFF, the distinct count per topic in `unique_counts`).
 
         `out` = (hit u64[>= n+1], values u32[cap], err u8[>= n]): caller-owned
         buffers reused across batches (what a NIF keeps per scheduler); the
@@ -196,13 +204,16 @@ class Index:
         n = len(offs) - 1
         blob = np.ascontiguousarray(blob, dtype=np.uint8)
         offs = np.ascontiguousarray(offs, dtype=np.uint64)
+        if unique_counts is not None and (len(unique_counts) < n or unique_counts.dtype != np.uint32):
+            raise ValueError("match_batch: unique_counts too small or not uint32")
+        uc = _ptr(unique_counts)
         if out is not None:
             hit, vals, err = out
             if len(hit) < n + 1 or len(err) < n or hit.dtype != np.uint64 or vals.dtype != np.uint32 \
                     or err.dtype != np.uint8:
                 raise ValueError("match_batch: out buffers too small or of the wrong dtype")
-            rc = self._lib.tm_match_batch(self._h, n, _ptr(blob), _ptr(offs), _ptr(hit), _ptr(vals), len(vals),
-                                          _ptr(err))
+            rc = self._lib.tm_match_batch_ex(self._h, n, _ptr(blob), _ptr(offs), _ptr(hit), _ptr(vals), len(vals),
+                                             _ptr(err), order, uc)
             self._check(rc)
             return hit[: n + 1], vals[: int(hit[n])], err[:n]
         hit = np.zeros(n + 1, dtype=np.uint64)
@@ -211,7 +222,8 @@ class Index:
             cap = max(4 * n, 1024)
         while True:
             out = np.empty(max(cap, 1), dtype=np.uint32)
-            rc = self._lib.tm_match_batch(self._h, n, _ptr(blob), _ptr(offs), _ptr(hit), _ptr(out), cap, _ptr(err))
+            rc = self._lib.tm_match_batch_ex(self._h, n, _ptr(blob), _ptr(offs), _ptr(hit), _ptr(out), cap, _ptr(err),
+                                             order, uc)
             if rc == TM_ECAP:
                 cap = int(hit[n])
                 continue
@@ -230,8 +242,14 @@ class Index:
 
     # ---- matching (device buffers, e.g. torch tensors' data_ptr())
     def match_batch_dev(self, n: int, d_blob: int, d_offs: int, d_hit: int, d_out: int, cap: int, d_err: int,
-                        stream: int | None = None):
-        self._check(self._lib.tm_match_batch_dev(self._h, n, d_blob, d_offs, d_hit, d_out, cap, d_err, stream))
+                        stream: int | None = None, order: int = TM_ORDER_TRAVERSAL, d_unique: int | None = None):
+        self._check(self._lib.tm_match_batch_dev_ex(self._h, n, d_blob, d_offs, d_hit, d_out, cap, d_err, order,
+                                                    d_unique, stream))
+
+    def sort_segments(self, n: int, d_hit: int, d_vals: int, cap: int, order: int = TM_ORDER_SORTED,
+                      d_unique: int | None = None, stream: int | None = None):
+        """tm_sort_segments: sort each of n CSR segments on the device in place."""
+        self._check(self._lib.tm_sort_segments(self._h, n, d_hit, d_vals, cap, order, d_unique, stream))
 
     def release_stream(self, stream: int | None):
         """Drop the batch scratch the library keeps for `stream`."""

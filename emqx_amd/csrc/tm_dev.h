@@ -35,8 +35,9 @@ struct Workspace {
     uint32_t *cnt;        // [n] hits per topic
     uint32_t *nr;         // [n] ranges per topic (RCAP+1 = overflow)
     uint2 *rng;           // [n * RCAP] (value offset, count)
-    uint32_t *lists;      // [L_COUNT * n] topic lists
-    uint32_t *list_n;     // [L_COUNT] list lengths, [L_COUNT] reset ticket, [L_COUNT + 1] scan ticket (zero between batches)
+    uint32_t *lists;      // [(L_COUNT + 1) * n] topic lists (the last one: long segments to sort)
+    uint32_t *list_n;     // [L_COUNT] list lengths, [L_COUNT] reset ticket, [L_COUNT + 1] scan ticket,
+                          // [L_COUNT + 2] long-segment count, [L_COUNT + 3] its reset ticket (zero between batches)
     uint64_t *blk;        // [n / TILE + 2] tile hit totals -> exclusive tile prefixes (zero between batches)
     uint32_t *deep_wid;   // [DEEP_LANES * MAX_LEVELS]
     uint2 *deep_stk;      // [DEEP_LANES * (MAX_LEVELS + 1)]
@@ -44,6 +45,7 @@ struct Workspace {
 };
 
 constexpr int TILE = 256;    // topics per walk block = per scan tile = per emit block
+constexpr int LIST_SLOTS = L_COUNT + 4;   // Workspace::list_n entries
 
 
 // Pipeline entry points (tm_kernels.hip).  All asynchronous on `s`.
@@ -62,6 +64,13 @@ hipError_t launch_first(const DevIndex &ix, const Workspace &ws, uint64_t n, con
 // filter-sharded merge of allgathered per-shard CSR hit lists (k_merge_shards)
 hipError_t launch_merge_shards(uint32_t world, uint64_t n, const uint64_t *shard_hit, const uint32_t *shard_vals,
                                uint64_t stride, uint64_t *out_hit, uint32_t *out, uint64_t cap, hipStream_t s);
+// sort each topic's segment of a CSR in place (ascending u32); unique: distinct
+// values first, padded with 0xFFFFFFFF, distinct count in ucnt (may be null)
+hipError_t launch_sort_segments(const Workspace &ws, uint64_t n, const uint64_t *hit_offs, uint32_t *out, uint64_t cap,
+                                int unique, uint32_t *ucnt, hipStream_t s);
+// out[0 .. min(hit[n], cap)) = src[...] (device -> device or mapped host memory)
+hipError_t launch_copy_values(const uint64_t *hit_offs, uint64_t n, const uint32_t *src, uint32_t *dst, uint64_t cap,
+                              hipStream_t s);
 // scatter patch: dst[i] (absolute device address of a u32) = val[i]
 hipError_t launch_patch(const uint64_t *d_addr, const uint32_t *d_val, uint64_t n, hipStream_t s);
 

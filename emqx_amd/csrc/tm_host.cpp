@@ -96,6 +96,7 @@ struct Lane {
     uint8_t *d_in = nullptr; uint64_t d_in_cap = 0;
     uint8_t *d_res = nullptr; uint64_t d_res_cap = 0;
     uint32_t *pin_vals = nullptr, *pin_vals_dev = nullptr; uint64_t pin_vals_cap = 0;
+    uint32_t *d_vals = nullptr; uint64_t d_vals_cap = 0;   // sorted output: values sorted in HBM first
 };
 
 // Patch staging: a small ring, so shipping a patch waits on the host only for
@@ -114,7 +115,6 @@ struct tm_index {
     std::mutex mu;
     std::condition_variable cv;      // a host lane was released
     int device = 0;
-    hipStream_t stream = nullptr;    // the index's own stream (tm_sync, device API with stream NULL)
 
     Mirror<VocabEntry> vocab; uint64_t vcount = 0;
     Mirror<uint8_t> wpool;
@@ -884,7 +884,7 @@ void free_workspace(Workspace &w) {
 
 void free_lane(Lane &l) {
     free_workspace(l.w);
-    void *dv[] = {l.d_in, l.d_res};
+    void *dv[] = {l.d_in, l.d_res, l.d_vals};
     for (void *p : dv) if (p) (void)hipFree(p);
     void *pins[] = {l.pin_in, l.pin_out, l.pin_vals};
     for (void *p : pins) if (p) (void)hipHostFree(p);
@@ -976,8 +976,8 @@ int ensure_ws(tm_index *ix, uint64_t n, Lane &ln) {
     if (!w.deep_wid) {
         HIPCHK(ix, hipMalloc(&w.deep_wid, (uint64_t)DEEP_LANES * MAX_LEVELS * 4));
         HIPCHK(ix, hipMalloc(&w.deep_stk, (uint64_t)DEEP_LANES * (MAX_LEVELS + 1) * 8));
-        HIPCHK(ix, hipMalloc(&w.list_n, (L_COUNT + 2) * 4));
-        HIPCHK(ix, hipMemsetAsync(w.list_n, 0, (L_COUNT + 2) * 4, ln.s));
+        HIPCHK(ix, hipMalloc(&w.list_n, LIST_SLOTS * 4));
+        HIPCHK(ix, hipMemsetAsync(w.list_n, 0, LIST_SLOTS * 4, ln.s));
     }
     // the batch must see every patch shipped so far, whichever stream it went on
     if (ix->last_patch) HIPCHK(ix, hipStreamWaitEvent(ln.s, ix->last_patch, 0));
@@ -988,7 +988,7 @@ int ensure_ws(tm_index *ix, uint64_t n, Lane &ln) {
     HIPCHK(ix, hipMalloc(&w.cnt, c * 4));
     HIPCHK(ix, hipMalloc(&w.nr, c * 4));
     HIPCHK(ix, hipMalloc(&w.rng, c * RCAP * 8));
-    HIPCHK(ix, hipMalloc(&w.lists, c * L_COUNT * 4));
+    HIPCHK(ix, hipMalloc(&w.lists, c * (L_COUNT + 1) * 4));
     HIPCHK(ix, hipMalloc(&w.blk, (c / TILE + 4) * 8));
     HIPCHK(ix, hipMemsetAsync(w.blk, 0, (c / TILE + 4) * 8, ln.s));   // zero between batches (k_emit)
     w.cap_n = c;
@@ -1009,7 +1009,9 @@ void init_tables(tm_index *ix, uint64_t hint) {
     ix->vals.h.reserve(hint + 16);
 }
 
-hipStream_t pick_stream(tm_index *ix, void *s) { return s ? reinterpret_cast<hipStream_t>(s) : ix->stream; }
+// NULL is HIP's default (null) stream -- the stream PyTorch's default stream
+// handle (0) names, so device-API batches order with the caller's torch work
+hipStream_t pick_stream(tm_index *, void *s) { return reinterpret_cast<hipStream_t>(s); }
 
 // events of one profiled batch (null set when profiling is off)
 int prof_begin(tm_index *ix, tm_index::ProfEv &ev, hipStream_t s) {
@@ -1059,7 +1061,6 @@ int tm_create(const tm_options *opts, tm_index **out) {
     }
     ix->device = dev;
     hipError_t e = hipSetDevice(dev);
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&ix->stream, hipStreamNonBlocking);
     for (int i = 0; i < PATCH_RING && e == hipSuccess; i++)
         e = hipEventCreateWithFlags(&ix->patch[i].done, hipEventDisableTiming);
     if (e != hipSuccess) {
@@ -1089,7 +1090,6 @@ int tm_destroy(tm_index *ix) {
     for (auto &b : ix->pinned) (void)hipHostFree(b.host);
     for (auto &ev : ix->prof_pending) { (void)hipEventDestroy(ev.b0); (void)hipEventDestroy(ev.w0); (void)hipEventDestroy(ev.w1); (void)hipEventDestroy(ev.b1); }
     for (auto &ev : ix->prof_free) { (void)hipEventDestroy(ev.b0); (void)hipEventDestroy(ev.w0); (void)hipEventDestroy(ev.w1); (void)hipEventDestroy(ev.b1); }
-    (void)hipStreamDestroy(ix->stream);
     delete ix;
     return TM_OK;
 }
@@ -1121,11 +1121,12 @@ int tm_sync(tm_index *ix, void *stream) {
     return sync_locked(ix, pick_stream(ix, stream));
 }
 
-int tm_match_batch_dev(tm_index *ix, uint64_t n, const uint8_t *bytes, const uint64_t *offs, uint64_t *hit_offs,
-                       uint32_t *out, uint64_t cap, uint8_t *err, void *stream) {
+int tm_match_batch_dev_ex(tm_index *ix, uint64_t n, const uint8_t *bytes, const uint64_t *offs, uint64_t *hit_offs,
+                          uint32_t *out, uint64_t cap, uint8_t *err, uint32_t order, uint32_t *ucnt, void *stream) {
     if (!ix) return fail(nullptr, TM_EINVAL, "tm_match_batch_dev: null handle");
     if (!hit_offs || (n && (!offs || !bytes || !err))) return fail(ix, TM_EINVAL, "tm_match_batch_dev: null buffer");
     if (n >= 0xFFFFFFFFull) return fail(ix, TM_EINVAL, "tm_match_batch_dev: batch too large");
+    if (order > TM_ORDER_UNIQUE) return fail(ix, TM_EINVAL, "tm_match_batch_dev: bad order");
     std::lock_guard<std::mutex> g(ix->mu);
     hipStream_t s = pick_stream(ix, stream);
     int rc;
@@ -1138,8 +1139,31 @@ int tm_match_batch_dev(tm_index *ix, uint64_t n, const uint8_t *bytes, const uin
     if ((rc = prof_begin(ix, ev, s))) return rc;
     HIPCHK(ix, launch_match_phase1(d, ln->w, n, bytes, offs, hit_offs, err, s, ev.w0, ev.w1));
     HIPCHK(ix, launch_match_phase2(d, ln->w, n, bytes, offs, hit_offs, out, out ? cap : 0, s));
+    if (order != TM_ORDER_TRAVERSAL && out)
+        HIPCHK(ix, launch_sort_segments(ln->w, n, hit_offs, out, cap, order == TM_ORDER_UNIQUE, ucnt, s));
     if ((rc = batch_done(ix, *ln))) return rc;
     return prof_end(ix, ev, s);
+}
+
+int tm_match_batch_dev(tm_index *ix, uint64_t n, const uint8_t *bytes, const uint64_t *offs, uint64_t *hit_offs,
+                       uint32_t *out, uint64_t cap, uint8_t *err, void *stream) {
+    return tm_match_batch_dev_ex(ix, n, bytes, offs, hit_offs, out, cap, err, TM_ORDER_TRAVERSAL, nullptr, stream);
+}
+
+int tm_sort_segments(tm_index *ix, uint64_t n, const uint64_t *hit_offs, uint32_t *vals, uint64_t cap, uint32_t order,
+                     uint32_t *ucnt, void *stream) {
+    if (!ix) return fail(nullptr, TM_EINVAL, "tm_sort_segments: null handle");
+    if (!hit_offs || (cap && !vals) || order > TM_ORDER_UNIQUE) return fail(ix, TM_EINVAL, "tm_sort_segments: bad argument");
+    if (n >= 0xFFFFFFFFull) return fail(ix, TM_EINVAL, "tm_sort_segments: too many segments");
+    if (order == TM_ORDER_TRAVERSAL || !n) return TM_OK;
+    std::lock_guard<std::mutex> g(ix->mu);
+    hipStream_t s = pick_stream(ix, stream);
+    Lane *ln;
+    int rc;
+    if ((rc = dev_lane(ix, s, ln))) return rc;
+    if ((rc = ensure_ws(ix, n, *ln))) return rc;
+    HIPCHK(ix, launch_sort_segments(ln->w, n, hit_offs, vals, cap, order == TM_ORDER_UNIQUE, ucnt, s));
+    return batch_done(ix, *ln);
 }
 
 int tm_stream_release(tm_index *ix, void *stream) {
@@ -1268,14 +1292,16 @@ static double now_us() {
 // the index's current device view and queue the kernels on the caller's lane;
 // they wait for the GPU and copy results out without it, so concurrent callers
 // overlap on the device (each lane is its own stream) and deltas keep flowing.
-int tm_match_batch(tm_index *ix, uint64_t n, const uint8_t *tb, const uint64_t *to, uint64_t *out_hit,
-                   uint32_t *out_vals, uint64_t cap, uint8_t *out_err) {
+int tm_match_batch_ex(tm_index *ix, uint64_t n, const uint8_t *tb, const uint64_t *to, uint64_t *out_hit,
+                      uint32_t *out_vals, uint64_t cap, uint8_t *out_err, uint32_t order, uint32_t *out_unique) {
     static const bool timing = getenv("TM_HOST_TIMING") != nullptr;
     double tt[8]; int nt = 0;
     if (timing) tt[nt++] = now_us();
     if (!ix) return fail(nullptr, TM_EINVAL, "tm_match_batch: null handle");
     if (!to || !out_hit || (n && !tb && to[n] != to[0])) return fail(ix, TM_EINVAL, "tm_match_batch: null buffer");
     if (n >= 0xFFFFFFFFull) return fail(ix, TM_EINVAL, "tm_match_batch: batch too large");
+    if (order > TM_ORDER_UNIQUE) return fail(ix, TM_EINVAL, "tm_match_batch: bad order");
+    const bool sorted = order != TM_ORDER_TRAVERSAL, unique = order == TM_ORDER_UNIQUE;
     std::unique_lock<std::mutex> g(ix->mu);
     HIPCHK(ix, hipSetDevice(ix->device));
     LaneLease lease{ix, g};
@@ -1295,17 +1321,27 @@ int tm_match_batch(tm_index *ix, uint64_t n, const uint8_t *tb, const uint64_t *
         uint8_t *dh = pinned_dev(ix, out_hit, (n + 1) * 8);
         uint8_t *dv = out_vals ? pinned_dev(ix, out_vals, cap * 4) : nullptr;
         uint8_t *de = out_err ? pinned_dev(ix, out_err, n) : nullptr;
+        uint8_t *du = out_unique ? pinned_dev(ix, out_unique, n * 4) : nullptr;
         const bool aligned = ((uintptr_t)tb & 15) == 0;
-        if ((db || !nbytes) && aligned && dof && dh && (dv || !out_vals) && (de || !out_err)) {
+        if ((db || !nbytes) && aligned && dof && dh && (dv || !out_vals) && (de || !out_err) && (du || !out_unique)) {
             if (!de) {   // flags nobody reads still need a home
                 if ((rc = stage_out(ix, ln, n, n, de))) return rc;
             }
             const DevIndex d = dev_view(ix);
             const uint8_t *dbytes = db ? db : dof;   // no bytes: any valid address
             uint64_t *dhit = reinterpret_cast<uint64_t *>(dh);
+            uint32_t *vdst = reinterpret_cast<uint32_t *>(dv);
+            if (sorted && dv) {   // sorted in HBM, then copied into the caller's buffer
+                if ((rc = grow_dev(ix, s, ln.d_vals, ln.d_vals_cap, cap))) return rc;
+                vdst = ln.d_vals;
+            }
             HIPCHK(ix, launch_match_phase1(d, ln.w, n, dbytes, reinterpret_cast<const uint64_t *>(dof), dhit, de, s));
-            HIPCHK(ix, launch_match_phase2(d, ln.w, n, dbytes, reinterpret_cast<const uint64_t *>(dof), dhit,
-                                           reinterpret_cast<uint32_t *>(dv), dv ? cap : 0, s));
+            HIPCHK(ix, launch_match_phase2(d, ln.w, n, dbytes, reinterpret_cast<const uint64_t *>(dof), dhit, vdst,
+                                           dv ? cap : 0, s));
+            if (sorted && dv) {
+                HIPCHK(ix, launch_sort_segments(ln.w, n, dhit, vdst, cap, unique, reinterpret_cast<uint32_t *>(du), s));
+                HIPCHK(ix, launch_copy_values(dhit, n, vdst, reinterpret_cast<uint32_t *>(dv), cap, s));
+            }
             if ((rc = batch_done(ix, ln))) return rc;
             g.unlock();
             if (timing) tt[nt++] = now_us();
@@ -1322,14 +1358,18 @@ int tm_match_batch(tm_index *ix, uint64_t n, const uint8_t *tb, const uint64_t *
     const uint64_t *doffs;
     if ((rc = stage_in(ix, ln, n, tb, to, dbytes, doffs))) return rc;
     if (timing) tt[nt++] = now_us();
-    // results: hit offsets (n + 1) x u64, then the badarg flags; the values are
-    // written by k_emit straight into mapped pinned memory, so the batch costs
-    // one host synchronisation (a second one only when that buffer must grow)
-    const uint64_t rbytes = (n + 1) * 8 + n;
+    // results: hit offsets (n + 1) x u64, then the badarg flags (then the
+    // distinct counts, u32, for UNIQUE); the values are written by k_emit
+    // straight into mapped pinned memory (sorted orders: sorted in HBM, then
+    // copied there), so the batch costs one host synchronisation (a second
+    // one only when that buffer must grow)
+    const uint64_t uoff = ((n + 1) * 8 + n + 3) & ~3ull;
+    const uint64_t rbytes = (sorted && out_unique) ? uoff + 4 * n : (n + 1) * 8 + n;
     uint8_t *dres;
     if ((rc = stage_out(ix, ln, n, rbytes, dres))) return rc;
     uint64_t *dhit = reinterpret_cast<uint64_t *>(dres);
     uint8_t *derr = dres + (n + 1) * 8;
+    uint32_t *dunq = (sorted && out_unique) ? reinterpret_cast<uint32_t *>(dres + uoff) : nullptr;
     uint64_t total = 0;
     for (int attempt = 0; attempt < 2; attempt++) {
         if (!ln.pin_vals) {
@@ -1337,9 +1377,16 @@ int tm_match_batch(tm_index *ix, uint64_t n, const uint8_t *tb, const uint64_t *
             HIPCHK(ix, hipHostMalloc(&ln.pin_vals, ln.pin_vals_cap * 4, hipHostMallocMapped));
             HIPCHK(ix, hipHostGetDevicePointer(reinterpret_cast<void **>(&ln.pin_vals_dev), ln.pin_vals, 0));
         }
+        uint32_t *vdst = ln.pin_vals_dev;
+        if (sorted && (rc = grow_dev(ix, s, ln.d_vals, ln.d_vals_cap, ln.pin_vals_cap))) return rc;
+        if (sorted) vdst = ln.d_vals;
         const DevIndex d = dev_view(ix);
         HIPCHK(ix, launch_match_phase1(d, ln.w, n, dbytes, doffs, dhit, derr, s));
-        HIPCHK(ix, launch_match_phase2(d, ln.w, n, dbytes, doffs, dhit, ln.pin_vals_dev, ln.pin_vals_cap, s));
+        HIPCHK(ix, launch_match_phase2(d, ln.w, n, dbytes, doffs, dhit, vdst, ln.pin_vals_cap, s));
+        if (sorted) {
+            HIPCHK(ix, launch_sort_segments(ln.w, n, dhit, vdst, ln.pin_vals_cap, unique, dunq, s));
+            HIPCHK(ix, launch_copy_values(dhit, n, vdst, ln.pin_vals_dev, ln.pin_vals_cap, s));
+        }
         if ((rc = fetch_out(ix, ln, n, rbytes))) return rc;
         if ((rc = batch_done(ix, ln))) return rc;
         g.unlock();
@@ -1358,6 +1405,7 @@ int tm_match_batch(tm_index *ix, uint64_t n, const uint8_t *tb, const uint64_t *
     }
     memcpy(out_hit, ln.pin_out, (n + 1) * 8);
     if (out_err && n) memcpy(out_err, ln.pin_out + (n + 1) * 8, n);
+    if (dunq && n) memcpy(out_unique, ln.pin_out + uoff, 4 * n);
     const uint64_t keep = std::min(total, out_vals ? cap : 0);
     if (keep) memcpy(out_vals, ln.pin_vals, keep * 4);
     if (timing) {
@@ -1366,6 +1414,11 @@ int tm_match_batch(tm_index *ix, uint64_t n, const uint8_t *tb, const uint64_t *
                 (unsigned long)n, tt[1] - tt[0], tt[2] - tt[1], tt[3] - tt[2], tt[4] - tt[3], tt[nt - 1] - tt[4]);
     }
     return (out_vals && total > cap) ? TM_ECAP : TM_OK;
+}
+
+int tm_match_batch(tm_index *ix, uint64_t n, const uint8_t *tb, const uint64_t *to, uint64_t *out_hit,
+                   uint32_t *out_vals, uint64_t cap, uint8_t *out_err) {
+    return tm_match_batch_ex(ix, n, tb, to, out_hit, out_vals, cap, out_err, TM_ORDER_TRAVERSAL, nullptr);
 }
 
 int tm_first_batch(tm_index *ix, uint64_t n, const uint8_t *tb, const uint64_t *to, uint32_t *out_value,

@@ -1256,6 +1256,186 @@ __global__ __launch_bounds__(256) void k_merge_shards(uint32_t world, uint64_t n
         if (d < cap) out[d] = src[i];
 }
 
+// ------------------------------------------------------ sorted hit lists
+//
+// Ascending-u32 output ("hit lists come out sorted (ascending
+// u32), plus a mode that emits the reference traversal order"): a post-pass
+// over any CSR of hit lists (the emit's, or the merged shards') sorts each
+// topic's segment in place; UNIQUE also drops repeated values (the
+// [unique] option of matches/3, emqx_trie_search.erl:201-211, when the u32
+// is the interned ID): the distinct values first, the rest of the segment
+// padded with 0xFFFFFFFF, and the distinct count per topic in ucnt.
+//
+// Segments of up to SS_SMALL values: one lane each (insertion sort in LDS,
+// laid out [k][thread]: conflict free).  Longer ones are listed and sorted by
+// one block each (bitonic, LDS up to SS_LDS values; beyond that chunks sorted
+// in LDS and merged with global-memory steps).  The bitonic network is the
+// all-ascending ("flip") form, so a segment of any length c sorts as if
+// padded to a power of two with +inf: comparators touching index >= c are
+// no-ops and never run.
+constexpr int SS_SMALL = 32;
+constexpr int SS_BLOCK = 256;
+constexpr int SS_LDS = 8192;
+constexpr int SS_GRID_BIG = 512;
+enum { SS_CNT = L_COUNT + 2, SS_TICKET = L_COUNT + 3 };   // Workspace::list_n slots
+
+__device__ __forceinline__ void cas_up(uint32_t *v, uint64_t i, uint64_t j) {
+    const uint32_t a = v[i], b = v[j];
+    if (a > b) { v[i] = b; v[j] = a; }
+}
+
+// comparator k of a step whose partner bit is b: index i has bit b clear
+__device__ __forceinline__ uint64_t cmp_index(uint64_t k, uint32_t b) {
+    return ((k >> b) << (b + 1)) | (k & ((1ull << b) - 1));
+}
+
+// bitonic steps of sizes [size0, size1] (flip + half-cleaners down to stride
+// smin) over v[0, c), by the block; v is LDS or global
+template <bool LDS>
+__device__ void bitonic_steps(uint32_t *v, uint64_t c, uint64_t P, uint64_t size0, uint64_t size1, uint64_t smin) {
+    for (uint64_t size = size0; size <= size1; size <<= 1) {
+        const uint32_t bf = 63 - __clzll(size >> 1);
+        for (uint64_t k = threadIdx.x; k < P / 2; k += blockDim.x) {   // flip: i <-> i ^ (size - 1)
+            const uint64_t i = cmp_index(k, bf), j = i ^ (size - 1);
+            if (j < c) cas_up(v, i, j);
+        }
+        if (!LDS) __threadfence_block();
+        __syncthreads();
+        for (uint64_t st = size >> 2; st >= smin && st > 0; st >>= 1) {   // half-cleaners: i <-> i + st
+            const uint32_t b = 63 - __clzll(st);
+            for (uint64_t k = threadIdx.x; k < P / 2; k += blockDim.x) {
+                const uint64_t i = cmp_index(k, b), j = i + st;
+                if (j < c) cas_up(v, i, j);
+            }
+            if (!LDS) __threadfence_block();
+            __syncthreads();
+        }
+    }
+}
+
+// the remaining half-cleaner strides < SS_LDS of a merge step, chunk by chunk in LDS
+__device__ void bitonic_tail_lds(uint32_t *g, uint64_t c, uint32_t *s, uint64_t st0) {
+    for (uint64_t base = 0; base < c; base += SS_LDS) {
+        const uint64_t len = c - base < (uint64_t)SS_LDS ? c - base : SS_LDS;
+        for (uint64_t k = threadIdx.x; k < len; k += blockDim.x) s[k] = g[base + k];
+        __syncthreads();
+        for (uint64_t st = st0; st > 0; st >>= 1) {
+            const uint32_t b = 63 - __clzll(st);
+            for (uint64_t k = threadIdx.x; k < SS_LDS / 2; k += blockDim.x) {
+                const uint64_t i = cmp_index(k, b), j = i + st;
+                if (j < len) cas_up(s, i, j);
+            }
+            __syncthreads();
+        }
+        for (uint64_t k = threadIdx.x; k < len; k += blockDim.x) g[base + k] = s[k];
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(SS_BLOCK) void k_segsort_small(uint64_t n, const uint64_t *hit, uint32_t *out, uint64_t cap,
+                                                            int unique, uint32_t *ucnt, Workspace ws) {
+    __shared__ uint32_t s[SS_SMALL * SS_BLOCK];
+    const uint64_t t = (uint64_t)blockIdx.x * SS_BLOCK + threadIdx.x;
+    if (t >= n) return;
+    const uint64_t o = hit[t], e = hit[t + 1], c = e - o;
+    if (e > cap) {   // not (wholly) written: the caller gets TM_ECAP and retries
+        if (ucnt) ucnt[t] = 0;
+        return;
+    }
+    if (c > SS_SMALL) {
+        const uint32_t i = atomicAdd(&ws.list_n[SS_CNT], 1u);
+        ws.lists[(uint64_t)L_COUNT * n + i] = (uint32_t)t;
+        return;
+    }
+    uint32_t *v = s + threadIdx.x;
+    for (uint32_t k = 0; k < c; k++) v[k * SS_BLOCK] = out[o + k];
+    for (uint32_t i = 1; i < c; i++) {
+        const uint32_t x = v[i * SS_BLOCK];
+        uint32_t j = i;
+        while (j > 0 && v[(j - 1) * SS_BLOCK] > x) { v[j * SS_BLOCK] = v[(j - 1) * SS_BLOCK]; j--; }
+        v[j * SS_BLOCK] = x;
+    }
+    uint32_t u = 0;
+    for (uint32_t k = 0; k < c; k++) {
+        const uint32_t x = v[k * SS_BLOCK];
+        if (!unique || k == 0 || x != v[(k - 1) * SS_BLOCK]) out[o + u++] = x;
+    }
+    for (uint32_t k = u; k < c; k++) out[o + k] = NONE;
+    if (ucnt) ucnt[t] = u;
+}
+
+__global__ __launch_bounds__(SS_BLOCK) void k_segsort_big(uint64_t n, const uint64_t *hit, uint32_t *out, int unique,
+                                                          uint32_t *ucnt, Workspace ws) {
+    __shared__ uint32_t s[SS_LDS];
+    __shared__ uint64_t s_w[4];
+    const uint32_t cnt = ws.list_n[SS_CNT];
+    const uint32_t *lst = ws.lists + (uint64_t)L_COUNT * n;
+    for (uint32_t li = blockIdx.x; li < cnt; li += gridDim.x) {
+        const uint64_t t = lst[li];
+        const uint64_t o = hit[t], c = hit[t + 1] - o;
+        uint64_t P = 1;
+        while (P < c) P <<= 1;
+        uint32_t *g = out + o;
+        if (c <= SS_LDS) {
+            for (uint64_t k = threadIdx.x; k < c; k += SS_BLOCK) s[k] = g[k];
+            __syncthreads();
+            bitonic_steps<true>(s, c, P, 2, P, 1);
+            for (uint64_t k = threadIdx.x; k < c; k += SS_BLOCK) g[k] = s[k];
+            __syncthreads();
+        } else {
+            for (uint64_t base = 0; base < c; base += SS_LDS) {   // every SS_LDS chunk sorted in LDS
+                const uint64_t len = c - base < (uint64_t)SS_LDS ? c - base : SS_LDS;
+                for (uint64_t k = threadIdx.x; k < len; k += SS_BLOCK) s[k] = g[base + k];
+                __syncthreads();
+                bitonic_steps<true>(s, len, SS_LDS, 2, SS_LDS, 1);
+                for (uint64_t k = threadIdx.x; k < len; k += SS_BLOCK) g[base + k] = s[k];
+                __syncthreads();
+            }
+            for (uint64_t size = 2 * SS_LDS; size <= P; size <<= 1) {   // merge levels: strides >= SS_LDS in global
+                bitonic_steps<false>(g, c, P, size, size, SS_LDS);
+                bitonic_tail_lds(g, c, s, SS_LDS / 2);
+            }
+        }
+        if (unique) {   // distinct values first (block scan of "differs from its left neighbour"), then padding
+            uint64_t carry = 0;
+            for (uint64_t b0 = 0; b0 < c; b0 += SS_BLOCK) {
+                const uint64_t k = b0 + threadIdx.x;
+                const uint32_t x = k < c ? g[k] : 0;
+                const bool f = k < c && (k == 0 || g[k - 1] != x);
+                uint64_t tot;
+                const uint64_t pos = carry + block_excl_scan(f ? 1 : 0, tot, s_w);
+                __syncthreads();   // every read of this window before any write into it
+                if (f) g[pos] = x;
+                carry += tot;
+                __threadfence_block();
+                __syncthreads();
+            }
+            for (uint64_t k = carry + threadIdx.x; k < c; k += SS_BLOCK) g[k] = NONE;
+            if (ucnt && threadIdx.x == 0) ucnt[t] = (uint32_t)carry;
+        } else if (ucnt && threadIdx.x == 0) {
+            ucnt[t] = (uint32_t)c;
+        }
+        __syncthreads();
+    }
+    // the last block resets the list for the next batch
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t ticket = atomicAdd(&ws.list_n[SS_TICKET], 1u);
+        if (ticket == gridDim.x - 1) {
+            atomicExch(&ws.list_n[SS_CNT], 0u);
+            atomicExch(&ws.list_n[SS_TICKET], 0u);
+        }
+    }
+}
+
+// copy a CSR's values (total = hit[n], at most cap) to dst (e.g. mapped host memory)
+__global__ __launch_bounds__(256) void k_copy_values(const uint64_t *hit, uint64_t n, const uint32_t *src, uint32_t *dst,
+                                                     uint64_t cap) {
+    const uint64_t total = hit[n] < cap ? hit[n] : cap;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (uint64_t)gridDim.x * 256)
+        dst[i] = src[i];
+}
+
 // ------------------------------------------------------------ launchers
 
 static inline uint32_t blocks_for(uint64_t n, uint32_t per) { return (uint32_t)((n + per - 1) / per); }
@@ -1322,6 +1502,23 @@ hipError_t launch_merge_shards(uint32_t world, uint64_t n, const uint64_t *shard
     const uint64_t threads = (uint64_t)world * (n + 1);
     hipLaunchKernelGGL(k_merge_shards, dim3(blocks_for(threads, 256)), dim3(256), 0, s, world, n, shard_hit,
                        shard_vals, stride, out_hit, out, cap);
+    return hipGetLastError();
+}
+
+hipError_t launch_sort_segments(const Workspace &ws, uint64_t n, const uint64_t *hit_offs, uint32_t *out, uint64_t cap,
+                                int unique, uint32_t *ucnt, hipStream_t s) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_segsort_small, dim3(blocks_for(n, SS_BLOCK)), dim3(SS_BLOCK), 0, s, n, hit_offs, out, cap, unique,
+                       ucnt, ws);
+    hipLaunchKernelGGL(k_segsort_big, dim3(SS_GRID_BIG), dim3(SS_BLOCK), 0, s, n, hit_offs, out, unique, ucnt, ws);
+    return hipGetLastError();
+}
+
+hipError_t launch_copy_values(const uint64_t *hit_offs, uint64_t n, const uint32_t *src, uint32_t *dst, uint64_t cap,
+                              hipStream_t s) {
+    if (!cap) return hipSuccess;
+    const uint64_t blocks = cap / 256 + 1 < 2048 ? cap / 256 + 1 : 2048;
+    hipLaunchKernelGGL(k_copy_values, dim3((uint32_t)blocks), dim3(256), 0, s, hit_offs, n, src, dst, cap);
     return hipGetLastError();
 }
 

@@ -101,7 +101,7 @@ int tm_destroy(tm_index *h);
 int tm_apply_deltas(tm_index *h, uint64_t n, const uint8_t *ops, const uint8_t *filter_bytes,
                     const uint64_t *filter_offsets, const uint32_t *values, const uint8_t *key_flags);
 
-/* Upload pending patches on `stream` (hipStream_t; NULL = the index's own stream). */
+/* Upload pending patches on `stream` (hipStream_t; NULL = the default stream). */
 int tm_sync(tm_index *h, void *stream);
 
 /* Host buffers in, host buffers out (pinned staging inside).  Blocks until the
@@ -118,6 +118,22 @@ int tm_sync(tm_index *h, void *stream);
 int tm_match_batch(tm_index *h, uint64_t n, const uint8_t *topic_bytes, const uint64_t *topic_offsets,
                    uint64_t *out_hit_offsets, uint32_t *out_values, uint64_t cap, uint8_t *out_err);
 
+/* Output order of a topic's hit list:
+ *   TM_ORDER_TRAVERSAL  the reference's traversal order (see "Output" above)
+ *   TM_ORDER_SORTED     ascending u32
+ *   TM_ORDER_UNIQUE     ascending u32 without repeats -- matches/3 with
+ *                       [unique] (emqx_trie_search.erl:201-211) when the NIF
+ *                       interns IDs (not whole keys) to u32: the distinct
+ *                       values come first in the topic's segment, the rest of
+ *                       the segment is 0xFFFFFFFF, and out_unique[i] (n
+ *                       entries, may be NULL) is topic i's distinct count.
+ * Offsets are the same in every order. */
+enum { TM_ORDER_TRAVERSAL = 0, TM_ORDER_SORTED = 1, TM_ORDER_UNIQUE = 2 };
+
+int tm_match_batch_ex(tm_index *h, uint64_t n, const uint8_t *topic_bytes, const uint64_t *topic_offsets,
+                      uint64_t *out_hit_offsets, uint32_t *out_values, uint64_t cap, uint8_t *out_err,
+                      uint32_t order, uint32_t *out_unique);
+
 /* Pinned host buffers, mapped into the index's device.  A NIF keeps its
  * per-scheduler batch buffers here: when every buffer given to tm_match_batch
  * (topic bytes -- 16-byte aligned --, offsets, hit offsets, values and err if
@@ -130,7 +146,8 @@ int tm_host_alloc(tm_index *h, uint64_t bytes, void **out);
 int tm_host_free(tm_index *h, void *p);
 
 /* Device-resident batch: every pointer is device memory; asynchronous on
- * `stream` (hipStream_t; NULL = the index's own stream).  d_out_hit_offsets has
+ * `stream` (hipStream_t; NULL = HIP's default stream, which PyTorch's default
+ * stream handle 0 also names).  d_out_hit_offsets has
  * n+1 entries and d_out_hit_offsets[n] is the total; values beyond `cap` are
  * dropped (the caller compares the total with cap after synchronising).
  * The library keeps batch scratch for the 16 most recently used streams (an
@@ -138,6 +155,18 @@ int tm_host_free(tm_index *h, void *p);
 int tm_match_batch_dev(tm_index *h, uint64_t n, const uint8_t *d_topic_bytes, const uint64_t *d_topic_offsets,
                        uint64_t *d_out_hit_offsets, uint32_t *d_out_values, uint64_t cap,
                        uint8_t *d_out_err, void *stream);
+
+int tm_match_batch_dev_ex(tm_index *h, uint64_t n, const uint8_t *d_topic_bytes, const uint64_t *d_topic_offsets,
+                          uint64_t *d_out_hit_offsets, uint32_t *d_out_values, uint64_t cap,
+                          uint8_t *d_out_err, uint32_t order, uint32_t *d_out_unique, void *stream);
+
+/* Sort each segment of a device CSR (n segments, d_hit_offsets[n+1]) in
+ * place in TM_ORDER_SORTED / TM_ORDER_UNIQUE order (d_out_unique as above),
+ * asynchronously on `stream`: e.g. the merged lists of tm_merge_shards, which
+ * then equal one index's sorted lists exactly.  Segments past `cap` values are
+ * left alone. */
+int tm_sort_segments(tm_index *h, uint64_t n, const uint64_t *d_hit_offsets, uint32_t *d_values, uint64_t cap,
+                     uint32_t order, uint32_t *d_out_unique, void *stream);
 
 /* Release the batch scratch kept for `stream` (after its batches finish);
  * a caller that retires a stream calls this.  No reference counterpart. */

@@ -13,6 +13,8 @@ export TMPDIR=/tmp
 if [ $BENCH = 1 ]; then
   timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/bench -o run --output-format csv -- \
     python3 -u bench.py > $OUT/bench.json 2> $OUT/bench.err
+  # the bench's concurrent-caller leg launches ~10^5 kernels: keep the trace compressed
+  gzip -f $OUT/bench/run_kernel_trace.csv
 fi
 timeout -k 10 200 python3 -u tools/profile_walk.py "$@" > $OUT/timing.txt 2>&1
 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- \

@@ -41,8 +41,15 @@ def short(name):
     return n
 
 
+def _open(path):
+    if os.path.isfile(path):
+        return open(path)
+    import gzip
+    return gzip.open(path + ".gz", "rt")
+
+
 def trace_table(path):
-    rows = list(csv.DictReader(open(path)))
+    rows = list(csv.DictReader(_open(path)))
     agg = defaultdict(list)
     for r in rows:
         grid = int(r.get("Grid_Size_X") or r.get("Grid_Size") or 0)
@@ -81,7 +88,7 @@ def pmc_values(prof, grid, last):
 def split_phases(path, grid, n_iso):
     """k_walk_fast full-grid launches of the bench run in time order -> (timed
     region + warmup, isolated pass) durations in ns"""
-    rows = [r for r in csv.DictReader(open(path)) if "k_walk_fast" in r["Kernel_Name"]
+    rows = [r for r in csv.DictReader(_open(path)) if "k_walk_fast" in r["Kernel_Name"]
             and int(r.get("Grid_Size_X") or r.get("Grid_Size") or 0) == grid]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     d = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows]
@@ -102,7 +109,7 @@ def main(prof, rnd, tag, config, filters, batch, rotate=4, batches=8):
     for sub, title in (("bench", "bench.py with its defaults (includes the 4k/64k latency batches and the isolated walk batches)"),
                        ("trace", "tools/profile_walk.py (full batches only)")):
         p = os.path.join(prof, sub, "run_kernel_trace.csv")
-        if not os.path.isfile(p):
+        if not (os.path.isfile(p) or os.path.isfile(p + ".gz")):
             continue
         tab, agg = trace_table(p)
         lines += [f"## Kernel trace: {title}", ""] + tab + [""]
