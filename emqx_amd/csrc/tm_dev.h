@@ -17,6 +17,10 @@ struct DevIndex {
     const ExactEntry *exact; uint32_t xmask;
     const uint16_t *xfp;
     const uint32_t *wseq;
+#ifdef TM_STUDY_HOSTWIDS
+    const uint32_t *study_wids;   // study build: level-major wids of the batch, looked up on the host
+    uint64_t study_n;
+#endif
 };
 
 constexpr int FAST_L = 8;        // levels handled by the main walk kernel (LDS frontier)

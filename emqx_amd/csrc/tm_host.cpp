@@ -139,6 +139,9 @@ struct tm_index {
     struct Pinned { uint8_t *host, *dev; uint64_t size; };
     std::vector<Pinned> pinned;
 
+#ifdef TM_STUDY_HOSTWIDS
+    const uint32_t *study_wids = nullptr; uint64_t study_n = 0;
+#endif
     // diagnostics (tm_profile_*)
     bool prof = false;
     struct ProfEv { hipEvent_t b0, w0, w1, b1; };
@@ -224,11 +227,14 @@ void vocab_bytes(tm_index *ix, const VocabEntry &e, std::string &out) {
     }
 }
 
+#ifndef TM_VOCAB_LOAD_SHIFT
+#define TM_VOCAB_LOAD_SHIFT 2
+#endif
 void vocab_grow(tm_index *ix, uint64_t need) {
     // load <= 1/4: the walk's deferred probes resolve on the first slot
     // almost always (one round trip per topic for all its levels)
-    if (need * 4 <= ix->vocab.h.size()) return;
-    std::vector<VocabEntry> nt(pow2_at_least(need * 4), empty_vocab());
+    if ((need << TM_VOCAB_LOAD_SHIFT) <= ix->vocab.h.size()) return;
+    std::vector<VocabEntry> nt(pow2_at_least(need << TM_VOCAB_LOAD_SHIFT), empty_vocab());
     const uint32_t mask = (uint32_t)nt.size() - 1;
     std::string w;
     for (const VocabEntry &e : ix->vocab.h) {
@@ -871,6 +877,9 @@ DevIndex dev_view(tm_index *ix) {
     d.exact = ix->exact.d; d.xmask = (uint32_t)ix->exact.h.size() - 1;
     d.xfp = ix->xfp.d;
     d.wseq = ix->wseq.d;
+#ifdef TM_STUDY_HOSTWIDS
+    d.study_wids = ix->study_wids; d.study_n = ix->study_n;
+#endif
     return d;
 }
 
@@ -1503,6 +1512,26 @@ int tm_profile_read(tm_index *ix, double *walk_ms, double *batch_ms, uint64_t *b
     if (reset) { ix->prof_walk_ms = ix->prof_batch_ms = 0; ix->prof_batches = 0; }
     return TM_OK;
 }
+
+#ifdef TM_STUDY_HOSTWIDS
+// study build only: the level-major wids (FAST_L levels) of a host batch, looked
+// up on the host, and the device copy the walk reads instead of probing the vocab
+int tm_study_wids(tm_index *ix, uint64_t n, const uint8_t *tb, const uint64_t *to, uint32_t *out) {
+    std::lock_guard<std::mutex> g(ix->mu);
+    std::vector<WordRef> w;
+    for (uint64_t t = 0; t < n; t++) {
+        split_words(tb + to[t], (uint32_t)(to[t + 1] - to[t]), w);
+        for (uint32_t l = 0; l < (uint32_t)FAST_L; l++)
+            out[(uint64_t)l * n + t] = l < w.size() ? vocab_find(ix, w[l].p, w[l].n) : NONE;
+    }
+    return TM_OK;
+}
+int tm_study_set_wids(tm_index *ix, const uint32_t *d_wids, uint64_t n) {
+    std::lock_guard<std::mutex> g(ix->mu);
+    ix->study_wids = d_wids; ix->study_n = n;
+    return TM_OK;
+}
+#endif
 
 int tm_stats(tm_index *ix, tm_stats_t *o) {
     if (!ix || !o) return fail(ix, TM_EINVAL, "tm_stats: null argument");

@@ -39,6 +39,22 @@ __device__ __forceinline__ uint4 ld4_once(const void *p) {
     return make_uint4(v.x, v.y, v.z, v.w);
 }
 
+// Loads of structures a topic touches once and no other topic is likely to
+// touch soon (study switches TM_NT_*): non-temporal, so they do not push the
+// hot upper trie levels and the vocab out of the XCD's L2.
+__device__ __forceinline__ uint4 ld4_cold(const void *p) {
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ uint32_t ld_xfp(const uint16_t *p) {
+#ifdef TM_NT_XFP
+    return __builtin_nontemporal_load(p);
+#else
+    return *p;
+#endif
+}
+
 // bit b (0..191) of a table-mode node's Bloom: words kw[2..3], kc[0..3]
 __device__ __forceinline__ uint32_t bloom_bit(const uint4 &n2, const uint4 &n3, uint32_t b) {
     const uint32_t j = b >> 5;
@@ -126,9 +142,13 @@ __device__ uint32_t vocab_find(const DevIndex &ix, const WordAcc &w, const uint8
 // literal child in a node's private table (table mode, nlit > KINL), with the
 // slot's summary of the child
 __device__ __forceinline__ uint32_t ctab_find(const DevIndex &ix, uint32_t off, uint32_t mask, uint32_t wid,
-                                              uint32_t h, uint32_t &slo, uint32_t &shi) {
+                                              uint32_t h, uint32_t &slo, uint32_t &shi, bool cold = false) {
     for (uint32_t s = h & mask;; s = (s + 1) & mask) {
+#ifdef TM_NT_CTAB
+        uint4 e = cold ? ld4_cold(ix.ctab + off + s) : ld4(ix.ctab + off + s);
+#else
         uint4 e = ld4(ix.ctab + off + s);
+#endif
         pin(e);
         if (e.x == wid) { slo = e.z; shi = e.w; return e.y; }
         if (e.x == NONE) return NONE;
@@ -147,6 +167,9 @@ struct LdsStore {
     uint8_t *len8;                           // [level][thread] word lengths (deferred probes)
     uint32_t stride;
     uint64_t mask;
+#ifdef TM_STUDY_HOSTWIDS
+    uint64_t study_t = ~0ull;                // study build: the topic (wids precomputed on the host)
+#endif
 #ifdef TM_STUDY
     uint32_t n_steps = 0, n_probe = 0;   // study build: node visits, child-table probes
 #endif
@@ -306,6 +329,15 @@ __device__ int tokenize(const DevIndex &ix, const uint8_t *blob, uint64_t beg, u
         if (rc) return rc;
         L = lev;
     }
+#ifdef TM_STUDY_HOSTWIDS   // study: wids from a host-computed array (the vocab's share of the walk)
+    if constexpr (S::deferred) {
+        if (st.study_t != ~0ull) {
+            for (uint32_t l = 0; l < L; l++)
+                if (!((longmask >> l) & 1)) st.set_wid(l, ix.study_wids[(uint64_t)l * ix.study_n + st.study_t]);
+            goto wids_done;
+        }
+    }
+#endif
 #ifdef TM_STUDY_SCANONLY   // timing study: no vocab probes (wrong results)
     if constexpr (S::deferred) {
         for (uint32_t l = 0; l < L; l++) if (!((longmask >> l) & 1)) st.set_wid(l, st.word_b0(l) ^ st.word_b1(l));
@@ -348,6 +380,9 @@ __device__ int tokenize(const DevIndex &ix, const uint8_t *blob, uint64_t beg, u
             }
         }
     }
+#ifdef TM_STUDY_HOSTWIDS
+wids_done:
+#endif
     for (uint32_t l = 0; l < L; l++) {
         const uint32_t wid = st.get_wid(l);
         all_found &= wid != NONE;
@@ -377,7 +412,11 @@ __device__ void exact_find(const DevIndex &ix, uint64_t xh, uint32_t L, const S 
         if (f == 0) return;
         if (f == fp) {
             const uint4 *e = reinterpret_cast<const uint4 *>(ix.exact + slot);
+#ifdef TM_NT_EXACT
+            uint4 a = ld4_cold(e), b = ld4_cold(e + 1), c = ld4_cold(e + 2), d = ld4_cold(e + 3);
+#else
             uint4 a = e[0], b = e[1], c = e[2], d = e[3];
+#endif
             pin(a); pin(b); pin(c); pin(d);
             if (a.x == (uint32_t)xh && a.y == (uint32_t)(xh >> 32) && a.z == L) {
                 bool eq = true;
@@ -393,7 +432,7 @@ __device__ void exact_find(const DevIndex &ix, uint64_t xh, uint32_t L, const S 
             }
         }
         slot = (slot + 1) & ix.xmask;
-        f = ix.xfp[slot];
+        f = ld_xfp(ix.xfp + slot);
     }
 }
 
@@ -451,7 +490,11 @@ __device__ bool dfs(const DevIndex &ix, uint32_t L, bool dollar, S &st, EM &em) 
                     const uint32_t m = bloom_bit(n2, n3, child_bit(h));
                     if (m & 1u) {
                         uint32_t slo, shi;
+#ifdef TM_NT_CTAB
+                        lit = ctab_find(ix, n2.x, n2.y, w, h, slo, shi, l >= TM_NT_CTAB);
+#else
                         lit = ctab_find(ix, n2.x, n2.y, w, h, slo, shi);
+#endif
 #ifdef TM_STUDY_MISS   // study: probes that find no child, by level (1), or at l >= 3 / found but dead (2)
                         if constexpr (S::deferred) {
                             const bool absent = lit == NONE;
@@ -481,6 +524,9 @@ __device__ bool dfs(const DevIndex &ix, uint32_t L, bool dollar, S &st, EM &em) 
             }
             if (!droot && !em(n0.y, n0.z)) return false;
             uint32_t plus = droot ? NONE : n0.x;
+#ifdef TM_STUDY_MAXL   // study: the walk cut below level TM_STUDY_MAXL (wrong results; requests per level)
+            if (l + 1 >= TM_STUDY_MAXL) { plus = NONE; lit = NONE; }
+#endif
 #ifndef TM_NO_PSUM
             if (plus != NONE && !child_alive(n1.z, n1.w, l + 1, L, l + 1 < L ? st.get_wid(l + 1) : NONE,
                                              l + 2 < L ? st.get_wid(l + 2) : NONE))
@@ -588,7 +634,7 @@ __device__ int match_topic(const DevIndex &ix, const uint8_t *blob, uint64_t beg
 #ifdef TM_STUDY_NOEXACT
     allf = false;   // timing study only: the exact-table probe skipped (wrong results)
 #endif
-    const uint32_t xf = allf ? ix.xfp[xslot] : 0;
+    const uint32_t xf = allf ? ld_xfp(ix.xfp + xslot) : 0;
     if (!dfs(ix, L, dollar, st, em)) return RC_OK;
     if (allf) {
         uint32_t xoff, xcnt;
@@ -688,14 +734,14 @@ __device__ __forceinline__ uint32_t wave_excl_scan32(uint32_t v, uint32_t &total
 
 // block-wide exclusive scan of one value per thread (blockDim = 256)
 __device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t &total, uint64_t *s_w) {
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
     uint64_t inc = wave_incl_scan(v);
     if (lane == 63) s_w[wv] = inc;
     __syncthreads();
     uint64_t pre = 0;
     total = 0;
 #pragma unroll
-    for (int i = 0; i < 4; i++) { if (i < wv) pre += s_w[i]; total += s_w[i]; }
+    for (int i = 0; i < 4; i++) { if (i < wv) pre += s_w[i]; if (i < nw) total += s_w[i]; }
     __syncthreads();
     return pre + inc - v;
 }
@@ -707,8 +753,11 @@ __device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t &total,
 // the walk writes each tile's hit total into ws.blk, k_scan_top turns those
 // into tile prefixes, k_emit finishes the scan inside its tile.
 
-constexpr int WALK_BLOCK = 256;
-static_assert(WALK_BLOCK == TILE, "walk blocks are scan tiles");
+#ifndef TM_WALK_BLOCK
+#define TM_WALK_BLOCK 64    // 64 vs 256: walk 0.2553 vs 0.2631 ms per 1M C3 topics (a block waits for its slowest lane)
+#endif
+constexpr int WALK_BLOCK = TM_WALK_BLOCK;   // a walk block is a scan tile, or a part of one (tile totals added atomically)
+static_assert(TILE % WALK_BLOCK == 0, "walk blocks tile the scan tiles");
 
 template <int MODE>
 __global__ __launch_bounds__(WALK_BLOCK, 8) void k_walk_fast(DevIndex ix, Workspace ws, uint64_t n,
@@ -721,6 +770,9 @@ __global__ __launch_bounds__(WALK_BLOCK, 8) void k_walk_fast(DevIndex ix, Worksp
     uint32_t hits = 0;
     if (t < n) {
         LdsStore<FAST_L> st{s_wid + threadIdx.x, s_pend + threadIdx.x, s_len + threadIdx.x, WALK_BLOCK, 0};
+#ifdef TM_STUDY_HOSTWIDS
+        if (ix.study_wids && ix.study_n == n) st.study_t = t;
+#endif
         int rc = run_topic<MODE>(ix, ws, n, blob, offs, t, st, o, &hits);
         if (rc == RC_DEEP) {
             hits = 0;   // counted by k_walk_tail (atomically added to this tile)
@@ -731,7 +783,11 @@ __global__ __launch_bounds__(WALK_BLOCK, 8) void k_walk_fast(DevIndex ix, Worksp
     if (MODE == MODE_COUNT) {
         uint64_t total;
         block_excl_scan(hits, total, s_w);
-        if (threadIdx.x == 0) ws.blk[blockIdx.x] = total;
+        if (WALK_BLOCK == TILE) {
+            if (threadIdx.x == 0) ws.blk[blockIdx.x] = total;
+        } else if (threadIdx.x == 0 && total) {
+            atomicAdd((unsigned long long *)&ws.blk[((uint64_t)blockIdx.x * WALK_BLOCK) / TILE], (unsigned long long)total);
+        }
     }
 }
 
@@ -1463,7 +1519,8 @@ hipError_t launch_match_phase1(const DevIndex &ix, const Workspace &ws, uint64_t
             hipLaunchKernelGGL((k_walk_wave<MODE_COUNT, WAVE_W>), dim3(blocks_for(n, WV_TOPICS_PER_BLOCK)),
                                dim3(WV_BLOCK), 0, s, ix, ws, n, bytes, offs, o);
         else
-            hipLaunchKernelGGL(k_walk_fast<MODE_COUNT>, dim3(nb), dim3(WALK_BLOCK), 0, s, ix, ws, n, bytes, offs, o);
+            hipLaunchKernelGGL(k_walk_fast<MODE_COUNT>, dim3(blocks_for(n, WALK_BLOCK)), dim3(WALK_BLOCK), 0, s, ix, ws,
+                               n, bytes, offs, o);
         if (ev_walk1 && (e = hipEventRecord(ev_walk1, s)) != hipSuccess) return e;
         // small batches: the tail kernel's last block also scans the (few) tile totals
         hipLaunchKernelGGL(k_walk_tail<MODE_COUNT>, dim3(TAIL_GRID), dim3(MID_BLOCK), 0, s, ix, ws, n, bytes, offs, o,
