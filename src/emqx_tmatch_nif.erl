@@ -1,0 +1,36 @@
+%% emqx_tmatch_nif -- Erlang stubs of c_src/emqx_tmatch_nif.c (libtmatch.so,
+%% include/tmatch.h).  Not built in this image (no OTP, SURVEY.md 8c).
+-module(emqx_tmatch_nif).
+
+-export([new/1, apply/2, match_batch/3, first_batch/2, stats/1]).
+-on_load(init/0).
+
+-type ref() :: reference().
+-type u32() :: 0..4294967295.
+%% Op: 1 insert, 0 delete.  Kind: 0 binary key, 1 word list, 2 the word list [].
+-type delta() :: {0 | 1, binary(), u32(), 0 | 1 | 2}.
+-type order() :: traversal | sorted | unique.
+-export_type([ref/0, u32/0, delta/0, order/0]).
+
+init() ->
+    Priv =
+        case code:priv_dir(emqx) of
+            {error, _} -> "priv";
+            Dir -> Dir
+        end,
+    erlang:load_nif(filename:join(Priv, "emqx_tmatch_nif"), 0).
+
+-spec new(integer()) -> {ok, ref()} | {error, integer()}.
+new(_Device) -> erlang:nif_error(nif_not_loaded).
+
+-spec apply(ref(), [delta()]) -> ok | {error, integer()}.
+apply(_Ref, _Deltas) -> erlang:nif_error(nif_not_loaded).
+
+-spec match_batch(ref(), [binary()], order()) -> [[u32()] | badarg | system_limit] | {error, integer()}.
+match_batch(_Ref, _Topics, _Order) -> erlang:nif_error(nif_not_loaded).
+
+-spec first_batch(ref(), [binary()]) -> [{ok, u32()} | false | badarg | system_limit] | {error, integer()}.
+first_batch(_Ref, _Topics) -> erlang:nif_error(nif_not_loaded).
+
+-spec stats(ref()) -> #{atom() => non_neg_integer()}.
+stats(_Ref) -> erlang:nif_error(nif_not_loaded).

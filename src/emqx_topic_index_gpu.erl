@@ -1,0 +1,311 @@
+%% emqx_topic_index_gpu -- emqx_topic_index (apps/emqx/src/emqx_topic_index.erl)
+%% with matching on the MI355X through emqx_tmatch_nif (c_src/emqx_tmatch_nif.c).
+%%
+%% Same API, argument meaning and results as the reference module; a table is
+%% a #gtab{} instead of a bare ETS table:
+%%   tab   the reference's ETS ordered_set {Key, Record} -- still the source of
+%%         truth (get_record/2, matches_filter/3 and every write go to it first)
+%%   kids  ETS set interning each key to a u32 the device stores:
+%%         {{k, Key}, Kid} and {{v, Kid}, Key}, plus {next, N}
+%%   free  ETS set of released kids, reused by later inserts
+%%   ref   the device index (emqx_tmatch_nif resource)
+%%
+%% Reads (match/2, matches/3, matches_batch/3) run lock-free from any process,
+%% as on the reference's read_concurrency table (:41-48); the NIF runs each
+%% call on its own HIP stream.  Writes (insert/4, delete/3) come from the
+%% table's owner process, as every reference caller does (emqx_rule_engine.erl:537,
+%% emqx_schema_validation_registry.erl:263, emqx_bridge_mqtt_ingress.erl:203,
+%% the router syncer): a write updates ETS, then ships one delta; a batch of
+%% writes (router syncer, boot from an existing table, node-down cleanup) ships
+%% as one NIF call.
+%%
+%% Not built in this image (no OTP, SURVEY.md 8c); the Python mirror
+%% emqx_amd/topic_index.py implements the same rules and is what the tests run.
+-module(emqx_topic_index_gpu).
+
+-export([new/0, new/1, attach/2]).
+-export([insert/4, delete/3, apply_batch/2]).
+-export([match/2, matches/3, matches_batch/3, matches_filter/3]).
+-export([make_key/2, get_id/1, get_topic/1, get_record/2]).
+-export([table_event/2, cleanup/2, stats/1]).
+
+-record(gtab, {tab, kids, free, ref}).
+-type gtab() :: #gtab{}.
+-export_type([gtab/0]).
+
+-define(INSERT, 1).
+-define(DELETE, 0).
+-define(KIND_BINARY, 0).
+-define(KIND_WORDS, 1).
+-define(KIND_EMPTY, 2).
+
+%%--------------------------------------------------------------------
+%% Tables
+
+-spec new() -> gtab().
+new() ->
+    new([public, {read_concurrency, true}]).
+
+%% new/1 (emqx_topic_index.erl:44-48): the ETS table with the caller's options
+%% plus its device mirror on the default device.
+-spec new(list()) -> gtab().
+new(Options) ->
+    mirror(ets:new(emqx_topic_index, [ordered_set | Options])).
+
+%% Put a device mirror next to an existing index table (e.g. the router's
+%% ?ROUTE_TAB_FILTERS, emqx_router.erl:148-160) and load its keys in batches:
+%% boot from ETS.  Records are taken to be the last element of each row.
+-spec attach(ets:table(), pos_integer()) -> gtab().
+attach(Tab, BatchSize) ->
+    G = mirror(Tab),
+    ets:safe_fixtable(Tab, true),
+    try
+        boot(G, ets:first(Tab), BatchSize, [])
+    after
+        ets:safe_fixtable(Tab, false)
+    end,
+    G.
+
+mirror(Tab) ->
+    {ok, Ref} = emqx_tmatch_nif:new(-1),
+    Kids = ets:new(emqx_topic_index_kids, [set, public, {read_concurrency, true}]),
+    true = ets:insert(Kids, {next, 0}),
+    Free = ets:new(emqx_topic_index_free, [set, public]),
+    #gtab{tab = Tab, kids = Kids, free = Free, ref = Ref}.
+
+boot(G, '$end_of_table', _N, Acc) ->
+    flush(G, Acc);
+boot(G, Key, N, Acc) when length(Acc) >= N ->
+    ok = flush(G, Acc),
+    boot(G, Key, N, []);
+boot(G, Key, N, Acc) ->
+    boot(G, ets:next(G#gtab.tab, Key), N, intern_delta(G, Key, Acc)).
+
+%%--------------------------------------------------------------------
+%% Writes
+
+%% insert/4 (emqx_topic_index.erl:53-56)
+-spec insert(emqx_types:topic() | emqx_trie_search:words(), _ID, _Record, gtab()) -> true.
+insert(Filter, ID, Record, G = #gtab{tab = Tab}) ->
+    Key = make_key(Filter, ID),
+    true = ets:insert(Tab, {Key, Record}),
+    ok = flush(G, intern_delta(G, Key, [])),
+    true.
+
+%% delete/3 (emqx_topic_index.erl:60-62): deleting a missing entry is not an error.
+-spec delete(emqx_types:topic() | emqx_trie_search:words(), _ID, gtab()) -> true.
+delete(Filter, ID, G = #gtab{tab = Tab}) ->
+    Key = make_key(Filter, ID),
+    true = ets:delete(Tab, Key),
+    ok = flush(G, release_delta(G, Key, [])),
+    true.
+
+%% A batch of {insert, Filter, ID, Record} | {delete, Filter, ID} as ONE device
+%% delta call (one router-syncer batch, emqx_router_syncer.erl:297-356).
+-spec apply_batch([tuple()], gtab()) -> ok.
+apply_batch(Ops, G = #gtab{tab = Tab}) ->
+    Deltas = lists:foldl(
+        fun
+            ({insert, F, ID, Rec}, Acc) ->
+                Key = make_key(F, ID),
+                true = ets:insert(Tab, {Key, Rec}),
+                intern_delta(G, Key, Acc);
+            ({delete, F, ID}, Acc) ->
+                Key = make_key(F, ID),
+                true = ets:delete(Tab, Key),
+                release_delta(G, Key, Acc)
+        end,
+        [],
+        Ops
+    ),
+    flush(G, Deltas).
+
+%% Replicated writes reach a core or replicant node as mnesia table events,
+%% bypassing emqx_router (SURVEY.md 3.2); the router helper subscribes with
+%% mnesia:subscribe({table, ?ROUTE_TAB_FILTERS, detailed}) and hands each
+%% event here (after mnesia has applied it to the ETS table itself).
+-spec table_event(tuple(), gtab()) -> ok.
+table_event({write, _Tab, Rec, _Old, _Tid}, G) ->
+    flush(G, intern_delta(G, element(2, Rec), []));
+table_event({delete, _Tab, {_, Key}, _Old, _Tid}, G) ->
+    flush(G, release_delta(G, Key, []));
+table_event({delete_object, _Tab, Rec, _Old, _Tid}, G) ->
+    flush(G, release_delta(G, element(2, Rec), []));
+table_event(_, _G) ->
+    ok.
+
+%% Node-down cleanup (emqx_router.erl:535-578, emqx_router_helper.erl:147-162):
+%% every key whose ID satisfies Pred is deleted, and the whole set of deletes
+%% ships as one device batch instead of one write per route.
+-spec cleanup(fun((_ID) -> boolean()), gtab()) -> ok.
+cleanup(Pred, G = #gtab{tab = Tab}) ->
+    Doomed = ets:foldl(
+        fun(Row, Acc) ->
+            Key = element(1, Row),
+            case Pred(get_id(Key)) of
+                true -> [Key | Acc];
+                false -> Acc
+            end
+        end,
+        [],
+        Tab
+    ),
+    Deltas = lists:foldl(
+        fun(Key, Acc) ->
+            true = ets:delete(Tab, Key),
+            release_delta(G, Key, Acc)
+        end,
+        [],
+        Doomed
+    ),
+    flush(G, Deltas).
+
+%% Key -> a device delta (prepended to Acc), interning the key on first sight.
+intern_delta(G = #gtab{kids = Kids}, Key, Acc) ->
+    case ets:lookup(Kids, {k, Key}) of
+        [_] ->
+            Acc;
+        [] ->
+            Kid = take_kid(G),
+            true = ets:insert(Kids, [{{k, Key}, Kid}, {{v, Kid}, Key}]),
+            add_delta(?INSERT, Key, Kid, Acc)
+    end.
+
+release_delta(#gtab{kids = Kids, free = Free}, Key, Acc) ->
+    case ets:take(Kids, {k, Key}) of
+        [{_, Kid}] ->
+            true = ets:delete(Kids, {v, Kid}),
+            true = ets:insert(Free, {Kid}),
+            add_delta(?DELETE, Key, Kid, Acc);
+        [] ->
+            Acc
+    end.
+
+take_kid(#gtab{kids = Kids, free = Free}) ->
+    case ets:first(Free) of
+        '$end_of_table' ->
+            ets:update_counter(Kids, next, 1) - 1;
+        Kid ->
+            true = ets:delete(Free, Kid),
+            Kid
+    end.
+
+%% make_key/2 forms (emqx_trie_search.erl:115-128) as the C ABI encodes them
+%% (include/tmatch.h "Keys").  A word list holding a binary word equal to
+%% "+"/"#" or containing '/' can never equal a topic's levels; it stays in ETS
+%% only (as does '#' not last, which the library itself keeps as never-matching).
+add_delta(Op, {Bin, _}, Kid, Acc) when is_binary(Bin) ->
+    [{Op, Bin, Kid, ?KIND_BINARY} | Acc];
+add_delta(Op, {[], _}, Kid, Acc) ->
+    [{Op, <<>>, Kid, ?KIND_EMPTY} | Acc];
+add_delta(Op, {Words, _}, Kid, Acc) when is_list(Words) ->
+    case lists:all(fun matchable_word/1, Words) of
+        true -> [{Op, join(Words), Kid, ?KIND_WORDS} | Acc];
+        false -> Acc
+    end.
+
+matchable_word('+') -> true;
+matchable_word('#') -> true;
+matchable_word(<<"+">>) -> false;
+matchable_word(<<"#">>) -> false;
+matchable_word(W) when is_binary(W) -> binary:match(W, <<"/">>) =:= nomatch.
+
+join(Words) ->
+    iolist_to_binary(lists:join($/, [word_bin(W) || W <- Words])).
+
+word_bin('+') -> <<"+">>;
+word_bin('#') -> <<"#">>;
+word_bin(W) -> W.
+
+%% Deltas were accumulated by prepending: ship them in the order they were made.
+flush(_G, []) ->
+    ok;
+flush(#gtab{ref = Ref}, Deltas) ->
+    ok = emqx_tmatch_nif:apply(Ref, lists:reverse(Deltas)).
+
+%%--------------------------------------------------------------------
+%% Reads
+
+%% match/2 (emqx_topic_index.erl:70-72): the first key in traversal order.
+-spec match(emqx_types:topic(), gtab()) -> emqx_trie_search:key(_) | false.
+match(Topic, G) ->
+    case matches_batch([Topic], G, [traversal]) of
+        [[K | _]] -> K;
+        [[]] -> false
+    end.
+
+%% matches/3 (emqx_topic_index.erl:76-78).
+-spec matches(emqx_types:topic(), gtab(), emqx_trie_search:opts()) -> [emqx_trie_search:key(_)].
+matches(Topic, G, Opts) ->
+    [Res] = matches_batch([Topic], G, Opts),
+    Res.
+
+%% matches/3 over a broker micro-batch (emqx_broker.erl:293-298) in one device
+%% call.  A topic with a '+'/'#' level fails only its own slot: with the
+%% option return_errors the slot holds {error, badarg}; without it the call
+%% raises badarg as the reference's single-topic call does (:374-375).
+-spec matches_batch([emqx_types:topic()], gtab(), list()) -> [[emqx_trie_search:key(_)] | {error, atom()}].
+matches_batch(Topics, #gtab{ref = Ref, kids = Kids}, Opts) ->
+    Rows = emqx_tmatch_nif:match_batch(Ref, Topics, traversal),
+    is_list(Rows) orelse error({tmatch, Rows}),
+    ReturnErrors = proplists:get_bool(return_errors, Opts),
+    [finish(Row, Kids, Opts, ReturnErrors) || Row <- Rows].
+
+finish(Err, _Kids, _Opts, true) when is_atom(Err) ->
+    {error, Err};
+finish(Err, _Kids, _Opts, false) when is_atom(Err) ->
+    error(Err);
+finish(Row, Kids, Opts, _) ->
+    Keys = traversal([kid_key(Kids, V) || V <- Row]),
+    case proplists:get_bool(traversal, Opts) of
+        true ->
+            Keys;
+        false ->
+            case proplists:get_bool(unique, Opts) of
+                %% match_add/2 on a map: a later key of the same ID wins (:350-352)
+                true -> maps:values(lists:foldl(fun(K = {_, ID}, M) -> M#{ID => K} end, #{}, Keys));
+                %% match_add/2 on a list prepends (:353-354)
+                false -> lists:reverse(Keys)
+            end
+    end.
+
+kid_key(Kids, V) ->
+    [{_, Key}] = ets:lookup(Kids, {v, V}),
+    Key.
+
+%% The device orders keys of different filters by term order; keys of ONE
+%% filter (several IDs) come by u32.  The reference's ordered_set orders them by
+%% {ID}: sort each run of equal filters (lists:sort on keys of one filter is
+%% exactly the ID's term order).
+traversal([]) ->
+    [];
+traversal([K = {F, _} | Rest]) ->
+    {Same, Tail} = lists:splitwith(fun({F2, _}) -> F2 =:= F end, Rest),
+    case Same of
+        [] -> [K | traversal(Tail)];
+        _ -> lists:sort([K | Same]) ++ traversal(Tail)
+    end.
+
+%% matches_filter/3 (emqx_topic_index.erl:82-84): a control-plane call whose
+%% result depends on the ordered walk's early stop (DESIGN.md 6b); it walks the
+%% ETS table exactly as the reference does.
+-spec matches_filter(emqx_types:topic(), gtab(), emqx_trie_search:opts()) -> [emqx_trie_search:key(_)].
+matches_filter(TopicFilter, #gtab{tab = Tab}, Opts) ->
+    emqx_topic_index:matches_filter(TopicFilter, Tab, Opts).
+
+make_key(TopicOrFilter, ID) ->
+    emqx_trie_search:make_key(TopicOrFilter, ID).
+
+get_id(Key) ->
+    emqx_trie_search:get_id(Key).
+
+get_topic(Key) ->
+    emqx_trie_search:get_topic(Key).
+
+-spec get_record(emqx_trie_search:key(_), gtab()) -> [_Record].
+get_record(K, #gtab{tab = Tab}) ->
+    emqx_topic_index:get_record(K, Tab).
+
+-spec stats(gtab()) -> map().
+stats(#gtab{ref = Ref}) ->
+    emqx_tmatch_nif:stats(Ref).
