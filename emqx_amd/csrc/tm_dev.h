@@ -23,7 +23,10 @@ struct DevIndex {
 #endif
 };
 
-constexpr int FAST_L = 8;        // levels handled by the main walk kernel (LDS frontier)
+#ifndef TM_FAST_L
+#define TM_FAST_L 8
+#endif
+constexpr int FAST_L = TM_FAST_L; // levels handled by the main walk kernel (LDS frontier)
 constexpr int MID_L = 32;        // levels handled by the list kernels with an LDS frontier
 constexpr int MAX_LEVELS = 65536;// MQTT topics are <= 65535 bytes
 #ifndef RCAP_N

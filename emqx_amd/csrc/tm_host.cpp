@@ -116,14 +116,19 @@ struct tm_index {
     std::condition_variable cv;      // a host lane was released
     int device = 0;
 
-    Mirror<VocabEntry> vocab; uint64_t vcount = 0;
-    Mirror<uint8_t> wpool;
+    // vocab: live words, next fresh wid, per-wid reference count (trie edges +
+    // exact-key levels) and slot, wids freed for reuse; a word nothing refers
+    // to any more is erased, so churn through unique levels (client ids, UUIDs)
+    // does not grow the tables
+    Mirror<VocabEntry> vocab; uint64_t vcount = 0; uint32_t wid_next = 0;
+    std::vector<uint32_t> wref, wslot, free_wids;
+    Mirror<uint8_t> wpool; uint64_t wpool_dead = 0;   // bytes of erased long words (compacted later)
     Mirror<Node> nodes; std::vector<NodeAux> aux; std::vector<uint32_t> free_nodes; uint64_t live_nodes = 0;
     Mirror<CSlot> ctab; std::vector<uint32_t> free_ctab[33]; uint64_t nlinks = 0, ntables = 0;
     Mirror<uint32_t> vals; std::vector<uint32_t> free_blocks[33];
     Mirror<ExactEntry> exact; std::vector<uint32_t> xcap, xroff; uint64_t xcount = 0;
     Mirror<uint16_t> xfp;   // exact-table fingerprints, slot for slot (0 = empty)
-    Mirror<uint32_t> wseq;
+    Mirror<uint32_t> wseq; uint64_t wseq_dead = 0;   // words of erased long exact keys
 
     std::unordered_set<std::string> dead;
     uint64_t n_wild = 0, n_exact = 0;
@@ -230,22 +235,30 @@ void vocab_bytes(tm_index *ix, const VocabEntry &e, std::string &out) {
 #ifndef TM_VOCAB_LOAD_SHIFT
 #define TM_VOCAB_LOAD_SHIFT 2
 #endif
+uint64_t vocab_entry_hash(tm_index *ix, const VocabEntry &e) {
+    std::string w;
+    vocab_bytes(ix, e, w);
+    return word_hash(reinterpret_cast<const uint8_t *>(w.data()), (uint32_t)w.size());
+}
+
+void vocab_rehash(tm_index *ix, uint64_t cap) {
+    std::vector<VocabEntry> nt(cap, empty_vocab());
+    const uint32_t mask = (uint32_t)nt.size() - 1;
+    for (const VocabEntry &e : ix->vocab.h) {
+        if (e.wid == NONE) continue;
+        const uint64_t h = vocab_entry_hash(ix, e);
+        for (uint32_t s = (uint32_t)h & mask;; s = (s + 1) & mask)
+            if (nt[s].wid == NONE) { nt[s] = e; ix->wslot[e.wid] = s; break; }
+    }
+    ix->vocab.h.swap(nt);
+    ix->vocab.dirty.set_all();
+}
+
 void vocab_grow(tm_index *ix, uint64_t need) {
     // load <= 1/4: the walk's deferred probes resolve on the first slot
     // almost always (one round trip per topic for all its levels)
     if ((need << TM_VOCAB_LOAD_SHIFT) <= ix->vocab.h.size()) return;
-    std::vector<VocabEntry> nt(pow2_at_least(need << TM_VOCAB_LOAD_SHIFT), empty_vocab());
-    const uint32_t mask = (uint32_t)nt.size() - 1;
-    std::string w;
-    for (const VocabEntry &e : ix->vocab.h) {
-        if (e.wid == NONE) continue;
-        vocab_bytes(ix, e, w);
-        const uint64_t h = word_hash(reinterpret_cast<const uint8_t *>(w.data()), (uint32_t)w.size());
-        for (uint32_t s = (uint32_t)h & mask;; s = (s + 1) & mask)
-            if (nt[s].wid == NONE) { nt[s] = e; break; }
-    }
-    ix->vocab.h.swap(nt);
-    ix->vocab.dirty.set_all();
+    vocab_rehash(ix, pow2_at_least(need << TM_VOCAB_LOAD_SHIFT));
 }
 
 uint32_t vocab_intern(tm_index *ix, const uint8_t *p, uint32_t n) {
@@ -255,7 +268,12 @@ uint32_t vocab_intern(tm_index *ix, const uint8_t *p, uint32_t n) {
     VocabEntry e = empty_vocab();
     const uint64_t h = word_hash(p, n);
     e.tag = vocab_tag(h, n);
-    e.wid = (uint32_t)ix->vcount;
+    if (!ix->free_wids.empty()) { e.wid = ix->free_wids.back(); ix->free_wids.pop_back(); }
+    else {
+        e.wid = ix->wid_next++;
+        ix->wref.push_back(0);
+        ix->wslot.push_back(NONE);
+    }
     if (n <= VINL) {
         pack8(p, n, e.b0, e.b1);
     } else {
@@ -268,9 +286,34 @@ uint32_t vocab_intern(tm_index *ix, const uint8_t *p, uint32_t n) {
     }
     const uint32_t mask = (uint32_t)ix->vocab.h.size() - 1;
     for (uint32_t s = (uint32_t)h & mask;; s = (s + 1) & mask)
-        if (ix->vocab.h[s].wid == NONE) { ix->vocab.h[s] = e; ix->vocab.touch(s); break; }
+        if (ix->vocab.h[s].wid == NONE) { ix->vocab.h[s] = e; ix->vocab.touch(s); ix->wslot[e.wid] = s; break; }
     ix->vcount++;
     return e.wid;
+}
+
+// the last trie edge / exact key using word `wid` is gone: erase it
+// (backward-shift deletion, as ctab_erase) and free its wid and wpool bytes
+void vocab_erase(tm_index *ix, uint32_t wid) {
+    auto &t = ix->vocab.h;
+    const uint32_t mask = (uint32_t)t.size() - 1;
+    uint32_t i = ix->wslot[wid];
+    if (t[i].wid != wid) return;   // never: wslot tracks every move
+    if ((t[i].tag & 0xFF) > VINL) ix->wpool_dead += (t[i].b1 + 3) & ~3u;
+    for (uint32_t j = (i + 1) & mask; t[j].wid != NONE; j = (j + 1) & mask) {
+        const uint32_t k = (uint32_t)vocab_entry_hash(ix, t[j]) & mask;
+        const bool stays = (i <= j) ? (i < k && k <= j) : (i < k || k <= j);
+        if (!stays) { t[i] = t[j]; ix->wslot[t[i].wid] = i; ix->vocab.touch(i); i = j; }
+    }
+    t[i] = empty_vocab();
+    ix->vocab.touch(i);
+    ix->wslot[wid] = NONE;
+    ix->free_wids.push_back(wid);
+    ix->vcount--;
+}
+
+void word_ref(tm_index *ix, uint32_t wid) { ix->wref[wid]++; }
+void word_unref(tm_index *ix, uint32_t wid) {
+    if (--ix->wref[wid] == 0) vocab_erase(ix, wid);
 }
 
 // ------------------------------------------------- private child tables
@@ -396,6 +439,7 @@ uint32_t node_new(tm_index *ix, uint32_t parent, uint32_t wid, bool is_plus) {
     NodeAux a; a.parent = parent; a.wid = wid; a.is_plus = is_plus;
     ix->aux[id] = a;
     ix->live_nodes++;
+    if (!is_plus && wid != NONE) word_ref(ix, wid);   // the edge parent -> id uses the word
     return id;
 }
 
@@ -559,6 +603,7 @@ void node_prune(tm_index *ix, uint32_t id) {
             summary_refresh(ix, a.parent);
         } else {
             child_remove(ix, a.parent, a.wid);
+            word_unref(ix, a.wid);
         }
         ix->free_nodes.push_back(id);
         ix->live_nodes--;
@@ -591,9 +636,13 @@ uint32_t exact_find_slot(tm_index *ix, uint64_t h, const std::vector<uint32_t> &
     }
 }
 
+void exact_rehash(tm_index *ix, uint32_t ncap);
 void exact_grow(tm_index *ix, uint64_t need) {
     if (need * 2 <= ix->exact.h.size()) return;
-    const uint32_t ncap = pow2_at_least(need * 2);
+    exact_rehash(ix, pow2_at_least(need * 2));
+}
+
+void exact_rehash(tm_index *ix, uint32_t ncap) {
     std::vector<ExactEntry> nt(ncap, empty_exact());
     std::vector<uint32_t> nc(ncap, 0), nr(ncap, 0);
     std::vector<uint16_t> nf(ncap, 0);
@@ -615,6 +664,13 @@ void exact_grow(tm_index *ix, uint64_t need) {
 void exact_erase_slot(tm_index *ix, uint32_t i) {
     auto &t = ix->exact.h;
     const uint32_t mask = (uint32_t)t.size() - 1;
+    {   // the key's levels no longer use their words
+        const uint32_t nl = t[i].nlev;
+        const uint32_t *ws = nl <= XINL ? t[i].wids : ix->wseq.h.data() + t[i].seq_off;
+        std::vector<uint32_t> used(ws, ws + nl);
+        if (nl > XINL) ix->wseq_dead += nl;
+        for (uint32_t w : used) word_unref(ix, w);
+    }
     for (uint32_t j = (i + 1) & mask; t[j].nlev != NONE; j = (j + 1) & mask) {
         uint32_t k = t[j].h_lo & mask;
         bool stays = (i <= j) ? (i < k && k <= j) : (i < k || k <= j);
@@ -631,6 +687,47 @@ void exact_erase_slot(tm_index *ix, uint32_t i) {
     ix->exact.touch(i);
     ix->xfp.touch(i);
     ix->xcount--;
+}
+
+// Reclaim what deletes left behind (end of every delta batch): long words'
+// bytes in wpool and long exact keys' wid runs in wseq are compacted once half
+// of the pool is dead; the vocab and exact tables shrink back when their load
+// falls below 1/16 and 1/8 (they double at 1/4 and 1/2).  Each of these
+// rewrites whole tables, so the next sync re-uploads them.
+void reclaim(tm_index *ix) {
+    if (ix->wpool_dead * 2 > ix->wpool.h.size() && ix->wpool.h.size() >= (64u << 10)) {
+        std::vector<uint8_t> np;
+        np.reserve(ix->wpool.h.size() - ix->wpool_dead);
+        for (VocabEntry &e : ix->vocab.h) {
+            if (e.wid == NONE || (e.tag & 0xFF) <= VINL) continue;
+            const uint64_t off = np.size(), padded = (e.b1 + 3) & ~3u;
+            np.insert(np.end(), ix->wpool.h.begin() + e.b0, ix->wpool.h.begin() + e.b0 + padded);
+            e.b0 = (uint32_t)off;
+        }
+        ix->wpool.h.swap(np);
+        ix->wpool_dead = 0;
+        ix->wpool.dirty.set_all();
+        ix->vocab.dirty.set_all();
+    }
+    if (ix->wseq_dead * 2 > ix->wseq.h.size() && ix->wseq.h.size() >= (16u << 10)) {
+        std::vector<uint32_t> nq;
+        nq.reserve(ix->wseq.h.size() - ix->wseq_dead);
+        for (ExactEntry &e : ix->exact.h) {
+            if (e.nlev == NONE || e.nlev <= XINL) continue;
+            const uint64_t off = nq.size();
+            nq.insert(nq.end(), ix->wseq.h.begin() + e.seq_off, ix->wseq.h.begin() + e.seq_off + e.nlev);
+            e.seq_off = (uint32_t)off;
+        }
+        ix->wseq.h.swap(nq);
+        ix->wseq_dead = 0;
+        ix->wseq.dirty.set_all();
+        ix->exact.dirty.set_all();
+    }
+    const uint64_t vmin = 1024;
+    if (ix->vocab.h.size() > vmin && (ix->vcount << (TM_VOCAB_LOAD_SHIFT + 2)) < ix->vocab.h.size())
+        vocab_rehash(ix, std::max<uint64_t>(vmin, pow2_at_least(std::max<uint64_t>(ix->vcount, 1) << TM_VOCAB_LOAD_SHIFT)));
+    if (ix->exact.h.size() > 1024 && ix->xcount * 8 < ix->exact.h.size())
+        exact_rehash(ix, std::max<uint32_t>(1024, pow2_at_least(ix->xcount * 2)));
 }
 
 // --------------------------------------------------------------- key ops
@@ -702,6 +799,7 @@ void key_op(tm_index *ix, bool ins, const uint8_t *f, uint32_t len, uint32_t v, 
             ix->xfp.h[s] = exact_fp(h);
             ix->xfp.touch(s);
             ix->xcount++;
+            for (uint32_t wd : wids) word_ref(ix, wd);
         }
         ExactEntry &e = ix->exact.h[s];
         if (ins) { if (run_op(ix, true, ix->xroff[s], ix->xcap[s], e.val_off, e.val_cnt, v)) ix->n_exact++; }
@@ -1118,6 +1216,7 @@ int tm_apply_deltas(tm_index *ix, uint64_t n, const uint8_t *ops, const uint8_t 
         for (uint64_t i = 0; i < n; i++)
             key_op(ix, ops[i] == TM_OP_INSERT, fb + fo[i], (uint32_t)(fo[i + 1] - fo[i]), values[i],
                    key_flags ? key_flags[i] : 0, w, wids);
+        reclaim(ix);
     } catch (const std::bad_alloc &) {
         return fail(ix, TM_ENOMEM, "tm_apply_deltas: out of host memory");
     }

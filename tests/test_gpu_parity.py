@@ -341,6 +341,40 @@ def test_stats_and_idempotence(torch_dev):
     assert hit.tolist() == [0, 0, 0]
 
 
+def test_churn_through_unique_words_stays_bounded(torch_dev):
+    """Subscription churn with unique levels (client ids, UUIDs): words nothing
+    refers to any more are erased from the vocab, long words' bytes and long
+    exact keys' wid runs are compacted, the tables shrink back -- n_words and
+    device_bytes stay bounded over rounds (advisor finding), and every round's
+    matches equal the oracle's (reused wids must never alias a live word)."""
+    r = random.Random(11)
+    ix = gpu_index()
+    o = Oracle()
+    base = items_of([b"fleet/+/status", b"fleet/#", b"+/+/+/+/+/+/+/+/+/+/+/+"], [1, 2, 3])
+    ix.apply(np.ones(len(base), np.uint8), base.blob, base.offs, base.vals)
+    o.apply(np.ones(len(base), np.uint8), base.blob, base.offs, base.vals)
+    words0 = ix.stats()["n_words"]
+    seen = []
+    for rnd in range(6):
+        uid = [b"client-%016x-%08x" % (r.getrandbits(64), i) for i in range(4000)]
+        keys = ([b"fleet/%s/+" % u for u in uid[:1500]] + [b"fleet/%s/status" % u for u in uid[1500:2500]] +
+                [b"/".join([b"deep", u] + [b"l%d" % k for k in range(11)]) for u in uid[2500:]])
+        d = items_of(keys, [10 + i for i in range(len(keys))])
+        ix.apply(np.ones(len(d), np.uint8), d.blob, d.offs, d.vals)
+        o.apply(np.ones(len(d), np.uint8), d.blob, d.offs, d.vals)
+        probe = items_of([b"fleet/%s/status" % u for u in uid[::97]] + [k for k in keys[2500::131]] +
+                         [b"fleet/%s/x" % u for u in uid[:40]] + [b"fleet/nobody/status"])
+        assert_same(ix, o, probe)
+        ix.apply(np.zeros(len(d), np.uint8), d.blob, d.offs, d.vals)
+        o.apply(np.zeros(len(d), np.uint8), d.blob, d.offs, d.vals)
+        assert_same(ix, o, probe)
+        st = ix.stats()
+        assert st["n_words"] == words0, (rnd, st["n_words"], words0)
+        assert st["n_keys"] == 3
+        seen.append(st["device_bytes"])
+    assert max(seen[2:]) <= seen[1], seen   # no growth once the first rounds sized the tables
+
+
 def test_c3_scale_properties(torch_dev):
     """2M filters, 1M topics: exact CSR vs the oracle on a 20k-topic sample, plus
     size-independent properties over the whole batch."""

@@ -23,7 +23,7 @@ def main(d, batch=1_000_000, batches=8):
             if not os.path.isfile(f):
                 continue
             for r in csv.DictReader(open(f)):
-                if "k_walk_fast" in r["Kernel_Name"] and int(r["Grid_Size"]) == grid:
+                if "k_walk_fast" in r["Kernel_Name"] and batch <= int(r["Grid_Size"]) <= grid:
                     vals[r["Counter_Name"]][int(r["Dispatch_Id"])] = float(r["Counter_Value"])
         c = {k: sum(sorted(x.items())[-batches:][i][1] for i in range(min(batches, len(x)))) / min(batches, len(x))
              for k, x in vals.items() if x}
