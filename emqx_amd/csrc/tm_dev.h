@@ -17,6 +17,11 @@ struct DevIndex {
     const ExactEntry *exact; uint32_t xmask;
     const uint16_t *xfp;
     const uint32_t *wseq;
+    // A walk needs a topic's level words only down to the trie's depth (no node
+    // deeper than `depth` exists), unless a binary key of the topic's length
+    // exists (xlen_mask bit L for L < 64, L <= xlen_max beyond): need_levels().
+    uint32_t depth, xlen_max;
+    uint64_t xlen_mask;
 #ifdef TM_STUDY_HOSTWIDS
     const uint32_t *study_wids;   // study build: level-major wids of the batch, looked up on the host
     uint64_t study_n;
@@ -27,6 +32,12 @@ struct DevIndex {
 #define TM_FAST_L 8
 #endif
 constexpr int FAST_L = TM_FAST_L; // levels handled by the main walk kernel (LDS frontier)
+
+// levels of an L-level topic whose words a walk must resolve (see DevIndex)
+__host__ __device__ __forceinline__ uint32_t need_levels(const DevIndex &ix, uint32_t L) {
+    const bool exact = L < 64 ? ((ix.xlen_mask >> L) & 1u) != 0 : L <= ix.xlen_max;
+    return exact || L < ix.depth ? L : ix.depth;
+}
 constexpr int MID_L = 32;        // levels handled by the list kernels with an LDS frontier
 constexpr int MAX_LEVELS = 65536;// MQTT topics are <= 65535 bytes
 #ifndef RCAP_N
@@ -78,7 +89,9 @@ hipError_t launch_sort_segments(const Workspace &ws, uint64_t n, const uint64_t 
 // out[0 .. min(hit[n], cap)) = src[...] (device -> device or mapped host memory)
 hipError_t launch_copy_values(const uint64_t *hit_offs, uint64_t n, const uint32_t *src, uint32_t *dst, uint64_t cap,
                               hipStream_t s);
-// scatter patch: dst[i] (absolute device address of a u32) = val[i]
-hipError_t launch_patch(const uint64_t *d_addr, const uint32_t *d_val, uint64_t n, hipStream_t s);
+// delta upload: run i copies runs[i].n u32 words from data + runs[i].src to
+// the device address runs[i].dst
+struct PatchRun { uint64_t dst; uint32_t src, n; };
+hipError_t launch_patch(const PatchRun *d_runs, const uint32_t *d_data, uint64_t n_runs, hipStream_t s);
 
 }  // namespace tmx

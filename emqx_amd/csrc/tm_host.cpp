@@ -66,6 +66,7 @@ struct Mirror {
 
 struct NodeAux {
     uint32_t parent = NONE, wid = NONE, hash_cap = 0, exact_cap = 0;
+    uint32_t depth = 0;                       // words on the path from the root
     uint32_t hash_roff = 0, exact_roff = 0;   // the runs' offsets in vals (the line may hold an inline value)
     uint8_t is_plus = 0;
 };
@@ -103,8 +104,8 @@ struct Lane {
 // the patch PATCH_RING before it, not for the one just enqueued.
 constexpr int PATCH_RING = 4;
 struct PatchSlot {
-    uint64_t *pin_addr = nullptr; uint32_t *pin_val = nullptr; uint64_t pin_cap = 0;
-    uint64_t *dev_addr = nullptr; uint32_t *dev_val = nullptr; uint64_t dev_cap = 0;
+    uint8_t *pin = nullptr; uint64_t pin_cap = 0;   // [PatchRun x runs | u32 data]
+    uint8_t *dev = nullptr; uint64_t dev_cap = 0;
     hipEvent_t done = nullptr; bool pending = false;
 };
 
@@ -129,6 +130,10 @@ struct tm_index {
     Mirror<ExactEntry> exact; std::vector<uint32_t> xcap, xroff; uint64_t xcount = 0;
     Mirror<uint16_t> xfp;   // exact-table fingerprints, slot for slot (0 = empty)
     Mirror<uint32_t> wseq; uint64_t wseq_dead = 0;   // words of erased long exact keys
+
+    // levels a walk must resolve (DevIndex::depth / xlen_*): live nodes per
+    // depth and live exact keys per level count
+    std::vector<uint64_t> depth_cnt, xlen_cnt;
 
     std::unordered_set<std::string> dead;
     uint64_t n_wild = 0, n_exact = 0;
@@ -437,8 +442,11 @@ uint32_t node_new(tm_index *ix, uint32_t parent, uint32_t wid, bool is_plus) {
     ix->nodes.h[id] = nd;
     ix->nodes.touch(id);
     NodeAux a; a.parent = parent; a.wid = wid; a.is_plus = is_plus;
+    a.depth = parent == NONE ? 0 : ix->aux[parent].depth + 1;
     ix->aux[id] = a;
     ix->live_nodes++;
+    if (ix->depth_cnt.size() <= a.depth) ix->depth_cnt.resize(a.depth + 1, 0);
+    ix->depth_cnt[a.depth]++;
     if (!is_plus && wid != NONE) word_ref(ix, wid);   // the edge parent -> id uses the word
     return id;
 }
@@ -607,6 +615,7 @@ void node_prune(tm_index *ix, uint32_t id) {
         }
         ix->free_nodes.push_back(id);
         ix->live_nodes--;
+        ix->depth_cnt[a.depth]--;
         id = a.parent;
     }
 }
@@ -670,6 +679,7 @@ void exact_erase_slot(tm_index *ix, uint32_t i) {
         std::vector<uint32_t> used(ws, ws + nl);
         if (nl > XINL) ix->wseq_dead += nl;
         for (uint32_t w : used) word_unref(ix, w);
+        ix->xlen_cnt[nl]--;
     }
     for (uint32_t j = (i + 1) & mask; t[j].nlev != NONE; j = (j + 1) & mask) {
         uint32_t k = t[j].h_lo & mask;
@@ -800,6 +810,8 @@ void key_op(tm_index *ix, bool ins, const uint8_t *f, uint32_t len, uint32_t v, 
             ix->xfp.touch(s);
             ix->xcount++;
             for (uint32_t wd : wids) word_ref(ix, wd);
+            if (ix->xlen_cnt.size() <= wids.size()) ix->xlen_cnt.resize(wids.size() + 1, 0);
+            ix->xlen_cnt[wids.size()]++;
         }
         ExactEntry &e = ix->exact.h[s];
         if (ins) { if (run_op(ix, true, ix->xroff[s], ix->xcap[s], e.val_off, e.val_cnt, v)) ix->n_exact++; }
@@ -880,8 +892,12 @@ int upload_full(tm_index *ix, Mirror<T> &m) {
     return TM_OK;
 }
 
+// One patch run: `n` (<= PATCH_RUN) consecutive 4-byte words copied from the
+// patch data at `src` to the device address `dst` (tm_dev.h PatchRun).
+constexpr uint32_t PATCH_RUN = 64;
+
 template <class T>
-int collect(tm_index *ix, Mirror<T> &m, std::vector<uint64_t> &addr, std::vector<uint32_t> &val) {
+int collect(tm_index *ix, Mirror<T> &m, std::vector<PatchRun> &runs, std::vector<uint32_t> &data) {
     if (m.h.size() > m.dcap) m.dirty.set_all();
     if (!m.dirty.all) {
         uint64_t words = 0;
@@ -889,16 +905,19 @@ int collect(tm_index *ix, Mirror<T> &m, std::vector<uint64_t> &addr, std::vector
         if (words * 4 > m.bytes() / 2) m.dirty.set_all();   // cheaper to ship the table
     }
     if (m.dirty.all) return upload_full(ix, m);
-    const uint32_t *src = reinterpret_cast<const uint32_t *>(m.h.data());
+    const uint8_t *src = reinterpret_cast<const uint8_t *>(m.h.data());
     const uint64_t base = reinterpret_cast<uint64_t>(m.d);
     const uint64_t limit = (m.bytes() + 3) / 4;
-    for (auto &r : m.dirty.r)
-        for (uint64_t i = r.first; i < r.second && i < limit; i++) {
-            addr.push_back(base + 4 * i);
-            uint32_t v = 0;
-            memcpy(&v, reinterpret_cast<const uint8_t *>(src) + 4 * i, std::min<uint64_t>(4, m.bytes() - 4 * i));
-            val.push_back(v);
+    for (auto &r : m.dirty.r) {
+        const uint64_t hi = std::min<uint64_t>(r.second, limit);
+        for (uint64_t lo = r.first; lo < hi; lo += PATCH_RUN) {
+            const uint32_t n = (uint32_t)std::min<uint64_t>(PATCH_RUN, hi - lo);
+            const uint64_t at = data.size();
+            runs.push_back(PatchRun{base + 4 * lo, (uint32_t)at, n});
+            data.resize(at + n, 0);
+            memcpy(data.data() + at, src + 4 * lo, std::min<uint64_t>(4ull * n, m.bytes() - 4 * lo));
         }
+    }
     m.dirty.clear();
     return TM_OK;
 }
@@ -917,50 +936,48 @@ int batch_done(tm_index *ix, Lane &ln) {
 // deltas applied before it (C5), whichever stream either ran on.
 int sync_locked(tm_index *ix, hipStream_t s) {
     HIPCHK(ix, hipSetDevice(ix->device));
-    std::vector<uint64_t> addr;
-    std::vector<uint32_t> val;
+    std::vector<PatchRun> runs;
+    std::vector<uint32_t> data;
     int rc;
-    if ((rc = collect(ix, ix->vocab, addr, val))) return rc;
-    if ((rc = collect(ix, ix->wpool, addr, val))) return rc;
-    if ((rc = collect(ix, ix->nodes, addr, val))) return rc;
-    if ((rc = collect(ix, ix->ctab, addr, val))) return rc;
-    if ((rc = collect(ix, ix->vals, addr, val))) return rc;
-    if ((rc = collect(ix, ix->exact, addr, val))) return rc;
-    if ((rc = collect(ix, ix->xfp, addr, val))) return rc;
-    if ((rc = collect(ix, ix->wseq, addr, val))) return rc;
-    const uint64_t n = addr.size();
-    if (!n) return TM_OK;
+    if ((rc = collect(ix, ix->vocab, runs, data))) return rc;
+    if ((rc = collect(ix, ix->wpool, runs, data))) return rc;
+    if ((rc = collect(ix, ix->nodes, runs, data))) return rc;
+    if ((rc = collect(ix, ix->ctab, runs, data))) return rc;
+    if ((rc = collect(ix, ix->vals, runs, data))) return rc;
+    if ((rc = collect(ix, ix->exact, runs, data))) return rc;
+    if ((rc = collect(ix, ix->xfp, runs, data))) return rc;
+    if ((rc = collect(ix, ix->wseq, runs, data))) return rc;
+    const uint64_t nr = runs.size(), nw = data.size();
+    if (!nr) return TM_OK;
+    // staging: [runs | data] in one pinned buffer, one H2D copy, one kernel
+    const uint64_t bytes = nr * sizeof(PatchRun) + nw * 4;
     PatchSlot &p = ix->patch[ix->patch_head % PATCH_RING];
     ix->patch_head++;
     if (p.pending) { HIPCHK(ix, hipEventSynchronize(p.done)); p.pending = false; }
-    if (n > p.pin_cap) {
-        if (p.pin_addr) HIPCHK(ix, hipHostFree(p.pin_addr));
-        if (p.pin_val) HIPCHK(ix, hipHostFree(p.pin_val));
-        p.pin_addr = nullptr; p.pin_val = nullptr;
-        p.pin_cap = n + n / 2 + 1024;
-        HIPCHK(ix, hipHostMalloc(&p.pin_addr, p.pin_cap * 8, hipHostMallocDefault));
-        HIPCHK(ix, hipHostMalloc(&p.pin_val, p.pin_cap * 4, hipHostMallocDefault));
+    if (bytes > p.pin_cap) {
+        if (p.pin) HIPCHK(ix, hipHostFree(p.pin));
+        p.pin = nullptr;
+        p.pin_cap = bytes + bytes / 2 + 4096;
+        HIPCHK(ix, hipHostMalloc(&p.pin, p.pin_cap, hipHostMallocDefault));
     }
-    if (n > p.dev_cap) {   // the slot's previous patch has completed (p.done above)
-        if (p.dev_addr) HIPCHK(ix, hipFree(p.dev_addr));
-        if (p.dev_val) HIPCHK(ix, hipFree(p.dev_val));
-        p.dev_addr = nullptr; p.dev_val = nullptr;
-        p.dev_cap = n + n / 2 + 1024;
-        HIPCHK(ix, hipMalloc(&p.dev_addr, p.dev_cap * 8));
-        HIPCHK(ix, hipMalloc(&p.dev_val, p.dev_cap * 4));
+    if (bytes > p.dev_cap) {   // the slot's previous patch has completed (p.done above)
+        if (p.dev) HIPCHK(ix, hipFree(p.dev));
+        p.dev = nullptr;
+        p.dev_cap = bytes + bytes / 2 + 4096;
+        HIPCHK(ix, hipMalloc(&p.dev, p.dev_cap));
     }
-    memcpy(p.pin_addr, addr.data(), n * 8);
-    memcpy(p.pin_val, val.data(), n * 4);
+    memcpy(p.pin, runs.data(), nr * sizeof(PatchRun));
+    memcpy(p.pin + nr * sizeof(PatchRun), data.data(), nw * 4);
     for (auto &l : ix->lanes)
         if (l->used && l->s != s) HIPCHK(ix, hipStreamWaitEvent(s, l->done, 0));
     if (ix->last_patch) HIPCHK(ix, hipStreamWaitEvent(s, ix->last_patch, 0));
-    HIPCHK(ix, hipMemcpyAsync(p.dev_addr, p.pin_addr, n * 8, hipMemcpyHostToDevice, s));
-    HIPCHK(ix, hipMemcpyAsync(p.dev_val, p.pin_val, n * 4, hipMemcpyHostToDevice, s));
-    HIPCHK(ix, launch_patch(p.dev_addr, p.dev_val, n, s));
+    HIPCHK(ix, hipMemcpyAsync(p.dev, p.pin, bytes, hipMemcpyHostToDevice, s));
+    HIPCHK(ix, launch_patch(reinterpret_cast<const PatchRun *>(p.dev),
+                            reinterpret_cast<const uint32_t *>(p.dev + nr * sizeof(PatchRun)), nr, s));
     HIPCHK(ix, hipEventRecord(p.done, s));
     p.pending = true;
     ix->last_patch = p.done;
-    ix->patch_bytes += n * 4;
+    ix->patch_bytes += nw * 4;
     ix->uploads++;
     return TM_OK;
 }
@@ -975,6 +992,15 @@ DevIndex dev_view(tm_index *ix) {
     d.exact = ix->exact.d; d.xmask = (uint32_t)ix->exact.h.size() - 1;
     d.xfp = ix->xfp.d;
     d.wseq = ix->wseq.d;
+    // levels a walk must resolve: the deepest live node's depth (no node below
+    // it has children), all of a topic's levels when a binary key has its length
+    auto &dc = ix->depth_cnt, &xc = ix->xlen_cnt;
+    while (dc.size() > 1 && dc.back() == 0) dc.pop_back();
+    while (!xc.empty() && xc.back() == 0) xc.pop_back();
+    d.depth = dc.empty() ? 0 : (uint32_t)dc.size() - 1;
+    d.xlen_max = xc.empty() ? 0 : (uint32_t)xc.size() - 1;
+    d.xlen_mask = 0;
+    for (size_t k = 0; k < xc.size() && k < 64; k++) if (xc[k]) d.xlen_mask |= 1ull << k;
 #ifdef TM_STUDY_HOSTWIDS
     d.study_wids = ix->study_wids; d.study_n = ix->study_n;
 #endif
@@ -1188,10 +1214,8 @@ int tm_destroy(tm_index *ix) {
     for (void *p : bufs) if (p) (void)hipFree(p);
     for (auto &l : ix->lanes) free_lane(*l);
     for (auto &p : ix->patch) {
-        void *dv[] = {p.dev_addr, p.dev_val};
-        for (void *q : dv) if (q) (void)hipFree(q);
-        void *pins[] = {p.pin_addr, p.pin_val};
-        for (void *q : pins) if (q) (void)hipHostFree(q);
+        if (p.dev) (void)hipFree(p.dev);
+        if (p.pin) (void)hipHostFree(p.pin);
         if (p.done) (void)hipEventDestroy(p.done);
     }
     for (auto &b : ix->pinned) (void)hipHostFree(b.host);

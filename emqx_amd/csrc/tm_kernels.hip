@@ -220,10 +220,37 @@ enum { RC_OK = 0, RC_BADARG = 1, RC_DEEP = 2 };
 
 // levels whose vocab probes are in flight together (6 covers MQTT's usual
 // topic depths in one round trip and keeps k_walk_fast within 64 VGPRs, i.e.
-// 8 waves per SIMD)
+// 8 waves per SIMD -- a budget small code changes can tip: check the
+// -Rpass-analysis=kernel-resource-usage remark after every change)
 #ifndef VGROUP
 #define VGROUP 6
 #endif
+
+// '/' bytes in [p, end), p 16-byte aligned: four 16-byte loads in flight per
+// round trip, bytes compared a word at a time
+__device__ __noinline__ uint32_t count_slashes(const uint8_t *blob, uint64_t p, uint64_t end) {
+    uint32_t n = 0;
+    for (; p < end; p += 64) {
+        uint4 v[4];
+#pragma unroll
+        for (int c = 0; c < 4; c++) v[c] = p + 16 * c < end ? ld4_once(blob + p + 16 * c) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            const uint32_t w[4] = {v[c].x, v[c].y, v[c].z, v[c].w};
+            const uint64_t q = p + 16 * c;
+            const int k1 = q >= end ? 0 : end - q < 16 ? (int)(end - q) : 16;   // bytes of the chunk inside [p, end)
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const uint32_t x = w[j] ^ 0x2F2F2F2Fu;   // '/' bytes -> 0
+                uint32_t nz = (((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;   // bit 7 set: byte != '/'
+                const int valid = k1 - 4 * j;
+                if (valid < 4) nz |= valid <= 0 ? 0x80808080u : 0x80808080u << (8 * valid);
+                n += 4 - __popc(nz);
+            }
+        }
+    }
+    return n;
+}
 
 // topic_words/1 (emqx_trie_search.erl:369-378): split on '/', a level that is
 // exactly '+' or '#' is badarg; level words are resolved to wids.  Also
@@ -252,18 +279,36 @@ __device__ int tokenize(const DevIndex &ix, const uint8_t *blob, uint64_t beg, u
         // '$', long words) run per level afterwards, so the divergent work at a
         // word end is three LDS stores.  A word longer than VINL bytes parks
         // its length and start instead (len8 = 255), resolved below.
+        // The main walk's store (FAST_L levels) takes topics that fit it whole;
+        // deeper ones go to the tail lists.  The tail's store (MID_L levels)
+        // resolves only the levels a walk can use: down to the trie's depth,
+        // or all of them when a binary key of L levels exists -- so a 64-level
+        // topic against a 6-level trie stays on the LDS path (need_levels).
+        constexpr bool NEED = S::maxl > FAST_L;
         uint32_t lev = 0, len = 0, b0 = 0, b1 = 0;
         uint64_t ws = beg;
+        bool bad = false;   // tail store: a level past the stored ones is exactly '+' or '#'
         auto park = [&]() {
             if (lev < S::maxl) {
                 if (len <= VINL) st.put_word(lev, b0, b1, len);
                 else st.put_word(lev, len, (uint32_t)(ws - beg), 255);
+            } else if constexpr (NEED) {
+                bad |= len == 1 && ((b0 & 0xFFu) == '+' || (b0 & 0xFFu) == '#');
             }
             lev++;
         };
         uint32_t ci = 0;
-        for (uint64_t p = p0; p < end; p += 16, ci++) {
-            const uint4 v = ci == 0 ? c0 : ci == 1 ? c1 : ld4_once(blob + p);
+        uint64_t p = p0;
+        uint4 ra = c0, rb = c1;   // tail store: chunks loaded two ahead (deep topics run hundreds of bytes)
+        for (; p < end; p += 16, ci++) {
+            if (!NEED && lev > S::maxl) break;   // deeper than the main walk's store
+            uint4 v;
+            if constexpr (NEED) {
+                v = ra; ra = rb;
+                rb = p + 32 < end ? ld4_once(blob + p + 32) : z;
+            } else {
+                v = ci == 0 ? c0 : ci == 1 ? c1 : ld4_once(blob + p);
+            }
             const uint32_t k0 = p < beg ? (uint32_t)(beg - p) : 0;
             const uint32_t k1 = end - p < 16 ? (uint32_t)(end - p) : 16;
 #pragma unroll
@@ -282,16 +327,28 @@ __device__ int tokenize(const DevIndex &ix, const uint8_t *blob, uint64_t beg, u
                 }
             }
         }
+        if (!NEED && p < end) {   // left early: count the rest (the tail list's choice), hand the topic over
+            L = lev + 1 + count_slashes(blob, p, end);
+            return RC_DEEP;
+        }
         park();
-        if (lev > S::maxl) return RC_DEEP;
+        if (lev > (NEED ? MAX_LEVELS : S::maxl)) { L = lev; return RC_DEEP; }   // (> MAX_LEVELS: the global walk flags it)
         L = lev;
-        for (uint32_t l = 0; l < L; l++) {   // a level exactly '+' or '#' is badarg (:374-375)
+        // a level exactly '+' or '#' is badarg (:374-375), at any depth: the
+        // stored levels here, the rest during the scan (park)
+        for (uint32_t l = 0; l < L && l < S::maxl; l++) {
             const uint32_t n = st.word_len(l), c = st.word_b0(l) & 0xFFu;
-            if (n == 1 && (c == '+' || c == '#')) return RC_BADARG;
+            bad |= n == 1 && (c == '+' || c == '#');
+        }
+        if (bad) return RC_BADARG;
+        if constexpr (NEED) {
+            const uint32_t Lw = need_levels(ix, L);
+            if (Lw + (Lw < L ? 2 : 0) > S::maxl) return RC_DEEP;
+            L |= Lw << 24;   // Lw rides in L's top byte until the probes are done
         }
         // base_init (:160-163): the first level starts with '$'
         dollar = st.word_len(0) == 255 ? blob[beg] == '$' : st.word_len(0) >= 1 && (st.word_b0(0) & 0xFFu) == '$';
-        for (uint32_t l = 0; l < L; l++) {
+        for (uint32_t l = 0; l < (S::maxl > FAST_L ? L >> 24 : L); l++) {
             if (st.word_len(l) != 255) continue;
             WordAcc w; w.reset(beg + st.word_b1(l)); w.len = st.word_b0(l);
             st.set_wid(l, vocab_find(ix, w, blob));
@@ -348,14 +405,14 @@ __device__ int tokenize(const DevIndex &ix, const uint8_t *blob, uint64_t beg, u
         // (unused levels read slot 0) and consumes all of them, so no load is
         // left pending on a skipped branch -- the compiler would otherwise drain
         // vmcnt(0) before reusing its registers and serialise the probes.
-        for (uint32_t base = 0; base < L; base += VGROUP) {
+        for (uint32_t base = 0; base < (S::maxl > FAST_L ? L >> 24 : L); base += VGROUP) {
             uint4 e[VGROUP];
             uint32_t tg[VGROUP];
             bool use[VGROUP];
 #pragma unroll
             for (uint32_t k = 0; k < VGROUP; k++) {
                 const uint32_t l = base + k;
-                use[k] = l < L && !((longmask >> l) & 1);
+                use[k] = l < (S::maxl > FAST_L ? L >> 24 : L) && !((longmask >> l) & 1);
                 const uint32_t ls = use[k] ? l : 0;
                 const uint32_t len = st.word_len(ls);
                 const uint64_t h = word_hash_short(st.word_b0(ls), st.word_b1(ls), len);
@@ -383,6 +440,19 @@ __device__ int tokenize(const DevIndex &ix, const uint8_t *blob, uint64_t beg, u
 #ifdef TM_STUDY_HOSTWIDS
 wids_done:
 #endif
+    if constexpr (S::deferred && S::maxl > FAST_L) {
+      const uint32_t Lw = L >> 24;
+      L &= 0xFFFFFFu;
+      if (Lw < L) {
+        // No binary key has L levels, and no trie node below level Lw has
+        // children: the walk reads levels Lw and Lw + 1 at most (a node's
+        // word and its summaries' look-ahead), which never match anything.
+        st.set_wid(Lw, NONE);
+        st.set_wid(Lw + 1, NONE);
+        all_found = false;
+        return RC_OK;
+      }
+    }
     for (uint32_t l = 0; l < L; l++) {
         const uint32_t wid = st.get_wid(l);
         all_found &= wid != NONE;
@@ -392,10 +462,10 @@ wids_done:
     return RC_OK;
 }
 
-__device__ uint32_t count_levels(const uint8_t *blob, uint64_t beg, uint64_t end) {
-    uint32_t n = 1;
-    for (uint64_t q = beg; q < end; q++) n += blob[q] == '/';
-    return n;
+// the tail list of a topic of nl levels the main walk could not take: the LDS
+// frontier (MID_L levels) if the levels it must resolve fit, else global scratch
+__device__ __forceinline__ int tail_list(const DevIndex &ix, uint32_t nl) {
+    return nl <= MAX_LEVELS && need_levels(ix, nl) <= MID_L ? L_MID : L_DEEP;
 }
 
 // match_topics/4 (emqx_trie_search.erl:381-389): binary keys equal to the topic.
@@ -621,9 +691,11 @@ struct FirstEmit {          // match/2: stop at the first hit
 };
 
 template <class S, class EM>
-__device__ int match_topic(const DevIndex &ix, const uint8_t *blob, uint64_t beg, uint64_t end, S &st, EM &em) {
+__device__ int match_topic(const DevIndex &ix, const uint8_t *blob, uint64_t beg, uint64_t end, S &st, EM &em,
+                            uint32_t *levels = nullptr) {
     uint32_t L = 0; bool dollar, allf; uint64_t xh;
     int rc = tokenize(ix, blob, beg, end, st, L, dollar, xh, allf);
+    if (levels) *levels = L;   // RC_DEEP: the topic's level count (the tail list's choice)
     if (rc) return rc;
 #ifdef TM_STUDY_TOKONLY   // timing study: tokenise + vocab only (wrong results)
     if (xh == 42) em(0, 1);   // keep the tokeniser's outputs live
@@ -652,6 +724,24 @@ struct Outs {               // per-mode outputs
     uint8_t *first_found;
 };
 
+// Wave-aggregated push (every lane of the wave calls it; k = -1: nothing to
+// push): one atomic per list and wave.  Per-lane atomics on one counter
+// serialise at the L2 -- a batch with 10 % deep topics spent 1 ms of its walk
+// on them.
+__device__ __forceinline__ void list_push_wave(const Workspace &ws, uint64_t n, int k, uint32_t t) {
+    const uint32_t lane = threadIdx.x & 63;
+    for (int j = 0; j < L_COUNT; j++) {
+        if (!__ballot(k >= 0)) break;   // (nothing to push: the common case, one ballot)
+        const uint64_t m = __ballot(k == j);
+        if (!m) continue;
+        const uint32_t leader = (uint32_t)__ffsll((unsigned long long)m) - 1;
+        uint32_t base = 0;
+        if (lane == leader) base = atomicAdd(&ws.list_n[j], (uint32_t)__popcll(m));
+        base = (uint32_t)__shfl((int)base, (int)leader, 64);
+        if (k == j) ws.lists[(uint64_t)j * n + base + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = t;
+    }
+}
+
 __device__ __forceinline__ void list_push(const Workspace &ws, uint64_t n, int k, uint32_t t) {
     uint32_t i = atomicAdd(&ws.list_n[k], 1u);
     ws.lists[(uint64_t)k * n + i] = t;
@@ -662,16 +752,18 @@ __device__ __forceinline__ void list_push(const Workspace &ws, uint64_t n, int k
 // receives the topic's hit count (count mode).
 template <int MODE, class S>
 __device__ int run_topic(const DevIndex &ix, const Workspace &ws, uint64_t n, const uint8_t *blob,
-                         const uint64_t *offs, uint64_t t, S &st, const Outs &o, uint32_t *hits) {
+                         const uint64_t *offs, uint64_t t, S &st, const Outs &o, uint32_t *hits,
+                         int *ovf = nullptr) {
     const uint64_t beg = offs[t], end = offs[t + 1];
     if (MODE == MODE_COUNT) {
         RangeEmit em;
         em.cnt = 0; em.nr = 0;
-        int rc = match_topic(ix, blob, beg, end, st, em);
+        uint32_t levels;
+        int rc = match_topic(ix, blob, beg, end, st, em, &levels);
         // more levels than the global scratch holds (> 65536: longer than any
         // MQTT topic, emqx_mqtt.hrl:44): flagged err 2, no hits
         const bool toolong = rc == RC_DEEP && S::maxl == MAX_LEVELS;
-        if (rc == RC_DEEP && !toolong) return rc;
+        if (rc == RC_DEEP && !toolong) { *hits = levels; return rc; }   // the caller lists it by depth
         if (rc != RC_OK) { em.cnt = 0; em.nr = 0; }
         // per-topic outputs, read once by k_emit: non-temporal (bench +1.6 %)
         __builtin_nontemporal_store(em.cnt, ws.cnt + t);
@@ -693,14 +785,18 @@ __device__ int run_topic(const DevIndex &ix, const Workspace &ws, uint64_t n, co
 #else
         __builtin_nontemporal_store((uint8_t)(rc == RC_BADARG ? 1 : (toolong ? 2 : 0)), o.err + t);
 #endif
-        if (em.nr > RCAP) list_push(ws, n, S::maxl <= MID_L ? L_OVF_MID : L_OVF_DEEP, (uint32_t)t);
+        if (em.nr > RCAP) {   // re-walked by k_rewalk_tail (ovf: the caller pushes it)
+            const int k = S::maxl <= MID_L ? L_OVF_MID : L_OVF_DEEP;
+            if (ovf) *ovf = k; else list_push(ws, n, k, (uint32_t)t);
+        }
         *hits = em.cnt;
         return rc;
     } else {
         FirstEmit em{ix.vals, 0, false};
-        int rc = match_topic(ix, blob, beg, end, st, em);
+        uint32_t levels;
+        int rc = match_topic(ix, blob, beg, end, st, em, &levels);
         const bool toolong = rc == RC_DEEP && S::maxl == MAX_LEVELS;
-        if (rc == RC_DEEP && !toolong) return rc;
+        if (rc == RC_DEEP && !toolong) { *hits = levels; return rc; }
         o.first_val[t] = toolong ? 0 : em.v;
         o.first_found[t] = rc == RC_BADARG ? 2 : (toolong ? 3 : (em.found ? 1 : 0));
         *hits = 0;
@@ -768,18 +864,21 @@ __global__ __launch_bounds__(WALK_BLOCK, 8) void k_walk_fast(DevIndex ix, Worksp
     __shared__ uint64_t s_w[4];
     const uint64_t t = (uint64_t)blockIdx.x * WALK_BLOCK + threadIdx.x;
     uint32_t hits = 0;
+    int deep = -1, ovf = -1;   // tail lists this topic goes to
     if (t < n) {
         LdsStore<FAST_L> st{s_wid + threadIdx.x, s_pend + threadIdx.x, s_len + threadIdx.x, WALK_BLOCK, 0};
 #ifdef TM_STUDY_HOSTWIDS
         if (ix.study_wids && ix.study_n == n) st.study_t = t;
 #endif
-        int rc = run_topic<MODE>(ix, ws, n, blob, offs, t, st, o, &hits);
-        if (rc == RC_DEEP) {
+        int rc = run_topic<MODE>(ix, ws, n, blob, offs, t, st, o, &hits, &ovf);
+        if (rc == RC_DEEP) {   // hits = the topic's level count
+            deep = tail_list(ix, hits);
             hits = 0;   // counted by k_walk_tail (atomically added to this tile)
-            uint32_t nl = count_levels(blob, offs[t], offs[t + 1]);
-            list_push(ws, n, nl <= MID_L ? L_MID : L_DEEP, (uint32_t)t);
         }
     }
+    static_assert(WALK_BLOCK % 64 == 0, "whole waves");
+    list_push_wave(ws, n, deep, (uint32_t)t);
+    list_push_wave(ws, n, ovf, (uint32_t)t);
     if (MODE == MODE_COUNT) {
         uint64_t total;
         block_excl_scan(hits, total, s_w);
@@ -869,8 +968,7 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_wave(DevIndex ix, Workspace w
     wave_sync();
     auto to_lists = [&]() {
         if (gl == 0) {
-            const uint32_t nl = count_levels(blob, beg, end);
-            list_push(ws, n, nl <= MID_L ? L_MID : L_DEEP, (uint32_t)t);
+            list_push(ws, n, tail_list(ix, L), (uint32_t)t);
         }
     };
     if (L > MAXL) { to_lists(); return; }
@@ -1006,7 +1104,7 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_wave(DevIndex ix, Workspace w
 }
 
 constexpr int MID_BLOCK = 64;
-constexpr int MID_GRID = 256;                         // LDS-frontier blocks of the tail kernels
+constexpr int MID_GRID = 512;                         // LDS-frontier blocks of the tail kernels
 constexpr int TAIL_GRID = MID_GRID + DEEP_LANES / 64; // + global-scratch blocks
 
 // last block of a grid (atomic ticket) resets the list counters for the next batch
@@ -1274,9 +1372,13 @@ __global__ __launch_bounds__(EMIT_BLOCK) void k_emit(DevIndex ix, Workspace ws, 
     }
 }
 
-__global__ void k_patch(const uint64_t *addr, const uint32_t *val, uint64_t n) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) *reinterpret_cast<uint32_t *>(addr[i]) = val[i];
+__global__ void k_patch(const PatchRun *runs, const uint32_t *data, uint64_t n) {
+    const uint64_t i = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4;
+    const uint32_t g = threadIdx.x & 15;
+    if (i >= n) return;
+    const PatchRun r = runs[i];
+    uint32_t *dst = reinterpret_cast<uint32_t *>(r.dst);
+    for (uint32_t k = g; k < r.n; k += 16) dst[k] = data[r.src + k];
 }
 
 // ------------------------------------------------------ filter-sharded merge
@@ -1579,9 +1681,9 @@ hipError_t launch_copy_values(const uint64_t *hit_offs, uint64_t n, const uint32
     return hipGetLastError();
 }
 
-hipError_t launch_patch(const uint64_t *d_addr, const uint32_t *d_val, uint64_t n, hipStream_t s) {
+hipError_t launch_patch(const PatchRun *d_runs, const uint32_t *d_data, uint64_t n, hipStream_t s) {
     if (!n) return hipSuccess;
-    hipLaunchKernelGGL(k_patch, dim3(blocks_for(n, 256)), dim3(256), 0, s, d_addr, d_val, n);
+    hipLaunchKernelGGL(k_patch, dim3(blocks_for(n * 16, 256)), dim3(256), 0, s, d_runs, d_data, n);
     return hipGetLastError();
 }
 

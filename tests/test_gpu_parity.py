@@ -236,6 +236,44 @@ def test_deep_topics_and_overflow(torch_dev):
     assert np.diff(hit.astype(np.int64))[4] > 8      # 'a/b' overflows the RCAP ranges
 
 
+def test_c3deep_reduced_vs_oracle(torch_dev):
+    """C3 filters with 10 % of the topics extended to 33-64 levels (cfg 30):
+    the deep topics resolve only the levels the 6-level trie can use and stay
+    on the main walk; exact CSR vs the oracle."""
+    fs = wl.filters(3, 200_000)
+    ts = wl.topics(30, 200_000, 60_000)
+    assert max(len(t.split(b"/")) for t in ts.items()) > 32
+    assert_same(gpu_index(fs), oracle_of(fs), ts)
+    # with a binary key as deep as some topics, those topics resolve every level
+    extra = items_of([t for t in ts.items() if len(t.split(b"/")) in (40, 64)][:50], [900_000 + i for i in range(50)])
+    both = wl.ItemSet(*_native.pack_strings(fs.items() + extra.items()), np.concatenate([fs.vals, extra.vals]),
+                      np.zeros(len(fs) + len(extra), np.uint8))
+    assert_same(gpu_index(both), oracle_of(both), ts)
+
+
+@pytest.mark.parametrize("batch", [3000, 40_000])   # wave walk + tails / lane walk + tails
+def test_levels_beyond_the_trie(torch_dev, batch):
+    """Topics deeper than every filter: badarg at any depth, '$' first levels,
+    long words past the trie, binary keys of 3, 20 and 70 levels, '#'
+    filters at the trie's bottom -- all against the oracle, in both walks."""
+    r = random.Random(3)
+    words = [b"a", b"b", b"c", b"$x", b"longer-than-eight-bytes", b""]
+    filters = [b"a/+/#", b"+/b", b"a/b/c", b"#", b"+/+/+/#", b"$x/#", b"a/longer-than-eight-bytes/#"]
+    keys20 = b"/".join([b"a"] * 20)
+    keys70 = b"/".join([b"b"] * 70)
+    filters += [keys20, keys70, b"c/c/c"]
+    topics = []
+    for _ in range(batch):
+        L = r.choice([1, 2, 3, 4, 9, 20, 33, 40, 70, 100])
+        ws = [r.choice(words) for _ in range(L)]
+        if r.random() < 0.05:
+            ws[r.randrange(L)] = r.choice([b"+", b"#"])
+        topics.append(b"/".join(ws))
+    topics += [keys20, keys70, keys70 + b"/b", b"/".join([b"a"] * 19), b"c/c/c", b"$x/" + b"/".join([b"a"] * 50)]
+    fs = items_of(filters)
+    assert_same(gpu_index(fs), oracle_of(fs), items_of(topics))
+
+
 def test_maximum_size_topics(torch_dev):
     """Topics at MQTT's 65535-byte maximum (emqx_mqtt.hrl:44): one 65535-byte
     word, 32768 one-byte levels, 65536 empty levels (the walk's scratch depth),
