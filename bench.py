@@ -13,8 +13,9 @@ matches its own batches; there is no data-path collective.
 
 Other modes (not the headline line):
   --config c4   filter-sharded (100M filters split over the ranks, each rank
-                matches the SAME batch against its shard, per-topic hit counts
-                and the hit lists are allgathered over RCCL and merged on the
+                matches the SAME batch against its shard; every rank receives
+                its own slice of the batch from every shard -- all_to_all of
+                u32 counts and padded values over RCCL -- and merges it on the
                 device): strong scaling
   --config c5   churn: every step first applies --deltas subscribe/unsubscribe
                 ops (one router-syncer batch) to the replicated index, then
@@ -48,7 +49,7 @@ CONFIGS = {
     "c2nm": (20, 1_000_000, "1M 'fleet/{id}/sensor/+' + 1k non-matching 'rules/{k}/#' globals"),
     "c3": (3, 10_000_000, "10M mixed-wildcard filters incl. $share groups and '$SYS' exclusion"),
     "c3deep": (30, 10_000_000, "C3 filters; 10% of the topics 33-64 levels deep"),
-    "c4": (4, 100_000_000, "100M mixed filters filter-sharded over the ranks, RCCL allgatherv of hit lists"),
+    "c4": (4, 100_000_000, "100M mixed filters filter-sharded over the ranks, RCCL all_to_all of hit-list slices"),
     "c5": (5, 10_000_000, "churn: 10M mixed filters, subscribe/unsubscribe deltas interleaved with match batches"),
 }
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
@@ -432,7 +433,7 @@ def main():
                        "source": "profiles/r1_gather.md (64-B random requests beyond L2, 256 MiB-2 GiB tables)"}
 
     metric = {"c3": "topic matches/sec at 10M filters"}.get(a.config, f"topic matches/sec ({a.config})")
-    par = (f"filter-sharded x{world} (RCCL allgather of counts + allgatherv of hit lists)" if filter_sharded
+    par = (f"filter-sharded x{world} (RCCL all_to_all of per-slice counts and hit lists, device merge)" if filter_sharded
            else f"topic-sharded x{world} (trie replicated)")
     res = {
         "metric": metric,
