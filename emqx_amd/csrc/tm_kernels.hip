@@ -1361,8 +1361,13 @@ __global__ __launch_bounds__(EMIT_BLOCK) void k_emit(DevIndex ix, Workspace ws, 
         }
     };
     // EMIT_Q quads per iteration, all their value loads issued before any
-    // store (the compiler cannot move a vals load above a store to out)
-    for (uint64_t q = (base >> 2) + lane; q < q1; q += 64 * EMIT_Q) {
+    // store (the compiler cannot move a vals load above a store to out).  The
+    // lanes start at the 128-byte line holding the span's first quad, so every
+    // store instruction covers 8 whole lines instead of 9 partial ones
+    // (tools/store_bench: 16-B- but not 128-B-aligned 1 KiB stores write at
+    // 4.2-4.8 TB/s, aligned ones at 5.2-5.7); lanes before the span store
+    // nothing.
+    for (uint64_t q = ((base >> 2) & ~7ull) + lane; q < q1; q += 64 * EMIT_Q) {
         uint32_t v[EMIT_Q][4];
         bool ok[EMIT_Q][4];
 #pragma unroll
@@ -1384,34 +1389,52 @@ __global__ void k_patch(const PatchRun *runs, const uint32_t *data, uint64_t n) 
 // ------------------------------------------------------ filter-sharded merge
 
 // Filter-sharded mode: `world` shards matched the same n topics
-// against disjoint key sets; their CSR hit lists were allgathered (RCCL) into
+// against disjoint key sets; their CSR hit lists were exchanged (RCCL) into
 // shard_hit [world][n+1] and shard_vals [world][stride].  Topic t's merged list
 // is shard 0's list, then shard 1's, ... -- the union of disjoint key sets, so
 // the same value set as one index holding every key.  Merged offsets are the
 // sums of the shards' offsets (a sum of exclusive prefix sums is the prefix sum
-// of the summed counts): no scan needed.  One thread per (shard, topic), shard
-// major, so neighbouring lanes read neighbouring source runs.
+// of the summed counts): no scan needed.  One wave per MERGE_TOPICS topics; a
+// segment (one shard's list of one topic) is copied by all 64 lanes, so loads
+// and stores are coalesced (one thread per segment walked its own range:
+// C4's 62 values per topic became 62 M scattered requests, 1.6 ms per batch).
+constexpr int MERGE_TOPICS = 16;
+constexpr int MERGE_LDS_WORLD = 16;   // shards whose offsets a wave stages in LDS (more: read in place)
 __global__ __launch_bounds__(256) void k_merge_shards(uint32_t world, uint64_t n, const uint64_t *shard_hit,
                                                       const uint32_t *shard_vals, uint64_t stride,
                                                       uint64_t *out_hit, uint32_t *out, uint64_t cap) {
-    const uint64_t id = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (id >= (uint64_t)world * (n + 1)) return;
-    const uint32_t r = (uint32_t)(id / (n + 1));
-    const uint64_t t = id % (n + 1);
-    uint64_t base = 0, before = 0;
-    for (uint32_t q = 0; q < world; q++) {
-        const uint64_t o = shard_hit[(uint64_t)q * (n + 1) + t];
-        base += o;
-        if (q < r && t < n) before += shard_hit[(uint64_t)q * (n + 1) + t + 1] - o;
+    __shared__ uint64_t s_h[4][MERGE_LDS_WORLD][MERGE_TOPICS + 1];
+    const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint64_t w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint64_t t0 = w * MERGE_TOPICS;
+    if (t0 > n) return;
+    const uint64_t t1 = t0 + MERGE_TOPICS < n ? t0 + MERGE_TOPICS : n;
+    const bool staged = world <= MERGE_LDS_WORLD;
+    // the wave's offsets, every shard at once (one round trip instead of one per topic)
+    if (staged) {
+        for (uint32_t q = 0; q < world; q++)
+            if (lane <= t1 - t0) s_h[wv][q][lane] = shard_hit[(uint64_t)q * (n + 1) + t0 + lane];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
-    if (r == 0) out_hit[t] = base;
-    if (t == n) return;
-    const uint64_t *h = shard_hit + (uint64_t)r * (n + 1);
-    const uint64_t s0 = h[t], s1 = h[t + 1];
-    const uint32_t *src = shard_vals + (uint64_t)r * stride;
-    uint64_t d = base + before;
-    for (uint64_t i = s0; i < s1; i++, d++)
-        if (d < cap) out[d] = src[i];
+    auto H = [&](uint32_t q, uint64_t t) -> uint64_t {
+        return staged ? s_h[wv][q][t - t0] : shard_hit[(uint64_t)q * (n + 1) + t];
+    };
+    for (uint64_t t = t0; t <= t1; t++) {
+        if (t == t1 && t1 != n) break;   // the next wave writes its own first offset
+        uint64_t d = 0;
+        for (uint32_t q = 0; q < world; q++) d += H(q, t);
+        if (lane == 0) out_hit[t] = d;
+        if (t == n) break;
+        for (uint32_t q = 0; q < world; q++) {
+            const uint64_t s0 = H(q, t), len = H(q, t + 1) - s0;
+            const uint32_t *src = shard_vals + (uint64_t)q * stride + s0;
+            for (uint64_t i = lane; i < len; i += 64)
+                if (d + i < cap) out[d + i] = src[i];
+            d += len;
+        }
+    }
 }
 
 // ------------------------------------------------------ sorted hit lists
@@ -1658,7 +1681,7 @@ hipError_t launch_first(const DevIndex &ix, const Workspace &ws, uint64_t n, con
 
 hipError_t launch_merge_shards(uint32_t world, uint64_t n, const uint64_t *shard_hit, const uint32_t *shard_vals,
                                uint64_t stride, uint64_t *out_hit, uint32_t *out, uint64_t cap, hipStream_t s) {
-    const uint64_t threads = (uint64_t)world * (n + 1);
+    const uint64_t threads = (n / MERGE_TOPICS + 1) * 64;   // one wave per MERGE_TOPICS topics (+ the final offset)
     hipLaunchKernelGGL(k_merge_shards, dim3(blocks_for(threads, 256)), dim3(256), 0, s, world, n, shard_hit,
                        shard_vals, stride, out_hit, out, cap);
     return hipGetLastError();

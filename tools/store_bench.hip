@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
 
 #define CHK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); exit(1); } } while (0)
 
@@ -52,6 +53,9 @@ int main(int argc, char **argv) {
     CHK(hipEventCreate(&e0)); CHK(hipEventCreate(&e1));
     printf("mode,blocks,per_wave_KiB,GBps\n");
     const char *names[4] = {"fill", "fill_nt", "copyrun", "copyrun_nt"};
+    // shift: the output starts `shift` bytes into the buffer (16-B aligned but not
+    // 128-B aligned, as k_emit's wave spans are) -- modes 0-3 at shift 0, then
+    // fill_nt at shifts 16 and 64 and per-wave spans of odd quad counts
     for (int mode = 0; mode < 4; mode++) {
         for (uint64_t blocks : {1024ull, 2048ull, 4096ull, 8192ull, 16384ull}) {
             const uint64_t waves = blocks * 4, per_wave = (nq + waves - 1) / waves;
@@ -74,6 +78,26 @@ int main(int argc, char **argv) {
             CHK(hipEventElapsedTime(&ms, e0, e1));
             printf("%s,%lu,%.1f,%.1f\n", names[mode], (unsigned long)blocks, per_wave * 16 / 1024.0,
                    (double)bytes * reps / (ms * 1e-3) / 1e9);
+            fflush(stdout);
+        }
+    }
+    for (uint64_t shift : {16ull, 64ull}) {
+        u32x4 *o = reinterpret_cast<u32x4 *>(reinterpret_cast<char *>(out) + shift);
+        const uint64_t nq2 = nq - 8, blocks = 4096, waves = blocks * 4;
+        for (int odd = 0; odd < 2; odd++) {
+            // odd: per-wave spans of an odd number of quads, so every wave starts mid-line
+            const uint64_t per_wave = odd ? ((nq2 / waves) | 1) : (nq2 + waves - 1) / waves;
+            hipLaunchKernelGGL(fill<true>, dim3(blocks), dim3(256), 0, 0, o, nq2, per_wave);
+            CHK(hipDeviceSynchronize());
+            CHK(hipEventRecord(e0));
+            for (int r = 0; r < 5; r++) hipLaunchKernelGGL(fill<true>, dim3(blocks), dim3(256), 0, 0, o, nq2, per_wave);
+            CHK(hipEventRecord(e1));
+            CHK(hipEventSynchronize(e1));
+            float ms;
+            CHK(hipEventElapsedTime(&ms, e0, e1));
+            const uint64_t written = std::min<uint64_t>(nq2, per_wave * waves) * 16;
+            printf("fill_nt_shift%lu%s,%lu,%.1f,%.1f\n", (unsigned long)shift, odd ? "_oddspan" : "", (unsigned long)blocks,
+                   per_wave * 16 / 1024.0, (double)written * 5 / (ms * 1e-3) / 1e9);
             fflush(stdout);
         }
     }
