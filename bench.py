@@ -17,6 +17,12 @@ Other modes (not the headline line):
                 its own slice of the batch from every shard -- all_to_all of
                 u32 counts and padded values over RCCL -- and merges it on the
                 device): strong scaling
+  --config c4l0 the same 100M filters sharded by their first topic level
+                (filters whose first level is '+' or '#' on every rank); a
+                publish is matched on the ONE rank owning its first level (the
+                host routes it there), whose lists are complete and in
+                traversal order: no merge, no data-path collective; weak
+                scaling (each rank matches its own batches)
   --config c5   churn: every step first applies --deltas subscribe/unsubscribe
                 ops (one router-syncer batch) to the replicated index, then
                 matches the batch; reports deltas/s beside topics/s
@@ -50,6 +56,8 @@ CONFIGS = {
     "c3": (3, 10_000_000, "10M mixed-wildcard filters incl. $share groups and '$SYS' exclusion"),
     "c3deep": (30, 10_000_000, "C3 filters; 10% of the topics 33-64 levels deep"),
     "c4": (4, 100_000_000, "100M mixed filters filter-sharded over the ranks, RCCL all_to_all of hit-list slices"),
+    "c4l0": (4, 100_000_000, "100M mixed filters sharded by the first topic level ('+'/'#'-rooted filters on "
+                             "every rank), publishes routed to the rank owning their first level"),
     "c5": (5, 10_000_000, "churn: 10M mixed filters, subscribe/unsubscribe deltas interleaved with match batches"),
 }
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
@@ -127,12 +135,29 @@ def main():
 
     gen_cfg, default_f, desc = CONFIGS[a.config]
     filter_sharded = a.config == "c4"
+    level0 = a.config == "c4l0"
     nf = a.filters or default_f
     B = a.batch
     R = max(1, a.rotate)
 
     t = time.time()
-    fs = wl.filters(gen_cfg, nf, shard=rank, nshards=world) if filter_sharded else wl.filters(gen_cfg, nf)
+    l0map = None
+    if level0:
+        # every rank draws the same owner map from the same sample, then keeps
+        # its own words' filters and the '+'/'#'-rooted ones, chunk by chunk
+        K = max(1, nf // 10_000_000)
+        l0map = shard.Level0Map.from_items(world, wl.filters(gen_cfg, nf, shard=0, nshards=K))
+        parts = []
+        for k in range(K):
+            fk = wl.filters(gen_cfg, nf, shard=k, nshards=K)
+            parts.append(wl.take(fk, l0map.filter_rows(fk, rank)))
+            del fk
+        fs = wl.concat(parts)
+        del parts
+    elif filter_sharded:
+        fs = wl.filters(gen_cfg, nf, shard=rank, nshards=world)
+    else:
+        fs = wl.filters(gen_cfg, nf)
     t_gen = time.time() - t
     log(f"[rank {rank}] generated {len(fs)} filters in {t_gen:.1f}s")
 
@@ -156,7 +181,20 @@ def main():
     # [(r R + k) B, (r R + k + 1) B) of the stream; filter-sharded: every rank
     # matches the same R batches against its shard.
     base = 0 if filter_sharded else rank * R
-    tsets = [wl.topics(gen_cfg, nf, B, first=(base + k) * B) for k in range(R)]
+    if level0:
+        # c4l0: the host routes each publish to the rank owning its first
+        # level; rank r's batches are the topics of the stream it owns
+        pool, have, pos, CH = [], 0, 0, max(B, 1_000_000)
+        while have < R * B:
+            cand = wl.topics(gen_cfg, nf, CH, first=pos)
+            pool.append(wl.take(cand, l0map.topic_rows(cand, rank)))
+            have += len(pool[-1])
+            pos += CH
+        allt = wl.concat(pool)
+        tsets = [allt.slice(k * B, (k + 1) * B) for k in range(R)]
+        del pool, allt
+    else:
+        tsets = [wl.topics(gen_cfg, nf, B, first=(base + k) * B) for k in range(R)]
     d_in = [(torch.from_numpy(ts.blob).to(dev), torch.from_numpy(ts.offs.view(np.int64)).to(dev)) for ts in tsets]
     # one output set per stream: consecutive steps rotate over the streams, so
     # step k+1's walk overlaps step k's scan / emit (the library keeps one
@@ -434,6 +472,8 @@ def main():
 
     metric = {"c3": "topic matches/sec at 10M filters"}.get(a.config, f"topic matches/sec ({a.config})")
     par = (f"filter-sharded x{world} (RCCL all_to_all of per-slice counts and hit lists, device merge)" if filter_sharded
+           else f"level-0 sharded x{world} (first-level words partitioned, '+'/'#' roots replicated; "
+                f"topics routed by first level; no data-path collective)" if level0
            else f"topic-sharded x{world} (trie replicated)")
     res = {
         "metric": metric,
@@ -448,7 +488,7 @@ def main():
         "vs_baseline": None,
         "dtype": "u8/u32",
         "data": "synthetic (emqx_amd/csrc/workload.cpp, seed 0x454D5158+cfg)",
-        "config": {"workload": f"{a.config}: {desc}", "filters": nf if filter_sharded else len(fs),
+        "config": {"workload": f"{a.config}: {desc}", "filters": nf if (filter_sharded or level0) else len(fs),
                    "topics_per_gpu_step": B, "global_batch": topics_per_step, "parallelism": par,
                    "streams": nstreams, "distinct_batches": R},
         "roofline": {"bound": "hbm", "achieved": None if achieved is None else round(achieved, 1),
@@ -476,7 +516,9 @@ def main():
         "batch_latency_host_pageable_ms": lat_pageable,
         "concurrent_callers": conc,
         "parity_sample": None if mism is None else {"topics": ns, "mismatches": mism,
-                                                    "against": "oracle over this rank's keys"},
+                                                    "against": "oracle over this rank's keys" + (
+                                                        " (every filter that can match a topic this rank owns: "
+                                                        "the unsharded answer, order included)" if level0 else "")},
         "build": {"generate_s": round(t_gen, 1), "compile_s": round(t_compile, 1), "upload_s": round(t_upload, 2),
                   "device_MiB": round(st["device_bytes"] / 2**20, 1), "nodes": st["n_nodes"],
                   "edges": st["n_edges"], "words": st["n_words"], "keys_this_rank": st["n_keys"],

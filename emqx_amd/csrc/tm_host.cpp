@@ -1140,6 +1140,9 @@ void init_tables(tm_index *ix, uint64_t hint) {
     ix->aux.reserve(hint / 2 + 1);
     node_new(ix, NONE, NONE, false);   // ROOT
     ix->vals.h.reserve(hint + 16);
+    // a 16-B guard before the first run: k_emit's run-by-run copy loads whole
+    // quads that may overhang a run by up to 3 words on either side
+    ix->vals.h.assign(4, 0);
 }
 
 // NULL is HIP's default (null) stream -- the stream PyTorch's default stream

@@ -1239,11 +1239,15 @@ __global__ __launch_bounds__(1024) void k_scan_top(uint64_t *blk, uint64_t nb, u
 constexpr int EMIT_BLOCK = TILE;
 constexpr int EMIT_WAVES = EMIT_BLOCK / 64;
 constexpr int WR = 64 * RCAP;   // ranges per wave
+typedef uint4 __attribute__((aligned(4))) uint4u;   // dword-aligned 16-B load (global_load_dwordx4)
 #ifndef TM_EMIT_Q
 #define TM_EMIT_Q 1
 #endif
-typedef uint4 __attribute__((aligned(4))) uint4u;   // dword-aligned 16-B load (global_load_dwordx4)
 constexpr int EMIT_Q = TM_EMIT_Q;   // quads per lane per iteration (loads in flight before the stores)
+#ifndef TM_EMIT_RUNS
+#define TM_EMIT_RUNS 16
+#endif
+constexpr uint64_t EMIT_RUNS = TM_EMIT_RUNS;   // average run length from which a wave copies run by run
 
 // One block = one tile of 256 topics: finishes the scan (tile prefix + local
 // exclusive scan -> hit_offs), then each wave flattens its 64 topics' value
@@ -1299,6 +1303,45 @@ __global__ __launch_bounds__(EMIT_BLOCK) void k_emit(DevIndex ix, Workspace ws, 
     if (!R) return;
     const bool vec = (reinterpret_cast<uintptr_t>(out) & 15) == 0;
     const uint64_t q1 = (endp + 3) >> 2;
+    if (endp - base >= (uint64_t)EMIT_RUNS * R) {
+        // Long runs (C2: 250 IDs per filter; average run >= EMIT_RUNS values):
+        // copy run by run.  The wave walks its ranges in order; for each, lane
+        // l writes the l-th 16-B quad of the run's output with one dword-
+        // aligned 16-B load from the run (the vals device copy has a 4-word
+        // guard before the first run and >= 16 words after the last, so the
+        // load may overhang the run) and one non-temporal store: a few
+        // instructions per KiB instead of a range search per quad.  The quads
+        // a run shares with its neighbours take dword stores of its own
+        // elements.  C2 batch 1.43 -> 1.10 ms (profiles/r2_emit_variants.txt;
+        // the variants that wrote every quad once, whole -- a window of <= 4
+        // ranges per 1 KiB, extra loads of the next runs, a quad carried
+        // between runs in scalar registers -- all measured slower: each extra
+        // load or cross-lane step per quad costs more than the partial writes).
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        for (uint32_t i = 0; i < R; i++) {
+            const uint32_t ro = s_off[wv][i], rc = s_cnt[wv][i];
+            const uint64_t P = base + s_rel[wv][i];
+            if (rc & RUN_INLINE) {
+                if (lane == 0 && P < cap) out[P] = ro;
+                continue;
+            }
+            const uint64_t E = P + (rc & RUN_CNT);
+            for (uint64_t Q = (P >> 2) + lane; (Q << 2) < E; Q += 64) {
+                const uint64_t p0 = Q << 2;
+                const uint4 a = *reinterpret_cast<const uint4u *>(ix.vals + ro + (int64_t)(p0 - P));
+                if (vec && p0 >= P && p0 + 4 <= E && p0 + 3 < cap) {
+                    const u32x4 x = {a.x, a.y, a.z, a.w};
+                    __builtin_nontemporal_store(x, reinterpret_cast<u32x4 *>(out + p0));
+                } else {
+                    const uint32_t e[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+                    for (int k = 0; k < 4; k++)
+                        if (p0 + k >= P && p0 + k < E && p0 + k < cap) out[p0 + k] = e[k];
+                }
+            }
+        }
+        return;
+    }
     uint32_t r = 0;   // last range starting at or before the lane's position (positions only grow)
     // one quad: its range found from the lane's previous one (positions only
     // grow; a lane moves 256 positions per quad, so a few steps forward cover

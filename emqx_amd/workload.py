@@ -63,6 +63,35 @@ class ItemSet:
         return ItemSet(blob, self.offs[lo:hi + 1] - np.uint64(b0), self.vals[lo:hi].copy(), self.flags[lo:hi].copy())
 
 
+def take(s: ItemSet, idx) -> ItemSet:
+    """The items s[idx] (idx: ascending int array) as a new packed set."""
+    idx = np.asarray(idx, dtype=np.int64)
+    starts = s.offs[idx].astype(np.int64)
+    lens = (s.offs[idx + 1] - s.offs[idx]).astype(np.int64)
+    offs = np.zeros(len(idx) + 1, np.uint64)
+    np.cumsum(lens, out=offs[1:].view(np.int64))
+    total = int(offs[-1])
+    pos = np.repeat(starts - offs[:-1].astype(np.int64), lens) + np.arange(total, dtype=np.int64)
+    blob = np.concatenate([s.blob[pos], np.zeros(16, np.uint8)])
+    return ItemSet(blob, offs, s.vals[idx].copy(), s.flags[idx].copy())
+
+
+def concat(sets) -> ItemSet:
+    """The items of several packed sets, in order, as one set."""
+    sets = list(sets)
+    if not sets:
+        return ItemSet(np.zeros(16, np.uint8), np.zeros(1, np.uint64), np.zeros(0, np.uint32), np.zeros(0, np.uint8))
+    blobs, offs, base = [], [np.zeros(1, np.uint64)], 0
+    for x in sets:
+        nb = int(x.offs[-1])
+        blobs.append(x.blob[:nb])
+        offs.append(x.offs[1:] + np.uint64(base))
+        base += nb
+    blobs.append(np.zeros(16, np.uint8))
+    return ItemSet(np.concatenate(blobs), np.concatenate(offs), np.concatenate([x.vals for x in sets]),
+                   np.concatenate([x.flags for x in sets]))
+
+
 def _take(s: _Set) -> ItemSet:
     n, nb = s.n, s.nbytes
     blob = np.ctypeslib.as_array(s.bytes, shape=(nb + 16,)).copy()

@@ -128,3 +128,97 @@ def test_filter_sharded_exchange_gloo():
                                   np.sort(m_vals[m_offs[i - lo]:m_offs[i - lo + 1]]))
     assert res[0][3] == [[0, 1000], [1000, 1000]]
     assert res[0][4] == 1.5
+
+
+# ---------------------------------------------------- level-0 filter sharding
+
+def _l0_worker(rank, world, port, q):
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parent.parent
+    sys.path.insert(0, str(root))
+    sys.path.insert(0, str(root / "oracle"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from emqx_amd import shard, workload as wl
+        from pyoracle import Oracle
+        nf, n = 20_000, 4_000
+        fs = wl.filters(3, nf)
+        ts = wl.topics(3, nf, n)
+        m = shard.Level0Map.from_items(world, fs, sample=5_000)   # every rank draws the same map
+        mine = wl.take(fs, m.filter_rows(fs, rank))
+        rows = m.topic_rows(ts, rank)
+        o = Oracle()   # this rank's shard (the GPU index on a GPU box)
+        o.apply(np.ones(len(mine), np.uint8), mine.blob, mine.offs, mine.vals)
+        sub = wl.take(ts, rows)
+        cnt, _, hit, vals = o.match_batch(sub.blob, sub.offs)
+        # every topic is matched on exactly one rank
+        c = torch.tensor([len(rows)], dtype=torch.int64)
+        dist.all_reduce(c)
+        q.put((rank, rows, hit, vals, len(mine), int(c)))
+    except BaseException as e:
+        q.put((rank, "error", repr(e), None, None, None))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_level0_sharding_gloo():
+    """Each rank holds its first-level words' filters plus the '+'/'#'-rooted
+    ones and matches only the topics whose first level it owns: the union of
+    the ranks' lists equals the unsharded oracle's, order included."""
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parent.parent
+    sys.path.insert(0, str(root / "oracle"))
+    from emqx_amd import workload as wl
+    from pyoracle import Oracle
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_l0_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(world)]
+    for p in ps:
+        p.join(timeout=60)
+    res.sort(key=lambda x: x[0])
+    for r in res:
+        assert not (isinstance(r[1], str) and r[1] == "error"), r
+    nf, n = 20_000, 4_000
+    fs = wl.filters(3, nf)
+    ts = wl.topics(3, nf, n)
+    o = Oracle()
+    o.apply(np.ones(len(fs), np.uint8), fs.blob, fs.offs, fs.vals)
+    _, _, hit, vals = o.match_batch(ts.blob, ts.offs)
+    seen = np.zeros(n, np.int64)
+    for rank, rows, rhit, rvals, nkeys, total in res:
+        assert total == n
+        assert nkeys < len(fs)                       # a shard, not a replica
+        seen[rows] += 1
+        for k, t in enumerate(rows.tolist()):
+            assert np.array_equal(rvals[rhit[k]:rhit[k + 1]], vals[hit[t]:hit[t + 1]]), (rank, t)
+    assert (seen == 1).all()
+    assert sum(r[4] for r in res) < 2 * len(fs)
+
+
+def test_level0_map_is_deterministic_and_wild_roots_replicate():
+    from emqx_amd import shard, workload as wl
+    fs = wl.filters(3, 50_000)
+    a = shard.Level0Map.from_items(4, fs, sample=10_000)
+    b = shard.Level0Map.from_items(4, fs, sample=10_000)
+    assert a.table == b.table
+    own = a.owners(fs)
+    for i in np.flatnonzero(own == -1)[:50].tolist():
+        assert fs.item(i).split(b"/")[0] in (b"+", b"#")
+    for i in np.flatnonzero(own >= 0)[:200].tolist():
+        w = fs.item(i).split(b"/")[0]
+        assert w not in (b"+", b"#") and own[i] == a.owner_of_word(w)
+    # words the sample never saw (and long words) still get a fixed owner
+    assert a.owner_of_word(b"never-seen-level-zero-word") == b.owner_of_word(b"never-seen-level-zero-word")
+    # balanced: no rank owns more than 1.5x its share of the literal-rooted filters
+    cnt = np.bincount(own[own >= 0], minlength=4)
+    assert cnt.max() <= 1.5 * cnt.sum() / 4

@@ -1152,3 +1152,81 @@ def test_filter_sharded_sorted_merge_equals_one_index(torch_dev):
     mh = m_hit.cpu().numpy().view(np.uint64)
     assert np.array_equal(mh, h1)
     assert np.array_equal(m_vals.cpu().numpy().view(np.uint32)[: int(h1[-1])], v1)
+
+
+def test_long_runs_emit_run_by_run(torch_dev):
+    """Waves whose runs average >= 16 IDs take k_emit's run-by-run copy: runs of
+    every length and alignment, single-ID (inline) runs between them, and
+    topics with more than RCAP ranges (written by the re-walk, gaps in the
+    wave's span) -- exact against the oracle."""
+    rnd = random.Random(7)
+    keys, vals = [], []
+    v = 0
+    filt = ["#", "a/#", "a/b/#", "a/b/c/#", "+/#", "+/b/#", "a/+/#", "+/+/#", "a/b/+/#", "+/+/+/#",
+            "a/+/c/#", "+/b/c/#"]
+    for f in filt:
+        for _ in range(rnd.choice([1, 2, 3, 5, 17, 40, 250, 333])):
+            keys.append(f); vals.append(v); v += 1
+    for k in range(3000):
+        keys.append(f"d/{k}/+"); vals.append(v); v += 1
+        if k % 7 == 0:
+            for _ in range(rnd.randint(2, 60)):
+                keys.append(f"d/{k}/x"); vals.append(v); v += 1
+    items = items_of([s.encode() for s in keys], vals)
+    ix, o = gpu_index(items), oracle_of(items)
+    tops = []
+    for j in range(20_000):
+        r = rnd.random()
+        if r < 0.1:
+            tops.append(b"a/b/c/d/e")          # > RCAP ranges: re-walked
+        elif r < 0.2:
+            tops.append(b"a/b/c")
+        else:
+            tops.append(b"d/%d/%s" % (rnd.randrange(3500), rnd.choice([b"x", b"y"])))
+    assert_same(ix, o, items_of(tops))
+    # the same batch on the device API with a torch stream (the bench's path)
+    torch = torch_dev
+    ts = items_of(tops)
+    dev = torch.device("cuda:0")
+    d_blob = torch.from_numpy(ts.blob).to(dev)
+    d_offs = torch.from_numpy(ts.offs.view(np.int64)).to(dev)
+    d_hit = torch.zeros(len(tops) + 1, dtype=torch.int64, device=dev)
+    d_err = torch.zeros(len(tops), dtype=torch.uint8, device=dev)
+    s = torch.cuda.current_stream().cuda_stream
+    ix.match_batch_dev(len(tops), d_blob.data_ptr(), d_offs.data_ptr(), d_hit.data_ptr(), 0, 0, d_err.data_ptr(), s)
+    torch.cuda.synchronize()
+    total = int(d_hit[-1])
+    d_out = torch.zeros(total, dtype=torch.int32, device=dev)
+    ix.match_batch_dev(len(tops), d_blob.data_ptr(), d_offs.data_ptr(), d_hit.data_ptr(), d_out.data_ptr(), total,
+                       d_err.data_ptr(), s)
+    torch.cuda.synchronize()
+    _, _, ohit, ovals = o.match_batch(ts.blob, ts.offs)
+    assert np.array_equal(d_hit.cpu().numpy().view(np.uint64), ohit)
+    assert np.array_equal(d_out.cpu().numpy().view(np.uint32), ovals)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_level0_shards_equal_one_index(torch_dev, world):
+    """Level-0 filter sharding (bench --config c4l0): `world` shard indices on
+    one GPU, each holding its first-level words' filters and the '+'/'#'-rooted
+    ones; every topic matched on its owner's shard gives the unsharded
+    oracle's list, order included."""
+    from emqx_amd import shard
+    fs = wl.filters(3, 200_000)
+    ts = wl.topics(3, 200_000, 60_000)
+    o = oracle_of(fs)
+    _, _, ohit, ovals = o.match_batch(ts.blob, ts.offs)
+    m = shard.Level0Map.from_items(world, fs, sample=50_000)
+    seen = np.zeros(len(ts), np.int64)
+    for r in range(world):
+        mine = wl.take(fs, m.filter_rows(fs, r))
+        assert len(mine) < len(fs)
+        ix = gpu_index(mine)
+        rows = m.topic_rows(ts, r)
+        seen[rows] += 1
+        sub = wl.take(ts, rows)
+        hit, vals, err = ix.match_batch(sub.blob, sub.offs)
+        assert not err.any()
+        for k, t in enumerate(rows.tolist()):
+            assert np.array_equal(vals[hit[k]:hit[k + 1]], ovals[ohit[t]:ohit[t + 1]]), (r, ts.item(t))
+    assert (seen == 1).all()
