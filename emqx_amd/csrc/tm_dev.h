@@ -17,6 +17,7 @@ struct DevIndex {
     const ExactEntry *exact; uint32_t xmask;
     const uint16_t *xfp;
     const uint32_t *wseq;
+    const uint32_t *wbits; uint32_t wcap;   // wide nodes' child bitmaps, bits per bitmap (tm_layout.h WIDE_LIT)
     // A walk needs a topic's level words only down to the trie's depth (no node
     // deeper than `depth` exists), unless a binary key of the topic's length
     // exists (xlen_mask bit L for L < 64, L <= xlen_max beyond): need_levels().

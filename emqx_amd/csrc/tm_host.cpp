@@ -21,6 +21,7 @@
 #include <mutex>
 #include <string>
 #include <unordered_set>
+#include <set>
 #include <vector>
 
 #include "../../include/tmatch.h"
@@ -69,6 +70,7 @@ struct NodeAux {
     uint32_t depth = 0;                       // words on the path from the root
     uint32_t hash_roff = 0, exact_roff = 0;   // the runs' offsets in vals (the line may hold an inline value)
     uint8_t is_plus = 0;
+    uint32_t bm = NONE;                       // word offset of its child bitmap in wbits (wide nodes)
 };
 
 struct WordRef { const uint8_t *p; uint32_t n; int kind; };   // kind: 0 binary, 1 '+', 2 '#'
@@ -130,6 +132,8 @@ struct tm_index {
     Mirror<ExactEntry> exact; std::vector<uint32_t> xcap, xroff; uint64_t xcount = 0;
     Mirror<uint16_t> xfp;   // exact-table fingerprints, slot for slot (0 = empty)
     Mirror<uint32_t> wseq; uint64_t wseq_dead = 0;   // words of erased long exact keys
+    Mirror<uint32_t> wbits; uint32_t wb_words = 0;   // wide nodes' child bitmaps, wb_words words each
+    std::vector<uint32_t> free_wbits; std::set<uint32_t> wide;
 
     // levels a walk must resolve (DevIndex::depth / xlen_*): live nodes per
     // depth and live exact keys per level count
@@ -259,6 +263,8 @@ void vocab_rehash(tm_index *ix, uint64_t cap) {
     ix->vocab.dirty.set_all();
 }
 
+void wide_cover(tm_index *ix);
+
 void vocab_grow(tm_index *ix, uint64_t need) {
     // load <= 1/4: the walk's deferred probes resolve on the first slot
     // almost always (one round trip per topic for all its levels)
@@ -278,6 +284,7 @@ uint32_t vocab_intern(tm_index *ix, const uint8_t *p, uint32_t n) {
         e.wid = ix->wid_next++;
         ix->wref.push_back(0);
         ix->wslot.push_back(NONE);
+        wide_cover(ix);
     }
     if (n <= VINL) {
         pack8(p, n, e.b0, e.b1);
@@ -467,6 +474,78 @@ void set_bloom(Node &n, uint32_t wid) {
     bloom_word(n, b >> 5) |= 1u << (b & 31);
 }
 
+// ---- wide nodes' exact child bitmaps (tm_layout.h WIDE_LIT)
+
+void wide_bit(tm_index *ix, uint32_t node, uint32_t wid, bool on) {
+    const uint32_t bm = ix->aux[node].bm;
+    if (bm == NONE) return;
+    uint32_t &w = ix->wbits.h[bm + (wid >> 5)];
+    if (on) w |= 1u << (wid & 31); else w &= ~(1u << (wid & 31));
+    ix->wbits.touch(bm + (wid >> 5));
+}
+
+// (re)write node's bitmap from its child table and point the line at it
+void wide_fill(tm_index *ix, uint32_t node) {
+    const uint32_t bm = ix->aux[node].bm;
+    std::fill(ix->wbits.h.begin() + bm, ix->wbits.h.begin() + bm + ix->wb_words, 0u);
+    Node &n = ix->nodes.h[node];
+    for (uint32_t i = 0; i <= n.kw[1]; i++) {
+        const uint32_t w = ix->ctab.h[n.kw[0] + i].wid;
+        if (w != NONE) ix->wbits.h[bm + (w >> 5)] |= 1u << (w & 31);
+    }
+    ix->wbits.touch(bm, ix->wb_words);
+    n.kw[2] = bm;
+    ix->nodes.touch(node);
+}
+
+uint32_t wide_alloc(tm_index *ix) {
+    if (!ix->free_wbits.empty()) { uint32_t o = ix->free_wbits.back(); ix->free_wbits.pop_back(); return o; }
+    const uint32_t o = (uint32_t)ix->wbits.h.size();
+    ix->wbits.h.resize(o + ix->wb_words, 0u);
+    return o;
+}
+
+// bitmaps cover every wid handed out so far: grow them all (rare: the vocab
+// doubles) before a new wid could be looked up in one
+void wide_cover(tm_index *ix) {
+    if (ix->wide.empty() || (uint64_t)ix->wb_words * 32 >= ix->wid_next) return;
+    uint32_t words = std::max<uint32_t>(ix->wb_words, 1024);
+    while ((uint64_t)words * 32 < ix->wid_next) words *= 2;
+    ix->wb_words = words;
+    ix->wbits.h.clear();
+    ix->free_wbits.clear();
+    for (uint32_t node : ix->wide) {
+        ix->aux[node].bm = wide_alloc(ix);
+        wide_fill(ix, node);
+    }
+    ix->wbits.dirty.set_all();
+}
+
+void to_wide(tm_index *ix, uint32_t node) {
+    if (ix->wide.empty()) ix->wb_words = 0;
+    ix->wide.insert(node);
+    if ((uint64_t)ix->wb_words * 32 < ix->wid_next) {
+        ix->aux[node].bm = NONE;
+        wide_cover(ix);   // sizes the bitmaps and fills this node's too
+        return;
+    }
+    ix->aux[node].bm = wide_alloc(ix);
+    wide_fill(ix, node);
+}
+
+void from_wide(tm_index *ix, uint32_t node) {
+    ix->free_wbits.push_back(ix->aux[node].bm);
+    ix->aux[node].bm = NONE;
+    ix->wide.erase(node);
+    Node &n = ix->nodes.h[node];
+    for (uint32_t j = 0; j < 6; j++) bloom_word(n, j) = 0;
+    for (uint32_t i = 0; i <= n.kw[1]; i++) {
+        const uint32_t w = ix->ctab.h[n.kw[0] + i].wid;
+        if (w != NONE) set_bloom(n, w);
+    }
+    ix->nodes.touch(node);
+}
+
 // summary of node q as its parent's psum (tm_layout.h): terminals, '+' child,
 // 61-bit Bloom of the literal child wids (all ones past 61 children)
 // literal-children Bloom of node q (29 bits), all ones past 29 children
@@ -555,6 +634,7 @@ void to_table(tm_index *ix, uint32_t node, uint32_t cap) {
         set_bloom(m, c.wid);
     }
     m.kw[0] = off; m.kw[1] = cap - 1;
+    if (ix->aux[node].bm != NONE) m.kw[2] = ix->aux[node].bm;   // wide: the bitmap, not the Bloom
 }
 
 void child_add(tm_index *ix, uint32_t node, uint32_t wid, uint32_t child) {
@@ -568,9 +648,11 @@ void child_add(tm_index *ix, uint32_t node, uint32_t wid, uint32_t child) {
         else if ((n->nlit + 1) * 2 > n->kw[1] + 1) to_table(ix, node, (n->kw[1] + 1) * 2);
         n = &ix->nodes.h[node];
         ctab_put(ix, n->kw[0], n->kw[1], wid, child, node_psum(ix, child));
-        set_bloom(*n, wid);
+        if (ix->aux[node].bm != NONE) wide_bit(ix, node, wid, true);
+        else set_bloom(*n, wid);
     }
     n->nlit++;
+    if (WIDE_LIT && n->nlit == WIDE_LIT && ix->aux[node].bm == NONE) { to_wide(ix, node); n = &ix->nodes.h[node]; }
     ix->nodes.touch(node);
     summary_refresh(ix, node);
 }
@@ -584,7 +666,9 @@ void child_remove(tm_index *ix, uint32_t node, uint32_t wid) {
         n.nlit--;
     } else {
         ctab_erase(ix, n.kw[0], n.kw[1], wid);
+        wide_bit(ix, node, wid, false);
         n.nlit--;
+        if (ix->aux[node].bm != NONE && n.nlit < WIDE_LIT) from_wide(ix, node);
         if (n.nlit == KINL) {   // back to inline mode
             std::vector<CSlot> kids;
             for (uint32_t i = 0; i <= n.kw[1]; i++) if (ix->ctab.h[n.kw[0] + i].wid != NONE) kids.push_back(ix->ctab.h[n.kw[0] + i]);
@@ -947,6 +1031,7 @@ int sync_locked(tm_index *ix, hipStream_t s) {
     if ((rc = collect(ix, ix->exact, runs, data))) return rc;
     if ((rc = collect(ix, ix->xfp, runs, data))) return rc;
     if ((rc = collect(ix, ix->wseq, runs, data))) return rc;
+    if ((rc = collect(ix, ix->wbits, runs, data))) return rc;
     const uint64_t nr = runs.size(), nw = data.size();
     if (!nr) return TM_OK;
     // staging: [runs | data] in one pinned buffer, one H2D copy, one kernel
@@ -992,6 +1077,7 @@ DevIndex dev_view(tm_index *ix) {
     d.exact = ix->exact.d; d.xmask = (uint32_t)ix->exact.h.size() - 1;
     d.xfp = ix->xfp.d;
     d.wseq = ix->wseq.d;
+    d.wbits = ix->wbits.d; d.wcap = ix->wide.empty() ? 0 : ix->wb_words * 32;
     // levels a walk must resolve: the deepest live node's depth (no node below
     // it has children), all of a topic's levels when a binary key has its length
     auto &dc = ix->depth_cnt, &xc = ix->xlen_cnt;
@@ -1213,7 +1299,8 @@ int tm_destroy(tm_index *ix) {
     if (!ix) return TM_EINVAL;
     (void)hipSetDevice(ix->device);
     (void)hipDeviceSynchronize();
-    void *bufs[] = {ix->vocab.d, ix->wpool.d, ix->nodes.d, ix->ctab.d, ix->vals.d, ix->exact.d, ix->xfp.d, ix->wseq.d};
+    void *bufs[] = {ix->vocab.d, ix->wpool.d, ix->nodes.d, ix->ctab.d, ix->vals.d, ix->exact.d, ix->xfp.d, ix->wseq.d,
+                    ix->wbits.d};
     for (void *p : bufs) if (p) (void)hipFree(p);
     for (auto &l : ix->lanes) free_lane(*l);
     for (auto &p : ix->patch) {
@@ -1672,7 +1759,7 @@ int tm_stats(tm_index *ix, tm_stats_t *o) {
     o->n_words = ix->vcount;
     o->device_bytes = ix->vocab.dcap * sizeof(VocabEntry) + ix->wpool.dcap + ix->nodes.dcap * sizeof(Node) +
                       ix->ctab.dcap * sizeof(CSlot) + ix->vals.dcap * 4 + ix->exact.dcap * sizeof(ExactEntry) + ix->xfp.dcap * 2 +
-                      ix->wseq.dcap * 4;
+                      ix->wseq.dcap * 4 + ix->wbits.dcap * 4;
     o->uploads = ix->uploads;
     o->patch_bytes = ix->patch_bytes;
     return TM_OK;

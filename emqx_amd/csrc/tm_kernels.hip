@@ -62,6 +62,16 @@ __device__ __forceinline__ uint32_t bloom_bit(const uint4 &n2, const uint4 &n3, 
     return (w >> (b & 31)) & 1u;
 }
 
+// may a table-mode node (line words n1, n2, n3) have a literal child for word
+// w?  Wide nodes answer exactly from their bitmap (an L2-resident line), the
+// others from the 192-bit Bloom in the line
+__device__ __forceinline__ uint32_t child_maybe(const DevIndex &ix, const uint4 &n1, const uint4 &n2, const uint4 &n3,
+                                                uint32_t w, uint32_t h) {
+    if (WIDE_LIT && n1.y >= WIDE_LIT)
+        return w < ix.wcap ? (ix.wbits[n2.z + (w >> 5)] >> (w & 31)) & 1u : 0u;
+    return bloom_bit(n2, n3, child_bit(h));
+}
+
 // can a child Q (summarised as Node.psum / CSlot.sum, tm_layout.h) contribute
 // to a topic of L levels when entered at level lq?  Q must emit at lq == L, or
 // below it emit ('#' terminal) or go on: a literal child for word wq, or its
@@ -557,7 +567,7 @@ __device__ bool dfs(const DevIndex &ix, uint32_t L, bool dollar, S &st, EM &em) 
                     lit = inl;
                 } else {
                     const uint32_t h = child_hash(w);
-                    const uint32_t m = bloom_bit(n2, n3, child_bit(h));
+                    const uint32_t m = child_maybe(ix, n1, n2, n3, w, h);
                     if (m & 1u) {
                         uint32_t slo, shi;
 #ifdef TM_NT_CTAB
@@ -1030,7 +1040,7 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_wave(DevIndex ix, Workspace w
                 lit = n2.x == wl_ ? n3.x : n2.y == wl_ ? n3.y : n2.z == wl_ ? n3.z : n2.w == wl_ ? n3.w : NONE;
             } else {
                 const uint32_t h = child_hash(wl_);
-                const uint32_t mb = bloom_bit(n2, n3, child_bit(h));
+                const uint32_t mb = child_maybe(ix, n1, n2, n3, wl_, h);
                 if (mb & 1u) {
                     uint32_t slo, shi;
                     lit = ctab_find(ix, n2.x, n2.y, wl_, h, slo, shi);

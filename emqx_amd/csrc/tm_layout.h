@@ -56,6 +56,18 @@ struct alignas(16) CSlot {          // 16 B: one literal child in a node's priva
 
 constexpr uint32_t KINL = 4;     // literal children kept inside the node's line
 
+// A table-mode node with at least WIDE_LIT literal children (its 192-bit Bloom
+// would be saturated: every probe passes it) keeps an exact bitmap over the
+// whole wid space instead, in the `wbits` pool (kw[2] = its word offset).
+// The few such nodes are the widest of the upper trie -- C3: the level-1
+// nodes and the (w0,+) / (+,+) level-2 nodes -- so their bitmaps stay in L2
+// and a probe for a word the node has no child for costs an L2 hit instead of
+// a memory-side request into a multi-megabyte child table.
+#ifndef TM_WIDE_LIT
+#define TM_WIDE_LIT 256
+#endif
+constexpr uint32_t WIDE_LIT = TM_WIDE_LIT;   // 0: bitmaps off
+
 // One 64-byte line per trie state: everything a walk step needs -- the '+'
 // child, both terminals and, for nodes with <= KINL literal children (almost
 // every node below the top levels), the literal children themselves.  A node

@@ -447,17 +447,18 @@ def test_child_table_grow_and_shrink(torch_dev):
     back to inline, with matches checked against the oracle at every stage."""
     ix = gpu_index()
     o = Oracle()
-    topics = items_of([b"a/%d/x" % i for i in range(200)] + [b"a/%d" % i for i in range(200)] + [b"b/1/x"])
+    topics = items_of([b"a/%d/x" % i for i in range(700)] + [b"a/%d" % i for i in range(700)] + [b"b/1/x"])
     live = []
     r = random.Random(5)
-    for stage in [3, 5, 6, 17, 33, 130, 200]:
+    # past WIDE_LIT (256) children the node answers from an exact bitmap
+    for stage in [3, 5, 6, 17, 33, 130, 200, 255, 256, 257, 600]:
         add = [i for i in range(stage) if i not in live]
         d = items_of([b"a/%d/+" % i for i in add] + [b"a/%d/#" % i for i in add], add + [1000 + i for i in add])
         ix.apply(np.ones(len(d), np.uint8), d.blob, d.offs, d.vals)
         o.apply(np.ones(len(d), np.uint8), d.blob, d.offs, d.vals)
         live += add
         assert_same(ix, o, topics)
-    for keep in [120, 40, 9, 5, 4, 2, 0]:
+    for keep in [400, 256, 255, 120, 40, 9, 5, 4, 2, 0]:
         drop = r.sample(live, len(live) - keep)
         live = [i for i in live if i not in drop]
         d = items_of([b"a/%d/+" % i for i in drop] + [b"a/%d/#" % i for i in drop], drop + [1000 + i for i in drop])
@@ -1230,3 +1231,29 @@ def test_level0_shards_equal_one_index(torch_dev, world):
         for k, t in enumerate(rows.tolist()):
             assert np.array_equal(vals[hit[k]:hit[k + 1]], ovals[ohit[t]:ohit[t + 1]]), (r, ts.item(t))
     assert (seen == 1).all()
+
+
+def test_wide_node_bitmaps_follow_vocab_growth(torch_dev):
+    """A wide node's bitmap must cover every word id: 40k new words arrive while
+    it is wide (the bitmaps regrow), then children with those new ids are added
+    and removed, and the node drops back to its Bloom -- exact throughout."""
+    ix, o = gpu_index(), Oracle()
+
+    def put(strings, vals, op):
+        d = items_of(strings, vals)
+        ix.apply(np.full(len(d), op, np.uint8), d.blob, d.offs, d.vals)
+        o.apply(np.full(len(d), op, np.uint8), d.blob, d.offs, d.vals)
+
+    put([b"a/w%d/+" % i for i in range(300)], list(range(300)), 1)
+    put([b"z/n%d" % k for k in range(40_000)], list(range(1000, 41_000)), 1)     # binary keys: new words
+    new = list(range(0, 40_000, 97))
+    put([b"a/n%d/+" % k for k in new], [50_000 + k for k in new], 1)            # children with the new ids
+    r = random.Random(11)
+    tops = [b"a/n%d/x" % r.randrange(40_000) for _ in range(3000)] + [b"a/w%d/y" % r.randrange(400) for _ in range(3000)]
+    tops += [b"z/n%d" % r.randrange(41_000) for _ in range(1000)] + [b"a/never/x", b"a/z/x"]
+    ts = items_of(tops)
+    assert_same(ix, o, ts)
+    put([b"a/w%d/+" % i for i in range(300)], list(range(300)), 0)             # 713 -> 413 children: still wide
+    assert_same(ix, o, ts)
+    put([b"a/n%d/+" % k for k in new[:300]], [50_000 + k for k in new[:300]], 0)   # 113: the Bloom again
+    assert_same(ix, o, ts)
