@@ -35,6 +35,7 @@ Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3]
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import math
 import os
@@ -79,8 +80,11 @@ def parse():
     p.add_argument("--rotate", type=int, default=4, help="distinct topic batches the steps rotate over")
     p.add_argument("--deltas", type=int, default=100,
                    help="c5: deltas applied per step (100 x ~2.5k steps/s = 2.5x the configured 100k deltas/s)")
-    p.add_argument("--streams", type=int, default=3,
-                   help="HIP streams the steps rotate over (batch k+1's walk overlaps batch k's scan/emit)")
+    p.add_argument("--streams", type=int, default=None,
+                   help="HIP streams the steps rotate over (batch k+1's walk overlaps batch k's scan/emit); "
+                        "default 3, and 1 for c5: a churn step's patch waits for every batch in flight, so "
+                        "its steps cannot overlap and a second stream only adds cross-stream waits "
+                        "(0.41 vs 0.54-0.64 ms per step measured)")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     p.add_argument("--cpu-threads", type=int, default=None,
                    help="CPU baseline threads (default: the CPUs this process may use)")
@@ -199,7 +203,7 @@ def main():
     # one output set per stream: consecutive steps rotate over the streams, so
     # step k+1's walk overlaps step k's scan / emit (the library keeps one
     # workspace per stream and orders index patches across streams)
-    nstreams = 1 if filter_sharded else max(1, a.streams)
+    nstreams = 1 if filter_sharded else max(1, a.streams if a.streams is not None else (1 if a.config == "c5" else 3))
     streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(nstreams - 1)]
     outs = [{"hit": torch.zeros(B + 1, dtype=torch.int64, device=dev),
              "err": torch.zeros(B, dtype=torch.uint8, device=dev),
@@ -213,6 +217,7 @@ def main():
         dchunks = [dl.slice(k * a.deltas, (k + 1) * a.deltas) for k in range(a.steps + a.warmup + 1)]
     dpos = [0]
     kstep = [0]
+    apply_s = [0.0]   # c5: host time inside tm_apply_deltas (the syncer's side of a churn step)
     xch = shard.Exchange(B, dev) if filter_sharded and world > 1 else None
 
     def step(cap):
@@ -224,7 +229,9 @@ def main():
         if dchunks:
             d = dchunks[dpos[0]]
             dpos[0] += 1
+            ta = time.perf_counter()
             ix.apply(d.flags, d.blob, d.offs, d.vals)
+            apply_s[0] += time.perf_counter() - ta
         ix.match_batch_dev(B, d_blob.data_ptr(), d_offs.data_ptr(), o["hit"].data_ptr(), o["out"].data_ptr(), cap,
                            o["err"].data_ptr(), sid)
         if filter_sharded:
@@ -256,12 +263,20 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    apply_s[0] = 0.0
+    # the host loop stands in for the NIF's C caller: keep Python's cyclic
+    # collector out of the timed region (a full collection stalled the GPU
+    # ~7 ms at a time in c5 traces, where each step waits for its deltas)
+    gc.collect()
+    gc.freeze()
+    gc.disable()
     t0 = time.perf_counter()
     merged = None
     for _ in range(a.steps):
         merged = step(cap)
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
+    gc.enable()
     if world > 1:
         dist.barrier()
     walk_ms, batch_ms, nb = ix.profile_read(reset=True)
@@ -325,7 +340,7 @@ def main():
     ts = tsets[0]
     lat = {}
     conc = None
-    if not filter_sharded:
+    if not filter_sharded and a.latency_batches > 0:
         for lb in sorted({min(4096, B), min(65536, B)}):
             sub = ts.slice(0, lb)
             _, v0, _ = ix.match_batch(sub.blob, sub.offs)          # sizes the value buffer
@@ -346,6 +361,7 @@ def main():
                     xs.append((time.perf_counter() - t1) * 1e3)
                 xs = np.array(xs[2:])
                 lat[f"{kind}/{lb}"] = {"p50_ms": float(np.percentile(xs, 50)), "p99_ms": float(np.percentile(xs, 99))}
+    if not filter_sharded:
         if a.concurrency > 0 and hasattr(ix, "host_array"):
             conc = concurrent_latency(ix, ts, a.concurrency, min(4096, B))
     if world > 1 and lat:
@@ -528,6 +544,7 @@ def main():
     if dchunks:
         res["deltas_per_step"] = a.deltas
         res["deltas_per_s"] = round(a.deltas * a.steps / el_max, 1)
+        res["delta_apply_host_ms_per_step"] = round(apply_s[0] / a.steps * 1e3, 4)
     if filter_sharded:
         res["merged_hits_this_rank_slice"] = merged_total
         res["merged_topics_this_rank_slice"] = merged_topics

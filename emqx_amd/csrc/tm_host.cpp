@@ -971,6 +971,9 @@ int upload_full(tm_index *ix, Mirror<T> &m) {
     if (m.bytes()) {
         HIPCHK(ix, hipMemcpy(m.d, m.h.data(), m.bytes(), hipMemcpyHostToDevice));
     }
+    if (getenv("TM_DEBUG_UPLOADS"))   // diagnostics: which table was shipped whole, and why
+        fprintf(stderr, "tm upload_full: %zu-byte elements x %zu (%.1f MB), dcap %lu\n", sizeof(T), m.h.size(),
+                m.bytes() / 1e6, (unsigned long)m.dcap);
     m.dirty.clear();
     ix->uploads++;
     return TM_OK;
@@ -1042,13 +1045,15 @@ int sync_locked(tm_index *ix, hipStream_t s) {
     if (bytes > p.pin_cap) {
         if (p.pin) HIPCHK(ix, hipHostFree(p.pin));
         p.pin = nullptr;
-        p.pin_cap = bytes + bytes / 2 + 4096;
+        // generous steps: a reallocation (hipHostFree / hipFree) synchronises
+        // the device, a multi-millisecond stall inside a churn stream (C5)
+        p.pin_cap = std::max<uint64_t>(bytes * 2, 1u << 20);
         HIPCHK(ix, hipHostMalloc(&p.pin, p.pin_cap, hipHostMallocDefault));
     }
     if (bytes > p.dev_cap) {   // the slot's previous patch has completed (p.done above)
         if (p.dev) HIPCHK(ix, hipFree(p.dev));
         p.dev = nullptr;
-        p.dev_cap = bytes + bytes / 2 + 4096;
+        p.dev_cap = std::max<uint64_t>(bytes * 2, 1u << 20);
         HIPCHK(ix, hipMalloc(&p.dev, p.dev_cap));
     }
     memcpy(p.pin, runs.data(), nr * sizeof(PatchRun));
