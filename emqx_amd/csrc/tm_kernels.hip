@@ -1115,6 +1115,14 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_wave(DevIndex ix, Workspace w
 
 constexpr int MID_BLOCK = 64;
 constexpr int MID_GRID = 512;                         // LDS-frontier blocks of the tail kernels
+// k_walk_tail of a large count-mode batch: more LDS-frontier blocks (it takes
+// no grid-wide ticket then, so idle blocks cost only their dispatch).  512
+// blocks = 2 waves per CU: C3deep (100k topics of 33-64 levels per 1M batch)
+// spent 0.57 ms per batch in the tail; 2048: 0.25 ms
+#ifndef TM_MID_GRID_BIG
+#define TM_MID_GRID_BIG 2048
+#endif
+constexpr int MID_GRID_BIG = TM_MID_GRID_BIG;
 constexpr int TAIL_GRID = MID_GRID + DEEP_LANES / 64; // + global-scratch blocks
 
 // last block of a grid (atomic ticket) resets the list counters for the next batch
@@ -1140,21 +1148,21 @@ __device__ __forceinline__ void reset_lists_if_last(const Workspace &ws) {
 template <int MODE>
 __global__ __launch_bounds__(MID_BLOCK) void k_walk_tail(DevIndex ix, Workspace ws, uint64_t n,
                                                          const uint8_t *blob, const uint64_t *offs, Outs o,
-                                                         uint64_t nb, uint64_t *scan_hit) {
+                                                         uint64_t nb, uint64_t *scan_hit, uint32_t mid_grid) {
     __shared__ uint32_t s_wid[MID_L * MID_BLOCK];
     __shared__ uint32_t s_pend[(MID_L + 1) * MID_BLOCK];
     __shared__ uint8_t s_len[MID_L * MID_BLOCK];
     uint32_t hits = 0;
-    if (blockIdx.x < MID_GRID) {
+    if (blockIdx.x < mid_grid) {
         const uint32_t cnt = ws.list_n[L_MID];
         const uint32_t *lst = ws.lists + (uint64_t)L_MID * n;
         LdsStore<MID_L> st{s_wid + threadIdx.x, s_pend + threadIdx.x, s_len + threadIdx.x, MID_BLOCK, 0};
-        for (uint32_t i = blockIdx.x * MID_BLOCK + threadIdx.x; i < cnt; i += MID_GRID * MID_BLOCK) {
+        for (uint32_t i = blockIdx.x * MID_BLOCK + threadIdx.x; i < cnt; i += mid_grid * MID_BLOCK) {
             run_topic<MODE>(ix, ws, n, blob, offs, lst[i], st, o, &hits);
             if (MODE == MODE_COUNT && hits) atomicAdd((unsigned long long *)&ws.blk[lst[i] / TILE], hits);
         }
     } else {
-        const uint32_t lane = (blockIdx.x - MID_GRID) * 64 + threadIdx.x;   // < DEEP_LANES
+        const uint32_t lane = (blockIdx.x - mid_grid) * 64 + threadIdx.x;   // < DEEP_LANES
         const uint32_t cnt = ws.list_n[L_DEEP];
         const uint32_t *lst = ws.lists + (uint64_t)L_DEEP * n;
         GlobalStore st{ws.deep_wid + (uint64_t)lane * MAX_LEVELS, ws.deep_stk + (uint64_t)lane * (MAX_LEVELS + 1), 0};
@@ -1701,8 +1709,9 @@ hipError_t launch_match_phase1(const DevIndex &ix, const Workspace &ws, uint64_t
                                n, bytes, offs, o);
         if (ev_walk1 && (e = hipEventRecord(ev_walk1, s)) != hipSuccess) return e;
         // small batches: the tail kernel's last block also scans the (few) tile totals
-        hipLaunchKernelGGL(k_walk_tail<MODE_COUNT>, dim3(TAIL_GRID), dim3(MID_BLOCK), 0, s, ix, ws, n, bytes, offs, o,
-                           (uint64_t)nb, wave ? hit_offs : nullptr);
+        const uint32_t mg = wave ? MID_GRID : MID_GRID_BIG;
+        hipLaunchKernelGGL(k_walk_tail<MODE_COUNT>, dim3(mg + DEEP_LANES / 64), dim3(MID_BLOCK), 0, s, ix, ws, n,
+                           bytes, offs, o, (uint64_t)nb, wave ? hit_offs : nullptr, mg);
     }
     if (!wave) hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(1024), 0, s, ws.blk, (uint64_t)nb, hit_offs, n);
     return hipGetLastError();
@@ -1728,7 +1737,7 @@ hipError_t launch_first(const DevIndex &ix, const Workspace &ws, uint64_t n, con
         hipLaunchKernelGGL(k_walk_fast<MODE_FIRST>, dim3(blocks_for(n, WALK_BLOCK)), dim3(WALK_BLOCK), 0, s,
                            ix, ws, n, bytes, offs, o);
     hipLaunchKernelGGL(k_walk_tail<MODE_FIRST>, dim3(TAIL_GRID), dim3(MID_BLOCK), 0, s, ix, ws, n, bytes, offs, o,
-                       (uint64_t)0, nullptr);
+                       (uint64_t)0, nullptr, (uint32_t)MID_GRID);
     return hipGetLastError();
 }
 
