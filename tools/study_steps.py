@@ -35,6 +35,11 @@ def main():
         print(f"{cfg}: child-table probes {what[0]} mean {a.mean():.2f}, {what[1]} mean {b.mean():.2f} "
               f"(each capped at 15)", flush=True)
         return
+    if os.environ.get("TM_STUDY_LEAF2"):
+        imm, pop = (err & 15).astype(np.int64), (err >> 4).astype(np.int64)
+        print(f"{cfg}: visits of single-value leaves reached directly ('+' or the only literal child) mean "
+              f"{imm.mean():.2f}, off the pending-branch stack mean {pop.mean():.2f} (each capped at 15)", flush=True)
+        return
     if os.environ.get("TM_STUDY_LEAF"):
         ct, other = (err & 15).astype(np.int64), (err >> 4).astype(np.int64)
         print(f"{cfg}: visits at the topic's last level (emit only) reached through a child table mean "
