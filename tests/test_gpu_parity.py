@@ -1257,3 +1257,42 @@ def test_wide_node_bitmaps_follow_vocab_growth(torch_dev):
     assert_same(ix, o, ts)
     put([b"a/n%d/+" % k for k in new[:300]], [50_000 + k for k in new[:300]], 0)   # 113: the Bloom again
     assert_same(ix, o, ts)
+
+
+def test_emit_misaligned_and_short_output_buffers(torch_dev):
+    """Every emit path (run-by-run for long runs, the per-lane search for short
+    ones) with an output buffer that is not 16-B aligned and with a capacity
+    below the hit total: values up to the capacity equal the oracle's, and
+    nothing is written past it."""
+    torch = torch_dev
+    rnd = random.Random(3)
+    keys, vals, v = [], [], 0
+    for f in ["#", "a/#", "+/b/#", "a/+/c/#", "+/+/+/#"]:
+        for _ in range(rnd.choice([3, 37, 250])):
+            keys.append(f); vals.append(v); v += 1
+    for k in range(2000):
+        keys.append(f"a/{k}/c/+"); vals.append(v); v += 1
+    items = items_of([s.encode() for s in keys], vals)
+    ix, o = gpu_index(items), oracle_of(items)
+    tops = [b"a/%d/c/%d" % (rnd.randrange(2500), rnd.randrange(9)) for _ in range(3000)] + [b"x/b/c/d"] * 300
+    ts = items_of(tops)
+    _, _, ohit, ovals = o.match_batch(ts.blob, ts.offs)
+    total = int(ohit[-1])
+    dev = torch.device("cuda:0")
+    d_blob = torch.from_numpy(ts.blob).to(dev)
+    d_offs = torch.from_numpy(ts.offs.view(np.int64)).to(dev)
+    d_hit = torch.zeros(len(tops) + 1, dtype=torch.int64, device=dev)
+    d_err = torch.zeros(len(tops), dtype=torch.uint8, device=dev)
+    s = torch.cuda.current_stream().cuda_stream
+    guard = 4096
+    for shift, cap in [(1, total), (3, total), (0, total // 3 + 1), (1, total // 2 + 3)]:
+        buf = torch.full((shift + total + guard,), -7, dtype=torch.int32, device=dev)
+        ptr = buf.data_ptr() + 4 * shift              # 4-B aligned, not 16-B aligned for shift 1, 3
+        ix.match_batch_dev(len(tops), d_blob.data_ptr(), d_offs.data_ptr(), d_hit.data_ptr(), ptr, cap,
+                           d_err.data_ptr(), s)
+        torch.cuda.synchronize()
+        h = buf.cpu().numpy().view(np.uint32)
+        assert np.array_equal(d_hit.cpu().numpy().view(np.uint64), ohit)
+        assert np.array_equal(h[shift:shift + cap], ovals[:cap]), (shift, cap)
+        assert (h[:shift] == np.uint32(0xFFFFFFF9)).all() and (h[shift + cap:] == np.uint32(0xFFFFFFF9)).all(), \
+            (shift, cap, "written outside [0, cap)")
