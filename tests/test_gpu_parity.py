@@ -1296,3 +1296,31 @@ def test_emit_misaligned_and_short_output_buffers(torch_dev):
         assert np.array_equal(h[shift:shift + cap], ovals[:cap]), (shift, cap)
         assert (h[:shift] == np.uint32(0xFFFFFFF9)).all() and (h[shift + cap:] == np.uint32(0xFFFFFFF9)).all(), \
             (shift, cap, "written outside [0, cap)")
+
+
+def test_wide_threshold_flapping_under_churn(torch_dev):
+    """Nodes crossing the wide-node threshold (256 literal children) both ways,
+    many times, under interleaved subscribes and unsubscribes -- bitmap, Bloom
+    and child-table growth all rebuilt in place; exact against the oracle at
+    every step."""
+    rnd = random.Random(17)
+    ix, o = gpu_index(), Oracle()
+    live = set()
+    tops = items_of([b"r%d/w%d/x" % (a, b) for a in range(3) for b in range(0, 400, 3)] +
+                    [b"r%d/w%d" % (a, b) for a in range(3) for b in range(0, 400, 7)])
+    for step in range(24):
+        target = 300 if step % 2 == 0 else 200            # above / below 256 children
+        ops, strs, vals = [], [], []
+        for a in range(3):
+            mine = sorted(k for k in live if k[0] == a)
+            if len(mine) < target:
+                for b in rnd.sample([b for b in range(400) if (a, b) not in live], target - len(mine)):
+                    live.add((a, b)); ops.append(1); strs.append(b"r%d/w%d/+" % (a, b)); vals.append(a * 1000 + b)
+            else:
+                for (aa, b) in rnd.sample(mine, len(mine) - target):
+                    live.discard((aa, b)); ops.append(0); strs.append(b"r%d/w%d/+" % (aa, b)); vals.append(aa * 1000 + b)
+        d = items_of(strs, vals)
+        op = np.array(ops, np.uint8)
+        ix.apply(op, d.blob, d.offs, d.vals)
+        o.apply(op, d.blob, d.offs, d.vals)
+        assert_same(ix, o, tops)
