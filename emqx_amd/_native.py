@@ -23,7 +23,8 @@ TM_ORDER_TRAVERSAL, TM_ORDER_SORTED, TM_ORDER_UNIQUE = 0, 1, 2
 EXPORTS = ("tm_create", "tm_destroy", "tm_apply_deltas", "tm_sync", "tm_match_batch",
            "tm_match_batch_dev", "tm_first_batch", "tm_stats", "tm_profile_enable", "tm_profile_read",
            "tm_last_error", "tm_abi_version", "tm_merge_shards", "tm_host_alloc", "tm_host_free",
-           "tm_stream_release", "tm_match_batch_ex", "tm_match_batch_dev_ex", "tm_sort_segments")
+           "tm_stream_release", "tm_match_batch_ex", "tm_match_batch_dev_ex", "tm_sort_segments",
+           "tm_matches_filter")
 
 
 class NativeUnavailable(RuntimeError):
@@ -69,6 +70,7 @@ def load_library(path: Path | None = None):
         "tm_match_batch": (i32, [vp, u64, vp, vp, vp, vp, u64, vp]),
         "tm_match_batch_dev": (i32, [vp, u64, vp, vp, vp, vp, u64, vp, vp]),
         "tm_first_batch": (i32, [vp, u64, vp, vp, vp, vp]),
+        "tm_matches_filter": (i32, [vp, u64, vp, vp, vp, vp, u64, vp]),
         "tm_stats": (i32, [vp, C.POINTER(tm_stats_t)]),
         "tm_profile_enable": (i32, [vp, i32]),
         "tm_profile_read": (i32, [vp, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(u64), i32]),
@@ -239,6 +241,24 @@ class Index:
         found = np.zeros(max(n, 1), dtype=np.uint8)
         self._check(self._lib.tm_first_batch(self._h, n, _ptr(blob), _ptr(offs), _ptr(val), _ptr(found)))
         return val[:n], found[:n]
+
+    def matches_filter_batch(self, blob: np.ndarray, offs: np.ndarray):
+        """matches_filter/3 for n subscription filters on the device (tm_matches_filter):
+        -> (hit_offsets u64[n+1], values u32 in traversal order, err u8[n])."""
+        n = len(offs) - 1
+        blob = np.ascontiguousarray(blob, dtype=np.uint8)
+        offs = np.ascontiguousarray(offs, dtype=np.uint64)
+        hit = np.zeros(n + 1, dtype=np.uint64)
+        err = np.zeros(max(n, 1), dtype=np.uint8)
+        cap = 1024
+        while True:
+            out = np.zeros(max(cap, 1), dtype=np.uint32)
+            rc = self._lib.tm_matches_filter(self._h, n, _ptr(blob), _ptr(offs), _ptr(hit), _ptr(out), cap, _ptr(err))
+            if rc == TM_ECAP and int(hit[n]) > cap:
+                cap = int(hit[n])
+                continue
+            self._check(rc)
+            return hit, out[: int(hit[n])], err[:n]
 
     # ---- matching (device buffers, e.g. torch tensors' data_ptr())
     def match_batch_dev(self, n: int, d_blob: int, d_offs: int, d_hit: int, d_out: int, cap: int, d_err: int,

@@ -94,5 +94,10 @@ hipError_t launch_copy_values(const uint64_t *hit_offs, uint64_t n, const uint32
 // the device address runs[i].dst
 struct PatchRun { uint64_t dst; uint32_t src, n; };
 hipError_t launch_patch(const PatchRun *d_runs, const uint32_t *d_data, uint64_t n_runs, hipStream_t s);
+// matches_filter/3 over the term-ordered word-list keys (pass 1: hit == null, per-query counts; pass 2: values)
+hipError_t launch_matches_filter(uint64_t n, const uint32_t *qoff, const uint32_t *qr, const uint32_t *qbase,
+                                 const uint32_t *pool, const uint64_t *koff, const uint32_t *kval, uint64_t K,
+                                 uint32_t *cnt, const uint64_t *hit, uint32_t *out, uint64_t cap, uint8_t *err,
+                                 hipStream_t s);
 
 }  // namespace tmx

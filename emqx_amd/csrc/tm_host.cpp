@@ -140,6 +140,16 @@ struct tm_index {
     std::vector<uint64_t> depth_cnt, xlen_cnt;
 
     std::unordered_set<std::string> dead;
+    uint64_t key_gen = 0;   // bumped by every key operation (matches_filter's sorted keys follow it)
+    struct MfState {        // matches_filter/3: the word-list keys in term order (built on demand)
+        uint64_t gen = ~0ull, K = 0;
+        std::vector<std::string> words;   // distinct binary words, byte order
+        uint32_t *pool = nullptr, *val = nullptr; uint64_t *koff = nullptr;
+        uint32_t *q = nullptr; uint64_t qcap = 0;   // staging: query offsets, ranks, bases, counts
+        uint8_t *err = nullptr; uint64_t *hit = nullptr; uint32_t *out = nullptr;
+        uint64_t ecap = 0, ocap = 0, hcap = 0;
+        hipStream_t s = nullptr;
+    } mf;
     uint64_t n_wild = 0, n_exact = 0;
     uint64_t uploads = 0, patch_bytes = 0;
 
@@ -851,6 +861,7 @@ std::string dead_key(const uint8_t *f, uint32_t len, uint32_t v, uint8_t flags) 
 // one insert (ins = true) or delete of the key make_key(Filter, V)
 void key_op(tm_index *ix, bool ins, const uint8_t *f, uint32_t len, uint32_t v, uint8_t flags,
             std::vector<WordRef> &w, std::vector<uint32_t> &wids) {
+    ix->key_gen++;
     if (flags & TM_KEY_EMPTY_LIST) {   // [] never matches a topic (topics have >= 1 level)
         auto k = dead_key(nullptr, 0, v, TM_KEY_EMPTY_LIST);
         if (ins) ix->dead.insert(k); else ix->dead.erase(k);
@@ -1300,6 +1311,8 @@ int tm_create(const tm_options *opts, tm_index **out) {
     return TM_OK;
 }
 
+namespace { void mf_free_keys(tm_index::MfState &m); }
+
 int tm_destroy(tm_index *ix) {
     if (!ix) return TM_EINVAL;
     (void)hipSetDevice(ix->device);
@@ -1308,6 +1321,9 @@ int tm_destroy(tm_index *ix) {
                     ix->wbits.d};
     for (void *p : bufs) if (p) (void)hipFree(p);
     for (auto &l : ix->lanes) free_lane(*l);
+    mf_free_keys(ix->mf);
+    for (void *p : {(void *)ix->mf.q, (void *)ix->mf.err, (void *)ix->mf.hit, (void *)ix->mf.out}) if (p) (void)hipFree(p);
+    if (ix->mf.s) (void)hipStreamDestroy(ix->mf.s);
     for (auto &p : ix->patch) {
         if (p.dev) (void)hipFree(p.dev);
         if (p.pin) (void)hipHostFree(p.pin);
@@ -1750,6 +1766,200 @@ int tm_study_set_wids(tm_index *ix, const uint32_t *d_wids, uint64_t n) {
     return TM_OK;
 }
 #endif
+
+// ------------------------------------------------------- matches_filter/3
+
+}  // extern "C"
+
+namespace {
+
+void mf_words_of(const uint8_t *p, uint32_t n, std::vector<std::string> &out) {
+    out.clear();
+    uint32_t s0 = 0;
+    for (uint32_t i = 0; i <= n; i++)
+        if (i == n || p[i] == '/') { out.emplace_back(reinterpret_cast<const char *>(p) + s0, i - s0); s0 = i + 1; }
+}
+
+// rank of a word: '#' 0, '+' 1, a binary word 3 + 2 i if it is words[i], else
+// 2 + 2 i (i = the words before it): term order (atoms < binaries, bytes)
+uint32_t mf_rank(const std::vector<std::string> &words, const std::string &w) {
+    if (w == "#") return 0;
+    if (w == "+") return 1;
+    const auto it = std::lower_bound(words.begin(), words.end(), w);
+    const uint32_t i = (uint32_t)(it - words.begin());
+    return it != words.end() && *it == w ? 3 + 2 * i : 2 + 2 * i;
+}
+
+void mf_free_keys(tm_index::MfState &m) {
+    if (m.pool) (void)hipFree(m.pool);
+    if (m.koff) (void)hipFree(m.koff);
+    if (m.val) (void)hipFree(m.val);
+    m.pool = nullptr; m.koff = nullptr; m.val = nullptr; m.K = 0;
+}
+
+// the word-list keys (trie terminals + keys that never match a topic) as rank
+// sequences sorted by (ranks, value) -- emqx_trie_search's ordered_set order
+int mf_build(tm_index *ix) {
+    auto &m = ix->mf;
+    if (m.gen == ix->key_gen && m.pool) return TM_OK;
+    std::vector<std::string> words;
+    std::string tmp;
+    std::vector<uint32_t> vwid;
+    for (const VocabEntry &e : ix->vocab.h)
+        if (e.wid != NONE) { vocab_bytes(ix, e, tmp); words.push_back(tmp); vwid.push_back(e.wid); }
+    std::vector<std::string> dw;
+    for (const std::string &k : ix->dead) {
+        if ((uint8_t)k[0] & TM_KEY_EMPTY_LIST) continue;
+        mf_words_of(reinterpret_cast<const uint8_t *>(k.data()) + 5, (uint32_t)k.size() - 5, dw);
+        for (auto &x : dw) if (x != "+" && x != "#") words.push_back(x);
+    }
+    std::vector<std::string> sorted = words;
+    std::sort(sorted.begin(), sorted.end());
+    sorted.erase(std::unique(sorted.begin(), sorted.end()), sorted.end());
+    std::vector<uint32_t> rank_of(ix->wid_next + 1, 0);
+    for (size_t i = 0; i < vwid.size(); i++) rank_of[vwid[i]] = mf_rank(sorted, words[i]);
+    // keys: (offset into pool, length, value)
+    std::vector<uint32_t> pool;
+    struct K { uint64_t off; uint32_t len, val; };
+    std::vector<K> keys;
+    auto add_run = [&](const std::vector<uint32_t> &path, uint32_t roff, uint32_t cnt) {
+        for (uint32_t i = 0; i < cnt; i++) {
+            keys.push_back(K{pool.size(), (uint32_t)path.size(), ix->vals.h[roff + i]});
+            pool.insert(pool.end(), path.begin(), path.end());
+        }
+    };
+    std::vector<std::pair<uint32_t, uint32_t>> st{{ROOT, 0}};   // (node, depth)
+    std::vector<uint32_t> path;
+    while (!st.empty()) {
+        const auto [node, d] = st.back();
+        st.pop_back();
+        path.resize(d);
+        if (node != ROOT) path.push_back(ix->aux[node].is_plus ? 1u : rank_of[ix->aux[node].wid]);
+        const Node &n = ix->nodes.h[node];
+        const NodeAux &a = ix->aux[node];
+        if (n.exact_cnt & RUN_CNT) add_run(path, a.exact_roff, n.exact_cnt & RUN_CNT);
+        if (n.hash_cnt & RUN_CNT) {
+            path.push_back(0);
+            add_run(path, a.hash_roff, n.hash_cnt & RUN_CNT);
+            path.pop_back();
+        }
+        const uint32_t cd = node == ROOT ? 0 : d + 1;
+        if (n.plus != NONE) st.push_back({n.plus, cd});
+        if (n.nlit <= KINL) {
+            for (uint32_t k = 0; k < KINL; k++) if (n.kw[k] != NONE) st.push_back({n.kc[k], cd});
+        } else {
+            for (uint32_t i = 0; i <= n.kw[1]; i++) {
+                const CSlot &c = ix->ctab.h[n.kw[0] + i];
+                if (c.wid != NONE) st.push_back({c.child, cd});
+            }
+        }
+    }
+    for (const std::string &k : ix->dead) {
+        uint32_t v;
+        memcpy(&v, k.data() + 1, 4);
+        std::vector<uint32_t> r;
+        if (!((uint8_t)k[0] & TM_KEY_EMPTY_LIST)) {
+            mf_words_of(reinterpret_cast<const uint8_t *>(k.data()) + 5, (uint32_t)k.size() - 5, dw);
+            for (auto &x : dw) r.push_back(mf_rank(sorted, x));
+        }
+        keys.push_back(K{pool.size(), (uint32_t)r.size(), v});
+        pool.insert(pool.end(), r.begin(), r.end());
+    }
+    std::sort(keys.begin(), keys.end(), [&](const K &x, const K &y) {
+        const uint32_t m2 = std::min(x.len, y.len);
+        for (uint32_t i = 0; i < m2; i++)
+            if (pool[x.off + i] != pool[y.off + i]) return pool[x.off + i] < pool[y.off + i];
+        if (x.len != y.len) return x.len < y.len;
+        return x.val < y.val;
+    });
+    std::vector<uint32_t> spool;
+    spool.reserve(pool.size());
+    std::vector<uint64_t> koff(keys.size() + 1, 0);
+    std::vector<uint32_t> kval(keys.size());
+    for (size_t i = 0; i < keys.size(); i++) {
+        koff[i] = spool.size();
+        spool.insert(spool.end(), pool.begin() + keys[i].off, pool.begin() + keys[i].off + keys[i].len);
+        kval[i] = keys[i].val;
+    }
+    koff[keys.size()] = spool.size();
+    mf_free_keys(m);
+    HIPCHK(ix, hipMalloc(&m.pool, std::max<size_t>(spool.size(), 1) * 4));
+    HIPCHK(ix, hipMalloc(&m.koff, koff.size() * 8));
+    HIPCHK(ix, hipMalloc(&m.val, std::max<size_t>(kval.size(), 1) * 4));
+    if (!spool.empty()) HIPCHK(ix, hipMemcpy(m.pool, spool.data(), spool.size() * 4, hipMemcpyHostToDevice));
+    HIPCHK(ix, hipMemcpy(m.koff, koff.data(), koff.size() * 8, hipMemcpyHostToDevice));
+    if (!kval.empty()) HIPCHK(ix, hipMemcpy(m.val, kval.data(), kval.size() * 4, hipMemcpyHostToDevice));
+    m.K = keys.size();
+    m.words.swap(sorted);
+    m.gen = ix->key_gen;
+    return TM_OK;
+}
+
+template <class T>
+int mf_grow(tm_index *ix, T *&p, uint64_t &cap, uint64_t need) {
+    if (need <= cap && p) return TM_OK;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = std::max<uint64_t>(need + need / 2, 1024);
+    HIPCHK(ix, hipMalloc(&p, cap * sizeof(T)));
+    return TM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int tm_matches_filter(tm_index *ix, uint64_t n, const uint8_t *fb, const uint64_t *fo, uint64_t *out_hit_offsets,
+                      uint32_t *out_values, uint64_t cap, uint8_t *out_err) {
+    if (!ix) return fail(nullptr, TM_EINVAL, "tm_matches_filter: null handle");
+    if (!fo || !out_hit_offsets || !out_err || (n && !fb && fo[n] != fo[0]) || (cap && !out_values))
+        return fail(ix, TM_EINVAL, "tm_matches_filter: null buffer");
+    if (n >= 0xFFFFFFFFull) return fail(ix, TM_EINVAL, "tm_matches_filter: batch too large");
+    std::lock_guard<std::mutex> g(ix->mu);   // control plane: one call at a time
+    HIPCHK(ix, hipSetDevice(ix->device));
+    auto &m = ix->mf;
+    if (!m.s) HIPCHK(ix, hipStreamCreateWithFlags(&m.s, hipStreamNonBlocking));
+    int rc;
+    if ((rc = mf_build(ix))) return rc;
+    // queries: filter_words/1 (:359-366) -> ranks; base_init on a '$' first word
+    std::vector<uint32_t> qoff(n + 1, 0), qr, qbase(n, NONE);
+    std::vector<std::string> w;
+    for (uint64_t i = 0; i < n; i++) {
+        mf_words_of(fb + fo[i], (uint32_t)(fo[i + 1] - fo[i]), w);
+        for (auto &x : w) qr.push_back(mf_rank(m.words, x));
+        if (!w[0].empty() && w[0][0] == '$' && w[0] != "+" && w[0] != "#") qbase[i] = mf_rank(m.words, w[0]);
+        qoff[i + 1] = (uint32_t)qr.size();
+    }
+    const uint64_t qwords = (n + 1) + qr.size() + n + n;   // offsets, ranks, bases, counts
+    if ((rc = mf_grow(ix, m.q, m.qcap, qwords))) return rc;
+    if ((rc = mf_grow(ix, m.err, m.ecap, n + 1))) return rc;
+    if ((rc = mf_grow(ix, m.hit, m.hcap, n + 1))) return rc;
+    uint32_t *d_qoff = m.q, *d_qr = m.q + n + 1, *d_qbase = d_qr + qr.size(), *d_cnt = d_qbase + n;
+    HIPCHK(ix, hipMemcpyAsync(d_qoff, qoff.data(), (n + 1) * 4, hipMemcpyHostToDevice, m.s));
+    if (!qr.empty()) HIPCHK(ix, hipMemcpyAsync(d_qr, qr.data(), qr.size() * 4, hipMemcpyHostToDevice, m.s));
+    if (n) HIPCHK(ix, hipMemcpyAsync(d_qbase, qbase.data(), n * 4, hipMemcpyHostToDevice, m.s));
+    HIPCHK(ix, hipMemsetAsync(m.err, 0, n + 1, m.s));
+    HIPCHK(ix, launch_matches_filter(n, d_qoff, d_qr, d_qbase, m.pool, m.koff, m.val, m.K, d_cnt, nullptr, nullptr,
+                                     0, m.err, m.s));
+    std::vector<uint32_t> cnt(n);
+    if (n) HIPCHK(ix, hipMemcpyAsync(cnt.data(), d_cnt, n * 4, hipMemcpyDeviceToHost, m.s));
+    HIPCHK(ix, hipStreamSynchronize(m.s));
+    out_hit_offsets[0] = 0;
+    for (uint64_t i = 0; i < n; i++) out_hit_offsets[i + 1] = out_hit_offsets[i] + cnt[i];
+    const uint64_t total = out_hit_offsets[n];
+    if (total && cap) {
+        const uint64_t wcap = std::min(total, cap);
+        if ((rc = mf_grow(ix, m.out, m.ocap, wcap))) return rc;
+        HIPCHK(ix, hipMemcpyAsync(m.hit, out_hit_offsets, (n + 1) * 8, hipMemcpyHostToDevice, m.s));
+        HIPCHK(ix, launch_matches_filter(n, d_qoff, d_qr, d_qbase, m.pool, m.koff, m.val, m.K, d_cnt, m.hit, m.out,
+                                         wcap, m.err, m.s));
+        HIPCHK(ix, hipMemcpyAsync(out_values, m.out, wcap * 4, hipMemcpyDeviceToHost, m.s));
+    }
+    if (n) HIPCHK(ix, hipMemcpyAsync(out_err, m.err, n, hipMemcpyDeviceToHost, m.s));
+    HIPCHK(ix, hipStreamSynchronize(m.s));
+    if (total > cap) return fail(ix, TM_ECAP, "tm_matches_filter: output capacity too small");
+    return TM_OK;
+}
 
 int tm_stats(tm_index *ix, tm_stats_t *o) {
     if (!ix || !o) return fail(ix, TM_EINVAL, "tm_stats: null argument");

@@ -1766,6 +1766,110 @@ hipError_t launch_copy_values(const uint64_t *hit_offs, uint64_t n, const uint32
     return hipGetLastError();
 }
 
+// ------------------------------------------------------- matches_filter/3
+//
+// emqx_topic_index:matches_filter/3 -> emqx_trie_search:search/3 with
+// [topic_filter] (:186-189): the ordered walk over the key set with the filter
+// clauses of compare/3 (:291-300).  Its result depends on where that walk stops
+// (a query '+' passes a stored word without leaving a seek point, so one
+// stored key above the query ends the whole search), so it runs on the keys in
+// Erlang term order, not on the trie: the word-list keys as sequences of word
+// ranks ('#' = 0, '+' = 1, binary words 3 + 2 i in byte order; a query word
+// the index lacks ranks 2 + 2 i, between its neighbours), sorted by (ranks,
+// value), with the reference's seeks as binary searches.  Binary keys sort
+// after every list and compare `lower` (:260-261): the walk ends at the last
+// list key.  One thread per query; pass 1 counts, pass 2 writes.
+struct MfSeek { uint64_t ks; uint32_t pos, w; bool fin; };   // key ks's first pos ranks, then w if fin
+
+__device__ __forceinline__ int mf_cmp(const uint32_t *pool, const uint64_t *koff, uint64_t k, const MfSeek &sk) {
+    const uint64_t a0 = koff[k], kl = koff[k + 1] - a0;
+    const uint64_t b0 = sk.ks == ~0ull ? 0 : koff[sk.ks];
+    const uint64_t sl = sk.pos + (sk.fin ? 1 : 0);
+    const uint64_t m = kl < sl ? kl : sl;
+    for (uint64_t i = 0; i < m; i++) {
+        const uint32_t a = pool[a0 + i], b = i < sk.pos ? pool[b0 + i] : sk.w;
+        if (a != b) return a < b ? -1 : 1;
+    }
+    return kl < sl ? -1 : kl == sl ? 0 : 1;
+}
+
+__device__ __forceinline__ uint64_t mf_lower_bound(const uint32_t *pool, const uint64_t *koff, uint64_t K,
+                                                   const MfSeek &sk) {
+    uint64_t lo = 0, hi = K;
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (mf_cmp(pool, koff, mid, sk) < 0) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+
+constexpr int64_t MF_FULL = -1, MF_PREFIX = -2, MF_LOWER = -3;
+
+// compare/3 with a filter as the query (tm_oracle.c compare_filter restates
+// the clauses; ranks as above)
+__device__ __forceinline__ int64_t mf_compare(const uint32_t *pool, const uint64_t *koff, uint64_t k,
+                                              const uint32_t *q, uint32_t nq) {
+    const uint64_t a0 = koff[k];
+    const uint32_t kl = (uint32_t)(koff[k + 1] - a0);
+    int64_t lastplus = -1;
+    for (uint32_t i = 0;; i++) {
+        if (i == kl) return i == nq ? MF_FULL : MF_PREFIX;          // :262-281
+        const uint32_t f = pool[a0 + i];
+        if (f == 0 && i == kl - 1) return MF_FULL;                  // stored '#' last, :282-290
+        if (i < nq && q[i] == 0 && i == nq - 1) return MF_FULL;     // query '#' last, :292-293
+        if (i == nq) break;                                         // :333-340
+        if (q[i] == 1) continue;                                    // query '+', :294-300
+        if (f == 1) { lastplus = i; continue; }                     // stored '+', :302-320
+        if (f == q[i]) continue;                                    // :321-324
+        if (f > q[i]) break;                                        // :325-332
+        return (int64_t)i;                                          // seek, :341-348
+    }
+    return lastplus >= 0 ? lastplus : MF_LOWER;
+}
+
+__global__ __launch_bounds__(64) void k_matches_filter(uint64_t n, const uint32_t *qoff, const uint32_t *qr,
+                                                       const uint32_t *qbase, const uint32_t *pool,
+                                                       const uint64_t *koff, const uint32_t *kval, uint64_t K,
+                                                       uint32_t *cnt, const uint64_t *hit, uint32_t *out,
+                                                       uint64_t cap, uint8_t *err) {
+    const uint64_t t = (uint64_t)blockIdx.x * 64 + threadIdx.x;
+    if (t >= n) return;
+    const uint32_t *q = qr + qoff[t];
+    const uint32_t nq = qoff[t + 1] - qoff[t];
+    // base_init (:160-163): a query whose first word starts with '$' starts at base([W0])
+    MfSeek sk{~0ull, 0, qbase[t], qbase[t] != NONE};
+    uint64_t cur = mf_lower_bound(pool, koff, K, sk);
+    uint64_t o = hit ? hit[t] : 0, c = 0;
+    const uint64_t limit = 2 * K + 64;   // every step moves forward; a bound every thread reaches regardless
+    for (uint64_t steps = 0; cur < K; steps++) {
+        if (steps > limit) { err[t] = 1; break; }
+        const int64_t r = mf_compare(pool, koff, cur, q, nq);
+        if (r == MF_FULL) {
+            if (hit && o < cap) out[o] = kval[cur];
+            o++; c++; cur++;
+        } else if (r == MF_PREFIX) {
+            cur++;
+        } else if (r == MF_LOWER) {
+            break;
+        } else {
+            const MfSeek s2{cur, (uint32_t)r, q[r], true};
+            const uint64_t nx = mf_lower_bound(pool, koff, K, s2);
+            cur = nx > cur ? nx : cur + 1;   // a seek target is above the current key (:341-348)
+        }
+    }
+    if (!hit) cnt[t] = (uint32_t)c;
+}
+
+hipError_t launch_matches_filter(uint64_t n, const uint32_t *qoff, const uint32_t *qr, const uint32_t *qbase,
+                                 const uint32_t *pool, const uint64_t *koff, const uint32_t *kval, uint64_t K,
+                                 uint32_t *cnt, const uint64_t *hit, uint32_t *out, uint64_t cap, uint8_t *err,
+                                 hipStream_t s) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_matches_filter, dim3(blocks_for(n, 64)), dim3(64), 0, s, n, qoff, qr, qbase, pool, koff,
+                       kval, K, cnt, hit, out, cap, err);
+    return hipGetLastError();
+}
+
 hipError_t launch_patch(const PatchRun *d_runs, const uint32_t *d_data, uint64_t n, hipStream_t s) {
     if (!n) return hipSuccess;
     hipLaunchKernelGGL(k_patch, dim3(blocks_for(n * 16, 256)), dim3(256), 0, s, d_runs, d_data, n);

@@ -228,11 +228,20 @@ def matches_filter(filter_, tab: Tab, opts=()):
     ordered search (filter_words/1, base_init/1, compare/3 with the filter
     clauses :291-300, no match_topics phase -- binary keys never match).
 
-    A host-side call over the table's ordered key set, not the publish path:
-    its result depends on where the ordered walk stops (a stored key below the
-    query at a query '+' ends the whole search), which the device NFA walk has
-    no notion of.  Callers are control-plane (durable-storage stream
-    discovery, emqx_ds_new_streams.erl:325)."""
+    Its result depends on where the ordered walk stops (a stored key below the
+    query at a query '+' ends the whole search), which the trie walk has no
+    notion of, so the device runs the reference's walk itself over the keys in
+    term order (tm_matches_filter).  Keys the device does not hold (binary
+    words '+'/'#' or words containing '/', kept host-side) take their place in
+    that order too: a table holding any, or a word-list query, runs the same
+    walk on the host over the table's ordered key set.  Callers are
+    control-plane (durable-storage stream discovery,
+    emqx_ds_new_streams.erl:325)."""
+    if not tab._dead and isinstance(filter_, (bytes, bytearray)):
+        tab.flush()
+        blob, offs = _native.pack_strings([bytes(filter_)])
+        _, vals, _ = tab._index.matches_filter_batch(blob, offs)
+        return _finish([tab._keys[int(v)] for v in vals], opts)
     keys, order = tab.sorted_keys()
     return _finish(search_filter(keys, order, filter_words(filter_)), opts)
 

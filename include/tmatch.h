@@ -178,6 +178,18 @@ int tm_stream_release(tm_index *h, void *stream);
 int tm_first_batch(tm_index *h, uint64_t n, const uint8_t *topic_bytes, const uint64_t *topic_offsets,
                    uint32_t *out_value, uint8_t *out_found);
 
+/* emqx_topic_index:matches_filter/3 (emqx_topic_index.erl:82-84 ->
+ * emqx_trie_search.erl:186-189, filter clauses :291-300): for each of n
+ * subscription filters, the values of the word-list keys the reference's
+ * ordered search returns, in traversal order (the reference's list is the
+ * reverse).  Runs on the device over the keys in Erlang term order (rebuilt
+ * after key changes; seconds at 10M keys -- a control-plane call).  Host
+ * buffers; out_hit_offsets[n+1] always written; TM_ECAP when the values do
+ * not fit `cap` (the first `cap` are written).  out_err[i] = 1 if filter i's
+ * walk exceeded its step bound (never for a valid filter). */
+int tm_matches_filter(tm_index *h, uint64_t n, const uint8_t *filter_bytes, const uint64_t *filter_offsets,
+                      uint64_t *out_hit_offsets, uint32_t *out_values, uint64_t cap, uint8_t *out_err);
+
 int tm_stats(tm_index *h, tm_stats_t *out);
 
 /* Filter-sharded merge (device buffers, asynchronous on `stream`; runs on the

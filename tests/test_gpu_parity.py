@@ -1324,3 +1324,43 @@ def test_wide_threshold_flapping_under_churn(torch_dev):
         ix.apply(op, d.blob, d.offs, d.vals)
         o.apply(op, d.blob, d.offs, d.vals)
         assert_same(ix, o, tops)
+
+
+def test_matches_filter_on_device_vs_oracle(torch_dev):
+    """tm_matches_filter (the reference's ordered filter search on the device
+    over the keys in term order) against the known answers derived from
+    compare/3's clauses and against the C oracle on random key sets (binary
+    keys, word-list keys, '+'/'#' anywhere in stored keys, '$' words)."""
+    from test_matches_filter_cpu import KNOWN, _rand_filter
+    for filters, query, expect in KNOWN:
+        ix = gpu_index(items_of(filters))
+        blob, offs = _native.pack_strings([query])
+        hit, vals, err = ix.matches_filter_batch(blob, offs)
+        assert vals.tolist() == expect and not err.any(), (filters, query)
+    for seed in range(6):
+        r = random.Random(0x454D5158 + 500 + seed)
+        filters = [_rand_filter(r, r.randint(1, 5), [6, 2, 1]) for _ in range(300)]
+        wf = np.array([1 if r.random() < 0.1 else 0 for _ in filters], np.uint8)
+        items = items_of(filters)
+        ix = gpu_index()
+        ix.apply(np.ones(len(items), np.uint8), items.blob, items.offs, items.vals, wf)
+        o = Oracle()
+        for i, f in enumerate(filters):
+            o.insert(f, i, int(wf[i]))
+        qs = [_rand_filter(r, r.randint(1, 5), [4, 3, 1], hash_last=True) for _ in range(200)]
+        blob, offs = _native.pack_strings(qs)
+        hit, vals, err = ix.matches_filter_batch(blob, offs)
+        assert not err.any()
+        for i, q in enumerate(qs):
+            assert vals[hit[i]:hit[i + 1]].tolist() == o.matches_filter(q), (seed, q)
+    # deltas after a call: the term-ordered key array follows them
+    ix = gpu_index(items_of([b"a/+/c", b"a/#"]))
+    blob, offs = _native.pack_strings([b"a/+/c"])
+    assert ix.matches_filter_batch(blob, offs)[1].tolist() == [1, 0]
+    d = items_of([b"a/b/x/#", b"a/z/c/#"], [7, 9])
+    ix.apply(np.ones(2, np.uint8), d.blob, d.offs, d.vals)
+    # a/b/x/# is above a/+/c at the query's '+' level: the walk ends there and never reaches a/z/c/#
+    assert ix.matches_filter_batch(blob, offs)[1].tolist() == [1, 0]
+    d = items_of([b"a/b/x/#"], [7])
+    ix.apply(np.zeros(1, np.uint8), d.blob, d.offs, d.vals)
+    assert ix.matches_filter_batch(blob, offs)[1].tolist() == [1, 0, 9]
