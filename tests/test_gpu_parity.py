@@ -1364,3 +1364,30 @@ def test_matches_filter_on_device_vs_oracle(torch_dev):
     d = items_of([b"a/b/x/#"], [7])
     ix.apply(np.zeros(1, np.uint8), d.blob, d.offs, d.vals)
     assert ix.matches_filter_batch(blob, offs)[1].tolist() == [1, 0, 9]
+
+
+def test_ds_beamformer_waitq_known_answers(torch_dev):
+    """emqx_ds_beamformer_waitq (the durable-storage consumer with a custom
+    NextF, emqx_ds_beamformer_waitq.erl:43-62): per-stream matching on the
+    device, pinned by the reference module's own topic_match_test (:66-105)."""
+    from emqx_amd import waitq
+    from emqx_amd.trie_search import PLUS
+    tab = waitq.new()
+    waitq.insert("s1", [b"foo", PLUS], 1, ("val", 1), tab)
+    waitq.insert("s1", [b"foo", b"bar"], 2, ("val", 2), tab)
+    waitq.insert("s1", [b"1", b"2"], 3, ("val", 3), tab)
+    waitq.insert("s2", [b"foo", PLUS], 4, ("val", 4), tab)
+    waitq.insert("s2", [b"foo", b"bar"], 5, ("val", 5), tab)
+    waitq.insert("s2", [b"1", b"2"], 6, ("val", 6), tab)
+    assert sorted(waitq.matches("s1", [b"foo", b"2"], tab)) == [("val", 1)]
+    assert sorted(waitq.matches("s2", [b"foo", b"2"], tab)) == [("val", 4)]
+    assert sorted(waitq.matches("s1", [b"foo", b"bar"], tab)) == [("val", 1), ("val", 2)]
+    assert sorted(waitq.matches("s2", [b"foo", b"bar"], tab)) == [("val", 4), ("val", 5)]
+    assert waitq.matches("s3", [b"foo", b"bar"], tab) == []
+    assert waitq.matches("s1", [b"1", b"2"], tab) == [("val", 3)]
+    assert waitq.matches("s2", [b"1", b"2"], tab) == [("val", 6)]
+    # delete/4, and an insert of an existing key replaces its record (ets:insert on a set)
+    waitq.delete("s1", [b"foo", PLUS], 1, tab)
+    waitq.insert("s1", [b"foo", b"bar"], 2, ("val", 22), tab)
+    assert sorted(waitq.matches("s1", [b"foo", b"bar"], tab)) == [("val", 22)]
+    assert waitq.matches("s1", b"foo/2", tab) == []
