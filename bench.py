@@ -129,10 +129,20 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # TM_BENCH_DIST_BACKEND=gloo rehearses the N > 1 path with several ranks on
+    # one GPU (the timing collectives then run on host tensors); the driver's
+    # multi-GPU runs use the default, RCCL.
+    backend = os.environ.get("TM_BENCH_DIST_BACKEND", "nccl")
+    if backend != "nccl":
+        local %= torch.cuda.device_count()
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device(f"cuda:{local}")
+    cdev = dev if backend == "nccl" else torch.device("cpu")   # where the timing collectives' tensors live
 
     from emqx_amd import _native, shard, workload as wl
     from emqx_amd.build import source_hash
@@ -318,7 +328,7 @@ def main():
     torch.cuda.synchronize()
     iso_walk_ms, iso_batch_ms, iso_nb = ix.profile_read(reset=True)
     ix.profile(False)
-    el_t = torch.tensor([el], dtype=torch.float64, device=dev)
+    el_t = torch.tensor([el], dtype=torch.float64, device=cdev)
     if world > 1:
         dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
     el_max = float(el_t.item())
@@ -367,7 +377,7 @@ def main():
     if world > 1 and lat:
         # the slowest rank's percentiles (max over ranks)
         keys = sorted(lat)
-        v = torch.tensor([lat[k][q] for k in keys for q in ("p50_ms", "p99_ms")], dtype=torch.float64, device=dev)
+        v = torch.tensor([lat[k][q] for k in keys for q in ("p50_ms", "p99_ms")], dtype=torch.float64, device=cdev)
         dist.all_reduce(v, op=dist.ReduceOp.MAX)
         v = v.tolist()
         lat = {k: {"p50_ms": v[2 * i], "p99_ms": v[2 * i + 1]} for i, k in enumerate(keys)}
