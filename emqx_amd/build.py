@@ -62,16 +62,19 @@ def build_tmatch(force: bool = False) -> Path:
     return LIB_TMATCH
 
 
-def build_variant(name: str, defines=(), force: bool = False) -> Path:
-    """An experimental build of libtmatch with extra -D flags (perf studies:
-    tools/gpu_variants.sh loads it through TM_LIB).  Not the product library."""
+def build_variant(name: str, kernel_src: str | None = None, force: bool = False) -> Path:
+    """An experimental build of libtmatch (perf studies: tools/gpu_variants.sh
+    loads it through TM_LIB).  `kernel_src` replaces tm_kernels.hip with a
+    study copy (e.g. under emqx_amd/study/, not tracked), so experiments never
+    put switches into the product source.  Not the product library."""
     out = PKG / "variants" / f"libtmatch_{name}.so"
     out.parent.mkdir(exist_ok=True)
-    srcs = [CSRC / "tm_host.cpp", CSRC / "tm_kernels.hip"]
+    kern = Path(kernel_src) if kernel_src else CSRC / "tm_kernels.hip"
+    srcs = [CSRC / "tm_host.cpp", kern]
     deps = srcs + [CSRC / "tm_layout.h", CSRC / "tm_dev.h", ROOT / "include" / "tmatch.h"]
     if force or _stale(out, deps):
         _run(["hipcc", "-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-shared", "-Wall",
-              "-Wno-unused-function", "-o", str(out)] + [f"-D{d}" for d in defines] + [str(s) for s in srcs])
+              "-Wno-unused-function", f"-I{CSRC}", "-o", str(out)] + [str(s) for s in srcs])
     return out
 
 

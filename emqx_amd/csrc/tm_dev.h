@@ -23,16 +23,9 @@ struct DevIndex {
     // exists (xlen_mask bit L for L < 64, L <= xlen_max beyond): need_levels().
     uint32_t depth, xlen_max;
     uint64_t xlen_mask;
-#ifdef TM_STUDY_HOSTWIDS
-    const uint32_t *study_wids;   // study build: level-major wids of the batch, looked up on the host
-    uint64_t study_n;
-#endif
 };
 
-#ifndef TM_FAST_L
-#define TM_FAST_L 8
-#endif
-constexpr int FAST_L = TM_FAST_L; // levels handled by the main walk kernel (LDS frontier)
+constexpr int FAST_L = 8;        // levels handled by the main walk kernel (LDS frontier)
 
 // levels of an L-level topic whose words a walk must resolve (see DevIndex)
 __host__ __device__ __forceinline__ uint32_t need_levels(const DevIndex &ix, uint32_t L) {
@@ -41,10 +34,7 @@ __host__ __device__ __forceinline__ uint32_t need_levels(const DevIndex &ix, uin
 }
 constexpr int MID_L = 32;        // levels handled by the list kernels with an LDS frontier
 constexpr int MAX_LEVELS = 65536;// MQTT topics are <= 65535 bytes
-#ifndef RCAP_N
-#define RCAP_N 8
-#endif
-constexpr int RCAP = RCAP_N;          // terminal ranges kept per topic before the re-walk path
+constexpr int RCAP = 8;          // terminal ranges kept per topic before the re-walk path
 constexpr int DEEP_LANES = 64;   // lanes of the global-scratch (deep / overflow) kernels
 
 enum { L_MID = 0, L_DEEP = 1, L_OVF_MID = 2, L_OVF_DEEP = 3, L_COUNT = 4 };

@@ -163,9 +163,6 @@ struct tm_index {
     struct Pinned { uint8_t *host, *dev; uint64_t size; };
     std::vector<Pinned> pinned;
 
-#ifdef TM_STUDY_HOSTWIDS
-    const uint32_t *study_wids = nullptr; uint64_t study_n = 0;
-#endif
     // diagnostics (tm_profile_*)
     bool prof = false;
     struct ProfEv { hipEvent_t b0, w0, w1, b1; };
@@ -251,9 +248,7 @@ void vocab_bytes(tm_index *ix, const VocabEntry &e, std::string &out) {
     }
 }
 
-#ifndef TM_VOCAB_LOAD_SHIFT
-#define TM_VOCAB_LOAD_SHIFT 2
-#endif
+constexpr uint32_t VOCAB_LOAD_SHIFT = 2;   // vocab load <= 1/4
 uint64_t vocab_entry_hash(tm_index *ix, const VocabEntry &e) {
     std::string w;
     vocab_bytes(ix, e, w);
@@ -278,8 +273,8 @@ void wide_cover(tm_index *ix);
 void vocab_grow(tm_index *ix, uint64_t need) {
     // load <= 1/4: the walk's deferred probes resolve on the first slot
     // almost always (one round trip per topic for all its levels)
-    if ((need << TM_VOCAB_LOAD_SHIFT) <= ix->vocab.h.size()) return;
-    vocab_rehash(ix, pow2_at_least(need << TM_VOCAB_LOAD_SHIFT));
+    if ((need << VOCAB_LOAD_SHIFT) <= ix->vocab.h.size()) return;
+    vocab_rehash(ix, pow2_at_least(need << VOCAB_LOAD_SHIFT));
 }
 
 uint32_t vocab_intern(tm_index *ix, const uint8_t *p, uint32_t n) {
@@ -828,8 +823,8 @@ void reclaim(tm_index *ix) {
         ix->exact.dirty.set_all();
     }
     const uint64_t vmin = 1024;
-    if (ix->vocab.h.size() > vmin && (ix->vcount << (TM_VOCAB_LOAD_SHIFT + 2)) < ix->vocab.h.size())
-        vocab_rehash(ix, std::max<uint64_t>(vmin, pow2_at_least(std::max<uint64_t>(ix->vcount, 1) << TM_VOCAB_LOAD_SHIFT)));
+    if (ix->vocab.h.size() > vmin && (ix->vcount << (VOCAB_LOAD_SHIFT + 2)) < ix->vocab.h.size())
+        vocab_rehash(ix, std::max<uint64_t>(vmin, pow2_at_least(std::max<uint64_t>(ix->vcount, 1) << VOCAB_LOAD_SHIFT)));
     if (ix->exact.h.size() > 1024 && ix->xcount * 8 < ix->exact.h.size())
         exact_rehash(ix, std::max<uint32_t>(1024, pow2_at_least(ix->xcount * 2)));
 }
@@ -966,6 +961,8 @@ void key_op(tm_index *ix, bool ins, const uint8_t *f, uint32_t len, uint32_t v, 
 
 // ------------------------------------------------------------- device side
 
+constexpr uint64_t DEV_GUARD = 16;   // device elements kept allocated past the host size (see collect)
+
 template <class T>
 int upload_full(tm_index *ix, Mirror<T> &m) {
     uint64_t need = std::max<uint64_t>(m.h.size(), 1);
@@ -975,7 +972,7 @@ int upload_full(tm_index *ix, Mirror<T> &m) {
     if (need > m.dcap) {
         if (m.d) HIPCHK(ix, hipFree(m.d));
         m.d = nullptr;
-        uint64_t cap = need + need / 2 + 16;
+        uint64_t cap = need + need / 2 + DEV_GUARD;
         HIPCHK(ix, hipMalloc(&m.d, cap * sizeof(T)));
         m.dcap = cap;
     }
@@ -996,7 +993,10 @@ constexpr uint32_t PATCH_RUN = 64;
 
 template <class T>
 int collect(tm_index *ix, Mirror<T> &m, std::vector<PatchRun> &runs, std::vector<uint32_t> &data) {
-    if (m.h.size() > m.dcap) m.dirty.set_all();
+    // the device copy keeps >= DEV_GUARD elements allocated past the host
+    // size: k_emit's 16-B loads may overhang the last value run by 3 words
+    // (with h.size() == dcap such a load would leave the allocation)
+    if (m.h.size() + DEV_GUARD > m.dcap) m.dirty.set_all();
     if (!m.dirty.all) {
         uint64_t words = 0;
         for (auto &r : m.dirty.r) words += r.second - r.first;
@@ -1103,9 +1103,6 @@ DevIndex dev_view(tm_index *ix) {
     d.xlen_max = xc.empty() ? 0 : (uint32_t)xc.size() - 1;
     d.xlen_mask = 0;
     for (size_t k = 0; k < xc.size() && k < 64; k++) if (xc[k]) d.xlen_mask |= 1ull << k;
-#ifdef TM_STUDY_HOSTWIDS
-    d.study_wids = ix->study_wids; d.study_n = ix->study_n;
-#endif
     return d;
 }
 
@@ -1243,7 +1240,8 @@ void init_tables(tm_index *ix, uint64_t hint) {
     node_new(ix, NONE, NONE, false);   // ROOT
     ix->vals.h.reserve(hint + 16);
     // a 16-B guard before the first run: k_emit's run-by-run copy loads whole
-    // quads that may overhang a run by up to 3 words on either side
+    // quads that may overhang a run by up to 3 words on either side (the
+    // guard after the last run is the device copy's DEV_GUARD slack)
     ix->vals.h.assign(4, 0);
 }
 
@@ -1431,9 +1429,7 @@ namespace {
 // memory over PCIe.  A small batch then costs its kernels plus one host
 // synchronisation -- no copy commands and no gaps between them.  Larger
 // batches move in one H2D and one D2H transfer.
-#ifndef ZC_TOPICS
-#define ZC_TOPICS 65536
-#endif
+constexpr uint64_t ZC_TOPICS = 65536;
 
 int pin_mapped(tm_index *ix, hipStream_t s, uint8_t *&host, uint8_t *&dev, uint64_t &cap, uint64_t need) {
     if (need <= cap) return TM_OK;
@@ -1747,25 +1743,6 @@ int tm_profile_read(tm_index *ix, double *walk_ms, double *batch_ms, uint64_t *b
     return TM_OK;
 }
 
-#ifdef TM_STUDY_HOSTWIDS
-// study build only: the level-major wids (FAST_L levels) of a host batch, looked
-// up on the host, and the device copy the walk reads instead of probing the vocab
-int tm_study_wids(tm_index *ix, uint64_t n, const uint8_t *tb, const uint64_t *to, uint32_t *out) {
-    std::lock_guard<std::mutex> g(ix->mu);
-    std::vector<WordRef> w;
-    for (uint64_t t = 0; t < n; t++) {
-        split_words(tb + to[t], (uint32_t)(to[t + 1] - to[t]), w);
-        for (uint32_t l = 0; l < (uint32_t)FAST_L; l++)
-            out[(uint64_t)l * n + t] = l < w.size() ? vocab_find(ix, w[l].p, w[l].n) : NONE;
-    }
-    return TM_OK;
-}
-int tm_study_set_wids(tm_index *ix, const uint32_t *d_wids, uint64_t n) {
-    std::lock_guard<std::mutex> g(ix->mu);
-    ix->study_wids = d_wids; ix->study_n = n;
-    return TM_OK;
-}
-#endif
 
 // ------------------------------------------------------- matches_filter/3
 

@@ -39,22 +39,6 @@ __device__ __forceinline__ uint4 ld4_once(const void *p) {
     return make_uint4(v.x, v.y, v.z, v.w);
 }
 
-// Loads of structures a topic touches once and no other topic is likely to
-// touch soon (study switches TM_NT_*): non-temporal, so they do not push the
-// hot upper trie levels and the vocab out of the XCD's L2.
-__device__ __forceinline__ uint4 ld4_cold(const void *p) {
-    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
-    return make_uint4(v.x, v.y, v.z, v.w);
-}
-__device__ __forceinline__ uint32_t ld_xfp(const uint16_t *p) {
-#ifdef TM_NT_XFP
-    return __builtin_nontemporal_load(p);
-#else
-    return *p;
-#endif
-}
-
 // bit b (0..191) of a table-mode node's Bloom: words kw[2..3], kc[0..3]
 __device__ __forceinline__ uint32_t bloom_bit(const uint4 &n2, const uint4 &n3, uint32_t b) {
     const uint32_t j = b >> 5;
@@ -152,13 +136,9 @@ __device__ uint32_t vocab_find(const DevIndex &ix, const WordAcc &w, const uint8
 // literal child in a node's private table (table mode, nlit > KINL), with the
 // slot's summary of the child
 __device__ __forceinline__ uint32_t ctab_find(const DevIndex &ix, uint32_t off, uint32_t mask, uint32_t wid,
-                                              uint32_t h, uint32_t &slo, uint32_t &shi, bool cold = false) {
+                                              uint32_t h, uint32_t &slo, uint32_t &shi) {
     for (uint32_t s = h & mask;; s = (s + 1) & mask) {
-#ifdef TM_NT_CTAB
-        uint4 e = cold ? ld4_cold(ix.ctab + off + s) : ld4(ix.ctab + off + s);
-#else
         uint4 e = ld4(ix.ctab + off + s);
-#endif
         pin(e);
         if (e.x == wid) { slo = e.z; shi = e.w; return e.y; }
         if (e.x == NONE) return NONE;
@@ -177,12 +157,6 @@ struct LdsStore {
     uint8_t *len8;                           // [level][thread] word lengths (deferred probes)
     uint32_t stride;
     uint64_t mask;
-#ifdef TM_STUDY_HOSTWIDS
-    uint64_t study_t = ~0ull;                // study build: the topic (wids precomputed on the host)
-#endif
-#ifdef TM_STUDY
-    uint32_t n_steps = 0, n_probe = 0;   // study build: node visits, child-table probes
-#endif
     __device__ __forceinline__ uint32_t get_wid(uint32_t l) const { return wid[l * stride]; }
     __device__ __forceinline__ void set_wid(uint32_t l, uint32_t w) { wid[l * stride] = w; }
     __device__ __forceinline__ void reset() { mask = 0; }
@@ -232,9 +206,7 @@ enum { RC_OK = 0, RC_BADARG = 1, RC_DEEP = 2 };
 // topic depths in one round trip and keeps k_walk_fast within 64 VGPRs, i.e.
 // 8 waves per SIMD -- a budget small code changes can tip: check the
 // -Rpass-analysis=kernel-resource-usage remark after every change)
-#ifndef VGROUP
-#define VGROUP 6
-#endif
+constexpr uint32_t VGROUP = 6;
 
 // '/' bytes in [p, end), p 16-byte aligned: four 16-byte loads in flight per
 // round trip, bytes compared a word at a time
@@ -396,20 +368,6 @@ __device__ int tokenize(const DevIndex &ix, const uint8_t *blob, uint64_t beg, u
         if (rc) return rc;
         L = lev;
     }
-#ifdef TM_STUDY_HOSTWIDS   // study: wids from a host-computed array (the vocab's share of the walk)
-    if constexpr (S::deferred) {
-        if (st.study_t != ~0ull) {
-            for (uint32_t l = 0; l < L; l++)
-                if (!((longmask >> l) & 1)) st.set_wid(l, ix.study_wids[(uint64_t)l * ix.study_n + st.study_t]);
-            goto wids_done;
-        }
-    }
-#endif
-#ifdef TM_STUDY_SCANONLY   // timing study: no vocab probes (wrong results)
-    if constexpr (S::deferred) {
-        for (uint32_t l = 0; l < L; l++) if (!((longmask >> l) & 1)) st.set_wid(l, st.word_b0(l) ^ st.word_b1(l));
-    } else
-#endif
     if constexpr (S::deferred) {
         // Branch-free issue and consumption: every lane issues VGROUP loads
         // (unused levels read slot 0) and consumes all of them, so no load is
@@ -447,9 +405,6 @@ __device__ int tokenize(const DevIndex &ix, const uint8_t *blob, uint64_t beg, u
             }
         }
     }
-#ifdef TM_STUDY_HOSTWIDS
-wids_done:
-#endif
     if constexpr (S::deferred && S::maxl > FAST_L) {
       const uint32_t Lw = L >> 24;
       L &= 0xFFFFFFu;
@@ -492,11 +447,7 @@ __device__ void exact_find(const DevIndex &ix, uint64_t xh, uint32_t L, const S 
         if (f == 0) return;
         if (f == fp) {
             const uint4 *e = reinterpret_cast<const uint4 *>(ix.exact + slot);
-#ifdef TM_NT_EXACT
-            uint4 a = ld4_cold(e), b = ld4_cold(e + 1), c = ld4_cold(e + 2), d = ld4_cold(e + 3);
-#else
             uint4 a = e[0], b = e[1], c = e[2], d = e[3];
-#endif
             pin(a); pin(b); pin(c); pin(d);
             if (a.x == (uint32_t)xh && a.y == (uint32_t)(xh >> 32) && a.z == L) {
                 bool eq = true;
@@ -512,7 +463,7 @@ __device__ void exact_find(const DevIndex &ix, uint64_t xh, uint32_t L, const S 
             }
         }
         slot = (slot + 1) & ix.xmask;
-        f = ld_xfp(ix.xfp + slot);
+        f = ix.xfp[slot];
     }
 }
 
@@ -528,17 +479,7 @@ __device__ void exact_find(const DevIndex &ix, uint64_t xh, uint32_t L, const S 
 template <class S, class EM>
 __device__ bool dfs(const DevIndex &ix, uint32_t L, bool dollar, S &st, EM &em) {
     uint32_t cur = ROOT, l = 0;
-#ifdef TM_STUDY_DEAD
-    bool via_plus = false;   // study: how the current node was reached
-#endif
-#ifdef TM_STUDY_LEAF
-    uint32_t via = 2;        // study: 0 '+', 1 child table, 2 inline child
-    uint64_t via_ct = 0;     // study: pushed literal branches that came from a child table
-#endif
     for (;;) {
-#ifdef TM_STUDY
-        if constexpr (S::deferred) st.n_steps++;
-#endif
         // the whole state is one 64-byte line (tm_layout.h Node)
         const uint4 *np = reinterpret_cast<const uint4 *>(ix.nodes + cur);
         const uint4 n0 = np[0];   // plus, hash_off, hash_cnt, exact_off
@@ -555,9 +496,6 @@ __device__ bool dfs(const DevIndex &ix, uint32_t L, bool dollar, S &st, EM &em) 
         uint32_t inl = n2.x == w ? n3.x : n2.y == w ? n3.y : n2.z == w ? n3.z : n2.w == w ? n3.w : NONE;
         pin(inl);
         if (l == L) {
-#ifdef TM_STUDY_LEAF
-            if constexpr (S::deferred) { if (via == 1) st.n_steps += 1u << 16; else st.n_probe++; }
-#endif
             if (!em(n0.w, n1.x)) return false;
             if (!droot && !em(n0.y, n0.z)) return false;
         } else {
@@ -567,90 +505,31 @@ __device__ bool dfs(const DevIndex &ix, uint32_t L, bool dollar, S &st, EM &em) 
                     lit = inl;
                 } else {
                     const uint32_t h = child_hash(w);
-                    const uint32_t m = child_maybe(ix, n1, n2, n3, w, h);
-                    if (m & 1u) {
+                    if (child_maybe(ix, n1, n2, n3, w, h) & 1u) {
                         uint32_t slo, shi;
-#ifdef TM_NT_CTAB
-                        lit = ctab_find(ix, n2.x, n2.y, w, h, slo, shi, l >= TM_NT_CTAB);
-#else
                         lit = ctab_find(ix, n2.x, n2.y, w, h, slo, shi);
-#endif
-#ifdef TM_STUDY_MISS   // study: probes that find no child, by level (1), or at l >= 3 / found but dead (2)
-                        if constexpr (S::deferred) {
-                            const bool absent = lit == NONE;
-                            const bool dead = !absent && !child_alive(slo, shi, l + 1, L,
-                                l + 1 < L ? st.get_wid(l + 1) : NONE, l + 2 < L ? st.get_wid(l + 2) : NONE);
-                            if (TM_STUDY_MISS == 1) {
-                                if (absent && l <= 1) st.n_steps += 1u << 16;
-                                if (absent && l == 2) st.n_probe++;
-                            } else {
-                                if (absent && l >= 3) st.n_steps += 1u << 16;
-                                if (dead) st.n_probe++;
-                            }
-                        }
-#endif
-#ifndef TM_NO_PSUM
                         if (lit != NONE && !child_alive(slo, shi, l + 1, L, l + 1 < L ? st.get_wid(l + 1) : NONE,
                                                         l + 2 < L ? st.get_wid(l + 2) : NONE))
                             lit = NONE;
-#endif
                     }
-#if defined(TM_STUDY) && !defined(TM_STUDY_DEAD) && !defined(TM_STUDY_LEAF) && !defined(TM_STUDY_MISS)
-                    if constexpr (S::deferred) {
-                        if (m & 1u) { if (lit != NONE) st.n_steps += 1u << 16; else st.n_probe++; }
-                    }
-#endif
                 }
             }
             if (!droot && !em(n0.y, n0.z)) return false;
             uint32_t plus = droot ? NONE : n0.x;
-#ifdef TM_STUDY_MAXL   // study: the walk cut below level TM_STUDY_MAXL (wrong results; requests per level)
-            if (l + 1 >= TM_STUDY_MAXL) { plus = NONE; lit = NONE; }
-#endif
-#ifndef TM_NO_PSUM
             if (plus != NONE && !child_alive(n1.z, n1.w, l + 1, L, l + 1 < L ? st.get_wid(l + 1) : NONE,
                                              l + 2 < L ? st.get_wid(l + 2) : NONE))
                 plus = NONE;
-#endif
-#ifdef TM_STUDY_DEAD
-            if constexpr (S::deferred) {   // a visit that emits nothing and leads nowhere
-                if (plus == NONE && lit == NONE && (droot || !n0.z)) {
-                    if (via_plus) st.n_steps += 1u << 16; else st.n_probe++;
-                }
-            }
-#endif
             if (plus != NONE) {
-#ifdef TM_STUDY_LEAF
-                if (lit != NONE) via_ct = (via_ct & ~(1ull << (l + 1))) | ((uint64_t)(n1.y > KINL) << (l + 1));
-#endif
                 if (lit != NONE) st.push(l + 1, lit);
                 cur = plus; l++;
-#ifdef TM_STUDY_LEAF
-                via = 0;
-#endif
-#ifdef TM_STUDY_DEAD
-                via_plus = true;
-#endif
                 continue;
             }
             if (lit != NONE) {
                 cur = lit; l++;
-#ifdef TM_STUDY_LEAF
-                via = n1.y <= KINL ? 2 : 1;
-#endif
-#ifdef TM_STUDY_DEAD
-                via_plus = false;
-#endif
                 continue;
             }
         }
-#ifdef TM_STUDY_DEAD
-        via_plus = false;
-#endif
         if (!st.pop(l, cur)) return true;
-#ifdef TM_STUDY_LEAF
-        via = ((via_ct >> l) & 1) ? 1 : 2;
-#endif
     }
 }
 
@@ -707,16 +586,9 @@ __device__ int match_topic(const DevIndex &ix, const uint8_t *blob, uint64_t beg
     int rc = tokenize(ix, blob, beg, end, st, L, dollar, xh, allf);
     if (levels) *levels = L;   // RC_DEEP: the topic's level count (the tail list's choice)
     if (rc) return rc;
-#ifdef TM_STUDY_TOKONLY   // timing study: tokenise + vocab only (wrong results)
-    if (xh == 42) em(0, 1);   // keep the tokeniser's outputs live
-    return RC_OK;
-#endif
     st.reset();
     const uint32_t xslot = (uint32_t)xh & ix.xmask;
-#ifdef TM_STUDY_NOEXACT
-    allf = false;   // timing study only: the exact-table probe skipped (wrong results)
-#endif
-    const uint32_t xf = allf ? ld_xfp(ix.xfp + xslot) : 0;
+    const uint32_t xf = allf ? ix.xfp[xslot] : 0;
     if (!dfs(ix, L, dollar, st, em)) return RC_OK;
     if (allf) {
         uint32_t xoff, xcnt;
@@ -779,22 +651,7 @@ __device__ int run_topic(const DevIndex &ix, const Workspace &ws, uint64_t n, co
         __builtin_nontemporal_store(em.cnt, ws.cnt + t);
         __builtin_nontemporal_store(em.nr, ws.nr + t);
         em.store(ws.rng, n, t);
-#ifdef TM_STUDY   // study build (tools/study_steps.py): visits and probes in the err byte
-        if constexpr (S::maxl == FAST_L)
-        {   // TM_STUDY_HITS: ctab probes that found the child (low nibble) / missed (high nibble)
-#ifdef TM_STUDY_HITS
-            const uint32_t hit = st.n_steps >> 16;
-            o.err[t] = (uint8_t)((hit < 15 ? hit : 15) | ((st.n_probe < 15 ? st.n_probe : 15) << 4));
-#else
-            const uint32_t vis = st.n_steps & 0xFFFF, pr = (st.n_steps >> 16) + st.n_probe;
-            o.err[t] = (uint8_t)((vis < 31 ? vis : 31) | ((pr < 7 ? pr : 7) << 5));
-#endif
-        }
-        else
-            o.err[t] = rc == RC_BADARG ? 1 : (toolong ? 2 : 0);
-#else
         __builtin_nontemporal_store((uint8_t)(rc == RC_BADARG ? 1 : (toolong ? 2 : 0)), o.err + t);
-#endif
         if (em.nr > RCAP) {   // re-walked by k_rewalk_tail (ovf: the caller pushes it)
             const int k = S::maxl <= MID_L ? L_OVF_MID : L_OVF_DEEP;
             if (ovf) *ovf = k; else list_push(ws, n, k, (uint32_t)t);
@@ -859,10 +716,10 @@ __device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t &total,
 // the walk writes each tile's hit total into ws.blk, k_scan_top turns those
 // into tile prefixes, k_emit finishes the scan inside its tile.
 
-#ifndef TM_WALK_BLOCK
-#define TM_WALK_BLOCK 64    // 64 vs 256: walk 0.2553 vs 0.2631 ms per 1M C3 topics (a block waits for its slowest lane)
-#endif
-constexpr int WALK_BLOCK = TM_WALK_BLOCK;   // a walk block is a scan tile, or a part of one (tile totals added atomically)
+// a walk block is a scan tile, or a part of one (tile totals added
+// atomically); 64 vs 256 threads: walk 0.2553 vs 0.2631 ms per 1M C3 topics
+// (a block waits for its slowest lane)
+constexpr int WALK_BLOCK = 64;
 static_assert(TILE % WALK_BLOCK == 0, "walk blocks tile the scan tiles");
 
 template <int MODE>
@@ -877,9 +734,6 @@ __global__ __launch_bounds__(WALK_BLOCK, 8) void k_walk_fast(DevIndex ix, Worksp
     int deep = -1, ovf = -1;   // tail lists this topic goes to
     if (t < n) {
         LdsStore<FAST_L> st{s_wid + threadIdx.x, s_pend + threadIdx.x, s_len + threadIdx.x, WALK_BLOCK, 0};
-#ifdef TM_STUDY_HOSTWIDS
-        if (ix.study_wids && ix.study_n == n) st.study_t = t;
-#endif
         int rc = run_topic<MODE>(ix, ws, n, blob, offs, t, st, o, &hits, &ovf);
         if (rc == RC_DEEP) {   // hits = the topic's level count
             deep = tail_list(ix, hits);
@@ -1044,16 +898,12 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_wave(DevIndex ix, Workspace w
                 if (mb & 1u) {
                     uint32_t slo, shi;
                     lit = ctab_find(ix, n2.x, n2.y, wl_, h, slo, shi);
-#ifndef TM_NO_PSUM
                     if (lit != NONE && !child_alive(slo, shi, l + 1, L, wnext, wnext2)) lit = NONE;
-#endif
                 }
             }
         }
         uint32_t plus = act && !droot ? n0.x : NONE;
-#ifndef TM_NO_PSUM
         if (plus != NONE && !child_alive(n1.z, n1.w, l + 1, L, wnext, wnext2)) plus = NONE;
-#endif
         const uint64_t mp = grp.ballot(plus != NONE), ml = grp.ballot(lit != NONE);
         const uint32_t np_ = (uint32_t)__popcll(mp), nn = np_ + (uint32_t)__popcll(ml);
         if (nn > W) { ovf = true; break; }
@@ -1119,10 +969,7 @@ constexpr int MID_GRID = 512;                         // LDS-frontier blocks of 
 // no grid-wide ticket then, so idle blocks cost only their dispatch).  512
 // blocks = 2 waves per CU: C3deep (100k topics of 33-64 levels per 1M batch)
 // spent 0.57 ms per batch in the tail; 2048: 0.25 ms
-#ifndef TM_MID_GRID_BIG
-#define TM_MID_GRID_BIG 2048
-#endif
-constexpr int MID_GRID_BIG = TM_MID_GRID_BIG;
+constexpr int MID_GRID_BIG = 2048;
 constexpr int TAIL_GRID = MID_GRID + DEEP_LANES / 64; // + global-scratch blocks
 
 // last block of a grid (atomic ticket) resets the list counters for the next batch
@@ -1258,14 +1105,8 @@ constexpr int EMIT_BLOCK = TILE;
 constexpr int EMIT_WAVES = EMIT_BLOCK / 64;
 constexpr int WR = 64 * RCAP;   // ranges per wave
 typedef uint4 __attribute__((aligned(4))) uint4u;   // dword-aligned 16-B load (global_load_dwordx4)
-#ifndef TM_EMIT_Q
-#define TM_EMIT_Q 1
-#endif
-constexpr int EMIT_Q = TM_EMIT_Q;   // quads per lane per iteration (loads in flight before the stores)
-#ifndef TM_EMIT_RUNS
-#define TM_EMIT_RUNS 16
-#endif
-constexpr uint64_t EMIT_RUNS = TM_EMIT_RUNS;   // average run length from which a wave copies run by run
+constexpr int EMIT_Q = 1;   // quads per lane per iteration (loads in flight before the stores)
+constexpr uint64_t EMIT_RUNS = 16;   // average run length from which a wave copies run by run
 
 // One block = one tile of 256 topics: finishes the scan (tile prefix + local
 // exclusive scan -> hit_offs), then each wave flattens its 64 topics' value
@@ -1381,11 +1222,7 @@ __global__ __launch_bounds__(EMIT_BLOCK) void k_emit(DevIndex ix, Workspace ws, 
         if (q < q1 && p0 >= base && p0 + 3 < endp) {   // whole quad inside one run: one 16-B load
             const uint32_t rs = s_rel[wv][r], rc = s_cnt[wv][r];
             if (!(rc & RUN_INLINE) && first >= rs && first + 3 - rs < (rc & RUN_CNT)) {
-#ifdef TM_STUDY_EMIT_NOREAD   // study: store-only bound of the emit (wrong values)
-                const uint4 a = make_uint4(first, rs, rc, 0);
-#else
                 const uint4 a = *reinterpret_cast<const uint4u *>(ix.vals + s_off[wv][r] + (first - rs));
-#endif
                 v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
                 ok[0] = ok[1] = ok[2] = ok[3] = true;
                 return;
@@ -1682,12 +1519,8 @@ __global__ __launch_bounds__(256) void k_copy_values(const uint64_t *hit, uint64
 
 static inline uint32_t blocks_for(uint64_t n, uint32_t per) { return (uint32_t)((n + per - 1) / per); }
 
-#ifndef WAVE_TOPICS
-#define WAVE_TOPICS 8192   // batches of up to this many topics take the wave-per-topic walk (latency)
-#endif
-#ifndef WAVE_W
-#define WAVE_W 16          // lanes per topic in the wave walk
-#endif
+constexpr uint64_t WAVE_TOPICS = 8192;   // batches of up to this many topics take the wave-per-topic walk (latency)
+constexpr int WAVE_W = 16;               // lanes per topic in the wave walk
 constexpr uint32_t WV_TOPICS_PER_BLOCK = WV_WAVES * (64 / WAVE_W);
 
 hipError_t launch_match_phase1(const DevIndex &ix, const Workspace &ws, uint64_t n, const uint8_t *bytes,

@@ -63,10 +63,7 @@ constexpr uint32_t KINL = 4;     // literal children kept inside the node's line
 // nodes and the (w0,+) / (+,+) level-2 nodes -- so their bitmaps stay in L2
 // and a probe for a word the node has no child for costs an L2 hit instead of
 // a memory-side request into a multi-megabyte child table.
-#ifndef TM_WIDE_LIT
-#define TM_WIDE_LIT 256
-#endif
-constexpr uint32_t WIDE_LIT = TM_WIDE_LIT;   // 0: bitmaps off
+constexpr uint32_t WIDE_LIT = 256;
 
 // One 64-byte line per trie state: everything a walk step needs -- the '+'
 // child, both terminals and, for nodes with <= KINL literal children (almost

@@ -67,23 +67,8 @@ def main():
         tot = max(tot, int(d_hit[-1]))
     d_out = torch.zeros(max(tot, 1), dtype=torch.int32, device=dev)
 
-    study = None
-    if os.environ.get("TM_STUDY_HOSTWIDS"):   # study build: wids looked up on the host (the vocab's share)
-        import ctypes as C
-        lib = _native.load_library()
-        study = []
-        for k in range(R):
-            ts = wl.topics(gen, nf, a.batch, first=k * a.batch)
-            w = np.zeros(8 * a.batch, np.uint32)
-            lib.tm_study_wids(ix._h, C.c_uint64(a.batch), _native._ptr(ts.blob), _native._ptr(ts.offs), _native._ptr(w))
-            study.append(torch.from_numpy(w.view(np.int32)).to(dev))
-        torch.cuda.synchronize()
-
     def launch(k):
         d_blob, d_offs = d_in[k % R]
-        if study is not None:
-            import ctypes as C
-            _native.load_library().tm_study_set_wids(ix._h, C.c_void_p(study[k % R].data_ptr()), C.c_uint64(a.batch))
         ix.match_batch_dev(a.batch, d_blob.data_ptr(), d_offs.data_ptr(), d_hit.data_ptr(), d_out.data_ptr(), tot,
                            d_err.data_ptr(), s)
 
