@@ -50,6 +50,7 @@ struct Workspace {
     uint64_t *blk;        // [n / TILE + 2] tile hit totals -> exclusive tile prefixes (zero between batches)
     uint32_t *deep_wid;   // [DEEP_LANES * MAX_LEVELS]
     uint2 *deep_stk;      // [DEEP_LANES * (MAX_LEVELS + 1)]
+    uint8_t *deep_plus;   // [DEEP_LANES * MAX_LEVELS] '+' levels of each deep lane's path
     uint64_t cap_n;
 };
 

@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdlib>
 #include <cstdio>
@@ -20,6 +21,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <map>
 #include <unordered_set>
 #include <set>
 #include <vector>
@@ -71,9 +73,13 @@ struct NodeAux {
     uint32_t hash_roff = 0, exact_roff = 0;   // the runs' offsets in vals (the line may hold an inline value)
     uint8_t is_plus = 0;
     uint32_t bm = NONE;                       // word offset of its child bitmap in wbits (wide nodes)
+    uint32_t hdesc = 0;                       // keys P/#/... ('#' not last) ending their walk here (NLIT_HDESC)
 };
 
 struct WordRef { const uint8_t *p; uint32_t n; int kind; };   // kind: 0 binary, 1 '+', 2 '#'
+
+// literal children of a node (its nlit word also carries NLIT_HDESC)
+inline uint32_t nlit_of(const Node &n) { return n.nlit & NLIT_MASK; }
 
 }  // namespace
 
@@ -162,6 +168,14 @@ struct tm_index {
     // caller buffers from tm_host_alloc (host address -> size, device address)
     struct Pinned { uint8_t *host, *dev; uint64_t size; };
     std::vector<Pinned> pinned;
+
+    // reader epochs (tm_read_begin / tm_read_end / tm_epoch): the epoch
+    // advances after each delta batch is applied; registered readers' epochs
+    std::atomic<uint64_t> epoch{1};
+    std::mutex ep_mu;
+    uint64_t next_ticket = 1;
+    std::map<uint64_t, uint64_t> readers;     // ticket -> epoch at tm_read_begin
+    std::multiset<uint64_t> reader_epochs;
 
     // diagnostics (tm_profile_*)
     bool prof = false;
@@ -466,7 +480,7 @@ uint32_t node_new(tm_index *ix, uint32_t parent, uint32_t wid, bool is_plus) {
 // literal child of `node` for word `wid`
 uint32_t child_find(tm_index *ix, uint32_t node, uint32_t wid) {
     const Node &n = ix->nodes.h[node];
-    if (n.nlit <= KINL) {
+    if (nlit_of(n) <= KINL) {
         for (uint32_t k = 0; k < KINL; k++) if (n.kw[k] == wid) return n.kc[k];
         return NONE;
     }
@@ -551,17 +565,15 @@ void from_wide(tm_index *ix, uint32_t node) {
     ix->nodes.touch(node);
 }
 
-// summary of node q as its parent's psum (tm_layout.h): terminals, '+' child,
-// 61-bit Bloom of the literal child wids (all ones past 61 children)
-// literal-children Bloom of node q (29 bits), all ones past 29 children
+// literal-children Bloom of node q (PSUM_BLOOM bits), all ones past PSUM_BLOOM children
 uint64_t lit_bloom(tm_index *ix, uint32_t q) {
     const Node &n = ix->nodes.h[q];
     uint64_t m = 0;
     auto add = [&](uint32_t wid) { m |= 1ull << psum_bit(child_hash(wid)); };
-    if (n.nlit <= KINL) {
+    if (nlit_of(n) <= KINL) {
         for (uint32_t k = 0; k < KINL; k++) if (n.kw[k] != NONE) add(n.kw[k]);
-    } else if (n.nlit > 29) {
-        m = (1ull << 29) - 1;
+    } else if (nlit_of(n) > PSUM_BLOOM) {
+        m = (1ull << PSUM_BLOOM) - 1;
     } else {
         for (uint32_t i = 0; i <= n.kw[1]; i++) if (ix->ctab.h[n.kw[0] + i].wid != NONE) add(ix->ctab.h[n.kw[0] + i].wid);
     }
@@ -569,14 +581,15 @@ uint64_t lit_bloom(tm_index *ix, uint32_t q) {
 }
 
 uint64_t node_flags(const Node &n) {
-    return (n.hash_cnt ? PSUM_HASH : 0) | (n.exact_cnt ? PSUM_EXACT : 0) | (n.plus != NONE ? PSUM_PLUS : 0);
+    return (n.hash_cnt ? PSUM_HASH : 0) | (n.exact_cnt ? PSUM_EXACT : 0) | (n.plus != NONE ? PSUM_PLUS : 0) |
+           ((n.nlit & NLIT_HDESC) ? PSUM_HDESC : 0);
 }
 
 // summary of node q as its parent keeps it (tm_layout.h PSUM_*)
 uint64_t node_psum(tm_index *ix, uint32_t q) {
     const Node &n = ix->nodes.h[q];
-    uint64_t m = node_flags(n) | lit_bloom(ix, q) << 6;
-    if (n.plus != NONE) m |= node_flags(ix->nodes.h[n.plus]) << 3 | lit_bloom(ix, n.plus) << 35;
+    uint64_t m = node_flags(n) | lit_bloom(ix, q) << PSUM_BQ;
+    if (n.plus != NONE) m |= node_flags(ix->nodes.h[n.plus]) << PSUM_QQ | lit_bloom(ix, n.plus) << PSUM_BQQ;
     return m;
 }
 
@@ -605,7 +618,7 @@ void summary_refresh1(tm_index *ix, uint32_t x) {
         }
         return;
     }
-    if (pn.nlit <= KINL) return;
+    if (nlit_of(pn) <= KINL) return;
     const uint32_t sl = ctab_find(ix, pn.kw[0], pn.kw[1], a.wid);
     if (sl == NONE) return;
     CSlot &c = ix->ctab.h[pn.kw[0] + sl];
@@ -621,7 +634,7 @@ void summary_refresh1(tm_index *ix, uint32_t x) {
 void to_table(tm_index *ix, uint32_t node, uint32_t cap) {
     Node &n = ix->nodes.h[node];
     std::vector<CSlot> kids;
-    if (n.nlit <= KINL) {
+    if (nlit_of(n) <= KINL) {
         for (uint32_t k = 0; k < KINL; k++)
             if (n.kw[k] != NONE) {
                 const uint64_t m = node_psum(ix, n.kc[k]);
@@ -645,19 +658,19 @@ void to_table(tm_index *ix, uint32_t node, uint32_t cap) {
 void child_add(tm_index *ix, uint32_t node, uint32_t wid, uint32_t child) {
     ix->nlinks++;
     Node *n = &ix->nodes.h[node];
-    if (n->nlit < KINL) {
+    if (nlit_of(*n) < KINL) {
         for (uint32_t k = 0; k < KINL; k++)
             if (n->kw[k] == NONE) { n->kw[k] = wid; n->kc[k] = child; break; }
     } else {
-        if (n->nlit == KINL) to_table(ix, node, 16);
-        else if ((n->nlit + 1) * 2 > n->kw[1] + 1) to_table(ix, node, (n->kw[1] + 1) * 2);
+        if (nlit_of(*n) == KINL) to_table(ix, node, 16);
+        else if ((nlit_of(*n) + 1) * 2 > n->kw[1] + 1) to_table(ix, node, (n->kw[1] + 1) * 2);
         n = &ix->nodes.h[node];
         ctab_put(ix, n->kw[0], n->kw[1], wid, child, node_psum(ix, child));
         if (ix->aux[node].bm != NONE) wide_bit(ix, node, wid, true);
         else set_bloom(*n, wid);
     }
     n->nlit++;
-    if (WIDE_LIT && n->nlit == WIDE_LIT && ix->aux[node].bm == NONE) { to_wide(ix, node); n = &ix->nodes.h[node]; }
+    if (nlit_of(*n) == WIDE_LIT && ix->aux[node].bm == NONE) { to_wide(ix, node); n = &ix->nodes.h[node]; }
     ix->nodes.touch(node);
     summary_refresh(ix, node);
 }
@@ -665,7 +678,7 @@ void child_add(tm_index *ix, uint32_t node, uint32_t wid, uint32_t child) {
 void child_remove(tm_index *ix, uint32_t node, uint32_t wid) {
     ix->nlinks--;
     Node &n = ix->nodes.h[node];
-    if (n.nlit <= KINL) {
+    if (nlit_of(n) <= KINL) {
         for (uint32_t k = 0; k < KINL; k++)
             if (n.kw[k] == wid) { n.kw[k] = NONE; n.kc[k] = NONE; break; }
         n.nlit--;
@@ -673,8 +686,8 @@ void child_remove(tm_index *ix, uint32_t node, uint32_t wid) {
         ctab_erase(ix, n.kw[0], n.kw[1], wid);
         wide_bit(ix, node, wid, false);
         n.nlit--;
-        if (ix->aux[node].bm != NONE && n.nlit < WIDE_LIT) from_wide(ix, node);
-        if (n.nlit == KINL) {   // back to inline mode
+        if (ix->aux[node].bm != NONE && nlit_of(n) < WIDE_LIT) from_wide(ix, node);
+        if (nlit_of(n) == KINL) {   // back to inline mode
             std::vector<CSlot> kids;
             for (uint32_t i = 0; i <= n.kw[1]; i++) if (ix->ctab.h[n.kw[0] + i].wid != NONE) kids.push_back(ix->ctab.h[n.kw[0] + i]);
             ctab_free(ix, n.kw[0], n.kw[1] + 1);
@@ -687,7 +700,7 @@ void child_remove(tm_index *ix, uint32_t node, uint32_t wid) {
 
 bool node_empty(tm_index *ix, uint32_t id) {
     const Node &n = ix->nodes.h[id];
-    return n.plus == NONE && n.nlit == 0 && n.hash_cnt == 0 && n.exact_cnt == 0;
+    return n.plus == NONE && n.nlit == 0 && n.hash_cnt == 0 && n.exact_cnt == 0 && ix->aux[id].hdesc == 0;
 }
 
 void node_prune(tm_index *ix, uint32_t id) {
@@ -913,15 +926,18 @@ void key_op(tm_index *ix, bool ins, const uint8_t *f, uint32_t len, uint32_t v, 
         return;
     }
     // word-list key.  '#' anywhere but last never matches (compare/3 has no
-    // clause for it, emqx_trie_search.erl:282-290 vs :341-348; emqx_topic.erl:110)
+    // clause for it, emqx_trie_search.erl:282-290 vs :341-348; emqx_topic.erl:110),
+    // but the key still steers the reference's walk at the node P of its
+    // prefix before that '#' (tm_layout.h NLIT_HDESC): P counts such keys
+    size_t hpos = w.size();
     for (size_t i = 0; i + 1 < w.size(); i++)
-        if (w[i].kind == 2) {
-            auto k = dead_key(f, len, v, flags & TM_KEY_WORDS);
-            if (ins) ix->dead.insert(k); else ix->dead.erase(k);
-            return;
-        }
-    const bool hash_term = w.back().kind == 2;
-    const size_t end = hash_term ? w.size() - 1 : w.size();
+        if (w[i].kind == 2) { hpos = i; break; }
+    if (hpos < w.size()) {
+        auto k = dead_key(f, len, v, flags & TM_KEY_WORDS);
+        if (ins ? !ix->dead.insert(k).second : !ix->dead.erase(k)) return;   // present / absent: no-op
+    }
+    const bool hash_term = hpos == w.size() && w.back().kind == 2;
+    const size_t end = hpos < w.size() ? hpos : hash_term ? w.size() - 1 : w.size();
     uint32_t node = ROOT;
     for (size_t i = 0; i < end; i++) {
         if (w[i].kind == 1) {
@@ -949,6 +965,14 @@ void key_op(tm_index *ix, bool ins, const uint8_t *f, uint32_t len, uint32_t v, 
     }
     Node &nd = ix->nodes.h[node];
     NodeAux &a = ix->aux[node];
+    if (hpos < w.size()) {   // a '#'-not-last key: P's count (the path exists: the key was inserted)
+        a.hdesc += ins ? 1 : -1;
+        nd.nlit = nlit_of(nd) | (a.hdesc ? NLIT_HDESC : 0);
+        ix->nodes.touch(node);
+        summary_refresh(ix, node);
+        if (!ins) node_prune(ix, node);
+        return;
+    }
     bool changed;
     changed = hash_term ? run_op(ix, ins, a.hash_roff, a.hash_cap, nd.hash_off, nd.hash_cnt, v)
                         : run_op(ix, ins, a.exact_roff, a.exact_cap, nd.exact_off, nd.exact_cnt, v);
@@ -1109,7 +1133,7 @@ DevIndex dev_view(tm_index *ix) {
 // ------------------------------------------------------------------ lanes
 
 void free_workspace(Workspace &w) {
-    void *wb[] = {w.cnt, w.nr, w.rng, w.lists, w.list_n, w.blk, w.deep_wid, w.deep_stk};
+    void *wb[] = {w.cnt, w.nr, w.rng, w.lists, w.list_n, w.blk, w.deep_wid, w.deep_stk, w.deep_plus};
     for (void *p : wb) if (p) (void)hipFree(p);
     w = Workspace{};
 }
@@ -1208,6 +1232,7 @@ int ensure_ws(tm_index *ix, uint64_t n, Lane &ln) {
     if (!w.deep_wid) {
         HIPCHK(ix, hipMalloc(&w.deep_wid, (uint64_t)DEEP_LANES * MAX_LEVELS * 4));
         HIPCHK(ix, hipMalloc(&w.deep_stk, (uint64_t)DEEP_LANES * (MAX_LEVELS + 1) * 8));
+        HIPCHK(ix, hipMalloc(&w.deep_plus, (uint64_t)DEEP_LANES * MAX_LEVELS));
         HIPCHK(ix, hipMalloc(&w.list_n, LIST_SLOTS * 4));
         HIPCHK(ix, hipMemsetAsync(w.list_n, 0, LIST_SLOTS * 4, ln.s));
     }
@@ -1282,7 +1307,7 @@ int drain_lanes(tm_index *ix) {
 
 extern "C" {
 
-uint32_t tm_abi_version(void) { return (1u << 16) | 3u; }
+uint32_t tm_abi_version(void) { return (1u << 16) | 4u; }
 
 const char *tm_last_error(tm_index *) { return g_last_error.c_str(); }
 
@@ -1334,8 +1359,8 @@ int tm_destroy(tm_index *ix) {
     return TM_OK;
 }
 
-int tm_apply_deltas(tm_index *ix, uint64_t n, const uint8_t *ops, const uint8_t *fb, const uint64_t *fo,
-                    const uint32_t *values, const uint8_t *key_flags) {
+int tm_apply_deltas_ex(tm_index *ix, uint64_t n, const uint8_t *ops, const uint8_t *fb, const uint64_t *fo,
+                       const uint32_t *values, const uint8_t *key_flags, uint64_t *out_epoch) {
     if (!ix) return fail(nullptr, TM_EINVAL, "tm_apply_deltas: null handle");
     if (n && (!ops || !fo || !values || (!fb && fo[n] != fo[0])))
         return fail(ix, TM_EINVAL, "tm_apply_deltas: null buffer");
@@ -1353,6 +1378,44 @@ int tm_apply_deltas(tm_index *ix, uint64_t n, const uint8_t *ops, const uint8_t 
     } catch (const std::bad_alloc &) {
         return fail(ix, TM_ENOMEM, "tm_apply_deltas: out of host memory");
     }
+    // the keys changed above are what every batch queued from now on sees:
+    // a reader registered from now on begins at the new epoch
+    const uint64_t e = n ? ix->epoch.fetch_add(1, std::memory_order_acq_rel) + 1 : ix->epoch.load();
+    if (out_epoch) *out_epoch = e;
+    return TM_OK;
+}
+
+int tm_apply_deltas(tm_index *ix, uint64_t n, const uint8_t *ops, const uint8_t *fb, const uint64_t *fo,
+                    const uint32_t *values, const uint8_t *key_flags) {
+    return tm_apply_deltas_ex(ix, n, ops, fb, fo, values, key_flags, nullptr);
+}
+
+int tm_read_begin(tm_index *ix, uint64_t *ticket) {
+    if (!ix || !ticket) return fail(ix, TM_EINVAL, "tm_read_begin: null argument");
+    std::lock_guard<std::mutex> g(ix->ep_mu);
+    const uint64_t e = ix->epoch.load(std::memory_order_acquire);
+    *ticket = ix->next_ticket++;
+    ix->readers.emplace(*ticket, e);
+    ix->reader_epochs.insert(e);
+    return TM_OK;
+}
+
+int tm_read_end(tm_index *ix, uint64_t ticket) {
+    if (!ix) return fail(nullptr, TM_EINVAL, "tm_read_end: null handle");
+    std::lock_guard<std::mutex> g(ix->ep_mu);
+    auto it = ix->readers.find(ticket);
+    if (it == ix->readers.end()) return fail(ix, TM_EINVAL, "tm_read_end: unknown ticket");
+    ix->reader_epochs.erase(ix->reader_epochs.find(it->second));
+    ix->readers.erase(it);
+    return TM_OK;
+}
+
+int tm_epoch(tm_index *ix, uint64_t *current, uint64_t *safe) {
+    if (!ix) return fail(nullptr, TM_EINVAL, "tm_epoch: null handle");
+    std::lock_guard<std::mutex> g(ix->ep_mu);
+    const uint64_t e = ix->epoch.load(std::memory_order_acquire);
+    if (current) *current = e;
+    if (safe) *safe = ix->reader_epochs.empty() ? e : *ix->reader_epochs.begin();
     return TM_OK;
 }
 
@@ -1822,7 +1885,7 @@ int mf_build(tm_index *ix) {
         }
         const uint32_t cd = node == ROOT ? 0 : d + 1;
         if (n.plus != NONE) st.push_back({n.plus, cd});
-        if (n.nlit <= KINL) {
+        if (nlit_of(n) <= KINL) {
             for (uint32_t k = 0; k < KINL; k++) if (n.kw[k] != NONE) st.push_back({n.kc[k], cd});
         } else {
             for (uint32_t i = 0; i <= n.kw[1]; i++) {

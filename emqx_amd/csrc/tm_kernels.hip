@@ -51,26 +51,28 @@ __device__ __forceinline__ uint32_t bloom_bit(const uint4 &n2, const uint4 &n3, 
 // others from the 192-bit Bloom in the line
 __device__ __forceinline__ uint32_t child_maybe(const DevIndex &ix, const uint4 &n1, const uint4 &n2, const uint4 &n3,
                                                 uint32_t w, uint32_t h) {
-    if (WIDE_LIT && n1.y >= WIDE_LIT)
+    if ((n1.y & NLIT_MASK) >= WIDE_LIT)
         return w < ix.wcap ? (ix.wbits[n2.z + (w >> 5)] >> (w & 31)) & 1u : 0u;
     return bloom_bit(n2, n3, child_bit(h));
 }
 
-// can a child Q (summarised as Node.psum / CSlot.sum, tm_layout.h) contribute
-// to a topic of L levels when entered at level lq?  Q must emit at lq == L, or
-// below it emit ('#' terminal) or go on: a literal child for word wq, or its
-// '+' child QQ, which in turn must be able to contribute at lq + 1 (word wq2)
+// can a child Q (summarised as Node.psum / CSlot.sum, tm_layout.h) matter to
+// a topic of L levels when entered at level lq?  At lq == L, Q must emit or cut
+// the walk (NLIT_HDESC); below it Q must emit ('#' terminal) or go on: a
+// literal child for word wq, or its '+' child QQ, which in turn must be able to
+// matter at lq + 1 (word wq2)
 __device__ __forceinline__ bool child_alive(uint32_t lo, uint32_t hi, uint32_t lq, uint32_t L, uint32_t wq,
                                             uint32_t wq2) {
     const uint64_t m = (uint64_t)hi << 32 | lo;
-    if (lq == L) return (m & (PSUM_HASH | PSUM_EXACT)) != 0;
+    constexpr uint32_t AT_END = PSUM_HASH | PSUM_EXACT | PSUM_HDESC;
+    if (lq == L) return (m & AT_END) != 0;
     if (m & PSUM_HASH) return true;
-    if (wq != NONE && ((m >> (6 + psum_bit(child_hash(wq)))) & 1u)) return true;
+    if (wq != NONE && ((m >> (PSUM_BQ + psum_bit(child_hash(wq)))) & 1u)) return true;
     if (!(m & PSUM_PLUS)) return false;
-    const uint32_t qq = (uint32_t)(m >> 3) & 7u;
-    if (lq + 1 == L) return (qq & (PSUM_HASH | PSUM_EXACT)) != 0;
+    const uint32_t qq = (uint32_t)(m >> PSUM_QQ) & 15u;
+    if (lq + 1 == L) return (qq & AT_END) != 0;
     if (qq & (PSUM_HASH | PSUM_PLUS)) return true;
-    return wq2 != NONE && ((m >> (35 + psum_bit(child_hash(wq2)))) & 1u);
+    return wq2 != NONE && ((m >> (PSUM_BQQ + psum_bit(child_hash(wq2)))) & 1u);
 }
 
 // Empty asm "uses": pin a loaded value at this point on every path.  Without
@@ -149,17 +151,36 @@ __device__ __forceinline__ uint32_t ctab_find(const DevIndex &ix, uint32_t off, 
 
 // LDS frontier: wid[level] and the pending literal child of each level,
 // laid out [level][thread] so that any mix of levels is bank-conflict free.
+//
+// Stores deeper than the main walk's also carry what the cut of a '#'-not-last
+// key needs (tm_layout.h NLIT_HDESC): which levels of the current path were
+// entered through '+' (pm, bit q: the node at depth q + 1 is a '+' child).  The
+// main walk's store does not: a topic that meets such a cut is handed to the
+// tail lists (DFS_REROUTE), keeping k_walk_fast within its register budget.
 template <int ML>
 struct LdsStore {
     static constexpr uint32_t maxl = ML;
     static constexpr bool deferred = true;   // vocab probes of short words after tokenisation
+    static constexpr bool cuts = ML > FAST_L;
     uint32_t *wid, *pend;
     uint8_t *len8;                           // [level][thread] word lengths (deferred probes)
     uint32_t stride;
     uint64_t mask;
+    uint32_t pm;
+    __device__ __forceinline__ void down(uint32_t l, bool via_plus) {   // depth l -> l + 1
+        if constexpr (cuts) pm = via_plus ? pm | (1u << l) : pm & ~(1u << l);
+    }
+    __device__ __forceinline__ void popped(uint32_t l) {   // resumed at depth l (>= 1): a literal child
+        if constexpr (cuts) pm &= (1u << (l - 1)) - 1u;
+    }
+    // the walk hit the cut at the topic's last level: keep the pending literal
+    // branches up to the innermost '+' of the path (the seek target), or none
+    __device__ __forceinline__ void cut(uint32_t) {
+        if constexpr (cuts) mask &= pm ? (1ull << (33u - __clz(pm))) - 1ull : 0ull;
+    }
     __device__ __forceinline__ uint32_t get_wid(uint32_t l) const { return wid[l * stride]; }
     __device__ __forceinline__ void set_wid(uint32_t l, uint32_t w) { wid[l * stride] = w; }
-    __device__ __forceinline__ void reset() { mask = 0; }
+    __device__ __forceinline__ void reset() { mask = 0; pm = 0; }
     // deferred vocab probes: a short word's packed bytes + length, parked in
     // the wid / pend slots of its level until the probe resolves it
     __device__ __forceinline__ void put_word(uint32_t l, uint32_t b0, uint32_t b1, uint32_t len) {
@@ -180,16 +201,26 @@ struct LdsStore {
     }
 };
 
-// Global-scratch frontier for arbitrarily deep topics (one slot per lane).
+// Global-scratch frontier for arbitrarily deep topics (one slot per lane);
+// plus_at[q] = 1: the path's node at depth q + 1 is a '+' child (for cut()).
 struct GlobalStore {
     static constexpr uint32_t maxl = MAX_LEVELS;
     static constexpr bool deferred = false;
+    static constexpr bool cuts = true;
     uint32_t *wid;
     uint2 *stk;
+    uint8_t *plus_at;
     uint32_t top;
     __device__ __forceinline__ uint32_t get_wid(uint32_t l) const { return wid[l]; }
     __device__ __forceinline__ void set_wid(uint32_t l, uint32_t w) { wid[l] = w; }
     __device__ __forceinline__ void reset() { top = 0; }
+    __device__ __forceinline__ void down(uint32_t l, bool via_plus) { plus_at[l] = via_plus; }
+    __device__ __forceinline__ void popped(uint32_t l) { plus_at[l - 1] = 0; }
+    __device__ void cut(uint32_t L) {   // as LdsStore::cut, the path being L levels deep
+        int64_t q = (int64_t)L - 1;
+        while (q >= 0 && !plus_at[q]) q--;
+        while (top && (int64_t)stk[top - 1].x > q + 1) top--;
+    }
     __device__ __forceinline__ void push(uint32_t l, uint32_t node) { stk[top++] = make_uint2(l, node); }
     __device__ __forceinline__ bool pop(uint32_t &l, uint32_t &node) {
         if (!top) return false;
@@ -475,15 +506,17 @@ __device__ void exact_find(const DevIndex &ix, uint64_t xh, uint32_t L, const S 
 // subtree, then the literal subtree -- so visiting them in that order emits
 // hits in exactly the reference's traversal order (search_up, :239-253).
 // First-level '$' words skip the root's '+' and '#' (base_init, :160-163).
-// Returns false if the emitter asked to stop (match/2 first-hit mode).
+// A '#'-not-last key below P (NLIT_HDESC) skips P's '+' subtree when the topic
+// goes on, and cuts the walk when it ends at P (tm_layout.h).
+enum { DFS_DONE = 0, DFS_STOP = 1, DFS_REROUTE = 2 };   // STOP: the emitter asked (match/2 first hit)
 template <class S, class EM>
-__device__ bool dfs(const DevIndex &ix, uint32_t L, bool dollar, S &st, EM &em) {
+__device__ int dfs(const DevIndex &ix, uint32_t L, bool dollar, S &st, EM &em) {
     uint32_t cur = ROOT, l = 0;
     for (;;) {
         // the whole state is one 64-byte line (tm_layout.h Node)
         const uint4 *np = reinterpret_cast<const uint4 *>(ix.nodes + cur);
         const uint4 n0 = np[0];   // plus, hash_off, hash_cnt, exact_off
-        const uint4 n1 = np[1];   // exact_cnt, nlit, psum_lo, psum_hi
+        const uint4 n1 = np[1];   // exact_cnt, nlit | NLIT_HDESC, psum_lo, psum_hi
         const uint4 n2 = np[2];   // kw[0..3] (table mode: offset, size-1)
         const uint4 n3 = np[3];   // kc[0..3]
         const bool droot = dollar && l == 0;
@@ -496,12 +529,16 @@ __device__ bool dfs(const DevIndex &ix, uint32_t L, bool dollar, S &st, EM &em) 
         uint32_t inl = n2.x == w ? n3.x : n2.y == w ? n3.y : n2.z == w ? n3.z : n2.w == w ? n3.w : NONE;
         pin(inl);
         if (l == L) {
-            if (!em(n0.w, n1.x)) return false;
-            if (!droot && !em(n0.y, n0.z)) return false;
+            if (!em(n0.w, n1.x)) return DFS_STOP;
+            if (!droot && !em(n0.y, n0.z)) return DFS_STOP;
+            if (n1.y & NLIT_HDESC) {   // [P,'#',...] returns lower here (compare/3, :333-340)
+                if constexpr (!S::cuts) return DFS_REROUTE;
+                st.cut(L);
+            }
         } else {
             uint32_t lit = NONE;
             if (w != NONE) {
-                if (n1.y <= KINL) {
+                if ((n1.y & NLIT_MASK) <= KINL) {
                     lit = inl;
                 } else {
                     const uint32_t h = child_hash(w);
@@ -514,22 +551,26 @@ __device__ bool dfs(const DevIndex &ix, uint32_t L, bool dollar, S &st, EM &em) 
                     }
                 }
             }
-            if (!droot && !em(n0.y, n0.z)) return false;
-            uint32_t plus = droot ? NONE : n0.x;
+            if (!droot && !em(n0.y, n0.z)) return DFS_STOP;
+            // [P,'#',...] seeks to P/W past the '+' subtree (:341-348)
+            uint32_t plus = droot || (n1.y & NLIT_HDESC) ? NONE : n0.x;
             if (plus != NONE && !child_alive(n1.z, n1.w, l + 1, L, l + 1 < L ? st.get_wid(l + 1) : NONE,
                                              l + 2 < L ? st.get_wid(l + 2) : NONE))
                 plus = NONE;
             if (plus != NONE) {
                 if (lit != NONE) st.push(l + 1, lit);
+                st.down(l, true);
                 cur = plus; l++;
                 continue;
             }
             if (lit != NONE) {
+                st.down(l, false);
                 cur = lit; l++;
                 continue;
             }
         }
-        if (!st.pop(l, cur)) return true;
+        if (!st.pop(l, cur)) return DFS_DONE;
+        st.popped(l);
     }
 }
 
@@ -589,7 +630,12 @@ __device__ int match_topic(const DevIndex &ix, const uint8_t *blob, uint64_t beg
     st.reset();
     const uint32_t xslot = (uint32_t)xh & ix.xmask;
     const uint32_t xf = allf ? ix.xfp[xslot] : 0;
-    if (!dfs(ix, L, dollar, st, em)) return RC_OK;
+    const int d = dfs(ix, L, dollar, st, em);
+    if (d == DFS_STOP) return RC_OK;
+    if (d == DFS_REROUTE) {   // a cut the main walk's store cannot make: the tail lists walk it
+        if (levels) *levels = L;
+        return RC_DEEP;
+    }
     if (allf) {
         uint32_t xoff, xcnt;
         exact_find(ix, xh, L, st, xslot, xf, xoff, xcnt);
@@ -880,6 +926,8 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_wave(DevIndex ix, Workspace w
         const bool droot = dollar && l == 0;
         const uint32_t sh = 62 - 2 * l;
         if (l == L) {
+            // a '#'-not-last key's cut (NLIT_HDESC) drops later hits: the lane walk's lists make it
+            if (grp.ballot(act && (n1.y & NLIT_HDESC))) { to_lists(); return; }
             add_hits(act && n1.x, code, n0.w, n1.x);                              // exact terminal: digit 0
             add_hits(act && !droot && n0.z, code | (1ull << sh), n0.y, n0.z);     // '#' terminal: digit 1
             break;
@@ -890,7 +938,7 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_wave(DevIndex ix, Workspace w
         const uint32_t wnext2 = l + 2 < L ? grp.bcast(wid, l + 2) : NONE;
         uint32_t lit = NONE;
         if (act && wl_ != NONE) {
-            if (n1.y <= KINL) {
+            if ((n1.y & NLIT_MASK) <= KINL) {
                 lit = n2.x == wl_ ? n3.x : n2.y == wl_ ? n3.y : n2.z == wl_ ? n3.z : n2.w == wl_ ? n3.w : NONE;
             } else {
                 const uint32_t h = child_hash(wl_);
@@ -902,7 +950,7 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_wave(DevIndex ix, Workspace w
                 }
             }
         }
-        uint32_t plus = act && !droot ? n0.x : NONE;
+        uint32_t plus = act && !droot && !(n1.y & NLIT_HDESC) ? n0.x : NONE;   // seek past '+' (dfs)
         if (plus != NONE && !child_alive(n1.z, n1.w, l + 1, L, wnext, wnext2)) plus = NONE;
         const uint64_t mp = grp.ballot(plus != NONE), ml = grp.ballot(lit != NONE);
         const uint32_t np_ = (uint32_t)__popcll(mp), nn = np_ + (uint32_t)__popcll(ml);
@@ -1012,7 +1060,8 @@ __global__ __launch_bounds__(MID_BLOCK) void k_walk_tail(DevIndex ix, Workspace 
         const uint32_t lane = (blockIdx.x - mid_grid) * 64 + threadIdx.x;   // < DEEP_LANES
         const uint32_t cnt = ws.list_n[L_DEEP];
         const uint32_t *lst = ws.lists + (uint64_t)L_DEEP * n;
-        GlobalStore st{ws.deep_wid + (uint64_t)lane * MAX_LEVELS, ws.deep_stk + (uint64_t)lane * (MAX_LEVELS + 1), 0};
+        GlobalStore st{ws.deep_wid + (uint64_t)lane * MAX_LEVELS, ws.deep_stk + (uint64_t)lane * (MAX_LEVELS + 1),
+                       ws.deep_plus + (uint64_t)lane * MAX_LEVELS, 0};
         for (uint32_t i = lane; i < cnt; i += DEEP_LANES) {
             run_topic<MODE>(ix, ws, n, blob, offs, lst[i], st, o, &hits);
             if (MODE == MODE_COUNT && hits) atomicAdd((unsigned long long *)&ws.blk[lst[i] / TILE], hits);
@@ -1068,7 +1117,8 @@ __global__ __launch_bounds__(MID_BLOCK) void k_rewalk_tail(DevIndex ix, Workspac
         const uint32_t lane = (blockIdx.x - MID_GRID) * 64 + threadIdx.x;
         const uint32_t cnt = ws.list_n[L_OVF_DEEP];
         const uint32_t *lst = ws.lists + (uint64_t)L_OVF_DEEP * n;
-        GlobalStore st{ws.deep_wid + (uint64_t)lane * MAX_LEVELS, ws.deep_stk + (uint64_t)lane * (MAX_LEVELS + 1), 0};
+        GlobalStore st{ws.deep_wid + (uint64_t)lane * MAX_LEVELS, ws.deep_stk + (uint64_t)lane * (MAX_LEVELS + 1),
+                       ws.deep_plus + (uint64_t)lane * MAX_LEVELS, 0};
         for (uint32_t i = lane; i < cnt; i += DEEP_LANES)
             rewalk(ix, blob, offs, lst[i], hit_offs, out, cap, st);
     }

@@ -82,20 +82,37 @@ struct alignas(64) Node {          // 64 B
     uint32_t plus;                 // '+' child or NONE
     uint32_t hash_off, hash_cnt;   // values of filter <path>/#
     uint32_t exact_off, exact_cnt; // values of filter <path> (word-list form)
-    uint32_t nlit;                 // literal children; > KINL: table mode
+    uint32_t nlit;                 // literal children (NLIT_MASK; > KINL: table mode) | NLIT_HDESC
     uint32_t psum_lo, psum_hi;     // summary of the '+' child (PSUM_*)
     uint32_t kw[KINL];             // inline: child wids (NONE = free); table mode: kw[0] = table
                                    // offset (CSlots), kw[1] = table size - 1, kw[2..3] Bloom bits 0-63
     uint32_t kc[KINL];             // inline: child node ids; table mode: Bloom bits 64-191
 };
 
+// NLIT_HDESC: some stored key continues past this node P with a '#' that is
+// not its last word (P/#/X..., a filter emqx_topic:validate/2 would reject but
+// an index that does not validate -- the rule engine's FROM topics,
+// emqx_rule_engine.erl:534-540 -- may hold).  Such a key never matches, but it
+// moves the reference's ordered walk: compare/3 has no clause for a non-final
+// '#' (emqx_trie_search.erl:282-290 vs :341-348), so at that key it
+//   - seeks to P/W when the topic has a word W at that level: the walk skips
+//     P's '+' subtree ('#' < '+' < binaries in term order);
+//   - returns `lower` when the topic ends at P: the wildcard phase ends, or,
+//     under the innermost '+' of P's path at position q, it seeks to the
+//     literal branch P[0..q)/W_q (the '+' frame turns lower into a seek,
+//     :302-320).
+constexpr uint32_t NLIT_HDESC = 0x80000000u;
+constexpr uint32_t NLIT_MASK = 0x7FFFFFFFu;
+
 // Summary of a child Q (Node.psum for the '+' child, CSlot.sum for a literal
 // child), two levels deep so a '+' chain that dies one level down is skipped too:
-//   bits 0-2  Q has a '#' terminal / an exact terminal / a '+' child (QQ)
-//   bits 3-5  the same for QQ (0 if Q has no '+' child)
-//   bits 6-34  29-bit Bloom of Q's literal child wids  (all ones past 29 children)
-//   bits 35-63 29-bit Bloom of QQ's literal child wids
-constexpr uint32_t PSUM_HASH = 1u, PSUM_EXACT = 2u, PSUM_PLUS = 4u;   // bits of psum_lo (<< 3: QQ's)
+//   bits 0-3  Q has a '#' terminal / an exact terminal / a '+' child (QQ) /
+//             NLIT_HDESC (a visit at the topic's last level cuts the walk)
+//   bits 4-7  the same for QQ (0 if Q has no '+' child)
+//   bits 8-35  28-bit Bloom of Q's literal child wids  (all ones past 28 children)
+//   bits 36-63 28-bit Bloom of QQ's literal child wids
+constexpr uint32_t PSUM_HASH = 1u, PSUM_EXACT = 2u, PSUM_PLUS = 4u, PSUM_HDESC = 8u;   // psum_lo bits (<< 4: QQ's)
+constexpr uint32_t PSUM_QQ = 4, PSUM_BQ = 8, PSUM_BQQ = 36, PSUM_BLOOM = 28;
 
 struct alignas(16) ExactEntry {    // 64 B
     uint32_t h_lo, h_hi;           // hash of the wid sequence
@@ -145,7 +162,7 @@ TM_HD uint32_t vocab_tag(uint64_t h, uint32_t len) {
 // child table hash: low bits pick the slot, the high 16 bits the Bloom bits
 TM_HD uint32_t child_hash(uint32_t wid) { return (uint32_t)mix64((uint64_t)wid * 0x9e3779b97f4a7c15ull + 1); }
 TM_HD uint32_t child_bit(uint32_t h) { return ((h >> 16) * 192u) >> 16; }      // 0..191, table-mode Bloom
-TM_HD uint32_t psum_bit(uint32_t h) { return ((h >> 16) * 29u) >> 16; }      // 0..28, + 6 (Q) or + 35 (QQ)
+TM_HD uint32_t psum_bit(uint32_t h) { return ((h >> 16) * PSUM_BLOOM) >> 16; }   // 0..27, + PSUM_BQ / PSUM_BQQ
 // Bloom word j (bits 32j .. 32j+31) of a table-mode node line
 TM_HD uint32_t &bloom_word(Node &n, uint32_t j) { return j < 2 ? n.kw[2 + j] : n.kc[j - 2]; }
 

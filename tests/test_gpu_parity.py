@@ -1391,3 +1391,97 @@ def test_ds_beamformer_waitq_known_answers(torch_dev):
     waitq.insert("s1", [b"foo", b"bar"], 2, ("val", 22), tab)
     assert sorted(waitq.matches("s1", [b"foo", b"bar"], tab)) == [("val", 22)]
     assert waitq.matches("s1", b"foo/2", tab) == []
+
+
+# ------------------------------------- '#' not last (tm_layout.h NLIT_HDESC)
+
+def _hdesc_sets(seed, n_topics=60, deep=False):
+    """Small alphabets so the cuts and seeks of '#'-not-last keys interact
+    with '+' branches, terminals and binary keys (filters drawn from the
+    topics, '#' at any level)."""
+    r = random.Random(0x454D5158 + 700 + seed)
+
+    def lvl():
+        c = r.random()
+        if c < 0.4:
+            return r.choice([b"a", b"b", b"c"])
+        if c < 0.5:
+            return b""
+        if c < 0.55:
+            return b"$x"
+        return b"%d" % r.randint(0, 3)
+
+    hi = 40 if deep else 6
+    topics = [b"/".join(lvl() for _ in range(r.randint(1, hi if r.random() < 0.3 else 6))) for _ in range(n_topics)]
+    filters, flags = [], []
+    for _ in range(r.randint(5, 60)):
+        base = r.choice(topics).split(b"/")
+        f = [r.choices([x, b"+", b"#", lvl()], [4, 2, 1, 1])[0] for x in base]
+        if r.random() < 0.3:
+            f.append(b"#")
+        filters.append(b"/".join(f))
+        flags.append(int(r.random() < 0.2))
+    return topics, filters, np.array(flags, np.uint8)
+
+
+def test_reference_quirk_hash_not_last_on_device(torch_dev):
+    """The known answer of tests/test_oracle_golden.py::test_reference_quirk_hash_not_last
+    on the device: '+/#/#' makes the reference's walk seek past '+/+//#' for
+    topic 'E//' (compare/3 has no clause for a non-final '#',
+    emqx_trie_search.erl:341-348); without it the filter matches."""
+    for filters, exp in (([b"+/+//#", b"+/#/#"], []), ([b"+/+//#"], [0])):
+        fs = items_of(filters)
+        ix, o = gpu_index(fs), oracle_of(fs)
+        for batch in (1, 9000):   # wave walk / lane walk
+            ts = items_of([b"E//"] * batch)
+            hit, vals = assert_same(ix, o, ts)
+            assert vals[: hit[1]].tolist() == exp
+        val, found = ix.first_batch(*_native.pack_strings([b"E//"]))
+        assert found[0] == (1 if exp else 0)
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_hash_not_last_random_sets_vs_oracle(torch_dev, seed):
+    """'#'-not-last keys in random sets: the seek past '+' and the cut at the
+    topic's last level, through both walks (a batch of <= 8192 topics takes
+    the wave walk, a larger one the lane walk and its tail kernels -- LDS and,
+    beyond 32 levels, global-scratch stores), match/2's first hit, and after
+    deletes / re-inserts of those keys."""
+    topics, filters, flags = _hdesc_sets(seed, deep=seed % 3 == 0)
+    fs = items_of(filters)
+    ix, o = gpu_index(fs, flags), oracle_of(fs, flags)
+    small = items_of(topics)
+    big = items_of(topics * (9000 // len(topics) + 1))
+    assert_same(ix, o, small)
+    assert_same(ix, o, big)
+    for ts in (small, big):
+        val, found = ix.first_batch(ts.blob, ts.offs)
+        for i in range(len(topics)):
+            rc, v = o.first(ts.item(i))
+            assert found[i] == {-1: 2, 0: 0, 1: 1}[rc], ts.item(i)
+            if rc == 1:
+                assert val[i] == v, ts.item(i)
+    r = random.Random(seed)
+    dele = sorted(r.sample(range(len(filters)), len(filters) // 2))
+    d = items_of([filters[i] for i in dele], dele)
+    for ops in (np.zeros(len(dele), np.uint8), np.ones(len(dele), np.uint8)):
+        ix.apply(ops, d.blob, d.offs, d.vals, flags[dele])
+        o.apply(ops, d.blob, d.offs, d.vals, flags[dele])
+        assert_same(ix, o, small)
+        assert_same(ix, o, big)
+
+
+def test_hash_not_last_keys_leave_no_trie_behind(torch_dev):
+    """A '#'-not-last key keeps the trie path of its prefix alive (its node
+    holds the cut); deleting it prunes that path like any other key."""
+    ix = gpu_index()
+    base = ix.stats()
+    keys = items_of([b"a/b/#/c", b"x/+/#/#", b"#/y"])
+    ix.apply(np.ones(3, np.uint8), keys.blob, keys.offs, keys.vals)
+    st = ix.stats()
+    assert st["n_dead_keys"] == 3 and st["n_nodes"] > base["n_nodes"]
+    ix.apply(np.ones(3, np.uint8), keys.blob, keys.offs, keys.vals)   # re-insert: no-op
+    assert ix.stats()["n_nodes"] == st["n_nodes"]
+    ix.apply(np.zeros(3, np.uint8), keys.blob, keys.offs, keys.vals)
+    st2 = ix.stats()
+    assert st2["n_dead_keys"] == 0 and st2["n_nodes"] == base["n_nodes"] and st2["n_words"] == base["n_words"]

@@ -131,9 +131,9 @@ def test_reference_quirk_hash_not_last():
     produced by the reference's generator mk_topic_filter/2) makes compare/3
     return a seek past the '+' siblings at that level ('#' < '+' in term order,
     emqx_trie_search.erl:341-348), so '+/+//#' is skipped for topic 'E//'.
-    The oracle reproduces the reference walk; the spec matcher and the GPU
-    index (which stores such keys as never-matching) do not.  DESIGN.md
-    "Parity domain" records this."""
+    The oracle reproduces the reference walk and the spec matcher does not;
+    the device reproduces it too (tm_layout.h NLIT_HDESC,
+    test_gpu_parity.py::test_reference_quirk_hash_not_last_on_device)."""
     o = Oracle()
     o.insert(b"+/+//#", 41)
     o.insert(b"+/#/#", 62)
