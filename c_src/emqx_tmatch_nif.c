@@ -3,95 +3,60 @@
  *
  * The binding a maintainer adds to EMQX so that emqx_topic_index (and the
  * router's filter table, emqx_router.erl:511-516) matches on the MI355X.
- * Erlang side: src/emqx_topic_index_gpu.erl.  Not built in this image (no
- * OTP, no erl_nif.h -- SURVEY.md 8c); build line in INTEGRATION.md.
+ * Erlang side: src/emqx_tmatch_nif.erl, src/emqx_topic_index_gpu.erl.  Not
+ * built in this image (no OTP, no erl_nif.h -- SURVEY.md 8c); build line in
+ * INTEGRATION.md.  Everything that does not touch ERTS -- buffer pool, packing,
+ * the TM_ECAP retry, result rows -- is in tmatch_nif_core.c, which the CPU
+ * tests compile and run (tests/test_nif_core_cpu.py); this file only converts
+ * terms.
  *
  * Concurrency follows the reference's read path: every publishing process
  * calls emqx_topic_index:matches/3 on its own, lock-free, against a
  * read_concurrency ETS table (emqx_topic_index.erl:41-48).  Here:
- *   - tm_match_batch_ex / tm_first_batch / tm_apply_deltas are thread safe
+ *   - tm_match_batch_ex / tm_first_batch / tm_apply_deltas_ex are thread safe
  *     (include/tmatch.h): each host batch runs on its own stream and the
  *     library never holds its index lock across a GPU wait;
- *   - the NIF keeps a pool of pinned batch-buffer sets (tm_host_alloc, so a
- *     batch of <= 64k topics runs in place with no staging copies).  A dirty
- *     scheduler takes a set from the pool under `pool_mu` for a few
- *     instructions, runs its batch with no lock held, and returns the set.
- *     Nothing is locked while the GPU works.
+ *   - a dirty scheduler takes a pinned buffer set from the pool (a few
+ *     instructions under the pool mutex), runs its batch with no lock held,
+ *     and gives the set back;
+ *   - readers register with the library's reader epochs (read_begin/read_end)
+ *     around the batch and the decoding of its u32s, and the writer reuses a
+ *     deleted key's u32 only once epoch/1's safe epoch has passed the delete's
+ *     epoch (src/emqx_topic_index_gpu.erl), so no reader decodes a stale u32
+ *     into a newer key.
  *
- * Functions (all on dirty schedulers; a 4k-topic batch takes ~0.1 ms):
- *   new(Device)                         -> {ok, Ref} | {error, Code}
- *   apply(Ref, [{Op, Filter, U32, Kind}]) -> ok      Op 1 insert, 0 delete;
- *                                                   Kind 0 binary, 1 words, 2 []
- *   match_batch(Ref, [Topic], Order)    -> [[U32] | badarg | system_limit]
- *                                          Order: traversal | sorted | unique
- *   first_batch(Ref, [Topic])           -> [{ok, U32} | false | badarg | system_limit]
- *   stats(Ref)                          -> #{n_keys => ..., ...}
+ * Functions:
+ *   new(Device)                           -> {ok, Ref} | {error, Code}
+ *   apply(Ref, [{Op, Filter, U32, Kind}]) -> {ok, Epoch} | {error, Code}
+ *                                            Op 1 insert, 0 delete; Kind 0 binary, 1 words, 2 []
+ *   match_batch(Ref, [Topic], Order)      -> [[U32] | badarg | system_limit] | {error, Code}
+ *                                            Order: traversal | sorted | unique
+ *   first_batch(Ref, [Topic])             -> [{ok, U32} | false | badarg | system_limit] | {error, Code}
+ *   read_begin(Ref)                       -> {ok, Ticket}
+ *   read_end(Ref, Ticket)                 -> ok
+ *   epoch(Ref)                            -> {Current, Safe}
+ *   stats(Ref)                            -> #{n_keys => ..., ...}
  */
 #include <erl_nif.h>
 #include <string.h>
 
 #include "tmatch.h"
-
-#define POOL_MAX 64      /* buffer sets kept; more concurrent callers allocate and free their own */
-
-typedef struct { void *p; uint64_t cap; } pbuf;
-
-typedef struct bufset {
-    pbuf blob, offs, hit, vals, err, uniq;
-    struct bufset *next;
-} bufset;
+#include "tmatch_nif_core.h"
 
 typedef struct {
     tm_index *h;
-    ErlNifMutex *pool_mu;   /* guards `pool` and `npool` only */
-    bufset *pool;
-    int npool;
+    tmn_pool pool;
 } idx_res;
 
 static ErlNifResourceType *IDX_RT;
 static ERL_NIF_TERM A_OK, A_ERROR, A_FALSE, A_BADARG, A_SYSTEM_LIMIT, A_TRAVERSAL, A_SORTED, A_UNIQUE;
 
-/* grow-only pinned buffer (contents are not kept across a grow) */
-static void *pget(tm_index *h, pbuf *b, uint64_t need) {
-    if (need <= b->cap) return b->p;
-    if (b->p) tm_host_free(h, b->p);
-    b->cap = need + need / 2 + 4096;
-    if (tm_host_alloc(h, b->cap, &b->p) != TM_OK) { b->p = NULL; b->cap = 0; }
-    return b->p;
-}
-
-static void set_free(tm_index *h, bufset *s) {
-    pbuf *all[] = {&s->blob, &s->offs, &s->hit, &s->vals, &s->err, &s->uniq};
-    for (unsigned i = 0; i < sizeof all / sizeof all[0]; i++)
-        if (all[i]->p) tm_host_free(h, all[i]->p);
-    enif_free(s);
-}
-
-static bufset *set_take(idx_res *r) {
-    enif_mutex_lock(r->pool_mu);
-    bufset *s = r->pool;
-    if (s) { r->pool = s->next; r->npool--; }
-    enif_mutex_unlock(r->pool_mu);
-    if (!s) {
-        s = enif_alloc(sizeof *s);
-        if (s) memset(s, 0, sizeof *s);
-    }
-    return s;
-}
-
-static void set_give(idx_res *r, bufset *s) {
-    enif_mutex_lock(r->pool_mu);
-    if (r->npool < POOL_MAX) { s->next = r->pool; r->pool = s; r->npool++; s = NULL; }
-    enif_mutex_unlock(r->pool_mu);
-    if (s) set_free(r->h, s);
-}
-
 static void idx_dtor(ErlNifEnv *env, void *obj) {
     idx_res *r = obj;
     (void)env;
-    while (r->pool) { bufset *s = r->pool; r->pool = s->next; set_free(r->h, s); }
-    if (r->h) tm_destroy(r->h);
-    if (r->pool_mu) enif_mutex_destroy(r->pool_mu);
+    if (!r->h) return;
+    tmn_pool_destroy(&r->pool);
+    tm_destroy(r->h);
 }
 
 static int load(ErlNifEnv *env, void **priv, ERL_NIF_TERM info) {
@@ -119,16 +84,16 @@ static ERL_NIF_TERM nif_new(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[])
     if (!enif_get_int(env, argv[0], &dev)) return enif_make_badarg(env);
     idx_res *r = enif_alloc_resource(IDX_RT, sizeof *r);
     memset(r, 0, sizeof *r);
-    r->pool_mu = enif_mutex_create("tm_index_pool");
     tm_options o = {dev, 0, 0};
     int rc = tm_create(&o, &r->h);
     if (rc != TM_OK) { r->h = NULL; enif_release_resource(r); return err_term(env, rc); }
+    tmn_pool_init(&r->pool, r->h);
     ERL_NIF_TERM t = enif_make_resource(env, r);
     enif_release_resource(r);
     return enif_make_tuple2(env, A_OK, t);
 }
 
-/* apply(Ref, [{Op, FilterBin, U32, Kind}]) -> ok | {error, Code}
+/* apply(Ref, [{Op, FilterBin, U32, Kind}]) -> {ok, Epoch} | {error, Code}
    One router-syncer batch (emqx_router_syncer.erl:297-356) = one call. */
 static ERL_NIF_TERM nif_apply(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
     idx_res *r;
@@ -136,13 +101,17 @@ static ERL_NIF_TERM nif_apply(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[
     (void)argc;
     if (!enif_get_resource(env, argv[0], IDX_RT, (void **)&r) || !enif_get_list_length(env, argv[1], &n))
         return enif_make_badarg(env);
-    if (n == 0) return A_OK;
+    uint64_t epoch = 0;
+    if (n == 0) {
+        tm_epoch(r->h, &epoch, NULL);
+        return enif_make_tuple2(env, A_OK, enif_make_uint64(env, epoch));
+    }
     uint8_t *ops = enif_alloc(n), *kinds = enif_alloc(n);
     uint32_t *vals = enif_alloc(4ull * n);
     uint64_t *offs = enif_alloc(8ull * (n + 1));
     ErlNifBinary *bins = enif_alloc(sizeof(ErlNifBinary) * n);
     uint8_t *blob = NULL;
-    ERL_NIF_TERM l = argv[1], h, res = A_OK;
+    ERL_NIF_TERM l = argv[1], h, res;
     uint64_t tot = 0;
     for (unsigned i = 0; enif_get_list_cell(env, l, &h, &l); i++) {
         const ERL_NIF_TERM *e;
@@ -159,39 +128,28 @@ static ERL_NIF_TERM nif_apply(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[
     offs[n] = tot;
     blob = enif_alloc(tot + 1);
     for (unsigned i = 0; i < n; i++) memcpy(blob + offs[i], bins[i].data, bins[i].size);
-    int rc = tm_apply_deltas(r->h, n, ops, blob, offs, vals, kinds);   /* thread safe, no NIF lock */
-    if (rc != TM_OK) res = err_term(env, rc);
+    int rc = tm_apply_deltas_ex(r->h, n, ops, blob, offs, vals, kinds, &epoch);   /* thread safe, no NIF lock */
+    res = rc == TM_OK ? enif_make_tuple2(env, A_OK, enif_make_uint64(env, epoch)) : err_term(env, rc);
 out:
     enif_free(ops); enif_free(kinds); enif_free(vals); enif_free(offs); enif_free(bins);
     if (blob) enif_free(blob);
     return res;
 }
 
-/* pack a topic list into the set's pinned blob/offs; n = list length */
-static int pack_topics(ErlNifEnv *env, idx_res *r, bufset *s, ERL_NIF_TERM list, unsigned n,
-                       uint8_t **blob_out, uint64_t **offs_out) {
+/* the topic list's binaries (views into the caller's terms, valid during the call) */
+static int topic_views(ErlNifEnv *env, ERL_NIF_TERM list, unsigned n, const uint8_t ***ps, uint64_t **ls) {
+    const uint8_t **p = enif_alloc(sizeof *p * (n + 1));
+    uint64_t *len = enif_alloc(sizeof *len * (n + 1));
     ERL_NIF_TERM l = list, h;
-    uint64_t tot = 0;
     ErlNifBinary b;
-    while (enif_get_list_cell(env, l, &h, &l)) {
-        if (!enif_inspect_binary(env, h, &b)) return TM_EINVAL;
-        tot += b.size;
-    }
-    uint8_t *blob = pget(r->h, &s->blob, tot + 16);
-    uint64_t *offs = pget(r->h, &s->offs, 8ull * (n + 1));
-    if (!blob || !offs) return TM_ENOMEM;
-    tot = 0;
-    l = list;
     for (unsigned i = 0; enif_get_list_cell(env, l, &h, &l); i++) {
-        enif_inspect_binary(env, h, &b);
-        offs[i] = tot;
-        memcpy(blob + tot, b.data, b.size);
-        tot += b.size;
+        if (!enif_inspect_binary(env, h, &b)) { enif_free(p); enif_free(len); return 0; }
+        p[i] = b.data;
+        len[i] = b.size;
     }
-    offs[n] = tot;
-    *blob_out = blob;
-    *offs_out = offs;
-    return TM_OK;
+    *ps = p;
+    *ls = len;
+    return 1;
 }
 
 /* match_batch(Ref, [TopicBin], Order) -> [[U32] | badarg | system_limit]
@@ -210,40 +168,28 @@ static ERL_NIF_TERM nif_match_batch(ErlNifEnv *env, int argc, const ERL_NIF_TERM
     else if (enif_is_identical(argv[2], A_UNIQUE)) order = TM_ORDER_UNIQUE;
     else return enif_make_badarg(env);
     if (n == 0) return enif_make_list(env, 0);
-    bufset *s = set_take(r);
-    if (!s) return err_term(env, TM_ENOMEM);
-    uint8_t *blob;
-    uint64_t *offs;
-    int rc = pack_topics(env, r, s, argv[1], n, &blob, &offs);
-    if (rc == TM_EINVAL) { set_give(r, s); return enif_make_badarg(env); }
-    uint64_t *hit = pget(r->h, &s->hit, 8ull * (n + 1));
-    uint8_t *err = pget(r->h, &s->err, (uint64_t)n + 1);
-    uint32_t *uniq = order == TM_ORDER_UNIQUE ? pget(r->h, &s->uniq, 4ull * n) : NULL;
-    /* capacity: what the set already holds, at least 16 ids per topic */
-    uint64_t cap = s->vals.cap / 4 > 16ull * n ? s->vals.cap / 4 : 16ull * n + 1024;
-    uint32_t *vals = pget(r->h, &s->vals, 4 * cap);
-    if (rc == TM_OK && (!hit || !err || !vals || (order == TM_ORDER_UNIQUE && !uniq))) rc = TM_ENOMEM;
-    if (rc == TM_OK) {
-        rc = tm_match_batch_ex(r->h, n, blob, offs, hit, vals, cap, err, order, uniq);
-        if (rc == TM_ECAP) {   /* offsets are valid: rerun with room for every id */
-            cap = hit[n];
-            vals = pget(r->h, &s->vals, 4 * cap);
-            rc = vals ? tm_match_batch_ex(r->h, n, blob, offs, hit, vals, cap, err, order, uniq) : TM_ENOMEM;
-        }
-    }
+    const uint8_t **tp;
+    uint64_t *tl;
+    if (!topic_views(env, argv[1], n, &tp, &tl)) return enif_make_badarg(env);
+    tmn_set *s = tmn_take(&r->pool);
+    int rc = s ? tmn_pack(s, r->h, n, tp, tl) : TM_ENOMEM;
+    enif_free(tp); enif_free(tl);
+    if (rc == TM_OK) rc = tmn_match(s, r->h, n, order);
     ERL_NIF_TERM out = enif_make_list(env, 0);
+    const uint32_t *vals = s ? tmn_vals(s) : NULL;
     for (unsigned i = n; rc == TM_OK && i-- > 0;) {
+        uint64_t b, e;
+        const int err = tmn_row(s, n, order, i, &b, &e);
         ERL_NIF_TERM row;
-        if (err[i]) {
-            row = err[i] == 2 ? A_SYSTEM_LIMIT : A_BADARG;   /* 2: > 65536 levels */
+        if (err) {
+            row = err == 2 ? A_SYSTEM_LIMIT : A_BADARG;   /* 2: > 65536 levels */
         } else {
-            const uint64_t b = hit[i], e = order == TM_ORDER_UNIQUE ? hit[i] + uniq[i] : hit[i + 1];
             row = enif_make_list(env, 0);
             for (uint64_t k = e; k-- > b;) row = enif_make_list_cell(env, enif_make_uint(env, vals[k]), row);
         }
         out = enif_make_list_cell(env, row, out);
     }
-    set_give(r, s);
+    tmn_give(&r->pool, s);
     return rc == TM_OK ? out : err_term(env, rc);
 }
 
@@ -256,24 +202,55 @@ static ERL_NIF_TERM nif_first_batch(ErlNifEnv *env, int argc, const ERL_NIF_TERM
     if (!enif_get_resource(env, argv[0], IDX_RT, (void **)&r) || !enif_get_list_length(env, argv[1], &n))
         return enif_make_badarg(env);
     if (n == 0) return enif_make_list(env, 0);
-    bufset *s = set_take(r);
-    if (!s) return err_term(env, TM_ENOMEM);
-    uint8_t *blob;
-    uint64_t *offs;
-    int rc = pack_topics(env, r, s, argv[1], n, &blob, &offs);
-    if (rc == TM_EINVAL) { set_give(r, s); return enif_make_badarg(env); }
-    uint32_t *val = pget(r->h, &s->vals, 4ull * n);
-    uint8_t *found = pget(r->h, &s->err, n);
-    if (rc == TM_OK && (!val || !found)) rc = TM_ENOMEM;
-    if (rc == TM_OK) rc = tm_first_batch(r->h, n, blob, offs, val, found);
+    const uint8_t **tp;
+    uint64_t *tl;
+    if (!topic_views(env, argv[1], n, &tp, &tl)) return enif_make_badarg(env);
+    tmn_set *s = tmn_take(&r->pool);
+    int rc = s ? tmn_pack(s, r->h, n, tp, tl) : TM_ENOMEM;
+    enif_free(tp); enif_free(tl);
+    if (rc == TM_OK) rc = tmn_first(s, r->h, n);
     ERL_NIF_TERM out = enif_make_list(env, 0);
     for (unsigned i = n; rc == TM_OK && i-- > 0;) {
-        ERL_NIF_TERM row = found[i] == 1 ? enif_make_tuple2(env, A_OK, enif_make_uint(env, val[i]))
-                         : found[i] == 2 ? A_BADARG : found[i] == 3 ? A_SYSTEM_LIMIT : A_FALSE;
+        uint32_t v;
+        const int f = tmn_first_row(s, i, &v);
+        ERL_NIF_TERM row = f == 1 ? enif_make_tuple2(env, A_OK, enif_make_uint(env, v))
+                         : f == 2 ? A_BADARG : f == 3 ? A_SYSTEM_LIMIT : A_FALSE;
         out = enif_make_list_cell(env, row, out);
     }
-    set_give(r, s);
+    tmn_give(&r->pool, s);
     return rc == TM_OK ? out : err_term(env, rc);
+}
+
+/* read_begin(Ref) -> {ok, Ticket}: a reader registers before its batch */
+static ERL_NIF_TERM nif_read_begin(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
+    idx_res *r;
+    uint64_t t;
+    (void)argc;
+    if (!enif_get_resource(env, argv[0], IDX_RT, (void **)&r)) return enif_make_badarg(env);
+    int rc = tm_read_begin(r->h, &t);
+    return rc == TM_OK ? enif_make_tuple2(env, A_OK, enif_make_uint64(env, t)) : err_term(env, rc);
+}
+
+/* read_end(Ref, Ticket) -> ok: after the reader has decoded its results */
+static ERL_NIF_TERM nif_read_end(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
+    idx_res *r;
+    ErlNifUInt64 t;
+    (void)argc;
+    if (!enif_get_resource(env, argv[0], IDX_RT, (void **)&r) || !enif_get_uint64(env, argv[1], &t))
+        return enif_make_badarg(env);
+    int rc = tm_read_end(r->h, t);
+    return rc == TM_OK ? A_OK : err_term(env, rc);
+}
+
+/* epoch(Ref) -> {Current, Safe} (include/tmatch.h "Reader epochs") */
+static ERL_NIF_TERM nif_epoch(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
+    idx_res *r;
+    uint64_t cur, safe;
+    (void)argc;
+    if (!enif_get_resource(env, argv[0], IDX_RT, (void **)&r)) return enif_make_badarg(env);
+    int rc = tm_epoch(r->h, &cur, &safe);
+    return rc == TM_OK ? enif_make_tuple2(env, enif_make_uint64(env, cur), enif_make_uint64(env, safe))
+                       : err_term(env, rc);
 }
 
 /* stats(Ref) -> map (emqx_router:stats/1's n_routes part, emqx_router.erl:632-635) */
@@ -299,6 +276,9 @@ static ErlNifFunc funcs[] = {
     {"apply", 2, nif_apply, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"match_batch", 3, nif_match_batch, ERL_NIF_DIRTY_JOB_IO_BOUND},
     {"first_batch", 2, nif_first_batch, ERL_NIF_DIRTY_JOB_IO_BOUND},
+    {"read_begin", 1, nif_read_begin, 0},
+    {"read_end", 2, nif_read_end, 0},
+    {"epoch", 1, nif_epoch, 0},
     {"stats", 1, nif_stats, 0},
 };
 

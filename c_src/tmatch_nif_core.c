@@ -1,0 +1,118 @@
+/*
+ * tmatch_nif_core.c -- ERTS-free half of the NIF (see tmatch_nif_core.h).
+ */
+#include "tmatch_nif_core.h"
+
+#include <stdlib.h>
+#include <string.h>
+
+void tmn_pool_init(tmn_pool *p, tm_index *h) {
+    memset(p, 0, sizeof *p);
+    p->h = h;
+    pthread_mutex_init(&p->mu, NULL);
+}
+
+static void set_free(tm_index *h, tmn_set *s) {
+    tmn_buf *all[] = {&s->blob, &s->offs, &s->hit, &s->vals, &s->err, &s->uniq};
+    for (unsigned i = 0; i < sizeof all / sizeof all[0]; i++)
+        if (all[i]->p) tm_host_free(h, all[i]->p);
+    free(s);
+}
+
+void tmn_pool_destroy(tmn_pool *p) {
+    while (p->pool) {
+        tmn_set *s = p->pool;
+        p->pool = s->next;
+        set_free(p->h, s);
+    }
+    p->npool = 0;
+    pthread_mutex_destroy(&p->mu);
+}
+
+tmn_set *tmn_take(tmn_pool *p) {
+    pthread_mutex_lock(&p->mu);
+    tmn_set *s = p->pool;
+    if (s) { p->pool = s->next; p->npool--; }
+    pthread_mutex_unlock(&p->mu);
+    if (!s) s = calloc(1, sizeof *s);
+    if (s) s->next = NULL;
+    return s;
+}
+
+void tmn_give(tmn_pool *p, tmn_set *s) {
+    if (!s) return;
+    pthread_mutex_lock(&p->mu);
+    if (p->npool < TMN_POOL_MAX) { s->next = p->pool; p->pool = s; p->npool++; s = NULL; }
+    pthread_mutex_unlock(&p->mu);
+    if (s) set_free(p->h, s);
+}
+
+void *tmn_get(tm_index *h, tmn_buf *b, uint64_t need) {
+    if (need <= b->cap && b->p) return b->p;
+    if (b->p) tm_host_free(h, b->p);
+    b->p = NULL;
+    b->cap = need + need / 2 + 4096;
+    if (tm_host_alloc(h, b->cap, &b->p) != TM_OK) { b->p = NULL; b->cap = 0; }
+    return b->p;
+}
+
+int tmn_pack(tmn_set *s, tm_index *h, uint32_t n, const uint8_t *const *topics, const uint64_t *lens) {
+    uint64_t tot = 0;
+    for (uint32_t i = 0; i < n; i++) tot += lens[i];
+    uint8_t *blob = tmn_get(h, &s->blob, tot + 16);
+    uint64_t *offs = tmn_get(h, &s->offs, 8ull * (n + 1));
+    if (!blob || !offs) return TM_ENOMEM;
+    tot = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        offs[i] = tot;
+        if (lens[i]) memcpy(blob + tot, topics[i], lens[i]);
+        tot += lens[i];
+    }
+    offs[n] = tot;
+    return TM_OK;
+}
+
+int tmn_match(tmn_set *s, tm_index *h, uint32_t n, uint32_t order) {
+    uint64_t *hit = tmn_get(h, &s->hit, 8ull * (n + 1));
+    uint8_t *err = tmn_get(h, &s->err, (uint64_t)n + 1);
+    uint32_t *uniq = order == TM_ORDER_UNIQUE ? tmn_get(h, &s->uniq, 4ull * n + 4) : NULL;
+    /* capacity: what the set already holds, at least TMN_IDS_PER_TOPIC ids per topic */
+    const uint64_t want = (uint64_t)TMN_IDS_PER_TOPIC * n + 1024;
+    uint64_t cap = s->vals.cap / 4 > want ? s->vals.cap / 4 : want;
+    uint32_t *vals = tmn_get(h, &s->vals, 4 * cap);
+    if (!hit || !err || !vals || (order == TM_ORDER_UNIQUE && !uniq)) return TM_ENOMEM;
+    cap = s->vals.cap / 4;
+    int rc = tm_match_batch_ex(h, n, s->blob.p, s->offs.p, hit, vals, cap, err, order, uniq);
+    /* TM_ECAP: the offsets are valid, so rerun with room for every id (again
+       if concurrent inserts grew the total in between; a few times at most) */
+    for (int tries = 0; rc == TM_ECAP && tries < 4; tries++) {
+        s->reruns++;
+        vals = tmn_get(h, &s->vals, 4 * hit[n]);
+        rc = vals ? tm_match_batch_ex(h, n, s->blob.p, s->offs.p, hit, vals, s->vals.cap / 4, err, order, uniq)
+                  : TM_ENOMEM;
+    }
+    return rc;
+}
+
+int tmn_first(tmn_set *s, tm_index *h, uint32_t n) {
+    uint32_t *val = tmn_get(h, &s->vals, 4ull * n + 4);
+    uint8_t *found = tmn_get(h, &s->err, (uint64_t)n + 1);
+    if (!val || !found) return TM_ENOMEM;
+    return tm_first_batch(h, n, s->blob.p, s->offs.p, val, found);
+}
+
+int tmn_row(const tmn_set *s, uint32_t n, uint32_t order, uint32_t i, uint64_t *b, uint64_t *e) {
+    const uint64_t *hit = s->hit.p;
+    const uint8_t *err = s->err.p;
+    (void)n;
+    *b = *e = 0;
+    if (err[i]) return err[i];
+    *b = hit[i];
+    *e = order == TM_ORDER_UNIQUE ? hit[i] + ((const uint32_t *)s->uniq.p)[i] : hit[i + 1];
+    return 0;
+}
+
+int tmn_first_row(const tmn_set *s, uint32_t i, uint32_t *v) {
+    *v = ((const uint32_t *)s->vals.p)[i];
+    return ((const uint8_t *)s->err.p)[i];
+}

@@ -24,7 +24,7 @@ EXPORTS = ("tm_create", "tm_destroy", "tm_apply_deltas", "tm_sync", "tm_match_ba
            "tm_match_batch_dev", "tm_first_batch", "tm_stats", "tm_profile_enable", "tm_profile_read",
            "tm_last_error", "tm_abi_version", "tm_merge_shards", "tm_host_alloc", "tm_host_free",
            "tm_stream_release", "tm_match_batch_ex", "tm_match_batch_dev_ex", "tm_sort_segments",
-           "tm_matches_filter")
+           "tm_matches_filter", "tm_apply_deltas_ex", "tm_read_begin", "tm_read_end", "tm_epoch")
 
 
 class NativeUnavailable(RuntimeError):
@@ -83,6 +83,10 @@ def load_library(path: Path | None = None):
         "tm_match_batch_ex": (i32, [vp, u64, vp, vp, vp, vp, u64, vp, u32, vp]),
         "tm_match_batch_dev_ex": (i32, [vp, u64, vp, vp, vp, vp, u64, vp, u32, vp, vp]),
         "tm_sort_segments": (i32, [vp, u64, vp, vp, u64, u32, vp, vp]),
+        "tm_apply_deltas_ex": (i32, [vp, u64, vp, vp, vp, vp, vp, C.POINTER(u64)]),
+        "tm_read_begin": (i32, [vp, C.POINTER(u64)]),
+        "tm_read_end": (i32, [vp, u64]),
+        "tm_epoch": (i32, [vp, C.POINTER(u64), C.POINTER(u64)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -164,8 +168,25 @@ class Index:
         blob = np.ascontiguousarray(blob, dtype=np.uint8)
         if flags is not None:
             flags = np.ascontiguousarray(flags, dtype=np.uint8)
-        self._check(self._lib.tm_apply_deltas(self._h, len(ops), _ptr(ops), _ptr(blob), _ptr(offs),
-                                              _ptr(values), _ptr(flags)))
+        e = C.c_uint64()
+        self._check(self._lib.tm_apply_deltas_ex(self._h, len(ops), _ptr(ops), _ptr(blob), _ptr(offs),
+                                                 _ptr(values), _ptr(flags), C.byref(e)))
+        return e.value
+
+    # ---- reader epochs (include/tmatch.h "Reader epochs")
+    def read_begin(self) -> int:
+        t = C.c_uint64()
+        self._check(self._lib.tm_read_begin(self._h, C.byref(t)))
+        return t.value
+
+    def read_end(self, ticket: int):
+        self._check(self._lib.tm_read_end(self._h, ticket))
+
+    def epoch(self) -> tuple[int, int]:
+        """-> (current epoch, safe epoch: the oldest running reader's, or current)."""
+        cur, safe = C.c_uint64(), C.c_uint64()
+        self._check(self._lib.tm_epoch(self._h, C.byref(cur), C.byref(safe)))
+        return cur.value, safe.value
 
     def sync(self, stream: int | None = None):
         self._check(self._lib.tm_sync(self._h, stream))

@@ -146,15 +146,29 @@ struct tm_index {
     std::vector<uint64_t> depth_cnt, xlen_cnt;
 
     std::unordered_set<std::string> dead;
-    uint64_t key_gen = 0;   // bumped by every key operation (matches_filter's sorted keys follow it)
-    struct MfState {        // matches_filter/3: the word-list keys in term order (built on demand)
-        uint64_t gen = ~0ull, K = 0;
-        std::vector<std::string> words;   // distinct binary words, byte order
-        uint32_t *pool = nullptr, *val = nullptr; uint64_t *koff = nullptr;
+    // matches_filter/3 (tm_matches_filter) keeps its own copy of the word-list
+    // keys, in term order on the device.  It is built from a fuzzy snapshot
+    // of the trie taken in short slices under `mu` plus the log of every
+    // word-list key op since the snapshot began (replayed afterwards), and
+    // follows the log from then on, so the index lock is held only for
+    // slices of a few hundred microseconds and to swap the log -- never for a
+    // sort, an upload or a GPU wait (matches_filter stalled every
+    // match batch for a second at 10M keys).
+    struct MfState {
+        std::mutex mu;                        // one matches_filter call at a time (never taken by matching)
+        bool log_on = false, log_lost = false;   // (under ix->mu) ops logged since the snapshot / log dropped
+        std::vector<std::pair<bool, std::string>> log;   // (insert?, key) -- under ix->mu
+        std::unordered_set<std::string> keys; // kind | value | filter of every word-list key (under mu)
+        bool have_keys = false, dev_stale = true;
+        std::atomic<size_t> nkeys{0};         // keys.size(), for the log bound (read under ix->mu)
+        std::vector<std::string> words;       // distinct binary words, byte order
+        uint32_t *pool = nullptr, *val = nullptr; uint64_t *koff = nullptr, K = 0;
+        uint64_t pcap = 0, vcap = 0, kcap = 0;
         uint32_t *q = nullptr; uint64_t qcap = 0;   // staging: query offsets, ranks, bases, counts
         uint8_t *err = nullptr; uint64_t *hit = nullptr; uint32_t *out = nullptr;
         uint64_t ecap = 0, ocap = 0, hcap = 0;
         hipStream_t s = nullptr;
+        uint64_t snapshots = 0, slices = 0;   // diagnostics
     } mf;
     uint64_t n_wild = 0, n_exact = 0;
     uint64_t uploads = 0, patch_bytes = 0;
@@ -866,13 +880,27 @@ std::string dead_key(const uint8_t *f, uint32_t len, uint32_t v, uint8_t flags) 
     return k;
 }
 
+// matches_filter's log of word-list key ops (tm_index::MfState; caller holds
+// ix->mu).  Unbounded growth between calls is cut: past a bound the log is
+// dropped and the next call takes a new snapshot.
+void mf_log(tm_index *ix, bool ins, const std::string &key) {
+    auto &m = ix->mf;
+    if (!m.log_on) return;
+    if (m.log.size() >= std::max<size_t>(size_t(1) << 22, 2 * m.nkeys.load(std::memory_order_relaxed))) {
+        m.log_on = false; m.log_lost = true;
+        std::vector<std::pair<bool, std::string>>().swap(m.log);
+        return;
+    }
+    m.log.emplace_back(ins, key);
+}
+
 // one insert (ins = true) or delete of the key make_key(Filter, V)
 void key_op(tm_index *ix, bool ins, const uint8_t *f, uint32_t len, uint32_t v, uint8_t flags,
             std::vector<WordRef> &w, std::vector<uint32_t> &wids) {
-    ix->key_gen++;
     if (flags & TM_KEY_EMPTY_LIST) {   // [] never matches a topic (topics have >= 1 level)
         auto k = dead_key(nullptr, 0, v, TM_KEY_EMPTY_LIST);
         if (ins) ix->dead.insert(k); else ix->dead.erase(k);
+        mf_log(ix, ins, k);
         return;
     }
     split_words(f, len, w);
@@ -925,6 +953,7 @@ void key_op(tm_index *ix, bool ins, const uint8_t *f, uint32_t len, uint32_t v, 
         ix->exact.touch(s);
         return;
     }
+    if (ix->mf.log_on) mf_log(ix, ins, dead_key(f, len, v, TM_KEY_WORDS));
     // word-list key.  '#' anywhere but last never matches (compare/3 has no
     // clause for it, emqx_trie_search.erl:282-290 vs :341-348; emqx_topic.erl:110),
     // but the key still steers the reference's walk at the node P of its
@@ -933,7 +962,8 @@ void key_op(tm_index *ix, bool ins, const uint8_t *f, uint32_t len, uint32_t v, 
     for (size_t i = 0; i + 1 < w.size(); i++)
         if (w[i].kind == 2) { hpos = i; break; }
     if (hpos < w.size()) {
-        auto k = dead_key(f, len, v, flags & TM_KEY_WORDS);
+        // (a wildcard filter is a word list whatever the flag: one key)
+        auto k = dead_key(f, len, v, TM_KEY_WORDS);
         if (ins ? !ix->dead.insert(k).second : !ix->dead.erase(k)) return;   // present / absent: no-op
     }
     const bool hash_term = hpos == w.size() && w.back().kind == 2;
@@ -1831,79 +1861,102 @@ uint32_t mf_rank(const std::vector<std::string> &words, const std::string &w) {
 }
 
 void mf_free_keys(tm_index::MfState &m) {
-    if (m.pool) (void)hipFree(m.pool);
-    if (m.koff) (void)hipFree(m.koff);
-    if (m.val) (void)hipFree(m.val);
-    m.pool = nullptr; m.koff = nullptr; m.val = nullptr; m.K = 0;
+    for (void *p : {(void *)m.pool, (void *)m.koff, (void *)m.val}) if (p) (void)hipFree(p);
+    m.pool = nullptr; m.koff = nullptr; m.val = nullptr; m.K = 0; m.pcap = m.kcap = m.vcap = 0;
 }
 
-// the word-list keys (trie terminals + keys that never match a topic) as rank
-// sequences sorted by (ranks, value) -- emqx_trie_search's ordered_set order
-int mf_build(tm_index *ix) {
+// the filter of trie node `node` (words joined by '/'), for the snapshot
+void mf_path(tm_index *ix, uint32_t node, std::string &out) {
+    std::vector<uint32_t> up;
+    for (uint32_t x = node; x != ROOT; x = ix->aux[x].parent) up.push_back(x);
+    out.clear();
+    std::string w;
+    for (size_t i = up.size(); i-- > 0;) {
+        const NodeAux &a = ix->aux[up[i]];
+        if (a.is_plus) w = "+";
+        else vocab_bytes(ix, ix->vocab.h[ix->wslot[a.wid]], w);
+        if (i + 1 != up.size()) out.push_back('/');
+        out += w;
+    }
+}
+
+// Fuzzy snapshot of the word-list keys (caller holds m.mu, not ix->mu): the
+// log starts first, then the trie's nodes are read in slices under the index
+// lock, each ending after MF_SLICE_US (checked every 64 nodes); replaying the
+// log afterwards makes the copy exact (a key untouched since the log started
+// sits on a node that cannot move, so a slice sees it; any other key ends as
+// its last logged op leaves it).
+constexpr double MF_SLICE_US = 100.0;
+
+void mf_snapshot(tm_index *ix) {
     auto &m = ix->mf;
-    if (m.gen == ix->key_gen && m.pool) return TM_OK;
-    std::vector<std::string> words;
-    std::string tmp;
-    std::vector<uint32_t> vwid;
-    for (const VocabEntry &e : ix->vocab.h)
-        if (e.wid != NONE) { vocab_bytes(ix, e, tmp); words.push_back(tmp); vwid.push_back(e.wid); }
-    std::vector<std::string> dw;
-    for (const std::string &k : ix->dead) {
+    m.keys.clear();
+    {
+        std::lock_guard<std::mutex> g(ix->mu);
+        m.log.clear();
+        m.log_on = true;
+        m.log_lost = false;
+        for (const std::string &k : ix->dead) m.keys.insert(k);
+    }
+    std::string path, key;
+    for (uint64_t cur = 0;;) {
+        std::lock_guard<std::mutex> g(ix->mu);
+        const auto t0 = std::chrono::steady_clock::now();
+        uint64_t end = ix->nodes.h.size(), x = cur;
+        for (; x < end; x++) {
+            if ((x & 63) == 63 &&
+                std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() > MF_SLICE_US) {
+                end = x;
+                break;
+            }
+            const Node &n = ix->nodes.h[x];
+            if (!(n.exact_cnt & RUN_CNT) && !(n.hash_cnt & RUN_CNT)) continue;
+            mf_path(ix, (uint32_t)x, path);
+            const NodeAux &a = ix->aux[x];
+            auto add = [&](uint32_t roff, uint32_t cnt, bool hash) {
+                for (uint32_t i = 0; i < cnt; i++) {
+                    const uint32_t v = ix->vals.h[roff + i];
+                    std::string f = hash ? (path.empty() ? std::string("#") : path + "/#") : path;
+                    m.keys.insert(dead_key(reinterpret_cast<const uint8_t *>(f.data()), (uint32_t)f.size(), v,
+                                           TM_KEY_WORDS));
+                }
+            };
+            add(a.exact_roff, n.exact_cnt & RUN_CNT, false);
+            add(a.hash_roff, n.hash_cnt & RUN_CNT, true);
+        }
+        m.slices++;
+        cur = end;
+        if (cur >= ix->nodes.h.size()) break;
+    }
+    m.snapshots++;
+    m.have_keys = true;
+}
+
+// the device's term-ordered key arrays from m.keys (caller holds m.mu only)
+int mf_upload(tm_index *ix) {
+    auto &m = ix->mf;
+    std::vector<std::string> dw, sorted;
+    std::unordered_set<std::string> distinct;
+    for (const std::string &k : m.keys) {
         if ((uint8_t)k[0] & TM_KEY_EMPTY_LIST) continue;
         mf_words_of(reinterpret_cast<const uint8_t *>(k.data()) + 5, (uint32_t)k.size() - 5, dw);
-        for (auto &x : dw) if (x != "+" && x != "#") words.push_back(x);
+        for (auto &x : dw) if (x != "+" && x != "#") distinct.insert(x);
     }
-    std::vector<std::string> sorted = words;
+    sorted.assign(distinct.begin(), distinct.end());
     std::sort(sorted.begin(), sorted.end());
-    sorted.erase(std::unique(sorted.begin(), sorted.end()), sorted.end());
-    std::vector<uint32_t> rank_of(ix->wid_next + 1, 0);
-    for (size_t i = 0; i < vwid.size(); i++) rank_of[vwid[i]] = mf_rank(sorted, words[i]);
-    // keys: (offset into pool, length, value)
     std::vector<uint32_t> pool;
     struct K { uint64_t off; uint32_t len, val; };
     std::vector<K> keys;
-    auto add_run = [&](const std::vector<uint32_t> &path, uint32_t roff, uint32_t cnt) {
-        for (uint32_t i = 0; i < cnt; i++) {
-            keys.push_back(K{pool.size(), (uint32_t)path.size(), ix->vals.h[roff + i]});
-            pool.insert(pool.end(), path.begin(), path.end());
-        }
-    };
-    std::vector<std::pair<uint32_t, uint32_t>> st{{ROOT, 0}};   // (node, depth)
-    std::vector<uint32_t> path;
-    while (!st.empty()) {
-        const auto [node, d] = st.back();
-        st.pop_back();
-        path.resize(d);
-        if (node != ROOT) path.push_back(ix->aux[node].is_plus ? 1u : rank_of[ix->aux[node].wid]);
-        const Node &n = ix->nodes.h[node];
-        const NodeAux &a = ix->aux[node];
-        if (n.exact_cnt & RUN_CNT) add_run(path, a.exact_roff, n.exact_cnt & RUN_CNT);
-        if (n.hash_cnt & RUN_CNT) {
-            path.push_back(0);
-            add_run(path, a.hash_roff, n.hash_cnt & RUN_CNT);
-            path.pop_back();
-        }
-        const uint32_t cd = node == ROOT ? 0 : d + 1;
-        if (n.plus != NONE) st.push_back({n.plus, cd});
-        if (nlit_of(n) <= KINL) {
-            for (uint32_t k = 0; k < KINL; k++) if (n.kw[k] != NONE) st.push_back({n.kc[k], cd});
-        } else {
-            for (uint32_t i = 0; i <= n.kw[1]; i++) {
-                const CSlot &c = ix->ctab.h[n.kw[0] + i];
-                if (c.wid != NONE) st.push_back({c.child, cd});
-            }
-        }
-    }
-    for (const std::string &k : ix->dead) {
+    keys.reserve(m.keys.size());
+    for (const std::string &k : m.keys) {
         uint32_t v;
         memcpy(&v, k.data() + 1, 4);
-        std::vector<uint32_t> r;
+        const uint64_t off = pool.size();
         if (!((uint8_t)k[0] & TM_KEY_EMPTY_LIST)) {
             mf_words_of(reinterpret_cast<const uint8_t *>(k.data()) + 5, (uint32_t)k.size() - 5, dw);
-            for (auto &x : dw) r.push_back(mf_rank(sorted, x));
+            for (auto &x : dw) pool.push_back(mf_rank(sorted, x));
         }
-        keys.push_back(K{pool.size(), (uint32_t)r.size(), v});
-        pool.insert(pool.end(), r.begin(), r.end());
+        keys.push_back(K{off, (uint32_t)(pool.size() - off), v});
     }
     std::sort(keys.begin(), keys.end(), [&](const K &x, const K &y) {
         const uint32_t m2 = std::min(x.len, y.len);
@@ -1922,17 +1975,53 @@ int mf_build(tm_index *ix) {
         kval[i] = keys[i].val;
     }
     koff[keys.size()] = spool.size();
-    mf_free_keys(m);
-    HIPCHK(ix, hipMalloc(&m.pool, std::max<size_t>(spool.size(), 1) * 4));
-    HIPCHK(ix, hipMalloc(&m.koff, koff.size() * 8));
-    HIPCHK(ix, hipMalloc(&m.val, std::max<size_t>(kval.size(), 1) * 4));
-    if (!spool.empty()) HIPCHK(ix, hipMemcpy(m.pool, spool.data(), spool.size() * 4, hipMemcpyHostToDevice));
-    HIPCHK(ix, hipMemcpy(m.koff, koff.data(), koff.size() * 8, hipMemcpyHostToDevice));
-    if (!kval.empty()) HIPCHK(ix, hipMemcpy(m.val, kval.data(), kval.size() * 4, hipMemcpyHostToDevice));
+    // grow-only device arrays (a free would wait for the device), async copies on the mf stream
+    auto grow = [&](auto *&p, uint64_t &cap, uint64_t need, size_t elt) -> int {
+        if (need <= cap && p) return TM_OK;
+        if (p) { HIPCHK(ix, hipStreamSynchronize(m.s)); HIPCHK(ix, hipFree(p)); }
+        p = nullptr;
+        cap = need + need / 4 + 1024;
+        HIPCHK(ix, hipMalloc(reinterpret_cast<void **>(&p), cap * elt));
+        return TM_OK;
+    };
+    int rc;
+    if ((rc = grow(m.pool, m.pcap, spool.size(), 4))) return rc;
+    if ((rc = grow(m.koff, m.kcap, koff.size(), 8))) return rc;
+    if ((rc = grow(m.val, m.vcap, kval.size(), 4))) return rc;
+    if (!spool.empty()) HIPCHK(ix, hipMemcpyAsync(m.pool, spool.data(), spool.size() * 4, hipMemcpyHostToDevice, m.s));
+    HIPCHK(ix, hipMemcpyAsync(m.koff, koff.data(), koff.size() * 8, hipMemcpyHostToDevice, m.s));
+    if (!kval.empty()) HIPCHK(ix, hipMemcpyAsync(m.val, kval.data(), kval.size() * 4, hipMemcpyHostToDevice, m.s));
+    HIPCHK(ix, hipStreamSynchronize(m.s));   // the host vectors die here
     m.K = keys.size();
     m.words.swap(sorted);
-    m.gen = ix->key_gen;
+    m.dev_stale = false;
     return TM_OK;
+}
+
+// bring m.keys up to date: a new snapshot when there is none (or its log was
+// dropped), else the logged ops since the last call -- the index lock is
+// held only to swap the log out
+int mf_refresh(tm_index *ix) {
+    auto &m = ix->mf;
+    std::vector<std::pair<bool, std::string>> log;
+    bool lost;
+    {
+        std::lock_guard<std::mutex> g(ix->mu);
+        lost = m.log_lost || !m.log_on;
+        if (!lost) log.swap(m.log);
+    }
+    if (lost || !m.have_keys) {
+        mf_snapshot(ix);
+        std::lock_guard<std::mutex> g(ix->mu);
+        log.swap(m.log);
+        m.dev_stale = true;
+    }
+    for (auto &op : log) {
+        if (op.first) m.keys.insert(op.second); else m.keys.erase(op.second);
+    }
+    if (!log.empty()) m.dev_stale = true;
+    m.nkeys.store(m.keys.size(), std::memory_order_relaxed);
+    return m.dev_stale ? mf_upload(ix) : TM_OK;
 }
 
 template <class T>
@@ -1955,12 +2044,12 @@ int tm_matches_filter(tm_index *ix, uint64_t n, const uint8_t *fb, const uint64_
     if (!fo || !out_hit_offsets || !out_err || (n && !fb && fo[n] != fo[0]) || (cap && !out_values))
         return fail(ix, TM_EINVAL, "tm_matches_filter: null buffer");
     if (n >= 0xFFFFFFFFull) return fail(ix, TM_EINVAL, "tm_matches_filter: batch too large");
-    std::lock_guard<std::mutex> g(ix->mu);   // control plane: one call at a time
-    HIPCHK(ix, hipSetDevice(ix->device));
     auto &m = ix->mf;
+    std::lock_guard<std::mutex> g(m.mu);   // control plane: one call at a time; the index lock stays free
+    HIPCHK(ix, hipSetDevice(ix->device));
     if (!m.s) HIPCHK(ix, hipStreamCreateWithFlags(&m.s, hipStreamNonBlocking));
     int rc;
-    if ((rc = mf_build(ix))) return rc;
+    if ((rc = mf_refresh(ix))) return rc;
     // queries: filter_words/1 (:359-366) -> ranks; base_init on a '$' first word
     std::vector<uint32_t> qoff(n + 1, 0), qr, qbase(n, NONE);
     std::vector<std::string> w;

@@ -50,8 +50,16 @@ def pack_slices(hit: torch.Tensor, vals: torch.Tensor, world: int, per_peer: int
     n = hit.numel() - 1
     s, _ = slice_bounds(n, world)
     dev = hit.device
-    counts = torch.zeros(world * s, dtype=torch.int32, device=dev)
-    counts[:n] = (hit[1:] - hit[:-1]).to(torch.int32)
+    c = torch.zeros(world * s, dtype=torch.int64, device=dev)
+    c[:n] = hit[1:] - hit[:-1]
+    # a slice that overflows per_peer ships its first per_peer values only, and
+    # its counts are cut to match: the receiver's offsets (a scan of the
+    # counts) stay inside the per_peer values it gets, so the merge never
+    # reads past a peer's slot; check() reports the overflow and the caller
+    # reruns the batch with a larger capacity
+    c = c.view(world, s)
+    start = torch.cumsum(c, dim=1) - c
+    counts = torch.minimum(c, torch.clamp(per_peer - start, min=0)).to(torch.int32).view(-1)
     edges = torch.clamp(torch.arange(world + 1, device=dev, dtype=torch.int64) * s, max=n)
     bounds = hit[edges]                                    # slice q = vals[bounds[q] : bounds[q+1]]
     lens = bounds[1:] - bounds[:-1]

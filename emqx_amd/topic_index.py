@@ -11,6 +11,14 @@ deletes are queued and shipped with one ``tm_apply_deltas`` call before the
 next match (the router-syncer batch boundary, emqx_router_syncer.erl:297-356).
 Matching always runs on the GPU through ``libtmatch``; there is no CPU path.
 
+Concurrency (as on the reference's read_concurrency table,
+emqx_topic_index.erl:41-48): any number of threads may match while one
+thread writes.  A reader registers with the library's reader epochs
+(include/tmatch.h) around its device batch AND the decoding of the returned
+u32s; a deleted key's u32 sits in quarantine until every reader that began
+before the delete has finished, so a value decodes to its own key or to
+nothing (a key deleted meanwhile is dropped) -- never to a key inserted later.
+
 Result order: the device returns keys in traversal order (ascending Erlang
 term order).  ``matches/3`` returns them like the reference does -- reversed,
 because match_add/2 prepends (emqx_trie_search.erl:350-356); ``[unique]``
@@ -18,6 +26,9 @@ keeps the last key per ID (maps:values, sorted by ID as small maps are);
 ``match/2`` is the first key in traversal order.
 """
 from __future__ import annotations
+
+import threading
+from collections import deque
 
 import numpy as np
 
@@ -29,14 +40,17 @@ from .trie_search import (BadArg, HASH, PLUS, filter_words, get_id, get_topic, k
 class Tab:
     """An index table: records + the device-resident mirror of its keys."""
 
-    def __init__(self, device: int = -1, hint_keys: int = 0):
-        self._index = _native.Index(device=device, hint_keys=hint_keys)
+    def __init__(self, device: int = -1, hint_keys: int = 0, index=None):
+        self._index = index if index is not None else _native.Index(device=device, hint_keys=hint_keys)
         self._records: dict = {}        # key -> record        (the ETS rows)
         self._kid: dict = {}            # key -> u32 value on the device
-        self._keys: list = []           # u32 -> key
-        self._free: list[int] = []
+        self._keys: list = []           # u32 -> key (None: deleted)
+        self._free: list[int] = []      # u32s no reader can still return
+        self._released: list[int] = []  # freed by deletes not yet shipped
+        self._quarantine = deque()      # (epoch of the delete, u32): reusable once the safe epoch reaches it
         self._dead: set = set()         # keys that can never match (kept host-side only)
         self._ops: list = []            # pending (op, filter_bytes, kid, flags)
+        self._lock = threading.Lock()   # pending deltas and u32 bookkeeping (writer side)
         self._sorted = None             # (keys, order keys) in term order, for matches_filter/3
 
     # -- key <-> device encoding
@@ -70,36 +84,51 @@ class Tab:
         self._ops.append((op, enc[0], kid, enc[1]))
 
     def flush(self):
-        if not self._ops:
-            return
-        ops = np.array([o[0] for o in self._ops], dtype=np.uint8)
-        blob, offs = _native.pack_strings([o[1] for o in self._ops])
-        vals = np.array([o[2] for o in self._ops], dtype=np.uint32)
-        flags = np.array([o[3] for o in self._ops], dtype=np.uint8)
-        self._ops = []
-        self._index.apply(ops, blob, offs, vals, flags)
+        with self._lock:
+            if not self._ops:
+                return
+            ops = np.array([o[0] for o in self._ops], dtype=np.uint8)
+            blob, offs = _native.pack_strings([o[1] for o in self._ops])
+            vals = np.array([o[2] for o in self._ops], dtype=np.uint32)
+            flags = np.array([o[3] for o in self._ops], dtype=np.uint8)
+            self._ops = []
+            epoch = self._index.apply(ops, blob, offs, vals, flags)
+            # the deletes just shipped are visible from `epoch` on: their u32s
+            # wait until no reader that began earlier is running
+            for kid in self._released:
+                self._quarantine.append((epoch, kid))
+            self._released = []
 
-    # -- table operations
+    def _take_kid(self) -> int:
+        if not self._free and self._quarantine:
+            _, safe = self._index.epoch()
+            while self._quarantine and self._quarantine[0][0] <= safe:
+                self._free.append(self._quarantine.popleft()[1])
+        if self._free:
+            return self._free.pop()
+        self._keys.append(None)
+        return len(self._keys) - 1
+
+    # -- table operations (one writer at a time, as the reference's callers)
     def insert_key(self, key, record):
-        if key not in self._records:
-            self._sorted = None
-            kid = self._free.pop() if self._free else len(self._keys)
-            if kid == len(self._keys):
-                self._keys.append(key)
-            else:
+        with self._lock:
+            if key not in self._records:
+                self._sorted = None
+                kid = self._take_kid()
                 self._keys[kid] = key
-            self._kid[key] = kid
-            self._queue(_native.TM_OP_INSERT, key, kid)
-        self._records[key] = record
+                self._kid[key] = kid
+                self._queue(_native.TM_OP_INSERT, key, kid)
+            self._records[key] = record
 
     def delete_key(self, key):
-        if key in self._records:
-            self._sorted = None
-            kid = self._kid.pop(key)
-            del self._records[key]
-            self._queue(_native.TM_OP_DELETE, key, kid)
-            self._keys[kid] = None
-            self._free.append(kid)
+        with self._lock:
+            if key in self._records:
+                self._sorted = None
+                kid = self._kid.pop(key)
+                del self._records[key]
+                self._queue(_native.TM_OP_DELETE, key, kid)
+                self._keys[kid] = None
+                self._released.append(kid)
 
     def size(self) -> int:
         return len(self._records)
@@ -119,11 +148,24 @@ class Tab:
 
     # -- matching (batched: the unit the broker micro-batch hands over)
     def match_kids(self, topics):
-        """-> (list of kid arrays in traversal order, badarg flags)."""
+        """-> (list of kid arrays in traversal order, badarg flags).  The
+        caller decodes the kids inside a read_begin()/read_end() pair."""
         self.flush()
         blob, offs = _native.pack_strings(topics)
         hit, vals, err = self._index.match_batch(blob, offs)
         return [vals[hit[i]:hit[i + 1]] for i in range(len(topics))], err
+
+    def read_begin(self) -> int:
+        return self._index.read_begin()
+
+    def read_end(self, ticket: int):
+        self._index.read_end(ticket)
+
+    def decode(self, kids):
+        """u32s -> keys; a key deleted since the batch began is dropped (its
+        u32 is quarantined, so it cannot name a newer key yet)."""
+        keys = self._keys
+        return [k for k in (keys[i] for i in kids.tolist()) if k is not None]
 
     def stats(self) -> dict:
         self.flush()
@@ -164,17 +206,20 @@ def matches_batch(topics, tab: Tab, opts=(), errors: str = "raise"):
     micro-batch of many publishers fails only the bad publish, as each
     publishing process does in the reference."""
     topics = [bytes(t) for t in topics]
-    kids, err = tab.match_kids(topics)
-    out = []
-    for i, ks in enumerate(kids):
-        if err[i]:
-            e = TopicTooDeep(len(topics[i])) if err[i] == 2 else BadArg(topics[i])
-            if errors == "raise":
-                raise e
-            out.append(e)
-            continue
-        keys = [tab._keys[k] for k in ks.tolist()]
-        out.append(_finish(keys, opts))
+    ticket = tab.read_begin()
+    try:
+        kids, err = tab.match_kids(topics)
+        out = []
+        for i, ks in enumerate(kids):
+            if err[i]:
+                e = TopicTooDeep(len(topics[i])) if err[i] == 2 else BadArg(topics[i])
+                if errors == "raise":
+                    raise e
+                out.append(e)
+                continue
+            out.append(_finish(tab.decode(ks), opts))
+    finally:
+        tab.read_end(ticket)
     return out
 
 
@@ -238,10 +283,16 @@ def matches_filter(filter_, tab: Tab, opts=()):
     control-plane (durable-storage stream discovery,
     emqx_ds_new_streams.erl:325)."""
     if not tab._dead and isinstance(filter_, (bytes, bytearray)):
-        tab.flush()
-        blob, offs = _native.pack_strings([bytes(filter_)])
-        _, vals, _ = tab._index.matches_filter_batch(blob, offs)
-        return _finish([tab._keys[int(v)] for v in vals], opts)
+        ticket = tab.read_begin()
+        try:
+            tab.flush()
+            blob, offs = _native.pack_strings([bytes(filter_)])
+            _, vals, err = tab._index.matches_filter_batch(blob, offs)
+            if len(err) and err[0]:   # the device walk hit its step bound: no silent truncation
+                raise RuntimeError(f"matches_filter: device walk exceeded its step bound for {bytes(filter_)!r}")
+            return _finish(tab.decode(vals), opts)
+        finally:
+            tab.read_end(ticket)
     keys, order = tab.sorted_keys()
     return _finish(search_filter(keys, order, filter_words(filter_)), opts)
 

@@ -55,5 +55,18 @@ def matches(stream, topic, tab: WaitQ):
     if t is None:
         return []
     if isinstance(topic, (list, tuple)):
+        if not topic:
+            return [r for k in _matches_no_levels(t) for r in ti.get_record(k, t)]
         topic = b"/".join(bytes(w) for w in topic)
     return [r for k in ti.matches(topic, t, []) for r in ti.get_record(k, t)]
+
+
+def _matches_no_levels(t):
+    """matches/3 of the word list [] (zero levels -- no topic binary has that
+    form: b"" is one empty level): compare/3 gives match_full for a stored []
+    and a stored ['#'] (emqx_trie_search.erl:262-290) and `lower` for every
+    other word list, and match_topics/4 then stops (:381-389).  So the keys are
+    those two filters' keys, in traversal order reversed (match_add/2)."""
+    keys, _ = t.sorted_keys()
+    hits = [k for k in keys if isinstance(k[0], tuple) and k[0] in ((), (ti.HASH,))]
+    return hits[::-1]

@@ -20,6 +20,9 @@
  *   tm_first_batch
  *       emqx_topic_index:match/2            apps/emqx/src/emqx_topic_index.erl:70-72
  *       (first key in traversal order; emqx_trie_search.erl:171-178,350-356)
+ *   tm_apply_deltas_ex, tm_read_begin / tm_read_end / tm_epoch
+ *       safe reuse of u32 values under lock-free readers (see "Reader epochs";
+ *       emqx_topic_index.erl:41-48 is the read_concurrency contract kept)
  *   tm_stats
  *       emqx_router:stats/1 n_routes part    apps/emqx/src/emqx_router.erl:632-635
  *   tm_merge_shards
@@ -100,6 +103,32 @@ int tm_destroy(tm_index *h);
  * stream order, so a batch sees exactly the deltas applied before it). */
 int tm_apply_deltas(tm_index *h, uint64_t n, const uint8_t *ops, const uint8_t *filter_bytes,
                     const uint64_t *filter_offsets, const uint32_t *values, const uint8_t *key_flags);
+
+/* tm_apply_deltas, also returning the delta epoch the batch made current
+ * (*out_epoch, may be NULL): every call with n > 0 advances the index's epoch
+ * by one (see "Reader epochs" below). */
+int tm_apply_deltas_ex(tm_index *h, uint64_t n, const uint8_t *ops, const uint8_t *filter_bytes,
+                       const uint64_t *filter_offsets, const uint32_t *values, const uint8_t *key_flags,
+                       uint64_t *out_epoch);
+
+/* Reader epochs: when may a caller hand a value freed by a delete to a new key?
+ * The reference's readers walk a read_concurrency ETS table and decode keys
+ * from it lock-free (emqx_topic_index.erl:41-48): a concurrent delete can hide
+ * a key, but a reader never sees a key that does not match.  Here a reader gets
+ * u32 values back and turns them into keys afterwards, so a value must not be
+ * reused while a reader that may still return it is running:
+ *   tm_read_begin   registers a reader at the current epoch (before it queues
+ *                   its batches); *ticket identifies it;
+ *   tm_read_end     unregisters it (after it has decoded its results);
+ *   tm_epoch        *current = the index's epoch, *safe = the smallest epoch
+ *                   of a registered reader (= *current when there is none).
+ * A value freed by a delete that tm_apply_deltas_ex reported as epoch E may be
+ * reused once *safe >= E: every reader still running began after the delete,
+ * and its batches cannot see the old key.  No reference counterpart (ETS
+ * keys are their own identity).  Thread safe; never blocks on the GPU. */
+int tm_read_begin(tm_index *h, uint64_t *ticket);
+int tm_read_end(tm_index *h, uint64_t ticket);
+int tm_epoch(tm_index *h, uint64_t *current, uint64_t *safe);
 
 /* Upload pending patches on `stream` (hipStream_t; NULL = the default stream). */
 int tm_sync(tm_index *h, void *stream);

@@ -2,7 +2,7 @@
 %% include/tmatch.h).  Not built in this image (no OTP, SURVEY.md 8c).
 -module(emqx_tmatch_nif).
 
--export([new/1, apply/2, match_batch/3, first_batch/2, stats/1]).
+-export([new/1, apply/2, match_batch/3, first_batch/2, read_begin/1, read_end/2, epoch/1, stats/1]).
 -on_load(init/0).
 
 -type ref() :: reference().
@@ -23,7 +23,8 @@ init() ->
 -spec new(integer()) -> {ok, ref()} | {error, integer()}.
 new(_Device) -> erlang:nif_error(nif_not_loaded).
 
--spec apply(ref(), [delta()]) -> ok | {error, integer()}.
+%% {ok, Epoch}: the delta epoch the batch made current (include/tmatch.h "Reader epochs").
+-spec apply(ref(), [delta()]) -> {ok, non_neg_integer()} | {error, integer()}.
 apply(_Ref, _Deltas) -> erlang:nif_error(nif_not_loaded).
 
 -spec match_batch(ref(), [binary()], order()) -> [[u32()] | badarg | system_limit] | {error, integer()}.
@@ -31,6 +32,17 @@ match_batch(_Ref, _Topics, _Order) -> erlang:nif_error(nif_not_loaded).
 
 -spec first_batch(ref(), [binary()]) -> [{ok, u32()} | false | badarg | system_limit] | {error, integer()}.
 first_batch(_Ref, _Topics) -> erlang:nif_error(nif_not_loaded).
+
+%% A reader registers before its batch and unregisters after decoding it.
+-spec read_begin(ref()) -> {ok, non_neg_integer()}.
+read_begin(_Ref) -> erlang:nif_error(nif_not_loaded).
+
+-spec read_end(ref(), non_neg_integer()) -> ok.
+read_end(_Ref, _Ticket) -> erlang:nif_error(nif_not_loaded).
+
+%% {Current, Safe}: a kid released at epoch E may be reused once Safe >= E.
+-spec epoch(ref()) -> {non_neg_integer(), non_neg_integer()}.
+epoch(_Ref) -> erlang:nif_error(nif_not_loaded).
 
 -spec stats(ref()) -> #{atom() => non_neg_integer()}.
 stats(_Ref) -> erlang:nif_error(nif_not_loaded).

@@ -7,12 +7,20 @@
 %%         truth (get_record/2, matches_filter/3 and every write go to it first)
 %%   kids  ETS set interning each key to a u32 the device stores:
 %%         {{k, Key}, Kid} and {{v, Kid}, Key}, plus {next, N}
-%%   free  ETS set of released kids, reused by later inserts
+%%   quar  ETS ordered_set {{Epoch, Kid}}: kids released by a delete that the
+%%         device saw from Epoch on; a kid leaves quarantine for `free` once
+%%         no reader that began before that epoch is still running
+%%   free  ETS set of kids no reader can still return, reused by later inserts
 %%   ref   the device index (emqx_tmatch_nif resource)
 %%
 %% Reads (match/2, matches/3, matches_batch/3) run lock-free from any process,
 %% as on the reference's read_concurrency table (:41-48); the NIF runs each
-%% call on its own HIP stream.  Writes (insert/4, delete/3) come from the
+%% call on its own HIP stream.  A read registers with the library's reader
+%% epochs (read_begin/read_end, include/tmatch.h) around its device batch and
+%% the decoding of the returned kids, so a kid it gets back names its own key
+%% or -- deleted meanwhile -- nothing (dropped), never a key inserted later:
+%% the reference's ETS walk may miss a concurrent write but never returns a
+%% key that does not match.  Writes (insert/4, delete/3) come from the
 %% table's owner process, as every reference caller does (emqx_rule_engine.erl:537,
 %% emqx_schema_validation_registry.erl:263, emqx_bridge_mqtt_ingress.erl:203,
 %% the router syncer): a write updates ETS, then ships one delta; a batch of
@@ -29,7 +37,7 @@
 -export([make_key/2, get_id/1, get_topic/1, get_record/2]).
 -export([table_event/2, cleanup/2, stats/1]).
 
--record(gtab, {tab, kids, free, ref}).
+-record(gtab, {tab, kids, quar, free, ref}).
 -type gtab() :: #gtab{}.
 -export_type([gtab/0]).
 
@@ -60,7 +68,7 @@ attach(Tab, BatchSize) ->
     G = mirror(Tab),
     ets:safe_fixtable(Tab, true),
     try
-        boot(G, ets:first(Tab), BatchSize, [])
+        boot(G, ets:first(Tab), BatchSize, ?NOACC)
     after
         ets:safe_fixtable(Tab, false)
     end,
@@ -70,14 +78,18 @@ mirror(Tab) ->
     {ok, Ref} = emqx_tmatch_nif:new(-1),
     Kids = ets:new(emqx_topic_index_kids, [set, public, {read_concurrency, true}]),
     true = ets:insert(Kids, {next, 0}),
+    Quar = ets:new(emqx_topic_index_quar, [ordered_set, public]),
     Free = ets:new(emqx_topic_index_free, [set, public]),
-    #gtab{tab = Tab, kids = Kids, free = Free, ref = Ref}.
+    #gtab{tab = Tab, kids = Kids, quar = Quar, free = Free, ref = Ref}.
+
+%% Deltas accumulate as {DeviceDeltas, ReleasedKids}, both prepended.
+-define(NOACC, {[], []}).
 
 boot(G, '$end_of_table', _N, Acc) ->
     flush(G, Acc);
-boot(G, Key, N, Acc) when length(Acc) >= N ->
+boot(G, Key, N, Acc = {D, _}) when length(D) >= N ->
     ok = flush(G, Acc),
-    boot(G, Key, N, []);
+    boot(G, Key, N, ?NOACC);
 boot(G, Key, N, Acc) ->
     boot(G, ets:next(G#gtab.tab, Key), N, intern_delta(G, Key, Acc)).
 
@@ -89,7 +101,7 @@ boot(G, Key, N, Acc) ->
 insert(Filter, ID, Record, G = #gtab{tab = Tab}) ->
     Key = make_key(Filter, ID),
     true = ets:insert(Tab, {Key, Record}),
-    ok = flush(G, intern_delta(G, Key, [])),
+    ok = flush(G, intern_delta(G, Key, ?NOACC)),
     true.
 
 %% delete/3 (emqx_topic_index.erl:60-62): deleting a missing entry is not an error.
@@ -97,7 +109,7 @@ insert(Filter, ID, Record, G = #gtab{tab = Tab}) ->
 delete(Filter, ID, G = #gtab{tab = Tab}) ->
     Key = make_key(Filter, ID),
     true = ets:delete(Tab, Key),
-    ok = flush(G, release_delta(G, Key, [])),
+    ok = flush(G, release_delta(G, Key, ?NOACC)),
     true.
 
 %% A batch of {insert, Filter, ID, Record} | {delete, Filter, ID} as ONE device
@@ -115,7 +127,7 @@ apply_batch(Ops, G = #gtab{tab = Tab}) ->
                 true = ets:delete(Tab, Key),
                 release_delta(G, Key, Acc)
         end,
-        [],
+        ?NOACC,
         Ops
     ),
     flush(G, Deltas).
@@ -126,11 +138,11 @@ apply_batch(Ops, G = #gtab{tab = Tab}) ->
 %% event here (after mnesia has applied it to the ETS table itself).
 -spec table_event(tuple(), gtab()) -> ok.
 table_event({write, _Tab, Rec, _Old, _Tid}, G) ->
-    flush(G, intern_delta(G, element(2, Rec), []));
+    flush(G, intern_delta(G, element(2, Rec), ?NOACC));
 table_event({delete, _Tab, {_, Key}, _Old, _Tid}, G) ->
-    flush(G, release_delta(G, Key, []));
+    flush(G, release_delta(G, Key, ?NOACC));
 table_event({delete_object, _Tab, Rec, _Old, _Tid}, G) ->
-    flush(G, release_delta(G, element(2, Rec), []));
+    flush(G, release_delta(G, element(2, Rec), ?NOACC));
 table_event(_, _G) ->
     ok.
 
@@ -155,40 +167,62 @@ cleanup(Pred, G = #gtab{tab = Tab}) ->
             true = ets:delete(Tab, Key),
             release_delta(G, Key, Acc)
         end,
-        [],
+        ?NOACC,
         Doomed
     ),
     flush(G, Deltas).
 
 %% Key -> a device delta (prepended to Acc), interning the key on first sight.
-intern_delta(G = #gtab{kids = Kids}, Key, Acc) ->
+intern_delta(G = #gtab{kids = Kids}, Key, Acc = {D, R}) ->
     case ets:lookup(Kids, {k, Key}) of
         [_] ->
             Acc;
         [] ->
             Kid = take_kid(G),
             true = ets:insert(Kids, [{{k, Key}, Kid}, {{v, Kid}, Key}]),
-            add_delta(?INSERT, Key, Kid, Acc)
+            {add_delta(?INSERT, Key, Kid, D), R}
     end.
 
-release_delta(#gtab{kids = Kids, free = Free}, Key, Acc) ->
+%% The released kid waits for the delta's epoch (flush/2) before quarantine.
+release_delta(#gtab{kids = Kids}, Key, Acc = {D, R}) ->
     case ets:take(Kids, {k, Key}) of
         [{_, Kid}] ->
             true = ets:delete(Kids, {v, Kid}),
-            true = ets:insert(Free, {Kid}),
-            add_delta(?DELETE, Key, Kid, Acc);
+            {add_delta(?DELETE, Key, Kid, D), [Kid | R]};
         [] ->
             Acc
     end.
 
-take_kid(#gtab{kids = Kids, free = Free}) ->
+take_kid(G = #gtab{kids = Kids, free = Free}) ->
     case ets:first(Free) of
         '$end_of_table' ->
-            ets:update_counter(Kids, next, 1) - 1;
+            case reclaim(G) of
+                0 -> ets:update_counter(Kids, next, 1) - 1;
+                _ -> take_kid(G)
+            end;
         Kid ->
             true = ets:delete(Free, Kid),
             Kid
     end.
+
+%% Quarantined kids whose delete every running reader has seen (epoch =< the
+%% safe epoch: the oldest running reader began after it) become free.
+reclaim(#gtab{ref = Ref, quar = Quar, free = Free}) ->
+    case ets:first(Quar) of
+        '$end_of_table' ->
+            0;
+        First ->
+            {_Current, Safe} = emqx_tmatch_nif:epoch(Ref),
+            reclaim(Quar, Free, Safe, First, 0)
+    end.
+
+reclaim(Quar, Free, Safe, K = {Epoch, Kid}, N) when Epoch =< Safe ->
+    Next = ets:next(Quar, K),
+    true = ets:delete(Quar, K),
+    true = ets:insert(Free, {Kid}),
+    reclaim(Quar, Free, Safe, Next, N + 1);
+reclaim(_Quar, _Free, _Safe, _K, N) ->
+    N.
 
 %% make_key/2 forms (emqx_trie_search.erl:115-128) as the C ABI encodes them
 %% (include/tmatch.h "Keys").  A word list holding a binary word equal to
@@ -217,18 +251,50 @@ word_bin('+') -> <<"+">>;
 word_bin('#') -> <<"#">>;
 word_bin(W) -> W.
 
-%% Deltas were accumulated by prepending: ship them in the order they were made.
-flush(_G, []) ->
+%% Deltas were accumulated by prepending: ship them in the order they were
+%% made; the kids they release are quarantined under the epoch the batch made
+%% current (a reader that began earlier may still return them).
+flush(_G, {[], []}) ->
     ok;
-flush(#gtab{ref = Ref}, Deltas) ->
-    ok = emqx_tmatch_nif:apply(Ref, lists:reverse(Deltas)).
+flush(#gtab{ref = Ref, quar = Quar}, {Deltas, Released}) ->
+    {ok, Epoch} = emqx_tmatch_nif:apply(Ref, lists:reverse(Deltas)),
+    true = ets:insert(Quar, [{{Epoch, Kid}} || Kid <- Released]),
+    ok.
 
 %%--------------------------------------------------------------------
 %% Reads
 
 %% match/2 (emqx_topic_index.erl:70-72): the first key in traversal order.
 -spec match(emqx_types:topic(), gtab()) -> emqx_trie_search:key(_) | false.
-match(Topic, G) ->
+%% The device's first hit names the first filter F in traversal order; the
+%% reference's first key is F's smallest {ID}, which the ordered_set itself
+%% gives: ets:next(Tab, {F, {}}) ({} sorts below every {ID}, the base key of
+%% emqx_trie_search.erl:157-158).  If F's keys vanished meanwhile, the full
+%% match decides.
+match(Topic, G = #gtab{tab = Tab, ref = Ref, kids = Kids}) ->
+    {ok, Ticket} = emqx_tmatch_nif:read_begin(Ref),
+    try emqx_tmatch_nif:first_batch(Ref, [Topic]) of
+        [{ok, V}] ->
+            case kid_key(Kids, V) of
+                {true, {F, _}} ->
+                    case ets:next(Tab, {F, {}}) of
+                        First = {F, _} -> First;
+                        _ -> first_of(Topic, G)
+                    end;
+                false ->
+                    first_of(Topic, G)
+            end;
+        [false] ->
+            false;
+        [Err] when is_atom(Err) ->
+            error(Err);
+        Other ->
+            error({tmatch, Other})
+    after
+        ok = emqx_tmatch_nif:read_end(Ref, Ticket)
+    end.
+
+first_of(Topic, G) ->
     case matches_batch([Topic], G, [traversal]) of
         [[K | _]] -> K;
         [[]] -> false
@@ -246,17 +312,22 @@ matches(Topic, G, Opts) ->
 %% raises badarg as the reference's single-topic call does (:374-375).
 -spec matches_batch([emqx_types:topic()], gtab(), list()) -> [[emqx_trie_search:key(_)] | {error, atom()}].
 matches_batch(Topics, #gtab{ref = Ref, kids = Kids}, Opts) ->
-    Rows = emqx_tmatch_nif:match_batch(Ref, Topics, traversal),
-    is_list(Rows) orelse error({tmatch, Rows}),
-    ReturnErrors = proplists:get_bool(return_errors, Opts),
-    [finish(Row, Kids, Opts, ReturnErrors) || Row <- Rows].
+    {ok, Ticket} = emqx_tmatch_nif:read_begin(Ref),
+    try
+        Rows = emqx_tmatch_nif:match_batch(Ref, Topics, traversal),
+        is_list(Rows) orelse error({tmatch, Rows}),
+        ReturnErrors = proplists:get_bool(return_errors, Opts),
+        [finish(Row, Kids, Opts, ReturnErrors) || Row <- Rows]
+    after
+        ok = emqx_tmatch_nif:read_end(Ref, Ticket)
+    end.
 
 finish(Err, _Kids, _Opts, true) when is_atom(Err) ->
     {error, Err};
 finish(Err, _Kids, _Opts, false) when is_atom(Err) ->
     error(Err);
 finish(Row, Kids, Opts, _) ->
-    Keys = traversal([kid_key(Kids, V) || V <- Row]),
+    Keys = traversal(lists:filtermap(fun(V) -> kid_key(Kids, V) end, Row)),
     case proplists:get_bool(traversal, Opts) of
         true ->
             Keys;
@@ -269,9 +340,13 @@ finish(Row, Kids, Opts, _) ->
             end
     end.
 
+%% A key deleted since the batch began is gone from Kids: dropped (its kid is
+%% quarantined, so it cannot name a newer key while this reader runs).
 kid_key(Kids, V) ->
-    [{_, Key}] = ets:lookup(Kids, {v, V}),
-    Key.
+    case ets:lookup(Kids, {v, V}) of
+        [{_, Key}] -> {true, Key};
+        [] -> false
+    end.
 
 %% The device orders keys of different filters by term order; keys of ONE
 %% filter (several IDs) come by u32.  The reference's ordered_set orders them by

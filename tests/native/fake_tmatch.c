@@ -1,0 +1,76 @@
+/*
+ * fake_tmatch.c -- TEST INFRASTRUCTURE: a stand-in for libtmatch's C ABI
+ * (include/tmatch.h) with no device, so c_src/tmatch_nif_core.c can be
+ * exercised on the CPU (tests/test_nif_core_cpu.py).  Topic i "matches" one
+ * value per byte: values 1000 * i + k; a topic whose first byte is '+' is
+ * badarg.  Counts host allocations and batch calls.
+ */
+#include <stdlib.h>
+#include <string.h>
+
+#include "tmatch.h"
+#include "tmatch_nif_core.h"
+
+static long n_alloc, n_free, n_match, n_first;
+
+int tm_host_alloc(tm_index *h, uint64_t bytes, void **out) {
+    (void)h;
+    *out = malloc(bytes ? bytes : 1);
+    if (!*out) return TM_ENOMEM;
+    n_alloc++;
+    return TM_OK;
+}
+
+int tm_host_free(tm_index *h, void *p) {
+    (void)h;
+    free(p);
+    n_free++;
+    return TM_OK;
+}
+
+int tm_match_batch_ex(tm_index *h, uint64_t n, const uint8_t *tb, const uint64_t *to, uint64_t *hit,
+                      uint32_t *vals, uint64_t cap, uint8_t *err, uint32_t order, uint32_t *uniq) {
+    (void)h;
+    n_match++;
+    hit[0] = 0;
+    for (uint64_t i = 0; i < n; i++) {
+        const uint64_t len = to[i + 1] - to[i];
+        err[i] = len && tb[to[i]] == '+';
+        const uint64_t c = err[i] ? 0 : len;
+        for (uint64_t k = 0; k < c; k++) {
+            const uint64_t pos = hit[i] + k;
+            /* unique: distinct values first (here: every other one), padded */
+            uint32_t v = (uint32_t)(1000 * i + k);
+            if (order == TM_ORDER_UNIQUE) v = k < (c + 1) / 2 ? (uint32_t)(1000 * i + k) : 0xFFFFFFFFu;
+            if (pos < cap) vals[pos] = v;
+        }
+        if (uniq) uniq[i] = (uint32_t)((c + 1) / 2);
+        hit[i + 1] = hit[i] + c;
+    }
+    return hit[n] > cap ? TM_ECAP : TM_OK;
+}
+
+int tm_first_batch(tm_index *h, uint64_t n, const uint8_t *tb, const uint64_t *to, uint32_t *val, uint8_t *found) {
+    (void)h;
+    n_first++;
+    for (uint64_t i = 0; i < n; i++) {
+        const uint64_t len = to[i + 1] - to[i];
+        found[i] = len && tb[to[i]] == '+' ? 2 : len ? 1 : 0;
+        val[i] = found[i] == 1 ? (uint32_t)(1000 * i) : 0;
+    }
+    return TM_OK;
+}
+
+long fake_count(int what) { return what == 0 ? n_alloc : what == 1 ? n_free : what == 2 ? n_match : n_first; }
+
+/* pool / set handles for ctypes */
+tmn_pool *fake_pool_new(void) {
+    tmn_pool *p = malloc(sizeof *p);
+    tmn_pool_init(p, (tm_index *)0x1);
+    return p;
+}
+void fake_pool_free(tmn_pool *p) { tmn_pool_destroy(p); free(p); }
+int fake_pool_size(tmn_pool *p) { return p->npool; }
+uint64_t fake_set_vals_cap(tmn_set *s) { return s->vals.cap; }
+uint64_t fake_set_reruns(tmn_set *s) { return s->reruns; }
+const uint32_t *fake_set_vals(tmn_set *s) { return tmn_vals(s); }

@@ -70,7 +70,9 @@ def _body(rank, world, q):
     vals_t = torch.from_numpy(vals.view(np.int32).copy())
     # a capacity far too small first: the overflow check must catch it and grow
     xch = shard.Exchange(n, "cpu", per_peer=8)
-    xch.swap(hit_t, vals_t)
+    o_offs, o_rv = xch.swap(hit_t, vals_t)
+    # an overflowing slice ships cut counts: the merge stays inside each peer's values
+    assert int(o_offs[:, -1].max()) <= 8 and o_rv.shape[1] == 8
     overflowed = not xch.check()
     offs, rv = xch.swap(hit_t, vals_t)
     fitted = xch.check()

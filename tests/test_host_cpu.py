@@ -119,3 +119,66 @@ def test_broker_badarg_fails_only_that_message():
     for f in futs[:10]:
         assert f.result(0)[0] == [(f.result(0)[0][0][0], "n1")]
     assert isinstance(futs[10].exception(0), BadArg)
+
+
+class _EpochIndex:
+    """Stand-in for _native.Index with the library's reader-epoch rule
+    (include/tmatch.h "Reader epochs"), no device: for Tab's bookkeeping."""
+
+    def __init__(self):
+        self.cur, self.readers, self.next = 1, {}, 1
+        self.applied = []
+
+    def apply(self, ops, blob, offs, vals, flags=None):
+        self.applied.append((ops.tolist(), vals.tolist()))
+        self.cur += 1
+        return self.cur
+
+    def read_begin(self):
+        t = self.next
+        self.next += 1
+        self.readers[t] = self.cur
+        return t
+
+    def read_end(self, t):
+        del self.readers[t]
+
+    def epoch(self):
+        return self.cur, min(self.readers.values(), default=self.cur)
+
+
+def test_freed_values_wait_for_older_readers():
+    """A u32 freed by a delete is not handed to a new key while a reader that
+    began before the delete runs; decoding drops keys deleted meanwhile."""
+    ix = _EpochIndex()
+    tab = Tab(index=ix)
+    ka, kb, kc = make_key(b"a/+", 1), make_key(b"b/+", 2), make_key(b"c/+", 3)
+    tab.insert_key(ka, None)
+    tab.insert_key(kb, None)
+    tab.flush()
+    kid_a = tab._kid[ka]
+    reader = tab.read_begin()              # a batch in flight that may return kid_a
+    tab.delete_key(ka)
+    tab.flush()
+    assert tab.decode(np.array([kid_a, tab._kid[kb]], np.uint32)) == [kb]   # deleted: dropped
+    tab.insert_key(kc, None)
+    assert tab._kid[kc] != kid_a           # quarantined while the reader runs
+    tab.read_end(reader)
+    tab.delete_key(kc)
+    tab.flush()
+    kd = make_key(b"d/+", 4)
+    tab.insert_key(kd, None)               # no reader left: both freed values are reusable
+    assert tab._kid[kd] in (kid_a, 2)
+    assert tab.decode(np.array([tab._kid[kd]], np.uint32)) == [kd]
+
+
+def test_unshipped_deletes_are_not_reused():
+    """A delete not yet shipped (no epoch yet) keeps its u32 out of reuse."""
+    tab = Tab(index=_EpochIndex())
+    ka = make_key(b"a/+", 1)
+    tab.insert_key(ka, None)
+    tab.flush()
+    kid = tab._kid[ka]
+    tab.delete_key(ka)
+    tab.insert_key(make_key(b"b/+", 2), None)   # same pending batch: the device still holds kid
+    assert tab._kid[make_key(b"b/+", 2)] != kid
