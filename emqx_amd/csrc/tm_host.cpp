@@ -1916,7 +1916,8 @@ void mf_snapshot(tm_index *ix) {
             auto add = [&](uint32_t roff, uint32_t cnt, bool hash) {
                 for (uint32_t i = 0; i < cnt; i++) {
                     const uint32_t v = ix->vals.h[roff + i];
-                    std::string f = hash ? (path.empty() ? std::string("#") : path + "/#") : path;
+                    // (the root has no words; a node whose path is one empty word has path "")
+                    std::string f = hash ? (x == ROOT ? std::string("#") : path + "/#") : path;
                     m.keys.insert(dead_key(reinterpret_cast<const uint8_t *>(f.data()), (uint32_t)f.size(), v,
                                            TM_KEY_WORDS));
                 }

@@ -713,7 +713,7 @@ def test_exchange_overflow_stays_in_buffer(torch_dev):
         got_hit = out_hit.cpu().numpy()
         assert np.array_equal(got_hit, exp_hit)
         got = out_vals.cpu().numpy()[: int(exp_hit[-1])].view(np.uint32)
-        exp = np.concatenate([vals[hit[i]:hit[i] + cut[i]] for i in range(len(ts))])
+        exp = np.concatenate([vals[int(hit[i]):int(hit[i]) + int(cut[i])] for i in range(len(ts))])
         assert np.array_equal(got, exp)
         assert not xch.check() and xch.per_peer > int(hit[-1])
         out_hit, out_vals = xch.run(h, v)
