@@ -35,12 +35,12 @@ Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3]
 from __future__ import annotations
 
 import argparse
+import ctypes
 import gc
 import json
 import math
 import os
 import sys
-import threading
 import time
 from pathlib import Path
 
@@ -92,7 +92,7 @@ def parse():
     p.add_argument("--no-parity", action="store_true")
     p.add_argument("--latency-batches", type=int, default=20)
     p.add_argument("--concurrency", type=int, default=8,
-                   help="host threads of the concurrent-caller latency leg (0 = skip)")
+                   help="native caller threads of the concurrent-caller leg (and twice as many; 0 = skip)")
     p.add_argument("--frontier-sample", type=int, default=20_000)
     return p.parse_args()
 
@@ -342,49 +342,65 @@ def main():
     iso_ms = iso_walk_ms / max(iso_nb, 1)
     iso_batch = iso_batch_ms / max(iso_nb, 1)
 
-    # p50/p99 batch latency: host topics in, hit lists back in host memory
-    # (every rank).  "pinned": the caller's buffers come from tm_host_alloc
-    # (what a NIF keeps per scheduler), so the kernels read the topics and
-    # write the hit lists in place; "pageable": ordinary caller buffers,
-    # staged through the library's pinned buffers (one copy in, one out).
+    # Host-side legs, driven by native threads (emqx_amd/csrc/hostbench.cpp:
+    # what the NIF's dirty schedulers do, without Python's GIL in the loop):
+    #  - p50/p99 of host-to-host batches of n topics (tm_host_alloc buffers:
+    #    the kernels read the topics and write the hit lists in place),
+    #  - concurrent callers: 8 and 16 threads of 4k-topic batches while one
+    #    thread applies subscribe/unsubscribe deltas,
+    #  - host-fed pipeline: 1M-topic batches from pinned host memory, H2D +
+    #    match + D2H overlapped on 3 streams (LookupRps's host-side unit,
+    #    emqx_broker_bench.erl:68-76), next to the PCIe bytes it moves.
     ts = tsets[0]
-    lat = {}
-    conc = None
+    lat_native, conc, hostfed = {}, None, None
     if not filter_sharded and a.latency_batches > 0:
-        for lb in sorted({min(4096, B), min(65536, B)}):
+        hb = host_bench_lib()
+        for lb in sorted({1, 64, 1024, min(4096, B), min(65536, B)}):
             sub = ts.slice(0, lb)
-            _, v0, _ = ix.match_batch(sub.blob, sub.offs)          # sizes the value buffer
-            nbytes = int(sub.offs[-1] - sub.offs[0])
-            pb = ix.host_array(nbytes + 16, np.uint8)
-            po = ix.host_array(lb + 1, np.uint64)
-            pb[:nbytes] = sub.blob[int(sub.offs[0]):int(sub.offs[-1])]
-            po[:] = sub.offs - sub.offs[0]
-            kinds = {"pinned": (pb, po, (ix.host_array(lb + 1, np.uint64), ix.host_array(len(v0) + 1024, np.uint32),
-                                         ix.host_array(lb, np.uint8))),
-                     "pageable": (sub.blob, sub.offs, (np.zeros(lb + 1, np.uint64),
-                                                       np.zeros(len(v0) + 1024, np.uint32), np.zeros(lb, np.uint8)))}
-            for kind, (tb, to, bufs) in kinds.items():
-                xs = []
-                for k in range(a.latency_batches + 2):
-                    t1 = time.perf_counter()
-                    ix.match_batch(tb, to, out=bufs)
-                    xs.append((time.perf_counter() - t1) * 1e3)
-                xs = np.array(xs[2:])
-                lat[f"{kind}/{lb}"] = {"p50_ms": float(np.percentile(xs, 50)), "p99_ms": float(np.percentile(xs, 99))}
-    if not filter_sharded:
-        if a.concurrency > 0 and hasattr(ix, "host_array"):
-            conc = concurrent_latency(ix, ts, a.concurrency, min(4096, B))
-    if world > 1 and lat:
-        # the slowest rank's percentiles (max over ranks)
-        keys = sorted(lat)
-        v = torch.tensor([lat[k][q] for k in keys for q in ("p50_ms", "p99_ms")], dtype=torch.float64, device=cdev)
+            hh, _, _ = ix.match_batch(sub.blob, sub.offs)
+            out = (ctypes.c_double * 3)()
+            rc = hb.tmb_single(ix._h, lb, _native._ptr(sub.blob), _native._ptr(sub.offs), int(hh[-1]) + 4096,
+                               a.latency_batches * 5, out)
+            assert rc == 0, rc
+            lat_native[str(lb)] = {"p50_ms": round(out[0], 4), "p99_ms": round(out[1], 4), "mean_ms": round(out[2], 4)}
+        if a.concurrency > 0:
+            conc = []
+            for nth in (a.concurrency, 2 * a.concurrency):
+                lb = min(4096, B)
+                sub = ts.slice(0, nth * lb)
+                hh, _, _ = ix.match_batch(sub.blob, sub.offs)
+                cap = int(np.diff(hh.astype(np.int64)).reshape(nth, lb).sum(axis=1).max()) + 65536
+                out = (ctypes.c_double * 6)()
+                rc = hb.tmb_callers(ix._h, nth, lb, _native._ptr(sub.blob), _native._ptr(sub.offs), cap, 1.0, 256, out)
+                assert rc == 0, rc
+                conc.append({"threads": nth, "topics_per_batch": lb, "batches": int(out[0]),
+                             "topics_per_s": round(out[1], 1), "p50_ms": round(out[2], 4), "p99_ms": round(out[3], 4),
+                             "deltas_per_s": round(out[4], 1),
+                             "callers": "native threads, tm_host_alloc buffers each (in place)"})
+        if B >= 65536:
+            allt = wl.concat(tsets)
+            out = (ctypes.c_double * 5)()
+            iters = 24
+            rc = hb.tmb_pipeline(ix._h, local, _native._ptr(allt.blob), _native._ptr(allt.offs), B, R, 3, iters, out)
+            assert rc == 0, rc
+            h2d, d2h = out[2], out[3]
+            hostfed = {"topics_per_s": round(out[0], 1), "ms_per_batch": round(out[1], 4), "batch": B,
+                       "streams": 3, "h2d_MB_per_batch": round(h2d / 1e6, 2), "d2h_MB_per_batch": round(d2h / 1e6, 2),
+                       "pcie_GBps": {"h2d": round(h2d / (out[1] * 1e-3) / 1e9, 1),
+                                     "d2h": round(d2h / (out[1] * 1e-3) / 1e9, 1)},
+                       "note": "topics in pinned host memory -> H2D -> match -> D2H of offsets and values into pinned "
+                               "host memory, 3 streams; value bytes per batch from a sizing pass"}
+    if world > 1 and lat_native:
+        # the slowest rank's percentiles (max over ranks); the caller and
+        # host-fed legs are rank 0's (each rank drives its own GPU alike)
+        keys = sorted(lat_native)
+        v = torch.tensor([lat_native[k][q] for k in keys for q in ("p50_ms", "p99_ms")], dtype=torch.float64,
+                         device=cdev)
         dist.all_reduce(v, op=dist.ReduceOp.MAX)
         v = v.tolist()
-        lat = {k: {"p50_ms": v[2 * i], "p99_ms": v[2 * i + 1]} for i, k in enumerate(keys)}
-    lat_pinned = {k.split("/")[1]: {q: round(x, 3) for q, x in d.items()} for k, d in lat.items()
-                  if k.startswith("pinned/")}
-    lat_pageable = {k.split("/")[1]: {q: round(x, 3) for q, x in d.items()} for k, d in lat.items()
-                    if k.startswith("pageable/")}
+        lat_native = {k: {"p50_ms": v[2 * i], "p99_ms": v[2 * i + 1], "mean_ms": lat_native[k]["mean_ms"]}
+                      for i, k in enumerate(keys)}
+    lat_pinned = lat_native
 
     if rank != 0:
         if world > 1:
@@ -539,8 +555,8 @@ def main():
         "batch_device_ms": round(batch_avg_ms, 4),
         "batch_device_isolated_ms": round(iso_batch, 4),
         "batch_latency_host_ms": lat_pinned,
-        "batch_latency_host_pageable_ms": lat_pageable,
         "concurrent_callers": conc,
+        "host_fed": hostfed,
         "parity_sample": None if mism is None else {"topics": ns, "mismatches": mism,
                                                     "against": "oracle over this rank's keys" + (
                                                         " (every filter that can match a topic this rank owns: "
@@ -571,62 +587,16 @@ def main():
         dist.destroy_process_group()
 
 
-def concurrent_latency(ix, ts, nthreads: int, lb: int, seconds: float = 1.0):
-    """Concurrent callers (SURVEY.md 8b Threading: every client process calls
-    matches/3 at once): `nthreads` host threads each submit lb-topic batches
-    through tm_match_batch with their own tm_host_alloc buffers while one more
-    thread applies subscribe/unsubscribe deltas; ctypes drops the GIL for the
-    call, so the batches overlap inside the library.  -> per-batch p50/p99 and
-    the aggregate rate."""
-    from emqx_amd import _native
-    subs = []
-    for k in range(nthreads):
-        sub = ts.slice(k * lb, (k + 1) * lb)
-        nbytes = int(sub.offs[-1])
-        pb = ix.host_array(nbytes + 16, np.uint8)
-        po = ix.host_array(lb + 1, np.uint64)
-        pb[:nbytes] = sub.blob[:nbytes]
-        po[:] = sub.offs
-        _, v0, _ = ix.match_batch(sub.blob, sub.offs)
-        bufs = (ix.host_array(lb + 1, np.uint64), ix.host_array(len(v0) + 4096, np.uint32), ix.host_array(lb, np.uint8))
-        subs.append((pb, po, bufs))
-    stop = threading.Event()
-    lat = [[] for _ in range(nthreads)]
-
-    def caller(k):
-        pb, po, bufs = subs[k]
-        while not stop.is_set():
-            t1 = time.perf_counter()
-            ix.match_batch(pb, po, out=bufs)
-            lat[k].append((time.perf_counter() - t1) * 1e3)
-
-    nd = [0]
-
-    def churn():
-        d = _native.pack_strings([b"bench/concurrent/%d/+" % i for i in range(256)])
-        vals = np.arange(256, dtype=np.uint32) + np.uint32(0xF0000000)
-        op = 1
-        while not stop.is_set():
-            ix.apply(np.full(256, op, np.uint8), d[0], d[1], vals)
-            nd[0] += 256
-            op ^= 1
-            time.sleep(0.001)
-
-    th = [threading.Thread(target=caller, args=(k,)) for k in range(nthreads)] + [threading.Thread(target=churn)]
-    t0 = time.perf_counter()
-    for x in th:
-        x.start()
-    time.sleep(seconds)
-    stop.set()
-    for x in th:
-        x.join()
-    el = time.perf_counter() - t0
-    xs = np.concatenate([np.array(v[2:]) for v in lat if len(v) > 2])
-    nbatches = sum(len(v) for v in lat)
-    return {"threads": nthreads, "topics_per_batch": lb, "batches": int(nbatches),
-            "p50_ms": round(float(np.percentile(xs, 50)), 3), "p99_ms": round(float(np.percentile(xs, 99)), 3),
-            "topics_per_s": round(nbatches * lb / el, 1), "deltas_per_s": round(nd[0] / el, 1),
-            "buffers": "tm_host_alloc per thread (in place)"}
+def host_bench_lib():
+    """libtmbench.so (emqx_amd/csrc/hostbench.cpp): native caller threads and
+    the host-fed pipeline over the same libtmatch this process loaded."""
+    from emqx_amd.build import LIB_BENCH
+    lib = ctypes.CDLL(str(LIB_BENCH))
+    vp, u64, dp = ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_double)
+    lib.tmb_single.argtypes = [vp, u64, vp, vp, u64, ctypes.c_int, dp]
+    lib.tmb_callers.argtypes = [vp, ctypes.c_int, u64, vp, vp, u64, ctypes.c_double, ctypes.c_int, dp]
+    lib.tmb_pipeline.argtypes = [vp, ctypes.c_int, vp, vp, u64, ctypes.c_int, ctypes.c_int, ctypes.c_int, dp]
+    return lib
 
 
 if __name__ == "__main__":

@@ -3,6 +3,8 @@
 - ``emqx_amd/libtmatch.so``  product: host index compiler + HIP kernels + C ABI
   (``include/tmatch.h``), compiled by hipcc for ``--offload-arch=gfx950``.
 - ``emqx_amd/libtmwork.so``  synthetic workload generator (bench / tests).
+- ``emqx_amd/libtmbench.so`` native host-side bench drivers (caller threads,
+  host-fed pipeline) over libtmatch (bench.py only).
 - ``oracle/liboracle.so``    CPU oracle (tests / smoke / bench cpu_baseline only).
 """
 from __future__ import annotations
@@ -17,6 +19,7 @@ CSRC = PKG / "csrc"
 
 LIB_TMATCH = PKG / "libtmatch.so"
 LIB_WORK = PKG / "libtmwork.so"
+LIB_BENCH = PKG / "libtmbench.so"
 LIB_ORACLE = ROOT / "oracle" / "liboracle.so"
 
 ARCH = os.environ.get("TM_OFFLOAD_ARCH", "gfx950")
@@ -87,6 +90,16 @@ def build_work(force: bool = False) -> Path:
     return LIB_WORK
 
 
+def build_bench(force: bool = False) -> Path:
+    src = CSRC / "hostbench.cpp"
+    if force or _stale(LIB_BENCH, [src, LIB_TMATCH, ROOT / "include" / "tmatch.h"]):
+        tmp = LIB_BENCH.with_suffix(".so.tmp")
+        _run(["hipcc", "-O2", "-std=c++17", "-fPIC", "-shared", "-pthread", "-o", str(tmp), str(src),
+              f"-L{PKG}", "-l:libtmatch.so", "-Wl,-rpath,$ORIGIN"])
+        os.replace(tmp, LIB_BENCH)
+    return LIB_BENCH
+
+
 def build_oracle(force: bool = False) -> Path:
     src = ROOT / "oracle" / "tm_oracle.c"
     if force or _stale(LIB_ORACLE, [src]):
@@ -97,6 +110,7 @@ def build_oracle(force: bool = False) -> Path:
 def build_all(force: bool = False) -> None:
     build_tmatch(force)
     build_work(force)
+    build_bench(force)
     build_oracle(force)
 
 

@@ -1,0 +1,253 @@
+// hostbench.cpp -- bench infrastructure (libtmbench.so), not part of the match
+// path: the host-side measurements of bench.py done by native threads, as the
+// NIF's dirty schedulers would drive libtmatch (c_src/emqx_tmatch_nif.c), so
+// Python's GIL is not what is measured.
+//
+//   tmb_single     one caller: p50 / p99 of host-to-host batches of n topics
+//                  (tm_host_alloc buffers: the batch runs in place)
+//   tmb_callers    N caller threads (their own tm_host_alloc buffers) plus one
+//                  thread applying subscribe/unsubscribe deltas, for a while:
+//                  aggregate topics/s and per-batch p50 / p99 -- the reference's
+//                  concurrent publishers (emqx_broker.erl:293-298)
+//   tmb_pipeline   host-fed throughput: batches of topics in pinned host memory,
+//                  H2D copy, match, D2H of offsets and values, overlapped on
+//                  several streams -- the rate a caller that hands over host
+//                  buffers sees, next to the PCIe bytes it moves
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "../../include/tmatch.h"
+
+namespace {
+
+double now_s() { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); }
+
+double pct(std::vector<double> &v, double q) {
+    if (v.empty()) return 0;
+    std::sort(v.begin(), v.end());
+    return v[std::min(v.size() - 1, (size_t)(q / 100.0 * (v.size() - 1) + 0.5))];
+}
+
+// one caller's pinned buffers for batches of `n` topics taken from a topic set
+struct Caller {
+    tm_index *h;
+    uint64_t n, cap;
+    uint8_t *blob = nullptr; uint64_t *offs = nullptr, *hit = nullptr; uint32_t *vals = nullptr; uint8_t *err = nullptr;
+    int init(tm_index *ix, uint64_t nt, const uint8_t *tb, const uint64_t *to, uint64_t first, uint64_t cap_) {
+        h = ix; n = nt; cap = cap_;
+        const uint64_t b0 = to[first], nb = to[first + nt] - b0;
+        int rc;
+        if ((rc = tm_host_alloc(h, nb + 16, (void **)&blob)) || (rc = tm_host_alloc(h, 8 * (nt + 1), (void **)&offs)) ||
+            (rc = tm_host_alloc(h, 8 * (nt + 1), (void **)&hit)) || (rc = tm_host_alloc(h, 4 * cap, (void **)&vals)) ||
+            (rc = tm_host_alloc(h, nt + 1, (void **)&err)))
+            return rc;
+        memcpy(blob, tb + b0, nb);
+        for (uint64_t i = 0; i <= nt; i++) offs[i] = to[first + i] - b0;
+        return TM_OK;
+    }
+    int run() { return tm_match_batch(h, n, blob, offs, hit, vals, cap, err); }
+    void fini() {
+        for (void *p : {(void *)blob, (void *)offs, (void *)hit, (void *)vals, (void *)err}) if (p) tm_host_free(h, p);
+    }
+};
+
+}  // namespace
+
+extern "C" {
+
+// out: [p50_ms, p99_ms, mean_ms]
+int tmb_single(tm_index *h, uint64_t n, const uint8_t *tb, const uint64_t *to, uint64_t cap, int iters, double *out) {
+    Caller c;
+    int rc = c.init(h, n, tb, to, 0, cap);
+    if (rc) return rc;
+    std::vector<double> lat;
+    for (int k = 0; k < iters + 3 && !rc; k++) {
+        const double t0 = now_s();
+        rc = c.run();
+        if (k >= 3) lat.push_back((now_s() - t0) * 1e3);
+    }
+    double sum = 0;
+    for (double x : lat) sum += x;
+    c.fini();
+    if (rc) return rc;
+    out[2] = sum / std::max<size_t>(lat.size(), 1);
+    out[0] = pct(lat, 50);
+    out[1] = pct(lat, 99);
+    return TM_OK;
+}
+
+// nthreads callers, each with batches of n topics (caller k takes topics
+// [k n, (k + 1) n) of the set, which must hold nthreads * n); one churn thread
+// applies `churn_ops` deltas per millisecond (0: none).
+// out: [batches, topics_per_s, p50_ms, p99_ms, deltas_per_s, seconds]
+int tmb_callers(tm_index *h, int nthreads, uint64_t n, const uint8_t *tb, const uint64_t *to, uint64_t cap,
+                double seconds, int churn_ops, double *out) {
+    std::vector<Caller> cs(nthreads);
+    for (int k = 0; k < nthreads; k++) {
+        int rc = cs[k].init(h, n, tb, to, (uint64_t)k * n, cap);
+        if (rc) return rc;
+        if ((rc = cs[k].run())) return rc;   // warm: lane, workspace
+    }
+    std::atomic<bool> stop{false};
+    std::atomic<int> err{0};
+    std::vector<std::vector<double>> lat(nthreads);
+    std::atomic<uint64_t> deltas{0};
+    std::vector<std::thread> th;
+    const double t0 = now_s();
+    for (int k = 0; k < nthreads; k++)
+        th.emplace_back([&, k] {
+            while (!stop.load(std::memory_order_relaxed)) {
+                const double a = now_s();
+                const int rc = cs[k].run();
+                if (rc) { err = rc; break; }
+                lat[k].push_back((now_s() - a) * 1e3);
+            }
+        });
+    if (churn_ops > 0)
+        th.emplace_back([&] {
+            std::vector<std::string> fs;
+            std::vector<uint8_t> blob;
+            std::vector<uint64_t> offs{0};
+            std::vector<uint32_t> vals;
+            for (int i = 0; i < churn_ops; i++) {
+                std::string f = "bench/concurrent/" + std::to_string(i) + "/+";
+                blob.insert(blob.end(), f.begin(), f.end());
+                offs.push_back(blob.size());
+                vals.push_back(0xF0000000u + i);
+            }
+            std::vector<uint8_t> ops(churn_ops, 1);
+            while (!stop.load(std::memory_order_relaxed)) {
+                if (tm_apply_deltas(h, churn_ops, ops.data(), blob.data(), offs.data(), vals.data(), nullptr)) {
+                    err = -1;
+                    break;
+                }
+                deltas += churn_ops;
+                for (auto &o : ops) o ^= 1;
+                std::this_thread::sleep_for(std::chrono::milliseconds(1));
+            }
+        });
+    std::this_thread::sleep_for(std::chrono::duration<double>(seconds));
+    stop = true;
+    for (auto &t : th) t.join();
+    const double el = now_s() - t0;
+    for (auto &c : cs) c.fini();
+    if (err) return err;
+    std::vector<double> all;
+    uint64_t nb = 0;
+    for (auto &v : lat) { nb += v.size(); all.insert(all.end(), v.begin() + std::min<size_t>(2, v.size()), v.end()); }
+    out[0] = (double)nb;
+    out[1] = nb * (double)n / el;
+    out[2] = pct(all, 50);
+    out[3] = pct(all, 99);
+    out[4] = deltas / el;
+    out[5] = el;
+    return TM_OK;
+}
+
+// Host-fed pipeline.  R batches of n topics (batch k = topics [k n, (k + 1) n)
+// of the set) are copied into pinned host memory (setup); a sizing pass
+// records each batch's hit total.  Timed: `iters` batches rotate over the R
+// host batches and over `nstreams` streams; per batch, on its stream: H2D of
+// offsets + bytes, tm_match_batch_dev, D2H of the n + 1 offsets and of the
+// values into pinned host buffers of that stream; before a stream's buffers
+// are reused the host waits for its previous batch.
+// out: [topics_per_s, ms_per_batch, h2d_bytes_per_batch, d2h_bytes_per_batch, seconds]
+int tmb_pipeline(tm_index *h, int device, const uint8_t *tb, const uint64_t *to, uint64_t n, int R, int nstreams,
+                 int iters, double *out) {
+    if (hipSetDevice(device) != hipSuccess) return TM_EDEVICE;
+    struct HostBatch { uint8_t *p; uint64_t bytes, total; };
+    std::vector<HostBatch> hb(R);
+    uint64_t maxb = 0;
+    for (int k = 0; k < R; k++) {
+        const uint64_t b0 = to[(uint64_t)k * n], nb = to[(uint64_t)(k + 1) * n] - b0;
+        const uint64_t boff = ((n + 1) * 8 + 15) & ~15ull;
+        hb[k].bytes = boff + nb;
+        if (hipHostMalloc(&hb[k].p, hb[k].bytes + 16, hipHostMallocDefault) != hipSuccess) return TM_ENOMEM;
+        uint64_t *o = reinterpret_cast<uint64_t *>(hb[k].p);
+        for (uint64_t i = 0; i <= n; i++) o[i] = to[(uint64_t)k * n + i] - b0;
+        memcpy(hb[k].p + boff, tb + b0, nb);
+        maxb = std::max(maxb, hb[k].bytes);
+    }
+    struct Lane { hipStream_t s; hipEvent_t done; uint8_t *d_in; uint64_t *d_hit; uint32_t *d_vals; uint8_t *d_err;
+                  uint64_t *h_hit; uint32_t *h_vals; bool busy; };
+    std::vector<Lane> ls(nstreams);
+    uint64_t cap = 0;
+    for (auto &l : ls) {
+        if (hipStreamCreateWithFlags(&l.s, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&l.done, hipEventDisableTiming) != hipSuccess ||
+            hipMalloc(&l.d_in, maxb + 16) != hipSuccess || hipMalloc(&l.d_hit, 8 * (n + 1)) != hipSuccess ||
+            hipMalloc(&l.d_err, n + 1) != hipSuccess || hipHostMalloc(&l.h_hit, 8 * (n + 1), hipHostMallocDefault) != hipSuccess)
+            return TM_EDEVICE;
+        l.d_vals = nullptr; l.h_vals = nullptr; l.busy = false;
+    }
+    // sizing pass: every batch's hit total
+    {
+        Lane &l = ls[0];
+        for (int k = 0; k < R; k++) {
+            const uint64_t boff = ((n + 1) * 8 + 15) & ~15ull;
+            hipMemcpyAsync(l.d_in, hb[k].p, hb[k].bytes, hipMemcpyHostToDevice, l.s);
+            int rc = tm_match_batch_dev(h, n, l.d_in + boff, reinterpret_cast<uint64_t *>(l.d_in), l.d_hit, nullptr, 0,
+                                        l.d_err, l.s);
+            if (rc) return rc;
+            hipMemcpyAsync(l.h_hit, l.d_hit, 8 * (n + 1), hipMemcpyDeviceToHost, l.s);
+            hipStreamSynchronize(l.s);
+            hb[k].total = l.h_hit[n];
+            cap = std::max(cap, hb[k].total);
+        }
+    }
+    for (auto &l : ls)
+        if (hipMalloc(&l.d_vals, 4 * (cap + 16)) != hipSuccess ||
+            hipHostMalloc(&l.h_vals, 4 * (cap + 16), hipHostMallocDefault) != hipSuccess)
+            return TM_ENOMEM;
+    double h2d = 0, d2h = 0;
+    auto issue = [&](int k, Lane &l) -> int {
+        const HostBatch &b = hb[k % R];
+        const uint64_t boff = ((n + 1) * 8 + 15) & ~15ull;
+        if (hipMemcpyAsync(l.d_in, b.p, b.bytes, hipMemcpyHostToDevice, l.s) != hipSuccess) return TM_EDEVICE;
+        int rc = tm_match_batch_dev(h, n, l.d_in + boff, reinterpret_cast<uint64_t *>(l.d_in), l.d_hit, l.d_vals, cap,
+                                    l.d_err, l.s);
+        if (rc) return rc;
+        if (hipMemcpyAsync(l.h_hit, l.d_hit, 8 * (n + 1), hipMemcpyDeviceToHost, l.s) != hipSuccess ||
+            hipMemcpyAsync(l.h_vals, l.d_vals, 4 * b.total, hipMemcpyDeviceToHost, l.s) != hipSuccess ||
+            hipEventRecord(l.done, l.s) != hipSuccess)
+            return TM_EDEVICE;
+        h2d += b.bytes;
+        d2h += 8.0 * (n + 1) + 4.0 * b.total;
+        l.busy = true;
+        return TM_OK;
+    };
+    for (int k = 0; k < nstreams; k++) issue(k, ls[k]);   // warm
+    for (auto &l : ls) { hipEventSynchronize(l.done); l.busy = false; }
+    h2d = d2h = 0;
+    const double t0 = now_s();
+    for (int k = 0; k < iters; k++) {
+        Lane &l = ls[k % nstreams];
+        if (l.busy && hipEventSynchronize(l.done) != hipSuccess) return TM_EDEVICE;   // its results consumed
+        int rc = issue(k, l);
+        if (rc) return rc;
+    }
+    for (auto &l : ls) if (l.busy) hipEventSynchronize(l.done);
+    const double el = now_s() - t0;
+    for (auto &l : ls) {
+        hipStreamSynchronize(l.s);
+        tm_stream_release(h, l.s);
+        hipFree(l.d_in); hipFree(l.d_hit); hipFree(l.d_vals); hipFree(l.d_err);
+        hipHostFree(l.h_hit); hipHostFree(l.h_vals);
+        hipEventDestroy(l.done); hipStreamDestroy(l.s);
+    }
+    for (auto &b : hb) hipHostFree(b.p);
+    out[0] = iters * (double)n / el;
+    out[1] = el / iters * 1e3;
+    out[2] = h2d / iters;
+    out[3] = d2h / iters;
+    out[4] = el;
+    return TM_OK;
+}
+
+}  // extern "C"

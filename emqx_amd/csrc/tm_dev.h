@@ -46,16 +46,20 @@ struct Workspace {
     uint2 *rng;           // [n * RCAP] (value offset, count)
     uint32_t *lists;      // [(L_COUNT + 1) * n] topic lists (the last one: long segments to sort)
     uint32_t *list_n;     // [L_COUNT] list lengths, [L_COUNT] reset ticket, [L_COUNT + 1] scan ticket,
-                          // [L_COUNT + 2] long-segment count, [L_COUNT + 3] its reset ticket (zero between batches)
+                          // [L_COUNT + 2] long-segment count, [L_COUNT + 3] its reset ticket,
+                          // [L_COUNT + 4] the one-launch path's block ticket (zero between batches)
     uint64_t *blk;        // [n / TILE + 2] tile hit totals -> exclusive tile prefixes (zero between batches)
     uint32_t *deep_wid;   // [DEEP_LANES * MAX_LEVELS]
     uint2 *deep_stk;      // [DEEP_LANES * (MAX_LEVELS + 1)]
     uint8_t *deep_plus;   // [DEEP_LANES * MAX_LEVELS] '+' levels of each deep lane's path
+    uint32_t *look_flag;  // [n / SM_TOPICS + 2] one-launch path: per block, (launch tag << 2) | LB_AGG / LB_INCL
+    uint64_t *look_val;   //   and the block's hit total (LB_AGG) or inclusive prefix (LB_INCL)
     uint64_t cap_n;
 };
 
 constexpr int TILE = 256;    // topics per walk block = per scan tile = per emit block
-constexpr int LIST_SLOTS = L_COUNT + 4;   // Workspace::list_n entries
+constexpr int LIST_SLOTS = L_COUNT + 5;   // Workspace::list_n entries
+constexpr int SM_TOPICS = 16;             // topics per block of the one-launch small-batch path
 
 
 // Pipeline entry points (tm_kernels.hip).  All asynchronous on `s`.
@@ -69,6 +73,14 @@ hipError_t launch_match_phase1(const DevIndex &ix, const Workspace &ws, uint64_t
 hipError_t launch_match_phase2(const DevIndex &ix, const Workspace &ws, uint64_t n, const uint8_t *bytes,
                                const uint64_t *offs, uint64_t *hit_offs, uint32_t *out, uint64_t cap,
                                hipStream_t s);
+// The whole batch (phase 1 + phase 2): one launch for a small batch when the
+// index allows it (small_path_ok), both phases otherwise.  `tag` must differ
+// between consecutive launches on one workspace (the one-launch path's
+// look-back scan tells its own blocks' words from older ones by it).
+bool small_path_ok(const DevIndex &ix, uint64_t n);
+hipError_t launch_match(const DevIndex &ix, const Workspace &ws, uint64_t n, const uint8_t *bytes,
+                        const uint64_t *offs, uint64_t *hit_offs, uint8_t *err, uint32_t *out, uint64_t cap,
+                        uint32_t tag, hipStream_t s, hipEvent_t ev_walk0 = nullptr, hipEvent_t ev_walk1 = nullptr);
 hipError_t launch_first(const DevIndex &ix, const Workspace &ws, uint64_t n, const uint8_t *bytes,
                         const uint64_t *offs, uint32_t *out_value, uint8_t *out_found, hipStream_t s);
 // filter-sharded merge of allgathered per-shard CSR hit lists (k_merge_shards)

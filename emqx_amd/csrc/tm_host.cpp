@@ -97,6 +97,7 @@ struct Lane {
     bool used = false;        // `done` has been recorded
     hipEvent_t done = nullptr;   // after the lane's last batch: later patches wait for it
     uint64_t tick = 0;        // last use (LRU of device-API lanes)
+    uint32_t tag = 0;         // launches on this workspace (the one-launch path's look-back tag)
     Workspace w{};
     // host-API staging: mapped pinned buffers (*_dev = their device
     // addresses) and the HBM copies used for batches above ZC_TOPICS
@@ -1074,6 +1075,13 @@ int collect(tm_index *ix, Mirror<T> &m, std::vector<PatchRun> &runs, std::vector
     return TM_OK;
 }
 
+// a fresh launch tag of the lane's workspace (never 0, 30 bits)
+uint32_t next_tag(Lane &ln) {
+    ln.tag = (ln.tag + 1) & 0x3FFFFFFFu;
+    if (!ln.tag) ln.tag = 1;
+    return ln.tag;
+}
+
 // the lane's batch is done with the index: later patches (on any stream) wait for it
 int batch_done(tm_index *ix, Lane &ln) {
     HIPCHK(ix, hipEventRecord(ln.done, ln.s));
@@ -1163,7 +1171,8 @@ DevIndex dev_view(tm_index *ix) {
 // ------------------------------------------------------------------ lanes
 
 void free_workspace(Workspace &w) {
-    void *wb[] = {w.cnt, w.nr, w.rng, w.lists, w.list_n, w.blk, w.deep_wid, w.deep_stk, w.deep_plus};
+    void *wb[] = {w.cnt, w.nr, w.rng, w.lists, w.list_n, w.blk, w.deep_wid, w.deep_stk, w.deep_plus, w.look_flag,
+                  w.look_val};
     for (void *p : wb) if (p) (void)hipFree(p);
     w = Workspace{};
 }
@@ -1270,7 +1279,10 @@ int ensure_ws(tm_index *ix, uint64_t n, Lane &ln) {
     if (ix->last_patch) HIPCHK(ix, hipStreamWaitEvent(ln.s, ix->last_patch, 0));
     if (n <= w.cap_n && w.cnt) return TM_OK;
     HIPCHK(ix, hipStreamSynchronize(ln.s));
-    if (w.cnt) { (void)hipFree(w.cnt); (void)hipFree(w.nr); (void)hipFree(w.rng); (void)hipFree(w.lists); (void)hipFree(w.blk); }
+    if (w.cnt) {
+        void *old[] = {w.cnt, w.nr, w.rng, w.lists, w.blk, w.look_flag, w.look_val};
+        for (void *p : old) (void)hipFree(p);
+    }
     uint64_t c = std::max<uint64_t>(n + n / 4, 1024);
     HIPCHK(ix, hipMalloc(&w.cnt, c * 4));
     HIPCHK(ix, hipMalloc(&w.nr, c * 4));
@@ -1278,6 +1290,9 @@ int ensure_ws(tm_index *ix, uint64_t n, Lane &ln) {
     HIPCHK(ix, hipMalloc(&w.lists, c * (L_COUNT + 1) * 4));
     HIPCHK(ix, hipMalloc(&w.blk, (c / TILE + 4) * 8));
     HIPCHK(ix, hipMemsetAsync(w.blk, 0, (c / TILE + 4) * 8, ln.s));   // zero between batches (k_emit)
+    HIPCHK(ix, hipMalloc(&w.look_flag, (c / SM_TOPICS + 4) * 4));
+    HIPCHK(ix, hipMalloc(&w.look_val, (c / SM_TOPICS + 4) * 8));
+    HIPCHK(ix, hipMemsetAsync(w.look_flag, 0, (c / SM_TOPICS + 4) * 4, ln.s));   // no launch tag is 0
     w.cap_n = c;
     return TM_OK;
 }
@@ -1471,8 +1486,8 @@ int tm_match_batch_dev_ex(tm_index *ix, uint64_t n, const uint8_t *bytes, const 
     const DevIndex d = dev_view(ix);
     tm_index::ProfEv ev;
     if ((rc = prof_begin(ix, ev, s))) return rc;
-    HIPCHK(ix, launch_match_phase1(d, ln->w, n, bytes, offs, hit_offs, err, s, ev.w0, ev.w1));
-    HIPCHK(ix, launch_match_phase2(d, ln->w, n, bytes, offs, hit_offs, out, out ? cap : 0, s));
+    HIPCHK(ix, launch_match(d, ln->w, n, bytes, offs, hit_offs, err, out, out ? cap : 0, next_tag(*ln), s, ev.w0,
+                            ev.w1));
     if (order != TM_ORDER_TRAVERSAL && out)
         HIPCHK(ix, launch_sort_segments(ln->w, n, hit_offs, out, cap, order == TM_ORDER_UNIQUE, ucnt, s));
     if ((rc = batch_done(ix, *ln))) return rc;
@@ -1667,9 +1682,8 @@ int tm_match_batch_ex(tm_index *ix, uint64_t n, const uint8_t *tb, const uint64_
                 if ((rc = grow_dev(ix, s, ln.d_vals, ln.d_vals_cap, cap))) return rc;
                 vdst = ln.d_vals;
             }
-            HIPCHK(ix, launch_match_phase1(d, ln.w, n, dbytes, reinterpret_cast<const uint64_t *>(dof), dhit, de, s));
-            HIPCHK(ix, launch_match_phase2(d, ln.w, n, dbytes, reinterpret_cast<const uint64_t *>(dof), dhit, vdst,
-                                           dv ? cap : 0, s));
+            HIPCHK(ix, launch_match(d, ln.w, n, dbytes, reinterpret_cast<const uint64_t *>(dof), dhit, de, vdst,
+                                    dv ? cap : 0, next_tag(ln), s));
             if (sorted && dv) {
                 HIPCHK(ix, launch_sort_segments(ln.w, n, dhit, vdst, cap, unique, reinterpret_cast<uint32_t *>(du), s));
                 HIPCHK(ix, launch_copy_values(dhit, n, vdst, reinterpret_cast<uint32_t *>(dv), cap, s));
@@ -1713,8 +1727,7 @@ int tm_match_batch_ex(tm_index *ix, uint64_t n, const uint8_t *tb, const uint64_
         if (sorted && (rc = grow_dev(ix, s, ln.d_vals, ln.d_vals_cap, ln.pin_vals_cap))) return rc;
         if (sorted) vdst = ln.d_vals;
         const DevIndex d = dev_view(ix);
-        HIPCHK(ix, launch_match_phase1(d, ln.w, n, dbytes, doffs, dhit, derr, s));
-        HIPCHK(ix, launch_match_phase2(d, ln.w, n, dbytes, doffs, dhit, vdst, ln.pin_vals_cap, s));
+        HIPCHK(ix, launch_match(d, ln.w, n, dbytes, doffs, dhit, derr, vdst, ln.pin_vals_cap, next_tag(ln), s));
         if (sorted) {
             HIPCHK(ix, launch_sort_segments(ln.w, n, dhit, vdst, ln.pin_vals_cap, unique, dunq, s));
             HIPCHK(ix, launch_copy_values(dhit, n, vdst, ln.pin_vals_dev, ln.pin_vals_cap, s));

@@ -815,6 +815,8 @@ __global__ __launch_bounds__(WALK_BLOCK, 8) void k_walk_fast(DevIndex ix, Worksp
 // group of WAVE_W lanes (16: four topics per wavefront); a topic deeper than
 // the group, whose frontier outgrows it, or with more hit ranges than lanes
 // goes to the lane-walk tail lists instead.
+constexpr uint64_t WAVE_TOPICS = 8192;   // batches of up to this many topics take the wave-per-topic walk (latency)
+constexpr int WAVE_W = 16;               // lanes per topic in the wave walk
 constexpr int WV_BLOCK = 256;   // 4 waves per block
 constexpr int WV_WAVES = WV_BLOCK / 64;
 
@@ -1008,6 +1010,277 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_wave(DevIndex ix, Workspace w
             if (!nh) o.first_val[t] = 0;
             o.first_found[t] = badarg ? 2 : (nh ? 1 : 0);
         }
+    }
+}
+
+// ------------------------------------------- small batches in one launch
+//
+// A batch of <= WAVE_TOPICS topics is latency: its walk, scan and emit as
+// separate kernels (k_walk_wave, the tail kernels, k_emit) cost ~4 launches
+// of mostly idle grids.  k_walk_small does all of it in one: each group of W
+// lanes walks its topic as k_walk_wave does; a topic the group cannot take
+// (deeper than the group, a frontier or hit list wider than it, a
+// '#'-not-last cut) is walked by the group's first lane with an LDS store of
+// MID_L levels (small_path_ok: the index never needs more); the block's 16
+// hit counts get their global offset from a single-pass decoupled look-back
+// scan over the blocks in the order they started (a ticket, so a block only
+// ever waits for blocks already running); then each group copies its values
+// straight into the CSR.  No range lists, no device-side lists, no other kernel.
+enum { LB_AGG = 1, LB_INCL = 2 };
+
+struct CountEmit {          // one-launch path: hit count only (the values come from a re-walk)
+    uint64_t cnt;
+    __device__ __forceinline__ bool operator()(uint32_t, uint32_t n) { cnt += n & RUN_CNT; return true; }
+};
+
+bool small_path_ok(const DevIndex &ix, uint64_t n) {
+    // the fallback store resolves need_levels() (+2 look-ahead levels) within MID_L
+    return n && n <= WAVE_TOPICS && ix.depth + 2 <= (uint32_t)MID_L && ix.xlen_max + 2 <= (uint32_t)MID_L;
+}
+
+template <int MODE>
+__global__ __launch_bounds__(WV_BLOCK) void k_walk_small(DevIndex ix, Workspace ws, uint64_t n, const uint8_t *blob,
+                                                         const uint64_t *offs, Outs o, uint64_t *hit_offs,
+                                                         uint32_t *out, uint64_t cap, uint32_t tag) {
+    constexpr int W = WAVE_W;
+    constexpr uint32_t G = 64 / W;                        // topics per wave
+    constexpr uint32_t MAXL = W < 31 ? W : 31;
+    static_assert(WV_WAVES * G == SM_TOPICS, "a block is SM_TOPICS topics");
+    __shared__ uint32_t s_slash[WV_WAVES][64];
+    __shared__ uint32_t s_node[WV_WAVES][64];
+    __shared__ uint64_t s_code[WV_WAVES][64];
+    __shared__ uint64_t s_hcode[WV_WAVES][64];
+    __shared__ uint32_t s_hoff[WV_WAVES][64], s_hcnt[WV_WAVES][64];
+    __shared__ uint32_t s_roff[WV_WAVES][64], s_rcnt[WV_WAVES][64];   // hits by rank
+    __shared__ uint64_t s_rpos[WV_WAVES][64];
+    __shared__ uint32_t s_mwid[SM_TOPICS][MID_L], s_mpend[SM_TOPICS][MID_L + 1];   // fallback lane-walk stores
+    __shared__ uint8_t s_mlen[SM_TOPICS][MID_L];
+    __shared__ uint64_t s_cnt[SM_TOPICS];
+    __shared__ uint64_t s_base;
+    __shared__ uint32_t s_vb;
+    if (threadIdx.x == 0) s_vb = atomicAdd(&ws.list_n[L_COUNT + 4], 1u);   // blocks scan in start order
+    __syncthreads();
+    const uint32_t vb = s_vb;
+    const Group<W> grp;
+    const uint32_t wv = threadIdx.x >> 6, gl = grp.gl, base = grp.g * W;
+    const uint32_t gi = wv * G + grp.g;                   // topic slot in the block
+    const uint64_t t = (uint64_t)vb * SM_TOPICS + gi;
+    const bool live = t < n;
+    uint32_t *sl_ = s_slash[wv] + base, *sn_ = s_node[wv] + base, *hoff = s_hoff[wv] + base, *hcnt = s_hcnt[wv] + base;
+    uint64_t *sc_ = s_code[wv] + base, *hcode = s_hcode[wv] + base;
+    const uint64_t beg = live ? offs[t] : 0, end = live ? offs[t + 1] : 0, len = end - beg;
+
+    // ---- the wave walk (k_walk_wave), falling back instead of listing
+    bool fb = false;   // the group's first lane walks this topic
+    uint32_t nsl = 0;
+    for (uint64_t p = 0; p < len; p += W) {
+        const bool sl = p + gl < len && blob[beg + p + gl] == '/';
+        const uint64_t m = grp.ballot(sl);
+        if (sl) {
+            const uint32_t k = nsl + grp.rank(m);
+            if (k < W) sl_[k] = (uint32_t)(p + gl);
+        }
+        nsl += (uint32_t)__popcll(m);
+    }
+    const uint32_t L = nsl + 1;
+    wave_sync();
+    fb = live && L > MAXL;
+    const bool mine = live && !fb && gl < L;
+    const uint32_t ws0 = !mine || gl == 0 ? 0 : sl_[gl - 1] + 1;
+    const uint32_t we0 = !mine ? 0 : gl == L - 1 ? (uint32_t)len : sl_[gl];
+    const uint32_t wl = we0 - ws0;
+    const uint8_t *wp = blob + beg + ws0;
+    WordAcc w; w.reset(beg + ws0);
+    if (mine) for (uint32_t i = 0; i < wl; i++) w.push(wp[i]);
+    const bool bad = mine && wl == 1 && (w.b0 == '+' || w.b0 == '#');
+    const bool badarg = grp.ballot(bad) != 0;
+    const bool dollar = grp.bcast(mine && wl >= 1 && (w.b0 & 0xFFu) == '$' ? 1u : 0u, 0) != 0;
+    uint32_t wid = mine && !badarg ? vocab_find(ix, w, blob) : NONE;
+    const bool allf = grp.ballot(mine && wid == NONE) == 0;
+    uint64_t xh = FNV_OFF;
+    for (uint32_t l = 0; l < L && !fb; l++) xh = seq_hash_step(xh, grp.bcast(wid, l));
+    xh = seq_hash_finish(xh, L);
+    const uint32_t xslot = (uint32_t)xh & ix.xmask;
+    const uint32_t xf = live && !fb && allf && !badarg ? ix.xfp[xslot] : 0;   // in flight during the walk
+
+    uint32_t nst = live && !fb && !badarg ? 1 : 0, nh = 0;
+    uint32_t node = ROOT;
+    uint64_t code = 0;
+    auto add_hits = [&](bool h, uint64_t c, uint32_t off, uint32_t cnt) {
+        const uint64_t m = grp.ballot(h);
+        if (h) {
+            const uint32_t k = nh + grp.rank(m);
+            if (k < W) { hcode[k] = c; hoff[k] = off; hcnt[k] = cnt; }
+        }
+        nh += (uint32_t)__popcll(m);
+    };
+    for (uint32_t l = 0; nst; l++) {
+        const bool act = gl < nst;
+        uint4 n0 = make_uint4(NONE, 0, 0, 0), n1 = make_uint4(0, 0, 0, 0), n2 = n1, n3 = n1;
+        if (act) {
+            const uint4 *np = reinterpret_cast<const uint4 *>(ix.nodes + node);
+            n0 = np[0]; n1 = np[1]; n2 = np[2]; n3 = np[3];
+        }
+        pin(n0); pin(n1); pin(n2); pin(n3);
+        const bool droot = dollar && l == 0;
+        const uint32_t sh = 62 - 2 * l;
+        if (l == L) {
+            if (grp.ballot(act && (n1.y & NLIT_HDESC))) { fb = true; break; }   // the cut: the lane walk makes it
+            add_hits(act && n1.x, code, n0.w, n1.x);                              // exact terminal: digit 0
+            add_hits(act && !droot && n0.z, code | (1ull << sh), n0.y, n0.z);     // '#' terminal: digit 1
+            break;
+        }
+        add_hits(act && !droot && n0.z, code, n0.y, n0.z);                       // '#' terminal: digit 0
+        const uint32_t wl_ = grp.bcast(wid, l);
+        const uint32_t wnext = l + 1 < L ? grp.bcast(wid, l + 1) : NONE;
+        const uint32_t wnext2 = l + 2 < L ? grp.bcast(wid, l + 2) : NONE;
+        uint32_t lit = NONE;
+        if (act && wl_ != NONE) {
+            if ((n1.y & NLIT_MASK) <= KINL) {
+                lit = n2.x == wl_ ? n3.x : n2.y == wl_ ? n3.y : n2.z == wl_ ? n3.z : n2.w == wl_ ? n3.w : NONE;
+            } else {
+                const uint32_t h = child_hash(wl_);
+                const uint32_t mb = child_maybe(ix, n1, n2, n3, wl_, h);
+                if (mb & 1u) {
+                    uint32_t slo, shi;
+                    lit = ctab_find(ix, n2.x, n2.y, wl_, h, slo, shi);
+                    if (lit != NONE && !child_alive(slo, shi, l + 1, L, wnext, wnext2)) lit = NONE;
+                }
+            }
+        }
+        uint32_t plus = act && !droot && !(n1.y & NLIT_HDESC) ? n0.x : NONE;   // seek past '+' (dfs)
+        if (plus != NONE && !child_alive(n1.z, n1.w, l + 1, L, wnext, wnext2)) plus = NONE;
+        const uint64_t mp = grp.ballot(plus != NONE), ml = grp.ballot(lit != NONE);
+        const uint32_t np_ = (uint32_t)__popcll(mp), nn = np_ + (uint32_t)__popcll(ml);
+        if (nn > W) { fb = true; break; }
+        wave_sync();   // every lane has read its state before the slots are reused
+        if (plus != NONE) { const uint32_t k = grp.rank(mp); sn_[k] = plus; sc_[k] = code | (1ull << sh); }
+        if (lit != NONE) { const uint32_t k = np_ + grp.rank(ml); sn_[k] = lit; sc_[k] = code | (2ull << sh); }
+        wave_sync();
+        nst = nn;
+        if (gl < nst) { node = sn_[gl]; code = sc_[gl]; }
+    }
+    // ---- match_topics/4: the binary key equal to the topic, after every list key
+    if (live && !fb && allf && !badarg) {
+        uint32_t slot = xslot, f = xf, xoff = 0, xcnt = 0;
+        const uint32_t fp = exact_fp(xh);
+        for (;;) {
+            if (f == 0) break;
+            if (f == fp) {
+                const uint32_t *e = reinterpret_cast<const uint32_t *>(ix.exact + slot);
+                const bool keyok = e[0] == (uint32_t)xh && e[1] == (uint32_t)(xh >> 32) && e[2] == L;
+                if (keyok) {
+                    const uint32_t ew = !mine ? wid : L <= XINL ? e[6 + gl] : ix.wseq[e[5] + gl];
+                    if (grp.ballot(mine && ew != wid) == 0) { xoff = e[3]; xcnt = e[4]; break; }
+                }
+            }
+            slot = (slot + 1) & ix.xmask;
+            f = ix.xfp[slot];
+        }
+        add_hits(gl == 0 && xcnt, ~0ull, xoff, xcnt);
+    }
+    fb |= live && nh > W;
+
+    // ---- rank the hits by path code (traversal order)
+    wave_sync();
+    const bool hv = live && !fb && gl < nh;
+    const uint64_t my = hv ? hcode[gl] : 0;
+    uint32_t rank = 0;
+    uint64_t total = 0;
+    if (live && !fb)
+        for (uint32_t j = 0; j < nh; j++) {
+            rank += hcode[j] < my;
+            total += hcnt[j] & RUN_CNT;
+        }
+
+    // ---- topics the group could not take: its first lane walks them (LDS store of MID_L levels)
+    LdsStore<MID_L> st{s_mwid[gi], s_mpend[gi], s_mlen[gi], 1, 0};
+    int frc = RC_OK;
+    if (fb && gl == 0) {
+        if (MODE == MODE_COUNT) {
+            CountEmit em{0};
+            frc = match_topic(ix, blob, beg, end, st, em);
+            total = frc == RC_OK ? em.cnt : 0;
+        } else {
+            FirstEmit em{ix.vals, 0, false};
+            frc = match_topic(ix, blob, beg, end, st, em);
+            o.first_val[t] = frc == RC_OK ? em.v : 0;
+            o.first_found[t] = frc == RC_BADARG ? 2 : frc == RC_DEEP ? 3 : (em.found ? 1 : 0);
+        }
+    }
+    if (MODE == MODE_FIRST) {
+        if (live && !fb) {
+            if (hv && rank == 0) o.first_val[t] = (hcnt[gl] & RUN_INLINE) ? hoff[gl] : ix.vals[hoff[gl]];
+            if (gl == 0) {
+                if (!nh) o.first_val[t] = 0;
+                o.first_found[t] = badarg ? 2 : (nh ? 1 : 0);
+            }
+        }
+        if (threadIdx.x == 0 && vb == gridDim.x - 1) ws.list_n[L_COUNT + 4] = 0;   // every ticket is taken
+        return;
+    }
+
+    // ---- the block's offset: exclusive scan of its 16 counts + decoupled look-back
+    if (gl == 0) s_cnt[gi] = live ? total : 0;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t sum = 0;
+        for (int i = 0; i < SM_TOPICS; i++) sum += s_cnt[i];
+        uint64_t pre = 0;
+        if (vb > 0) {
+            ws.look_val[vb] = sum;
+            __hip_atomic_store(&ws.look_flag[vb], (tag << 2) | LB_AGG, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            for (int64_t j = (int64_t)vb - 1; j >= 0; j--) {
+                uint32_t f;
+                do {
+                    f = __hip_atomic_load(&ws.look_flag[j], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+                } while ((f >> 2) != tag);   // block j started before this one: it publishes soon
+                pre += ws.look_val[j];
+                if ((f & 3u) == LB_INCL) break;
+            }
+        }
+        ws.look_val[vb] = pre + sum;
+        __hip_atomic_store(&ws.look_flag[vb], (tag << 2) | LB_INCL, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        s_base = pre;
+        if (vb == gridDim.x - 1) {
+            hit_offs[n] = pre + sum;
+            ws.list_n[L_COUNT + 4] = 0;   // every ticket is taken
+        }
+    }
+    __syncthreads();
+    if (!live) return;
+    uint64_t pos = s_base;
+    for (uint32_t i = 0; i < gi; i++) pos += s_cnt[i];
+    if (gl == 0) {
+        hit_offs[t] = pos;
+        o.err[t] = fb ? (frc == RC_BADARG ? 1 : frc == RC_DEEP ? 2 : 0) : badarg;
+    }
+
+    // ---- the values, straight into the CSR
+    if (fb) {
+        if (gl == 0 && frc == RC_OK) {
+            DirectEmit em{ix.vals, out, pos, cap};
+            match_topic(ix, blob, beg, end, st, em);
+        }
+        return;
+    }
+    uint32_t *roff = s_roff[wv] + base, *rcnt = s_rcnt[wv] + base;
+    uint64_t *rpos = s_rpos[wv] + base;
+    if (hv) {
+        uint64_t before = 0;   // values of the hits ranked before this one
+        for (uint32_t j = 0; j < nh; j++) if (hcode[j] < my) before += hcnt[j] & RUN_CNT;
+        roff[rank] = hoff[gl]; rcnt[rank] = hcnt[gl]; rpos[rank] = pos + before;
+    }
+    wave_sync();
+    for (uint32_t r = 0; r < nh; r++) {
+        const uint32_t ro = roff[r], rc = rcnt[r];
+        const uint64_t P = rpos[r];
+        if (rc & RUN_INLINE) {
+            if (gl == 0 && P < cap) out[P] = ro;
+            continue;
+        }
+        for (uint32_t k = gl; k < (rc & RUN_CNT); k += W)
+            if (P + k < cap) out[P + k] = ix.vals[ro + k];
     }
 }
 
@@ -1569,8 +1842,6 @@ __global__ __launch_bounds__(256) void k_copy_values(const uint64_t *hit, uint64
 
 static inline uint32_t blocks_for(uint64_t n, uint32_t per) { return (uint32_t)((n + per - 1) / per); }
 
-constexpr uint64_t WAVE_TOPICS = 8192;   // batches of up to this many topics take the wave-per-topic walk (latency)
-constexpr int WAVE_W = 16;               // lanes per topic in the wave walk
 constexpr uint32_t WV_TOPICS_PER_BLOCK = WV_WAVES * (64 / WAVE_W);
 
 hipError_t launch_match_phase1(const DevIndex &ix, const Workspace &ws, uint64_t n, const uint8_t *bytes,
@@ -1609,10 +1880,32 @@ hipError_t launch_match_phase2(const DevIndex &ix, const Workspace &ws, uint64_t
     return hipGetLastError();
 }
 
+hipError_t launch_match(const DevIndex &ix, const Workspace &ws, uint64_t n, const uint8_t *bytes,
+                        const uint64_t *offs, uint64_t *hit_offs, uint8_t *err, uint32_t *out, uint64_t cap,
+                        uint32_t tag, hipStream_t s, hipEvent_t ev_walk0, hipEvent_t ev_walk1) {
+    if (small_path_ok(ix, n)) {
+        hipError_t e;
+        Outs o{err, nullptr, nullptr};
+        if (ev_walk0 && (e = hipEventRecord(ev_walk0, s)) != hipSuccess) return e;
+        hipLaunchKernelGGL(k_walk_small<MODE_COUNT>, dim3(blocks_for(n, SM_TOPICS)), dim3(WV_BLOCK), 0, s, ix, ws, n,
+                           bytes, offs, o, hit_offs, out, cap, tag & 0x3FFFFFFFu);
+        if (ev_walk1 && (e = hipEventRecord(ev_walk1, s)) != hipSuccess) return e;
+        return hipGetLastError();
+    }
+    hipError_t e = launch_match_phase1(ix, ws, n, bytes, offs, hit_offs, err, s, ev_walk0, ev_walk1);
+    if (e != hipSuccess) return e;
+    return launch_match_phase2(ix, ws, n, bytes, offs, hit_offs, out, cap, s);
+}
+
 hipError_t launch_first(const DevIndex &ix, const Workspace &ws, uint64_t n, const uint8_t *bytes,
                         const uint64_t *offs, uint32_t *out_value, uint8_t *out_found, hipStream_t s) {
     if (!n) return hipSuccess;
     Outs o{nullptr, out_value, out_found};
+    if (small_path_ok(ix, n)) {
+        hipLaunchKernelGGL(k_walk_small<MODE_FIRST>, dim3(blocks_for(n, SM_TOPICS)), dim3(WV_BLOCK), 0, s, ix, ws, n,
+                           bytes, offs, o, nullptr, nullptr, (uint64_t)0, 0u);
+        return hipGetLastError();
+    }
     if (n <= WAVE_TOPICS)
         hipLaunchKernelGGL((k_walk_wave<MODE_FIRST, WAVE_W>), dim3(blocks_for(n, WV_TOPICS_PER_BLOCK)),
                            dim3(WV_BLOCK), 0, s, ix, ws, n, bytes, offs, o);
