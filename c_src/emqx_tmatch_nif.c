@@ -26,7 +26,7 @@
  *     into a newer key.
  *
  * Functions:
- *   new(Device)                           -> {ok, Ref} | {error, Code}
+ *   new(Device | [Device])                -> {ok, Ref} | {error, Code}   (a list: one replica per device)
  *   apply(Ref, [{Op, Filter, U32, Kind}]) -> {ok, Epoch} | {error, Code}
  *                                            Op 1 insert, 0 delete; Kind 0 binary, 1 words, 2 []
  *   match_batch(Ref, [Topic], Order)      -> [[U32] | badarg | system_limit] | {error, Code}
@@ -77,15 +77,24 @@ static ERL_NIF_TERM err_term(ErlNifEnv *env, int rc) {
     return enif_make_tuple2(env, A_ERROR, enif_make_int(env, rc));
 }
 
-/* new(Device) -> {ok, Ref} | {error, Code} */
+/* new(Device | [Device]) -> {ok, Ref} | {error, Code}
+   A list: one host image with a replica on each device (tm_create_replicas). */
 static ERL_NIF_TERM nif_new(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
-    int dev;
+    int dev = -1, devs[8];
+    unsigned nd = 0;
     (void)argc;
-    if (!enif_get_int(env, argv[0], &dev)) return enif_make_badarg(env);
+    if (enif_get_list_length(env, argv[0], &nd)) {
+        ERL_NIF_TERM l = argv[0], h;
+        if (nd == 0 || nd > 8) return enif_make_badarg(env);
+        for (unsigned i = 0; enif_get_list_cell(env, l, &h, &l); i++)
+            if (!enif_get_int(env, h, &devs[i])) return enif_make_badarg(env);
+    } else if (!enif_get_int(env, argv[0], &dev)) {
+        return enif_make_badarg(env);
+    }
     idx_res *r = enif_alloc_resource(IDX_RT, sizeof *r);
     memset(r, 0, sizeof *r);
     tm_options o = {dev, 0, 0};
-    int rc = tm_create(&o, &r->h);
+    int rc = nd ? tm_create_replicas(&o, devs, nd, &r->h) : tm_create(&o, &r->h);
     if (rc != TM_OK) { r->h = NULL; enif_release_resource(r); return err_term(env, rc); }
     tmn_pool_init(&r->pool, r->h);
     ERL_NIF_TERM t = enif_make_resource(env, r);

@@ -24,7 +24,8 @@ EXPORTS = ("tm_create", "tm_destroy", "tm_apply_deltas", "tm_sync", "tm_match_ba
            "tm_match_batch_dev", "tm_first_batch", "tm_stats", "tm_profile_enable", "tm_profile_read",
            "tm_last_error", "tm_abi_version", "tm_merge_shards", "tm_host_alloc", "tm_host_free",
            "tm_stream_release", "tm_match_batch_ex", "tm_match_batch_dev_ex", "tm_sort_segments",
-           "tm_matches_filter", "tm_apply_deltas_ex", "tm_read_begin", "tm_read_end", "tm_epoch")
+           "tm_matches_filter", "tm_apply_deltas_ex", "tm_read_begin", "tm_read_end", "tm_epoch",
+           "tm_create_replicas", "tm_replica_stats")
 
 
 class NativeUnavailable(RuntimeError):
@@ -87,6 +88,8 @@ def load_library(path: Path | None = None):
         "tm_read_begin": (i32, [vp, C.POINTER(u64)]),
         "tm_read_end": (i32, [vp, u64]),
         "tm_epoch": (i32, [vp, C.POINTER(u64), C.POINTER(u64)]),
+        "tm_create_replicas": (i32, [C.POINTER(tm_options), C.POINTER(C.c_int32), u32, C.POINTER(vp)]),
+        "tm_replica_stats": (i32, [vp, u32, C.POINTER(u64), C.POINTER(C.c_int32)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -132,13 +135,19 @@ def pack_strings(items) -> tuple[np.ndarray, np.ndarray]:
 class Index:
     """Owning handle of one device-resident topic index (tm_index*)."""
 
-    def __init__(self, device: int = -1, hint_keys: int = 0):
+    def __init__(self, device: int = -1, hint_keys: int = 0, devices=None):
+        """devices: a list of HIP devices -> one host image with a replica on
+        each (tm_create_replicas); otherwise one device."""
         if not _gpu_present():
             raise NativeUnavailable("no HIP device visible: the topic index runs on the GPU only")
         self._lib = load_library()
         opts = tm_options(device, 0, hint_keys)
         h = C.c_void_p()
-        rc = self._lib.tm_create(C.byref(opts), C.byref(h))
+        if devices is not None:
+            devs = (C.c_int32 * len(devices))(*devices)
+            rc = self._lib.tm_create_replicas(C.byref(opts), devs, len(devices), C.byref(h))
+        else:
+            rc = self._lib.tm_create(C.byref(opts), C.byref(h))
         if rc != TM_OK:
             raise TmError(rc, self._lib.tm_last_error(None).decode())
         self._h = h
@@ -304,6 +313,12 @@ class Index:
         w, b, n = C.c_double(), C.c_double(), C.c_uint64()
         self._check(self._lib.tm_profile_read(self._h, C.byref(w), C.byref(b), C.byref(n), int(reset)))
         return w.value, b.value, n.value
+
+    def replica_stats(self, r: int) -> tuple[int, int]:
+        """-> (host-API batches replica r served, its device)."""
+        b, d = C.c_uint64(), C.c_int32()
+        self._check(self._lib.tm_replica_stats(self._h, r, C.byref(b), C.byref(d)))
+        return b.value, d.value
 
     def stats(self) -> dict:
         s = tm_stats_t()

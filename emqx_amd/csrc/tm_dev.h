@@ -94,9 +94,14 @@ hipError_t launch_sort_segments(const Workspace &ws, uint64_t n, const uint64_t 
 hipError_t launch_copy_values(const uint64_t *hit_offs, uint64_t n, const uint32_t *src, uint32_t *dst, uint64_t cap,
                               hipStream_t s);
 // delta upload: run i copies runs[i].n u32 words from data + runs[i].src to
-// the device address runs[i].dst
+// word (dst & PATCH_OFF) of table (dst >> 48), whose device address on the
+// replica being patched is bases.b[table] (the same runs patch every replica)
+constexpr int N_TABLES = 9;   // vocab, wpool, nodes, ctab, vals, exact, xfp, wseq, wbits
+constexpr uint64_t PATCH_OFF = (1ull << 48) - 1;
 struct PatchRun { uint64_t dst; uint32_t src, n; };
-hipError_t launch_patch(const PatchRun *d_runs, const uint32_t *d_data, uint64_t n_runs, hipStream_t s);
+struct PatchBases { uint64_t b[N_TABLES]; };
+hipError_t launch_patch(const PatchRun *d_runs, const uint32_t *d_data, uint64_t n_runs, PatchBases bases,
+                        hipStream_t s);
 // matches_filter/3 over the term-ordered word-list keys (pass 1: hit == null, per-query counts; pass 2: values)
 hipError_t launch_matches_filter(uint64_t n, const uint32_t *qoff, const uint32_t *qr, const uint32_t *qbase,
                                  const uint32_t *pool, const uint64_t *koff, const uint32_t *kval, uint64_t K,

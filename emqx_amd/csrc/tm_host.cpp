@@ -53,12 +53,14 @@ struct Dirty {
     void clear() { all = false; r.clear(); }
 };
 
-// host vector + its HBM copy
+constexpr int MAX_REPLICAS = 8;   // device copies of one host image (tm_create_replicas)
+
+// host vector + its HBM copy on every replica
 template <class T>
 struct Mirror {
     std::vector<T> h;
-    T *d = nullptr;
-    uint64_t dcap = 0;   // elements allocated on the device
+    T *d[MAX_REPLICAS] = {};
+    uint64_t dcap = 0;   // elements allocated on each replica's device
     Dirty dirty;
     void touch(uint64_t i, uint64_t n = 1) {
         uint64_t lo = i * sizeof(T), hi = (i + n) * sizeof(T);
@@ -91,6 +93,7 @@ inline uint32_t nlit_of(const Node &n) { return n.nlit & NLIT_MASK; }
 // the GPU without holding the index lock.  Device-API callers
 // (tm_match_batch_dev) get one per stream they pass, in a bounded LRU pool.
 struct Lane {
+    int r = 0;                // the replica whose tables this lane's batches read
     hipStream_t s = nullptr;
     bool owned = false;       // stream created by the library (host-API lane)
     bool busy = false;        // checked out by a host-API caller
@@ -110,21 +113,34 @@ struct Lane {
 };
 
 // Patch staging: a small ring, so shipping a patch waits on the host only for
-// the patch PATCH_RING before it, not for the one just enqueued.
+// the patch PATCH_RING before it, not for the one just enqueued.  The pinned
+// [PatchRun x runs | u32 data] buffer of a slot is shared by every replica
+// (one host image: collected once, copied to each device).
 constexpr int PATCH_RING = 4;
 struct PatchSlot {
-    uint8_t *pin = nullptr; uint64_t pin_cap = 0;   // [PatchRun x runs | u32 data]
-    uint8_t *dev = nullptr; uint64_t dev_cap = 0;
-    hipEvent_t done = nullptr; bool pending = false;
+    uint8_t *pin = nullptr; uint64_t pin_cap = 0;
 };
 
-constexpr int MAX_HOST_LANES = 16;   // concurrent host-API batches in flight
+// One device copy of the tables.  Patches reach it on the stream of the batch
+// that ships them (its own replica) or on the replica's patch stream.
+struct Replica {
+    int device = 0;
+    hipStream_t ps = nullptr;                 // patch stream (patches shipped by another replica's batch)
+    hipEvent_t last_patch = nullptr;          // event of its latest patch (every batch waits for it)
+    uint8_t *pdev[PATCH_RING] = {}; uint64_t pdev_cap[PATCH_RING] = {};
+    hipEvent_t pdone[PATCH_RING] = {}; bool ppending[PATCH_RING] = {};
+    uint64_t batches = 0;                     // host-API batches served (tm_replica_stats)
+};
+
+constexpr int MAX_HOST_LANES = 16;   // concurrent host-API batches in flight, per replica
 constexpr int MAX_DEV_LANES = 16;    // device-API streams with a workspace kept
 
 struct tm_index {
     std::mutex mu;
     std::condition_variable cv;      // a host lane was released
-    int device = 0;
+    int nrep = 1;
+    Replica rep[MAX_REPLICAS];
+    uint64_t rr = 0;                 // round-robin among equally loaded replicas
 
     // vocab: live words, next fresh wid, per-wid reference count (trie edges +
     // exact-key levels) and slot, wids freed for reuse; a word nothing refers
@@ -175,7 +191,6 @@ struct tm_index {
     uint64_t uploads = 0, patch_bytes = 0;
 
     PatchSlot patch[PATCH_RING]; uint32_t patch_head = 0;
-    hipEvent_t last_patch = nullptr;   // event of the latest patch (every batch waits for it)
 
     std::vector<std::unique_ptr<Lane>> lanes;
     uint64_t tick = 0;
@@ -194,7 +209,7 @@ struct tm_index {
 
     // diagnostics (tm_profile_*)
     bool prof = false;
-    struct ProfEv { hipEvent_t b0, w0, w1, b1; };
+    struct ProfEv { hipEvent_t b0, w0, w1, b1; int device; };
     std::vector<ProfEv> prof_pending, prof_free;
     double prof_walk_ms = 0, prof_batch_ms = 0;
     uint64_t prof_batches = 0;
@@ -1021,33 +1036,36 @@ constexpr uint64_t DEV_GUARD = 16;   // device elements kept allocated past the 
 template <class T>
 int upload_full(tm_index *ix, Mirror<T> &m) {
     uint64_t need = std::max<uint64_t>(m.h.size(), 1);
-    // rare (first upload, growth, rehash): drain every stream that may still
-    // read the old copy before touching it
-    HIPCHK(ix, hipDeviceSynchronize());
-    if (need > m.dcap) {
-        if (m.d) HIPCHK(ix, hipFree(m.d));
-        m.d = nullptr;
-        uint64_t cap = need + need / 2 + DEV_GUARD;
-        HIPCHK(ix, hipMalloc(&m.d, cap * sizeof(T)));
-        m.dcap = cap;
+    const bool grow = need > m.dcap;
+    const uint64_t cap = grow ? need + need / 2 + DEV_GUARD : m.dcap;
+    for (int r = 0; r < ix->nrep; r++) {
+        // rare (first upload, growth, rehash): drain every stream that may
+        // still read the old copy before touching it
+        HIPCHK(ix, hipSetDevice(ix->rep[r].device));
+        HIPCHK(ix, hipDeviceSynchronize());
+        if (grow) {
+            if (m.d[r]) HIPCHK(ix, hipFree(m.d[r]));
+            m.d[r] = nullptr;
+            HIPCHK(ix, hipMalloc(&m.d[r], cap * sizeof(T)));
+        }
+        if (m.bytes()) HIPCHK(ix, hipMemcpy(m.d[r], m.h.data(), m.bytes(), hipMemcpyHostToDevice));
     }
-    if (m.bytes()) {
-        HIPCHK(ix, hipMemcpy(m.d, m.h.data(), m.bytes(), hipMemcpyHostToDevice));
-    }
+    m.dcap = cap;
     if (getenv("TM_DEBUG_UPLOADS"))   // diagnostics: which table was shipped whole, and why
-        fprintf(stderr, "tm upload_full: %zu-byte elements x %zu (%.1f MB), dcap %lu\n", sizeof(T), m.h.size(),
-                m.bytes() / 1e6, (unsigned long)m.dcap);
+        fprintf(stderr, "tm upload_full: %zu-byte elements x %zu (%.1f MB), dcap %lu, %d replicas\n", sizeof(T),
+                m.h.size(), m.bytes() / 1e6, (unsigned long)m.dcap, ix->nrep);
     m.dirty.clear();
     ix->uploads++;
     return TM_OK;
 }
 
 // One patch run: `n` (<= PATCH_RUN) consecutive 4-byte words copied from the
-// patch data at `src` to the device address `dst` (tm_dev.h PatchRun).
+// patch data at `src` to word `dst & PATCH_OFF` of table `dst >> 48` (tm_dev.h
+// PatchRun): the same runs serve every replica, each with its table bases.
 constexpr uint32_t PATCH_RUN = 64;
 
 template <class T>
-int collect(tm_index *ix, Mirror<T> &m, std::vector<PatchRun> &runs, std::vector<uint32_t> &data) {
+int collect(tm_index *ix, Mirror<T> &m, uint32_t table, std::vector<PatchRun> &runs, std::vector<uint32_t> &data) {
     // the device copy keeps >= DEV_GUARD elements allocated past the host
     // size: k_emit's 16-B loads may overhang the last value run by 3 words
     // (with h.size() == dcap such a load would leave the allocation)
@@ -1059,20 +1077,27 @@ int collect(tm_index *ix, Mirror<T> &m, std::vector<PatchRun> &runs, std::vector
     }
     if (m.dirty.all) return upload_full(ix, m);
     const uint8_t *src = reinterpret_cast<const uint8_t *>(m.h.data());
-    const uint64_t base = reinterpret_cast<uint64_t>(m.d);
     const uint64_t limit = (m.bytes() + 3) / 4;
     for (auto &r : m.dirty.r) {
         const uint64_t hi = std::min<uint64_t>(r.second, limit);
         for (uint64_t lo = r.first; lo < hi; lo += PATCH_RUN) {
             const uint32_t n = (uint32_t)std::min<uint64_t>(PATCH_RUN, hi - lo);
             const uint64_t at = data.size();
-            runs.push_back(PatchRun{base + 4 * lo, (uint32_t)at, n});
+            runs.push_back(PatchRun{(uint64_t)table << 48 | lo, (uint32_t)at, n});
             data.resize(at + n, 0);
             memcpy(data.data() + at, src + 4 * lo, std::min<uint64_t>(4ull * n, m.bytes() - 4 * lo));
         }
     }
     m.dirty.clear();
     return TM_OK;
+}
+
+PatchBases patch_bases(tm_index *ix, int r) {
+    PatchBases b;
+    const void *t[N_TABLES] = {ix->vocab.d[r], ix->wpool.d[r], ix->nodes.d[r], ix->ctab.d[r], ix->vals.d[r],
+                               ix->exact.d[r], ix->xfp.d[r], ix->wseq.d[r], ix->wbits.d[r]};
+    for (int i = 0; i < N_TABLES; i++) b.b[i] = reinterpret_cast<uint64_t>(t[i]);
+    return b;
 }
 
 // a fresh launch tag of the lane's workspace (never 0, 30 bits)
@@ -1089,73 +1114,91 @@ int batch_done(tm_index *ix, Lane &ln) {
     return TM_OK;
 }
 
-// Ship every dirty word to HBM on stream s (caller holds ix->mu).  Patches
-// rewrite the tables in place, so a patch first waits for every batch still
-// reading them (each lane's `done`) and for the patch before it; every later
-// batch waits for this one (`last_patch`, ensure_ws): a batch sees exactly the
-// deltas applied before it (C5), whichever stream either ran on.
-int sync_locked(tm_index *ix, hipStream_t s) {
-    HIPCHK(ix, hipSetDevice(ix->device));
+// Ship every dirty word to every replica (caller holds ix->mu): to replica
+// `r0` on stream s (the batch about to run there), to the others on their
+// patch streams.  Patches rewrite the tables in place, so on each replica a
+// patch first waits for every batch still reading them (each of its lanes'
+// `done`) and for the patch before it; every later batch there waits for this
+// one (`last_patch`, ensure_ws): a batch sees exactly the deltas applied
+// before it (C5), whichever stream either ran on.  The calling thread's
+// device is replica r0's afterwards.
+int sync_locked(tm_index *ix, int r0, hipStream_t s) {
     std::vector<PatchRun> runs;
     std::vector<uint32_t> data;
     int rc;
-    if ((rc = collect(ix, ix->vocab, runs, data))) return rc;
-    if ((rc = collect(ix, ix->wpool, runs, data))) return rc;
-    if ((rc = collect(ix, ix->nodes, runs, data))) return rc;
-    if ((rc = collect(ix, ix->ctab, runs, data))) return rc;
-    if ((rc = collect(ix, ix->vals, runs, data))) return rc;
-    if ((rc = collect(ix, ix->exact, runs, data))) return rc;
-    if ((rc = collect(ix, ix->xfp, runs, data))) return rc;
-    if ((rc = collect(ix, ix->wseq, runs, data))) return rc;
-    if ((rc = collect(ix, ix->wbits, runs, data))) return rc;
+    if ((rc = collect(ix, ix->vocab, 0, runs, data))) return rc;
+    if ((rc = collect(ix, ix->wpool, 1, runs, data))) return rc;
+    if ((rc = collect(ix, ix->nodes, 2, runs, data))) return rc;
+    if ((rc = collect(ix, ix->ctab, 3, runs, data))) return rc;
+    if ((rc = collect(ix, ix->vals, 4, runs, data))) return rc;
+    if ((rc = collect(ix, ix->exact, 5, runs, data))) return rc;
+    if ((rc = collect(ix, ix->xfp, 6, runs, data))) return rc;
+    if ((rc = collect(ix, ix->wseq, 7, runs, data))) return rc;
+    if ((rc = collect(ix, ix->wbits, 8, runs, data))) return rc;
     const uint64_t nr = runs.size(), nw = data.size();
-    if (!nr) return TM_OK;
-    // staging: [runs | data] in one pinned buffer, one H2D copy, one kernel
-    const uint64_t bytes = nr * sizeof(PatchRun) + nw * 4;
-    PatchSlot &p = ix->patch[ix->patch_head % PATCH_RING];
-    ix->patch_head++;
-    if (p.pending) { HIPCHK(ix, hipEventSynchronize(p.done)); p.pending = false; }
-    if (bytes > p.pin_cap) {
-        if (p.pin) HIPCHK(ix, hipHostFree(p.pin));
-        p.pin = nullptr;
-        // generous steps: a reallocation (hipHostFree / hipFree) synchronises
-        // the device, a multi-millisecond stall inside a churn stream (C5)
-        p.pin_cap = std::max<uint64_t>(bytes * 2, 1u << 20);
-        HIPCHK(ix, hipHostMalloc(&p.pin, p.pin_cap, hipHostMallocDefault));
+    if (nr) {
+        // staging: [runs | data] in one pinned buffer, one H2D copy + one kernel per replica
+        const uint64_t bytes = nr * sizeof(PatchRun) + nw * 4;
+        const uint32_t k = ix->patch_head % PATCH_RING;
+        PatchSlot &p = ix->patch[k];
+        ix->patch_head++;
+        for (int r = 0; r < ix->nrep; r++) {   // the slot's previous patch has left its pinned buffer
+            Replica &R = ix->rep[r];
+            if (R.ppending[k]) {
+                HIPCHK(ix, hipSetDevice(R.device));
+                HIPCHK(ix, hipEventSynchronize(R.pdone[k]));
+                R.ppending[k] = false;
+            }
+        }
+        if (bytes > p.pin_cap) {
+            if (p.pin) HIPCHK(ix, hipHostFree(p.pin));
+            p.pin = nullptr;
+            // generous steps: a reallocation (hipHostFree / hipFree) synchronises
+            // the device, a multi-millisecond stall inside a churn stream (C5)
+            p.pin_cap = std::max<uint64_t>(bytes * 2, 1u << 20);
+            HIPCHK(ix, hipHostMalloc(&p.pin, p.pin_cap, hipHostMallocPortable));
+        }
+        memcpy(p.pin, runs.data(), nr * sizeof(PatchRun));
+        memcpy(p.pin + nr * sizeof(PatchRun), data.data(), nw * 4);
+        for (int r = 0; r < ix->nrep; r++) {
+            Replica &R = ix->rep[r];
+            HIPCHK(ix, hipSetDevice(R.device));
+            const hipStream_t st = r == r0 ? s : R.ps;
+            if (bytes > R.pdev_cap[k]) {   // the slot's previous patch on this replica has completed
+                if (R.pdev[k]) HIPCHK(ix, hipFree(R.pdev[k]));
+                R.pdev[k] = nullptr;
+                R.pdev_cap[k] = std::max<uint64_t>(bytes * 2, 1u << 20);
+                HIPCHK(ix, hipMalloc(&R.pdev[k], R.pdev_cap[k]));
+            }
+            for (auto &l : ix->lanes)
+                if (l->r == r && l->used && l->s != st) HIPCHK(ix, hipStreamWaitEvent(st, l->done, 0));
+            if (R.last_patch) HIPCHK(ix, hipStreamWaitEvent(st, R.last_patch, 0));
+            HIPCHK(ix, hipMemcpyAsync(R.pdev[k], p.pin, bytes, hipMemcpyHostToDevice, st));
+            HIPCHK(ix, launch_patch(reinterpret_cast<const PatchRun *>(R.pdev[k]),
+                                    reinterpret_cast<const uint32_t *>(R.pdev[k] + nr * sizeof(PatchRun)), nr,
+                                    patch_bases(ix, r), st));
+            HIPCHK(ix, hipEventRecord(R.pdone[k], st));
+            R.ppending[k] = true;
+            R.last_patch = R.pdone[k];
+        }
+        ix->patch_bytes += nw * 4;
+        ix->uploads++;
     }
-    if (bytes > p.dev_cap) {   // the slot's previous patch has completed (p.done above)
-        if (p.dev) HIPCHK(ix, hipFree(p.dev));
-        p.dev = nullptr;
-        p.dev_cap = std::max<uint64_t>(bytes * 2, 1u << 20);
-        HIPCHK(ix, hipMalloc(&p.dev, p.dev_cap));
-    }
-    memcpy(p.pin, runs.data(), nr * sizeof(PatchRun));
-    memcpy(p.pin + nr * sizeof(PatchRun), data.data(), nw * 4);
-    for (auto &l : ix->lanes)
-        if (l->used && l->s != s) HIPCHK(ix, hipStreamWaitEvent(s, l->done, 0));
-    if (ix->last_patch) HIPCHK(ix, hipStreamWaitEvent(s, ix->last_patch, 0));
-    HIPCHK(ix, hipMemcpyAsync(p.dev, p.pin, bytes, hipMemcpyHostToDevice, s));
-    HIPCHK(ix, launch_patch(reinterpret_cast<const PatchRun *>(p.dev),
-                            reinterpret_cast<const uint32_t *>(p.dev + nr * sizeof(PatchRun)), nr, s));
-    HIPCHK(ix, hipEventRecord(p.done, s));
-    p.pending = true;
-    ix->last_patch = p.done;
-    ix->patch_bytes += nw * 4;
-    ix->uploads++;
+    HIPCHK(ix, hipSetDevice(ix->rep[r0].device));
     return TM_OK;
 }
 
-DevIndex dev_view(tm_index *ix) {
+DevIndex dev_view(tm_index *ix, int r) {
     DevIndex d;
-    d.vocab = ix->vocab.d; d.vmask = (uint32_t)ix->vocab.h.size() - 1;
-    d.wpool = ix->wpool.d;
-    d.nodes = ix->nodes.d;
-    d.ctab = ix->ctab.d;
-    d.vals = ix->vals.d;
-    d.exact = ix->exact.d; d.xmask = (uint32_t)ix->exact.h.size() - 1;
-    d.xfp = ix->xfp.d;
-    d.wseq = ix->wseq.d;
-    d.wbits = ix->wbits.d; d.wcap = ix->wide.empty() ? 0 : ix->wb_words * 32;
+    d.vocab = ix->vocab.d[r]; d.vmask = (uint32_t)ix->vocab.h.size() - 1;
+    d.wpool = ix->wpool.d[r];
+    d.nodes = ix->nodes.d[r];
+    d.ctab = ix->ctab.d[r];
+    d.vals = ix->vals.d[r];
+    d.exact = ix->exact.d[r]; d.xmask = (uint32_t)ix->exact.h.size() - 1;
+    d.xfp = ix->xfp.d[r];
+    d.wseq = ix->wseq.d[r];
+    d.wbits = ix->wbits.d[r]; d.wcap = ix->wide.empty() ? 0 : ix->wb_words * 32;
     // levels a walk must resolve: the deepest live node's depth (no node below
     // it has children), all of a topic's levels when a binary key has its length
     auto &dc = ix->depth_cnt, &xc = ix->xlen_cnt;
@@ -1187,8 +1230,10 @@ void free_lane(Lane &l) {
     if (l.owned && l.s) (void)hipStreamDestroy(l.s);
 }
 
-int make_lane(tm_index *ix, hipStream_t s, bool owned, Lane *&out) {
+// a lane of replica r (the calling thread's device is r's)
+int make_lane(tm_index *ix, int r, hipStream_t s, bool owned, Lane *&out) {
     auto l = std::make_unique<Lane>();
+    l->r = r;
     l->owned = owned;
     if (owned) HIPCHK(ix, hipStreamCreateWithFlags(&l->s, hipStreamNonBlocking));
     else l->s = s;
@@ -1198,17 +1243,25 @@ int make_lane(tm_index *ix, hipStream_t s, bool owned, Lane *&out) {
     return TM_OK;
 }
 
-// a host-API lane for this caller (waits while MAX_HOST_LANES are in use)
+// A host-API lane for this caller: on the replica with the fewest batches in
+// flight (round robin among equals), waiting while every replica has
+// MAX_HOST_LANES in use.  Leaves the calling thread on the lane's device.
 int host_lane(tm_index *ix, std::unique_lock<std::mutex> &g, Lane *&out) {
     for (;;) {
-        int owned = 0;
-        for (auto &l : ix->lanes) {
-            if (!l->owned) continue;
-            owned++;
-            if (!l->busy) { l->busy = true; out = l.get(); return TM_OK; }
+        int busy[MAX_REPLICAS] = {}, owned[MAX_REPLICAS] = {};
+        for (auto &l : ix->lanes)
+            if (l->owned) { owned[l->r]++; busy[l->r] += l->busy; }
+        int best = -1;
+        for (int k = 0; k < ix->nrep; k++) {
+            const int r = (int)((ix->rr + k) % ix->nrep);
+            if (busy[r] < MAX_HOST_LANES && (best < 0 || busy[r] < busy[best])) best = r;
         }
-        if (owned < MAX_HOST_LANES) {
-            int rc = make_lane(ix, nullptr, true, out);
+        if (best >= 0) {
+            ix->rr++;
+            HIPCHK(ix, hipSetDevice(ix->rep[best].device));
+            for (auto &l : ix->lanes)
+                if (l->owned && l->r == best && !l->busy) { l->busy = true; out = l.get(); return TM_OK; }
+            int rc = make_lane(ix, best, nullptr, true, out);
             if (rc) return rc;
             out->busy = true;
             return TM_OK;
@@ -1231,9 +1284,14 @@ struct LaneLease {
     }
 };
 
-// the device-API lane of stream s; the least recently used one is retired
-// (after its batches finish) when MAX_DEV_LANES streams hold a workspace
+// the device-API lane of stream s (on the replica of the calling thread's
+// current device: the first one there); the least recently used one is
+// retired (after its batches finish) when MAX_DEV_LANES streams hold a workspace
 int dev_lane(tm_index *ix, hipStream_t s, Lane *&out) {
+    int dev = 0, r = -1;
+    HIPCHK(ix, hipGetDevice(&dev));
+    for (int k = 0; k < ix->nrep && r < 0; k++) if (ix->rep[k].device == dev) r = k;
+    if (r < 0) return fail(ix, TM_EINVAL, "device API: the current HIP device holds no replica of this index");
     int n = 0;
     size_t lru = SIZE_MAX;
     for (size_t i = 0; i < ix->lanes.size(); i++) {
@@ -1245,11 +1303,13 @@ int dev_lane(tm_index *ix, hipStream_t s, Lane *&out) {
     }
     if (n >= MAX_DEV_LANES && lru != SIZE_MAX) {
         Lane &l = *ix->lanes[lru];
+        HIPCHK(ix, hipSetDevice(ix->rep[l.r].device));
         if (l.used) HIPCHK(ix, hipEventSynchronize(l.done));
         free_lane(l);
         ix->lanes.erase(ix->lanes.begin() + lru);
+        HIPCHK(ix, hipSetDevice(dev));
     }
-    int rc = make_lane(ix, s, false, out);
+    int rc = make_lane(ix, r, s, false, out);
     if (rc) return rc;
     out->tick = ++ix->tick;
     return TM_OK;
@@ -1276,7 +1336,7 @@ int ensure_ws(tm_index *ix, uint64_t n, Lane &ln) {
         HIPCHK(ix, hipMemsetAsync(w.list_n, 0, LIST_SLOTS * 4, ln.s));
     }
     // the batch must see every patch shipped so far, whichever stream it went on
-    if (ix->last_patch) HIPCHK(ix, hipStreamWaitEvent(ln.s, ix->last_patch, 0));
+    if (ix->rep[ln.r].last_patch) HIPCHK(ix, hipStreamWaitEvent(ln.s, ix->rep[ln.r].last_patch, 0));
     if (n <= w.cap_n && w.cnt) return TM_OK;
     HIPCHK(ix, hipStreamSynchronize(ln.s));
     if (w.cnt) {
@@ -1321,12 +1381,20 @@ hipStream_t pick_stream(tm_index *, void *s) { return reinterpret_cast<hipStream
 
 // events of one profiled batch (null set when profiling is off)
 int prof_begin(tm_index *ix, tm_index::ProfEv &ev, hipStream_t s) {
-    ev = {nullptr, nullptr, nullptr, nullptr};
+    ev = {nullptr, nullptr, nullptr, nullptr, 0};
     if (!ix->prof) return TM_OK;
-    if (!ix->prof_free.empty()) { ev = ix->prof_free.back(); ix->prof_free.pop_back(); }
-    else {
+    int dev = 0;
+    HIPCHK(ix, hipGetDevice(&dev));
+    for (size_t i = 0; i < ix->prof_free.size(); i++)   // events of this device
+        if (ix->prof_free[i].device == dev) {
+            ev = ix->prof_free[i];
+            ix->prof_free.erase(ix->prof_free.begin() + i);
+            break;
+        }
+    if (!ev.b0) {
         HIPCHK(ix, hipEventCreate(&ev.b0)); HIPCHK(ix, hipEventCreate(&ev.w0));
         HIPCHK(ix, hipEventCreate(&ev.w1)); HIPCHK(ix, hipEventCreate(&ev.b1));
+        ev.device = dev;
     }
     HIPCHK(ix, hipEventRecord(ev.b0, s));
     return TM_OK;
@@ -1342,7 +1410,10 @@ int prof_end(tm_index *ix, tm_index::ProfEv &ev, hipStream_t s) {
 // wait for every batch of every lane (caller holds ix->mu)
 int drain_lanes(tm_index *ix) {
     for (auto &l : ix->lanes)
-        if (l->used) HIPCHK(ix, hipEventSynchronize(l->done));
+        if (l->used) {
+            HIPCHK(ix, hipSetDevice(ix->rep[l->r].device));
+            HIPCHK(ix, hipEventSynchronize(l->done));
+        }
     return TM_OK;
 }
 
@@ -1356,26 +1427,50 @@ uint32_t tm_abi_version(void) { return (1u << 16) | 4u; }
 
 const char *tm_last_error(tm_index *) { return g_last_error.c_str(); }
 
-int tm_create(const tm_options *opts, tm_index **out) {
+int tm_create_replicas(const tm_options *opts, const int32_t *devices, uint32_t n, tm_index **out) {
     if (!out) return fail(nullptr, TM_EINVAL, "tm_create: out is NULL");
     *out = nullptr;
+    if (!devices || n == 0 || n > (uint32_t)MAX_REPLICAS)
+        return fail(nullptr, TM_EINVAL, "tm_create_replicas: 1 to 8 devices");
     tm_index *ix = new (std::nothrow) tm_index();
     if (!ix) return fail(nullptr, TM_ENOMEM, "tm_create: out of host memory");
-    int dev = opts ? opts->device : -1;
-    if (dev < 0) {
-        if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    ix->nrep = (int)n;
+    hipError_t e = hipSuccess;
+    for (uint32_t r = 0; r < n && e == hipSuccess; r++) {
+        Replica &R = ix->rep[r];
+        R.device = devices[r];
+        e = hipSetDevice(R.device);
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&R.ps, hipStreamNonBlocking);
+        for (int i = 0; i < PATCH_RING && e == hipSuccess; i++)
+            e = hipEventCreateWithFlags(&R.pdone[i], hipEventDisableTiming);
     }
-    ix->device = dev;
-    hipError_t e = hipSetDevice(dev);
-    for (int i = 0; i < PATCH_RING && e == hipSuccess; i++)
-        e = hipEventCreateWithFlags(&ix->patch[i].done, hipEventDisableTiming);
     if (e != hipSuccess) {
         std::string m = std::string("tm_create: ") + hipGetErrorString(e);
-        delete ix;
+        tm_destroy(ix);
         return fail(nullptr, TM_EDEVICE, m);
     }
+    (void)hipSetDevice(ix->rep[0].device);
     init_tables(ix, opts ? opts->hint_keys : 0);
     *out = ix;
+    return TM_OK;
+}
+
+int tm_create(const tm_options *opts, tm_index **out) {
+    int32_t dev = opts ? opts->device : -1;
+    if (dev < 0) {
+        int d = 0;
+        if (hipGetDevice(&d) != hipSuccess) d = 0;
+        dev = d;
+    }
+    return tm_create_replicas(opts, &dev, 1, out);
+}
+
+int tm_replica_stats(tm_index *ix, uint32_t r, uint64_t *batches, int32_t *device) {
+    if (!ix) return fail(nullptr, TM_EINVAL, "tm_replica_stats: null handle");
+    std::lock_guard<std::mutex> g(ix->mu);
+    if (r >= (uint32_t)ix->nrep) return fail(ix, TM_EINVAL, "tm_replica_stats: no such replica");
+    if (batches) *batches = ix->rep[r].batches;
+    if (device) *device = ix->rep[r].device;
     return TM_OK;
 }
 
@@ -1383,23 +1478,37 @@ namespace { void mf_free_keys(tm_index::MfState &m); }
 
 int tm_destroy(tm_index *ix) {
     if (!ix) return TM_EINVAL;
-    (void)hipSetDevice(ix->device);
-    (void)hipDeviceSynchronize();
-    void *bufs[] = {ix->vocab.d, ix->wpool.d, ix->nodes.d, ix->ctab.d, ix->vals.d, ix->exact.d, ix->xfp.d, ix->wseq.d,
-                    ix->wbits.d};
-    for (void *p : bufs) if (p) (void)hipFree(p);
-    for (auto &l : ix->lanes) free_lane(*l);
+    for (int r = 0; r < ix->nrep; r++) {
+        (void)hipSetDevice(ix->rep[r].device);
+        (void)hipDeviceSynchronize();
+    }
+    for (auto &l : ix->lanes) {
+        (void)hipSetDevice(ix->rep[l->r].device);
+        free_lane(*l);
+    }
+    for (int r = 0; r < ix->nrep; r++) {
+        Replica &R = ix->rep[r];
+        (void)hipSetDevice(R.device);
+        void *bufs[] = {ix->vocab.d[r], ix->wpool.d[r], ix->nodes.d[r], ix->ctab.d[r], ix->vals.d[r], ix->exact.d[r],
+                        ix->xfp.d[r], ix->wseq.d[r], ix->wbits.d[r]};
+        for (void *p : bufs) if (p) (void)hipFree(p);
+        for (int i = 0; i < PATCH_RING; i++) {
+            if (R.pdev[i]) (void)hipFree(R.pdev[i]);
+            if (R.pdone[i]) (void)hipEventDestroy(R.pdone[i]);
+        }
+        if (R.ps) (void)hipStreamDestroy(R.ps);
+    }
+    (void)hipSetDevice(ix->rep[0].device);
     mf_free_keys(ix->mf);
     for (void *p : {(void *)ix->mf.q, (void *)ix->mf.err, (void *)ix->mf.hit, (void *)ix->mf.out}) if (p) (void)hipFree(p);
     if (ix->mf.s) (void)hipStreamDestroy(ix->mf.s);
-    for (auto &p : ix->patch) {
-        if (p.dev) (void)hipFree(p.dev);
-        if (p.pin) (void)hipHostFree(p.pin);
-        if (p.done) (void)hipEventDestroy(p.done);
-    }
+    for (auto &p : ix->patch) if (p.pin) (void)hipHostFree(p.pin);
     for (auto &b : ix->pinned) (void)hipHostFree(b.host);
-    for (auto &ev : ix->prof_pending) { (void)hipEventDestroy(ev.b0); (void)hipEventDestroy(ev.w0); (void)hipEventDestroy(ev.w1); (void)hipEventDestroy(ev.b1); }
-    for (auto &ev : ix->prof_free) { (void)hipEventDestroy(ev.b0); (void)hipEventDestroy(ev.w0); (void)hipEventDestroy(ev.w1); (void)hipEventDestroy(ev.b1); }
+    for (auto *v : {&ix->prof_pending, &ix->prof_free})
+        for (auto &ev : *v) {
+            (void)hipSetDevice(ev.device);
+            for (hipEvent_t x : {ev.b0, ev.w0, ev.w1, ev.b1}) (void)hipEventDestroy(x);
+        }
     delete ix;
     return TM_OK;
 }
@@ -1467,7 +1576,13 @@ int tm_epoch(tm_index *ix, uint64_t *current, uint64_t *safe) {
 int tm_sync(tm_index *ix, void *stream) {
     if (!ix) return fail(nullptr, TM_EINVAL, "tm_sync: null handle");
     std::lock_guard<std::mutex> g(ix->mu);
-    return sync_locked(ix, pick_stream(ix, stream));
+    int dev = 0, r0 = 0;   // `stream` belongs to the current device: its replica (else replica 0, its patch stream)
+    HIPCHK(ix, hipGetDevice(&dev));
+    hipStream_t s = pick_stream(ix, stream);
+    bool found = false;
+    for (int r = 0; r < ix->nrep && !found; r++) if (ix->rep[r].device == dev) { r0 = r; found = true; }
+    if (!found) s = ix->rep[0].ps;
+    return sync_locked(ix, r0, s);
 }
 
 int tm_match_batch_dev_ex(tm_index *ix, uint64_t n, const uint8_t *bytes, const uint64_t *offs, uint64_t *hit_offs,
@@ -1479,11 +1594,11 @@ int tm_match_batch_dev_ex(tm_index *ix, uint64_t n, const uint8_t *bytes, const 
     std::lock_guard<std::mutex> g(ix->mu);
     hipStream_t s = pick_stream(ix, stream);
     int rc;
-    if ((rc = sync_locked(ix, s))) return rc;
     Lane *ln;
     if ((rc = dev_lane(ix, s, ln))) return rc;
+    if ((rc = sync_locked(ix, ln->r, s))) return rc;
     if ((rc = ensure_ws(ix, n, *ln))) return rc;
-    const DevIndex d = dev_view(ix);
+    const DevIndex d = dev_view(ix, ln->r);
     tm_index::ProfEv ev;
     if ((rc = prof_begin(ix, ev, s))) return rc;
     HIPCHK(ix, launch_match(d, ln->w, n, bytes, offs, hit_offs, err, out, out ? cap : 0, next_tag(*ln), s, ev.w0,
@@ -1519,9 +1634,11 @@ int tm_stream_release(tm_index *ix, void *stream) {
     if (!ix) return fail(nullptr, TM_EINVAL, "tm_stream_release: null handle");
     std::lock_guard<std::mutex> g(ix->mu);
     hipStream_t s = pick_stream(ix, stream);
+    int dev = 0;
+    HIPCHK(ix, hipGetDevice(&dev));
     for (size_t i = 0; i < ix->lanes.size(); i++) {
         Lane &l = *ix->lanes[i];
-        if (l.owned || l.s != s) continue;
+        if (l.owned || l.s != s || ix->rep[l.r].device != dev) continue;
         if (l.used) HIPCHK(ix, hipEventSynchronize(l.done));
         free_lane(l);
         ix->lanes.erase(ix->lanes.begin() + i);
@@ -1604,9 +1721,10 @@ int tm_host_alloc(tm_index *ix, uint64_t bytes, void **out) {
     if (!ix || !out) return fail(ix, TM_EINVAL, "tm_host_alloc: null argument");
     *out = nullptr;
     std::lock_guard<std::mutex> g(ix->mu);
-    HIPCHK(ix, hipSetDevice(ix->device));
+    HIPCHK(ix, hipSetDevice(ix->rep[0].device));
     void *h = nullptr, *d = nullptr;
-    if (hipHostMalloc(&h, bytes ? bytes : 1, hipHostMallocMapped) != hipSuccess || !h)
+    // portable: every replica's device reads it in place (one virtual address on ROCm)
+    if (hipHostMalloc(&h, bytes ? bytes : 1, hipHostMallocMapped | hipHostMallocPortable) != hipSuccess || !h)
         return fail(ix, TM_ENOMEM, "tm_host_alloc: hipHostMalloc failed");
     HIPCHK(ix, hipHostGetDevicePointer(&d, h, 0));
     ix->pinned.push_back({static_cast<uint8_t *>(h), static_cast<uint8_t *>(d), bytes});
@@ -1620,7 +1738,6 @@ int tm_host_free(tm_index *ix, void *p) {
     std::lock_guard<std::mutex> g(ix->mu);
     for (size_t i = 0; i < ix->pinned.size(); i++) {
         if (ix->pinned[i].host != p) continue;
-        HIPCHK(ix, hipSetDevice(ix->device));
         int rc = drain_lanes(ix);   // no batch may still read or write it
         if (rc) return rc;
         HIPCHK(ix, hipHostFree(p));
@@ -1650,14 +1767,14 @@ int tm_match_batch_ex(tm_index *ix, uint64_t n, const uint8_t *tb, const uint64_
     if (order > TM_ORDER_UNIQUE) return fail(ix, TM_EINVAL, "tm_match_batch: bad order");
     const bool sorted = order != TM_ORDER_TRAVERSAL, unique = order == TM_ORDER_UNIQUE;
     std::unique_lock<std::mutex> g(ix->mu);
-    HIPCHK(ix, hipSetDevice(ix->device));
     LaneLease lease{ix, g};
     int rc;
     if ((rc = host_lane(ix, g, lease.ln))) return rc;
     Lane &ln = *lease.ln;
     const hipStream_t s = ln.s;
-    if ((rc = sync_locked(ix, s))) return rc;
+    if ((rc = sync_locked(ix, ln.r, s))) return rc;
     if ((rc = ensure_ws(ix, n, ln))) return rc;
+    ix->rep[ln.r].batches++;
     if (timing) tt[nt++] = now_us();
     if (n && n <= ZC_TOPICS) {
         // every buffer from tm_host_alloc: the kernels read the topics and
@@ -1674,7 +1791,7 @@ int tm_match_batch_ex(tm_index *ix, uint64_t n, const uint8_t *tb, const uint64_
             if (!de) {   // flags nobody reads still need a home
                 if ((rc = stage_out(ix, ln, n, n, de))) return rc;
             }
-            const DevIndex d = dev_view(ix);
+            const DevIndex d = dev_view(ix, ln.r);
             const uint8_t *dbytes = db ? db : dof;   // no bytes: any valid address
             uint64_t *dhit = reinterpret_cast<uint64_t *>(dh);
             uint32_t *vdst = reinterpret_cast<uint32_t *>(dv);
@@ -1726,7 +1843,7 @@ int tm_match_batch_ex(tm_index *ix, uint64_t n, const uint8_t *tb, const uint64_
         uint32_t *vdst = ln.pin_vals_dev;
         if (sorted && (rc = grow_dev(ix, s, ln.d_vals, ln.d_vals_cap, ln.pin_vals_cap))) return rc;
         if (sorted) vdst = ln.d_vals;
-        const DevIndex d = dev_view(ix);
+        const DevIndex d = dev_view(ix, ln.r);
         HIPCHK(ix, launch_match(d, ln.w, n, dbytes, doffs, dhit, derr, vdst, ln.pin_vals_cap, next_tag(ln), s));
         if (sorted) {
             HIPCHK(ix, launch_sort_segments(ln.w, n, dhit, vdst, ln.pin_vals_cap, unique, dunq, s));
@@ -1745,7 +1862,8 @@ int tm_match_batch_ex(tm_index *ix, uint64_t n, const uint8_t *tb, const uint64_
         HIPCHK(ix, hipHostFree(ln.pin_vals));
         ln.pin_vals = nullptr;
         ln.pin_vals_cap = total + total / 4;
-        if ((rc = sync_locked(ix, s))) return rc;
+        HIPCHK(ix, hipSetDevice(ix->rep[ln.r].device));
+        if ((rc = sync_locked(ix, ln.r, s))) return rc;
         if ((rc = ensure_ws(ix, n, ln))) return rc;
     }
     memcpy(out_hit, ln.pin_out, (n + 1) * 8);
@@ -1773,21 +1891,21 @@ int tm_first_batch(tm_index *ix, uint64_t n, const uint8_t *tb, const uint64_t *
         return fail(ix, TM_EINVAL, "tm_first_batch: null buffer");
     if (n >= 0xFFFFFFFFull) return fail(ix, TM_EINVAL, "tm_first_batch: batch too large");
     std::unique_lock<std::mutex> g(ix->mu);
-    HIPCHK(ix, hipSetDevice(ix->device));
     LaneLease lease{ix, g};
     int rc;
     if ((rc = host_lane(ix, g, lease.ln))) return rc;
     Lane &ln = *lease.ln;
     const hipStream_t s = ln.s;
-    if ((rc = sync_locked(ix, s))) return rc;
+    if ((rc = sync_locked(ix, ln.r, s))) return rc;
     if ((rc = ensure_ws(ix, n, ln))) return rc;
+    ix->rep[ln.r].batches++;
     if (n && n <= ZC_TOPICS) {   // tm_host_alloc buffers: in place, as tm_match_batch
         const uint64_t nbytes = to[n];
         uint8_t *db = nbytes ? pinned_dev(ix, tb, nbytes) : nullptr;
         uint8_t *dof = pinned_dev(ix, to, (n + 1) * 8);
         uint8_t *dv = pinned_dev(ix, out_value, n * 4), *df = pinned_dev(ix, out_found, n);
         if ((db || !nbytes) && ((uintptr_t)tb & 15) == 0 && dof && dv && df) {
-            HIPCHK(ix, launch_first(dev_view(ix), ln.w, n, db ? db : dof, reinterpret_cast<const uint64_t *>(dof),
+            HIPCHK(ix, launch_first(dev_view(ix, ln.r), ln.w, n, db ? db : dof, reinterpret_cast<const uint64_t *>(dof),
                                     reinterpret_cast<uint32_t *>(dv), df, s));
             if ((rc = batch_done(ix, ln))) return rc;
             g.unlock();
@@ -1801,7 +1919,7 @@ int tm_first_batch(tm_index *ix, uint64_t n, const uint8_t *tb, const uint64_t *
     const uint64_t rbytes = n * 5;   // first value u32 per topic, then the found flags
     uint8_t *dres;
     if ((rc = stage_out(ix, ln, n, rbytes, dres))) return rc;
-    HIPCHK(ix, launch_first(dev_view(ix), ln.w, n, dbytes, doffs, reinterpret_cast<uint32_t *>(dres), dres + n * 4, s));
+    HIPCHK(ix, launch_first(dev_view(ix, ln.r), ln.w, n, dbytes, doffs, reinterpret_cast<uint32_t *>(dres), dres + n * 4, s));
     if ((rc = fetch_out(ix, ln, n, rbytes))) return rc;
     if ((rc = batch_done(ix, ln))) return rc;
     g.unlock();
@@ -2060,7 +2178,7 @@ int tm_matches_filter(tm_index *ix, uint64_t n, const uint8_t *fb, const uint64_
     if (n >= 0xFFFFFFFFull) return fail(ix, TM_EINVAL, "tm_matches_filter: batch too large");
     auto &m = ix->mf;
     std::lock_guard<std::mutex> g(m.mu);   // control plane: one call at a time; the index lock stays free
-    HIPCHK(ix, hipSetDevice(ix->device));
+    HIPCHK(ix, hipSetDevice(ix->rep[0].device));   // matches_filter's arrays live on replica 0
     if (!m.s) HIPCHK(ix, hipStreamCreateWithFlags(&m.s, hipStreamNonBlocking));
     int rc;
     if ((rc = mf_refresh(ix))) return rc;
@@ -2115,7 +2233,7 @@ int tm_stats(tm_index *ix, tm_stats_t *o) {
     o->n_nodes = ix->live_nodes;
     o->n_edges = ix->nlinks;
     o->n_words = ix->vcount;
-    o->device_bytes = ix->vocab.dcap * sizeof(VocabEntry) + ix->wpool.dcap + ix->nodes.dcap * sizeof(Node) +
+    o->device_bytes = ix->vocab.dcap * sizeof(VocabEntry)   /* per replica */ + ix->wpool.dcap + ix->nodes.dcap * sizeof(Node) +
                       ix->ctab.dcap * sizeof(CSlot) + ix->vals.dcap * 4 + ix->exact.dcap * sizeof(ExactEntry) + ix->xfp.dcap * 2 +
                       ix->wseq.dcap * 4 + ix->wbits.dcap * 4;
     o->uploads = ix->uploads;

@@ -1598,12 +1598,12 @@ __global__ __launch_bounds__(EMIT_BLOCK) void k_emit(DevIndex ix, Workspace ws, 
     }
 }
 
-__global__ void k_patch(const PatchRun *runs, const uint32_t *data, uint64_t n) {
+__global__ void k_patch(const PatchRun *runs, const uint32_t *data, uint64_t n, PatchBases bases) {
     const uint64_t i = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4;
     const uint32_t g = threadIdx.x & 15;
     if (i >= n) return;
     const PatchRun r = runs[i];
-    uint32_t *dst = reinterpret_cast<uint32_t *>(r.dst);
+    uint32_t *dst = reinterpret_cast<uint32_t *>(bases.b[r.dst >> 48]) + (r.dst & PATCH_OFF);
     for (uint32_t k = g; k < r.n; k += 16) dst[k] = data[r.src + k];
 }
 
@@ -2046,9 +2046,9 @@ hipError_t launch_matches_filter(uint64_t n, const uint32_t *qoff, const uint32_
     return hipGetLastError();
 }
 
-hipError_t launch_patch(const PatchRun *d_runs, const uint32_t *d_data, uint64_t n, hipStream_t s) {
+hipError_t launch_patch(const PatchRun *d_runs, const uint32_t *d_data, uint64_t n, PatchBases bases, hipStream_t s) {
     if (!n) return hipSuccess;
-    hipLaunchKernelGGL(k_patch, dim3(blocks_for(n * 16, 256)), dim3(256), 0, s, d_runs, d_data, n);
+    hipLaunchKernelGGL(k_patch, dim3(blocks_for(n * 16, 256)), dim3(256), 0, s, d_runs, d_data, n, bases);
     return hipGetLastError();
 }
 

@@ -5,8 +5,9 @@
  * pointers, sizes, status codes; no exceptions cross this boundary.  What each
  * entry point replaces in the reference (paths relative to the reference root):
  *
- *   tm_create / tm_destroy
+ *   tm_create / tm_create_replicas / tm_destroy
  *       emqx_topic_index:new/0,1          apps/emqx/src/emqx_topic_index.erl:40-48
+ *       (replicas: the node-wide replicated route table, emqx_router.erl:133-162)
  *       (the ETS ordered_set stays the source of truth on the Erlang side; this
  *        handle is its HBM mirror -- SURVEY.md 8b "Ownership")
  *   tm_apply_deltas
@@ -95,6 +96,22 @@ typedef struct {
 /* Create an empty index on a device.  opts may be NULL. */
 int tm_create(const tm_options *opts, tm_index **out);
 int tm_destroy(tm_index *h);
+
+/* One host image, n device replicas (1 <= n <= 8; a device may repeat):
+ * the topic-sharded mode of SURVEY.md 8e in one process, as one EMQX node
+ * (one BEAM VM) drives all its GPUs.  The reference keeps one replicated route
+ * table per node (emqx_router.erl:133-162); here the host key set, its
+ * compiler and tm_apply_deltas run once, and every patch's staged runs are
+ * copied to every replica (one pinned buffer, one H2D copy + one patch kernel
+ * per device).  Host-API batches go to the replica with the fewest batches in
+ * flight (round robin among equals); device-API calls use the replica of the
+ * calling thread's current HIP device (the first one there).  opts->device is
+ * ignored; matches_filter runs on replica 0.  tm_stats().device_bytes is per
+ * replica. */
+int tm_create_replicas(const tm_options *opts, const int32_t *devices, uint32_t n, tm_index **out);
+
+/* Host-API batches replica r has served so far, and its device. */
+int tm_replica_stats(tm_index *h, uint32_t r, uint64_t *batches, int32_t *device);
 
 /* Apply n deltas in order (a later op on the same key wins).  Host buffers:
  * filter i is filter_bytes[filter_offsets[i] .. filter_offsets[i+1]).

@@ -20,7 +20,8 @@ init() ->
         end,
     erlang:load_nif(filename:join(Priv, "emqx_tmatch_nif"), 0).
 
--spec new(integer()) -> {ok, ref()} | {error, integer()}.
+%% A list of devices: one host image with a replica on each (tm_create_replicas).
+-spec new(integer() | [integer()]) -> {ok, ref()} | {error, integer()}.
 new(_Device) -> erlang:nif_error(nif_not_loaded).
 
 %% {ok, Epoch}: the delta epoch the batch made current (include/tmatch.h "Reader epochs").

@@ -31,7 +31,7 @@
 %% emqx_amd/topic_index.py implements the same rules and is what the tests run.
 -module(emqx_topic_index_gpu).
 
--export([new/0, new/1, attach/2]).
+-export([new/0, new/1, attach/2, attach/3]).
 -export([insert/4, delete/3, apply_batch/2]).
 -export([match/2, matches/3, matches_batch/3, matches_filter/3]).
 -export([make_key/2, get_id/1, get_topic/1, get_record/2]).
@@ -55,17 +55,25 @@ new() ->
     new([public, {read_concurrency, true}]).
 
 %% new/1 (emqx_topic_index.erl:44-48): the ETS table with the caller's options
-%% plus its device mirror on the default device.
+%% plus its device mirror -- on the default device, or with {devices, [D]} one
+%% host image with a replica on each device (tm_create_replicas).
 -spec new(list()) -> gtab().
 new(Options) ->
-    mirror(ets:new(emqx_topic_index, [ordered_set | Options])).
+    Devices = proplists:get_value(devices, Options, -1),
+    mirror(ets:new(emqx_topic_index, [ordered_set | proplists:delete(devices, Options)]), Devices).
 
 %% Put a device mirror next to an existing index table (e.g. the router's
 %% ?ROUTE_TAB_FILTERS, emqx_router.erl:148-160) and load its keys in batches:
 %% boot from ETS.  Records are taken to be the last element of each row.
 -spec attach(ets:table(), pos_integer()) -> gtab().
 attach(Tab, BatchSize) ->
-    G = mirror(Tab),
+    attach(Tab, BatchSize, -1).
+
+%% Devices: -1 (the default device), a device, or a list of devices (one
+%% replica each, one host image -- SURVEY.md 8e topic-sharded mode in one node).
+-spec attach(ets:table(), pos_integer(), integer() | [integer()]) -> gtab().
+attach(Tab, BatchSize, Devices) ->
+    G = mirror(Tab, Devices),
     ets:safe_fixtable(Tab, true),
     try
         boot(G, ets:first(Tab), BatchSize, ?NOACC)
@@ -74,8 +82,8 @@ attach(Tab, BatchSize) ->
     end,
     G.
 
-mirror(Tab) ->
-    {ok, Ref} = emqx_tmatch_nif:new(-1),
+mirror(Tab, Devices) ->
+    {ok, Ref} = emqx_tmatch_nif:new(Devices),
     Kids = ets:new(emqx_topic_index_kids, [set, public, {read_concurrency, true}]),
     true = ets:insert(Kids, {next, 0}),
     Quar = ets:new(emqx_topic_index_quar, [ordered_set, public]),

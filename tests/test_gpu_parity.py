@@ -1700,3 +1700,54 @@ def test_hash_not_last_keys_leave_no_trie_behind(torch_dev):
     ix.apply(np.zeros(3, np.uint8), keys.blob, keys.offs, keys.vals)
     st2 = ix.stats()
     assert st2["n_dead_keys"] == 0 and st2["n_nodes"] == base["n_nodes"] and st2["n_words"] == base["n_words"]
+
+
+# ---------------------------------- one host image, N replicas
+
+def test_replicas_share_one_host_image(torch_dev):
+    """tm_create_replicas with two replicas on device 0: one host key set and
+    one tm_apply_deltas per delta batch feed both device copies; host batches
+    alternate between them and each equals the oracle after every step of a C5
+    delta replay; the 2-replica index costs the host about what 1 does."""
+    import gc
+    import psutil
+    nf = 20_000
+    fs = wl.filters(5, nf)
+    ix = _native.Index(devices=[0, 0])
+    ix.apply(np.ones(len(fs), np.uint8), fs.blob, fs.offs, fs.vals)
+    o = oracle_of(fs)
+    ts = wl.topics(5, nf, 6_000)
+    st0 = ix.stats()
+    for k in range(4):
+        d = wl.deltas(nf, k * 2_000, 2_000)
+        ix.apply(d.flags, d.blob, d.offs, d.vals)
+        o.apply(d.flags, d.blob, d.offs, d.vals)
+        o.prepare()
+        before = [ix.replica_stats(r)[0] for r in (0, 1)]
+        for _ in range(2):   # consecutive host batches: one per replica (round robin)
+            assert_same(ix, o, ts)
+        after = [ix.replica_stats(r)[0] for r in (0, 1)]
+        assert [a - b for a, b in zip(after, before)] == [1, 1], (before, after)
+    st = ix.stats()
+    assert st["n_keys"] == o.size() != st0["n_keys"]   # one host key set, whatever the replica count
+    ix.close()
+
+    def build(devices):
+        gc.collect()
+        r0 = psutil.Process().memory_info().rss
+        big = wl.filters(3, 400_000)
+        x = _native.Index(devices=devices, hint_keys=len(big))
+        x.apply(np.ones(len(big), np.uint8), big.blob, big.offs, big.vals)
+        x.match_batch(ts.blob, ts.offs)        # both replicas uploaded (first sync)
+        x.match_batch(ts.blob, ts.offs)
+        del big
+        gc.collect()
+        rss = psutil.Process().memory_info().rss - r0
+        dev_bytes = x.stats()["device_bytes"]
+        x.close()
+        return rss, dev_bytes
+    one, db1 = build([0])
+    two, db2 = build([0, 0])
+    print(f"host RSS growth: 1 replica {one / 2**20:.0f} MiB, 2 replicas {two / 2**20:.0f} MiB "
+          f"(device {db1 / 2**20:.0f} MiB per replica)")
+    assert db1 == db2 and two <= 1.2 * one + (32 << 20)
