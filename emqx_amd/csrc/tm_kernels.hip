@@ -1057,7 +1057,7 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_small(DevIndex ix, Workspace 
     __shared__ uint8_t s_mlen[SM_TOPICS][MID_L];
     __shared__ uint64_t s_cnt[SM_TOPICS];
     __shared__ uint64_t s_base;
-    __shared__ uint32_t s_vb;
+    __shared__ uint32_t s_vb, s_fail;
     if (threadIdx.x == 0) s_vb = atomicAdd(&ws.list_n[L_COUNT + 4], 1u);   // blocks scan in start order
     __syncthreads();
     const uint32_t vb = s_vb;
@@ -1227,18 +1227,29 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_small(DevIndex ix, Workspace 
         uint64_t sum = 0;
         for (int i = 0; i < SM_TOPICS; i++) sum += s_cnt[i];
         uint64_t pre = 0;
+        uint32_t fail = 0;
         if (vb > 0) {
             ws.look_val[vb] = sum;
             __hip_atomic_store(&ws.look_flag[vb], (tag << 2) | LB_AGG, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-            for (int64_t j = (int64_t)vb - 1; j >= 0; j--) {
+            // block j started before this one (its ticket is smaller), so it
+            // publishes soon; the wait is bounded all the same (a lost
+            // publication must not leave a spinning grid behind): past the
+            // bound the block's topics get err 4 and the batch fails loudly
+            uint32_t spins = 0;
+            for (int64_t j = (int64_t)vb - 1; j >= 0 && !fail; j--) {
                 uint32_t f;
-                do {
+                for (;;) {
                     f = __hip_atomic_load(&ws.look_flag[j], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-                } while ((f >> 2) != tag);   // block j started before this one: it publishes soon
+                    if ((f >> 2) == tag) break;
+                    if (++spins > (1u << 22)) { fail = 1; break; }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+                if (fail) break;
                 pre += ws.look_val[j];
                 if ((f & 3u) == LB_INCL) break;
             }
         }
+        s_fail = fail;
         ws.look_val[vb] = pre + sum;
         __hip_atomic_store(&ws.look_flag[vb], (tag << 2) | LB_INCL, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         s_base = pre;
@@ -1253,8 +1264,9 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_small(DevIndex ix, Workspace 
     for (uint32_t i = 0; i < gi; i++) pos += s_cnt[i];
     if (gl == 0) {
         hit_offs[t] = pos;
-        o.err[t] = fb ? (frc == RC_BADARG ? 1 : frc == RC_DEEP ? 2 : 0) : badarg;
+        o.err[t] = s_fail ? 4 : fb ? (frc == RC_BADARG ? 1 : frc == RC_DEEP ? 2 : 0) : badarg;
     }
+    if (s_fail) return;
 
     // ---- the values, straight into the CSR
     if (fb) {

@@ -51,7 +51,9 @@
  * its err flag is 1 and it has no hits.
  * A topic of more than 65536 levels (longer than MQTT's 65535-byte maximum,
  * emqx_mqtt.hrl:44, so never seen from a client) is not matched: err flag 2,
- * no hits.
+ * no hits.  Err flag 4 marks a topic whose batch failed inside the device
+ * (a bounded wait of the one-launch small-batch scan expired): no result --
+ * never expected; the batch should be retried and reported.
  */
 #ifndef TMATCH_H
 #define TMATCH_H
