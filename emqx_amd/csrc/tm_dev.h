@@ -53,7 +53,7 @@ struct Workspace {
     uint2 *deep_stk;      // [DEEP_LANES * (MAX_LEVELS + 1)]
     uint8_t *deep_plus;   // [DEEP_LANES * MAX_LEVELS] '+' levels of each deep lane's path
     uint32_t *look_flag;  // [n / SM_TOPICS + 2] one-launch path: per block, (launch tag << 2) | LB_AGG / LB_INCL
-    uint64_t *look_val;   //   and the block's hit total (LB_AGG) or inclusive prefix (LB_INCL)
+    uint64_t *look_val;   //   [2 v] block v's hit total (LB_AGG), [2 v + 1] its inclusive prefix (LB_INCL)
     uint64_t cap_n;
 };
 

@@ -1351,7 +1351,7 @@ int ensure_ws(tm_index *ix, uint64_t n, Lane &ln) {
     HIPCHK(ix, hipMalloc(&w.blk, (c / TILE + 4) * 8));
     HIPCHK(ix, hipMemsetAsync(w.blk, 0, (c / TILE + 4) * 8, ln.s));   // zero between batches (k_emit)
     HIPCHK(ix, hipMalloc(&w.look_flag, (c / SM_TOPICS + 4) * 4));
-    HIPCHK(ix, hipMalloc(&w.look_val, (c / SM_TOPICS + 4) * 8));
+    HIPCHK(ix, hipMalloc(&w.look_val, (c / SM_TOPICS + 4) * 16));
     HIPCHK(ix, hipMemsetAsync(w.look_flag, 0, (c / SM_TOPICS + 4) * 4, ln.s));   // no launch tag is 0
     w.cap_n = c;
     return TM_OK;

@@ -1228,8 +1228,11 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_small(DevIndex ix, Workspace 
         for (int i = 0; i < SM_TOPICS; i++) sum += s_cnt[i];
         uint64_t pre = 0;
         uint32_t fail = 0;
+        // look_val[2 v] = block v's aggregate, [2 v + 1] its inclusive prefix: two
+        // words, so a reader that saw LB_AGG never reads the inclusive prefix
+        // written over it meanwhile
         if (vb > 0) {
-            ws.look_val[vb] = sum;
+            ws.look_val[2 * vb] = sum;
             __hip_atomic_store(&ws.look_flag[vb], (tag << 2) | LB_AGG, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
             // block j started before this one (its ticket is smaller), so it
             // publishes soon; the wait is bounded all the same (a lost
@@ -1245,12 +1248,13 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_small(DevIndex ix, Workspace 
                     __builtin_amdgcn_s_sleep(1);
                 }
                 if (fail) break;
-                pre += ws.look_val[j];
-                if ((f & 3u) == LB_INCL) break;
+                const bool incl = (f & 3u) == LB_INCL;
+                pre += ws.look_val[2 * j + (incl ? 1 : 0)];
+                if (incl) break;
             }
         }
         s_fail = fail;
-        ws.look_val[vb] = pre + sum;
+        ws.look_val[2 * vb + 1] = pre + sum;
         __hip_atomic_store(&ws.look_flag[vb], (tag << 2) | LB_INCL, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         s_base = pre;
         if (vb == gridDim.x - 1) {
