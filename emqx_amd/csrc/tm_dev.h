@@ -60,6 +60,7 @@ struct Workspace {
 constexpr int TILE = 256;    // topics per walk block = per scan tile = per emit block
 constexpr int LIST_SLOTS = L_COUNT + 5;   // Workspace::list_n entries
 constexpr int SM_TOPICS = 16;             // topics per block of the one-launch small-batch path
+constexpr int SM_TB = 256;                // topic bytes it stages in LDS (longer topics: the lane walk)
 
 
 // Pipeline entry points (tm_kernels.hip).  All asynchronous on `s`.

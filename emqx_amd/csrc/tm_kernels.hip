@@ -1058,6 +1058,8 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_small(DevIndex ix, Workspace 
     __shared__ uint64_t s_cnt[SM_TOPICS];
     __shared__ uint64_t s_base;
     __shared__ uint32_t s_vb, s_fail;
+    constexpr uint32_t TBQ = SM_TB / 16 + 1;              // 16-B chunks of a topic staged in LDS
+    __shared__ uint4 s_tb[SM_TOPICS][TBQ];
     if (threadIdx.x == 0) s_vb = atomicAdd(&ws.list_n[L_COUNT + 4], 1u);   // blocks scan in start order
     __syncthreads();
     const uint32_t vb = s_vb;
@@ -1070,11 +1072,24 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_small(DevIndex ix, Workspace 
     uint64_t *sc_ = s_code[wv] + base, *hcode = s_hcode[wv] + base;
     const uint64_t beg = live ? offs[t] : 0, end = live ? offs[t + 1] : 0, len = end - beg;
 
+    // ---- the topic into LDS: one round of 16-B loads by the group's lanes
+    // (the caller's buffers may be host memory read over PCIe: every byte
+    // read from there would be a round trip).  Aligned chunks share their
+    // granule with a valid byte, so they never touch a page the caller does
+    // not own.  A topic longer than SM_TB bytes goes to the lane walk.
+    const uint64_t a0 = beg & ~15ull;
+    const uint32_t nq = live ? (uint32_t)((end - a0 + 15) >> 4) : 0;
+    bool fb = nq > TBQ;   // the group's first lane walks this topic (lane walk, global reads)
+    if (!fb)
+        for (uint32_t c = gl; c < nq; c += W) s_tb[gi][c] = ld4_once(blob + a0 + 16ull * c);
+    wave_sync();
+    const uint8_t *tb = reinterpret_cast<const uint8_t *>(s_tb[gi]) + (beg - a0);   // topic byte i = tb[i]
+    const uint64_t tlen = fb ? 0 : len;
+
     // ---- the wave walk (k_walk_wave), falling back instead of listing
-    bool fb = false;   // the group's first lane walks this topic
     uint32_t nsl = 0;
-    for (uint64_t p = 0; p < len; p += W) {
-        const bool sl = p + gl < len && blob[beg + p + gl] == '/';
+    for (uint64_t p = 0; p < tlen; p += W) {
+        const bool sl = p + gl < tlen && tb[p + gl] == '/';
         const uint64_t m = grp.ballot(sl);
         if (sl) {
             const uint32_t k = nsl + grp.rank(m);
@@ -1084,18 +1099,18 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_small(DevIndex ix, Workspace 
     }
     const uint32_t L = nsl + 1;
     wave_sync();
-    fb = live && L > MAXL;
+    fb = live && (fb || L > MAXL);
     const bool mine = live && !fb && gl < L;
     const uint32_t ws0 = !mine || gl == 0 ? 0 : sl_[gl - 1] + 1;
     const uint32_t we0 = !mine ? 0 : gl == L - 1 ? (uint32_t)len : sl_[gl];
     const uint32_t wl = we0 - ws0;
-    const uint8_t *wp = blob + beg + ws0;
-    WordAcc w; w.reset(beg + ws0);
+    const uint8_t *wp = tb + ws0;
+    WordAcc w; w.reset(ws0);
     if (mine) for (uint32_t i = 0; i < wl; i++) w.push(wp[i]);
     const bool bad = mine && wl == 1 && (w.b0 == '+' || w.b0 == '#');
     const bool badarg = grp.ballot(bad) != 0;
     const bool dollar = grp.bcast(mine && wl >= 1 && (w.b0 & 0xFFu) == '$' ? 1u : 0u, 0) != 0;
-    uint32_t wid = mine && !badarg ? vocab_find(ix, w, blob) : NONE;
+    uint32_t wid = mine && !badarg ? vocab_find(ix, w, tb) : NONE;   // (long words: bytes from LDS)
     const bool allf = grp.ballot(mine && wid == NONE) == 0;
     uint64_t xh = FNV_OFF;
     for (uint32_t l = 0; l < L && !fb; l++) xh = seq_hash_step(xh, grp.bcast(wid, l));
