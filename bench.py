@@ -596,6 +596,9 @@ def host_bench_lib():
     lib.tmb_single.argtypes = [vp, u64, vp, vp, u64, ctypes.c_int, dp]
     lib.tmb_callers.argtypes = [vp, ctypes.c_int, u64, vp, vp, u64, ctypes.c_double, ctypes.c_int, dp]
     lib.tmb_pipeline.argtypes = [vp, ctypes.c_int, vp, vp, u64, ctypes.c_int, ctypes.c_int, ctypes.c_int, dp]
+    lib.tmb_bind.argtypes = [vp]
+    from emqx_amd import _native
+    assert lib.tmb_bind(ctypes.c_void_p(_native.load_library()._handle)) == 0   # the libtmatch this process uses
     return lib
 
 

@@ -92,10 +92,9 @@ def build_work(force: bool = False) -> Path:
 
 def build_bench(force: bool = False) -> Path:
     src = CSRC / "hostbench.cpp"
-    if force or _stale(LIB_BENCH, [src, LIB_TMATCH, ROOT / "include" / "tmatch.h"]):
+    if force or _stale(LIB_BENCH, [src, ROOT / "include" / "tmatch.h"]):
         tmp = LIB_BENCH.with_suffix(".so.tmp")
-        _run(["hipcc", "-O2", "-std=c++17", "-fPIC", "-shared", "-pthread", "-o", str(tmp), str(src),
-              f"-L{PKG}", "-l:libtmatch.so", "-Wl,-rpath,$ORIGIN"])
+        _run(["hipcc", "-O2", "-std=c++17", "-fPIC", "-shared", "-pthread", "-o", str(tmp), str(src), "-ldl"])
         os.replace(tmp, LIB_BENCH)
     return LIB_BENCH
 

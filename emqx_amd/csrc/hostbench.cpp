@@ -13,6 +13,7 @@
 //                  H2D copy, match, D2H of offsets and values, overlapped on
 //                  several streams -- the rate a caller that hands over host
 //                  buffers sees, next to the PCIe bytes it moves
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -23,6 +24,20 @@
 #include <vector>
 
 #include "../../include/tmatch.h"
+
+// The C ABI of the libtmatch instance the caller loaded (tmb_bind: a bench or
+// study may load an experimental build under another name; every tm_index*
+// must go back to the library that made it).
+namespace api {
+int (*host_alloc)(tm_index *, uint64_t, void **);
+int (*host_free)(tm_index *, void *);
+int (*match_batch)(tm_index *, uint64_t, const uint8_t *, const uint64_t *, uint64_t *, uint32_t *, uint64_t, uint8_t *);
+int (*match_batch_dev)(tm_index *, uint64_t, const uint8_t *, const uint64_t *, uint64_t *, uint32_t *, uint64_t,
+                       uint8_t *, void *);
+int (*apply_deltas)(tm_index *, uint64_t, const uint8_t *, const uint8_t *, const uint64_t *, const uint32_t *,
+                    const uint8_t *);
+int (*stream_release)(tm_index *, void *);
+}  // namespace api
 
 namespace {
 
@@ -43,23 +58,35 @@ struct Caller {
         h = ix; n = nt; cap = cap_;
         const uint64_t b0 = to[first], nb = to[first + nt] - b0;
         int rc;
-        if ((rc = tm_host_alloc(h, nb + 16, (void **)&blob)) || (rc = tm_host_alloc(h, 8 * (nt + 1), (void **)&offs)) ||
-            (rc = tm_host_alloc(h, 8 * (nt + 1), (void **)&hit)) || (rc = tm_host_alloc(h, 4 * cap, (void **)&vals)) ||
-            (rc = tm_host_alloc(h, nt + 1, (void **)&err)))
+        if ((rc = api::host_alloc(h, nb + 16, (void **)&blob)) || (rc = api::host_alloc(h, 8 * (nt + 1), (void **)&offs)) ||
+            (rc = api::host_alloc(h, 8 * (nt + 1), (void **)&hit)) || (rc = api::host_alloc(h, 4 * cap, (void **)&vals)) ||
+            (rc = api::host_alloc(h, nt + 1, (void **)&err)))
             return rc;
         memcpy(blob, tb + b0, nb);
         for (uint64_t i = 0; i <= nt; i++) offs[i] = to[first + i] - b0;
         return TM_OK;
     }
-    int run() { return tm_match_batch(h, n, blob, offs, hit, vals, cap, err); }
+    int run() { return api::match_batch(h, n, blob, offs, hit, vals, cap, err); }
     void fini() {
-        for (void *p : {(void *)blob, (void *)offs, (void *)hit, (void *)vals, (void *)err}) if (p) tm_host_free(h, p);
+        for (void *p : {(void *)blob, (void *)offs, (void *)hit, (void *)vals, (void *)err}) if (p) api::host_free(h, p);
     }
 };
 
 }  // namespace
 
 extern "C" {
+
+// bind to the libtmatch the caller loaded (dlopen handle, e.g. ctypes' _handle)
+int tmb_bind(void *lib) {
+    api::host_alloc = reinterpret_cast<decltype(api::host_alloc)>(dlsym(lib, "tm_host_alloc"));
+    api::host_free = reinterpret_cast<decltype(api::host_free)>(dlsym(lib, "tm_host_free"));
+    api::match_batch = reinterpret_cast<decltype(api::match_batch)>(dlsym(lib, "tm_match_batch"));
+    api::match_batch_dev = reinterpret_cast<decltype(api::match_batch_dev)>(dlsym(lib, "tm_match_batch_dev"));
+    api::apply_deltas = reinterpret_cast<decltype(api::apply_deltas)>(dlsym(lib, "tm_apply_deltas"));
+    api::stream_release = reinterpret_cast<decltype(api::stream_release)>(dlsym(lib, "tm_stream_release"));
+    return api::host_alloc && api::host_free && api::match_batch && api::match_batch_dev && api::apply_deltas &&
+                   api::stream_release ? 0 : -1;
+}
 
 // out: [p50_ms, p99_ms, mean_ms]
 int tmb_single(tm_index *h, uint64_t n, const uint8_t *tb, const uint64_t *to, uint64_t cap, int iters, double *out) {
@@ -123,7 +150,7 @@ int tmb_callers(tm_index *h, int nthreads, uint64_t n, const uint8_t *tb, const 
             }
             std::vector<uint8_t> ops(churn_ops, 1);
             while (!stop.load(std::memory_order_relaxed)) {
-                if (tm_apply_deltas(h, churn_ops, ops.data(), blob.data(), offs.data(), vals.data(), nullptr)) {
+                if (api::apply_deltas(h, churn_ops, ops.data(), blob.data(), offs.data(), vals.data(), nullptr)) {
                     err = -1;
                     break;
                 }
@@ -192,7 +219,7 @@ int tmb_pipeline(tm_index *h, int device, const uint8_t *tb, const uint64_t *to,
         for (int k = 0; k < R; k++) {
             const uint64_t boff = ((n + 1) * 8 + 15) & ~15ull;
             hipMemcpyAsync(l.d_in, hb[k].p, hb[k].bytes, hipMemcpyHostToDevice, l.s);
-            int rc = tm_match_batch_dev(h, n, l.d_in + boff, reinterpret_cast<uint64_t *>(l.d_in), l.d_hit, nullptr, 0,
+            int rc = api::match_batch_dev(h, n, l.d_in + boff, reinterpret_cast<uint64_t *>(l.d_in), l.d_hit, nullptr, 0,
                                         l.d_err, l.s);
             if (rc) return rc;
             hipMemcpyAsync(l.h_hit, l.d_hit, 8 * (n + 1), hipMemcpyDeviceToHost, l.s);
@@ -210,7 +237,7 @@ int tmb_pipeline(tm_index *h, int device, const uint8_t *tb, const uint64_t *to,
         const HostBatch &b = hb[k % R];
         const uint64_t boff = ((n + 1) * 8 + 15) & ~15ull;
         if (hipMemcpyAsync(l.d_in, b.p, b.bytes, hipMemcpyHostToDevice, l.s) != hipSuccess) return TM_EDEVICE;
-        int rc = tm_match_batch_dev(h, n, l.d_in + boff, reinterpret_cast<uint64_t *>(l.d_in), l.d_hit, l.d_vals, cap,
+        int rc = api::match_batch_dev(h, n, l.d_in + boff, reinterpret_cast<uint64_t *>(l.d_in), l.d_hit, l.d_vals, cap,
                                     l.d_err, l.s);
         if (rc) return rc;
         if (hipMemcpyAsync(l.h_hit, l.d_hit, 8 * (n + 1), hipMemcpyDeviceToHost, l.s) != hipSuccess ||
@@ -236,7 +263,7 @@ int tmb_pipeline(tm_index *h, int device, const uint8_t *tb, const uint64_t *to,
     const double el = now_s() - t0;
     for (auto &l : ls) {
         hipStreamSynchronize(l.s);
-        tm_stream_release(h, l.s);
+        api::stream_release(h, l.s);
         hipFree(l.d_in); hipFree(l.d_hit); hipFree(l.d_vals); hipFree(l.d_err);
         hipHostFree(l.h_hit); hipHostFree(l.h_vals);
         hipEventDestroy(l.done); hipStreamDestroy(l.s);
