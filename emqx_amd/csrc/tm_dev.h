@@ -41,6 +41,20 @@ constexpr int DEEP_LANES = 64;   // lanes of the global-scratch (deep / overflow
 enum { L_MID = 0, L_DEEP = 1, L_OVF_MID = 2, L_OVF_DEEP = 3, L_COUNT = 4 };
 
 // Per-batch device scratch (grow-only, owned by the index).
+// k_walk_small's look-back word of a block: launch tag (20 bits), state
+// (LB_AGG: its own hit total; LB_INCL: the total of it and every block before
+// it) and the value (42 bits) in ONE 64-bit word, so a reader gets state and
+// value from one coherent load (no acquire / release: those write back and
+// invalidate the whole L2 of the XCD, under every kernel running there)
+enum : uint32_t { LB_AGG = 1, LB_INCL = 2 };
+constexpr uint32_t LB_TAG_BITS = 20, LB_TAG_MASK = (1u << LB_TAG_BITS) - 1;
+constexpr uint64_t LB_VAL_MASK = (1ull << 42) - 1;
+__host__ __device__ constexpr uint64_t lb_word(uint32_t tag, uint32_t st, uint64_t v) {
+    return (uint64_t)tag << 44 | (uint64_t)st << 42 | (v & LB_VAL_MASK);
+}
+__host__ __device__ constexpr uint32_t lb_tag(uint64_t w) { return (uint32_t)(w >> 44); }
+__host__ __device__ constexpr uint32_t lb_state(uint64_t w) { return (uint32_t)(w >> 42) & 3u; }
+
 struct Workspace {
     uint32_t *cnt;        // [n] hits per topic
     uint32_t *nr;         // [n] ranges per topic (RCAP+1 = overflow)
@@ -53,8 +67,7 @@ struct Workspace {
     uint32_t *deep_wid;   // [DEEP_LANES * MAX_LEVELS]
     uint2 *deep_stk;      // [DEEP_LANES * (MAX_LEVELS + 1)]
     uint8_t *deep_plus;   // [DEEP_LANES * MAX_LEVELS] '+' levels of each deep lane's path
-    uint32_t *look_flag;  // [n / SM_TOPICS + 2] one-launch path: per block, (launch tag << 2) | LB_AGG / LB_INCL
-    uint64_t *look_val;   //   [2 v] block v's hit total (LB_AGG), [2 v + 1] its inclusive prefix (LB_INCL)
+    uint64_t *look;       // [n / SM_TOPICS + 4] one-launch path: per block, one look-back word (lb_word)
     uint64_t cap_n;
 };
 

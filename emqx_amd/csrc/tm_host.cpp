@@ -1136,11 +1136,17 @@ PatchBases patch_bases(tm_index *ix, int r) {
     return b;
 }
 
-// a fresh launch tag of the lane's workspace (never 0, 30 bits)
-uint32_t next_tag(Lane &ln) {
-    ln.tag = (ln.tag + 1) & 0x3FFFFFFFu;
-    if (!ln.tag) ln.tag = 1;
-    return ln.tag;
+// a fresh launch tag of the lane's workspace (1 .. LB_TAG_MASK); when the tags
+// wrap, the look-back words are cleared first, on the launch's stream, so no
+// word an earlier launch left can carry the new tag
+int next_tag(tm_index *ix, Lane &ln, hipStream_t s, uint32_t &tag) {
+    ln.tag = (ln.tag + 1) & LB_TAG_MASK;
+    if (!ln.tag) {
+        ln.tag = 1;
+        HIPCHK(ix, hipMemsetAsync(ln.w.look, 0, (ln.w.cap_n / SM_TOPICS + 4) * 8, s));
+    }
+    tag = ln.tag;
+    return TM_OK;
 }
 
 // the lane's batch is done with the index: later patches (on any stream) wait for it
@@ -1252,8 +1258,7 @@ DevIndex dev_view(tm_index *ix, int r) {
 // ------------------------------------------------------------------ lanes
 
 void free_workspace(Workspace &w) {
-    void *wb[] = {w.cnt, w.nr, w.rng, w.lists, w.list_n, w.blk, w.deep_wid, w.deep_stk, w.deep_plus, w.look_flag,
-                  w.look_val};
+    void *wb[] = {w.cnt, w.nr, w.rng, w.lists, w.list_n, w.blk, w.deep_wid, w.deep_stk, w.deep_plus, w.look};
     for (void *p : wb) if (p) (void)hipFree(p);
     w = Workspace{};
 }
@@ -1378,7 +1383,7 @@ int ensure_ws(tm_index *ix, uint64_t n, Lane &ln) {
     if (n <= w.cap_n && w.cnt) return TM_OK;
     HIPCHK(ix, hipStreamSynchronize(ln.s));
     if (w.cnt) {
-        void *old[] = {w.cnt, w.nr, w.rng, w.lists, w.blk, w.look_flag, w.look_val};
+        void *old[] = {w.cnt, w.nr, w.rng, w.lists, w.blk, w.look};
         for (void *p : old) (void)hipFree(p);
     }
     uint64_t c = std::max<uint64_t>(n + n / 4, 1024);
@@ -1388,9 +1393,8 @@ int ensure_ws(tm_index *ix, uint64_t n, Lane &ln) {
     HIPCHK(ix, hipMalloc(&w.lists, c * (L_COUNT + 1) * 4));
     HIPCHK(ix, hipMalloc(&w.blk, (c / TILE + 4) * 8));
     HIPCHK(ix, hipMemsetAsync(w.blk, 0, (c / TILE + 4) * 8, ln.s));   // zero between batches (k_emit)
-    HIPCHK(ix, hipMalloc(&w.look_flag, (c / SM_TOPICS + 4) * 4));
-    HIPCHK(ix, hipMalloc(&w.look_val, (c / SM_TOPICS + 4) * 16));
-    HIPCHK(ix, hipMemsetAsync(w.look_flag, 0, (c / SM_TOPICS + 4) * 4, ln.s));   // no launch tag is 0
+    HIPCHK(ix, hipMalloc(&w.look, (c / SM_TOPICS + 4) * 8));
+    HIPCHK(ix, hipMemsetAsync(w.look, 0, (c / SM_TOPICS + 4) * 8, ln.s));   // no launch tag is 0
     w.cap_n = c;
     return TM_OK;
 }
@@ -1639,7 +1643,9 @@ int tm_match_batch_dev_ex(tm_index *ix, uint64_t n, const uint8_t *bytes, const 
     const DevIndex d = dev_view(ix, ln->r);
     tm_index::ProfEv ev;
     if ((rc = prof_begin(ix, ev, s))) return rc;
-    HIPCHK(ix, launch_match(d, ln->w, n, bytes, offs, hit_offs, err, out, out ? cap : 0, next_tag(*ln), s, ev.w0,
+    uint32_t tag;
+    if ((rc = next_tag(ix, *ln, s, tag))) return rc;
+    HIPCHK(ix, launch_match(d, ln->w, n, bytes, offs, hit_offs, err, out, out ? cap : 0, tag, s, ev.w0,
                             ev.w1));
     if (order != TM_ORDER_TRAVERSAL && out)
         HIPCHK(ix, launch_sort_segments(ln->w, n, hit_offs, out, cap, order == TM_ORDER_UNIQUE, ucnt, s));
@@ -1837,8 +1843,10 @@ int tm_match_batch_ex(tm_index *ix, uint64_t n, const uint8_t *tb, const uint64_
                 if ((rc = grow_dev(ix, s, ln.d_vals, ln.d_vals_cap, cap))) return rc;
                 vdst = ln.d_vals;
             }
+            uint32_t tag;
+            if (int rc = next_tag(ix, ln, s, tag)) return rc;
             HIPCHK(ix, launch_match(d, ln.w, n, dbytes, reinterpret_cast<const uint64_t *>(dof), dhit, de, vdst,
-                                    dv ? cap : 0, next_tag(ln), s));
+                                    dv ? cap : 0, tag, s));
             if (sorted && dv) {
                 HIPCHK(ix, launch_sort_segments(ln.w, n, dhit, vdst, cap, unique, reinterpret_cast<uint32_t *>(du), s));
                 HIPCHK(ix, launch_copy_values(dhit, n, vdst, reinterpret_cast<uint32_t *>(dv), cap, s));
@@ -1882,7 +1890,9 @@ int tm_match_batch_ex(tm_index *ix, uint64_t n, const uint8_t *tb, const uint64_
         if (sorted && (rc = grow_dev(ix, s, ln.d_vals, ln.d_vals_cap, ln.pin_vals_cap))) return rc;
         if (sorted) vdst = ln.d_vals;
         const DevIndex d = dev_view(ix, ln.r);
-        HIPCHK(ix, launch_match(d, ln.w, n, dbytes, doffs, dhit, derr, vdst, ln.pin_vals_cap, next_tag(ln), s));
+        uint32_t tag;
+        if (int rc = next_tag(ix, ln, s, tag)) return rc;
+        HIPCHK(ix, launch_match(d, ln.w, n, dbytes, doffs, dhit, derr, vdst, ln.pin_vals_cap, tag, s));
         if (sorted) {
             HIPCHK(ix, launch_sort_segments(ln.w, n, dhit, vdst, ln.pin_vals_cap, unique, dunq, s));
             HIPCHK(ix, launch_copy_values(dhit, n, vdst, ln.pin_vals_dev, ln.pin_vals_cap, s));

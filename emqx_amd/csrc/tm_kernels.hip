@@ -1026,8 +1026,6 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_wave(DevIndex ix, Workspace w
 // scan over the blocks in the order they started (a ticket, so a block only
 // ever waits for blocks already running); then each group copies its values
 // straight into the CSR.  No range lists, no device-side lists, no other kernel.
-enum { LB_AGG = 1, LB_INCL = 2 };
-
 struct CountEmit {          // one-launch path: hit count only (the values come from a re-walk)
     uint64_t cnt;
     __device__ __forceinline__ bool operator()(uint32_t, uint32_t n) { cnt += n & RUN_CNT; return true; }
@@ -1238,43 +1236,47 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_small(DevIndex ix, Workspace 
     // ---- the block's offset: exclusive scan of its 16 counts + decoupled look-back
     if (gl == 0) s_cnt[gi] = live ? total : 0;
     __syncthreads();
-    if (threadIdx.x == 0) {
+    if (wv == 0) {
+        const uint32_t lane = threadIdx.x;
         uint64_t sum = 0;
         for (int i = 0; i < SM_TOPICS; i++) sum += s_cnt[i];
+        if (vb > 0 && lane == 0)
+            __hip_atomic_store(&ws.look[vb], lb_word(tag, LB_AGG, sum), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // The wave reads 64 predecessors at once (lane k: block hi - k), so
+        // the look-back costs one flag round trip per 64 blocks, not one per
+        // block.  Block j started before this one (its ticket is smaller), so
+        // it publishes soon; the wait is bounded all the same (a lost
+        // publication must not leave a spinning grid behind): past the bound
+        // the block's topics get err 4 and the batch fails loudly.
         uint64_t pre = 0;
-        uint32_t fail = 0;
-        // look_val[2 v] = block v's aggregate, [2 v + 1] its inclusive prefix: two
-        // words, so a reader that saw LB_AGG never reads the inclusive prefix
-        // written over it meanwhile
-        if (vb > 0) {
-            ws.look_val[2 * vb] = sum;
-            __hip_atomic_store(&ws.look_flag[vb], (tag << 2) | LB_AGG, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-            // block j started before this one (its ticket is smaller), so it
-            // publishes soon; the wait is bounded all the same (a lost
-            // publication must not leave a spinning grid behind): past the
-            // bound the block's topics get err 4 and the batch fails loudly
-            uint32_t spins = 0;
-            for (int64_t j = (int64_t)vb - 1; j >= 0 && !fail; j--) {
-                uint32_t f;
+        uint32_t fail = 0, spins = 0;
+        for (int64_t hi = (int64_t)vb - 1; hi >= 0;) {
+            const int64_t j = hi - (int64_t)lane;
+            uint64_t f = lb_word(tag, LB_INCL, 0);   // before block 0: an inclusive prefix of 0
+            if (j >= 0)
                 for (;;) {
-                    f = __hip_atomic_load(&ws.look_flag[j], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-                    if ((f >> 2) == tag) break;
-                    if (++spins > (1u << 22)) { fail = 1; break; }
+                    f = __hip_atomic_load(&ws.look[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (lb_tag(f) == tag || ++spins > (1u << 22)) break;
                     __builtin_amdgcn_s_sleep(1);
                 }
-                if (fail) break;
-                const bool incl = (f & 3u) == LB_INCL;
-                pre += ws.look_val[2 * j + (incl ? 1 : 0)];
-                if (incl) break;
-            }
+            if (__ballot(lb_tag(f) != tag)) { fail = 1; break; }
+            const uint64_t mi = __ballot(lb_state(f) == LB_INCL);
+            const uint32_t k = mi ? (uint32_t)__ffsll((long long)mi) - 1 : 63;   // nearest inclusive prefix
+            uint64_t v = lane <= k ? f & LB_VAL_MASK : 0;
+            for (int d = 32; d; d >>= 1) v += __shfl_xor(v, d, 64);
+            pre += v;
+            if (mi) break;
+            hi -= 64;
         }
-        s_fail = fail;
-        ws.look_val[2 * vb + 1] = pre + sum;
-        __hip_atomic_store(&ws.look_flag[vb], (tag << 2) | LB_INCL, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        s_base = pre;
-        if (vb == gridDim.x - 1) {
-            hit_offs[n] = pre + sum;
-            ws.list_n[L_COUNT + 4] = 0;   // every ticket is taken
+        if (lane == 0) {
+            s_fail = fail;
+            __hip_atomic_store(&ws.look[vb], lb_word(tag, LB_INCL, pre + sum), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+            s_base = pre;
+            if (vb == gridDim.x - 1) {
+                hit_offs[n] = pre + sum;
+                ws.list_n[L_COUNT + 4] = 0;   // every ticket is taken
+            }
         }
     }
     __syncthreads();
