@@ -390,6 +390,15 @@ def main():
                                      "d2h": round(d2h / (out[1] * 1e-3) / 1e9, 1)},
                        "note": "topics in pinned host memory -> H2D -> match -> D2H of offsets and values into pinned "
                                "host memory, 3 streams; value bytes per batch from a sizing pass"}
+            # the PCIe bound this implies: plain pinned copies of 256 MiB, both directions at once
+            pc = (ctypes.c_double * 4)()
+            assert hb.tmb_pcie(local, 256 << 20, 16, 4, pc) == 0
+            per = max(h2d / pc[2], d2h / pc[3]) if pc[2] > 0 and pc[3] > 0 else 0.0   # s per batch at the ceiling
+            hostfed["pcie_ceiling_GBps"] = {"h2d_alone": round(pc[0], 1), "d2h_alone": round(pc[1], 1),
+                                            "both_each": round(pc[2], 1)}
+            if per > 0:
+                hostfed["pcie_bound_topics_per_s"] = round(B / per, 1)
+                hostfed["frac_of_pcie_bound"] = round(out[0] / (B / per), 3)
     if world > 1 and lat_native:
         # the slowest rank's percentiles (max over ranks); the caller and
         # host-fed legs are rank 0's (each rank drives its own GPU alike)
@@ -595,7 +604,9 @@ def host_bench_lib():
     vp, u64, dp = ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_double)
     lib.tmb_single.argtypes = [vp, u64, vp, vp, u64, ctypes.c_int, dp]
     lib.tmb_callers.argtypes = [vp, ctypes.c_int, u64, vp, vp, u64, ctypes.c_double, ctypes.c_int, dp]
+    lib.tmb_callers_ex.argtypes = [vp, ctypes.c_int, u64, vp, vp, u64, ctypes.c_double, ctypes.c_int, ctypes.c_int, dp]
     lib.tmb_pipeline.argtypes = [vp, ctypes.c_int, vp, vp, u64, ctypes.c_int, ctypes.c_int, ctypes.c_int, dp]
+    lib.tmb_pcie.argtypes = [ctypes.c_int, u64, ctypes.c_int, ctypes.c_int, dp]
     lib.tmb_bind.argtypes = [vp]
     from emqx_amd import _native
     assert lib.tmb_bind(ctypes.c_void_p(_native.load_library()._handle)) == 0   # the libtmatch this process uses

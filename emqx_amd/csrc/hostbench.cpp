@@ -66,9 +66,33 @@ struct Caller {
         for (uint64_t i = 0; i <= nt; i++) offs[i] = to[first + i] - b0;
         return TM_OK;
     }
-    int run() { return api::match_batch(h, n, blob, offs, hit, vals, cap, err); }
+    // device mode: the same batch copied into HBM once, run through the device
+    // API on the caller's own stream (no PCIe traffic inside the batch)
+    hipStream_t s = nullptr;
+    uint8_t *dblob = nullptr, *derr = nullptr; uint64_t *doffs = nullptr, *dhit = nullptr; uint32_t *dvals = nullptr;
+    int to_device() {
+        const uint64_t nb = offs[n];
+        if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess ||
+            hipMalloc(&dblob, nb + 16) != hipSuccess || hipMalloc(&doffs, 8 * (n + 1)) != hipSuccess ||
+            hipMalloc(&dhit, 8 * (n + 1)) != hipSuccess || hipMalloc(&dvals, 4 * cap) != hipSuccess ||
+            hipMalloc(&derr, n + 1) != hipSuccess || hipMemcpy(dblob, blob, nb, hipMemcpyHostToDevice) != hipSuccess ||
+            hipMemcpy(doffs, offs, 8 * (n + 1), hipMemcpyHostToDevice) != hipSuccess)
+            return TM_EDEVICE;
+        return TM_OK;
+    }
+    int run() {
+        if (!s) return api::match_batch(h, n, blob, offs, hit, vals, cap, err);
+        int rc = api::match_batch_dev(h, n, dblob, doffs, dhit, dvals, cap, derr, s);
+        if (rc) return rc;
+        return hipStreamSynchronize(s) == hipSuccess ? TM_OK : TM_EDEVICE;
+    }
     void fini() {
         for (void *p : {(void *)blob, (void *)offs, (void *)hit, (void *)vals, (void *)err}) if (p) api::host_free(h, p);
+        if (s) {
+            for (void *p : {(void *)dblob, (void *)doffs, (void *)dhit, (void *)dvals, (void *)derr}) if (p) (void)hipFree(p);
+            api::stream_release(h, s);
+            (void)hipStreamDestroy(s);
+        }
     }
 };
 
@@ -111,14 +135,17 @@ int tmb_single(tm_index *h, uint64_t n, const uint8_t *tb, const uint64_t *to, u
 
 // nthreads callers, each with batches of n topics (caller k takes topics
 // [k n, (k + 1) n) of the set, which must hold nthreads * n); one churn thread
-// applies `churn_ops` deltas per millisecond (0: none).
+// applies `churn_ops` deltas per millisecond (0: none).  device_buffers: each
+// caller's batch lives in HBM and goes through tm_match_batch_dev on its own
+// stream (what the device can take without the PCIe leg of in-place batches).
 // out: [batches, topics_per_s, p50_ms, p99_ms, deltas_per_s, seconds]
-int tmb_callers(tm_index *h, int nthreads, uint64_t n, const uint8_t *tb, const uint64_t *to, uint64_t cap,
-                double seconds, int churn_ops, double *out) {
+int tmb_callers_ex(tm_index *h, int nthreads, uint64_t n, const uint8_t *tb, const uint64_t *to, uint64_t cap,
+                   double seconds, int churn_ops, int device_buffers, double *out) {
     std::vector<Caller> cs(nthreads);
     for (int k = 0; k < nthreads; k++) {
         int rc = cs[k].init(h, n, tb, to, (uint64_t)k * n, cap);
         if (rc) return rc;
+        if (device_buffers && (rc = cs[k].to_device())) return rc;
         if ((rc = cs[k].run())) return rc;   // warm: lane, workspace
     }
     std::atomic<bool> stop{false};
@@ -175,6 +202,11 @@ int tmb_callers(tm_index *h, int nthreads, uint64_t n, const uint8_t *tb, const 
     out[4] = deltas / el;
     out[5] = el;
     return TM_OK;
+}
+
+int tmb_callers(tm_index *h, int nthreads, uint64_t n, const uint8_t *tb, const uint64_t *to, uint64_t cap,
+                double seconds, int churn_ops, double *out) {
+    return tmb_callers_ex(h, nthreads, n, tb, to, cap, seconds, churn_ops, 0, out);
 }
 
 // Host-fed pipeline.  R batches of n topics (batch k = topics [k n, (k + 1) n)
@@ -274,6 +306,41 @@ int tmb_pipeline(tm_index *h, int device, const uint8_t *tb, const uint64_t *to,
     out[2] = h2d / iters;
     out[3] = d2h / iters;
     out[4] = el;
+    return TM_OK;
+}
+
+// The PCIe ceiling the host-fed pipeline runs against: pinned-host <-> HBM
+// copies of `bytes` in `chunks` pieces, H2D alone, D2H alone, and both
+// directions at once on two streams.  out: [h2d_GBps, d2h_GBps, both_h2d_GBps, both_d2h_GBps]
+int tmb_pcie(int device, uint64_t bytes, int chunks, int reps, double *out) {
+    if (hipSetDevice(device) != hipSuccess) return TM_EDEVICE;
+    uint8_t *hin = nullptr, *hout = nullptr, *din = nullptr, *dout = nullptr;
+    hipStream_t a = nullptr, b = nullptr;
+    if (hipHostMalloc(&hin, bytes, hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc(&hout, bytes, hipHostMallocDefault) != hipSuccess || hipMalloc(&din, bytes) != hipSuccess ||
+        hipMalloc(&dout, bytes) != hipSuccess || hipStreamCreateWithFlags(&a, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&b, hipStreamNonBlocking) != hipSuccess)
+        return TM_EDEVICE;
+    memset(hin, 1, bytes);
+    const uint64_t c = bytes / chunks;
+    auto run = [&](bool up, bool down) -> double {
+        const double t0 = now_s();
+        for (int r = 0; r < reps; r++)
+            for (int k = 0; k < chunks; k++) {
+                if (up) (void)hipMemcpyAsync(din + k * c, hin + k * c, c, hipMemcpyHostToDevice, a);
+                if (down) (void)hipMemcpyAsync(hout + k * c, dout + k * c, c, hipMemcpyDeviceToHost, b);
+            }
+        (void)hipStreamSynchronize(a);
+        (void)hipStreamSynchronize(b);
+        return (double)c * chunks * reps / (now_s() - t0) / 1e9;
+    };
+    run(true, true);   // warm
+    out[0] = run(true, false);
+    out[1] = run(false, true);
+    const double both = run(true, true);   // each direction moved the same bytes in that time
+    out[2] = out[3] = both;
+    (void)hipStreamDestroy(a); (void)hipStreamDestroy(b);
+    (void)hipFree(din); (void)hipFree(dout); (void)hipHostFree(hin); (void)hipHostFree(hout);
     return TM_OK;
 }
 

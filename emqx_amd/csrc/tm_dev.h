@@ -18,7 +18,6 @@ struct DevIndex {
     const uint16_t *xfp;
     const uint32_t *wseq;
     const uint32_t *wbits; uint32_t wcap;   // wide nodes' child bitmaps, bits per bitmap (tm_layout.h WIDE_LIT)
-    const uint32_t *cinfo;                  // slot for slot with ctab: the child's child table (ctab_enc)
     // A walk needs a topic's level words only down to the trie's depth (no node
     // deeper than `depth` exists), unless a binary key of the topic's length
     // exists (xlen_mask bit L for L < 64, L <= xlen_max beyond): need_levels().
@@ -111,7 +110,7 @@ hipError_t launch_copy_values(const uint64_t *hit_offs, uint64_t n, const uint32
 // delta upload: run i copies runs[i].n u32 words from data + runs[i].src to
 // word (dst & PATCH_OFF) of table (dst >> 48), whose device address on the
 // replica being patched is bases.b[table] (the same runs patch every replica)
-constexpr int N_TABLES = 10;  // vocab, wpool, nodes, ctab, vals, exact, xfp, wseq, wbits, cinfo
+constexpr int N_TABLES = 9;   // vocab, wpool, nodes, ctab, vals, exact, xfp, wseq, wbits
 constexpr uint64_t PATCH_OFF = (1ull << 48) - 1;
 struct PatchRun { uint64_t dst; uint32_t src, n; };
 struct PatchBases { uint64_t b[N_TABLES]; };

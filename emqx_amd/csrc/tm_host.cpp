@@ -151,7 +151,6 @@ struct tm_index {
     Mirror<uint8_t> wpool; uint64_t wpool_dead = 0;   // bytes of erased long words (compacted later)
     Mirror<Node> nodes; std::vector<NodeAux> aux; std::vector<uint32_t> free_nodes; uint64_t live_nodes = 0;
     Mirror<CSlot> ctab; std::vector<uint32_t> free_ctab[33]; uint64_t nlinks = 0, ntables = 0;
-    Mirror<uint32_t> cinfo;   // slot for slot with ctab: the child's own child table (tm_layout.h ctab_enc)
     Mirror<uint32_t> vals; std::vector<uint32_t> free_blocks[33];
     Mirror<ExactEntry> exact; std::vector<uint32_t> xcap, xroff; uint64_t xcount = 0;
     Mirror<uint16_t> xfp;   // exact-table fingerprints, slot for slot (0 = empty)
@@ -386,10 +385,9 @@ uint32_t ctab_alloc(tm_index *ix, uint32_t cap) {
     auto &fl = ix->free_ctab[cls_of(cap)];
     uint32_t o;
     if (!fl.empty()) { o = fl.back(); fl.pop_back(); }
-    else { o = (uint32_t)ix->ctab.h.size(); ix->ctab.h.resize(o + cap); ix->cinfo.h.resize(o + cap, NONE); }
-    for (uint32_t i = 0; i < cap; i++) { ix->ctab.h[o + i] = CSlot{NONE, NONE, 0, 0}; ix->cinfo.h[o + i] = NONE; }
+    else { o = (uint32_t)ix->ctab.h.size(); ix->ctab.h.resize(o + cap); }
+    for (uint32_t i = 0; i < cap; i++) ix->ctab.h[o + i] = CSlot{NONE, NONE, 0, 0};
     ix->ctab.touch(o, cap);
-    ix->cinfo.touch(o, cap);
     ix->ntables++;
     return o;
 }
@@ -399,15 +397,11 @@ void ctab_free(tm_index *ix, uint32_t off, uint32_t cap) {
     ix->ntables--;
 }
 
-uint32_t child_tab_enc(tm_index *ix, uint32_t node);
-
 void ctab_put(tm_index *ix, uint32_t off, uint32_t mask, uint32_t wid, uint32_t child, uint64_t sum) {
     for (uint32_t s = child_hash(wid) & mask;; s = (s + 1) & mask)
         if (ix->ctab.h[off + s].wid == NONE) {
             ix->ctab.h[off + s] = CSlot{wid, child, (uint32_t)sum, (uint32_t)(sum >> 32)};
-            ix->cinfo.h[off + s] = child_tab_enc(ix, child);
             ix->ctab.touch(off + s);
-            ix->cinfo.touch(off + s);
             return;
         }
 }
@@ -428,18 +422,10 @@ void ctab_erase(tm_index *ix, uint32_t off, uint32_t mask, uint32_t wid) {
     for (uint32_t j = (i + 1) & mask; t[j].wid != NONE; j = (j + 1) & mask) {
         uint32_t k = child_hash(t[j].wid) & mask;
         bool stays = (i <= j) ? (i < k && k <= j) : (i < k || k <= j);
-        if (!stays) {
-            t[i] = t[j];
-            ix->cinfo.h[off + i] = ix->cinfo.h[off + j];
-            ix->ctab.touch(off + i);
-            ix->cinfo.touch(off + i);
-            i = j;
-        }
+        if (!stays) { t[i] = t[j]; ix->ctab.touch(off + i); i = j; }
     }
     t[i] = CSlot{NONE, NONE, 0, 0};
-    ix->cinfo.h[off + i] = NONE;
     ix->ctab.touch(off + i);
-    ix->cinfo.touch(off + i);
 }
 
 // ------------------------------------------------------------- value runs
@@ -674,26 +660,6 @@ void summary_refresh1(tm_index *ix, uint32_t x) {
     }
 }
 
-// a table-mode node's child table as its parent's cinfo slot carries it
-// (tm_layout.h ctab_enc), NONE for an inline-mode node
-uint32_t child_tab_enc(tm_index *ix, uint32_t node) {
-    const Node &n = ix->nodes.h[node];
-    return nlit_of(n) > KINL ? ctab_enc(n.kw[0], n.kw[1]) : NONE;
-}
-
-// node's child table moved or went (to_table, back to inline): refresh the
-// cinfo slot its parent's table keeps for it
-void cinfo_refresh(tm_index *ix, uint32_t node) {
-    if (node == ROOT || ix->aux[node].is_plus) return;
-    const uint32_t p = ix->aux[node].parent;
-    const Node &pn = ix->nodes.h[p];
-    if (nlit_of(pn) <= KINL) return;
-    const uint32_t sl = ctab_find(ix, pn.kw[0], pn.kw[1], ix->aux[node].wid);
-    if (sl == NONE) return;
-    const uint32_t e = child_tab_enc(ix, node);
-    if (ix->cinfo.h[pn.kw[0] + sl] != e) { ix->cinfo.h[pn.kw[0] + sl] = e; ix->cinfo.touch(pn.kw[0] + sl); }
-}
-
 // move a node's children into a private table of `cap` slots (cap = pow2)
 void to_table(tm_index *ix, uint32_t node, uint32_t cap) {
     Node &n = ix->nodes.h[node];
@@ -737,7 +703,6 @@ void child_add(tm_index *ix, uint32_t node, uint32_t wid, uint32_t child) {
     if (nlit_of(*n) == WIDE_LIT && ix->aux[node].bm == NONE) { to_wide(ix, node); n = &ix->nodes.h[node]; }
     ix->nodes.touch(node);
     summary_refresh(ix, node);
-    if (nlit_of(*n) > KINL) cinfo_refresh(ix, node);   // (its table may have moved or just appeared)
 }
 
 void child_remove(tm_index *ix, uint32_t node, uint32_t wid) {
@@ -757,7 +722,6 @@ void child_remove(tm_index *ix, uint32_t node, uint32_t wid) {
             for (uint32_t i = 0; i <= n.kw[1]; i++) if (ix->ctab.h[n.kw[0] + i].wid != NONE) kids.push_back(ix->ctab.h[n.kw[0] + i]);
             ctab_free(ix, n.kw[0], n.kw[1] + 1);
             for (uint32_t k = 0; k < KINL; k++) { n.kw[k] = kids[k].wid; n.kc[k] = kids[k].child; }
-            cinfo_refresh(ix, node);
         }
     }
     ix->nodes.touch(node);
@@ -1131,7 +1095,7 @@ int collect(tm_index *ix, Mirror<T> &m, uint32_t table, std::vector<PatchRun> &r
 PatchBases patch_bases(tm_index *ix, int r) {
     PatchBases b;
     const void *t[N_TABLES] = {ix->vocab.d[r], ix->wpool.d[r], ix->nodes.d[r], ix->ctab.d[r], ix->vals.d[r],
-                               ix->exact.d[r], ix->xfp.d[r], ix->wseq.d[r], ix->wbits.d[r], ix->cinfo.d[r]};
+                               ix->exact.d[r], ix->xfp.d[r], ix->wseq.d[r], ix->wbits.d[r]};
     for (int i = 0; i < N_TABLES; i++) b.b[i] = reinterpret_cast<uint64_t>(t[i]);
     return b;
 }
@@ -1177,7 +1141,6 @@ int sync_locked(tm_index *ix, int r0, hipStream_t s) {
     if ((rc = collect(ix, ix->xfp, 6, runs, data))) return rc;
     if ((rc = collect(ix, ix->wseq, 7, runs, data))) return rc;
     if ((rc = collect(ix, ix->wbits, 8, runs, data))) return rc;
-    if ((rc = collect(ix, ix->cinfo, 9, runs, data))) return rc;
     const uint64_t nr = runs.size(), nw = data.size();
     if (nr) {
         // staging: [runs | data] in one pinned buffer, one H2D copy + one kernel per replica
@@ -1242,7 +1205,6 @@ DevIndex dev_view(tm_index *ix, int r) {
     d.xfp = ix->xfp.d[r];
     d.wseq = ix->wseq.d[r];
     d.wbits = ix->wbits.d[r]; d.wcap = ix->wide.empty() ? 0 : ix->wb_words * 32;
-    d.cinfo = ix->cinfo.d[r];
     // levels a walk must resolve: the deepest live node's depth (no node below
     // it has children), all of a topic's levels when a binary key has its length
     auto &dc = ix->depth_cnt, &xc = ix->xlen_cnt;
@@ -1532,7 +1494,7 @@ int tm_destroy(tm_index *ix) {
         Replica &R = ix->rep[r];
         (void)hipSetDevice(R.device);
         void *bufs[] = {ix->vocab.d[r], ix->wpool.d[r], ix->nodes.d[r], ix->ctab.d[r], ix->vals.d[r], ix->exact.d[r],
-                        ix->xfp.d[r], ix->wseq.d[r], ix->wbits.d[r], ix->cinfo.d[r]};
+                        ix->xfp.d[r], ix->wseq.d[r], ix->wbits.d[r]};
         for (void *p : bufs) if (p) (void)hipFree(p);
         for (int i = 0; i < PATCH_RING; i++) {
             if (R.pdev[i]) (void)hipFree(R.pdev[i]);
@@ -2283,7 +2245,7 @@ int tm_stats(tm_index *ix, tm_stats_t *o) {
     o->n_words = ix->vcount;
     o->device_bytes = ix->vocab.dcap * sizeof(VocabEntry)   /* per replica */ + ix->wpool.dcap + ix->nodes.dcap * sizeof(Node) +
                       ix->ctab.dcap * sizeof(CSlot) + ix->vals.dcap * 4 + ix->exact.dcap * sizeof(ExactEntry) + ix->xfp.dcap * 2 +
-                      ix->wseq.dcap * 4 + ix->wbits.dcap * 4 + ix->cinfo.dcap * 4;
+                      ix->wseq.dcap * 4 + ix->wbits.dcap * 4;
     o->uploads = ix->uploads;
     o->patch_bytes = ix->patch_bytes;
     return TM_OK;

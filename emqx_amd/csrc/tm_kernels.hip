@@ -1058,9 +1058,16 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_small(DevIndex ix, Workspace 
     __shared__ uint32_t s_vb, s_fail;
     constexpr uint32_t TBQ = SM_TB / 16 + 1;              // 16-B chunks of a topic staged in LDS
     __shared__ uint4 s_tb[SM_TOPICS][TBQ];
+    __shared__ uint64_t s_off[SM_TOPICS + 1];
+    __shared__ uint8_t s_err[SM_TOPICS];
     if (threadIdx.x == 0) s_vb = atomicAdd(&ws.list_n[L_COUNT + 4], 1u);   // blocks scan in start order
     __syncthreads();
     const uint32_t vb = s_vb;
+    // the block's SM_TOPICS + 1 topic offsets, read once by one wave (the
+    // caller's buffers may be host memory: one coalesced read, not one per group)
+    if (threadIdx.x <= SM_TOPICS && (uint64_t)vb * SM_TOPICS + threadIdx.x <= n)
+        s_off[threadIdx.x] = offs[(uint64_t)vb * SM_TOPICS + threadIdx.x];
+    __syncthreads();
     const Group<W> grp;
     const uint32_t wv = threadIdx.x >> 6, gl = grp.gl, base = grp.g * W;
     const uint32_t gi = wv * G + grp.g;                   // topic slot in the block
@@ -1068,7 +1075,7 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_small(DevIndex ix, Workspace 
     const bool live = t < n;
     uint32_t *sl_ = s_slash[wv] + base, *sn_ = s_node[wv] + base, *hoff = s_hoff[wv] + base, *hcnt = s_hcnt[wv] + base;
     uint64_t *sc_ = s_code[wv] + base, *hcode = s_hcode[wv] + base;
-    const uint64_t beg = live ? offs[t] : 0, end = live ? offs[t + 1] : 0, len = end - beg;
+    const uint64_t beg = live ? s_off[gi] : 0, end = live ? s_off[gi + 1] : 0, len = end - beg;
 
     // ---- the topic into LDS: one round of 16-B loads by the group's lanes
     // (the caller's buffers may be host memory read over PCIe: every byte
@@ -1234,7 +1241,10 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_small(DevIndex ix, Workspace 
     }
 
     // ---- the block's offset: exclusive scan of its 16 counts + decoupled look-back
-    if (gl == 0) s_cnt[gi] = live ? total : 0;
+    if (gl == 0) {
+        s_cnt[gi] = live ? total : 0;
+        s_err[gi] = fb ? (frc == RC_BADARG ? 1 : frc == RC_DEEP ? 2 : 0) : badarg;
+    }
     __syncthreads();
     if (wv == 0) {
         const uint32_t lane = threadIdx.x;
@@ -1280,13 +1290,16 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_small(DevIndex ix, Workspace 
         }
     }
     __syncthreads();
+    // the block's hit offsets and flags: lanes 0..15 of wave 0, one coalesced store each
+    if (threadIdx.x < SM_TOPICS && (uint64_t)vb * SM_TOPICS + threadIdx.x < n) {
+        uint64_t p = s_base;
+        for (uint32_t i = 0; i < threadIdx.x; i++) p += s_cnt[i];
+        hit_offs[(uint64_t)vb * SM_TOPICS + threadIdx.x] = p;
+        o.err[(uint64_t)vb * SM_TOPICS + threadIdx.x] = s_fail ? 4 : s_err[threadIdx.x];
+    }
     if (!live) return;
     uint64_t pos = s_base;
     for (uint32_t i = 0; i < gi; i++) pos += s_cnt[i];
-    if (gl == 0) {
-        hit_offs[t] = pos;
-        o.err[t] = s_fail ? 4 : fb ? (frc == RC_BADARG ? 1 : frc == RC_DEEP ? 2 : 0) : badarg;
-    }
     if (s_fail) return;
 
     // ---- the values, straight into the CSR
@@ -1305,13 +1318,13 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_small(DevIndex ix, Workspace 
         roff[rank] = hoff[gl]; rcnt[rank] = hcnt[gl]; rpos[rank] = pos + before;
     }
     wave_sync();
+    // single-value runs (C3: almost every hit): lane r writes the one ranked r --
+    // consecutive positions, so the group's inline hits leave in one store
+    if (gl < nh && (rcnt[gl] & RUN_INLINE) && rpos[gl] < cap) out[rpos[gl]] = roff[gl];
     for (uint32_t r = 0; r < nh; r++) {
         const uint32_t ro = roff[r], rc = rcnt[r];
         const uint64_t P = rpos[r];
-        if (rc & RUN_INLINE) {
-            if (gl == 0 && P < cap) out[P] = ro;
-            continue;
-        }
+        if (rc & RUN_INLINE) continue;
         for (uint32_t k = gl; k < (rc & RUN_CNT); k += W)
             if (P + k < cap) out[P + k] = ix.vals[ro + k];
     }

@@ -166,20 +166,6 @@ TM_HD uint32_t psum_bit(uint32_t h) { return ((h >> 16) * PSUM_BLOOM) >> 16; }  
 // Bloom word j (bits 32j .. 32j+31) of a table-mode node line
 TM_HD uint32_t &bloom_word(Node &n, uint32_t j) { return j < 2 ? n.kw[2 + j] : n.kc[j - 2]; }
 
-// A child table as its parent's slot can carry it (DevIndex::cinfo, slot for
-// slot with ctab): offset (27 bits) and log2 of the size (5 bits), so a walk
-// that found child C in its parent's table can probe C's own table for the
-// next word in the same round trip as C's node line.  NONE: C is inline-mode
-// (or its table lies beyond 2^27 slots).
-TM_HD uint32_t ctab_enc(uint32_t off, uint32_t mask) {
-    if (off >= (1u << 27)) return NONE;
-    uint32_t lg = 0;
-    while ((2u << lg) <= mask + 1 && lg < 31) lg++;   // size = mask + 1 = 2^lg
-    return lg << 27 | off;
-}
-TM_HD uint32_t ctab_enc_off(uint32_t e) { return e & ((1u << 27) - 1); }
-TM_HD uint32_t ctab_enc_mask(uint32_t e) { return (1u << (e >> 27)) - 1; }
-
 // exact-table fingerprint of a wid-sequence hash (never 0: 0 marks an empty slot)
 TM_HD uint16_t exact_fp(uint64_t h) { return (uint16_t)((h >> 48) | 1u); }
 

@@ -22,8 +22,13 @@ nothing (a key deleted meanwhile is dropped) -- never to a key inserted later.
 Result order: the device returns keys in traversal order (ascending Erlang
 term order).  ``matches/3`` returns them like the reference does -- reversed,
 because match_add/2 prepends (emqx_trie_search.erl:350-356); ``[unique]``
-keeps the last key per ID (maps:values, sorted by ID as small maps are);
-``match/2`` is the first key in traversal order.
+keeps the last key per ID (maps:values): for up to 32 IDs that is the
+reference's list element for element (a flatmap iterates in key term order);
+beyond 32 the BEAM iterates a HAMT in the order of its internal term hash,
+which this mirror does not restate, so the list is the same set of keys in
+ID term order (the Erlang module, src/emqx_topic_index_gpu.erl, calls
+maps:values itself and is exact); ``match/2`` is the first key in traversal
+order.
 """
 from __future__ import annotations
 

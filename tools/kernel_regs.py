@@ -7,7 +7,7 @@ import subprocess
 import sys
 from pathlib import Path
 
-src = Path(__file__).resolve().parent.parent / "emqx_amd" / "csrc" / "tm_kernels.hip"
+src = Path(sys.argv.pop(1)) if len(sys.argv) > 1 and sys.argv[1].endswith(".hip") else Path(__file__).resolve().parent.parent / "emqx_amd" / "csrc" / "tm_kernels.hip"
 r = subprocess.run(["hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "-c", "-o", "/dev/null", str(src),
                     "-Rpass-analysis=kernel-resource-usage"] + sys.argv[1:], capture_output=True, text=True)
 name, rows = None, {}
