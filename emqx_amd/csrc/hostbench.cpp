@@ -80,9 +80,19 @@ struct Caller {
             return TM_EDEVICE;
         return TM_OK;
     }
+    // mode 2: inputs in HBM, outputs in the mapped host buffers; mode 3: the
+    // reverse (which PCIe leg of an in-place batch costs what)
+    int mode = 1;
+    template <class T> static T *mapped(T *hp) {
+        void *d = nullptr;
+        return hipHostGetDevicePointer(&d, hp, 0) == hipSuccess ? static_cast<T *>(d) : nullptr;
+    }
     int run() {
         if (!s) return api::match_batch(h, n, blob, offs, hit, vals, cap, err);
-        int rc = api::match_batch_dev(h, n, dblob, doffs, dhit, dvals, cap, derr, s);
+        const bool hin = mode == 3, hout = mode == 2;
+        int rc = api::match_batch_dev(h, n, hin ? mapped(blob) : dblob, hin ? mapped(offs) : doffs,
+                                      hout ? mapped(hit) : dhit, hout ? mapped(vals) : dvals, cap,
+                                      hout ? mapped(err) : derr, s);
         if (rc) return rc;
         return hipStreamSynchronize(s) == hipSuccess ? TM_OK : TM_EDEVICE;
     }
@@ -137,7 +147,9 @@ int tmb_single(tm_index *h, uint64_t n, const uint8_t *tb, const uint64_t *to, u
 // [k n, (k + 1) n) of the set, which must hold nthreads * n); one churn thread
 // applies `churn_ops` deltas per millisecond (0: none).  device_buffers: each
 // caller's batch lives in HBM and goes through tm_match_batch_dev on its own
-// stream (what the device can take without the PCIe leg of in-place batches).
+// stream (what the device can take without the PCIe leg of in-place batches);
+// 2: inputs in HBM, outputs written into the mapped host buffers; 3: inputs
+// read from the mapped host buffers, outputs in HBM.
 // out: [batches, topics_per_s, p50_ms, p99_ms, deltas_per_s, seconds]
 int tmb_callers_ex(tm_index *h, int nthreads, uint64_t n, const uint8_t *tb, const uint64_t *to, uint64_t cap,
                    double seconds, int churn_ops, int device_buffers, double *out) {
@@ -146,6 +158,7 @@ int tmb_callers_ex(tm_index *h, int nthreads, uint64_t n, const uint8_t *tb, con
         int rc = cs[k].init(h, n, tb, to, (uint64_t)k * n, cap);
         if (rc) return rc;
         if (device_buffers && (rc = cs[k].to_device())) return rc;
+        cs[k].mode = device_buffers;
         if ((rc = cs[k].run())) return rc;   // warm: lane, workspace
     }
     std::atomic<bool> stop{false};

@@ -1160,7 +1160,9 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_small(DevIndex ix, Workspace 
                 lit = n2.x == wl_ ? n3.x : n2.y == wl_ ? n3.y : n2.z == wl_ ? n3.z : n2.w == wl_ ? n3.w : NONE;
             } else {
                 const uint32_t h = child_hash(wl_);
-                const uint32_t mb = child_maybe(ix, n1, n2, n3, wl_, h);
+                // a wide node's bitmap line would be one more round trip before
+                // the probe: at a small batch's load the probe itself is cheaper
+                const uint32_t mb = (n1.y & NLIT_MASK) >= WIDE_LIT ? 1u : child_maybe(ix, n1, n2, n3, wl_, h);
                 if (mb & 1u) {
                     uint32_t slo, shi;
                     lit = ctab_find(ix, n2.x, n2.y, wl_, h, slo, shi);

@@ -442,6 +442,36 @@ def test_c3_scale_properties(torch_dev):
         assert nf not in g and nf + 1 not in g
 
 
+def test_c3_full_size_sample(torch_dev):
+    """The headline configuration itself (BASELINE.json configs[2]: C3 at
+    10,000,002 filters, 1M-topic batches): a 20k-topic sample of the batch
+    exact against the oracle over all 10M keys (values and order), the whole
+    batch deterministic, and '$SYS' topics never hitting the root globals."""
+    nf = 10_000_000
+    fs = wl.filters(3, nf)
+    ts = wl.topics(3, nf, 1_000_000)
+    ix = _native.Index(hint_keys=len(fs))
+    for lo in range(0, len(fs), 2_000_000):
+        part = fs.slice(lo, min(lo + 2_000_000, len(fs)))
+        ix.apply(np.ones(len(part), np.uint8), part.blob, part.offs, part.vals)
+    assert ix.stats()["n_keys"] == len(fs)
+    hit, vals, err = ix.match_batch(ts.blob, ts.offs)
+    hit2, vals2, _ = ix.match_batch(ts.blob, ts.offs)
+    assert np.array_equal(hit, hit2) and np.array_equal(vals, vals2)
+    assert not err.any()
+    o = oracle_of(fs)
+    idx = np.random.default_rng(11).choice(len(ts), 20_000, replace=False)
+    sample = items_of([ts.item(int(i)) for i in idx])
+    cnt, _, ohit, ovals = o.match_batch(sample.blob, sample.offs)
+    assert (cnt >= 0).all()
+    for j, i in enumerate(idx):
+        assert np.array_equal(vals[int(hit[i]):int(hit[i + 1])], ovals[int(ohit[j]):int(ohit[j + 1])]), ts.item(int(i))
+    for i in range(0, len(ts), 97):
+        if ts.item(i).startswith(b"$"):
+            g = vals[int(hit[i]):int(hit[i + 1])]
+            assert nf not in g and nf + 1 not in g
+
+
 def test_child_table_grow_and_shrink(torch_dev):
     """A node going inline (<= 4 children) -> private table -> bigger tables ->
     back to inline, with matches checked against the oracle at every stage."""
