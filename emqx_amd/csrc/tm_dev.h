@@ -74,6 +74,7 @@ constexpr int TILE = 256;    // topics per walk block = per scan tile = per emit
 constexpr int LIST_SLOTS = L_COUNT + 5;   // Workspace::list_n entries
 constexpr int SM_TOPICS = 16;             // topics per block of the one-launch small-batch path
 constexpr int SM_TB = 256;                // topic bytes it stages in LDS (longer topics: the lane walk)
+constexpr int SM_VSTAGE = 1024;           // values of a block it stages in LDS before one contiguous write
 
 
 // Pipeline entry points (tm_kernels.hip).  All asynchronous on `s`.

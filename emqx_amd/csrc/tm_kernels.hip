@@ -1024,8 +1024,14 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_wave(DevIndex ix, Workspace w
 // MID_L levels (small_path_ok: the index never needs more); the block's 16
 // hit counts get their global offset from a single-pass decoupled look-back
 // scan over the blocks in the order they started (a ticket, so a block only
-// ever waits for blocks already running); then each group copies its values
-// straight into the CSR.  No range lists, no device-side lists, no other kernel.
+// ever waits for blocks already running); then each group puts its values in
+// the block's LDS span, written out as one contiguous run (or, for a block
+// whose values do not fit or that holds a lane-walked topic, straight into the
+// CSR).  The caller's buffers may be host memory (in-place host batches): the
+// block reads its offsets and its whole topic byte span once each, and writes
+// its offsets, flags and values as contiguous runs -- a few whole PCIe
+// transactions per block instead of several per topic.  No range lists, no
+// device-side lists, no other kernel.
 struct CountEmit {          // one-launch path: hit count only (the values come from a re-walk)
     uint64_t cnt;
     __device__ __forceinline__ bool operator()(uint32_t, uint32_t n) { cnt += n & RUN_CNT; return true; }
@@ -1057,9 +1063,17 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_small(DevIndex ix, Workspace 
     __shared__ uint64_t s_base;
     __shared__ uint32_t s_vb, s_fail;
     constexpr uint32_t TBQ = SM_TB / 16 + 1;              // 16-B chunks of a topic staged in LDS
-    __shared__ uint4 s_tb[SM_TOPICS][TBQ];
+    constexpr uint32_t TBQ_ALL = SM_TOPICS * TBQ;
+    // topic bytes in LDS: the block's whole byte span in one cooperative round
+    // of 16-B loads when it fits (each chunk read once -- consecutive topics
+    // share the chunk at their boundary), else one row per topic
+    __shared__ uint4 s_tb[TBQ_ALL];
     __shared__ uint64_t s_off[SM_TOPICS + 1];
-    __shared__ uint8_t s_err[SM_TOPICS];
+    __shared__ uint8_t s_err[SM_TOPICS], s_fbk[SM_TOPICS];
+    // the block's values staged in LDS and written as one contiguous span
+    // (in place batches: a few whole PCIe writes instead of one per group)
+    __shared__ uint32_t s_vals[SM_VSTAGE];
+    __shared__ uint64_t s_sum;
     if (threadIdx.x == 0) s_vb = atomicAdd(&ws.list_n[L_COUNT + 4], 1u);   // blocks scan in start order
     __syncthreads();
     const uint32_t vb = s_vb;
@@ -1085,10 +1099,20 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_small(DevIndex ix, Workspace 
     const uint64_t a0 = beg & ~15ull;
     const uint32_t nq = live ? (uint32_t)((end - a0 + 15) >> 4) : 0;
     bool fb = nq > TBQ;   // the group's first lane walks this topic (lane walk, global reads)
-    if (!fb)
-        for (uint32_t c = gl; c < nq; c += W) s_tb[gi][c] = ld4_once(blob + a0 + 16ull * c);
-    wave_sync();
-    const uint8_t *tb = reinterpret_cast<const uint8_t *>(s_tb[gi]) + (beg - a0);   // topic byte i = tb[i]
+    const uint32_t nt = (uint64_t)vb * SM_TOPICS + SM_TOPICS <= n ? SM_TOPICS : (uint32_t)(n - (uint64_t)vb * SM_TOPICS);
+    const uint64_t B0 = s_off[0] & ~15ull;
+    const uint64_t nqb = (s_off[nt] - B0 + 15) >> 4;
+    const bool span = nqb <= TBQ_ALL;                     // (block-uniform)
+    if (span) {
+        for (uint32_t c = threadIdx.x; c < nqb; c += WV_BLOCK) s_tb[c] = ld4_once(blob + B0 + 16ull * c);
+        __syncthreads();
+    } else {
+        if (!fb)
+            for (uint32_t c = gl; c < nq; c += W) s_tb[gi * TBQ + c] = ld4_once(blob + a0 + 16ull * c);
+        wave_sync();
+    }
+    const uint8_t *tb = span ? reinterpret_cast<const uint8_t *>(s_tb) + (live ? beg - B0 : 0)   // topic byte i = tb[i]
+                             : reinterpret_cast<const uint8_t *>(s_tb + gi * TBQ) + (beg - a0);
     const uint64_t tlen = fb ? 0 : len;
 
     // ---- the wave walk (k_walk_wave), falling back instead of listing
@@ -1246,6 +1270,7 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_small(DevIndex ix, Workspace 
     if (gl == 0) {
         s_cnt[gi] = live ? total : 0;
         s_err[gi] = fb ? (frc == RC_BADARG ? 1 : frc == RC_DEEP ? 2 : 0) : badarg;
+        s_fbk[gi] = live && fb;
     }
     __syncthreads();
     if (wv == 0) {
@@ -1282,6 +1307,7 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_small(DevIndex ix, Workspace 
         }
         if (lane == 0) {
             s_fail = fail;
+            s_sum = sum;
             __hip_atomic_store(&ws.look[vb], lb_word(tag, LB_INCL, pre + sum), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
             s_base = pre;
@@ -1299,36 +1325,48 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_small(DevIndex ix, Workspace 
         hit_offs[(uint64_t)vb * SM_TOPICS + threadIdx.x] = p;
         o.err[(uint64_t)vb * SM_TOPICS + threadIdx.x] = s_fail ? 4 : s_err[threadIdx.x];
     }
-    if (!live) return;
-    uint64_t pos = s_base;
+    if (s_fail) return;   // (block-uniform)
+    // stage the block's values in LDS when they fit and no topic of the block
+    // took the lane walk (which writes its values itself)
+    bool stage = s_sum <= SM_VSTAGE;
+    for (uint32_t i = 0; i < SM_TOPICS; i++) stage &= !s_fbk[i];
+    const uint64_t b0 = s_base;
+    uint64_t pos = b0;
     for (uint32_t i = 0; i < gi; i++) pos += s_cnt[i];
-    if (s_fail) return;
+    auto put = [&](uint64_t P, uint32_t v) {
+        if (stage) s_vals[P - b0] = v;
+        else if (P < cap) out[P] = v;
+    };
 
-    // ---- the values, straight into the CSR
-    if (fb) {
-        if (gl == 0 && frc == RC_OK) {
+    // ---- the values
+    if (live && fb) {
+        if (gl == 0 && frc == RC_OK) {   // (never with stage)
             DirectEmit em{ix.vals, out, pos, cap};
             match_topic(ix, blob, beg, end, st, em);
         }
-        return;
+    } else if (live) {
+        uint32_t *roff = s_roff[wv] + base, *rcnt = s_rcnt[wv] + base;
+        uint64_t *rpos = s_rpos[wv] + base;
+        if (hv) {
+            uint64_t before = 0;   // values of the hits ranked before this one
+            for (uint32_t j = 0; j < nh; j++) if (hcode[j] < my) before += hcnt[j] & RUN_CNT;
+            roff[rank] = hoff[gl]; rcnt[rank] = hcnt[gl]; rpos[rank] = pos + before;
+        }
+        wave_sync();
+        // single-value runs (C3: almost every hit): lane r writes the one ranked r
+        if (gl < nh && (rcnt[gl] & RUN_INLINE)) put(rpos[gl], roff[gl]);
+        for (uint32_t r = 0; r < nh; r++) {
+            const uint32_t ro = roff[r], rc = rcnt[r];
+            const uint64_t P = rpos[r];
+            if (rc & RUN_INLINE) continue;
+            for (uint32_t k = gl; k < (rc & RUN_CNT); k += W) put(P + k, ix.vals[ro + k]);
+        }
     }
-    uint32_t *roff = s_roff[wv] + base, *rcnt = s_rcnt[wv] + base;
-    uint64_t *rpos = s_rpos[wv] + base;
-    if (hv) {
-        uint64_t before = 0;   // values of the hits ranked before this one
-        for (uint32_t j = 0; j < nh; j++) if (hcode[j] < my) before += hcnt[j] & RUN_CNT;
-        roff[rank] = hoff[gl]; rcnt[rank] = hcnt[gl]; rpos[rank] = pos + before;
-    }
-    wave_sync();
-    // single-value runs (C3: almost every hit): lane r writes the one ranked r --
-    // consecutive positions, so the group's inline hits leave in one store
-    if (gl < nh && (rcnt[gl] & RUN_INLINE) && rpos[gl] < cap) out[rpos[gl]] = roff[gl];
-    for (uint32_t r = 0; r < nh; r++) {
-        const uint32_t ro = roff[r], rc = rcnt[r];
-        const uint64_t P = rpos[r];
-        if (rc & RUN_INLINE) continue;
-        for (uint32_t k = gl; k < (rc & RUN_CNT); k += W)
-            if (P + k < cap) out[P + k] = ix.vals[ro + k];
+    if (stage) {   // (block-uniform)
+        __syncthreads();
+        const uint32_t m = (uint32_t)s_sum;
+        for (uint32_t i = threadIdx.x; i < m; i += WV_BLOCK)
+            if (b0 + i < cap) out[b0 + i] = s_vals[i];
     }
 }
 

@@ -609,6 +609,41 @@ def test_host_batches_in_place_pinned_buffers(torch_dev):
         ix.host_free(np.zeros(4, np.uint8))
 
 
+def test_one_launch_staging_branches(torch_dev):
+    """k_walk_small's block-level staging, each branch against the oracle:
+    topic bytes as one block span (short topics) or per-topic rows (a block
+    whose span exceeds the LDS buffer), topics past SM_TB bytes on the lane
+    walk; values through the block's LDS span (a few hits per topic), straight
+    into the CSR (C2: ~1,000 values per topic, more than the block stages) and
+    around a lane-walked topic in the block; all of it in place in
+    tm_host_alloc buffers and from pageable memory."""
+    fs = wl.filters(2, 20_000)
+    ix, o = gpu_index(fs), oracle_of(fs)
+    assert_same(ix, o, wl.topics(2, 20_000, 300))              # direct: ~1,000 values per topic
+    fs3 = wl.filters(3, 50_000)
+    ix3, o3 = gpu_index(fs3), oracle_of(fs3)
+    ts = wl.topics(3, 50_000, 5000)
+    assert_same(ix3, o3, ts)                                   # one byte span per block, staged values
+    r = random.Random(3)
+    items = [ts.item(i) for i in range(600)]
+    long_ = [b"/".join(b"%030d" % r.randrange(10**9) for _ in range(9)) for _ in range(40)]   # 279 B
+    mid = [b"/".join(b"%028d" % r.randrange(10**9) for _ in range(8)) for _ in range(40)]     # 231 B
+    mixed = items[:200] + mid + items[200:400] + long_ + items[400:]
+    for order in (mixed, mid * 3 + items[:50], long_ + items[:100]):
+        t = items_of(order)
+        hit, vals = assert_same(ix3, o3, t)
+        nb = int(t.offs[-1])
+        pb, po = ix3.host_array(nb + 32, np.uint8), ix3.host_array(len(t) + 1, np.uint64)
+        ph, pv, pe = (ix3.host_array(len(t) + 1, np.uint64), ix3.host_array(len(vals) + 5, np.uint32),
+                      ix3.host_array(len(t), np.uint8))
+        pb[:nb] = t.blob[:nb]
+        po[:] = t.offs
+        h2, v2, e2 = ix3.match_batch(pb, po, out=(ph, pv, pe))
+        assert np.array_equal(h2, hit) and np.array_equal(v2, vals) and not e2.any()
+        for a_ in (pb, po, ph, pv, pe):
+            ix3.host_free(a_)
+
+
 def test_mixed_batch_sizes_and_modes_in_sequence(torch_dev):
     """Tile totals stay zero between batches (k_emit clears them; the wave walk
     adds into them, the lane walk overwrites them, the small-batch tail kernel
