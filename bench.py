@@ -82,9 +82,12 @@ def parse():
                    help="c5: deltas applied per step (100 x ~2.5k steps/s = 2.5x the configured 100k deltas/s)")
     p.add_argument("--streams", type=int, default=None,
                    help="HIP streams the steps rotate over (batch k+1's walk overlaps batch k's scan/emit); "
-                        "default 3, and 1 for c5: a churn step's patch waits for every batch in flight, so "
-                        "its steps cannot overlap and a second stream only adds cross-stream waits "
-                        "(0.41 vs 0.54-0.64 ms per step measured)")
+                        "default 3, and 1 for c5 with one copy of the tables: a churn step's patch then waits "
+                        "for every batch in flight, so its steps cannot overlap and a second stream only adds "
+                        "cross-stream waits (0.41 vs 0.54-0.64 ms per step measured in round 2)")
+    p.add_argument("--copies", type=int, default=1,
+                   help="copies of the tables on the GPU (tm_options.copies): a batch after a delta runs on a "
+                        "copy no batch is reading (measured: no gain on c5 or churned callers, DESIGN.md 3)")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     p.add_argument("--cpu-threads", type=int, default=None,
                    help="CPU baseline threads (default: the CPUs this process may use)")
@@ -176,7 +179,8 @@ def main():
     log(f"[rank {rank}] generated {len(fs)} filters in {t_gen:.1f}s")
 
     t = time.time()
-    ix = _native.Index(device=local, hint_keys=len(fs))
+    copies = a.copies
+    ix = _native.Index(device=local, hint_keys=len(fs), copies=copies)
     chunk = 2_000_000
     for lo in range(0, len(fs), chunk):
         part = fs.slice(lo, min(lo + chunk, len(fs)))
@@ -213,7 +217,8 @@ def main():
     # one output set per stream: consecutive steps rotate over the streams, so
     # step k+1's walk overlaps step k's scan / emit (the library keeps one
     # workspace per stream and orders index patches across streams)
-    nstreams = 1 if filter_sharded else max(1, a.streams if a.streams is not None else (1 if a.config == "c5" else 3))
+    nstreams = 1 if filter_sharded else max(1, a.streams if a.streams is not None else
+                                            (1 if a.config == "c5" and copies == 1 else 3))
     streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(nstreams - 1)]
     outs = [{"hit": torch.zeros(B + 1, dtype=torch.int64, device=dev),
              "err": torch.zeros(B, dtype=torch.uint8, device=dev),
@@ -365,13 +370,15 @@ def main():
             lat_native[str(lb)] = {"p50_ms": round(out[0], 4), "p99_ms": round(out[1], 4), "mean_ms": round(out[2], 4)}
         if a.concurrency > 0:
             conc = []
-            for nth in (a.concurrency, 2 * a.concurrency):
+            # (threads, deltas per ms from one more thread): without churn, then with
+            for nth, churn in ((a.concurrency, 0), (a.concurrency, 256), (2 * a.concurrency, 256)):
                 lb = min(4096, B)
                 sub = ts.slice(0, nth * lb)
                 hh, _, _ = ix.match_batch(sub.blob, sub.offs)
                 cap = int(np.diff(hh.astype(np.int64)).reshape(nth, lb).sum(axis=1).max()) + 65536
                 out = (ctypes.c_double * 6)()
-                rc = hb.tmb_callers(ix._h, nth, lb, _native._ptr(sub.blob), _native._ptr(sub.offs), cap, 1.0, 256, out)
+                rc = hb.tmb_callers(ix._h, nth, lb, _native._ptr(sub.blob), _native._ptr(sub.offs), cap, 1.0, churn,
+                                    out)
                 assert rc == 0, rc
                 conc.append({"threads": nth, "topics_per_batch": lb, "batches": int(out[0]),
                              "topics_per_s": round(out[1], 1), "p50_ms": round(out[2], 4), "p99_ms": round(out[3], 4),
@@ -541,7 +548,7 @@ def main():
         "data": "synthetic (emqx_amd/csrc/workload.cpp, seed 0x454D5158+cfg)",
         "config": {"workload": f"{a.config}: {desc}", "filters": nf if (filter_sharded or level0) else len(fs),
                    "topics_per_gpu_step": B, "global_batch": topics_per_step, "parallelism": par,
-                   "streams": nstreams, "distinct_batches": R},
+                   "streams": nstreams, "distinct_batches": R, "table_copies": copies},
         "roofline": {"bound": "hbm", "achieved": None if achieved is None else round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": None if achieved is None else round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
@@ -571,7 +578,8 @@ def main():
                                                         " (every filter that can match a topic this rank owns: "
                                                         "the unsharded answer, order included)" if level0 else "")},
         "build": {"generate_s": round(t_gen, 1), "compile_s": round(t_compile, 1), "upload_s": round(t_upload, 2),
-                  "device_MiB": round(st["device_bytes"] / 2**20, 1), "nodes": st["n_nodes"],
+                  "device_MiB": round(st["device_bytes"] / 2**20, 1),
+                  "device_MiB_all_copies": round(copies * st["device_bytes"] / 2**20, 1), "nodes": st["n_nodes"],
                   "edges": st["n_edges"], "words": st["n_words"], "keys_this_rank": st["n_keys"],
                   "kernel_source_hash": source_hash()},
     }

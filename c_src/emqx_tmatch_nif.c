@@ -77,23 +77,32 @@ static ERL_NIF_TERM err_term(ErlNifEnv *env, int rc) {
     return enif_make_tuple2(env, A_ERROR, enif_make_int(env, rc));
 }
 
-/* new(Device | [Device]) -> {ok, Ref} | {error, Code}
-   A list: one host image with a replica on each device (tm_create_replicas). */
+/* new(Device | [Device] | {Device | [Device], Copies}) -> {ok, Ref} | {error, Code}
+   A list: one host image with a replica on each device (tm_create_replicas).
+   Copies: copies of the tables per device (tm_options.copies, 1..4): a batch
+   after a delta runs on a copy no batch is reading instead of waiting. */
 static ERL_NIF_TERM nif_new(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
-    int dev = -1, devs[8];
+    int dev = -1, devs[8], copies = 1, arity = 0;
     unsigned nd = 0;
+    const ERL_NIF_TERM *tup;
+    ERL_NIF_TERM spec = argv[0];
     (void)argc;
-    if (enif_get_list_length(env, argv[0], &nd)) {
-        ERL_NIF_TERM l = argv[0], h;
+    if (enif_get_tuple(env, argv[0], &arity, &tup)) {
+        if (arity != 2 || !enif_get_int(env, tup[1], &copies) || copies < 1 || copies > 4)
+            return enif_make_badarg(env);
+        spec = tup[0];
+    }
+    if (enif_get_list_length(env, spec, &nd)) {
+        ERL_NIF_TERM l = spec, h;
         if (nd == 0 || nd > 8) return enif_make_badarg(env);
         for (unsigned i = 0; enif_get_list_cell(env, l, &h, &l); i++)
             if (!enif_get_int(env, h, &devs[i])) return enif_make_badarg(env);
-    } else if (!enif_get_int(env, argv[0], &dev)) {
+    } else if (!enif_get_int(env, spec, &dev)) {
         return enif_make_badarg(env);
     }
     idx_res *r = enif_alloc_resource(IDX_RT, sizeof *r);
     memset(r, 0, sizeof *r);
-    tm_options o = {dev, 0, 0};
+    tm_options o = {dev, (uint32_t)copies, 0};
     int rc = nd ? tm_create_replicas(&o, devs, nd, &r->h) : tm_create(&o, &r->h);
     if (rc != TM_OK) { r->h = NULL; enif_release_resource(r); return err_term(env, rc); }
     tmn_pool_init(&r->pool, r->h);

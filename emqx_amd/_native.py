@@ -39,7 +39,7 @@ class TmError(RuntimeError):
 
 
 class tm_options(C.Structure):
-    _fields_ = [("device", C.c_int32), ("reserved", C.c_uint32), ("hint_keys", C.c_uint64)]
+    _fields_ = [("device", C.c_int32), ("copies", C.c_uint32), ("hint_keys", C.c_uint64)]
 
 
 class tm_stats_t(C.Structure):
@@ -135,13 +135,15 @@ def pack_strings(items) -> tuple[np.ndarray, np.ndarray]:
 class Index:
     """Owning handle of one device-resident topic index (tm_index*)."""
 
-    def __init__(self, device: int = -1, hint_keys: int = 0, devices=None):
+    def __init__(self, device: int = -1, hint_keys: int = 0, devices=None, copies: int = 1):
         """devices: a list of HIP devices -> one host image with a replica on
-        each (tm_create_replicas); otherwise one device."""
+        each (tm_create_replicas); otherwise one device.  copies: copies of the
+        tables per device (tm_options.copies: deltas never wait for batches in
+        flight on another copy)."""
         if not _gpu_present():
             raise NativeUnavailable("no HIP device visible: the topic index runs on the GPU only")
         self._lib = load_library()
-        opts = tm_options(device, 0, hint_keys)
+        opts = tm_options(device, copies, hint_keys)
         h = C.c_void_p()
         if devices is not None:
             devs = (C.c_int32 * len(devices))(*devices)

@@ -53,7 +53,7 @@ struct Dirty {
     void clear() { all = false; r.clear(); }
 };
 
-constexpr int MAX_REPLICAS = 8;   // device copies of one host image (tm_create_replicas)
+constexpr int MAX_REPLICAS = 16;  // device copies of one host image (tm_create_replicas: devices x copies)
 
 // host vector + its HBM copy on every replica
 template <class T>
@@ -112,23 +112,32 @@ struct Lane {
     uint32_t *d_vals = nullptr; uint64_t d_vals_cap = 0;   // sorted output: values sorted in HBM first
 };
 
-// Patch staging: a small ring, so shipping a patch waits on the host only for
-// the patch PATCH_RING before it, not for the one just enqueued.  The pinned
-// [PatchRun x runs | u32 data] buffer of a slot is shared by every replica
-// (one host image: collected once, copied to each device).
-constexpr int PATCH_RING = 4;
+// Patch log: a ring of the last PATCH_RING patches (numbered 1, 2, ... in the
+// order they were collected).  A patch is one pinned [PatchRun x runs | u32
+// data] buffer shared by every replica (one host image: collected once), and
+// reaches each replica lazily -- when a batch is about to run there -- so a
+// replica no batch is reading can take a patch at once while the others are
+// still busy with theirs (tm_options.copies).  A slot is reused only once
+// every replica has applied the patch it holds (a lagging replica is brought
+// up on its patch stream then).
+constexpr int PATCH_RING = 16;
 struct PatchSlot {
     uint8_t *pin = nullptr; uint64_t pin_cap = 0;
+    uint64_t bytes = 0, nr = 0, seq = 0;      // the patch held: size, runs, number (0: none)
 };
 
 // One device copy of the tables.  Patches reach it on the stream of the batch
-// that ships them (its own replica) or on the replica's patch stream.
+// that is about to read it, or on the replica's patch stream.  Replicas of one
+// entry of tm_create_replicas' device list form a group (tm_options.copies
+// copies of the tables on that device).
 struct Replica {
-    int device = 0;
-    hipStream_t ps = nullptr;                 // patch stream (patches shipped by another replica's batch)
+    int device = 0, group = 0;
+    hipStream_t ps = nullptr;                 // patch stream (a lagging replica brought up out of band)
     hipEvent_t last_patch = nullptr;          // event of its latest patch (every batch waits for it)
     uint8_t *pdev[PATCH_RING] = {}; uint64_t pdev_cap[PATCH_RING] = {};
     hipEvent_t pdone[PATCH_RING] = {}; bool ppending[PATCH_RING] = {};
+    uint64_t applied = 0;                     // patches applied (== tm_index::patch_seq: up to date)
+    uint64_t last_use = 0;                    // tick of its latest batch
     uint64_t batches = 0;                     // host-API batches served (tm_replica_stats)
 };
 
@@ -138,7 +147,7 @@ constexpr int MAX_DEV_LANES = 16;    // device-API streams with a workspace kept
 struct tm_index {
     std::mutex mu;
     std::condition_variable cv;      // a host lane was released
-    int nrep = 1;
+    int nrep = 1, ngroups = 1;
     Replica rep[MAX_REPLICAS];
     uint64_t rr = 0;                 // round-robin among equally loaded replicas
 
@@ -190,7 +199,7 @@ struct tm_index {
     uint64_t n_wild = 0, n_exact = 0;
     uint64_t uploads = 0, patch_bytes = 0;
 
-    PatchSlot patch[PATCH_RING]; uint32_t patch_head = 0;
+    PatchSlot patch[PATCH_RING]; uint64_t patch_seq = 0;   // patches collected so far
 
     std::vector<std::unique_ptr<Lane>> lanes;
     uint64_t tick = 0;
@@ -1033,8 +1042,15 @@ void key_op(tm_index *ix, bool ins, const uint8_t *f, uint32_t len, uint32_t v, 
 
 constexpr uint64_t DEV_GUARD = 16;   // device elements kept allocated past the host size (see collect)
 
+int bring_up(tm_index *ix, int r, uint64_t upto, hipStream_t st);
+
 template <class T>
 int upload_full(tm_index *ix, Mirror<T> &m) {
+    // patches logged before this upload are older than it: every replica
+    // takes them first (a lagging replica applying one later would write old
+    // words over the new table)
+    for (int r = 0; r < ix->nrep; r++)
+        if (int rc = bring_up(ix, r, ix->patch_seq, ix->rep[r].ps)) return rc;
     uint64_t need = std::max<uint64_t>(m.h.size(), 1);
     const bool grow = need > m.dcap;
     const uint64_t cap = grow ? need + need / 2 + DEV_GUARD : m.dcap;
@@ -1120,15 +1136,50 @@ int batch_done(tm_index *ix, Lane &ln) {
     return TM_OK;
 }
 
-// Ship every dirty word to every replica (caller holds ix->mu): to replica
-// `r0` on stream s (the batch about to run there), to the others on their
-// patch streams.  Patches rewrite the tables in place, so on each replica a
-// patch first waits for every batch still reading them (each of its lanes'
-// `done`) and for the patch before it; every later batch there waits for this
-// one (`last_patch`, ensure_ws): a batch sees exactly the deltas applied
-// before it (C5), whichever stream either ran on.  The calling thread's
-// device is replica r0's afterwards.
-int sync_locked(tm_index *ix, int r0, hipStream_t s) {
+// Apply logged patch q to replica r on stream st.  Patches rewrite the tables
+// in place, so a patch first waits for every batch still reading the replica
+// (each of its lanes' `done`) and for the replica's patch before it; every
+// later batch there waits for this one (`last_patch`, ensure_ws): a batch
+// sees exactly the deltas applied before it was queued (C5), whichever stream
+// either ran on.
+int apply_patch(tm_index *ix, int r, uint64_t q, hipStream_t st) {
+    Replica &R = ix->rep[r];
+    const uint32_t k = (uint32_t)((q - 1) % PATCH_RING);
+    const PatchSlot &p = ix->patch[k];
+    HIPCHK(ix, hipSetDevice(R.device));
+    if (p.bytes > R.pdev_cap[k]) {
+        if (R.ppending[k]) { HIPCHK(ix, hipEventSynchronize(R.pdone[k])); R.ppending[k] = false; }
+        if (R.pdev[k]) HIPCHK(ix, hipFree(R.pdev[k]));
+        R.pdev[k] = nullptr;
+        // generous steps: a reallocation (hipHostFree / hipFree) synchronises
+        // the device, a multi-millisecond stall inside a churn stream (C5)
+        R.pdev_cap[k] = std::max<uint64_t>(p.bytes * 2, 1u << 20);
+        HIPCHK(ix, hipMalloc(&R.pdev[k], R.pdev_cap[k]));
+    }
+    for (auto &l : ix->lanes)
+        if (l->r == r && l->used && l->s != st) HIPCHK(ix, hipStreamWaitEvent(st, l->done, 0));
+    if (R.last_patch) HIPCHK(ix, hipStreamWaitEvent(st, R.last_patch, 0));
+    HIPCHK(ix, hipMemcpyAsync(R.pdev[k], p.pin, p.bytes, hipMemcpyHostToDevice, st));
+    HIPCHK(ix, launch_patch(reinterpret_cast<const PatchRun *>(R.pdev[k]),
+                            reinterpret_cast<const uint32_t *>(R.pdev[k] + p.nr * sizeof(PatchRun)), p.nr,
+                            patch_bases(ix, r), st));
+    HIPCHK(ix, hipEventRecord(R.pdone[k], st));
+    R.ppending[k] = true;
+    R.last_patch = R.pdone[k];
+    R.applied = q;
+    return TM_OK;
+}
+
+// replica r takes every logged patch up to `upto`, in order, on stream st
+int bring_up(tm_index *ix, int r, uint64_t upto, hipStream_t st) {
+    for (uint64_t q = ix->rep[r].applied + 1; q <= upto; q++)
+        if (int rc = apply_patch(ix, r, q, st)) return rc;
+    return TM_OK;
+}
+
+// Collect every dirty word into a new logged patch (caller holds ix->mu);
+// nothing reaches a device here
+int collect_patch(tm_index *ix) {
     std::vector<PatchRun> runs;
     std::vector<uint32_t> data;
     int rc;
@@ -1142,56 +1193,67 @@ int sync_locked(tm_index *ix, int r0, hipStream_t s) {
     if ((rc = collect(ix, ix->wseq, 7, runs, data))) return rc;
     if ((rc = collect(ix, ix->wbits, 8, runs, data))) return rc;
     const uint64_t nr = runs.size(), nw = data.size();
-    if (nr) {
-        // staging: [runs | data] in one pinned buffer, one H2D copy + one kernel per replica
-        const uint64_t bytes = nr * sizeof(PatchRun) + nw * 4;
-        const uint32_t k = ix->patch_head % PATCH_RING;
-        PatchSlot &p = ix->patch[k];
-        ix->patch_head++;
-        for (int r = 0; r < ix->nrep; r++) {   // the slot's previous patch has left its pinned buffer
+    if (!nr) return TM_OK;
+    const uint64_t q = ix->patch_seq + 1;
+    const uint32_t k = (uint32_t)((q - 1) % PATCH_RING);
+    PatchSlot &p = ix->patch[k];
+    if (p.seq) {   // the slot's patch must have reached every replica and left its pinned buffer
+        for (int r = 0; r < ix->nrep; r++) {
             Replica &R = ix->rep[r];
+            if (R.applied < p.seq && (rc = bring_up(ix, r, p.seq, R.ps))) return rc;
             if (R.ppending[k]) {
                 HIPCHK(ix, hipSetDevice(R.device));
                 HIPCHK(ix, hipEventSynchronize(R.pdone[k]));
                 R.ppending[k] = false;
             }
         }
-        if (bytes > p.pin_cap) {
-            if (p.pin) HIPCHK(ix, hipHostFree(p.pin));
-            p.pin = nullptr;
-            // generous steps: a reallocation (hipHostFree / hipFree) synchronises
-            // the device, a multi-millisecond stall inside a churn stream (C5)
-            p.pin_cap = std::max<uint64_t>(bytes * 2, 1u << 20);
-            HIPCHK(ix, hipHostMalloc(&p.pin, p.pin_cap, hipHostMallocPortable));
-        }
-        memcpy(p.pin, runs.data(), nr * sizeof(PatchRun));
-        memcpy(p.pin + nr * sizeof(PatchRun), data.data(), nw * 4);
-        for (int r = 0; r < ix->nrep; r++) {
-            Replica &R = ix->rep[r];
-            HIPCHK(ix, hipSetDevice(R.device));
-            const hipStream_t st = r == r0 ? s : R.ps;
-            if (bytes > R.pdev_cap[k]) {   // the slot's previous patch on this replica has completed
-                if (R.pdev[k]) HIPCHK(ix, hipFree(R.pdev[k]));
-                R.pdev[k] = nullptr;
-                R.pdev_cap[k] = std::max<uint64_t>(bytes * 2, 1u << 20);
-                HIPCHK(ix, hipMalloc(&R.pdev[k], R.pdev_cap[k]));
-            }
-            for (auto &l : ix->lanes)
-                if (l->r == r && l->used && l->s != st) HIPCHK(ix, hipStreamWaitEvent(st, l->done, 0));
-            if (R.last_patch) HIPCHK(ix, hipStreamWaitEvent(st, R.last_patch, 0));
-            HIPCHK(ix, hipMemcpyAsync(R.pdev[k], p.pin, bytes, hipMemcpyHostToDevice, st));
-            HIPCHK(ix, launch_patch(reinterpret_cast<const PatchRun *>(R.pdev[k]),
-                                    reinterpret_cast<const uint32_t *>(R.pdev[k] + nr * sizeof(PatchRun)), nr,
-                                    patch_bases(ix, r), st));
-            HIPCHK(ix, hipEventRecord(R.pdone[k], st));
-            R.ppending[k] = true;
-            R.last_patch = R.pdone[k];
-        }
-        ix->patch_bytes += nw * 4;
-        ix->uploads++;
     }
+    const uint64_t bytes = nr * sizeof(PatchRun) + nw * 4;
+    if (bytes > p.pin_cap) {
+        if (p.pin) HIPCHK(ix, hipHostFree(p.pin));
+        p.pin = nullptr;
+        p.pin_cap = std::max<uint64_t>(bytes * 2, 1u << 20);
+        HIPCHK(ix, hipHostMalloc(&p.pin, p.pin_cap, hipHostMallocPortable));
+    }
+    memcpy(p.pin, runs.data(), nr * sizeof(PatchRun));
+    memcpy(p.pin + nr * sizeof(PatchRun), data.data(), nw * 4);
+    p.bytes = bytes; p.nr = nr; p.seq = q;
+    ix->patch_seq = q;
+    ix->patch_bytes += nw * 4;
+    ix->uploads++;
+    return TM_OK;
+}
+
+// Every delta applied so far, onto replica r0 before a batch runs there on
+// stream s (caller holds ix->mu; the calling thread's device is r0's after)
+int sync_locked(tm_index *ix, int r0, hipStream_t s) {
+    int rc;
+    if ((rc = collect_patch(ix))) return rc;
+    if ((rc = bring_up(ix, r0, ix->patch_seq, s))) return rc;
     HIPCHK(ix, hipSetDevice(ix->rep[r0].device));
     return TM_OK;
+}
+
+// Which copy of group g a batch should read (caller holds ix->mu, pending
+// deltas collected): the lowest-numbered copy that is up to date (so without
+// churn one copy stays hot), else one no batch is reading (it takes the
+// patch without waiting), else the least recently used one.  busy (host
+// lanes per replica) excludes copies whose host lanes are all in use.
+int pick_copy(tm_index *ix, int g, const int *busy) {
+    auto ok = [&](int r) { return ix->rep[r].group == g && (!busy || busy[r] < MAX_HOST_LANES); };
+    for (int r = 0; r < ix->nrep; r++)
+        if (ok(r) && ix->rep[r].applied == ix->patch_seq) return r;
+    for (int r = 0; r < ix->nrep; r++) {
+        if (!ok(r)) continue;
+        bool idle = true;
+        for (auto &l : ix->lanes)
+            if (l->r == r && l->used && hipEventQuery(l->done) == hipErrorNotReady) { idle = false; break; }
+        if (idle) return r;
+    }
+    int best = -1;
+    for (int r = 0; r < ix->nrep; r++)
+        if (ok(r) && (best < 0 || ix->rep[r].last_use < ix->rep[best].last_use)) best = r;
+    return best;
 }
 
 DevIndex dev_view(tm_index *ix, int r) {
@@ -1248,21 +1310,31 @@ int make_lane(tm_index *ix, int r, hipStream_t s, bool owned, Lane *&out) {
     return TM_OK;
 }
 
-// A host-API lane for this caller: on the replica with the fewest batches in
-// flight (round robin among equals), waiting while every replica has
-// MAX_HOST_LANES in use.  Leaves the calling thread on the lane's device.
+// A host-API lane for this caller: on the group (one entry of the device
+// list) with the fewest batches in flight (round robin among equals), on the
+// copy pick_copy chooses there; waiting while every copy has MAX_HOST_LANES in
+// use.  Pending deltas are collected first (pick_copy must know which copies
+// are up to date).  Leaves the calling thread on the lane's device.
 int host_lane(tm_index *ix, std::unique_lock<std::mutex> &g, Lane *&out) {
     for (;;) {
-        int busy[MAX_REPLICAS] = {}, owned[MAX_REPLICAS] = {};
+        if (int rc = collect_patch(ix)) return rc;
+        int busy[MAX_REPLICAS] = {}, gbusy[MAX_REPLICAS] = {};
+        bool gfree[MAX_REPLICAS] = {};
         for (auto &l : ix->lanes)
-            if (l->owned) { owned[l->r]++; busy[l->r] += l->busy; }
-        int best = -1;
-        for (int k = 0; k < ix->nrep; k++) {
-            const int r = (int)((ix->rr + k) % ix->nrep);
-            if (busy[r] < MAX_HOST_LANES && (best < 0 || busy[r] < busy[best])) best = r;
+            if (l->owned) busy[l->r] += l->busy;
+        for (int r = 0; r < ix->nrep; r++) {
+            gbusy[ix->rep[r].group] += busy[r];
+            gfree[ix->rep[r].group] |= busy[r] < MAX_HOST_LANES;
         }
-        if (best >= 0) {
+        int bg = -1;
+        for (int k = 0; k < ix->ngroups; k++) {
+            const int gi = (int)((ix->rr + k) % ix->ngroups);
+            if (gfree[gi] && (bg < 0 || gbusy[gi] < gbusy[bg])) bg = gi;
+        }
+        if (bg >= 0) {
             ix->rr++;
+            const int best = pick_copy(ix, bg, busy);
+            ix->rep[best].last_use = ++ix->tick;
             HIPCHK(ix, hipSetDevice(ix->rep[best].device));
             for (auto &l : ix->lanes)
                 if (l->owned && l->r == best && !l->busy) { l->busy = true; out = l.get(); return TM_OK; }
@@ -1289,20 +1361,26 @@ struct LaneLease {
     }
 };
 
-// the device-API lane of stream s (on the replica of the calling thread's
-// current device: the first one there); the least recently used one is
-// retired (after its batches finish) when MAX_DEV_LANES streams hold a workspace
-int dev_lane(tm_index *ix, hipStream_t s, Lane *&out) {
-    int dev = 0, r = -1;
+// the group of the calling thread's current HIP device (the first entry of
+// the device list on it)
+int dev_group(tm_index *ix, int &g) {
+    int dev = 0;
     HIPCHK(ix, hipGetDevice(&dev));
-    for (int k = 0; k < ix->nrep && r < 0; k++) if (ix->rep[k].device == dev) r = k;
-    if (r < 0) return fail(ix, TM_EINVAL, "device API: the current HIP device holds no replica of this index");
+    for (int r = 0; r < ix->nrep; r++)
+        if (ix->rep[r].device == dev) { g = ix->rep[r].group; return TM_OK; }
+    return fail(ix, TM_EINVAL, "device API: the current HIP device holds no replica of this index");
+}
+
+// the device-API lane of stream s on replica r; the least recently used one is
+// retired (after its batches finish) when MAX_DEV_LANES (stream, replica)
+// pairs hold a workspace
+int dev_lane(tm_index *ix, hipStream_t s, int r, Lane *&out) {
     int n = 0;
     size_t lru = SIZE_MAX;
     for (size_t i = 0; i < ix->lanes.size(); i++) {
         Lane &l = *ix->lanes[i];
         if (l.owned) continue;
-        if (l.s == s) { l.tick = ++ix->tick; out = &l; return TM_OK; }
+        if (l.s == s && l.r == r) { l.tick = ++ix->tick; out = &l; return TM_OK; }
         n++;
         if (lru == SIZE_MAX || l.tick < ix->lanes[lru]->tick) lru = i;
     }
@@ -1312,8 +1390,8 @@ int dev_lane(tm_index *ix, hipStream_t s, Lane *&out) {
         if (l.used) HIPCHK(ix, hipEventSynchronize(l.done));
         free_lane(l);
         ix->lanes.erase(ix->lanes.begin() + lru);
-        HIPCHK(ix, hipSetDevice(dev));
     }
+    HIPCHK(ix, hipSetDevice(ix->rep[r].device));
     int rc = make_lane(ix, r, s, false, out);
     if (rc) return rc;
     out->tick = ++ix->tick;
@@ -1427,22 +1505,25 @@ int drain_lanes(tm_index *ix) {
 
 extern "C" {
 
-uint32_t tm_abi_version(void) { return (1u << 16) | 4u; }
+uint32_t tm_abi_version(void) { return (1u << 16) | 5u; }
 
 const char *tm_last_error(tm_index *) { return g_last_error.c_str(); }
 
 int tm_create_replicas(const tm_options *opts, const int32_t *devices, uint32_t n, tm_index **out) {
     if (!out) return fail(nullptr, TM_EINVAL, "tm_create: out is NULL");
     *out = nullptr;
-    if (!devices || n == 0 || n > (uint32_t)MAX_REPLICAS)
-        return fail(nullptr, TM_EINVAL, "tm_create_replicas: 1 to 8 devices");
+    const uint32_t copies = opts && opts->copies ? opts->copies : 1;
+    if (!devices || n == 0 || n > 8 || copies > 4 || n * copies > (uint32_t)MAX_REPLICAS)
+        return fail(nullptr, TM_EINVAL, "tm_create_replicas: 1 to 8 devices, 1 to 4 copies, at most 16 replicas");
     tm_index *ix = new (std::nothrow) tm_index();
     if (!ix) return fail(nullptr, TM_ENOMEM, "tm_create: out of host memory");
-    ix->nrep = (int)n;
+    ix->nrep = (int)(n * copies);
+    ix->ngroups = (int)n;
     hipError_t e = hipSuccess;
-    for (uint32_t r = 0; r < n && e == hipSuccess; r++) {
+    for (uint32_t r = 0; r < n * copies && e == hipSuccess; r++) {
         Replica &R = ix->rep[r];
-        R.device = devices[r];
+        R.device = devices[r / copies];
+        R.group = (int)(r / copies);
         e = hipSetDevice(R.device);
         if (e == hipSuccess) e = hipStreamCreateWithFlags(&R.ps, hipStreamNonBlocking);
         for (int i = 0; i < PATCH_RING && e == hipSuccess; i++)
@@ -1597,9 +1678,14 @@ int tm_match_batch_dev_ex(tm_index *ix, uint64_t n, const uint8_t *bytes, const 
     if (order > TM_ORDER_UNIQUE) return fail(ix, TM_EINVAL, "tm_match_batch_dev: bad order");
     std::lock_guard<std::mutex> g(ix->mu);
     hipStream_t s = pick_stream(ix, stream);
-    int rc;
+    int rc, grp = 0;
     Lane *ln;
-    if ((rc = dev_lane(ix, s, ln))) return rc;
+    if ((rc = dev_group(ix, grp))) return rc;
+    if ((rc = collect_patch(ix))) return rc;
+    const int r = pick_copy(ix, grp, nullptr);
+    ix->rep[r].last_use = ++ix->tick;
+    ix->rep[r].batches++;
+    if ((rc = dev_lane(ix, s, r, ln))) return rc;
     if ((rc = sync_locked(ix, ln->r, s))) return rc;
     if ((rc = ensure_ws(ix, n, *ln))) return rc;
     const DevIndex d = dev_view(ix, ln->r);
@@ -1629,8 +1715,11 @@ int tm_sort_segments(tm_index *ix, uint64_t n, const uint64_t *hit_offs, uint32_
     std::lock_guard<std::mutex> g(ix->mu);
     hipStream_t s = pick_stream(ix, stream);
     Lane *ln;
-    int rc;
-    if ((rc = dev_lane(ix, s, ln))) return rc;
+    int rc, grp = 0;
+    if ((rc = dev_group(ix, grp))) return rc;
+    int r = 0;
+    while (ix->rep[r].group != grp) r++;
+    if ((rc = dev_lane(ix, s, r, ln))) return rc;
     if ((rc = ensure_ws(ix, n, *ln))) return rc;
     HIPCHK(ix, launch_sort_segments(ln->w, n, hit_offs, vals, cap, order == TM_ORDER_UNIQUE, ucnt, s));
     return batch_done(ix, *ln);

@@ -80,7 +80,12 @@ enum { TM_KEY_BINARY = 0, TM_KEY_WORDS = 1, TM_KEY_EMPTY_LIST = 2 };
 
 typedef struct {
     int32_t device;          /* HIP device ordinal; -1 = current device        */
-    uint32_t reserved;
+    uint32_t copies;         /* copies of the tables per device (0 = 1; <= 4):
+                                with 2 or more a batch after a delta runs on a
+                                copy no batch is reading, which takes the delta
+                                at once, instead of waiting for the batches in
+                                flight on a single copy (churn, C5); without
+                                deltas every batch reads the first copy       */
     uint64_t hint_keys;      /* expected number of keys (sizes tables up front) */
 } tm_options;
 
@@ -105,14 +110,18 @@ int tm_destroy(tm_index *h);
  * table per node (emqx_router.erl:133-162); here the host key set, its
  * compiler and tm_apply_deltas run once, and every patch's staged runs are
  * copied to every replica (one pinned buffer, one H2D copy + one patch kernel
- * per device).  Host-API batches go to the replica with the fewest batches in
- * flight (round robin among equals); device-API calls use the replica of the
- * calling thread's current HIP device (the first one there).  opts->device is
- * ignored; matches_filter runs on replica 0.  tm_stats().device_bytes is per
- * replica. */
+ * per device), lazily: a replica takes the patches logged since its last batch
+ * when a batch is about to run there.  Each device entry holds opts->copies
+ * copies (replica r is copy r % copies of device entry r / copies).  Host-API
+ * batches go to the device entry with the fewest batches in flight (round
+ * robin among equals); device-API calls use the entry of the calling thread's
+ * current HIP device (the first one there); within an entry a batch reads its
+ * first up-to-date copy, else a copy no batch is reading, else the least
+ * recently used one.  opts->device is ignored; matches_filter runs on replica
+ * 0.  tm_stats().device_bytes is per replica. */
 int tm_create_replicas(const tm_options *opts, const int32_t *devices, uint32_t n, tm_index **out);
 
-/* Host-API batches replica r has served so far, and its device. */
+/* Batches (host and device API) replica r has served so far, and its device. */
 int tm_replica_stats(tm_index *h, uint32_t r, uint64_t *batches, int32_t *device);
 
 /* Apply n deltas in order (a later op on the same key wins).  Host buffers:

@@ -20,8 +20,9 @@ init() ->
         end,
     erlang:load_nif(filename:join(Priv, "emqx_tmatch_nif"), 0).
 
-%% A list of devices: one host image with a replica on each (tm_create_replicas).
--spec new(integer() | [integer()]) -> {ok, ref()} | {error, integer()}.
+%% A list of devices: one host image with a replica on each (tm_create_replicas);
+%% {Devices, Copies}: Copies copies of the tables per device (tm_options.copies).
+-spec new(integer() | [integer()] | {integer() | [integer()], 1..4}) -> {ok, ref()} | {error, integer()}.
 new(_Device) -> erlang:nif_error(nif_not_loaded).
 
 %% {ok, Epoch}: the delta epoch the batch made current (include/tmatch.h "Reader epochs").

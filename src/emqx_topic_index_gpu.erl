@@ -56,11 +56,18 @@ new() ->
 
 %% new/1 (emqx_topic_index.erl:44-48): the ETS table with the caller's options
 %% plus its device mirror -- on the default device, or with {devices, [D]} one
-%% host image with a replica on each device (tm_create_replicas).
+%% host image with a replica on each device (tm_create_replicas); {copies, N}
+%% keeps N copies of the tables per device, so subscribe/unsubscribe churn
+%% never makes a publish batch wait for the batches in flight.
 -spec new(list()) -> gtab().
 new(Options) ->
     Devices = proplists:get_value(devices, Options, -1),
-    mirror(ets:new(emqx_topic_index, [ordered_set | proplists:delete(devices, Options)]), Devices).
+    Spec = case proplists:get_value(copies, Options, 1) of
+               1 -> Devices;
+               N -> {Devices, N}
+           end,
+    EtsOpts = proplists:delete(copies, proplists:delete(devices, Options)),
+    mirror(ets:new(emqx_topic_index, [ordered_set | EtsOpts]), Spec).
 
 %% Put a device mirror next to an existing index table (e.g. the router's
 %% ?ROUTE_TAB_FILTERS, emqx_router.erl:148-160) and load its keys in batches:

@@ -963,27 +963,32 @@ def test_c2_full_size_sample_vs_oracle(torch_dev):
     assert np.array_equal(got, ovals)
 
 
-def test_batches_on_two_streams_see_patches_in_order(torch_dev):
-    """Per-stream workspaces: batches on two streams may overlap; a batch sees
-    every delta applied before it, whichever stream shipped the patch."""
+@pytest.mark.parametrize("copies,nstreams", [(1, 2), (2, 2), (3, 3)])
+def test_batches_on_two_streams_see_patches_in_order(torch_dev, copies, nstreams):
+    """Per-stream workspaces: batches on several streams may overlap; a batch
+    sees every delta applied before it, whichever stream shipped the patch --
+    with one copy of the tables, and with 2-3 copies (tm_options.copies), where
+    a patch reaches each copy lazily, when a batch is about to read it."""
     import torch
     nf = 30_000
     fs = wl.filters(5, nf)
-    ix, o = gpu_index(fs), oracle_of(fs)
+    ix = _native.Index(copies=copies)
+    ix.apply(np.ones(len(fs), np.uint8), fs.blob, fs.offs, fs.vals)
+    o = oracle_of(fs)
     ts = wl.topics(5, nf, 40_000)
     dev = torch.device("cuda:0")
     d_blob = torch.from_numpy(ts.blob.copy()).to(dev)
     d_offs = torch.from_numpy(ts.offs.view(np.int64).copy()).to(dev)
-    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    streams = [torch.cuda.Stream() for _ in range(nstreams)]
     n = len(ts)
     results = []
-    for k in range(4):
-        d = wl.deltas(nf, k * 3_000, 3_000)
+    for k in range(4 if copies == 1 else 9):
+        d = wl.deltas(nf, k * 3_000, 3_000 if k % 3 else 40)
         ix.apply(d.flags, d.blob, d.offs, d.vals)
         o.apply(d.flags, d.blob, d.offs, d.vals)
         o.prepare()
         _, _, ohit, ovals = o.match_batch(ts.blob, ts.offs)
-        s = streams[k % 2]
+        s = streams[k % nstreams]
         hit = torch.zeros(n + 1, dtype=torch.int64, device=dev)
         err = torch.zeros(n, dtype=torch.uint8, device=dev)
         out = torch.zeros(int(ohit[-1]) + 1, dtype=torch.int32, device=dev)
@@ -1023,7 +1028,8 @@ def test_topic_index_matches_filter(torch_dev):
 
 # ------------------------------------------------------ concurrent callers
 
-def test_concurrent_callers_see_consistent_snapshots(torch_dev):
+@pytest.mark.parametrize("copies", [1, 2])
+def test_concurrent_callers_see_consistent_snapshots(torch_dev, copies):
     """12 host threads submit 4k-topic batches through tm_match_batch at once
     (half with tm_host_alloc buffers, half pageable) while the main thread
     applies 16 epochs of subscribe/unsubscribe deltas.  Each epoch is one
@@ -1036,7 +1042,9 @@ def test_concurrent_callers_see_consistent_snapshots(torch_dev):
     import time
     nf, nthreads, lb, epochs = 10_000, 12, 4096, 16
     fs = wl.filters(1, nf)
-    ix, o = gpu_index(fs), oracle_of(fs)
+    ix = _native.Index(copies=copies)
+    ix.apply(np.ones(len(fs), np.uint8), fs.blob, fs.offs, fs.vals)
+    o = oracle_of(fs)
     r = random.Random(0x454D5158 + 77)
     tsets = []
     for t in range(nthreads):

@@ -23,6 +23,7 @@ def main():
     p.add_argument("--threads", default="1,4,8,16")
     p.add_argument("--churn", default="0,256")
     p.add_argument("--seconds", type=float, default=1.0)
+    p.add_argument("--copies", type=int, default=1, help="tm_options.copies of the index")
     p.add_argument("--dev", type=int, default=0, help="1: batches in HBM through the device API (no PCIe leg)")
     a = p.parse_args()
     import torch
@@ -30,7 +31,7 @@ def main():
     from bench import host_bench_lib
     from emqx_amd import _native, workload as wl
     fs = wl.filters(3, a.filters)
-    ix = _native.Index(device=0, hint_keys=len(fs))
+    ix = _native.Index(device=0, hint_keys=len(fs), copies=a.copies)
     for lo in range(0, len(fs), 2_000_000):
         part = fs.slice(lo, min(lo + 2_000_000, len(fs)))
         ix.apply(np.ones(len(part), np.uint8), part.blob, part.offs, part.vals)
@@ -45,7 +46,7 @@ def main():
             rc = hb.tmb_callers_ex(ix._h, t, a.batch, _native._ptr(ts.blob), _native._ptr(ts.offs), cap, a.seconds,
                                    churn, a.dev, out)
             assert rc == 0, rc
-            print(json.dumps({"hwq": os.environ.get("GPU_MAX_HW_QUEUES", "default"), "dev": a.dev, "threads": t, "churn": churn,
+            print(json.dumps({"hwq": os.environ.get("GPU_MAX_HW_QUEUES", "default"), "dev": a.dev, "copies": a.copies, "threads": t, "churn": churn,
                               "batches": out[0], "topics_per_s": out[1], "p50_ms": out[2], "p99_ms": out[3],
                               "deltas_per_s": out[4]}), flush=True)
 
