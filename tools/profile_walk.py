@@ -20,9 +20,10 @@ def main():
     p.add_argument("--batch", type=int, default=1_000_000)
     p.add_argument("--batches", type=int, default=8)
     p.add_argument("--rotate", type=int, default=4, help="distinct batches the launches cycle over (as bench.py)")
-    p.add_argument("--order", default="stream", choices=["stream", "sorted", "bucket"],
-                   help="topic order in the batch: generator stream, byte-sorted, or bucketed "
-                        "by the hash of the first two levels (locality study)")
+    p.add_argument("--order", default="stream", choices=["stream", "sorted", "bucket", "work"],
+                   help="topic order in the batch: generator stream, byte-sorted, bucketed "
+                        "by the hash of the first two levels (locality study), or by predicted work "
+                        "(level count, then hit count from a first device pass: divergence study)")
     p.add_argument("--filter-order", default="stream", choices=["stream", "sorted"],
                    help="insertion order of the filters (node ids follow it): generator stream or "
                         "byte-sorted, i.e. trie nodes numbered depth first (layout study)")
@@ -52,6 +53,11 @@ def main():
             items = ts.items()
             if a.order == "sorted":
                 items = sorted(items)
+            elif a.order == "work":   # lanes of a wave get topics of similar work
+                hh, _, _ = ix.match_batch(ts.blob, ts.offs)
+                hits = np.diff(hh.astype(np.int64))
+                key = [(t.count(b"/"), int(h)) for t, h in zip(items, hits)]
+                items = [items[i] for i in sorted(range(len(items)), key=key.__getitem__)]
             else:
                 items = sorted(items, key=lambda t: hash(b"/".join(t.split(b"/")[:2])) & 0xFFFF)
             blob, offs = _native.pack_strings(items)
