@@ -1015,7 +1015,7 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_wave(DevIndex ix, Workspace w
 
 // ------------------------------------------- small batches in one launch
 //
-// A batch of <= WAVE_TOPICS topics is latency: its walk, scan and emit as
+// A batch of <= SMALL_TOPICS topics is latency: its walk, scan and emit as
 // separate kernels (k_walk_wave, the tail kernels, k_emit) cost ~4 launches
 // of mostly idle grids.  k_walk_small does all of it in one: each group of W
 // lanes walks its topic as k_walk_wave does; a topic the group cannot take
@@ -1037,9 +1037,16 @@ struct CountEmit {          // one-launch path: hit count only (the values come 
     __device__ __forceinline__ bool operator()(uint32_t, uint32_t n) { cnt += n & RUN_CNT; return true; }
 };
 
+// Batches of up to SMALL_TOPICS topics take the one-launch path.  Up to 8192
+// topics it replaced the wave walk + tails + emit; up to 64k it also beats the
+// lane walk's five kernels, because it writes each block's values while the
+// other blocks still walk (C3, host-to-host p50, in place: 16k topics 0.112
+// -> 0.075 ms, 32k 0.173 -> 0.111, 64k 0.208 -> 0.189; profiles/r3/sm64k/).
+constexpr uint64_t SMALL_TOPICS = 65536;
+
 bool small_path_ok(const DevIndex &ix, uint64_t n) {
     // the fallback store resolves need_levels() (+2 look-ahead levels) within MID_L
-    return n && n <= WAVE_TOPICS && ix.depth + 2 <= (uint32_t)MID_L && ix.xlen_max + 2 <= (uint32_t)MID_L;
+    return n && n <= SMALL_TOPICS && ix.depth + 2 <= (uint32_t)MID_L && ix.xlen_max + 2 <= (uint32_t)MID_L;
 }
 
 template <int MODE>

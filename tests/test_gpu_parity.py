@@ -251,7 +251,7 @@ def test_c3deep_reduced_vs_oracle(torch_dev):
     assert_same(gpu_index(both), oracle_of(both), ts)
 
 
-@pytest.mark.parametrize("batch", [3000, 40_000])   # wave walk + tails / lane walk + tails
+@pytest.mark.parametrize("batch", [3000, 40_000, 70_000])   # one launch (<= 64k topics) / lane walk + tails
 def test_levels_beyond_the_trie(torch_dev, batch):
     """Topics deeper than every filter: badarg at any depth, '$' first levels,
     long words past the trie, binary keys of 3, 20 and 70 levels, '#'
@@ -652,7 +652,7 @@ def test_mixed_batch_sizes_and_modes_in_sequence(torch_dev):
     fs = wl.filters(1, 10_000)
     ix, o = gpu_index(fs), oracle_of(fs)
     deep = items_of([b"/".join([b"a"] * 40), b"/".join([b"+x"] * 12) + b"/y"] * 3)
-    seq = [5, 9000, 3000, 1, 20_000, 8192, 8193, 2]
+    seq = [5, 9000, 3000, 1, 20_000, 8192, 70_000, 8193, 65536, 65537, 2]
     for k, nt in enumerate(seq):
         ts = wl.topics(1, 10_000, nt, first=k * 7)
         hit, vals = assert_same(ix, o, ts)
@@ -666,10 +666,11 @@ def test_mixed_batch_sizes_and_modes_in_sequence(torch_dev):
 
 
 def test_wave_walk_limits_fall_back_exactly(torch_dev):
-    """Batches of <= 8192 topics take the wave-per-topic walk (16 lanes per
-    topic); its limits (a frontier wider than the group, more hit ranges than
-    lanes, more levels than lanes) hand the topic to the lane walk.  Small (wave) and large (lane) batches of
-    the same topics must both equal the oracle."""
+    """Batches of <= 64k topics take the one-launch wave-per-topic walk (16
+    lanes per topic); its limits (a frontier wider than the group, more hit
+    ranges than lanes, more levels than lanes) hand the topic to the group's
+    lane-walk fallback.  Small (one launch) and large (> 64k: lane walk and
+    tail kernels) batches of the same topics must both equal the oracle."""
     import itertools
     words = [b"a", b"b", b"c", b"d", b"e", b"f", b"g"]
     fl = []
@@ -689,7 +690,7 @@ def test_wave_walk_limits_fall_back_exactly(torch_dev):
     tl += [b"/".join(deep.split(b"/")[:L]) for L in range(28, 41)]
     small = items_of(tl)
     assert_same(ix, o, small)                                  # wave walk (+ fallbacks)
-    big = items_of(tl * 400)                                   # > 8192 topics: lane walk
+    big = items_of(tl * 3200)                                  # > 64k topics: lane walk
     assert_same(ix, o, big)
     first, found = ix.first_batch(small.blob, small.offs)
     cnt, _, ohit, ovals = o.match_batch(small.blob, small.offs)
@@ -1720,7 +1721,7 @@ def test_reference_quirk_hash_not_last_on_device(torch_dev):
     for filters, exp in (([b"+/+//#", b"+/#/#"], []), ([b"+/+//#"], [0])):
         fs = items_of(filters)
         ix, o = gpu_index(fs), oracle_of(fs)
-        for batch in (1, 9000):   # wave walk / lane walk
+        for batch in (1, 9000, 70_000):   # one launch / lane walk
             ts = items_of([b"E//"] * batch)
             hit, vals = assert_same(ix, o, ts)
             assert vals[: hit[1]].tolist() == exp
@@ -1731,15 +1732,15 @@ def test_reference_quirk_hash_not_last_on_device(torch_dev):
 @pytest.mark.parametrize("seed", range(12))
 def test_hash_not_last_random_sets_vs_oracle(torch_dev, seed):
     """'#'-not-last keys in random sets: the seek past '+' and the cut at the
-    topic's last level, through both walks (a batch of <= 8192 topics takes
-    the wave walk, a larger one the lane walk and its tail kernels -- LDS and,
-    beyond 32 levels, global-scratch stores), match/2's first hit, and after
+    topic's last level, through both walks (a batch of <= 64k topics takes
+    the one-launch wave walk, a larger one the lane walk and its tail kernels
+    -- LDS and, beyond 32 levels, global-scratch stores), match/2's first hit, and after
     deletes / re-inserts of those keys."""
     topics, filters, flags = _hdesc_sets(seed, deep=seed % 3 == 0)
     fs = items_of(filters)
     ix, o = gpu_index(fs, flags), oracle_of(fs, flags)
     small = items_of(topics)
-    big = items_of(topics * (9000 // len(topics) + 1))
+    big = items_of(topics * (70_000 // len(topics) + 1))
     assert_same(ix, o, small)
     assert_same(ix, o, big)
     for ts in (small, big):
