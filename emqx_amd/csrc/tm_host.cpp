@@ -145,7 +145,17 @@ constexpr int MAX_HOST_LANES = 16;   // concurrent host-API batches in flight, p
 constexpr int MAX_DEV_LANES = 16;    // device-API streams with a workspace kept
 
 struct tm_index {
+    // Two locks (order: mu, then img).  `mu` covers the device side: lanes,
+    // the patch log, the replicas, pinned buffers, profiling.  `img` covers
+    // the host image: the tables' host vectors and dirty sets, the key maps,
+    // matches_filter's log.  tm_apply_deltas takes only `img`, so compiling a
+    // syncer batch never blocks a match batch that has no delta to pick up: a
+    // batch takes `img` only to collect deltas applied since the last one
+    // (`img_dirty`), and otherwise launches on the device view cached then.
     std::mutex mu;
+    std::mutex img;
+    std::atomic<bool> img_dirty{true};
+    bool view_ok = false;
     std::condition_variable cv;      // a host lane was released
     int nrep = 1, ngroups = 1;
     Replica rep[MAX_REPLICAS];
@@ -182,11 +192,11 @@ struct tm_index {
     // match batch for a second at 10M keys).
     struct MfState {
         std::mutex mu;                        // one matches_filter call at a time (never taken by matching)
-        bool log_on = false, log_lost = false;   // (under ix->mu) ops logged since the snapshot / log dropped
-        std::vector<std::pair<bool, std::string>> log;   // (insert?, key) -- under ix->mu
+        bool log_on = false, log_lost = false;   // (under ix->img) ops logged since the snapshot / log dropped
+        std::vector<std::pair<bool, std::string>> log;   // (insert?, key) -- under ix->img
         std::unordered_set<std::string> keys; // kind | value | filter of every word-list key (under mu)
         bool have_keys = false, dev_stale = true;
-        std::atomic<size_t> nkeys{0};         // keys.size(), for the log bound (read under ix->mu)
+        std::atomic<size_t> nkeys{0};         // keys.size(), for the log bound (read under ix->img)
         std::vector<std::string> words;       // distinct binary words, byte order
         uint32_t *pool = nullptr, *val = nullptr; uint64_t *koff = nullptr, K = 0;
         uint64_t pcap = 0, vcap = 0, kcap = 0;
@@ -200,6 +210,7 @@ struct tm_index {
     uint64_t uploads = 0, patch_bytes = 0;
 
     PatchSlot patch[PATCH_RING]; uint64_t patch_seq = 0;   // patches collected so far
+    DevIndex view[MAX_REPLICAS];     // each replica's device view as of the last collect_patch
 
     std::vector<std::unique_ptr<Lane>> lanes;
     uint64_t tick = 0;
@@ -1043,6 +1054,7 @@ void key_op(tm_index *ix, bool ins, const uint8_t *f, uint32_t len, uint32_t v, 
 constexpr uint64_t DEV_GUARD = 16;   // device elements kept allocated past the host size (see collect)
 
 int bring_up(tm_index *ix, int r, uint64_t upto, hipStream_t st);
+int collect_patch_locked(tm_index *ix);
 
 template <class T>
 int upload_full(tm_index *ix, Mirror<T> &m) {
@@ -1177,9 +1189,23 @@ int bring_up(tm_index *ix, int r, uint64_t upto, hipStream_t st) {
     return TM_OK;
 }
 
-// Collect every dirty word into a new logged patch (caller holds ix->mu);
-// nothing reaches a device here
+DevIndex dev_view_build(tm_index *ix, int r);
+
+// Collect every dirty word into a new logged patch and refresh the replicas'
+// cached device views (caller holds ix->mu; takes ix->img, and only when a
+// delta was applied since the last call); nothing reaches a device here but
+// whole-table uploads
 int collect_patch(tm_index *ix) {
+    if (ix->view_ok && !ix->img_dirty.load(std::memory_order_acquire)) return TM_OK;
+    std::lock_guard<std::mutex> gi(ix->img);
+    ix->img_dirty.store(false, std::memory_order_relaxed);   // (an apply from here on sets it again)
+    int rc = collect_patch_locked(ix);
+    for (int r = 0; r < ix->nrep; r++) ix->view[r] = dev_view_build(ix, r);
+    ix->view_ok = rc == TM_OK;
+    return rc;
+}
+
+int collect_patch_locked(tm_index *ix) {
     std::vector<PatchRun> runs;
     std::vector<uint32_t> data;
     int rc;
@@ -1256,7 +1282,11 @@ int pick_copy(tm_index *ix, int g, const int *busy) {
     return best;
 }
 
-DevIndex dev_view(tm_index *ix, int r) {
+// the device view of replica r as of the last collect_patch (caller holds ix->mu)
+DevIndex dev_view(tm_index *ix, int r) { return ix->view[r]; }
+
+// (caller holds ix->img)
+DevIndex dev_view_build(tm_index *ix, int r) {
     DevIndex d;
     d.vocab = ix->vocab.d[r]; d.vmask = (uint32_t)ix->vocab.h.size() - 1;
     d.wpool = ix->wpool.d[r];
@@ -1606,7 +1636,7 @@ int tm_apply_deltas_ex(tm_index *ix, uint64_t n, const uint8_t *ops, const uint8
     for (uint64_t i = 0; i < n; i++)
         if (ops[i] > TM_OP_INSERT || fo[i + 1] < fo[i] || fo[i + 1] - fo[i] > 0xFFFFFFFFull)
             return fail(ix, TM_EINVAL, "tm_apply_deltas: bad op or offsets at " + std::to_string(i));
-    std::lock_guard<std::mutex> g(ix->mu);
+    std::lock_guard<std::mutex> g(ix->img);   // the host image only: batches without a delta to pick up go on
     std::vector<WordRef> w;
     std::vector<uint32_t> wids;
     try {
@@ -1619,6 +1649,7 @@ int tm_apply_deltas_ex(tm_index *ix, uint64_t n, const uint8_t *ops, const uint8
     }
     // the keys changed above are what every batch queued from now on sees:
     // a reader registered from now on begins at the new epoch
+    if (n) ix->img_dirty.store(true, std::memory_order_release);
     const uint64_t e = n ? ix->epoch.fetch_add(1, std::memory_order_acq_rel) + 1 : ix->epoch.load();
     if (out_epoch) *out_epoch = e;
     return TM_OK;
@@ -2111,8 +2142,8 @@ void mf_path(tm_index *ix, uint32_t node, std::string &out) {
 }
 
 // Fuzzy snapshot of the word-list keys (caller holds m.mu, not ix->mu): the
-// log starts first, then the trie's nodes are read in slices under the index
-// lock, each ending after MF_SLICE_US (checked every 64 nodes); replaying the
+// log starts first, then the trie's nodes are read in slices under the image
+// lock (ix->img), each ending after MF_SLICE_US (checked every 64 nodes); replaying the
 // log afterwards makes the copy exact (a key untouched since the log started
 // sits on a node that cannot move, so a slice sees it; any other key ends as
 // its last logged op leaves it).
@@ -2122,7 +2153,7 @@ void mf_snapshot(tm_index *ix) {
     auto &m = ix->mf;
     m.keys.clear();
     {
-        std::lock_guard<std::mutex> g(ix->mu);
+        std::lock_guard<std::mutex> g(ix->img);
         m.log.clear();
         m.log_on = true;
         m.log_lost = false;
@@ -2130,7 +2161,7 @@ void mf_snapshot(tm_index *ix) {
     }
     std::string path, key;
     for (uint64_t cur = 0;;) {
-        std::lock_guard<std::mutex> g(ix->mu);
+        std::lock_guard<std::mutex> g(ix->img);
         const auto t0 = std::chrono::steady_clock::now();
         uint64_t end = ix->nodes.h.size(), x = cur;
         for (; x < end; x++) {
@@ -2237,13 +2268,13 @@ int mf_refresh(tm_index *ix) {
     std::vector<std::pair<bool, std::string>> log;
     bool lost;
     {
-        std::lock_guard<std::mutex> g(ix->mu);
+        std::lock_guard<std::mutex> g(ix->img);
         lost = m.log_lost || !m.log_on;
         if (!lost) log.swap(m.log);
     }
     if (lost || !m.have_keys) {
         mf_snapshot(ix);
-        std::lock_guard<std::mutex> g(ix->mu);
+        std::lock_guard<std::mutex> g(ix->img);
         log.swap(m.log);
         m.dev_stale = true;
     }
@@ -2323,7 +2354,7 @@ int tm_matches_filter(tm_index *ix, uint64_t n, const uint8_t *fb, const uint64_
 
 int tm_stats(tm_index *ix, tm_stats_t *o) {
     if (!ix || !o) return fail(ix, TM_EINVAL, "tm_stats: null argument");
-    std::lock_guard<std::mutex> g(ix->mu);
+    std::lock_guard<std::mutex> g(ix->img);
     memset(o, 0, sizeof *o);
     o->n_wild_keys = ix->n_wild;
     o->n_exact_keys = ix->n_exact;

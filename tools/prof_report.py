@@ -103,6 +103,11 @@ def main(prof, rnd, tag, config, filters, batch, rotate=4, batches=8):
     lines = [f"# Profile {rnd}/{tag}: config {config}, {filters} filters, {batch}-topic batches", ""]
     bench_json = os.path.join(prof, "bench.json")
     if os.path.isfile(bench_json) and os.path.getsize(bench_json):
+        # the stamp names THIS tree's sources: refuse a profile of other sources
+        import json
+        profiled = json.loads(open(bench_json).read().strip().splitlines()[-1])["build"]["kernel_source_hash"]
+        if profiled != source_hash():
+            sys.exit(f"refused: {prof} profiled kernel sources {profiled}, this tree is {source_hash()}")
         lines += ["## bench.py line (run under rocprofv3 --kernel-trace --stats)", "", "```",
                   open(bench_json).read().strip(), "```", ""]
     durations = {}
