@@ -340,8 +340,14 @@ __device__ int tokenize(const DevIndex &ix, const uint8_t *blob, uint64_t beg, u
                 }
             }
         }
-        if (!NEED && p < end) {   // left early: count the rest (the tail list's choice), hand the topic over
-            L = lev + 1 + count_slashes(blob, p, end);
+        if (!NEED && p < end) {   // left early: hand the topic over to the tail lists
+            // The level count only picks the tail list.  With no binary key
+            // deeper than this store and a trie the LDS tail resolves, every
+            // count from here on picks the LDS list (need_levels <= depth), so
+            // the rest is not scanned: a long topic made its whole wave wait
+            const bool any = ix.xlen_max <= S::maxl && ix.depth + 2 <= (uint32_t)MID_L &&
+                             end - beg < (uint64_t)MAX_LEVELS;
+            L = any ? lev + 1 : lev + 1 + count_slashes(blob, p, end);
             return RC_DEEP;
         }
         park();
