@@ -400,7 +400,9 @@ def main():
             # the PCIe bound this implies: plain pinned copies of 256 MiB, both directions at once
             pc = (ctypes.c_double * 4)()
             assert hb.tmb_pcie(local, 256 << 20, 16, 4, pc) == 0
-            per = max(h2d / (pc[2] * 1e9), d2h / (pc[3] * 1e9)) if pc[2] > 0 and pc[3] > 0 else 0.0   # s per batch at the ceiling
+            # the bound: full duplex at each direction's one-way peak (the simultaneous
+            # two-stream copy rate, both_each, varies 28-44 GB/s between runs)
+            per = max(h2d / (pc[0] * 1e9), d2h / (pc[1] * 1e9)) if pc[0] > 0 and pc[1] > 0 else 0.0
             hostfed["pcie_ceiling_GBps"] = {"h2d_alone": round(pc[0], 1), "d2h_alone": round(pc[1], 1),
                                             "both_each": round(pc[2], 1)}
             if per > 0:

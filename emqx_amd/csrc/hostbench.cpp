@@ -348,10 +348,13 @@ int tmb_pcie(int device, uint64_t bytes, int chunks, int reps, double *out) {
         return (double)c * chunks * reps / (now_s() - t0) / 1e9;
     };
     run(true, true);   // warm
-    out[0] = run(true, false);
-    out[1] = run(false, true);
-    const double both = run(true, true);   // each direction moved the same bytes in that time
-    out[2] = out[3] = both;
+    out[0] = out[1] = out[2] = 0;
+    for (int k = 0; k < 3; k++) {   // best of three (the simultaneous rate varies between runs)
+        out[0] = std::max(out[0], run(true, false));
+        out[1] = std::max(out[1], run(false, true));
+        out[2] = std::max(out[2], run(true, true));   // each direction moved the same bytes in that time
+    }
+    out[3] = out[2];
     (void)hipStreamDestroy(a); (void)hipStreamDestroy(b);
     (void)hipFree(din); (void)hipFree(dout); (void)hipHostFree(hin); (void)hipHostFree(hout);
     return TM_OK;
