@@ -149,8 +149,12 @@ def _rand_filter(r, levels):
     return b"/".join(out)
 
 
-@pytest.mark.parametrize("seed", range(8))
+@pytest.mark.parametrize("seed", range(24))
 def test_random_sets_vs_oracle(torch_dev, seed):
+    """Random filter and topic sets (empty levels, '$' levels, words with '+'/'#'
+    inside, long words, word-list keys), through the one-launch path (a few
+    hundred topics) and the lane walk (> 64k topics), the first hit, and after
+    deletes and re-inserts."""
     r = random.Random(0x454D5158 + 100 + seed)
     topics = [b"/".join(_rand_level(r) for _ in range(r.randint(1, 12))) for _ in range(400)]
     topics += [b"a/+/b", b"#", b"", b"/", b"$SYS", b"$"]
@@ -164,6 +168,13 @@ def test_random_sets_vs_oracle(torch_dev, seed):
     o = oracle_of(fs, flags)
     ts = items_of(topics)
     assert_same(ix, o, ts)
+    big = items_of(topics * (66_000 // len(topics) + 1))        # > 64k topics: lane walk + tail kernels
+    assert_same(ix, o, big)
+    first, found = ix.first_batch(ts.blob, ts.offs)
+    cnt, _, ohit, ovals = o.match_batch(ts.blob, ts.offs)
+    assert np.array_equal(found == 2, cnt < 0)                   # badarg
+    for i in np.nonzero(cnt > 0)[0]:
+        assert found[i] == 1 and first[i] == ovals[ohit[i]]
     # deletes (and re-inserts) as deltas, then match again
     dele = sorted(r.sample(range(len(filters)), 150))
     ops = np.zeros(len(dele), np.uint8)
