@@ -160,10 +160,12 @@ def main():
     t = time.time()
     l0map = None
     if level0:
-        # every rank draws the same owner map from the same sample, then keeps
-        # its own words' filters and the '+'/'#'-rooted ones, chunk by chunk
+        # every rank draws the same owner map from the same samples (filters, and
+        # a publish sample: words spread by publish load under a filter cap),
+        # then keeps its own words' filters and the '+'/'#'-rooted ones, chunk by chunk
         K = max(1, nf // 10_000_000)
-        l0map = shard.Level0Map.from_items(world, wl.filters(gen_cfg, nf, shard=0, nshards=K))
+        l0map = shard.Level0Map.from_items(world, wl.filters(gen_cfg, nf, shard=0, nshards=K),
+                                           topics=wl.topics(gen_cfg, nf, 200_000, first=1 << 40))
         parts = []
         for k in range(K):
             fk = wl.filters(gen_cfg, nf, shard=k, nshards=K)

@@ -218,40 +218,75 @@ def _word_key(w: bytes) -> int:
     return int.from_bytes(w.ljust(8, b"\0"), "little") if len(w) <= 8 else -1
 
 
+def _word_counts(s, sample: int) -> dict:
+    """First-level word -> occurrences among the first `sample` items of s."""
+    n = min(len(s), sample)
+    sub = s.slice(0, n) if n < len(s) else s
+    key, long_, st, en = level0_keys(sub.blob, sub.offs)
+    counts = {}
+    u, c = np.unique(key[~long_], return_counts=True)
+    for k, cnt in zip(u.tolist(), c.tolist()):
+        counts[int(k).to_bytes(8, "little").rstrip(b"\0")] = cnt
+    for i in np.flatnonzero(long_).tolist():
+        w = sub.blob[st[i]:en[i]].tobytes()
+        counts[w] = counts.get(w, 0) + 1
+    return counts
+
+
 class Level0Map:
-    """Which rank owns each first-level word; '+' and '#' are everyone's."""
+    """Which rank owns each first-level word; '+' and '#' are everyone's.
+
+    Without a publish sample the words are spread by filter count (greedy,
+    heaviest first, onto the least loaded rank).  With one (`publish`: word ->
+    publishes in a recent sample), a rank's time goes with the publishes routed
+    to it -- each walks one shard -- so the words are spread by publish count
+    instead, while no rank takes more than `mem_slack` x its share of the
+    filters (its HBM): a hot tenant prefix no longer lands on a rank that
+    already holds other busy words.  One word that alone carries more than 1/N
+    of the publishes stays one rank's: splitting it needs its second level in
+    the key."""
 
     PLUS, HASH = _word_key(b"+"), _word_key(b"#")
 
-    def __init__(self, world: int, counts: dict):
+    def __init__(self, world: int, counts: dict, publish: dict | None = None, mem_slack: float = 1.25):
         self.world = world
-        load = [0] * world
         self.table = {}
-        for w, c in sorted(counts.items(), key=lambda x: (-x[1], x[0])):
-            if w in (b"+", b"#"):
-                continue
-            r = min(range(world), key=lambda q: (load[q], q))
-            self.table[w] = r
-            load[r] += c
+        words = [w for w in counts if w not in (b"+", b"#")]
+        if publish:
+            words += [w for w in publish if w not in counts and w not in (b"+", b"#")]
+            tot_f = sum(counts.get(w, 0) for w in words)
+            cap = mem_slack * tot_f / world + max((counts.get(w, 0) for w in words), default=0)
+            pload, fload = [0] * world, [0] * world
+            for w in sorted(words, key=lambda x: (-publish.get(x, 0), -counts.get(x, 0), x)):
+                f = counts.get(w, 0)
+                fit = [q for q in range(world) if fload[q] + f <= cap] or list(range(world))
+                r = min(fit, key=lambda q: (pload[q], fload[q], q))
+                self.table[w] = r
+                pload[r] += publish.get(w, 0)
+                fload[r] += f
+        else:
+            load = [0] * world
+            for w in sorted(words, key=lambda x: (-counts[x], x)):
+                r = min(range(world), key=lambda q: (load[q], q))
+                self.table[w] = r
+                load[r] += counts[w]
         known = [(_word_key(w), r) for w, r in self.table.items() if len(w) <= 8]
         known.sort()
         self._keys = np.array([k for k, _ in known], np.uint64)
         self._ranks = np.array([r for _, r in known], np.int64)
 
     @classmethod
-    def from_items(cls, world: int, s, sample: int = 1_000_000):
-        """The map over the first `sample` items of a filter set."""
-        n = min(len(s), sample)
-        sub = s.slice(0, n) if n < len(s) else s
-        key, long_, st, en = level0_keys(sub.blob, sub.offs)
-        counts = {}
-        u, c = np.unique(key[~long_], return_counts=True)
-        for k, cnt in zip(u.tolist(), c.tolist()):
-            counts[int(k).to_bytes(8, "little").rstrip(b"\0")] = cnt
-        for i in np.flatnonzero(long_).tolist():
-            w = sub.blob[st[i]:en[i]].tobytes()
-            counts[w] = counts.get(w, 0) + 1
-        return cls(world, counts)
+    def from_items(cls, world: int, s, sample: int = 1_000_000, topics=None, topic_sample: int = 1_000_000):
+        """The map over the first `sample` items of a filter set and, when given,
+        the first `topic_sample` of a recent publish sample (every rank must pass
+        the same ones: the map is computed on each)."""
+        pub = _word_counts(topics, topic_sample) if topics is not None else None
+        return cls(world, _word_counts(s, sample), pub)
+
+    def loads(self, s) -> np.ndarray:
+        """Items of s each rank gets (routed by first level; '+'/'#' roots count on every rank)."""
+        o = self.owners(s)
+        return np.bincount(o[o >= 0], minlength=self.world) + int((o == -1).sum())
 
     def owner_of_word(self, w: bytes) -> int:
         r = self.table.get(w)

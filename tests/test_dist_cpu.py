@@ -224,3 +224,30 @@ def test_level0_map_is_deterministic_and_wild_roots_replicate():
     # balanced: no rank owns more than 1.5x its share of the literal-rooted filters
     cnt = np.bincount(own[own >= 0], minlength=4)
     assert cnt.max() <= 1.5 * cnt.sum() / 4
+
+
+def test_level0_map_balances_publish_load():
+    """With a publish sample the first-level words are spread by publish count
+    under a per-rank filter cap: a hot tenant prefix gets a rank to itself
+    instead of sharing one with other words picked by filter count."""
+    from emqx_amd import shard
+    words = [b"w%02d" % i for i in range(16)]
+    counts = {w: 1000 for w in words}                       # filters: uniform
+    publish = {w: 100 for w in words}
+    publish[words[0]] = 4000                                # 4000 of 5500 publishes on one word
+    by_f = shard.Level0Map(4, counts)
+    by_p = shard.Level0Map(4, counts, publish)
+
+    def rank_loads(m, weights):
+        out = [0] * 4
+        for w in words:
+            out[m.table[w]] += weights[w]
+        return out
+    hot_f = rank_loads(by_f, publish)[by_f.table[words[0]]]
+    hot_p = rank_loads(by_p, publish)[by_p.table[words[0]]]
+    assert hot_f == 4000 + 3 * 100 and hot_p == 4000        # the hot word's rank holds nothing else busy
+    fl = rank_loads(by_p, counts)
+    assert max(fl) <= 1.25 * sum(fl) / 4 + 1000             # HBM per rank stays within the cap
+    assert sorted(by_p.table) == sorted(words)
+    # every rank computes the same map from the same samples
+    assert shard.Level0Map(4, counts, publish).table == by_p.table
