@@ -214,6 +214,44 @@ def level0_keys(blob: np.ndarray, offs: np.ndarray):
     return key, ln > 8, s, e
 
 
+def _mix(x: np.ndarray) -> np.ndarray:
+    """splitmix64 finaliser over a u64 array (wrapping arithmetic)."""
+    x = np.asarray(x, np.uint64).copy()
+    with np.errstate(over="ignore"):
+        x ^= x >> np.uint64(30)
+        x *= np.uint64(0xBF58476D1CE4E5B9)
+        x ^= x >> np.uint64(27)
+        x *= np.uint64(0x94D049BB133111EB)
+        x ^= x >> np.uint64(31)
+    return x
+
+
+def level1_info(blob: np.ndarray, offs: np.ndarray, e0: np.ndarray):
+    """Per item, given the end e0 of its first level: whether it has a second
+    level, whether that level is exactly '+' or '#', and a u64 hash of the
+    second level's bytes (its first 16 bytes and its length)."""
+    ends = offs[1:].astype(np.int64)
+    has1 = e0 < ends
+    b1 = np.minimum(e0 + 1, ends)
+    sl = np.flatnonzero(blob == ord("/"))
+    if len(sl):
+        j = np.searchsorted(sl, b1)
+        e1 = np.where(j < len(sl), sl[np.minimum(j, len(sl) - 1)], ends)
+    else:
+        e1 = ends
+    e1 = np.minimum(e1, ends)
+    ln = np.where(has1, e1 - b1, 0)
+    top = len(blob) - 1
+    first = blob[np.minimum(b1, top)]
+    wild = has1 & (ln == 1) & ((first == ord("+")) | (first == ord("#")))
+    ka = np.zeros(len(b1), np.uint64)
+    kb = np.zeros(len(b1), np.uint64)
+    for k in range(8):
+        ka |= np.where(ln > k, blob[np.minimum(b1 + k, top)], 0).astype(np.uint64) << np.uint64(8 * k)
+        kb |= np.where(ln > k + 8, blob[np.minimum(b1 + k + 8, top)], 0).astype(np.uint64) << np.uint64(8 * k)
+    return has1, wild, _mix(ka ^ _mix(kb ^ ln.astype(np.uint64)))
+
+
 def _word_key(w: bytes) -> int:
     return int.from_bytes(w.ljust(8, b"\0"), "little") if len(w) <= 8 else -1
 
@@ -242,21 +280,34 @@ class Level0Map:
     to it -- each walks one shard -- so the words are spread by publish count
     instead, while no rank takes more than `mem_slack` x its share of the
     filters (its HBM): a hot tenant prefix no longer lands on a rank that
-    already holds other busy words.  One word that alone carries more than 1/N
-    of the publishes stays one rank's: splitting it needs its second level in
-    the key."""
+    already holds other busy words.  A word that alone carries more than 1/N
+    of the publishes (one tenant prefix W) is split by its second level: the
+    filters W/w1/... go to the rank of (W, w1), those whose second level is
+    '+' or '#' (and W/#, which also matches the topic W) to every rank, the
+    filter W itself to the rank of (W, -); a topic W/w1/... goes to the rank of
+    (W, w1) and finds there every filter that can match it, so its list is
+    still the unsharded one, order included."""
 
     PLUS, HASH = _word_key(b"+"), _word_key(b"#")
 
     def __init__(self, world: int, counts: dict, publish: dict | None = None, mem_slack: float = 1.25):
         self.world = world
         self.table = {}
+        self.split = set()   # words split by their second level
         words = [w for w in counts if w not in (b"+", b"#")]
         if publish:
             words += [w for w in publish if w not in counts and w not in (b"+", b"#")]
-            tot_f = sum(counts.get(w, 0) for w in words)
+            tot_p = sum(publish.get(w, 0) for w in words)
+            if world > 1:
+                self.split = {w for w in words if len(w) <= 8 and publish.get(w, 0) * world > tot_p}
+            pload, fload = [0.0] * world, [0.0] * world
+            for w in self.split:   # spread over every rank (second levels by hash)
+                for q in range(world):
+                    pload[q] += publish.get(w, 0) / world
+                    fload[q] += counts.get(w, 0) / world
+            words = [w for w in words if w not in self.split]
+            tot_f = sum(fload) + sum(counts.get(w, 0) for w in words)
             cap = mem_slack * tot_f / world + max((counts.get(w, 0) for w in words), default=0)
-            pload, fload = [0] * world, [0] * world
             for w in sorted(words, key=lambda x: (-publish.get(x, 0), -counts.get(x, 0), x)):
                 f = counts.get(w, 0)
                 fit = [q for q in range(world) if fload[q] + f <= cap] or list(range(world))
@@ -270,6 +321,7 @@ class Level0Map:
                 r = min(range(world), key=lambda q: (load[q], q))
                 self.table[w] = r
                 load[r] += counts[w]
+        self._split_keys = np.array(sorted(_word_key(w) for w in self.split), np.uint64)
         known = [(_word_key(w), r) for w, r in self.table.items() if len(w) <= 8]
         known.sort()
         self._keys = np.array([k for k, _ in known], np.uint64)
@@ -293,7 +345,8 @@ class Level0Map:
         return r if r is not None else zlib.crc32(w) % self.world
 
     def owners(self, s) -> np.ndarray:
-        """Per item: its first level's owner, or -1 for '+' / '#' (every rank)."""
+        """Per item: its owner, or -1 (every rank): a '+' / '#' first level, or a
+        '+' / '#' second level under a split word."""
         key, long_, st, en = level0_keys(s.blob, s.offs)
         out = np.empty(len(key), np.int64)
         if len(self._keys):
@@ -308,6 +361,16 @@ class Level0Map:
         miss = np.flatnonzero(~hit & ~wild)
         for i in miss.tolist():
             out[i] = self.owner_of_word(s.blob[st[i]:en[i]].tobytes())
+        if len(self._split_keys):
+            j = np.minimum(np.searchsorted(self._split_keys, key), len(self._split_keys) - 1)
+            hot = np.flatnonzero((self._split_keys[j] == key) & ~long_)
+            if len(hot):
+                has1, wild, h = level1_info(s.blob, s.offs, en)
+                kk = key[hot]
+                w = np.uint64(self.world)
+                r1 = (_mix(h[hot] ^ _mix(kk)) % w).astype(np.int64)
+                r0 = (_mix(kk ^ np.uint64(0x9E3779B97F4A7C15)) % w).astype(np.int64)
+                out[hot] = np.where(~has1[hot], r0, np.where(wild[hot], -1, r1))
         return out
 
     def filter_rows(self, s, rank: int) -> np.ndarray:
@@ -316,5 +379,7 @@ class Level0Map:
         return np.flatnonzero((o == rank) | (o == -1))
 
     def topic_rows(self, s, rank: int) -> np.ndarray:
-        """Indices of the topics rank `rank` matches."""
-        return np.flatnonzero(self.owners(s) == rank)
+        """Indices of the topics rank `rank` matches (a topic whose first or
+        split second level is '+' / '#' -- badarg -- goes to rank 0)."""
+        o = self.owners(s)
+        return np.flatnonzero(np.where(o < 0, 0, o) == rank)

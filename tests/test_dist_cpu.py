@@ -234,9 +234,10 @@ def test_level0_map_balances_publish_load():
     words = [b"w%02d" % i for i in range(16)]
     counts = {w: 1000 for w in words}                       # filters: uniform
     publish = {w: 100 for w in words}
-    publish[words[0]] = 4000                                # 4000 of 5500 publishes on one word
+    publish[words[0]] = 450                                 # 23 % of the publishes on one word (< 1/4: not split)
     by_f = shard.Level0Map(4, counts)
     by_p = shard.Level0Map(4, counts, publish)
+    assert not by_p.split
 
     def rank_loads(m, weights):
         out = [0] * 4
@@ -245,9 +246,60 @@ def test_level0_map_balances_publish_load():
         return out
     hot_f = rank_loads(by_f, publish)[by_f.table[words[0]]]
     hot_p = rank_loads(by_p, publish)[by_p.table[words[0]]]
-    assert hot_f == 4000 + 3 * 100 and hot_p == 4000        # the hot word's rank holds nothing else busy
+    assert hot_f == 450 + 3 * 100 and hot_p == 450          # the hot word's rank holds nothing else busy
     fl = rank_loads(by_p, counts)
     assert max(fl) <= 1.25 * sum(fl) / 4 + 1000             # HBM per rank stays within the cap
     assert sorted(by_p.table) == sorted(words)
     # every rank computes the same map from the same samples
     assert shard.Level0Map(4, counts, publish).table == by_p.table
+    # past 1/N of the publishes a word is split by its second level instead
+    publish[words[0]] = 4000
+    assert shard.Level0Map(4, counts, publish).split == {words[0]}
+
+
+def test_level0_split_hot_prefix_equals_one_index():
+    """One tenant prefix carrying most publishes is split by its second level
+    (filters under it by (prefix, second word), its '+'/'#' second levels on
+    every rank): each rank's lists for the topics routed to it equal the
+    unsharded index's, order included, and the hot topics spread over the
+    ranks instead of landing on one."""
+    import random
+    import sys
+    from pathlib import Path
+    sys.path.insert(0, str(Path(__file__).resolve().parent.parent / "oracle"))
+    from pyoracle import Oracle
+    from emqx_amd import _native, shard, workload as wl
+    r = random.Random(0x454D5158 + 901)
+    base = wl.filters(1, 3_000)
+    hot = []
+    for i in range(1500):
+        d = b"d%d" % r.randrange(400)
+        hot.append(r.choice([b"tnt/%s/+/x" % d, b"tnt/%s/#" % d, b"tnt/%s/s/%d" % (d, i % 7), b"tnt/%s" % d]))
+    hot += [b"tnt", b"tnt/#", b"tnt/+/s/#", b"tnt/+", b"tnt/", b"tnt//x", b"+/+/s/#", b"#"]
+    items = base.items() + hot
+    blob, offs = _native.pack_strings(items)
+    fs = wl.ItemSet(blob, offs, np.arange(len(items), dtype=np.uint32), np.zeros(len(items), np.uint8))
+    tl = [b"tnt/d%d/%s" % (r.randrange(400), r.choice([b"a/x", b"s/3", b"s", b"q/w/e"])) for _ in range(3000)]
+    tl += [b"tnt", b"tnt/", b"tnt//x", b"tnt/d1"] + wl.topics(1, 3_000, 1000).items()
+    tb, to = _native.pack_strings(tl)
+    ts = wl.ItemSet(tb, to, np.zeros(len(tl), np.uint32), np.zeros(len(tl), np.uint8))
+    world = 4
+    m = shard.Level0Map.from_items(world, fs, topics=ts)
+    assert b"tnt" in m.split
+    full = Oracle()
+    full.apply(np.ones(len(fs), np.uint8), fs.blob, fs.offs, fs.vals)
+    _, _, fh, fv = full.match_batch(ts.blob, ts.offs)
+    per_rank = []
+    for rank in range(world):
+        rows = m.filter_rows(fs, rank)
+        sub = wl.take(fs, rows)
+        o = Oracle()
+        o.apply(np.ones(len(sub), np.uint8), sub.blob, sub.offs, sub.vals)
+        trows = m.topic_rows(ts, rank)
+        per_rank.append(len(trows))
+        tsub = wl.take(ts, trows)
+        _, _, h, v = o.match_batch(tsub.blob, tsub.offs)
+        for j, i in enumerate(trows.tolist()):
+            assert np.array_equal(v[h[j]:h[j + 1]], fv[fh[i]:fh[i + 1]]), tl[i]
+    assert sum(per_rank) == len(tl)
+    assert max(per_rank) <= 1.4 * len(tl) / world, per_rank   # the hot prefix spread, not on one rank
