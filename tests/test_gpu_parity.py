@@ -1525,6 +1525,43 @@ def test_level0_shards_equal_one_index(torch_dev, world):
     assert (seen == 1).all()
 
 
+def test_level0_split_hot_prefix_on_device(torch_dev):
+    """A tenant prefix with most of the publishes, split by its second level
+    over 3 shard indices on one GPU (shard.Level0Map with a publish sample):
+    every topic matched on its owner's shard gives the unsharded oracle's
+    list, order included, in the one-launch and lane walks."""
+    from emqx_amd import shard
+    r = random.Random(0x454D5158 + 902)
+    base = wl.filters(3, 50_000).items()
+    hot = []
+    for i in range(20_000):
+        d = b"d%d" % r.randrange(3000)
+        hot.append(r.choice([b"tnt/%s/+/x" % d, b"tnt/%s/#" % d, b"tnt/%s/s/%d" % (d, i % 7), b"tnt/%s" % d,
+                             b"tnt/+/%s" % d]))
+    hot += [b"tnt", b"tnt/#", b"tnt/+/s/#", b"tnt/+", b"tnt/", b"#", b"+/+/s/#"]
+    fs = items_of(base + hot)
+    tl = [b"tnt/d%d/%s" % (r.randrange(3000), r.choice([b"a/x", b"s/3", b"s", b"d7"])) for _ in range(200_000)]
+    tl += wl.topics(3, 50_000, 20_000).items() + [b"tnt", b"tnt/", b"tnt//x"]
+    ts = items_of(tl)
+    o = oracle_of(fs)
+    _, _, ohit, ovals = o.match_batch(ts.blob, ts.offs)
+    m = shard.Level0Map.from_items(3, fs, topics=ts)
+    assert b"tnt" in m.split
+    seen = np.zeros(len(ts), np.int64)
+    for rk in range(3):
+        ix = gpu_index(wl.take(fs, m.filter_rows(fs, rk)))
+        rows = m.topic_rows(ts, rk)
+        assert len(rows) < 0.45 * len(ts)
+        seen[rows] += 1
+        for part in (rows[:3000], rows):   # one launch / > 64k topics on the lane walk when big enough
+            sub = wl.take(ts, part)
+            hit, vals, err = ix.match_batch(sub.blob, sub.offs)
+            assert not err.any()
+            for k, t in enumerate(part.tolist()):
+                assert np.array_equal(vals[hit[k]:hit[k + 1]], ovals[ohit[t]:ohit[t + 1]]), (rk, ts.item(t))
+    assert (seen == 1).all()
+
+
 def test_wide_node_bitmaps_follow_vocab_growth(torch_dev):
     """A wide node's bitmap must cover every word id: 40k new words arrive while
     it is wide (the bitmaps regrow), then children with those new ids are added
