@@ -79,7 +79,10 @@ def parse():
     p.add_argument("--batch", type=int, default=1_000_000, help="topics per GPU per step")
     p.add_argument("--rotate", type=int, default=4, help="distinct topic batches the steps rotate over")
     p.add_argument("--deltas", type=int, default=100,
-                   help="c5: deltas applied per step (100 x ~2.5k steps/s = 2.5x the configured 100k deltas/s)")
+                   help="c5: deltas applied per application (100 x ~2.5k steps/s = 2.5x the configured 100k deltas/s)")
+    p.add_argument("--delta-every", type=int, default=1,
+                   help="c5: steps between delta applications (e.g. --deltas 1000 --delta-every 10: the same rate in "
+                        "the router syncer's batch size, emqx_router_syncer.erl's <= 1000 ops per run_batch)")
     p.add_argument("--streams", type=int, default=None,
                    help="HIP streams the steps rotate over (batch k+1's walk overlaps batch k's scan/emit); "
                         "default 3, and 1 for c5 with one copy of the tables: a churn step's patch then waits "
@@ -228,10 +231,11 @@ def main():
 
     # c5: the delta stream, generated up front (host buffers, as the syncer hands them over)
     dchunks = []
+    every = max(1, a.delta_every)
     if a.config == "c5":
-        nd = a.deltas * (a.steps + a.warmup + 1)
-        dl = wl.deltas(nf, 0, nd)
-        dchunks = [dl.slice(k * a.deltas, (k + 1) * a.deltas) for k in range(a.steps + a.warmup + 1)]
+        napp = (a.steps + a.warmup + 1) // every + 1
+        dl = wl.deltas(nf, 0, a.deltas * napp)
+        dchunks = [dl.slice(k * a.deltas, (k + 1) * a.deltas) for k in range(napp)]
     dpos = [0]
     kstep = [0]
     apply_s = [0.0]   # c5: host time inside tm_apply_deltas (the syncer's side of a churn step)
@@ -243,7 +247,7 @@ def main():
         o = outs[k % nstreams]
         d_blob, d_offs = d_in[k % R]
         sid = streams[k % nstreams].cuda_stream
-        if dchunks:
+        if dchunks and k % every == 0:
             d = dchunks[dpos[0]]
             dpos[0] += 1
             ta = time.perf_counter()
@@ -589,8 +593,9 @@ def main():
     }
     res.update(res_extra)
     if dchunks:
-        res["deltas_per_step"] = a.deltas
-        res["deltas_per_s"] = round(a.deltas * a.steps / el_max, 1)
+        res["deltas_per_step"] = a.deltas / every
+        res["delta_batch"] = {"deltas": a.deltas, "every_steps": every}
+        res["deltas_per_s"] = round(a.deltas / every * a.steps / el_max, 1)
         res["delta_apply_host_ms_per_step"] = round(apply_s[0] / a.steps * 1e3, 4)
     if filter_sharded:
         res["merged_hits_this_rank_slice"] = merged_total
