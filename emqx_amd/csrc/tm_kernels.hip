@@ -1529,6 +1529,7 @@ constexpr int WR = 64 * RCAP;   // ranges per wave
 typedef uint4 __attribute__((aligned(4))) uint4u;   // dword-aligned 16-B load (global_load_dwordx4)
 constexpr int EMIT_Q = 1;   // quads per lane per iteration (loads in flight before the stores)
 constexpr uint64_t EMIT_RUNS = 16;   // average run length from which a wave copies run by run
+constexpr uint8_t RF_INLINE = 1, RF_SKIP = 2;   // s_flg: a one-value run kept inline / an overflowed topic's positions
 
 // One block = one tile of 256 topics: finishes the scan (tile prefix + local
 // exclusive scan -> hit_offs), then each wave flattens its 64 topics' value
@@ -1540,9 +1541,13 @@ constexpr uint64_t EMIT_RUNS = 16;   // average run length from which a wave cop
 // RCAP ranges are skipped (k_rewalk_tail writes them).
 __global__ __launch_bounds__(EMIT_BLOCK) void k_emit(DevIndex ix, Workspace ws, uint64_t n,
                                                      uint64_t *hit_offs, uint32_t *out, uint64_t cap) {
+    // 9 B per range: a range's count is the distance to the next one's start
+    // (s_rel[R] = the wave's span), so 18 KiB per block: 8 waves per SIMD
+    // instead of 6 with an explicit count (C3 batch 0.338 -> 0.327 ms with the
+    // range prefetch below, profiles/r3/emit/)
     __shared__ uint32_t s_off[EMIT_WAVES][WR];
-    __shared__ uint32_t s_rel[EMIT_WAVES][WR];
-    __shared__ uint32_t s_cnt[EMIT_WAVES][WR];
+    __shared__ uint32_t s_rel[EMIT_WAVES][WR + 1];
+    __shared__ uint8_t s_flg[EMIT_WAVES][WR];
     __shared__ uint64_t s_w[4];
     __shared__ uint64_t s_end[EMIT_WAVES];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -1551,6 +1556,16 @@ __global__ __launch_bounds__(EMIT_BLOCK) void k_emit(DevIndex ix, Workspace ws, 
     // per-topic walk outputs are read once: non-temporal loads keep them from
     // evicting the concurrent walk's lines (bench, three streams: +1.3 %)
     const uint32_t c = valid ? __builtin_nontemporal_load(ws.cnt + t) : 0;
+    uint32_t nr = valid ? __builtin_nontemporal_load(ws.nr + t) : 0;
+    const bool ovf = nr > RCAP;   // written by k_rewalk_tail: one skip range over its positions
+    if (ovf) nr = 0;
+    // the topic's ranges do not depend on the scan: all its loads are issued
+    // here and fly across it (one round trip instead of one per range; loading
+    // all RCAP slots whatever nr is measured slower: +55 % range bytes)
+    uint64_t gr[RCAP];
+#pragma unroll
+    for (int i = 0; i < RCAP; i++)
+        gr[i] = (uint32_t)i < nr ? __builtin_nontemporal_load(reinterpret_cast<const uint64_t *>(ws.rng) + (uint64_t)i * n + t) : 0;
     uint64_t total;
     const uint64_t my = ws.blk[blockIdx.x] + block_excl_scan(c, total, s_w);
     // the GPU never reads the offsets (or the err flags) back: non-temporal
@@ -1564,20 +1579,25 @@ __global__ __launch_bounds__(EMIT_BLOCK) void k_emit(DevIndex ix, Workspace ws, 
     if (t0 >= n) return;   // whole wave leaves; only wave-level sync below
     const uint64_t base = __shfl(my, 0, 64);
     const uint64_t endp = s_end[wv];
-    uint32_t nr = valid ? __builtin_nontemporal_load(ws.nr + t) : 0;
-    if (nr > RCAP) nr = 0;   // written by k_rewalk_tail
     const uint32_t rel = (uint32_t)(my - base);
     uint32_t R;
-    const uint32_t r0 = wave_excl_scan32(nr, R);
+    const uint32_t r0 = wave_excl_scan32(ovf ? (c ? 1u : 0u) : nr, R);
+    if (ovf && c) {
+        s_off[wv][r0] = 0;
+        s_rel[wv][r0] = rel;
+        s_flg[wv][r0] = RF_SKIP;
+    }
     uint32_t acc = 0;
-    for (uint32_t i = 0; i < nr; i++) {
-        const uint64_t g64 = __builtin_nontemporal_load(reinterpret_cast<const uint64_t *>(ws.rng) + (uint64_t)i * n + t);
-        const uint2 g = make_uint2((uint32_t)g64, (uint32_t)(g64 >> 32));
-        s_off[wv][r0 + i] = g.x;
+#pragma unroll
+    for (int i = 0; i < RCAP; i++) {
+        if ((uint32_t)i >= nr) break;
+        const uint2 g = make_uint2((uint32_t)gr[i], (uint32_t)(gr[i] >> 32));
+        s_off[wv][r0 + i] = g.x;          // RUN_INLINE: the value itself
         s_rel[wv][r0 + i] = rel + acc;
-        s_cnt[wv][r0 + i] = g.y;          // device count (RUN_INLINE: g.x is the value)
+        s_flg[wv][r0 + i] = (g.y & RUN_INLINE) ? RF_INLINE : 0;
         acc += g.y & RUN_CNT;
     }
+    if (lane == 0) s_rel[wv][R] = (uint32_t)(endp - base);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1600,13 +1620,14 @@ __global__ __launch_bounds__(EMIT_BLOCK) void k_emit(DevIndex ix, Workspace ws, 
         // load or cross-lane step per quad costs more than the partial writes).
         typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
         for (uint32_t i = 0; i < R; i++) {
-            const uint32_t ro = s_off[wv][i], rc = s_cnt[wv][i];
+            const uint32_t ro = s_off[wv][i], rf = s_flg[wv][i];
             const uint64_t P = base + s_rel[wv][i];
-            if (rc & RUN_INLINE) {
+            if (rf & RF_SKIP) continue;
+            if (rf & RF_INLINE) {
                 if (lane == 0 && P < cap) out[P] = ro;
                 continue;
             }
-            const uint64_t E = P + (rc & RUN_CNT);
+            const uint64_t E = base + s_rel[wv][i + 1];
             for (uint64_t Q = (P >> 2) + lane; (Q << 2) < E; Q += 64) {
                 const uint64_t p0 = Q << 2;
                 const uint4 a = *reinterpret_cast<const uint4u *>(ix.vals + ro + (int64_t)(p0 - P));
@@ -1642,8 +1663,8 @@ __global__ __launch_bounds__(EMIT_BLOCK) void k_emit(DevIndex ix, Workspace ws, 
             r = lo;
         }
         if (q < q1 && p0 >= base && p0 + 3 < endp) {   // whole quad inside one run: one 16-B load
-            const uint32_t rs = s_rel[wv][r], rc = s_cnt[wv][r];
-            if (!(rc & RUN_INLINE) && first >= rs && first + 3 - rs < (rc & RUN_CNT)) {
+            const uint32_t rs = s_rel[wv][r], re = s_rel[wv][r + 1];
+            if (!s_flg[wv][r] && first >= rs && first + 3 < re) {
                 const uint4 a = *reinterpret_cast<const uint4u *>(ix.vals + s_off[wv][r] + (first - rs));
                 v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
                 ok[0] = ok[1] = ok[2] = ok[3] = true;
@@ -1657,10 +1678,9 @@ __global__ __launch_bounds__(EMIT_BLOCK) void k_emit(DevIndex ix, Workspace ws, 
             if (q >= q1 || p < base || p >= endp) continue;
             const uint32_t x = (uint32_t)(p - base);
             while (r + 1 < R && s_rel[wv][r + 1] <= x) r++;
-            const uint32_t rs = s_rel[wv][r];
-            const uint32_t rc = s_cnt[wv][r];
-            if (x >= rs && x - rs < (rc & RUN_CNT)) {
-                v[k] = (rc & RUN_INLINE) ? s_off[wv][r] : ix.vals[s_off[wv][r] + (x - rs)];
+            const uint32_t rs = s_rel[wv][r], rf = s_flg[wv][r];
+            if (!(rf & RF_SKIP) && x >= rs && x < s_rel[wv][r + 1]) {
+                v[k] = (rf & RF_INLINE) ? s_off[wv][r] : ix.vals[s_off[wv][r] + (x - rs)];
                 ok[k] = true;
             }
         }
