@@ -67,6 +67,10 @@ struct Workspace {
     uint2 *deep_stk;      // [DEEP_LANES * (MAX_LEVELS + 1)]
     uint8_t *deep_plus;   // [DEEP_LANES * MAX_LEVELS] '+' levels of each deep lane's path
     uint64_t *look;       // [n / SM_TOPICS + 4] one-launch path: per block, one look-back word (lb_word)
+    // list lengths of the last count-mode batch that finished here ([0, L_COUNT))
+    // and its topic count ([L_COUNT]; 0: none yet), written by the device into
+    // mapped host memory: the next batch sizes its tail grids from them
+    uint32_t *hint_h, *hint_d;
     uint64_t cap_n;
 };
 

@@ -1314,6 +1314,7 @@ DevIndex dev_view_build(tm_index *ix, int r) {
 void free_workspace(Workspace &w) {
     void *wb[] = {w.cnt, w.nr, w.rng, w.lists, w.list_n, w.blk, w.deep_wid, w.deep_stk, w.deep_plus, w.look};
     for (void *p : wb) if (p) (void)hipFree(p);
+    if (w.hint_h) (void)hipHostFree(w.hint_h);
     w = Workspace{};
 }
 
@@ -1447,6 +1448,9 @@ int ensure_ws(tm_index *ix, uint64_t n, Lane &ln) {
         HIPCHK(ix, hipMalloc(&w.deep_plus, (uint64_t)DEEP_LANES * MAX_LEVELS));
         HIPCHK(ix, hipMalloc(&w.list_n, LIST_SLOTS * 4));
         HIPCHK(ix, hipMemsetAsync(w.list_n, 0, LIST_SLOTS * 4, ln.s));
+        HIPCHK(ix, hipHostMalloc(&w.hint_h, (L_COUNT + 1) * 4, hipHostMallocMapped));
+        std::memset(w.hint_h, 0, (L_COUNT + 1) * 4);
+        HIPCHK(ix, hipHostGetDevicePointer(reinterpret_cast<void **>(&w.hint_d), w.hint_h, 0));
     }
     // the batch must see every patch shipped so far, whichever stream it went on
     if (ix->rep[ln.r].last_patch) HIPCHK(ix, hipStreamWaitEvent(ln.s, ix->rep[ln.r].last_patch, 0));

@@ -1384,23 +1384,45 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_small(DevIndex ix, Workspace 
 }
 
 constexpr int MID_BLOCK = 64;
-constexpr int MID_GRID = 512;                         // LDS-frontier blocks of the tail kernels
+constexpr int MID_GRID = 512;                         // LDS-frontier blocks of the tail kernels (at most)
 // k_walk_tail of a large count-mode batch: more LDS-frontier blocks (it takes
 // no grid-wide ticket then, so idle blocks cost only their dispatch).  512
 // blocks = 2 waves per CU: C3deep (100k topics of 33-64 levels per 1M batch)
 // spent 0.57 ms per batch in the tail; 2048: 0.25 ms
 constexpr int MID_GRID_BIG = 2048;
-constexpr int TAIL_GRID = MID_GRID + DEEP_LANES / 64; // + global-scratch blocks
+constexpr int MID_GRID_MIN = 32;
 
-// last block of a grid (atomic ticket) resets the list counters for the next batch
+// LDS-frontier blocks for a tail list: one lane per topic the list held in the
+// last count-mode batch on this workspace (scaled to this batch, x2 + 2048
+// topics of slack), between MID_GRID_MIN and `most`.  Idle blocks are not
+// free when other streams' walks fill the GPU: each waits for a workgroup
+// slot, so a 2049-block tail kernel took 110 us per C3 batch with three
+// streams (4 us alone); any grid is correct (the lists are walked grid-stride).
+static uint32_t tail_blocks(const Workspace &ws, uint64_t n, int list, uint32_t most) {
+    if (!ws.hint_h) return most;
+    const volatile uint32_t *h = ws.hint_h;
+    const uint32_t hn = h[L_COUNT];
+    if (!hn) return most;   // no count-mode batch has finished here yet
+    const double want = 2.0 * (double)h[list] * (double)n / (double)hn + 2048.0;
+    const double b = want / MID_BLOCK;
+    return b >= most ? most : (b <= MID_GRID_MIN ? (uint32_t)MID_GRID_MIN : (uint32_t)b);
+}
+
+// last block of a grid (atomic ticket) resets the list counters for the next
+// batch; hint_n != 0 (the count-mode batch's last kernel): it also leaves the
+// list lengths and hint_n in the workspace's mapped hint words (tail_blocks)
 // (no fence: a block only READ the list counters, and those loads completed
 // before its ticket was taken, so the reset cannot overtake them)
-__device__ __forceinline__ void reset_lists_if_last(const Workspace &ws) {
+__device__ __forceinline__ void reset_lists_if_last(const Workspace &ws, uint32_t hint_n = 0) {
     __syncthreads();
     if (threadIdx.x == 0) {
         const uint32_t ticket = atomicAdd(&ws.list_n[L_COUNT], 1u);
         if (ticket == gridDim.x - 1) {
-            for (int k = 0; k < L_COUNT; k++) atomicExch(&ws.list_n[k], 0u);
+            for (int k = 0; k < L_COUNT; k++) {
+                const uint32_t len = atomicExch(&ws.list_n[k], 0u);
+                if (hint_n && ws.hint_d) ws.hint_d[k] = len;
+            }
+            if (hint_n && ws.hint_d) ws.hint_d[L_COUNT] = hint_n;
             atomicExch(&ws.list_n[L_COUNT], 0u);
         }
     }
@@ -1475,18 +1497,18 @@ __device__ void rewalk(const DevIndex &ix, const uint8_t *blob, const uint64_t *
 
 __global__ __launch_bounds__(MID_BLOCK) void k_rewalk_tail(DevIndex ix, Workspace ws, uint64_t n, const uint8_t *blob,
                                                            const uint64_t *offs, const uint64_t *hit_offs,
-                                                           uint32_t *out, uint64_t cap) {
+                                                           uint32_t *out, uint64_t cap, uint32_t mid_grid) {
     __shared__ uint32_t s_wid[MID_L * MID_BLOCK];
     __shared__ uint32_t s_pend[(MID_L + 1) * MID_BLOCK];
     __shared__ uint8_t s_len[MID_L * MID_BLOCK];
-    if (blockIdx.x < MID_GRID) {
+    if (blockIdx.x < mid_grid) {
         const uint32_t cnt = ws.list_n[L_OVF_MID];
         const uint32_t *lst = ws.lists + (uint64_t)L_OVF_MID * n;
         LdsStore<MID_L> st{s_wid + threadIdx.x, s_pend + threadIdx.x, s_len + threadIdx.x, MID_BLOCK, 0};
-        for (uint32_t i = blockIdx.x * MID_BLOCK + threadIdx.x; i < cnt; i += MID_GRID * MID_BLOCK)
+        for (uint32_t i = blockIdx.x * MID_BLOCK + threadIdx.x; i < cnt; i += mid_grid * MID_BLOCK)
             rewalk(ix, blob, offs, lst[i], hit_offs, out, cap, st);
     } else {
-        const uint32_t lane = (blockIdx.x - MID_GRID) * 64 + threadIdx.x;
+        const uint32_t lane = (blockIdx.x - mid_grid) * 64 + threadIdx.x;
         const uint32_t cnt = ws.list_n[L_OVF_DEEP];
         const uint32_t *lst = ws.lists + (uint64_t)L_OVF_DEEP * n;
         GlobalStore st{ws.deep_wid + (uint64_t)lane * MAX_LEVELS, ws.deep_stk + (uint64_t)lane * (MAX_LEVELS + 1),
@@ -1494,7 +1516,7 @@ __global__ __launch_bounds__(MID_BLOCK) void k_rewalk_tail(DevIndex ix, Workspac
         for (uint32_t i = lane; i < cnt; i += DEEP_LANES)
             rewalk(ix, blob, offs, lst[i], hit_offs, out, cap, st);
     }
-    reset_lists_if_last(ws);
+    reset_lists_if_last(ws, n < 0xFFFFFFFFull ? (uint32_t)n : 0xFFFFFFFFu);
 }
 
 // tile totals -> exclusive tile prefixes; hit_offs[n] = grand total
@@ -1982,7 +2004,7 @@ hipError_t launch_match_phase1(const DevIndex &ix, const Workspace &ws, uint64_t
                                n, bytes, offs, o);
         if (ev_walk1 && (e = hipEventRecord(ev_walk1, s)) != hipSuccess) return e;
         // small batches: the tail kernel's last block also scans the (few) tile totals
-        const uint32_t mg = wave ? MID_GRID : MID_GRID_BIG;
+        const uint32_t mg = tail_blocks(ws, n, L_MID, wave ? MID_GRID : MID_GRID_BIG);
         hipLaunchKernelGGL(k_walk_tail<MODE_COUNT>, dim3(mg + DEEP_LANES / 64), dim3(MID_BLOCK), 0, s, ix, ws, n,
                            bytes, offs, o, (uint64_t)nb, wave ? hit_offs : nullptr, mg);
     }
@@ -1995,7 +2017,9 @@ hipError_t launch_match_phase2(const DevIndex &ix, const Workspace &ws, uint64_t
                                hipStream_t s) {
     if (!n) return hipSuccess;
     hipLaunchKernelGGL(k_emit, dim3(blocks_for(n, TILE)), dim3(EMIT_BLOCK), 0, s, ix, ws, n, hit_offs, out, cap);
-    hipLaunchKernelGGL(k_rewalk_tail, dim3(TAIL_GRID), dim3(MID_BLOCK), 0, s, ix, ws, n, bytes, offs, hit_offs, out, cap);
+    const uint32_t mg = tail_blocks(ws, n, L_OVF_MID, MID_GRID);
+    hipLaunchKernelGGL(k_rewalk_tail, dim3(mg + DEEP_LANES / 64), dim3(MID_BLOCK), 0, s, ix, ws, n, bytes, offs,
+                       hit_offs, out, cap, mg);
     return hipGetLastError();
 }
 
@@ -2031,7 +2055,7 @@ hipError_t launch_first(const DevIndex &ix, const Workspace &ws, uint64_t n, con
     else
         hipLaunchKernelGGL(k_walk_fast<MODE_FIRST>, dim3(blocks_for(n, WALK_BLOCK)), dim3(WALK_BLOCK), 0, s,
                            ix, ws, n, bytes, offs, o);
-    hipLaunchKernelGGL(k_walk_tail<MODE_FIRST>, dim3(TAIL_GRID), dim3(MID_BLOCK), 0, s, ix, ws, n, bytes, offs, o,
+    hipLaunchKernelGGL(k_walk_tail<MODE_FIRST>, dim3(MID_GRID + DEEP_LANES / 64), dim3(MID_BLOCK), 0, s, ix, ws, n, bytes, offs, o,
                        (uint64_t)0, nullptr, (uint32_t)MID_GRID);
     return hipGetLastError();
 }

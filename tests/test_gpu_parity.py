@@ -247,6 +247,26 @@ def test_deep_topics_and_overflow(torch_dev):
     assert np.diff(hit.astype(np.int64))[4] > 8      # 'a/b' overflows the RCAP ranges
 
 
+def test_tail_grids_sized_from_the_last_batch(torch_dev):
+    """The tail kernels' grids follow the list lengths of the last count-mode
+    batch on the workspace (tail_blocks): a batch whose deep / overflow lists
+    are far longer than the last one's walks them grid-stride with the small
+    grid, and a shallow batch after it runs on the large one -- exact CSR vs
+    the oracle each time (70k-topic batches: lane walk + tail kernels)."""
+    letters = [chr(ord("a") + i).encode() for i in range(26)]
+    T = b"/".join(letters)
+    filters = [b"#", T + b"/#", T + b"/+", b"+/" * 26 + b"#", b"a/#", b"+/#", b"+/+/#", b"a/b/#", b"+/b/#",
+               b"a/+/#", b"a/b/+", b"+/+", b"a/+", b"+/b", b"a/b", b"+/+/+/#", b"/".join(letters[:12]) + b"/#"]
+    fs = items_of(filters)
+    ix, o = gpu_index(fs), oracle_of(fs)
+    r = random.Random(11)
+    shallow = items_of([b"%s/%s" % (r.choice(letters), r.choice(letters)) for _ in range(70_000)])
+    heavy = items_of([r.choice([T, T + b"/1", b"/".join(letters[:12]), b"/".join(letters[:20]), b"a/b", b"a/b/c"])
+                      for _ in range(70_000)])
+    for ts in (shallow, heavy, heavy, shallow, heavy):
+        assert_same(ix, o, ts)
+
+
 def test_c3deep_reduced_vs_oracle(torch_dev):
     """C3 filters with 10 % of the topics extended to 33-64 levels (cfg 30):
     the deep topics resolve only the levels the 6-level trie can use and stay
