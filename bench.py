@@ -100,6 +100,9 @@ def parse():
     p.add_argument("--concurrency", type=int, default=8,
                    help="native caller threads of the concurrent-caller leg (and twice as many; 0 = skip)")
     p.add_argument("--frontier-sample", type=int, default=20_000)
+    p.add_argument("--large-path", default="default", choices=["default", "one", "phases"],
+                   help="batches above 65536 topics: the library's default, k_walk_one (one launch) or the "
+                        "two-phase path (TM_DEBUG_PHASES)")
     return p.parse_args()
 
 
@@ -186,6 +189,8 @@ def main():
     t = time.time()
     copies = a.copies
     ix = _native.Index(device=local, hint_keys=len(fs), copies=copies)
+    if a.large_path != "default":
+        ix.debug_set(_native.TM_DEBUG_PHASES, int(a.large_path == "phases"))
     chunk = 2_000_000
     for lo in range(0, len(fs), chunk):
         part = fs.slice(lo, min(lo + chunk, len(fs)))
@@ -263,11 +268,13 @@ def main():
 
     # sizing pass (no values written) over every batch, then the output buffers
     total_hits = 0
+    batch_hits = []
     for d_blob, d_offs in d_in:
         ix.match_batch_dev(B, d_blob.data_ptr(), d_offs.data_ptr(), outs[0]["hit"].data_ptr(),
                            outs[0]["out"].data_ptr(), 0, outs[0]["err"].data_ptr(), stream)
         torch.cuda.synchronize()
-        total_hits = max(total_hits, int(outs[0]["hit"][-1].item()))
+        batch_hits.append(int(outs[0]["hit"][-1].item()))
+        total_hits = max(total_hits, batch_hits[-1])
         if xch is not None:
             xch.size_from(outs[0]["hit"])   # per-peer exchange capacity: setup, not the data path
     slack = a.deltas * (a.steps + a.warmup) * 64 if dchunks else 0   # churn may add hits
@@ -333,12 +340,22 @@ def main():
     torch.cuda.synchronize()
     iso_launch(*d_in[0])
     ix.profile(True)
+    paths0 = [ix.debug_get(k) for k in (_native.TM_DEBUG_PATH_PHASES, _native.TM_DEBUG_PATH_SMALL,
+                                        _native.TM_DEBUG_PATH_ONE)]
     for _ in range(iso_passes):
         for d_blob, d_offs in d_in:
             iso_launch(d_blob, d_offs)
     torch.cuda.synchronize()
     iso_walk_ms, iso_batch_ms, iso_nb = ix.profile_read(reset=True)
     ix.profile(False)
+    # the kernel the events bracketed: k_walk_one (the whole batch in one launch:
+    # walk, look-back scan and emit), k_walk_small, or k_walk_fast (the walk of
+    # the two-phase path)
+    paths1 = [ix.debug_get(k) for k in (_native.TM_DEBUG_PATH_PHASES, _native.TM_DEBUG_PATH_SMALL,
+                                        _native.TM_DEBUG_PATH_ONE)]
+    path = max(range(3), key=lambda i: paths1[i] - paths0[i])
+    kernel = ("k_walk_fast", "k_walk_small", "k_walk_one")[path]
+    one_launch = path != 0
     el_t = torch.tensor([el], dtype=torch.float64, device=cdev)
     if world > 1:
         dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
@@ -467,9 +484,11 @@ def main():
             g = host_out[int(host_hit[i]):int(host_hit[i + 1])]
             e = ovals[int(ohit[j]):int(ohit[j + 1])]
             mism += int(not np.array_equal(g, e))
-        # algorithmic bytes per walk launch (SURVEY.md 8d per topic, minus the
-        # 4 H the emit kernel writes):  8 L + 32 sum|F_l| + 4, averaged over
-        # the R batches (L exact, sum|F_l| from an ns / R sample of each)
+        # algorithmic bytes per launch of the timed kernel (SURVEY.md 8d per
+        # topic):  8 L + 32 sum|F_l| + 4 H + 4 for a one-launch batch (the
+        # kernel writes the values too), minus the 4 H for k_walk_fast (the
+        # emit kernel writes them); averaged over the R batches (L and H
+        # exact, sum|F_l| from an ns / R sample of each)
         per = max(1, ns // R)
         wb = []
         for k, tk in enumerate(tsets):
@@ -478,10 +497,11 @@ def main():
             _, states = frontier(o, fb, fo, nthreads=cpu_threads)
             L_total = int(np.count_nonzero(tk.blob[: int(tk.offs[-1])] == ord("/"))) + B
             F_total = float(states.sum()) * B / per
-            wb.append(8 * L_total + 32 * F_total + 4 * B)
+            wb.append(8 * L_total + 32 * F_total + 4 * B + (4 * batch_hits[k] if one_launch else 0))
         walk_bytes = float(np.mean(wb))
         achieved = walk_bytes / (iso_ms * 1e-3) / 1e9
-        res_extra["full_path_GBps"] = round((walk_bytes + 4 * last_hits) / (iso_batch * 1e-3) / 1e9, 1)
+        res_extra["full_path_GBps"] = round((walk_bytes + (0 if one_launch else 4 * last_hits)) /
+                                            (iso_batch * 1e-3) / 1e9, 1)
 
         # ---- CPU baseline: the oracle (restated reference walk) on the host's CPUs
         if not a.no_cpu and world == 1 and a.config in ("c1", "c2", "c2nm", "c3", "c3deep"):
@@ -561,13 +581,16 @@ def main():
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": None if achieved is None else round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "traffic_source": traffic_note,
-                     "kernel": "k_walk_fast", "kernel_avg_ms": round(iso_ms, 4),
+                     "kernel": kernel, "kernel_avg_ms": round(iso_ms, 4),
                      "kernel_launches": int(iso_nb),
-                     "kernel_timing": (f"HIP events on the launch stream around k_walk_fast, {iso_passes} passes over "
+                     "kernel_timing": (f"HIP events on the launch stream around {kernel}, {iso_passes} passes over "
                                        f"the {R} batches back to back on one stream after the timed region"),
+                     "kernel_work": ("the whole batch: walk, look-back scan and CSR emission (8 L + 32 sum|F| + "
+                                     "4 H + 4 B per topic)" if one_launch else
+                                     "the walk (8 L + 32 sum|F| + 4 B per topic; the values are k_emit's)"),
                      "algorithmic_bytes_per_launch": None if walk_bytes is None else int(walk_bytes),
                      "random_request_roofline": req_ceiling,
-                     "effective": {"walk_avg_ms_overlapped": round(walk_avg_ms, 4),
+                     "effective": {"kernel_avg_ms_overlapped": round(walk_avg_ms, 4),
                                    "walk_GBps_per_step": None if walk_bytes is None
                                    else round(walk_bytes / (ms_per_step * 1e-3) / 1e9, 1),
                                    "note": f"the timed region's walks, overlapping the other {nstreams - 1} streams' "

@@ -29,10 +29,11 @@
  *   new(Device | [Device])                -> {ok, Ref} | {error, Code}   (a list: one replica per device)
  *   apply(Ref, [{Op, Filter, U32, Kind}]) -> {ok, Epoch} | {error, Code}
  *                                            Op 1 insert, 0 delete; Kind 0 binary, 1 words, 2 []
- *   match_batch(Ref, [Topic], Order)      -> [[U32] | badarg | system_limit] | {error, Code}
- *                                            Order: traversal | sorted | unique
+ *   match_batch(Ref, [Topic], Order)      -> [[U32] | badarg | system_limit] | {error, device | Code}
+ *                                            Order: traversal | sorted | unique; {error, device}: the
+ *                                            GPU failed the batch (never a per-topic badarg)
  *   first_batch(Ref, [Topic])             -> [{ok, U32} | false | badarg | system_limit] | {error, Code}
- *   read_begin(Ref)                       -> {ok, Ticket}
+ *   read_begin(Ref)                       -> {ok, Ticket}   (a resource: collected unended -> the read ends)
  *   read_end(Ref, Ticket)                 -> ok
  *   epoch(Ref)                            -> {Current, Safe}
  *   stats(Ref)                            -> #{n_keys => ..., ...}
@@ -48,8 +49,19 @@ typedef struct {
     tmn_pool pool;
 } idx_res;
 
-static ErlNifResourceType *IDX_RT;
-static ERL_NIF_TERM A_OK, A_ERROR, A_FALSE, A_BADARG, A_SYSTEM_LIMIT, A_TRAVERSAL, A_SORTED, A_UNIQUE;
+/* A reader's ticket (read_begin/1): a resource, so a reader that dies between
+   read_begin and read_end -- killed, brutal_kill at shutdown -- still ends its
+   read when its term is garbage collected (the destructor), and the safe epoch
+   moves on; a bare integer left in the library's reader set forever would pin
+   every deleted key's u32 in quarantine.  It holds a reference to
+   the index resource, so the index outlives its open readers. */
+typedef struct {
+    idx_res *idx;
+    tmn_ticket t;   /* tmatch_nif_core.c: ended exactly once */
+} ticket_res;
+
+static ErlNifResourceType *IDX_RT, *TICKET_RT;
+static ERL_NIF_TERM A_OK, A_ERROR, A_FALSE, A_BADARG, A_SYSTEM_LIMIT, A_TRAVERSAL, A_SORTED, A_UNIQUE, A_DEVICE;
 
 static void idx_dtor(ErlNifEnv *env, void *obj) {
     idx_res *r = obj;
@@ -59,9 +71,18 @@ static void idx_dtor(ErlNifEnv *env, void *obj) {
     tm_destroy(r->h);
 }
 
+static void ticket_dtor(ErlNifEnv *env, void *obj) {
+    ticket_res *t = obj;
+    (void)env;
+    if (!t->idx) return;
+    tmn_ticket_destroy(&t->t);
+    enif_release_resource(t->idx);
+}
+
 static int load(ErlNifEnv *env, void **priv, ERL_NIF_TERM info) {
     (void)priv; (void)info;
     IDX_RT = enif_open_resource_type(env, NULL, "tm_index", idx_dtor, ERL_NIF_RT_CREATE, NULL);
+    TICKET_RT = enif_open_resource_type(env, NULL, "tm_read_ticket", ticket_dtor, ERL_NIF_RT_CREATE, NULL);
     A_OK = enif_make_atom(env, "ok");
     A_ERROR = enif_make_atom(env, "error");
     A_FALSE = enif_make_atom(env, "false");
@@ -70,11 +91,17 @@ static int load(ErlNifEnv *env, void **priv, ERL_NIF_TERM info) {
     A_TRAVERSAL = enif_make_atom(env, "traversal");
     A_SORTED = enif_make_atom(env, "sorted");
     A_UNIQUE = enif_make_atom(env, "unique");
-    return IDX_RT ? 0 : 1;
+    A_DEVICE = enif_make_atom(env, "device");
+    return IDX_RT && TICKET_RT ? 0 : 1;
 }
 
+/* {error, device} when the GPU failed the call (TM_EDEVICE: e.g. a batch
+   whose look-back failed twice, include/tmatch.h err flag 4) -- the caller
+   logs it and may fall back to the ETS walk; never badarg, which the
+   reference raises only for a '+'/'#' topic level (emqx_trie_search.erl:374-375);
+   {error, Code} for the other library codes */
 static ERL_NIF_TERM err_term(ErlNifEnv *env, int rc) {
-    return enif_make_tuple2(env, A_ERROR, enif_make_int(env, rc));
+    return enif_make_tuple2(env, A_ERROR, rc == TM_EDEVICE ? A_DEVICE : enif_make_int(env, rc));
 }
 
 /* new(Device | [Device] | {Device | [Device], Copies}) -> {ok, Ref} | {error, Code}
@@ -199,8 +226,11 @@ static ERL_NIF_TERM nif_match_batch(ErlNifEnv *env, int argc, const ERL_NIF_TERM
         uint64_t b, e;
         const int err = tmn_row(s, n, order, i, &b, &e);
         ERL_NIF_TERM row;
-        if (err) {
-            row = err == 2 ? A_SYSTEM_LIMIT : A_BADARG;   /* 2: > 65536 levels */
+        if (err == TMN_ERR_DEVICE) {   /* (tmn_match already returned TM_EDEVICE for such a batch) */
+            rc = TM_EDEVICE;
+            break;
+        } else if (err) {
+            row = err == TMN_ERR_TOO_DEEP ? A_SYSTEM_LIMIT : A_BADARG;
         } else {
             row = enif_make_list(env, 0);
             for (uint64_t k = e; k-- > b;) row = enif_make_list_cell(env, enif_make_uint(env, vals[k]), row);
@@ -239,25 +269,38 @@ static ERL_NIF_TERM nif_first_batch(ErlNifEnv *env, int argc, const ERL_NIF_TERM
     return rc == TM_OK ? out : err_term(env, rc);
 }
 
-/* read_begin(Ref) -> {ok, Ticket}: a reader registers before its batch */
+/* read_begin(Ref) -> {ok, Ticket}: a reader registers before its batch; the
+   ticket is a resource (ticket_res) that ends the read if it is collected
+   before read_end */
 static ERL_NIF_TERM nif_read_begin(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
     idx_res *r;
-    uint64_t t;
     (void)argc;
     if (!enif_get_resource(env, argv[0], IDX_RT, (void **)&r)) return enif_make_badarg(env);
-    int rc = tm_read_begin(r->h, &t);
-    return rc == TM_OK ? enif_make_tuple2(env, A_OK, enif_make_uint64(env, t)) : err_term(env, rc);
+    ticket_res *tk = enif_alloc_resource(TICKET_RT, sizeof *tk);
+    tk->idx = NULL;
+    int rc = tmn_ticket_begin(&tk->t, r->h);
+    if (rc != TM_OK) {
+        enif_release_resource(tk);   /* idx NULL: the destructor does nothing */
+        return err_term(env, rc);
+    }
+    enif_keep_resource(r);
+    tk->idx = r;
+    ERL_NIF_TERM term = enif_make_resource(env, tk);
+    enif_release_resource(tk);
+    return enif_make_tuple2(env, A_OK, term);
 }
 
-/* read_end(Ref, Ticket) -> ok: after the reader has decoded its results */
+/* read_end(Ref, Ticket) -> ok: after the reader has decoded its results
+   (idempotent: a second call, or the ticket's later collection, does nothing) */
 static ERL_NIF_TERM nif_read_end(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
     idx_res *r;
-    ErlNifUInt64 t;
+    ticket_res *tk;
     (void)argc;
-    if (!enif_get_resource(env, argv[0], IDX_RT, (void **)&r) || !enif_get_uint64(env, argv[1], &t))
+    if (!enif_get_resource(env, argv[0], IDX_RT, (void **)&r) ||
+        !enif_get_resource(env, argv[1], TICKET_RT, (void **)&tk) || tk->idx != r)
         return enif_make_badarg(env);
-    int rc = tm_read_end(r->h, t);
-    return rc == TM_OK ? A_OK : err_term(env, rc);
+    tmn_ticket_end(&tk->t);
+    return A_OK;
 }
 
 /* epoch(Ref) -> {Current, Safe} (include/tmatch.h "Reader epochs") */

@@ -91,6 +91,11 @@ int tmn_match(tmn_set *s, tm_index *h, uint32_t n, uint32_t order) {
         rc = vals ? tm_match_batch_ex(h, n, s->blob.p, s->offs.p, hit, vals, s->vals.cap / 4, err, order, uniq)
                   : TM_ENOMEM;
     }
+    /* err flag 4 (a batch the device failed; the library runs it again and
+       returns TM_EDEVICE instead -- checked here all the same): the whole
+       call fails as a device error, never as a client badarg */
+    for (uint32_t i = 0; rc == TM_OK && i < n; i++)
+        if (err[i] > TMN_ERR_TOO_DEEP) rc = TM_EDEVICE;
     return rc;
 }
 
@@ -106,7 +111,7 @@ int tmn_row(const tmn_set *s, uint32_t n, uint32_t order, uint32_t i, uint64_t *
     const uint8_t *err = s->err.p;
     (void)n;
     *b = *e = 0;
-    if (err[i]) return err[i];
+    if (err[i]) return err[i] <= TMN_ERR_TOO_DEEP ? err[i] : TMN_ERR_DEVICE;
     *b = hit[i];
     *e = order == TM_ORDER_UNIQUE ? hit[i] + ((const uint32_t *)s->uniq.p)[i] : hit[i + 1];
     return 0;
@@ -115,4 +120,27 @@ int tmn_row(const tmn_set *s, uint32_t n, uint32_t order, uint32_t i, uint64_t *
 int tmn_first_row(const tmn_set *s, uint32_t i, uint32_t *v) {
     *v = ((const uint32_t *)s->vals.p)[i];
     return ((const uint8_t *)s->err.p)[i];
+}
+
+int tmn_ticket_begin(tmn_ticket *t, tm_index *h) {
+    memset(t, 0, sizeof *t);
+    t->h = h;
+    if (pthread_mutex_init(&t->mu, NULL)) return TM_ENOMEM;
+    int rc = tm_read_begin(h, &t->ticket);
+    t->open = rc == TM_OK;
+    return rc;
+}
+
+void tmn_ticket_end(tmn_ticket *t) {
+    pthread_mutex_lock(&t->mu);
+    if (t->open) {
+        t->open = 0;
+        (void)tm_read_end(t->h, t->ticket);
+    }
+    pthread_mutex_unlock(&t->mu);
+}
+
+void tmn_ticket_destroy(tmn_ticket *t) {
+    tmn_ticket_end(t);
+    pthread_mutex_destroy(&t->mu);
 }

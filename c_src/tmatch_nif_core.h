@@ -56,19 +56,40 @@ int tmn_pack(tmn_set *s, tm_index *h, uint32_t n, const uint8_t *const *topics, 
 /* matches/3 for the packed batch in `order` (TM_ORDER_*): sizes the value
  * buffer from what the set already holds (>= TMN_IDS_PER_TOPIC per topic), and
  * on TM_ECAP (offsets valid, values truncated) grows it to the exact total
- * and runs the batch again. */
+ * and runs the batch again.  TM_EDEVICE: the device failed the batch (the
+ * library's retry included, or a topic flagged err 4) -- a device error for
+ * the whole call, never a per-topic badarg. */
 int tmn_match(tmn_set *s, tm_index *h, uint32_t n, uint32_t order);
 
 /* match/2 for the packed batch: value and found flag per topic (tm_first_batch) */
 int tmn_first(tmn_set *s, tm_index *h, uint32_t n);
 
 /* Row i of a tmn_match result: 0 and its values vals()[*b .. *e), or the
- * topic's err flag (1 badarg, 2 more than 65536 levels) with no values. */
+ * topic's err flag with no values: TMN_ERR_BADARG (a '+'/'#' level),
+ * TMN_ERR_TOO_DEEP (more than 65536 levels), TMN_ERR_DEVICE (the batch failed
+ * on the device -- tmn_match returns TM_EDEVICE for such a batch, so a caller
+ * that checked its result never sees it). */
+enum { TMN_ERR_BADARG = 1, TMN_ERR_TOO_DEEP = 2, TMN_ERR_DEVICE = 4 };
 int tmn_row(const tmn_set *s, uint32_t n, uint32_t order, uint32_t i, uint64_t *b, uint64_t *e);
 static inline const uint32_t *tmn_vals(const tmn_set *s) { return (const uint32_t *)s->vals.p; }
 
 /* Row i of a tmn_first result: 1 and *v found, 0 none, 2 badarg, 3 too deep */
 int tmn_first_row(const tmn_set *s, uint32_t i, uint32_t *v);
+
+/* A reader's ticket (tm_read_begin / tm_read_end), held in an Erlang resource
+ * by the NIF: ended exactly once -- by read_end/2, or by the resource's
+ * destructor when a reader died before ending it (its term collected), so a
+ * killed reader never pins the safe epoch. */
+typedef struct {
+    tm_index *h;
+    uint64_t ticket;
+    int open;
+    pthread_mutex_t mu;
+} tmn_ticket;
+
+int tmn_ticket_begin(tmn_ticket *t, tm_index *h);   /* TM_OK: registered, open */
+void tmn_ticket_end(tmn_ticket *t);                 /* idempotent */
+void tmn_ticket_destroy(tmn_ticket *t);             /* ends it if still open */
 
 #ifdef __cplusplus
 }

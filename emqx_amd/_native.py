@@ -25,7 +25,10 @@ EXPORTS = ("tm_create", "tm_destroy", "tm_apply_deltas", "tm_sync", "tm_match_ba
            "tm_last_error", "tm_abi_version", "tm_merge_shards", "tm_host_alloc", "tm_host_free",
            "tm_stream_release", "tm_match_batch_ex", "tm_match_batch_dev_ex", "tm_sort_segments",
            "tm_matches_filter", "tm_apply_deltas_ex", "tm_read_begin", "tm_read_end", "tm_epoch",
-           "tm_create_replicas", "tm_replica_stats")
+           "tm_create_replicas", "tm_replica_stats", "tm_debug_set", "tm_debug_get")
+TM_DEBUG_LB_SPINS, TM_DEBUG_LB_FAIL_BLOCK, TM_DEBUG_LB_LAUNCHES, TM_DEBUG_PHASES = 1, 2, 3, 4
+TM_DEBUG_FAILED_BATCHES, TM_DEBUG_RETRIED_BATCHES = 5, 6
+TM_DEBUG_PATH_PHASES, TM_DEBUG_PATH_SMALL, TM_DEBUG_PATH_ONE = 7, 8, 9
 
 
 class NativeUnavailable(RuntimeError):
@@ -36,6 +39,13 @@ class TmError(RuntimeError):
     def __init__(self, code, msg):
         super().__init__(f"tmatch error {code}: {msg}")
         self.code = code
+
+
+class DeviceError(TmError):
+    """TM_EDEVICE: the GPU failed the call (e.g. a batch whose look-back wait
+    expired twice, include/tmatch.h err flag 4).  Never a client error: the
+    reference raises badarg only for a '+'/'#' topic level
+    (emqx_trie_search.erl:374-375)."""
 
 
 class tm_options(C.Structure):
@@ -90,6 +100,8 @@ def load_library(path: Path | None = None):
         "tm_epoch": (i32, [vp, C.POINTER(u64), C.POINTER(u64)]),
         "tm_create_replicas": (i32, [C.POINTER(tm_options), C.POINTER(C.c_int32), u32, C.POINTER(vp)]),
         "tm_replica_stats": (i32, [vp, u32, C.POINTER(u64), C.POINTER(C.c_int32)]),
+        "tm_debug_set": (i32, [vp, u32, u64]),
+        "tm_debug_get": (i32, [vp, u32, C.POINTER(u64)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -156,7 +168,8 @@ class Index:
 
     def _check(self, rc):
         if rc != TM_OK:
-            raise TmError(rc, self._lib.tm_last_error(self._h).decode())
+            cls = DeviceError if rc == TM_EDEVICE else TmError
+            raise cls(rc, self._lib.tm_last_error(self._h).decode())
 
     def close(self):
         if getattr(self, "_h", None):
@@ -321,6 +334,15 @@ class Index:
         b, d = C.c_uint64(), C.c_int32()
         self._check(self._lib.tm_replica_stats(self._h, r, C.byref(b), C.byref(d)))
         return b.value, d.value
+
+    def debug_set(self, key: int, value: int):
+        """tm_debug_set (test hooks, include/tmatch.h)."""
+        self._check(self._lib.tm_debug_set(self._h, key, value))
+
+    def debug_get(self, key: int) -> int:
+        v = C.c_uint64()
+        self._check(self._lib.tm_debug_get(self._h, key, C.byref(v)))
+        return v.value
 
     def stats(self) -> dict:
         s = tm_stats_t()

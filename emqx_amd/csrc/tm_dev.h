@@ -23,6 +23,7 @@ struct DevIndex {
     // exists (xlen_mask bit L for L < 64, L <= xlen_max beyond): need_levels().
     uint32_t depth, xlen_max;
     uint64_t xlen_mask;
+    uint32_t hdesc;   // keys with a '#' that is not last are stored (NLIT_HDESC nodes exist)
 };
 
 constexpr int FAST_L = 8;        // levels handled by the main walk kernel (LDS frontier)
@@ -40,12 +41,14 @@ constexpr int DEEP_LANES = 64;   // lanes of the global-scratch (deep / overflow
 enum { L_MID = 0, L_DEEP = 1, L_OVF_MID = 2, L_OVF_DEEP = 3, L_COUNT = 4 };
 
 // Per-batch device scratch (grow-only, owned by the index).
-// k_walk_small's look-back word of a block: launch tag (20 bits), state
-// (LB_AGG: its own hit total; LB_INCL: the total of it and every block before
-// it) and the value (42 bits) in ONE 64-bit word, so a reader gets state and
-// value from one coherent load (no acquire / release: those write back and
-// invalidate the whole L2 of the XCD, under every kernel running there)
-enum : uint32_t { LB_AGG = 1, LB_INCL = 2 };
+// The one-launch kernels' (k_walk_small, k_walk_one) look-back word of a
+// block: launch tag (20 bits), state (LB_AGG: its own hit total; LB_INCL: the
+// total of it and every block before it; LB_FAIL: its wait expired, or a
+// predecessor's did -- every later block fails too) and the value (42 bits) in
+// ONE 64-bit word, so a reader gets state and value from one coherent load (no
+// acquire / release: those write back and invalidate the whole L2 of the XCD,
+// under every kernel running there)
+enum : uint32_t { LB_AGG = 1, LB_INCL = 2, LB_FAIL = 3 };
 constexpr uint32_t LB_TAG_BITS = 20, LB_TAG_MASK = (1u << LB_TAG_BITS) - 1;
 constexpr uint64_t LB_VAL_MASK = (1ull << 42) - 1;
 __host__ __device__ constexpr uint64_t lb_word(uint32_t tag, uint32_t st, uint64_t v) {
@@ -53,6 +56,18 @@ __host__ __device__ constexpr uint64_t lb_word(uint32_t tag, uint32_t st, uint64
 }
 __host__ __device__ constexpr uint32_t lb_tag(uint64_t w) { return (uint32_t)(w >> 44); }
 __host__ __device__ constexpr uint32_t lb_state(uint64_t w) { return (uint32_t)(w >> 42) & 3u; }
+
+// The look-back's bounded wait.  A block waits only for blocks that took their
+// start ticket before it (so they are running and publish soon); the bound
+// keeps a lost publication (e.g. a predecessor's waves preempted for long) from
+// leaving a spinning grid behind: past it the block and every later one flag
+// their topics err 4 and raise the workspace's fail word, and the host API
+// runs the batch again (tm_host.cpp retry_or_fail).
+constexpr uint32_t LB_SPINS = 1u << 22;   // polls of one predecessor word (s_sleep(1) apart: ~0.1 s)
+struct LbCtl {
+    uint32_t spins;        // the bound (LB_SPINS; tm_debug_set can lower it)
+    uint32_t fail_block;   // test hook: this block (in start order) acts as if its wait expired (NONE: off)
+};
 
 struct Workspace {
     uint32_t *cnt;        // [n] hits per topic
@@ -69,13 +84,17 @@ struct Workspace {
     uint64_t *look;       // [n / SM_TOPICS + 4] one-launch path: per block, one look-back word (lb_word)
     // list lengths of the last count-mode batch that finished here ([0, L_COUNT))
     // and its topic count ([L_COUNT]; 0: none yet), written by the device into
-    // mapped host memory: the next batch sizes its tail grids from them
+    // mapped host memory: the next batch sizes its tail grids from them;
+    // [HINT_FAIL]: set by a one-launch kernel whose look-back failed (the host
+    // clears it)
     uint32_t *hint_h, *hint_d;
     uint64_t cap_n;
 };
 
 constexpr int TILE = 256;    // topics per walk block = per scan tile = per emit block
 constexpr int LIST_SLOTS = L_COUNT + 5;   // Workspace::list_n entries
+constexpr int HINT_FAIL = L_COUNT + 1;    // Workspace::hint_* word of the fail flag
+constexpr int HINT_WORDS = L_COUNT + 2;
 constexpr int SM_TOPICS = 16;             // topics per block of the one-launch small-batch path
 constexpr int SM_TB = 256;                // topic bytes it stages in LDS (longer topics: the lane walk)
 constexpr int SM_VSTAGE = 1024;           // values of a block it stages in LDS before one contiguous write
@@ -92,14 +111,21 @@ hipError_t launch_match_phase1(const DevIndex &ix, const Workspace &ws, uint64_t
 hipError_t launch_match_phase2(const DevIndex &ix, const Workspace &ws, uint64_t n, const uint8_t *bytes,
                                const uint64_t *offs, uint64_t *hit_offs, uint32_t *out, uint64_t cap,
                                hipStream_t s);
-// The whole batch (phase 1 + phase 2): one launch for a small batch when the
-// index allows it (small_path_ok), both phases otherwise.  `tag` must differ
-// between consecutive launches on one workspace (the one-launch path's
-// look-back scan tells its own blocks' words from older ones by it).
+// The whole batch in ONE launch when the index allows it: k_walk_small up to
+// SMALL_TOPICS topics (one_launch_ok: its depth fits the fallback store),
+// k_walk_one above (one_pass_ok: a shallow index without '#'-not-last keys);
+// the two phases otherwise (or when `phases` forces them: tests of that
+// path).  `tag` must differ between consecutive launches on one workspace (the
+// one-launch look-back scan tells its own blocks' words from older ones by it).  A one-launch batch whose
+// look-back failed flags its topics err 4 and sets ws.hint_h[HINT_FAIL].
 bool small_path_ok(const DevIndex &ix, uint64_t n);
+bool one_launch_ok(const DevIndex &ix);
+bool one_pass_ok(const DevIndex &ix);   // k_walk_one's condition (large batches)
+enum { PATH_PHASES = 0, PATH_SMALL = 1, PATH_ONE = 2, PATH_COUNT = 3 };   // *path of launch_match
 hipError_t launch_match(const DevIndex &ix, const Workspace &ws, uint64_t n, const uint8_t *bytes,
                         const uint64_t *offs, uint64_t *hit_offs, uint8_t *err, uint32_t *out, uint64_t cap,
-                        uint32_t tag, hipStream_t s, hipEvent_t ev_walk0 = nullptr, hipEvent_t ev_walk1 = nullptr);
+                        uint32_t tag, LbCtl lb, bool phases, hipStream_t s, hipEvent_t ev_walk0 = nullptr,
+                        hipEvent_t ev_walk1 = nullptr, int *path = nullptr);
 hipError_t launch_first(const DevIndex &ix, const Workspace &ws, uint64_t n, const uint8_t *bytes,
                         const uint64_t *offs, uint32_t *out_value, uint8_t *out_found, hipStream_t s);
 // filter-sharded merge of allgathered per-shard CSR hit lists (k_merge_shards)

@@ -141,6 +141,11 @@ struct Replica {
     uint64_t batches = 0;                     // host-API batches served (tm_replica_stats)
 };
 
+// Large batches (> 65536 topics) on an index one_pass_ok accepts: the two-phase
+// path (true) or k_walk_one (false) by default; TM_DEBUG_PHASES switches it
+// per index (which one is faster on C3, measured)
+constexpr bool LARGE_PHASES_DEFAULT = true;
+
 constexpr int MAX_HOST_LANES = 16;   // concurrent host-API batches in flight, per replica
 constexpr int MAX_DEV_LANES = 16;    // device-API streams with a workspace kept
 
@@ -207,6 +212,7 @@ struct tm_index {
         uint64_t snapshots = 0, slices = 0;   // diagnostics
     } mf;
     uint64_t n_wild = 0, n_exact = 0;
+    uint64_t n_hdesc_keys = 0;       // '#'-not-last keys stored (DevIndex::hdesc)
     uint64_t uploads = 0, patch_bytes = 0;
 
     PatchSlot patch[PATCH_RING]; uint64_t patch_seq = 0;   // patches collected so far
@@ -233,6 +239,15 @@ struct tm_index {
     std::vector<ProfEv> prof_pending, prof_free;
     double prof_walk_ms = 0, prof_batch_ms = 0;
     uint64_t prof_batches = 0;
+
+    // test hooks (tm_debug_set, under mu): the look-back control of the next
+    // dbg_lb_launches one-launch batches, and the two-phase path forced for
+    // large batches
+    LbCtl dbg_lb{LB_SPINS, NONE};
+    uint64_t dbg_lb_launches = 0;
+    bool dbg_phases = LARGE_PHASES_DEFAULT;
+    std::atomic<uint64_t> failed_batches{0}, retried_batches{0};   // one-launch look-back failures seen / retried
+    std::atomic<uint64_t> path_batches[PATH_COUNT] = {};             // match launches per kernel path
 };
 
 namespace {
@@ -1033,6 +1048,7 @@ void key_op(tm_index *ix, bool ins, const uint8_t *f, uint32_t len, uint32_t v, 
     NodeAux &a = ix->aux[node];
     if (hpos < w.size()) {   // a '#'-not-last key: P's count (the path exists: the key was inserted)
         a.hdesc += ins ? 1 : -1;
+        ix->n_hdesc_keys += ins ? 1 : -1;
         nd.nlit = nlit_of(nd) | (a.hdesc ? NLIT_HDESC : 0);
         ix->nodes.touch(node);
         summary_refresh(ix, node);
@@ -1066,17 +1082,27 @@ int upload_full(tm_index *ix, Mirror<T> &m) {
     uint64_t need = std::max<uint64_t>(m.h.size(), 1);
     const bool grow = need > m.dcap;
     const uint64_t cap = grow ? need + need / 2 + DEV_GUARD : m.dcap;
-    for (int r = 0; r < ix->nrep; r++) {
-        // rare (first upload, growth, rehash): drain every stream that may
-        // still read the old copy before touching it
-        HIPCHK(ix, hipSetDevice(ix->rep[r].device));
-        HIPCHK(ix, hipDeviceSynchronize());
-        if (grow) {
-            if (m.d[r]) HIPCHK(ix, hipFree(m.d[r]));
-            m.d[r] = nullptr;
-            HIPCHK(ix, hipMalloc(&m.d[r], cap * sizeof(T)));
+    // a failure part way leaves the device copies in doubt: dcap 0 makes the
+    // next collect reallocate and ship the whole table again (its dirty set
+    // is cleared only on success)
+    auto ship = [&]() -> int {
+        for (int r = 0; r < ix->nrep; r++) {
+            // rare (first upload, growth, rehash): drain every stream that may
+            // still read the old copy before touching it
+            HIPCHK(ix, hipSetDevice(ix->rep[r].device));
+            HIPCHK(ix, hipDeviceSynchronize());
+            if (grow) {
+                if (m.d[r]) HIPCHK(ix, hipFree(m.d[r]));
+                m.d[r] = nullptr;
+                HIPCHK(ix, hipMalloc(&m.d[r], cap * sizeof(T)));
+            }
+            if (m.bytes()) HIPCHK(ix, hipMemcpy(m.d[r], m.h.data(), m.bytes(), hipMemcpyHostToDevice));
         }
-        if (m.bytes()) HIPCHK(ix, hipMemcpy(m.d[r], m.h.data(), m.bytes(), hipMemcpyHostToDevice));
+        return TM_OK;
+    };
+    if (int rc = ship()) {
+        m.dcap = 0;
+        return rc;
     }
     m.dcap = cap;
     if (getenv("TM_DEBUG_UPLOADS"))   // diagnostics: which table was shipped whole, and why
@@ -1141,6 +1167,25 @@ int next_tag(tm_index *ix, Lane &ln, hipStream_t s, uint32_t &tag) {
     return TM_OK;
 }
 
+// the look-back control of the next launch (caller holds ix->mu): the
+// default bound, or the test hook's for the next dbg_lb_launches launches
+LbCtl next_lb(tm_index *ix) {
+    if (!ix->dbg_lb_launches) return LbCtl{LB_SPINS, NONE};
+    ix->dbg_lb_launches--;
+    return ix->dbg_lb;
+}
+
+// did the lane's last one-launch batch fail its look-back (err 4, the fail
+// word raised by the device)?  Clears the word.  After the lane's stream
+// has been synchronised.
+bool batch_failed(tm_index *ix, Lane &ln) {
+    volatile uint32_t *f = ln.w.hint_h + HINT_FAIL;
+    if (!*f) return false;
+    *f = 0;
+    ix->failed_batches++;
+    return true;
+}
+
 // the lane's batch is done with the index: later patches (on any stream) wait for it
 int batch_done(tm_index *ix, Lane &ln) {
     HIPCHK(ix, hipEventRecord(ln.done, ln.s));
@@ -1159,14 +1204,18 @@ int apply_patch(tm_index *ix, int r, uint64_t q, hipStream_t st) {
     const uint32_t k = (uint32_t)((q - 1) % PATCH_RING);
     const PatchSlot &p = ix->patch[k];
     HIPCHK(ix, hipSetDevice(R.device));
-    if (p.bytes > R.pdev_cap[k]) {
+    if (p.bytes > R.pdev_cap[k] || !R.pdev[k]) {
         if (R.ppending[k]) { HIPCHK(ix, hipEventSynchronize(R.pdone[k])); R.ppending[k] = false; }
         if (R.pdev[k]) HIPCHK(ix, hipFree(R.pdev[k]));
         R.pdev[k] = nullptr;
+        R.pdev_cap[k] = 0;
         // generous steps: a reallocation (hipHostFree / hipFree) synchronises
         // the device, a multi-millisecond stall inside a churn stream (C5)
-        R.pdev_cap[k] = std::max<uint64_t>(p.bytes * 2, 1u << 20);
-        HIPCHK(ix, hipMalloc(&R.pdev[k], R.pdev_cap[k]));
+        const uint64_t want = std::max<uint64_t>(p.bytes * 2, 1u << 20);
+        uint8_t *np = nullptr;   // the capacity is recorded only once the buffer exists
+        HIPCHK(ix, hipMalloc(&np, want));
+        R.pdev[k] = np;
+        R.pdev_cap[k] = want;
     }
     for (auto &l : ix->lanes)
         if (l->r == r && l->used && l->s != st) HIPCHK(ix, hipStreamWaitEvent(st, l->done, 0));
@@ -1205,7 +1254,24 @@ int collect_patch(tm_index *ix) {
     return rc;
 }
 
+int collect_patch_locked2(tm_index *ix);
+
+// Every table's dirty words go into one patch.  collect() clears a table's
+// dirty set as it takes its runs, so if anything fails after that (a pinned
+// allocation, a lagging replica's bring-up) those runs would never reach a
+// device: every table is then marked wholly dirty, and the next collect ships
+// them whole.
 int collect_patch_locked(tm_index *ix) {
+    const int rc = collect_patch_locked2(ix);
+    if (rc) {
+        ix->vocab.dirty.set_all(); ix->wpool.dirty.set_all(); ix->nodes.dirty.set_all();
+        ix->ctab.dirty.set_all(); ix->vals.dirty.set_all(); ix->exact.dirty.set_all();
+        ix->xfp.dirty.set_all(); ix->wseq.dirty.set_all(); ix->wbits.dirty.set_all();
+    }
+    return rc;
+}
+
+int collect_patch_locked2(tm_index *ix) {
     std::vector<PatchRun> runs;
     std::vector<uint32_t> data;
     int rc;
@@ -1235,11 +1301,15 @@ int collect_patch_locked(tm_index *ix) {
         }
     }
     const uint64_t bytes = nr * sizeof(PatchRun) + nw * 4;
-    if (bytes > p.pin_cap) {
+    if (bytes > p.pin_cap || !p.pin) {
         if (p.pin) HIPCHK(ix, hipHostFree(p.pin));
         p.pin = nullptr;
-        p.pin_cap = std::max<uint64_t>(bytes * 2, 1u << 20);
-        HIPCHK(ix, hipHostMalloc(&p.pin, p.pin_cap, hipHostMallocPortable));
+        p.pin_cap = 0;
+        const uint64_t want = std::max<uint64_t>(bytes * 2, 1u << 20);
+        uint8_t *np = nullptr;   // the capacity is recorded only once the buffer exists
+        HIPCHK(ix, hipHostMalloc(&np, want, hipHostMallocPortable));
+        p.pin = np;
+        p.pin_cap = want;
     }
     memcpy(p.pin, runs.data(), nr * sizeof(PatchRun));
     memcpy(p.pin + nr * sizeof(PatchRun), data.data(), nw * 4);
@@ -1306,6 +1376,7 @@ DevIndex dev_view_build(tm_index *ix, int r) {
     d.xlen_max = xc.empty() ? 0 : (uint32_t)xc.size() - 1;
     d.xlen_mask = 0;
     for (size_t k = 0; k < xc.size() && k < 64; k++) if (xc[k]) d.xlen_mask |= 1ull << k;
+    d.hdesc = ix->n_hdesc_keys != 0;
     return d;
 }
 
@@ -1448,8 +1519,8 @@ int ensure_ws(tm_index *ix, uint64_t n, Lane &ln) {
         HIPCHK(ix, hipMalloc(&w.deep_plus, (uint64_t)DEEP_LANES * MAX_LEVELS));
         HIPCHK(ix, hipMalloc(&w.list_n, LIST_SLOTS * 4));
         HIPCHK(ix, hipMemsetAsync(w.list_n, 0, LIST_SLOTS * 4, ln.s));
-        HIPCHK(ix, hipHostMalloc(&w.hint_h, (L_COUNT + 1) * 4, hipHostMallocMapped));
-        std::memset(w.hint_h, 0, (L_COUNT + 1) * 4);
+        HIPCHK(ix, hipHostMalloc(&w.hint_h, HINT_WORDS * 4, hipHostMallocMapped));
+        std::memset(w.hint_h, 0, HINT_WORDS * 4);
         HIPCHK(ix, hipHostGetDevicePointer(reinterpret_cast<void **>(&w.hint_d), w.hint_h, 0));
     }
     // the batch must see every patch shipped so far, whichever stream it went on
@@ -1539,7 +1610,7 @@ int drain_lanes(tm_index *ix) {
 
 extern "C" {
 
-uint32_t tm_abi_version(void) { return (1u << 16) | 5u; }
+uint32_t tm_abi_version(void) { return (1u << 16) | 6u; }
 
 const char *tm_last_error(tm_index *) { return g_last_error.c_str(); }
 
@@ -1728,8 +1799,11 @@ int tm_match_batch_dev_ex(tm_index *ix, uint64_t n, const uint8_t *bytes, const 
     if ((rc = prof_begin(ix, ev, s))) return rc;
     uint32_t tag;
     if ((rc = next_tag(ix, *ln, s, tag))) return rc;
-    HIPCHK(ix, launch_match(d, ln->w, n, bytes, offs, hit_offs, err, out, out ? cap : 0, tag, s, ev.w0,
-                            ev.w1));
+    // (asynchronous: a failed look-back reaches the caller as err 4 flags, include/tmatch.h)
+    int path = PATH_PHASES;
+    HIPCHK(ix, launch_match(d, ln->w, n, bytes, offs, hit_offs, err, out, out ? cap : 0, tag, next_lb(ix),
+                            ix->dbg_phases, s, ev.w0, ev.w1, &path));
+    ix->path_batches[path]++;
     if (order != TM_ORDER_TRAVERSAL && out)
         HIPCHK(ix, launch_sort_segments(ln->w, n, hit_offs, out, cap, order == TM_ORDER_UNIQUE, ucnt, s));
     if ((rc = batch_done(ix, *ln))) return rc;
@@ -1882,6 +1956,22 @@ static double now_us() {
     return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
+// After a failed one-launch batch (its look-back wait expired: err 4 flags,
+// never a client error -- the reference raises badarg only for a '+'/'#'
+// level, emqx_trie_search.erl:374-375): the first failure runs the batch
+// again, on the same lane with the current device view; the second returns
+// TM_EDEVICE for the whole call.  Retakes the index lock (released for the
+// GPU wait).
+static int retry_or_fail(tm_index *ix, std::unique_lock<std::mutex> &g, Lane &ln, int tries) {
+    if (tries >= 1)
+        return fail(ix, TM_EDEVICE, "tm_match_batch: the batch failed on the device twice (look-back wait expired, "
+                                    "err 4); not matched");
+    ix->retried_batches++;
+    g.lock();
+    HIPCHK(ix, hipSetDevice(ix->rep[ln.r].device));
+    return sync_locked(ix, ln.r, ln.s);
+}
+
 // Host-API batches hold the index lock only to ship pending patches, pick up
 // the index's current device view and queue the kernels on the caller's lane;
 // they wait for the GPU and copy results out without it, so concurrent callers
@@ -1921,7 +2011,6 @@ int tm_match_batch_ex(tm_index *ix, uint64_t n, const uint8_t *tb, const uint64_
             if (!de) {   // flags nobody reads still need a home
                 if ((rc = stage_out(ix, ln, n, n, de))) return rc;
             }
-            const DevIndex d = dev_view(ix, ln.r);
             const uint8_t *dbytes = db ? db : dof;   // no bytes: any valid address
             uint64_t *dhit = reinterpret_cast<uint64_t *>(dh);
             uint32_t *vdst = reinterpret_cast<uint32_t *>(dv);
@@ -1929,18 +2018,26 @@ int tm_match_batch_ex(tm_index *ix, uint64_t n, const uint8_t *tb, const uint64_
                 if ((rc = grow_dev(ix, s, ln.d_vals, ln.d_vals_cap, cap))) return rc;
                 vdst = ln.d_vals;
             }
-            uint32_t tag;
-            if (int rc = next_tag(ix, ln, s, tag)) return rc;
-            HIPCHK(ix, launch_match(d, ln.w, n, dbytes, reinterpret_cast<const uint64_t *>(dof), dhit, de, vdst,
-                                    dv ? cap : 0, tag, s));
-            if (sorted && dv) {
-                HIPCHK(ix, launch_sort_segments(ln.w, n, dhit, vdst, cap, unique, reinterpret_cast<uint32_t *>(du), s));
-                HIPCHK(ix, launch_copy_values(dhit, n, vdst, reinterpret_cast<uint32_t *>(dv), cap, s));
+            for (int tries = 0;; tries++) {
+                const DevIndex d = dev_view(ix, ln.r);
+                uint32_t tag;
+                if (int rc = next_tag(ix, ln, s, tag)) return rc;
+                int path = PATH_PHASES;
+                HIPCHK(ix, launch_match(d, ln.w, n, dbytes, reinterpret_cast<const uint64_t *>(dof), dhit, de, vdst,
+                                        dv ? cap : 0, tag, next_lb(ix), ix->dbg_phases, s, nullptr, nullptr, &path));
+                ix->path_batches[path]++;
+                if (sorted && dv) {
+                    HIPCHK(ix, launch_sort_segments(ln.w, n, dhit, vdst, cap, unique, reinterpret_cast<uint32_t *>(du), s));
+                    HIPCHK(ix, launch_copy_values(dhit, n, vdst, reinterpret_cast<uint32_t *>(dv), cap, s));
+                }
+                if ((rc = batch_done(ix, ln))) return rc;
+                g.unlock();
+                if (timing) tt[nt++] = now_us();
+                HIPCHK(ix, hipStreamSynchronize(s));
+                if (!batch_failed(ix, ln)) break;
+                if ((rc = retry_or_fail(ix, g, ln, tries))) return rc;
+                if (timing) nt = 1;
             }
-            if ((rc = batch_done(ix, ln))) return rc;
-            g.unlock();
-            if (timing) tt[nt++] = now_us();
-            HIPCHK(ix, hipStreamSynchronize(s));
             if (timing) {
                 tt[nt++] = now_us();
                 fprintf(stderr, "tm_match_batch n=%lu (in place): sync %.1f launch %.1f wait %.1f us\n",
@@ -1966,7 +2063,7 @@ int tm_match_batch_ex(tm_index *ix, uint64_t n, const uint8_t *tb, const uint64_
     uint8_t *derr = dres + (n + 1) * 8;
     uint32_t *dunq = (sorted && out_unique) ? reinterpret_cast<uint32_t *>(dres + uoff) : nullptr;
     uint64_t total = 0;
-    for (int attempt = 0; attempt < 2; attempt++) {
+    for (int attempt = 0, tries = 0; attempt < 3; attempt++) {
         if (!ln.pin_vals) {
             ln.pin_vals_cap = std::max<uint64_t>(ln.pin_vals_cap, 1 << 16);
             HIPCHK(ix, hipHostMalloc(&ln.pin_vals, ln.pin_vals_cap * 4, hipHostMallocMapped));
@@ -1978,7 +2075,10 @@ int tm_match_batch_ex(tm_index *ix, uint64_t n, const uint8_t *tb, const uint64_
         const DevIndex d = dev_view(ix, ln.r);
         uint32_t tag;
         if (int rc = next_tag(ix, ln, s, tag)) return rc;
-        HIPCHK(ix, launch_match(d, ln.w, n, dbytes, doffs, dhit, derr, vdst, ln.pin_vals_cap, tag, s));
+        int path = PATH_PHASES;
+        HIPCHK(ix, launch_match(d, ln.w, n, dbytes, doffs, dhit, derr, vdst, ln.pin_vals_cap, tag, next_lb(ix),
+                                ix->dbg_phases, s, nullptr, nullptr, &path));
+        ix->path_batches[path]++;
         if (sorted) {
             HIPCHK(ix, launch_sort_segments(ln.w, n, dhit, vdst, ln.pin_vals_cap, unique, dunq, s));
             HIPCHK(ix, launch_copy_values(dhit, n, vdst, ln.pin_vals_dev, ln.pin_vals_cap, s));
@@ -1989,8 +2089,14 @@ int tm_match_batch_ex(tm_index *ix, uint64_t n, const uint8_t *tb, const uint64_
         if (timing && nt < 5) tt[nt++] = now_us();
         HIPCHK(ix, hipStreamSynchronize(s));
         if (timing && nt < 6) tt[nt++] = now_us();
+        if (batch_failed(ix, ln)) {   // the look-back failed: run the batch again, once
+            if ((rc = retry_or_fail(ix, g, ln, tries++))) return rc;
+            attempt--;
+            continue;
+        }
         memcpy(&total, ln.pin_out + n * 8, 8);
         if (total <= ln.pin_vals_cap || !out_vals || total <= 0) break;
+        if (attempt == 2) return fail(ix, TM_EDEVICE, "tm_match_batch: hit total kept growing past the staging buffer");
         // grow the mapped buffer and run the batch again (rare: sizes are sticky)
         g.lock();
         HIPCHK(ix, hipHostFree(ln.pin_vals));
@@ -2101,6 +2207,31 @@ int tm_profile_read(tm_index *ix, double *walk_ms, double *batch_ms, uint64_t *b
     return TM_OK;
 }
 
+int tm_debug_set(tm_index *ix, uint32_t key, uint64_t value) {
+    if (!ix) return fail(nullptr, TM_EINVAL, "tm_debug_set: null handle");
+    std::lock_guard<std::mutex> g(ix->mu);
+    switch (key) {
+    case TM_DEBUG_LB_SPINS: ix->dbg_lb.spins = value > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)value; break;
+    case TM_DEBUG_LB_FAIL_BLOCK: ix->dbg_lb.fail_block = value > 0xFFFFFFFFull ? NONE : (uint32_t)value; break;
+    case TM_DEBUG_LB_LAUNCHES: ix->dbg_lb_launches = value; break;
+    case TM_DEBUG_PHASES: ix->dbg_phases = value != 0; break;
+    default: return fail(ix, TM_EINVAL, "tm_debug_set: unknown key");
+    }
+    return TM_OK;
+}
+
+int tm_debug_get(tm_index *ix, uint32_t key, uint64_t *value) {
+    if (!ix || !value) return fail(ix, TM_EINVAL, "tm_debug_get: null argument");
+    switch (key) {
+    case TM_DEBUG_FAILED_BATCHES: *value = ix->failed_batches.load(); break;
+    case TM_DEBUG_RETRIED_BATCHES: *value = ix->retried_batches.load(); break;
+    case TM_DEBUG_PATH_PHASES: *value = ix->path_batches[PATH_PHASES].load(); break;
+    case TM_DEBUG_PATH_SMALL: *value = ix->path_batches[PATH_SMALL].load(); break;
+    case TM_DEBUG_PATH_ONE: *value = ix->path_batches[PATH_ONE].load(); break;
+    default: return fail(ix, TM_EINVAL, "tm_debug_get: unknown key");
+    }
+    return TM_OK;
+}
 
 // ------------------------------------------------------- matches_filter/3
 

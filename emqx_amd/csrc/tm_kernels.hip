@@ -157,11 +157,17 @@ __device__ __forceinline__ uint32_t ctab_find(const DevIndex &ix, uint32_t off, 
 // entered through '+' (pm, bit q: the node at depth q + 1 is a '+' child).  The
 // main walk's store does not: a topic that meets such a cut is handed to the
 // tail lists (DFS_REROUTE), keeping k_walk_fast within its register budget.
-template <int ML>
+//
+// LITE (k_walk_one's second look at a topic deeper than FAST_L): the main
+// walk's FAST_L levels, but tokenised like the deeper stores -- every level
+// scanned (count, badarg), only the levels a walk can use resolved
+// (need_levels) -- which one_pass_ok guarantees fit FAST_L.
+template <int ML, bool LITE = false>
 struct LdsStore {
     static constexpr uint32_t maxl = ML;
     static constexpr bool deferred = true;   // vocab probes of short words after tokenisation
     static constexpr bool cuts = ML > FAST_L;
+    static constexpr bool need = ML > FAST_L || LITE;   // resolve only need_levels(), scan the rest
     uint32_t *wid, *pend;
     uint8_t *len8;                           // [level][thread] word lengths (deferred probes)
     uint32_t stride;
@@ -207,6 +213,7 @@ struct GlobalStore {
     static constexpr uint32_t maxl = MAX_LEVELS;
     static constexpr bool deferred = false;
     static constexpr bool cuts = true;
+    static constexpr bool need = true;
     uint32_t *wid;
     uint2 *stk;
     uint8_t *plus_at;
@@ -297,7 +304,7 @@ __device__ int tokenize(const DevIndex &ix, const uint8_t *blob, uint64_t beg, u
         // resolves only the levels a walk can use: down to the trie's depth,
         // or all of them when a binary key of L levels exists -- so a 64-level
         // topic against a 6-level trie stays on the LDS path (need_levels).
-        constexpr bool NEED = S::maxl > FAST_L;
+        constexpr bool NEED = S::need;
         uint32_t lev = 0, len = 0, b0 = 0, b1 = 0;
         uint64_t ws = beg;
         bool bad = false;   // tail store: a level past the stored ones is exactly '+' or '#'
@@ -367,7 +374,7 @@ __device__ int tokenize(const DevIndex &ix, const uint8_t *blob, uint64_t beg, u
         }
         // base_init (:160-163): the first level starts with '$'
         dollar = st.word_len(0) == 255 ? blob[beg] == '$' : st.word_len(0) >= 1 && (st.word_b0(0) & 0xFFu) == '$';
-        for (uint32_t l = 0; l < (S::maxl > FAST_L ? L >> 24 : L); l++) {
+        for (uint32_t l = 0; l < (S::need ? L >> 24 : L); l++) {
             if (st.word_len(l) != 255) continue;
             WordAcc w; w.reset(beg + st.word_b1(l)); w.len = st.word_b0(l);
             st.set_wid(l, vocab_find(ix, w, blob));
@@ -410,14 +417,14 @@ __device__ int tokenize(const DevIndex &ix, const uint8_t *blob, uint64_t beg, u
         // (unused levels read slot 0) and consumes all of them, so no load is
         // left pending on a skipped branch -- the compiler would otherwise drain
         // vmcnt(0) before reusing its registers and serialise the probes.
-        for (uint32_t base = 0; base < (S::maxl > FAST_L ? L >> 24 : L); base += VGROUP) {
+        for (uint32_t base = 0; base < (S::need ? L >> 24 : L); base += VGROUP) {
             uint4 e[VGROUP];
             uint32_t tg[VGROUP];
             bool use[VGROUP];
 #pragma unroll
             for (uint32_t k = 0; k < VGROUP; k++) {
                 const uint32_t l = base + k;
-                use[k] = l < (S::maxl > FAST_L ? L >> 24 : L) && !((longmask >> l) & 1);
+                use[k] = l < (S::need ? L >> 24 : L) && !((longmask >> l) & 1);
                 const uint32_t ls = use[k] ? l : 0;
                 const uint32_t len = st.word_len(ls);
                 const uint64_t h = word_hash_short(st.word_b0(ls), st.word_b1(ls), len);
@@ -442,7 +449,7 @@ __device__ int tokenize(const DevIndex &ix, const uint8_t *blob, uint64_t beg, u
             }
         }
     }
-    if constexpr (S::deferred && S::maxl > FAST_L) {
+    if constexpr (S::deferred && S::need) {
       const uint32_t Lw = L >> 24;
       L &= 0xFFFFFFu;
       if (Lw < L) {
@@ -627,7 +634,7 @@ struct FirstEmit {          // match/2: stop at the first hit
 };
 
 template <class S, class EM>
-__device__ int match_topic(const DevIndex &ix, const uint8_t *blob, uint64_t beg, uint64_t end, S &st, EM &em,
+__device__ __forceinline__ int match_topic(const DevIndex &ix, const uint8_t *blob, uint64_t beg, uint64_t end, S &st, EM &em,
                             uint32_t *levels = nullptr) {
     uint32_t L = 0; bool dollar, allf; uint64_t xh;
     int rc = tokenize(ix, blob, beg, end, st, L, dollar, xh, allf);
@@ -733,6 +740,50 @@ __device__ __forceinline__ uint64_t wave_incl_scan(uint64_t v) {
         if (lane >= d) v += o;
     }
     return v;
+}
+
+// Decoupled look-back of the one-launch kernels, by one whole wave: block vb
+// (in start order) publishes its own total `sum` (LB_AGG), reads its
+// predecessors' words 64 at a time (lane k: block hi - k) back to the nearest
+// inclusive prefix, publishes its own inclusive prefix and returns its
+// exclusive one (in every lane).  A predecessor took its ticket before vb, so
+// it is running and publishes soon; the wait for one word is still bounded
+// (lb.spins polls): past it -- or when a predecessor failed, or vb is the
+// test hook's lb.fail_block -- `fail` is set and vb publishes LB_FAIL, which
+// every later block meets and propagates.  Nothing after a failed block is
+// trusted: the caller flags its topics err 4 and raises the workspace's fail
+// word (a failed block used to publish a partial prefix that its
+// successors took as correct).
+__device__ __forceinline__ uint64_t look_back(uint64_t *look, uint32_t vb, uint32_t tag, uint64_t sum, const LbCtl &lb,
+                                              bool &fail) {
+    const uint32_t lane = threadIdx.x & 63;
+    uint64_t pre = 0;
+    fail = vb == lb.fail_block;
+    if (!fail && vb > 0 && lane == 0)
+        __hip_atomic_store(&look[vb], lb_word(tag, LB_AGG, sum), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t spins = 0;
+    for (int64_t hi = (int64_t)vb - 1; hi >= 0 && !fail;) {
+        const int64_t j = hi - (int64_t)lane;
+        uint64_t f = lb_word(tag, LB_INCL, 0);   // before block 0: an inclusive prefix of 0
+        if (j >= 0)
+            for (;;) {
+                f = __hip_atomic_load(&look[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (lb_tag(f) == tag || ++spins > lb.spins) break;
+                __builtin_amdgcn_s_sleep(1);
+            }
+        if (__ballot(lb_tag(f) != tag || lb_state(f) == LB_FAIL)) { fail = true; break; }
+        const uint64_t mi = __ballot(lb_state(f) == LB_INCL);
+        const uint32_t k = mi ? (uint32_t)__ffsll((long long)mi) - 1 : 63;   // nearest inclusive prefix
+        uint64_t v = lane <= k ? f & LB_VAL_MASK : 0;
+        for (int d = 32; d; d >>= 1) v += __shfl_xor(v, d, 64);
+        pre += v;
+        if (mi) break;
+        hi -= 64;
+    }
+    if (lane == 0)
+        __hip_atomic_store(&look[vb], fail ? lb_word(tag, LB_FAIL, 0) : lb_word(tag, LB_INCL, pre + sum),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return pre;
 }
 
 __device__ __forceinline__ uint32_t wave_excl_scan32(uint32_t v, uint32_t &total) {
@@ -1050,15 +1101,26 @@ struct CountEmit {          // one-launch path: hit count only (the values come 
 // -> 0.075 ms, 32k 0.173 -> 0.111, 64k 0.208 -> 0.189; profiles/r3/sm64k/).
 constexpr uint64_t SMALL_TOPICS = 65536;
 
-bool small_path_ok(const DevIndex &ix, uint64_t n) {
-    // the fallback store resolves need_levels() (+2 look-ahead levels) within MID_L
-    return n && n <= SMALL_TOPICS && ix.depth + 2 <= (uint32_t)MID_L && ix.xlen_max + 2 <= (uint32_t)MID_L;
+// the one-launch kernels' fallback store resolves need_levels() (+2 look-ahead
+// levels) within MID_L for every topic of this index
+bool one_launch_ok(const DevIndex &ix) {
+    return ix.depth + 2 <= (uint32_t)MID_L && ix.xlen_max + 2 <= (uint32_t)MID_L;
+}
+
+bool small_path_ok(const DevIndex &ix, uint64_t n) { return n && n <= SMALL_TOPICS && one_launch_ok(ix); }
+
+// k_walk_one walks every topic with FAST_L-level stores: a topic deeper than
+// that needs only the levels down to the trie's depth (+2 look-ahead) when no
+// binary key is longer than FAST_L levels, and its main store makes no
+// '#'-not-last cut (the deeper stores' job)
+bool one_pass_ok(const DevIndex &ix) {
+    return !ix.hdesc && ix.depth + 2 <= (uint32_t)FAST_L && ix.xlen_max <= (uint32_t)FAST_L;
 }
 
 template <int MODE>
 __global__ __launch_bounds__(WV_BLOCK) void k_walk_small(DevIndex ix, Workspace ws, uint64_t n, const uint8_t *blob,
                                                          const uint64_t *offs, Outs o, uint64_t *hit_offs,
-                                                         uint32_t *out, uint64_t cap, uint32_t tag) {
+                                                         uint32_t *out, uint64_t cap, uint32_t tag, LbCtl lb) {
     constexpr int W = WAVE_W;
     constexpr uint32_t G = 64 / W;                        // topics per wave
     constexpr uint32_t MAXL = W < 31 ? W : 31;
@@ -1287,45 +1349,19 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_small(DevIndex ix, Workspace 
     }
     __syncthreads();
     if (wv == 0) {
-        const uint32_t lane = threadIdx.x;
         uint64_t sum = 0;
         for (int i = 0; i < SM_TOPICS; i++) sum += s_cnt[i];
-        if (vb > 0 && lane == 0)
-            __hip_atomic_store(&ws.look[vb], lb_word(tag, LB_AGG, sum), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        // The wave reads 64 predecessors at once (lane k: block hi - k), so
-        // the look-back costs one flag round trip per 64 blocks, not one per
-        // block.  Block j started before this one (its ticket is smaller), so
-        // it publishes soon; the wait is bounded all the same (a lost
-        // publication must not leave a spinning grid behind): past the bound
-        // the block's topics get err 4 and the batch fails loudly.
-        uint64_t pre = 0;
-        uint32_t fail = 0, spins = 0;
-        for (int64_t hi = (int64_t)vb - 1; hi >= 0;) {
-            const int64_t j = hi - (int64_t)lane;
-            uint64_t f = lb_word(tag, LB_INCL, 0);   // before block 0: an inclusive prefix of 0
-            if (j >= 0)
-                for (;;) {
-                    f = __hip_atomic_load(&ws.look[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if (lb_tag(f) == tag || ++spins > (1u << 22)) break;
-                    __builtin_amdgcn_s_sleep(1);
-                }
-            if (__ballot(lb_tag(f) != tag)) { fail = 1; break; }
-            const uint64_t mi = __ballot(lb_state(f) == LB_INCL);
-            const uint32_t k = mi ? (uint32_t)__ffsll((long long)mi) - 1 : 63;   // nearest inclusive prefix
-            uint64_t v = lane <= k ? f & LB_VAL_MASK : 0;
-            for (int d = 32; d; d >>= 1) v += __shfl_xor(v, d, 64);
-            pre += v;
-            if (mi) break;
-            hi -= 64;
-        }
-        if (lane == 0) {
+        // one flag round trip per 64 predecessors (look_back); a failed wait
+        // fails this block and every later one: err 4, the fail word raised
+        bool fail;
+        const uint64_t pre = look_back(ws.look, vb, tag, sum, lb, fail);
+        if (threadIdx.x == 0) {
             s_fail = fail;
             s_sum = sum;
-            __hip_atomic_store(&ws.look[vb], lb_word(tag, LB_INCL, pre + sum), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
             s_base = pre;
+            if (fail) ws.hint_d[HINT_FAIL] = 1;
             if (vb == gridDim.x - 1) {
-                hit_offs[n] = pre + sum;
+                if (!fail) hit_offs[n] = pre + sum;
                 ws.list_n[L_COUNT + 4] = 0;   // every ticket is taken
             }
         }
@@ -1553,6 +1589,132 @@ constexpr int EMIT_Q = 1;   // quads per lane per iteration (loads in flight bef
 constexpr uint64_t EMIT_RUNS = 16;   // average run length from which a wave copies run by run
 constexpr uint8_t RF_INLINE = 1, RF_SKIP = 2;   // s_flg: a one-value run kept inline / an overflowed topic's positions
 
+// One wave writes the values of R ranges flattened in LDS into out[base, endp):
+// s_off = the range's value offset (RF_INLINE: the value itself), s_rel = its
+// first position relative to base (s_rel[R] = endp - base), s_flg (RF_SKIP: a
+// re-walked topic's positions, written by its re-walk).  Shared by k_emit
+// (ranges read back from the walk's range lists) and k_walk_one (ranges
+// straight from the walk's registers).
+__device__ __forceinline__ void wave_emit(const DevIndex &ix, const uint32_t *s_off, const uint32_t *s_rel,
+                                          const uint8_t *s_flg, uint32_t R, uint64_t base, uint64_t endp,
+                                          uint32_t *out, uint64_t cap) {
+    const int lane = threadIdx.x & 63;
+    if (!R) return;
+    const bool vec = (reinterpret_cast<uintptr_t>(out) & 15) == 0;
+    const uint64_t q1 = (endp + 3) >> 2;
+    if (endp - base >= (uint64_t)EMIT_RUNS * R) {
+        // Long runs (C2: 250 IDs per filter; average run >= EMIT_RUNS values):
+        // copy run by run.  The wave walks its ranges in order; for each, lane
+        // l writes the l-th 16-B quad of the run's output with one dword-
+        // aligned 16-B load from the run (the vals device copy has a 4-word
+        // guard before the first run and >= 16 words after the last, so the
+        // load may overhang the run) and one non-temporal store: a few
+        // instructions per KiB instead of a range search per quad.  The quads
+        // a run shares with its neighbours take dword stores of its own
+        // elements.  C2 batch 1.43 -> 1.10 ms (profiles/r2_emit_variants.txt;
+        // the variants that wrote every quad once, whole -- a window of <= 4
+        // ranges per 1 KiB, extra loads of the next runs, a quad carried
+        // between runs in scalar registers -- all measured slower: each extra
+        // load or cross-lane step per quad costs more than the partial writes).
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        for (uint32_t i = 0; i < R; i++) {
+            const uint32_t ro = s_off[i], rf = s_flg[i];
+            const uint64_t P = base + s_rel[i];
+            if (rf & RF_SKIP) continue;
+            if (rf & RF_INLINE) {
+                if (lane == 0 && P < cap) out[P] = ro;
+                continue;
+            }
+            const uint64_t E = base + s_rel[i + 1];
+            for (uint64_t Q = (P >> 2) + lane; (Q << 2) < E; Q += 64) {
+                const uint64_t p0 = Q << 2;
+                const uint4 a = *reinterpret_cast<const uint4u *>(ix.vals + ro + (int64_t)(p0 - P));
+                if (vec && p0 >= P && p0 + 4 <= E && p0 + 3 < cap) {
+                    const u32x4 x = {a.x, a.y, a.z, a.w};
+                    __builtin_nontemporal_store(x, reinterpret_cast<u32x4 *>(out + p0));
+                } else {
+                    const uint32_t e[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+                    for (int k = 0; k < 4; k++)
+                        if (p0 + k >= P && p0 + k < E && p0 + k < cap) out[p0 + k] = e[k];
+                }
+            }
+        }
+        return;
+    }
+    uint32_t r = 0;   // last range starting at or before the lane's position (positions only grow)
+    // one quad: its range found from the lane's previous one (positions only
+    // grow; a lane moves 256 positions per quad, so a few steps forward cover
+    // long ranges -- C2: 250 values -- and a binary search the rest), then its
+    // four values
+    auto fetch = [&](uint64_t q, uint32_t (&v)[4], bool (&ok)[4]) {
+        const uint64_t p0 = q << 2;
+        const uint32_t first = (uint32_t)((p0 > base ? p0 : base) - base);
+        uint32_t k = 0;
+        while (k < 2 && r + 1 < R && s_rel[r + 1] <= first) { r++; k++; }
+        if (r + 1 < R && s_rel[r + 1] <= first) {
+            uint32_t lo = r + 1, hi = R - 1;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi + 1) >> 1;
+                if (s_rel[mid] <= first) lo = mid; else hi = mid - 1;
+            }
+            r = lo;
+        }
+        if (q < q1 && p0 >= base && p0 + 3 < endp) {   // whole quad inside one run: one 16-B load
+            const uint32_t rs = s_rel[r], re = s_rel[r + 1];
+            if (!s_flg[r] && first >= rs && first + 3 < re) {
+                const uint4 a = *reinterpret_cast<const uint4u *>(ix.vals + s_off[r] + (first - rs));
+                v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+                ok[0] = ok[1] = ok[2] = ok[3] = true;
+                return;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint64_t p = p0 + k;
+            ok[k] = false; v[k] = 0;
+            if (q >= q1 || p < base || p >= endp) continue;
+            const uint32_t x = (uint32_t)(p - base);
+            while (r + 1 < R && s_rel[r + 1] <= x) r++;
+            const uint32_t rs = s_rel[r], rf = s_flg[r];
+            if (!(rf & RF_SKIP) && x >= rs && x < s_rel[r + 1]) {
+                v[k] = (rf & RF_INLINE) ? s_off[r] : ix.vals[s_off[r] + (x - rs)];
+                ok[k] = true;
+            }
+        }
+    };
+    auto put = [&](uint64_t q, const uint32_t (&v)[4], const bool (&ok)[4]) {
+        const uint64_t p0 = q << 2;
+        if (vec && ok[0] && ok[1] && ok[2] && ok[3] && p0 + 3 < cap) {
+            // non-temporal: the hit lists are not read back by the GPU, and
+            // dirty output lines left in L2 slow the next batch's walk (C2
+            // walk 0.150 -> 0.124 ms, C3 batch -1 %)
+            typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+            const u32x4 x = {v[0], v[1], v[2], v[3]};
+            __builtin_nontemporal_store(x, reinterpret_cast<u32x4 *>(out + p0));
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                if (ok[k] && p0 + k < cap) out[p0 + k] = v[k];
+        }
+    };
+    // EMIT_Q quads per iteration, all their value loads issued before any
+    // store (the compiler cannot move a vals load above a store to out).  The
+    // lanes start at the 128-byte line holding the span's first quad, so every
+    // store instruction covers 8 whole lines instead of 9 partial ones
+    // (tools/store_bench: 16-B- but not 128-B-aligned 1 KiB stores write at
+    // 4.2-4.8 TB/s, aligned ones at 5.2-5.7); lanes before the span store
+    // nothing.
+    for (uint64_t q = ((base >> 2) & ~7ull) + lane; q < q1; q += 64 * EMIT_Q) {
+        uint32_t v[EMIT_Q][4];
+        bool ok[EMIT_Q][4];
+#pragma unroll
+        for (int j = 0; j < EMIT_Q; j++) fetch(q + 64 * j, v[j], ok[j]);
+#pragma unroll
+        for (int j = 0; j < EMIT_Q; j++) put(q + 64 * j, v[j], ok[j]);
+    }
+}
+
 // One block = one tile of 256 topics: finishes the scan (tile prefix + local
 // exclusive scan -> hit_offs), then each wave flattens its 64 topics' value
 // ranges into LDS (sorted by output position) and every lane produces whole
@@ -1623,119 +1785,144 @@ __global__ __launch_bounds__(EMIT_BLOCK) void k_emit(DevIndex ix, Workspace ws, 
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (!R) return;
-    const bool vec = (reinterpret_cast<uintptr_t>(out) & 15) == 0;
-    const uint64_t q1 = (endp + 3) >> 2;
-    if (endp - base >= (uint64_t)EMIT_RUNS * R) {
-        // Long runs (C2: 250 IDs per filter; average run >= EMIT_RUNS values):
-        // copy run by run.  The wave walks its ranges in order; for each, lane
-        // l writes the l-th 16-B quad of the run's output with one dword-
-        // aligned 16-B load from the run (the vals device copy has a 4-word
-        // guard before the first run and >= 16 words after the last, so the
-        // load may overhang the run) and one non-temporal store: a few
-        // instructions per KiB instead of a range search per quad.  The quads
-        // a run shares with its neighbours take dword stores of its own
-        // elements.  C2 batch 1.43 -> 1.10 ms (profiles/r2_emit_variants.txt;
-        // the variants that wrote every quad once, whole -- a window of <= 4
-        // ranges per 1 KiB, extra loads of the next runs, a quad carried
-        // between runs in scalar registers -- all measured slower: each extra
-        // load or cross-lane step per quad costs more than the partial writes).
-        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-        for (uint32_t i = 0; i < R; i++) {
-            const uint32_t ro = s_off[wv][i], rf = s_flg[wv][i];
-            const uint64_t P = base + s_rel[wv][i];
-            if (rf & RF_SKIP) continue;
-            if (rf & RF_INLINE) {
-                if (lane == 0 && P < cap) out[P] = ro;
-                continue;
-            }
-            const uint64_t E = base + s_rel[wv][i + 1];
-            for (uint64_t Q = (P >> 2) + lane; (Q << 2) < E; Q += 64) {
-                const uint64_t p0 = Q << 2;
-                const uint4 a = *reinterpret_cast<const uint4u *>(ix.vals + ro + (int64_t)(p0 - P));
-                if (vec && p0 >= P && p0 + 4 <= E && p0 + 3 < cap) {
-                    const u32x4 x = {a.x, a.y, a.z, a.w};
-                    __builtin_nontemporal_store(x, reinterpret_cast<u32x4 *>(out + p0));
-                } else {
-                    const uint32_t e[4] = {a.x, a.y, a.z, a.w};
+    wave_emit(ix, s_off[wv], s_rel[wv], s_flg[wv], R, base, endp, out, cap);
+}
+
+// ------------------------------------------------ large batches in one pass
+//
+// k_walk_one: the whole count-mode batch above SMALL_TOPICS topics in ONE
+// launch.  The two-phase path (k_walk_fast, tails,
+// k_scan_top, k_emit, k_rewalk_tail) parks every topic's value ranges in HBM
+// between the walk and the emit -- 44 B/topic written and 73 B/topic read back
+// on C3 -- and its three short kernels queue behind other streams' walks for
+// workgroup slots.  Here a 64-lane block (one wave, one topic per lane)
+//   1. walks its topics exactly as k_walk_fast (the same dfs, LDS store and
+//      register ranges);
+//   2. counts the topics deeper than FAST_L levels with a second walk over the
+//      same LDS, tokenised with every level scanned and only the levels the
+//      trie can use resolved (LdsStore<FAST_L, true>; one_pass_ok: the index's
+//      depth and binary keys fit FAST_L, and it holds no '#'-not-last key);
+//      a lane's ranges wait in its own (dead) column of the walk store;
+//   3. gets its global offset from the decoupled look-back (look_back, over
+//      the blocks in start order -- a ticket, so it only waits for blocks
+//      already running);
+//   4. writes its offsets and flags, and its values straight from the
+//      registers: the ranges go to LDS (the walk store's space) and the wave
+//      writes the block's span with wave_emit, as k_emit does per wave;
+//   5. re-walks the topics whose values it could not keep (more than RCAP
+//      ranges, or deeper than FAST_L) and writes their values directly.
+// Per topic it writes only the CSR itself: 8 B offset + 1 B flag + 4 B per
+// value; nothing else crosses HBM between the steps.
+static_assert(WALK_BLOCK == 64, "k_walk_one: one wave per block");
+union OneLds {   // a k_walk_one block's LDS, reused step by step (4864 B: 8 waves per SIMD as k_walk_fast)
+    struct { uint32_t wid[FAST_L * WALK_BLOCK], pend[(FAST_L + 1) * WALK_BLOCK]; uint8_t len[FAST_L * WALK_BLOCK]; } walk;
+    struct { uint32_t off[WR], rel[WR + 1]; uint8_t flg[WR]; } emit;
+};
+
+// (the workspace comes as the four pointers k_walk_one uses -- ticket,
+// parked ranges, look-back words, fail word -- not the whole struct: fewer
+// scalar registers held across the walk)
+__global__ __launch_bounds__(WALK_BLOCK, 8) void k_walk_one(DevIndex ix, uint32_t *ticket, uint2 *rng, uint64_t *look,
+                                                          uint32_t *fail_word, uint64_t n, const uint8_t *blob,
+                                                          const uint64_t *offs, uint8_t *err, uint64_t *hit_offs,
+                                                          uint32_t *out, uint64_t cap, uint32_t tag, LbCtl lb) {
+    __shared__ OneLds S;
+    const uint32_t lane = threadIdx.x;
+    uint32_t vb = 0;
+    if (lane == 0) {
+        vb = atomicAdd(ticket, 1u);   // blocks scan in start order
+        if (vb == gridDim.x - 1) atomicExch(ticket, 0u);   // every ticket is taken
+    }
+    vb = __builtin_amdgcn_readfirstlane((uint32_t)__shfl((int)vb, 0, 64));
+    const uint64_t t = (uint64_t)vb * WALK_BLOCK + lane;
+    const bool live = t < n;
+
+    // ---- 1. the walk (k_walk_fast's)
+    uint32_t cnt = 0, nr = 0, e = 0;
+    int rc = RC_OK;
+    if (live) {
+        RangeEmit em;
+        em.cnt = 0; em.nr = 0;
+        LdsStore<FAST_L> st{S.walk.wid + lane, S.walk.pend + lane, S.walk.len + lane, WALK_BLOCK, 0};
+        rc = match_topic(ix, blob, offs[t], offs[t + 1], st, em);
+        if (rc == RC_OK) {
+            cnt = em.cnt; nr = em.nr;
+            // the ranges go into this lane's own column of the walk store
+            // (FAST_L + (FAST_L + 1) words >= 2 RCAP), dead once its walk is
+            // done: no register holds them across the rest of the kernel
+            static_assert(2 * RCAP <= 2 * FAST_L + 1, "a lane's store column holds its ranges");
 #pragma unroll
-                    for (int k = 0; k < 4; k++)
-                        if (p0 + k >= P && p0 + k < E && p0 + k < cap) out[p0 + k] = e[k];
-                }
-            }
+            for (uint32_t i = 0; i < RCAP; i++)
+                if (i < nr) { S.walk.wid[i * WALK_BLOCK + lane] = em.r[i].x; S.walk.pend[i * WALK_BLOCK + lane] = em.r[i].y; }
         }
+        e = rc == RC_BADARG ? 1u : 0u;
+    }
+    const bool deep = rc == RC_DEEP;
+    bool rew = deep || nr > RCAP;   // values written by a re-walk (step 5)
+
+    // ---- 2. topics deeper than the main store: counted by a second walk in
+    // their own store columns (the other lanes' columns hold their ranges)
+    if (deep) {   // (rare: C3 has none, C3deep ~6 per block)
+        LdsStore<FAST_L, true> st{S.walk.wid + lane, S.walk.pend + lane, S.walk.len + lane, WALK_BLOCK, 0};
+        CountEmit ce{0};
+        const int frc = match_topic(ix, blob, offs[t], offs[t + 1], st, ce);
+        cnt = frc == RC_OK ? (uint32_t)ce.cnt : 0u;
+        e = frc == RC_BADARG ? 1u : frc == RC_DEEP ? 2u : 0u;   // RC_DEEP here: > MAX_LEVELS levels
+    }
+    rew = rew && e == 0 && cnt > 0;
+
+    // ---- 3. the block's offset
+    const uint64_t inc = wave_incl_scan(cnt);
+    const uint64_t total = __shfl(inc, 63, 64), rel = inc - cnt;
+    bool fail;
+    const uint64_t base = look_back(look, vb, tag, total, lb, fail);
+    if (fail) {   // (wave-uniform) no trusted offset: the host runs the batch again
+        if (live) err[t] = 4;
+        if (lane == 0) *fail_word = 1;
         return;
     }
-    uint32_t r = 0;   // last range starting at or before the lane's position (positions only grow)
-    // one quad: its range found from the lane's previous one (positions only
-    // grow; a lane moves 256 positions per quad, so a few steps forward cover
-    // long ranges -- C2: 250 values -- and a binary search the rest), then its
-    // four values
-    auto fetch = [&](uint64_t q, uint32_t (&v)[4], bool (&ok)[4]) {
-        const uint64_t p0 = q << 2;
-        const uint32_t first = (uint32_t)((p0 > base ? p0 : base) - base);
-        uint32_t k = 0;
-        while (k < 2 && r + 1 < R && s_rel[wv][r + 1] <= first) { r++; k++; }
-        if (r + 1 < R && s_rel[wv][r + 1] <= first) {
-            uint32_t lo = r + 1, hi = R - 1;
-            while (lo < hi) {
-                const uint32_t mid = (lo + hi + 1) >> 1;
-                if (s_rel[wv][mid] <= first) lo = mid; else hi = mid - 1;
-            }
-            r = lo;
-        }
-        if (q < q1 && p0 >= base && p0 + 3 < endp) {   // whole quad inside one run: one 16-B load
-            const uint32_t rs = s_rel[wv][r], re = s_rel[wv][r + 1];
-            if (!s_flg[wv][r] && first >= rs && first + 3 < re) {
-                const uint4 a = *reinterpret_cast<const uint4u *>(ix.vals + s_off[wv][r] + (first - rs));
-                v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
-                ok[0] = ok[1] = ok[2] = ok[3] = true;
-                return;
-            }
-        }
+
+    // ---- 4. offsets, flags, values
+    if (live) {
+        __builtin_nontemporal_store(base + rel, hit_offs + t);
+        __builtin_nontemporal_store((uint8_t)e, err + t);
+    }
+    if (lane == 0 && vb == gridDim.x - 1) hit_offs[n] = base + total;
+    uint32_t R;
+    const uint32_t nrr = rew ? 1u : (rc == RC_OK ? nr : 0u);
+    const uint32_t r0 = wave_excl_scan32(nrr, R);
+    uint2 rg[RCAP];   // this lane's ranges, out of its store column before the stage overwrites it
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const uint64_t p = p0 + k;
-            ok[k] = false; v[k] = 0;
-            if (q >= q1 || p < base || p >= endp) continue;
-            const uint32_t x = (uint32_t)(p - base);
-            while (r + 1 < R && s_rel[wv][r + 1] <= x) r++;
-            const uint32_t rs = s_rel[wv][r], rf = s_flg[wv][r];
-            if (!(rf & RF_SKIP) && x >= rs && x < s_rel[wv][r + 1]) {
-                v[k] = (rf & RF_INLINE) ? s_off[wv][r] : ix.vals[s_off[wv][r] + (x - rs)];
-                ok[k] = true;
-            }
+    for (uint32_t i = 0; i < RCAP; i++)
+        rg[i] = i < nrr && !rew ? make_uint2(S.walk.wid[i * WALK_BLOCK + lane], S.walk.pend[i * WALK_BLOCK + lane])
+                                : make_uint2(0, 0);
+    wave_sync();   // every lane has its ranges: the LDS becomes the range stage
+    const uint32_t rel32 = (uint32_t)rel;
+    if (rew) {
+        S.emit.off[r0] = 0; S.emit.rel[r0] = rel32; S.emit.flg[r0] = RF_SKIP;
+    } else {
+        uint32_t acc = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < RCAP; i++) {
+            if (i >= nrr) break;
+            S.emit.off[r0 + i] = rg[i].x;          // RUN_INLINE: the value itself
+            S.emit.rel[r0 + i] = rel32 + acc;
+            S.emit.flg[r0 + i] = (rg[i].y & RUN_INLINE) ? RF_INLINE : 0;
+            acc += rg[i].y & RUN_CNT;
         }
-    };
-    auto put = [&](uint64_t q, const uint32_t (&v)[4], const bool (&ok)[4]) {
-        const uint64_t p0 = q << 2;
-        if (vec && ok[0] && ok[1] && ok[2] && ok[3] && p0 + 3 < cap) {
-            // non-temporal: the hit lists are not read back by the GPU, and
-            // dirty output lines left in L2 slow the next batch's walk (C2
-            // walk 0.150 -> 0.124 ms, C3 batch -1 %)
-            typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-            const u32x4 x = {v[0], v[1], v[2], v[3]};
-            __builtin_nontemporal_store(x, reinterpret_cast<u32x4 *>(out + p0));
-        } else {
-#pragma unroll
-            for (int k = 0; k < 4; k++)
-                if (ok[k] && p0 + k < cap) out[p0 + k] = v[k];
+    }
+    if (lane == 0) S.emit.rel[R] = (uint32_t)total;
+    wave_sync();
+    wave_emit(ix, S.emit.off, S.emit.rel, S.emit.flg, R, base, base + total, out, cap);
+
+    // ---- 5. re-walks: values straight into the CSR
+    if (__ballot(rew)) {
+        wave_sync();   // the LDS holds walk stores again
+        if (rew) {
+            LdsStore<FAST_L, true> st{S.walk.wid + lane, S.walk.pend + lane, S.walk.len + lane, WALK_BLOCK, 0};
+            DirectEmit de{ix.vals, out, base + rel, cap};
+            match_topic(ix, blob, offs[t], offs[t + 1], st, de);
         }
-    };
-    // EMIT_Q quads per iteration, all their value loads issued before any
-    // store (the compiler cannot move a vals load above a store to out).  The
-    // lanes start at the 128-byte line holding the span's first quad, so every
-    // store instruction covers 8 whole lines instead of 9 partial ones
-    // (tools/store_bench: 16-B- but not 128-B-aligned 1 KiB stores write at
-    // 4.2-4.8 TB/s, aligned ones at 5.2-5.7); lanes before the span store
-    // nothing.
-    for (uint64_t q = ((base >> 2) & ~7ull) + lane; q < q1; q += 64 * EMIT_Q) {
-        uint32_t v[EMIT_Q][4];
-        bool ok[EMIT_Q][4];
-#pragma unroll
-        for (int j = 0; j < EMIT_Q; j++) fetch(q + 64 * j, v[j], ok[j]);
-#pragma unroll
-        for (int j = 0; j < EMIT_Q; j++) put(q + 64 * j, v[j], ok[j]);
     }
 }
 
@@ -2025,13 +2212,21 @@ hipError_t launch_match_phase2(const DevIndex &ix, const Workspace &ws, uint64_t
 
 hipError_t launch_match(const DevIndex &ix, const Workspace &ws, uint64_t n, const uint8_t *bytes,
                         const uint64_t *offs, uint64_t *hit_offs, uint8_t *err, uint32_t *out, uint64_t cap,
-                        uint32_t tag, hipStream_t s, hipEvent_t ev_walk0, hipEvent_t ev_walk1) {
-    if (small_path_ok(ix, n)) {
+                        uint32_t tag, LbCtl lb, bool phases, hipStream_t s, hipEvent_t ev_walk0,
+                        hipEvent_t ev_walk1, int *path) {
+    const bool one = n && (n <= SMALL_TOPICS ? one_launch_ok(ix) : !phases && one_pass_ok(ix));
+    if (path) *path = !one ? PATH_PHASES : n <= SMALL_TOPICS ? PATH_SMALL : PATH_ONE;
+    if (one) {
         hipError_t e;
         Outs o{err, nullptr, nullptr};
         if (ev_walk0 && (e = hipEventRecord(ev_walk0, s)) != hipSuccess) return e;
-        hipLaunchKernelGGL(k_walk_small<MODE_COUNT>, dim3(blocks_for(n, SM_TOPICS)), dim3(WV_BLOCK), 0, s, ix, ws, n,
-                           bytes, offs, o, hit_offs, out, cap, tag & 0x3FFFFFFFu);
+        if (n <= SMALL_TOPICS)
+            hipLaunchKernelGGL(k_walk_small<MODE_COUNT>, dim3(blocks_for(n, SM_TOPICS)), dim3(WV_BLOCK), 0, s, ix, ws,
+                               n, bytes, offs, o, hit_offs, out, cap, tag & LB_TAG_MASK, lb);
+        else
+            hipLaunchKernelGGL(k_walk_one, dim3(blocks_for(n, WALK_BLOCK)), dim3(WALK_BLOCK), 0, s, ix,
+                               ws.list_n + L_COUNT + 4, ws.rng, ws.look, ws.hint_d + HINT_FAIL, n, bytes, offs, err,
+                               hit_offs, out, cap, tag & LB_TAG_MASK, lb);
         if (ev_walk1 && (e = hipEventRecord(ev_walk1, s)) != hipSuccess) return e;
         return hipGetLastError();
     }
@@ -2046,7 +2241,7 @@ hipError_t launch_first(const DevIndex &ix, const Workspace &ws, uint64_t n, con
     Outs o{nullptr, out_value, out_found};
     if (small_path_ok(ix, n)) {
         hipLaunchKernelGGL(k_walk_small<MODE_FIRST>, dim3(blocks_for(n, SM_TOPICS)), dim3(WV_BLOCK), 0, s, ix, ws, n,
-                           bytes, offs, o, nullptr, nullptr, (uint64_t)0, 0u);
+                           bytes, offs, o, nullptr, nullptr, (uint64_t)0, 0u, LbCtl{LB_SPINS, NONE});
         return hipGetLastError();
     }
     if (n <= WAVE_TOPICS)

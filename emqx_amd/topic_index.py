@@ -205,7 +205,9 @@ def matches_batch(topics, tab: Tab, opts=(), errors: str = "raise"):
 
     A topic with a '+'/'#' level is badarg (emqx_trie_search.erl:374-375) and
     one of more than 65536 levels is TopicTooDeep; the device flags each topic
-    on its own.  errors="raise" raises for the first such topic (one call, one
+    on its own.  A batch the device failed (err flag 4: the library already
+    ran it again once) raises DeviceError for the whole call -- never BadArg,
+    which the reference reserves for the topic itself.  errors="raise" raises for the first such topic (one call, one
     topic: the reference's behaviour); errors="return" puts the exception in
     that topic's slot and still returns every other topic's matches -- a
     micro-batch of many publishers fails only the bad publish, as each
@@ -214,6 +216,8 @@ def matches_batch(topics, tab: Tab, opts=(), errors: str = "raise"):
     ticket = tab.read_begin()
     try:
         kids, err = tab.match_kids(topics)
+        if len(err) and (err == 4).any():   # (the library returns TM_EDEVICE instead; never a client error)
+            raise _native.DeviceError(_native.TM_EDEVICE, "batch failed on the device (err flag 4)")
         out = []
         for i, ks in enumerate(kids):
             if err[i]:
@@ -307,5 +311,7 @@ def get_record(key, tab: Tab):
     return tab.lookup(key)
 
 
+DeviceError = _native.DeviceError
+
 __all__ = ["new", "insert", "delete", "match", "matches", "matches_batch", "matches_filter", "make_key", "get_id",
-           "get_topic", "get_record", "Tab", "BadArg", "TopicTooDeep"]
+           "get_topic", "get_record", "Tab", "BadArg", "TopicTooDeep", "DeviceError"]

@@ -52,8 +52,13 @@
  * A topic of more than 65536 levels (longer than MQTT's 65535-byte maximum,
  * emqx_mqtt.hrl:44, so never seen from a client) is not matched: err flag 2,
  * no hits.  Err flag 4 marks a topic whose batch failed inside the device
- * (a bounded wait of the one-launch small-batch scan expired): no result --
- * never expected; the batch should be retried and reported.
+ * (the bounded wait of a one-launch batch's look-back scan expired -- never
+ * expected: a block waits only for blocks already running); its offsets and
+ * values are undefined.  It is never a client error (the reference raises
+ * badarg only for a '+'/'#' level): the host API (tm_match_batch*) runs such
+ * a batch again once and returns TM_EDEVICE if it fails again, so its callers
+ * never see err 4; a device-API caller (tm_match_batch_dev*, asynchronous)
+ * finds the flags in d_out_err and submits the batch again.
  */
 #ifndef TMATCH_H
 #define TMATCH_H
@@ -261,11 +266,31 @@ int tm_merge_shards(uint32_t world, uint64_t n, const uint64_t *d_shard_hit_offs
                     void *stream);
 
 /* Diagnostics.  While enabled, every match batch records HIP events on its
- * stream around the main walk kernel (k_walk_fast) and around the whole batch;
+ * stream around the main walk kernel (k_walk_one / k_walk_small for a
+ * one-launch batch, k_walk_fast for a two-phase one) and around the whole batch;
  * tm_profile_read() resolves them and returns the accumulated device times
  * (milliseconds) and the number of batches since the last reset. */
 int tm_profile_enable(tm_index *h, int enable);
 int tm_profile_read(tm_index *h, double *walk_ms, double *batch_ms, uint64_t *batches, int reset);
+
+/* Test hooks (no reference counterpart; tests/test_gpu_parity.py):
+ *   TM_DEBUG_LB_SPINS       the look-back wait bound (polls of one word) of the
+ *   TM_DEBUG_LB_FAIL_BLOCK  next TM_DEBUG_LB_LAUNCHES one-launch batches, and
+ *   TM_DEBUG_LB_LAUNCHES    the block (in start order) that fails as if its
+ *                           wait expired (>= 2^32: none)
+ *   TM_DEBUG_PHASES         batches above 65536 topics: 1 the two-phase path
+ *                           (walk, tails, scan, emit), 0 one launch (k_walk_one,
+ *                           where the index allows it); the default is the
+ *                           faster of the two on C3
+ * tm_debug_get: TM_DEBUG_FAILED_BATCHES (one-launch batches whose look-back
+ * failed, host API), TM_DEBUG_RETRIED_BATCHES (of those, run again) and the
+ * match launches per kernel path: TM_DEBUG_PATH_PHASES (walk, tails, scan,
+ * emit), TM_DEBUG_PATH_SMALL (k_walk_small), TM_DEBUG_PATH_ONE (k_walk_one). */
+enum { TM_DEBUG_LB_SPINS = 1, TM_DEBUG_LB_FAIL_BLOCK = 2, TM_DEBUG_LB_LAUNCHES = 3, TM_DEBUG_PHASES = 4,
+       TM_DEBUG_FAILED_BATCHES = 5, TM_DEBUG_RETRIED_BATCHES = 6, TM_DEBUG_PATH_PHASES = 7,
+       TM_DEBUG_PATH_SMALL = 8, TM_DEBUG_PATH_ONE = 9 };
+int tm_debug_set(tm_index *h, uint32_t key, uint64_t value);
+int tm_debug_get(tm_index *h, uint32_t key, uint64_t *value);
 
 /* Last error text of the calling thread (h is ignored; kept for the ABI). */
 const char *tm_last_error(tm_index *h);

@@ -52,20 +52,28 @@ match_routes(Topic) ->
         undefined ->
             emqx_router_gpu:match_routes(Topic);
         Pid ->
-            Ref = erlang:monitor(process, Pid),
-            Pid ! {match, self(), Ref, Topic},
+            %% The reply goes to a process alias tied to the monitor
+            %% (reply_demonitor: the reply deactivates both), so a reply that
+            %% arrives after the timeout below -- the alias deactivated by the
+            %% demonitor -- is dropped by the runtime instead of landing in the
+            %% publisher's (connection process's) mailbox (VERDICT r3).
+            Alias = erlang:monitor(process, Pid, [{alias, reply_demonitor}]),
+            Pid ! {match, Alias, Topic},
             receive
-                {Ref, {error, Reason}} ->
-                    erlang:demonitor(Ref, [flush]),
+                {Alias, {error, Reason}} ->
                     error(Reason);
-                {Ref, Routes} ->
-                    erlang:demonitor(Ref, [flush]),
+                {Alias, Routes} ->
                     Routes;
-                {'DOWN', Ref, process, _, _} ->
+                {'DOWN', Alias, process, _, _} ->
                     %% the batcher died with our request: ask the router directly
                     emqx_router_gpu:match_routes(Topic)
             after ?CALL_TIMEOUT ->
-                erlang:demonitor(Ref, [flush]),
+                erlang:demonitor(Alias, [flush]),
+                %% a reply sent before the alias went inactive may already be queued
+                receive
+                    {Alias, _} -> ok
+                after 0 -> ok
+                end,
                 emqx_router_gpu:match_routes(Topic)
             end
     end.
@@ -79,11 +87,18 @@ handle_call(_Req, _From, St) ->
 handle_cast(_Msg, St) ->
     {noreply, St}.
 
-handle_info({match, From, Ref, Topic}, St = #st{batches = B}) ->
+handle_info({match, Alias, Topic}, St = #st{batches = B}) ->
     %% this request plus every one already queued behind it
-    Reqs = [{From, Ref, Topic} | drain(?MAX_BATCH - 1, [])],
-    Results = emqx_router_gpu:match_routes_batch([T || {_, _, T} <- Reqs]),
-    lists:foreach(fun({{F, R, _}, Res}) -> F ! {R, Res} end, lists:zip(Reqs, Results)),
+    Reqs = [{Alias, Topic} | drain(?MAX_BATCH - 1, [])],
+    Results =
+        try
+            emqx_router_gpu:match_routes_batch([T || {_, T} <- Reqs])
+        catch
+            %% a batch the device failed ({error, device}): every publisher of
+            %% the batch gets the error, none a badarg
+            error:{tmatch, {error, Reason}} -> [{error, Reason} || _ <- Reqs]
+        end,
+    lists:foreach(fun({{A, _}, Res}) -> A ! {A, Res} end, lists:zip(Reqs, Results)),
     {noreply, St#st{batches = B + 1}};
 handle_info(_Info, St) ->
     {noreply, St}.
@@ -92,7 +107,7 @@ drain(0, Acc) ->
     lists:reverse(Acc);
 drain(K, Acc) ->
     receive
-        {match, From, Ref, Topic} -> drain(K - 1, [{From, Ref, Topic} | Acc])
+        {match, Alias, Topic} -> drain(K - 1, [{Alias, Topic} | Acc])
     after 0 ->
         lists:reverse(Acc)
     end.

@@ -25,15 +25,22 @@
 -include_lib("emqx/include/emqx.hrl").
 -include_lib("emqx/include/emqx_router.hrl").
 
+-behaviour(gen_server).
+
 -export([attach/1, detach/0, mirror/0]).
 -export([match_routes/1, match_routes_batch/1]).
+-export([start_link/1, init/1, handle_call/3, handle_cast/2, handle_info/2, terminate/2]).
 
 -define(PT_KEY, {?MODULE, mirror}).
 -define(BOOT_BATCH, 100000).
+-define(MAX_EVENTS, 10000).
 
 %% Boot: mirror the existing ?ROUTE_TAB_FILTERS (emqx_router.erl:148-160) on the
 %% given devices and publish the handle.  Called from emqx_router_sup after
-%% emqx_router:create_tables/0 (emqx_router_sup.erl:25-33).
+%% emqx_router:create_tables/0 (emqx_router_sup.erl:25-33), as the child
+%% start_link(Devices): the process subscribes to the table's events FIRST,
+%% then loads the table, so no write is lost between the two (a write seen
+%% both ways is an idempotent delta).
 -spec attach([integer()]) -> ok.
 attach(Devices) ->
     G = emqx_topic_index_gpu:attach(?ROUTE_TAB_FILTERS, ?BOOT_BATCH, Devices),
@@ -44,6 +51,45 @@ attach(Devices) ->
 detach() ->
     _ = persistent_term:erase(?PT_KEY),
     ok.
+
+%% The mirror's event process: every write to ?ROUTE_TAB_FILTERS on this node
+%% -- local router writes, mria-replicated ones and the match_delete of a
+%% node-down cleanup_routes/1 (emqx_router.erl:535-550) alike -- reaches the
+%% device as table events, drained from the mailbox and shipped as one delta
+%% batch per drain (the router never writes the mria-managed table behind
+%% mria's back; VERDICT r3).
+start_link(Devices) ->
+    gen_server:start_link({local, ?MODULE}, ?MODULE, Devices, []).
+
+init(Devices) ->
+    {ok, _} = mnesia:subscribe({table, ?ROUTE_TAB_FILTERS, detailed}),
+    ok = attach(Devices),
+    {ok, mirror()}.
+
+handle_call(_Req, _From, G) ->
+    {reply, ignored, G}.
+
+handle_cast(_Msg, G) ->
+    {noreply, G}.
+
+handle_info({mnesia_table_event, E}, G) ->
+    ok = emqx_topic_index_gpu:table_events([E | drain_events(?MAX_EVENTS - 1, [])], G),
+    {noreply, G};
+handle_info(_Info, G) ->
+    {noreply, G}.
+
+terminate(_Reason, _G) ->
+    _ = mnesia:unsubscribe({table, ?ROUTE_TAB_FILTERS, detailed}),
+    detach().
+
+drain_events(0, Acc) ->
+    lists:reverse(Acc);
+drain_events(K, Acc) ->
+    receive
+        {mnesia_table_event, E} -> drain_events(K - 1, [E | Acc])
+    after 0 ->
+        lists:reverse(Acc)
+    end.
 
 -spec mirror() -> emqx_topic_index_gpu:gtab() | undefined.
 mirror() ->

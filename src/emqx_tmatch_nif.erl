@@ -10,7 +10,8 @@
 %% Op: 1 insert, 0 delete.  Kind: 0 binary key, 1 word list, 2 the word list [].
 -type delta() :: {0 | 1, binary(), u32(), 0 | 1 | 2}.
 -type order() :: traversal | sorted | unique.
--export_type([ref/0, u32/0, delta/0, order/0]).
+-type ticket() :: reference().
+-export_type([ref/0, u32/0, delta/0, order/0, ticket/0]).
 
 init() ->
     Priv =
@@ -29,17 +30,20 @@ new(_Device) -> erlang:nif_error(nif_not_loaded).
 -spec apply(ref(), [delta()]) -> {ok, non_neg_integer()} | {error, integer()}.
 apply(_Ref, _Deltas) -> erlang:nif_error(nif_not_loaded).
 
--spec match_batch(ref(), [binary()], order()) -> [[u32()] | badarg | system_limit] | {error, integer()}.
+%% {error, device}: the GPU failed the batch (never a per-topic badarg).
+-spec match_batch(ref(), [binary()], order()) -> [[u32()] | badarg | system_limit] | {error, device | integer()}.
 match_batch(_Ref, _Topics, _Order) -> erlang:nif_error(nif_not_loaded).
 
 -spec first_batch(ref(), [binary()]) -> [{ok, u32()} | false | badarg | system_limit] | {error, integer()}.
 first_batch(_Ref, _Topics) -> erlang:nif_error(nif_not_loaded).
 
-%% A reader registers before its batch and unregisters after decoding it.
--spec read_begin(ref()) -> {ok, non_neg_integer()}.
+%% A reader registers before its batch and unregisters after decoding it.  The
+%% ticket is a resource: a reader killed before read_end ends its read when
+%% the ticket is garbage collected, so the safe epoch never stays pinned.
+-spec read_begin(ref()) -> {ok, ticket()}.
 read_begin(_Ref) -> erlang:nif_error(nif_not_loaded).
 
--spec read_end(ref(), non_neg_integer()) -> ok.
+-spec read_end(ref(), ticket()) -> ok.
 read_end(_Ref, _Ticket) -> erlang:nif_error(nif_not_loaded).
 
 %% {Current, Safe}: a kid released at epoch E may be reused once Safe >= E.

@@ -35,7 +35,7 @@
 -export([insert/4, delete/3, apply_batch/2]).
 -export([match/2, matches/3, matches_batch/3, matches_filter/3]).
 -export([make_key/2, get_id/1, get_topic/1, get_record/2]).
--export([table_event/2, cleanup/2, stats/1]).
+-export([table_event/2, table_events/2, cleanup/2, stats/1]).
 
 -record(gtab, {tab, kids, quar, free, ref}).
 -type gtab() :: #gtab{}.
@@ -83,7 +83,7 @@ attach(Tab, BatchSize, Devices) ->
     G = mirror(Tab, Devices),
     ets:safe_fixtable(Tab, true),
     try
-        boot(G, ets:first(Tab), BatchSize, ?NOACC)
+        boot(G, ets:first(Tab), key_pos(Tab), BatchSize, 0, ?NOACC)
     after
         ets:safe_fixtable(Tab, false)
     end,
@@ -100,13 +100,22 @@ mirror(Tab, Devices) ->
 %% Deltas accumulate as {DeviceDeltas, ReleasedKids}, both prepended.
 -define(NOACC, {[], []}).
 
-boot(G, '$end_of_table', _N, Acc) ->
+%% Rows are walked in key order; every BatchSize keys ship as one device call.
+%% The batch is counted as it fills (K): a length/1 guard per key made each
+%% batch quadratic (VERDICT r3: 5e9 list steps per 100k-key batch).  The
+%% key is the row's key position (the table's keypos: 2 for the router's
+%% #routeidx{entry = Key} rows, emqx_router.erl:105-108), which is also
+%% what ets:first/next walk.
+boot(G, '$end_of_table', _Pos, _N, _K, Acc) ->
     flush(G, Acc);
-boot(G, Key, N, Acc = {D, _}) when length(D) >= N ->
+boot(G, Key, Pos, N, K, Acc) when K >= N ->
     ok = flush(G, Acc),
-    boot(G, Key, N, ?NOACC);
-boot(G, Key, N, Acc) ->
-    boot(G, ets:next(G#gtab.tab, Key), N, intern_delta(G, Key, Acc)).
+    boot(G, Key, Pos, N, 0, ?NOACC);
+boot(G, Key, Pos, N, K, Acc) ->
+    boot(G, ets:next(G#gtab.tab, Key), Pos, N, K + 1, intern_delta(G, Key, Acc)).
+
+key_pos(Tab) ->
+    ets:info(Tab, keypos).
 
 %%--------------------------------------------------------------------
 %% Writes
@@ -148,27 +157,43 @@ apply_batch(Ops, G = #gtab{tab = Tab}) ->
     flush(G, Deltas).
 
 %% Replicated writes reach a core or replicant node as mnesia table events,
-%% bypassing emqx_router (SURVEY.md 3.2); the router helper subscribes with
-%% mnesia:subscribe({table, ?ROUTE_TAB_FILTERS, detailed}) and hands each
-%% event here (after mnesia has applied it to the ETS table itself).
+%% bypassing emqx_router (SURVEY.md 3.2): emqx_router_gpu's event process
+%% subscribes with mnesia:subscribe({table, ?ROUTE_TAB_FILTERS, detailed}) and
+%% hands the events here (after mnesia has applied them to the ETS table
+%% itself) -- including the deletes of a node-down cleanup, which mria's
+%% match_delete makes (emqx_router.erl:535-550): the mirror never writes the
+%% mria-managed table itself.  Records are keyed at position 2 (#routeidx{}).
 -spec table_event(tuple(), gtab()) -> ok.
-table_event({write, _Tab, Rec, _Old, _Tid}, G) ->
-    flush(G, intern_delta(G, element(2, Rec), ?NOACC));
-table_event({delete, _Tab, {_, Key}, _Old, _Tid}, G) ->
-    flush(G, release_delta(G, Key, ?NOACC));
-table_event({delete_object, _Tab, Rec, _Old, _Tid}, G) ->
-    flush(G, release_delta(G, element(2, Rec), ?NOACC));
-table_event(_, _G) ->
-    ok.
+table_event(Event, G) ->
+    table_events([Event], G).
 
-%% Node-down cleanup (emqx_router.erl:535-578, emqx_router_helper.erl:147-162):
-%% every key whose ID satisfies Pred is deleted, and the whole set of deletes
-%% ships as one device batch instead of one write per route.
+%% A run of events (everything the event process found in its mailbox) as ONE
+%% device delta call, in order.
+-spec table_events([tuple()], gtab()) -> ok.
+table_events(Events, G) ->
+    flush(G, lists:foldl(fun(E, Acc) -> event_delta(E, G, Acc) end, ?NOACC, Events)).
+
+event_delta({write, _Tab, Rec, _Old, _Tid}, G, Acc) ->
+    intern_delta(G, element(2, Rec), Acc);
+event_delta({delete, _Tab, {_, Key}, _Old, _Tid}, G, Acc) ->
+    release_delta(G, Key, Acc);
+event_delta({delete_object, _Tab, Rec, _Old, _Tid}, G, Acc) ->
+    release_delta(G, element(2, Rec), Acc);
+event_delta(_, _G, Acc) ->
+    Acc.
+
+%% Node-down cleanup of an index table this mirror's owner writes (the
+%% standalone emqx_topic_index tables): every key whose ID satisfies Pred is
+%% deleted from ETS and the deletes ship as one device batch.  The key is taken
+%% at the table's keypos.  (The router's mria-managed table is cleaned by
+%% emqx_router:cleanup_routes/1 itself; its deletes reach the mirror as table
+%% events, table_events/2.)
 -spec cleanup(fun((_ID) -> boolean()), gtab()) -> ok.
 cleanup(Pred, G = #gtab{tab = Tab}) ->
+    Pos = key_pos(Tab),
     Doomed = ets:foldl(
         fun(Row, Acc) ->
-            Key = element(1, Row),
+            Key = element(Pos, Row),
             case Pred(get_id(Key)) of
                 true -> [Key | Acc];
                 false -> Acc
@@ -287,6 +312,8 @@ flush(#gtab{ref = Ref, quar = Quar}, {Deltas, Released}) ->
 %% emqx_trie_search.erl:157-158).  If F's keys vanished meanwhile, the full
 %% match decides.
 match(Topic, G = #gtab{tab = Tab, ref = Ref, kids = Kids}) ->
+    %% the ticket is a NIF resource: if this process dies before read_end,
+    %% its garbage collection ends the read (the safe epoch moves on)
     {ok, Ticket} = emqx_tmatch_nif:read_begin(Ref),
     try emqx_tmatch_nif:first_batch(Ref, [Topic]) of
         [{ok, V}] ->
@@ -315,16 +342,25 @@ first_of(Topic, G) ->
         [[]] -> false
     end.
 
-%% matches/3 (emqx_topic_index.erl:76-78).
--spec matches(emqx_types:topic(), gtab(), emqx_trie_search:opts()) -> [emqx_trie_search:key(_)].
+%% matches/3 (emqx_topic_index.erl:76-78).  With return_first the reference's
+%% search throws {first, Key} at the first hit and, with none, returns its
+%% accumulator, the atom `first` (emqx_trie_search.erl:201-211, 350-356):
+%% the same here.
+-spec matches(emqx_types:topic(), gtab(), emqx_trie_search:opts()) -> [emqx_trie_search:key(_)] | first.
 matches(Topic, G, Opts) ->
-    [Res] = matches_batch([Topic], G, Opts),
-    Res.
+    case matches_batch([Topic], G, Opts) of
+        [{first, K}] -> throw({first, K});
+        [Res] -> Res
+    end.
 
 %% matches/3 over a broker micro-batch (emqx_broker.erl:293-298) in one device
 %% call.  A topic with a '+'/'#' level fails only its own slot: with the
 %% option return_errors the slot holds {error, badarg}; without it the call
-%% raises badarg as the reference's single-topic call does (:374-375).
+%% raises badarg as the reference's single-topic call does (:374-375).  A
+%% batch the device failed ({error, device} from the NIF: its look-back failed
+%% twice) raises {tmatch, {error, device}} for the whole call -- never badarg.
+%% With return_first a slot holds {first, Key} (the first key in traversal
+%% order) or `first` (no match), the two outcomes of the reference's call.
 -spec matches_batch([emqx_types:topic()], gtab(), list()) -> [[emqx_trie_search:key(_)] | {error, atom()}].
 matches_batch(Topics, #gtab{ref = Ref, kids = Kids}, Opts) ->
     {ok, Ticket} = emqx_tmatch_nif:read_begin(Ref),
@@ -347,11 +383,16 @@ finish(Row, Kids, Opts, _) ->
         true ->
             Keys;
         false ->
-            case proplists:get_bool(unique, Opts) of
+            %% the accumulator the reference picks (emqx_trie_search.erl:201-211):
+            %% return_first before unique before a plain list
+            case {proplists:get_bool(return_first, Opts), proplists:get_bool(unique, Opts)} of
+                %% match_add/2 with `first` throws the first key (:355-356)
+                {true, _} when Keys =:= [] -> first;
+                {true, _} -> {first, hd(Keys)};
                 %% match_add/2 on a map: a later key of the same ID wins (:350-352)
-                true -> maps:values(lists:foldl(fun(K = {_, ID}, M) -> M#{ID => K} end, #{}, Keys));
+                {false, true} -> maps:values(lists:foldl(fun(K = {_, ID}, M) -> M#{ID => K} end, #{}, Keys));
                 %% match_add/2 on a list prepends (:353-354)
-                false -> lists:reverse(Keys)
+                {false, false} -> lists:reverse(Keys)
             end
     end.
 

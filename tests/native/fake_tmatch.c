@@ -3,7 +3,10 @@
  * (include/tmatch.h) with no device, so c_src/tmatch_nif_core.c can be
  * exercised on the CPU (tests/test_nif_core_cpu.py).  Topic i "matches" one
  * value per byte: values 1000 * i + k; a topic whose first byte is '+' is
- * badarg.  Counts host allocations and batch calls.
+ * badarg; one whose first byte is '!' gets err flag 4 (a batch the device
+ * failed, as a library that did not retry would leave it) and one whose first
+ * byte is '~' makes the call return TM_EDEVICE.  Counts host allocations and
+ * batch calls.
  */
 #include <stdlib.h>
 #include <string.h>
@@ -33,9 +36,11 @@ int tm_match_batch_ex(tm_index *h, uint64_t n, const uint8_t *tb, const uint64_t
     (void)h;
     n_match++;
     hit[0] = 0;
+    for (uint64_t i = 0; i < n; i++)
+        if (to[i + 1] > to[i] && tb[to[i]] == '~') return TM_EDEVICE;
     for (uint64_t i = 0; i < n; i++) {
         const uint64_t len = to[i + 1] - to[i];
-        err[i] = len && tb[to[i]] == '+';
+        err[i] = len && tb[to[i]] == '+' ? 1 : len && tb[to[i]] == '!' ? 4 : 0;
         const uint64_t c = err[i] ? 0 : len;
         for (uint64_t k = 0; k < c; k++) {
             const uint64_t pos = hit[i] + k;
@@ -61,7 +66,35 @@ int tm_first_batch(tm_index *h, uint64_t n, const uint8_t *tb, const uint64_t *t
     return TM_OK;
 }
 
-long fake_count(int what) { return what == 0 ? n_alloc : what == 1 ? n_free : what == 2 ? n_match : n_first; }
+static long n_readers, n_read_end;
+static uint64_t next_ticket = 1;
+
+int tm_read_begin(tm_index *h, uint64_t *ticket) {
+    (void)h;
+    *ticket = next_ticket++;
+    n_readers++;
+    return TM_OK;
+}
+
+int tm_read_end(tm_index *h, uint64_t ticket) {
+    (void)h; (void)ticket;
+    n_readers--;
+    n_read_end++;
+    return TM_OK;
+}
+
+long fake_count(int what) {
+    return what == 0 ? n_alloc : what == 1 ? n_free : what == 2 ? n_match : what == 3 ? n_first
+         : what == 4 ? n_readers : n_read_end;
+}
+
+/* a ticket on the heap, as the NIF's resource holds one */
+tmn_ticket *fake_ticket_new(void) {
+    tmn_ticket *t = malloc(sizeof *t);
+    if (t && tmn_ticket_begin(t, (tm_index *)0x1) != TM_OK) { free(t); t = NULL; }
+    return t;
+}
+void fake_ticket_free(tmn_ticket *t) { tmn_ticket_destroy(t); free(t); }
 
 /* pool / set handles for ctypes */
 tmn_pool *fake_pool_new(void) {

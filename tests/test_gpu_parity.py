@@ -1893,3 +1893,204 @@ def test_replicas_share_one_host_image(torch_dev):
     print(f"host RSS growth: 1 replica {one / 2**20:.0f} MiB, 2 replicas {two / 2**20:.0f} MiB "
           f"(device {db1 / 2**20:.0f} MiB per replica)")
     assert db1 == db2 and two <= 1.2 * one + (32 << 20)
+
+
+# ------------------------------------------ one-pass large batches (round 4)
+
+def _paths(ix):
+    """match launches so far per kernel path: (two-phase, k_walk_small, k_walk_one)"""
+    return tuple(ix.debug_get(k) for k in (_native.TM_DEBUG_PATH_PHASES, _native.TM_DEBUG_PATH_SMALL,
+                                           _native.TM_DEBUG_PATH_ONE))
+
+
+def _shallow_case(r, nt=700):
+    """Filters of at most 6 levels (trie depth <= 6, binary keys <= 6 levels:
+    k_walk_one's index condition, one_pass_ok), topics of 1-14 levels (the
+    ones deeper than FAST_L = 8 take k_walk_one's second, lite walk), dense
+    wildcard families over some prefixes (topics with more than RCAP = 8 value
+    ranges: re-walked), filters with several IDs (multi-value runs)."""
+    def lvl():
+        c = r.random()
+        if c < 0.1:
+            return b""
+        if c < 0.15:
+            return b"$" + r.choice([b"SYS", b"a"])
+        if c < 0.2:
+            return r.choice([b"b+", b"c#", b"a-very-long-level-word-over-16-bytes"])
+        return ("%X" % r.randint(1, 12)).encode()
+    topics = [b"/".join(lvl() for _ in range(r.choice([1, 2, 3, 4, 5, 6, 6, 9, 12, 14]))) for _ in range(nt)]
+    topics += [b"a/+/b", b"#", b"", b"/", b"$SYS", b"1/2/3/4/5/6/7/8/9/10/+/12", b"/" * 65536]   # badarg deep, > 65536 levels
+    filters, vals = [], []
+    for _ in range(900):
+        ws = r.choice(topics[:nt]).split(b"/")[:6]
+        out = []
+        for k, w in enumerate(ws):
+            p = r.choices(["w", "+", "#"], [5, 2, 1])[0]
+            if p == "#" or (k == len(ws) - 1 and r.random() < 0.2 and k < 5):
+                out.append(b"#")
+                break
+            out.append(b"+" if p == "+" else w)
+        filters.append(b"/".join(out))
+        vals.append(len(vals))
+    for t in r.sample(topics[:nt], 12):   # every '+' / '#' variant of a prefix: > RCAP ranges per topic
+        ws = t.split(b"/")[:4]
+        for m in range(1 << len(ws)):
+            f = [b"+" if (m >> k) & 1 else w for k, w in enumerate(ws)]
+            for g in (f, f[:-1] + [b"#"], f + [b"#"]):
+                if len(g) <= 6:
+                    filters.append(b"/".join(g))
+                    vals.append(len(vals))
+    for f in r.sample(filters, 60):   # several IDs on one filter: multi-value runs
+        for _ in range(r.randint(2, 40)):
+            filters.append(f)
+            vals.append(len(vals))
+    return filters, vals, topics
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_one_pass_vs_oracle_and_two_phase(torch_dev, seed):
+    """Batches above 65536 topics on a shallow index run in ONE launch
+    (k_walk_one: walk, look-back scan and emit): exact CSR
+    against the oracle, and bit-identical to the two-phase path (walk, tails,
+    scan, emit) forced on the same batch -- topics deeper than the main store,
+    badarg beyond it, more than 65536 levels, more than RCAP ranges,
+    multi-value runs; after deletes and re-inserts too; host and device API."""
+    torch = torch_dev
+    r = random.Random(0x454D5158 + 400 + seed)
+    filters, vals, topics = _shallow_case(r)
+    flags = np.array([r.random() < 0.2 for _ in filters], np.uint8)
+    fs = items_of(filters, vals)
+    ix, o = gpu_index(fs, flags), oracle_of(fs, flags)
+    ix.debug_set(_native.TM_DEBUG_PHASES, 0)
+    big = items_of([topics[i % len(topics)] for i in r.sample(range(70_000 * 2), 70_000)])
+    p0 = _paths(ix)
+    hit, vals1 = assert_same(ix, o, big)
+    p1 = _paths(ix)
+    assert p1[2] > p0[2] and p1[0] == p0[0], "the batch did not take k_walk_one"   # (> 1 launch: capacity reruns)
+    ix.debug_set(_native.TM_DEBUG_PHASES, 1)
+    hit2, vals2, err2 = ix.match_batch(big.blob, big.offs)
+    ix.debug_set(_native.TM_DEBUG_PHASES, 0)
+    assert _paths(ix)[0] > p1[0]
+    assert np.array_equal(hit, hit2) and np.array_equal(vals1, vals2)
+    assert np.diff(hit.astype(np.int64)).max() > 8 * 2        # some topic beyond RCAP ranges
+    # device API on a torch stream
+    d_blob, d_offs = torch.from_numpy(big.blob).cuda(), torch.from_numpy(big.offs.view(np.int64)).cuda()
+    d_hit = torch.zeros(len(big) + 1, dtype=torch.int64, device="cuda")
+    d_err = torch.zeros(len(big), dtype=torch.uint8, device="cuda")
+    d_out = torch.zeros(int(hit[-1]) + 1, dtype=torch.int32, device="cuda")
+    ix.match_batch_dev(len(big), d_blob.data_ptr(), d_offs.data_ptr(), d_hit.data_ptr(), d_out.data_ptr(),
+                       int(hit[-1]) + 1, d_err.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert np.array_equal(d_hit.cpu().numpy().view(np.uint64), hit)
+    assert np.array_equal(d_out.cpu().numpy().view(np.uint32)[: int(hit[-1])], vals1)
+    # deletes and re-inserts as deltas, then the one-pass batch again
+    dele = sorted(r.sample(range(len(filters)), len(filters) // 4))
+    d = items_of([filters[i] for i in dele], [vals[i] for i in dele])
+    ix.apply(np.zeros(len(dele), np.uint8), d.blob, d.offs, d.vals, flags[dele])
+    o.apply(np.zeros(len(dele), np.uint8), d.blob, d.offs, d.vals, flags[dele])
+    assert_same(ix, o, big)
+    back = dele[::2]
+    d2 = items_of([filters[i] for i in back], [vals[i] for i in back])
+    ix.apply(np.ones(len(back), np.uint8), d2.blob, d2.offs, d2.vals, flags[back])
+    o.apply(np.ones(len(back), np.uint8), d2.blob, d2.offs, d2.vals, flags[back])
+    p2 = _paths(ix)
+    assert_same(ix, o, big)
+    assert _paths(ix)[2] > p2[2] and _paths(ix)[0] == p2[0]
+
+
+def test_one_pass_c3deep_and_index_gates(torch_dev):
+    """C3deep above 65536 topics (10 % of the topics 33-64 levels) in one
+    launch; an index a topic could need more than FAST_L levels of (a binary
+    key of 40 levels) or with a '#'-not-last key takes the two-phase path,
+    exact either way."""
+    fs = wl.filters(3, 200_000)
+    ts = wl.topics(30, 200_000, 90_000)
+    ix, o = gpu_index(fs), oracle_of(fs)
+    ix.debug_set(_native.TM_DEBUG_PHASES, 0)
+    p0 = _paths(ix)
+    assert_same(ix, o, ts)
+    assert _paths(ix)[2] > p0[2] and _paths(ix)[0] == p0[0]
+    for extra in ([b"/".join([b"z"] * 40)], [b"a/#/b"]):   # deep binary key / '#'-not-last key
+        e = items_of(extra, [1_000_000])
+        ix.apply(np.ones(1, np.uint8), e.blob, e.offs, e.vals)
+        o.apply(np.ones(1, np.uint8), e.blob, e.offs, e.vals)
+        p0 = _paths(ix)
+        assert_same(ix, o, ts)
+        assert _paths(ix)[0] > p0[0] and _paths(ix)[2] == p0[2], "expected the two-phase path"
+        ix.apply(np.zeros(1, np.uint8), e.blob, e.offs, e.vals)
+        o.apply(np.zeros(1, np.uint8), e.blob, e.offs, e.vals)
+    p0 = _paths(ix)
+    assert_same(ix, o, ts)
+    assert _paths(ix)[2] > p0[2] and _paths(ix)[0] == p0[0]
+
+
+# ------------------------------------- device failures are not badarg (round 4)
+
+@pytest.mark.parametrize("nt", [5_000, 100_000])   # k_walk_small / k_walk_one
+def test_lookback_failure_is_retried_then_a_device_error(torch_dev, nt):
+    """A one-launch batch whose look-back wait expires (forced: block 3 acts
+    as if its wait expired, TM_DEBUG_LB_FAIL_BLOCK) flags err 4 from that block
+    on (LB_FAIL propagates: no later block takes a partial prefix), the host
+    API runs it again once -- exact results -- and a second failure is a
+    device error for the whole call: TM_EDEVICE / DeviceError, never BadArg
+    (the reference raises badarg only for a '+'/'#' level,
+    emqx_trie_search.erl:374-375)."""
+    torch = torch_dev
+    fs = wl.filters(3, 50_000)
+    ts = wl.topics(3, 50_000, nt)
+    ix, o = gpu_index(fs), oracle_of(fs)
+    ix.debug_set(_native.TM_DEBUG_PHASES, 0)   # (large batches: k_walk_one)
+    assert_same(ix, o, ts)
+    f0, r0 = ix.debug_get(_native.TM_DEBUG_FAILED_BATCHES), ix.debug_get(_native.TM_DEBUG_RETRIED_BATCHES)
+    assert f0 == 0 and r0 == 0                       # a normal run never fails
+    ix.debug_set(_native.TM_DEBUG_LB_FAIL_BLOCK, 3)
+    ix.debug_set(_native.TM_DEBUG_LB_LAUNCHES, 1)    # the first launch fails, the retry succeeds
+    assert_same(ix, o, ts)
+    assert ix.debug_get(_native.TM_DEBUG_FAILED_BATCHES) == 1
+    assert ix.debug_get(_native.TM_DEBUG_RETRIED_BATCHES) == 1
+    ix.debug_set(_native.TM_DEBUG_LB_LAUNCHES, 2)    # both fail: a device error
+    with pytest.raises(_native.DeviceError):
+        ix.match_batch(ts.blob, ts.offs)
+    assert ix.debug_get(_native.TM_DEBUG_FAILED_BATCHES) == 3
+    # the topic_index mirror raises DeviceError (not BadArg) for a valid topic
+    tab = ti.Tab(index=ix)
+    tab._keys = [None] * (int(fs.vals.max()) + 1)
+    ix.debug_set(_native.TM_DEBUG_LB_LAUNCHES, 2)
+    with pytest.raises(_native.DeviceError):
+        ti.matches_batch([ts.item(i) for i in range(nt)], tab)
+    # device API (asynchronous: no retry): err 4 from the failed block on, 0 before
+    ix.debug_set(_native.TM_DEBUG_LB_LAUNCHES, 1)
+    d_blob, d_offs = torch.from_numpy(ts.blob).cuda(), torch.from_numpy(ts.offs.view(np.int64)).cuda()
+    d_hit = torch.zeros(nt + 1, dtype=torch.int64, device="cuda")
+    d_err = torch.zeros(nt, dtype=torch.uint8, device="cuda")
+    d_out = torch.zeros(16 * nt, dtype=torch.int32, device="cuda")
+    ix.match_batch_dev(nt, d_blob.data_ptr(), d_offs.data_ptr(), d_hit.data_ptr(), d_out.data_ptr(), 16 * nt,
+                       d_err.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    err = d_err.cpu().numpy()
+    per_block = 16 if nt <= 65536 else 64
+    first = 3 * per_block
+    assert not err[:first].any() and (err[first:] == 4).all()
+    # the hook is spent: the next batches are exact again, with no failure
+    assert_same(ix, o, ts)
+    assert ix.debug_get(_native.TM_DEBUG_FAILED_BATCHES) == 5
+
+
+def test_lookback_without_waiting_is_exact_or_a_device_error(torch_dev):
+    """With no wait at all (TM_DEBUG_LB_SPINS 0: a block fails whenever a
+    predecessor has not published yet), every batch either matches exactly or
+    fails as a device error -- never a wrong result, never BadArg."""
+    fs = wl.filters(3, 50_000)
+    ix, o = gpu_index(fs), oracle_of(fs)
+    ix.debug_set(_native.TM_DEBUG_PHASES, 0)
+    for nt in (30_000, 200_000):
+        ts = wl.topics(3, 50_000, nt)
+        ix.debug_set(_native.TM_DEBUG_LB_SPINS, 0)
+        ix.debug_set(_native.TM_DEBUG_LB_LAUNCHES, 2)
+        try:
+            assert_same(ix, o, ts)
+        except _native.DeviceError:
+            pass
+        ix.debug_set(_native.TM_DEBUG_LB_LAUNCHES, 0)
+        ix.debug_set(_native.TM_DEBUG_LB_SPINS, 1 << 22)
+        assert_same(ix, o, ts)

@@ -9,7 +9,7 @@ from pathlib import Path
 import pytest
 
 ROOT = Path(__file__).resolve().parent.parent
-TM_OK, TM_ECAP = 0, -4
+TM_OK, TM_EDEVICE, TM_ECAP = 0, -3, -4
 TRAVERSAL, SORTED, UNIQUE = 0, 1, 2
 
 
@@ -40,6 +40,9 @@ def core(tmp_path_factory):
     lib.fake_set_reruns.restype = C.c_uint64
     lib.fake_set_vals.argtypes = [vp]
     lib.fake_set_vals.restype = C.POINTER(C.c_uint32)
+    lib.fake_ticket_new.restype = vp
+    lib.fake_ticket_free.argtypes = [vp]
+    lib.tmn_ticket_end.argtypes = [vp]
     return lib
 
 
@@ -121,3 +124,44 @@ def test_pool_reuses_sets_and_bounds_itself(core):
     assert core.fake_pool_size(pool) == 64   # TMN_POOL_MAX; the rest freed
     core.fake_pool_free(pool)
     assert core.fake_count(1) >= f0
+
+
+def test_device_failure_is_never_a_badarg_row(core):
+    """Err flag 4 (a batch the device failed) and TM_EDEVICE fail the whole
+    call as a device error -- the NIF returns {error, device} -- and never
+    become a per-topic badarg: the reference raises badarg only for a '+'/'#'
+    level (emqx_trie_search.erl:374-375).  ADVICE r3 (tmatch_nif_core.c
+    passed err 4 through as a row the NIF mapped to badarg)."""
+    pool = core.fake_pool_new()
+    s = core.tmn_take(pool)
+    for topics in ([b"ab", b"!x", b"cd"], [b"ab", b"~x"]):
+        assert pack(core, s, topics) == TM_OK
+        assert core.tmn_match(s, H, len(topics), TRAVERSAL) == TM_EDEVICE
+    # a row left with flag 4 (never after a TM_OK call) reads as the device code, not badarg (1)
+    assert pack(core, s, [b"!x"]) == TM_OK
+    core.tmn_match(s, H, 1, TRAVERSAL)
+    b, e = C.c_uint64(), C.c_uint64()
+    assert core.tmn_row(s, 1, TRAVERSAL, 0, C.byref(b), C.byref(e)) == 4
+    # a well-formed batch after it is unaffected
+    assert pack(core, s, [b"ab", b"+x"]) == TM_OK
+    assert core.tmn_match(s, H, 2, TRAVERSAL) == TM_OK
+    assert rows(core, s, 2, TRAVERSAL) == [[0, 1], 1]
+    core.tmn_give(pool, s)
+    core.fake_pool_free(pool)
+
+
+def test_reader_ticket_ends_once_even_if_never_ended(core):
+    """A reader's ticket is ended exactly once: read_end twice ends it once,
+    and a ticket whose reader died before read_end (the NIF resource's term
+    collected: its destructor) ends the read then, so the library's safe
+    epoch is never pinned by a killed reader."""
+    r0, e0 = core.fake_count(4), core.fake_count(5)
+    a = core.fake_ticket_new()
+    b = core.fake_ticket_new()
+    assert core.fake_count(4) == r0 + 2
+    core.tmn_ticket_end(a)
+    core.tmn_ticket_end(a)                      # idempotent
+    assert core.fake_count(4) == r0 + 1 and core.fake_count(5) == e0 + 1
+    core.fake_ticket_free(a)                    # already ended: nothing more
+    core.fake_ticket_free(b)                    # never ended: the destructor ends it
+    assert core.fake_count(4) == r0 and core.fake_count(5) == e0 + 2

@@ -20,7 +20,8 @@ request, so the value is taken as is (no x2).
 It also counts Infinity-Cache (MALL) hits, so it is an upper bound on HBM.
 
 The bench run's kernel trace is split by phase: its last 2 x rotate
-full-grid k_walk_fast launches are the isolated pass bench.py times for
+full-grid launches of the main kernel (k_walk_one for a one-launch batch,
+else k_walk_fast) are the isolated pass bench.py times for
 roofline.kernel_avg_ms (one stream, back to back), the launches before them
 ran overlapped on three streams.  pmc_<config>.json is stamped with the
 kernel-source hash (emqx_amd.build.source_hash) and the workload shape;
@@ -85,10 +86,24 @@ def pmc_values(prof, grid, last):
     return out
 
 
+MAIN_KERNELS = ("k_walk_one", "k_walk_fast")   # the timed kernel: the one-launch batch, else the two-phase walk
+
+
+def main_kernel(names):
+    for k in MAIN_KERNELS:
+        hit = [n for n in names if k in n]
+        if hit:
+            return hit[0]
+    return None
+
+
 def split_phases(path, grid, n_iso):
-    """k_walk_fast full-grid launches of the bench run in time order -> (timed
-    region + warmup, isolated pass) durations in ns"""
-    rows = [r for r in csv.DictReader(_open(path)) if "k_walk_fast" in r["Kernel_Name"]
+    """full-grid launches of the main kernel (k_walk_one, else k_walk_fast) of
+    the bench run in time order -> (timed region + warmup, isolated pass)
+    durations in ns"""
+    rows = list(csv.DictReader(_open(path)))
+    k = main_kernel({r["Kernel_Name"] for r in rows})
+    rows = [r for r in rows if k and k in r["Kernel_Name"]
             and grid - 255 <= int(r.get("Grid_Size_X") or r.get("Grid_Size") or 0) <= grid]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     d = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows]
@@ -121,7 +136,8 @@ def main(prof, rnd, tag, config, filters, batch, rotate=4, batches=8):
         if sub == "bench":
             timed, iso = split_phases(p, grid, 2 * rotate)
             if iso:
-                lines += [f"k_walk_fast (grid {grid}) by phase of the bench run: the last {len(iso)} launches "
+                lines += [f"{main_kernel(agg and {n for n, _ in agg})} (grid {grid}) by phase of the bench run: "
+                          f"the last {len(iso)} launches "
                           f"(bench.py's isolated pass, one stream, back to back) avg {sum(iso) / len(iso) / 1e3:.2f} us "
                           f"(min {min(iso) / 1e3:.2f}, max {max(iso) / 1e3:.2f}); the {len(timed)} before them "
                           f"(sizing, warmup, timed steps on three streams) avg {sum(timed) / max(len(timed), 1) / 1e3:.2f} us.",
@@ -134,7 +150,8 @@ def main(prof, rnd, tag, config, filters, batch, rotate=4, batches=8):
         if os.path.isfile(st):
             shutil.copy(st, os.path.join("profiles", f"{rnd}_{tag}_{sub}_kernel_stats.csv"))
     pm = pmc_values(prof, grid, batches)
-    walk = [k for k in pm if "k_walk_fast" in k]
+    mk = main_kernel(list(pm))
+    walk = [mk] if mk else []
     res = {"config": config, "filters": filters, "batch": batch, "rotate": rotate, "grid": grid,
            "source_hash": source_hash()}
     if pm:
