@@ -29,6 +29,7 @@ EXPORTS = ("tm_create", "tm_destroy", "tm_apply_deltas", "tm_sync", "tm_match_ba
 TM_DEBUG_LB_SPINS, TM_DEBUG_LB_FAIL_BLOCK, TM_DEBUG_LB_LAUNCHES, TM_DEBUG_PHASES = 1, 2, 3, 4
 TM_DEBUG_FAILED_BATCHES, TM_DEBUG_RETRIED_BATCHES = 5, 6
 TM_DEBUG_PATH_PHASES, TM_DEBUG_PATH_SMALL, TM_DEBUG_PATH_ONE = 7, 8, 9
+TM_DEBUG_LB_DEFER, TM_DEBUG_DEFERRED_BLOCKS = 10, 11
 
 
 class NativeUnavailable(RuntimeError):

@@ -42,20 +42,21 @@ enum { L_MID = 0, L_DEEP = 1, L_OVF_MID = 2, L_OVF_DEEP = 3, L_COUNT = 4 };
 
 // Per-batch device scratch (grow-only, owned by the index).
 // The one-launch kernels' (k_walk_small, k_walk_one) look-back word of a
-// block: launch tag (20 bits), state (LB_AGG: its own hit total; LB_INCL: the
+// block: launch tag (19 bits), state (LB_AGG: its own hit total; LB_INCL: the
 // total of it and every block before it; LB_FAIL: its wait expired, or a
-// predecessor's did -- every later block fails too) and the value (42 bits) in
-// ONE 64-bit word, so a reader gets state and value from one coherent load (no
-// acquire / release: those write back and invalidate the whole L2 of the XCD,
-// under every kernel running there)
-enum : uint32_t { LB_AGG = 1, LB_INCL = 2, LB_FAIL = 3 };
-constexpr uint32_t LB_TAG_BITS = 20, LB_TAG_MASK = (1u << LB_TAG_BITS) - 1;
+// predecessor's did -- every later block fails too; LB_DEF: its own total, the
+// block parked its results and left, k_one_finish emits them) and the value
+// (42 bits) in ONE 64-bit word, so a reader gets state and value from one
+// coherent load (no acquire / release: those write back and invalidate the
+// whole L2 of the XCD, under every kernel running there)
+enum : uint32_t { LB_AGG = 1, LB_INCL = 2, LB_FAIL = 3, LB_DEF = 4 };
+constexpr uint32_t LB_TAG_BITS = 19, LB_TAG_MASK = (1u << LB_TAG_BITS) - 1;
 constexpr uint64_t LB_VAL_MASK = (1ull << 42) - 1;
 __host__ __device__ constexpr uint64_t lb_word(uint32_t tag, uint32_t st, uint64_t v) {
-    return (uint64_t)tag << 44 | (uint64_t)st << 42 | (v & LB_VAL_MASK);
+    return (uint64_t)tag << 45 | (uint64_t)st << 42 | (v & LB_VAL_MASK);
 }
-__host__ __device__ constexpr uint32_t lb_tag(uint64_t w) { return (uint32_t)(w >> 44); }
-__host__ __device__ constexpr uint32_t lb_state(uint64_t w) { return (uint32_t)(w >> 42) & 3u; }
+__host__ __device__ constexpr uint32_t lb_tag(uint64_t w) { return (uint32_t)(w >> 45); }
+__host__ __device__ constexpr uint32_t lb_state(uint64_t w) { return (uint32_t)(w >> 42) & 7u; }
 
 // The look-back's bounded wait.  A block waits only for blocks that took their
 // start ticket before it (so they are running and publish soon); the bound
@@ -63,10 +64,18 @@ __host__ __device__ constexpr uint32_t lb_state(uint64_t w) { return (uint32_t)(
 // leaving a spinning grid behind: past it the block and every later one flag
 // their topics err 4 and raise the workspace's fail word, and the host API
 // runs the batch again (tm_host.cpp retry_or_fail).
-constexpr uint32_t LB_SPINS = 1u << 22;   // polls of one predecessor word (s_sleep(1) apart: ~0.1 s)
+constexpr uint32_t LB_SPINS = 1u << 22;   // polls of one predecessor word (LB_SLEEP apart: >= 0.1 s)
+constexpr uint32_t LB_SLEEP = 1;          // s_sleep between polls of a word not yet published (x 64 clocks)
+constexpr uint32_t LB_STRIDE = 1;         // 8-B words between consecutive blocks' look-back words
+// k_walk_one: polls of a predecessor still walking before the block parks its
+// results (LB_DEF) instead of holding its slot: one slow block would otherwise
+// stall every block after it that finished meanwhile (a convoy filling the GPU
+// with waiting waves)
+constexpr uint32_t LB_DEFER = 8;
 struct LbCtl {
     uint32_t spins;        // the bound (LB_SPINS; tm_debug_set can lower it)
-    uint32_t fail_block;   // test hook: this block (in start order) acts as if its wait expired (NONE: off)
+    uint32_t fail_block;   // test hook: this block acts as if its wait expired (k_walk_one: parks) (NONE: off)
+    uint32_t defer;        // k_walk_one: LB_DEFER (tm_debug_set can change it)
 };
 
 struct Workspace {
@@ -76,12 +85,13 @@ struct Workspace {
     uint32_t *lists;      // [(L_COUNT + 1) * n] topic lists (the last one: long segments to sort)
     uint32_t *list_n;     // [L_COUNT] list lengths, [L_COUNT] reset ticket, [L_COUNT + 1] scan ticket,
                           // [L_COUNT + 2] long-segment count, [L_COUNT + 3] its reset ticket,
-                          // [L_COUNT + 4] the one-launch path's block ticket (zero between batches)
+                          // [L_COUNT + 4] the one-launch path's block ticket (zero between batches),
+                          // [LS_PARKED] k_walk_one blocks parked so far (diagnostics)
     uint64_t *blk;        // [n / TILE + 2] tile hit totals -> exclusive tile prefixes (zero between batches)
     uint32_t *deep_wid;   // [DEEP_LANES * MAX_LEVELS]
     uint2 *deep_stk;      // [DEEP_LANES * (MAX_LEVELS + 1)]
     uint8_t *deep_plus;   // [DEEP_LANES * MAX_LEVELS] '+' levels of each deep lane's path
-    uint64_t *look;       // [n / SM_TOPICS + 4] one-launch path: per block, one look-back word (lb_word)
+    uint64_t *look;       // [(n / SM_TOPICS + 4) * LB_STRIDE] one-launch path: per block, one look-back word (lb_word)
     // list lengths of the last count-mode batch that finished here ([0, L_COUNT))
     // and its topic count ([L_COUNT]; 0: none yet), written by the device into
     // mapped host memory: the next batch sizes its tail grids from them;
@@ -92,7 +102,8 @@ struct Workspace {
 };
 
 constexpr int TILE = 256;    // topics per walk block = per scan tile = per emit block
-constexpr int LIST_SLOTS = L_COUNT + 5;   // Workspace::list_n entries
+constexpr int LS_PARKED = L_COUNT + 5;    // Workspace::list_n word: k_walk_one blocks that parked, so far (diagnostics)
+constexpr int LIST_SLOTS = L_COUNT + 6;   // Workspace::list_n entries
 constexpr int HINT_FAIL = L_COUNT + 1;    // Workspace::hint_* word of the fail flag
 constexpr int HINT_WORDS = L_COUNT + 2;
 constexpr int SM_TOPICS = 16;             // topics per block of the one-launch small-batch path

@@ -243,8 +243,9 @@ struct tm_index {
     // test hooks (tm_debug_set, under mu): the look-back control of the next
     // dbg_lb_launches one-launch batches, and the two-phase path forced for
     // large batches
-    LbCtl dbg_lb{LB_SPINS, NONE};
+    LbCtl dbg_lb{LB_SPINS, NONE, LB_DEFER};
     uint64_t dbg_lb_launches = 0;
+    uint32_t lb_defer = LB_DEFER;   // k_walk_one's polls before a block parks (TM_DEBUG_LB_DEFER)
     bool dbg_phases = LARGE_PHASES_DEFAULT;
     std::atomic<uint64_t> failed_batches{0}, retried_batches{0};   // one-launch look-back failures seen / retried
     std::atomic<uint64_t> path_batches[PATH_COUNT] = {};             // match launches per kernel path
@@ -1161,7 +1162,7 @@ int next_tag(tm_index *ix, Lane &ln, hipStream_t s, uint32_t &tag) {
     ln.tag = (ln.tag + 1) & LB_TAG_MASK;
     if (!ln.tag) {
         ln.tag = 1;
-        HIPCHK(ix, hipMemsetAsync(ln.w.look, 0, (ln.w.cap_n / SM_TOPICS + 4) * 8, s));
+        HIPCHK(ix, hipMemsetAsync(ln.w.look, 0, (ln.w.cap_n / SM_TOPICS + 4) * 8 * LB_STRIDE, s));
     }
     tag = ln.tag;
     return TM_OK;
@@ -1170,7 +1171,7 @@ int next_tag(tm_index *ix, Lane &ln, hipStream_t s, uint32_t &tag) {
 // the look-back control of the next launch (caller holds ix->mu): the
 // default bound, or the test hook's for the next dbg_lb_launches launches
 LbCtl next_lb(tm_index *ix) {
-    if (!ix->dbg_lb_launches) return LbCtl{LB_SPINS, NONE};
+    if (!ix->dbg_lb_launches) return LbCtl{LB_SPINS, NONE, ix->lb_defer};
     ix->dbg_lb_launches--;
     return ix->dbg_lb;
 }
@@ -1538,8 +1539,8 @@ int ensure_ws(tm_index *ix, uint64_t n, Lane &ln) {
     HIPCHK(ix, hipMalloc(&w.lists, c * (L_COUNT + 1) * 4));
     HIPCHK(ix, hipMalloc(&w.blk, (c / TILE + 4) * 8));
     HIPCHK(ix, hipMemsetAsync(w.blk, 0, (c / TILE + 4) * 8, ln.s));   // zero between batches (k_emit)
-    HIPCHK(ix, hipMalloc(&w.look, (c / SM_TOPICS + 4) * 8));
-    HIPCHK(ix, hipMemsetAsync(w.look, 0, (c / SM_TOPICS + 4) * 8, ln.s));   // no launch tag is 0
+    HIPCHK(ix, hipMalloc(&w.look, (c / SM_TOPICS + 4) * 8 * LB_STRIDE));
+    HIPCHK(ix, hipMemsetAsync(w.look, 0, (c / SM_TOPICS + 4) * 8 * LB_STRIDE, ln.s));   // no launch tag is 0
     w.cap_n = c;
     return TM_OK;
 }
@@ -2215,6 +2216,10 @@ int tm_debug_set(tm_index *ix, uint32_t key, uint64_t value) {
     case TM_DEBUG_LB_FAIL_BLOCK: ix->dbg_lb.fail_block = value > 0xFFFFFFFFull ? NONE : (uint32_t)value; break;
     case TM_DEBUG_LB_LAUNCHES: ix->dbg_lb_launches = value; break;
     case TM_DEBUG_PHASES: ix->dbg_phases = value != 0; break;
+    case TM_DEBUG_LB_DEFER:
+        ix->lb_defer = value > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)value;
+        ix->dbg_lb.defer = ix->lb_defer;
+        break;
     default: return fail(ix, TM_EINVAL, "tm_debug_set: unknown key");
     }
     return TM_OK;
@@ -2228,6 +2233,20 @@ int tm_debug_get(tm_index *ix, uint32_t key, uint64_t *value) {
     case TM_DEBUG_PATH_PHASES: *value = ix->path_batches[PATH_PHASES].load(); break;
     case TM_DEBUG_PATH_SMALL: *value = ix->path_batches[PATH_SMALL].load(); break;
     case TM_DEBUG_PATH_ONE: *value = ix->path_batches[PATH_ONE].load(); break;
+    case TM_DEBUG_DEFERRED_BLOCKS: {   // every lane's counter, after its batches (device memory: copied back)
+        std::lock_guard<std::mutex> g(ix->mu);
+        uint64_t v = 0;
+        for (auto &l : ix->lanes) {
+            if (!l->w.list_n) continue;
+            uint32_t c = 0;
+            HIPCHK(ix, hipSetDevice(ix->rep[l->r].device));
+            if (l->used) HIPCHK(ix, hipEventSynchronize(l->done));
+            HIPCHK(ix, hipMemcpy(&c, l->w.list_n + LS_PARKED, 4, hipMemcpyDeviceToHost));
+            v += c;
+        }
+        *value = v;
+        break;
+    }
     default: return fail(ix, TM_EINVAL, "tm_debug_get: unknown key");
     }
     return TM_OK;

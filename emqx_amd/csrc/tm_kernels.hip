@@ -743,35 +743,45 @@ __device__ __forceinline__ uint64_t wave_incl_scan(uint64_t v) {
 }
 
 // Decoupled look-back of the one-launch kernels, by one whole wave: block vb
-// (in start order) publishes its own total `sum` (LB_AGG), reads its
-// predecessors' words 64 at a time (lane k: block hi - k) back to the nearest
-// inclusive prefix, publishes its own inclusive prefix and returns its
-// exclusive one (in every lane).  A predecessor took its ticket before vb, so
-// it is running and publishes soon; the wait for one word is still bounded
-// (lb.spins polls): past it -- or when a predecessor failed, or vb is the
-// test hook's lb.fail_block -- `fail` is set and vb publishes LB_FAIL, which
-// every later block meets and propagates.  Nothing after a failed block is
-// trusted: the caller flags its topics err 4 and raises the workspace's fail
-// word (a failed block used to publish a partial prefix that its
-// successors took as correct).
+// publishes its own total `sum` (LB_AGG), reads its predecessors' words 64 at
+// a time (lane k: block hi - k) back to the nearest inclusive prefix, summing
+// the totals in between (LB_AGG / LB_DEF), publishes its own inclusive prefix
+// and returns its exclusive one (in every lane).  A predecessor dispatched
+// before vb is running or done, so it publishes soon; the wait for one word is
+// still bounded:
+//  - k_walk_small (DEFER false): past lb.spins polls -- or when a predecessor
+//    failed, or vb is the test hook's lb.fail_block -- the result is LBR_FAIL
+//    and vb publishes LB_FAIL, which every later block meets and propagates:
+//    nothing after a failed block is trusted, the caller flags its topics err
+//    4 and raises the workspace's fail word (a failed block used to
+//    publish a partial prefix its successors took as correct);
+//  - k_walk_one (DEFER true): past lb.defer polls of a predecessor still
+//    walking (or for the hook's block) the result is LBR_DEFER: vb publishes
+//    LB_DEF with its own total -- later blocks sum it like LB_AGG -- parks its
+//    results and leaves; k_one_finish, after the kernel, emits them.
+enum { LBR_OK = 0, LBR_FAIL = 1, LBR_DEFER = 2 };
+template <bool DEFER>
 __device__ __forceinline__ uint64_t look_back(uint64_t *look, uint32_t vb, uint32_t tag, uint64_t sum, const LbCtl &lb,
-                                              bool &fail) {
+                                              int &res) {
     const uint32_t lane = threadIdx.x & 63;
     uint64_t pre = 0;
-    fail = vb == lb.fail_block;
-    if (!fail && vb > 0 && lane == 0)
-        __hip_atomic_store(&look[vb], lb_word(tag, LB_AGG, sum), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    res = vb == lb.fail_block ? (DEFER ? LBR_DEFER : LBR_FAIL) : LBR_OK;
+    if (res == LBR_OK && vb > 0 && lane == 0)
+        __hip_atomic_store(&look[(uint64_t)vb * LB_STRIDE], lb_word(tag, LB_AGG, sum), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t bound = DEFER ? lb.defer : lb.spins;
     uint32_t spins = 0;
-    for (int64_t hi = (int64_t)vb - 1; hi >= 0 && !fail;) {
+    for (int64_t hi = (int64_t)vb - 1; hi >= 0 && res == LBR_OK;) {
         const int64_t j = hi - (int64_t)lane;
         uint64_t f = lb_word(tag, LB_INCL, 0);   // before block 0: an inclusive prefix of 0
         if (j >= 0)
             for (;;) {
-                f = __hip_atomic_load(&look[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (lb_tag(f) == tag || ++spins > lb.spins) break;
-                __builtin_amdgcn_s_sleep(1);
+                f = __hip_atomic_load(&look[(uint64_t)j * LB_STRIDE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (lb_tag(f) == tag || ++spins > bound) break;
+                __builtin_amdgcn_s_sleep(LB_SLEEP);
             }
-        if (__ballot(lb_tag(f) != tag || lb_state(f) == LB_FAIL)) { fail = true; break; }
+        if (__ballot(lb_tag(f) == tag && lb_state(f) == LB_FAIL)) { res = LBR_FAIL; break; }
+        if (__ballot(lb_tag(f) != tag)) { res = DEFER ? LBR_DEFER : LBR_FAIL; break; }
         const uint64_t mi = __ballot(lb_state(f) == LB_INCL);
         const uint32_t k = mi ? (uint32_t)__ffsll((long long)mi) - 1 : 63;   // nearest inclusive prefix
         uint64_t v = lane <= k ? f & LB_VAL_MASK : 0;
@@ -781,7 +791,9 @@ __device__ __forceinline__ uint64_t look_back(uint64_t *look, uint32_t vb, uint3
         hi -= 64;
     }
     if (lane == 0)
-        __hip_atomic_store(&look[vb], fail ? lb_word(tag, LB_FAIL, 0) : lb_word(tag, LB_INCL, pre + sum),
+        __hip_atomic_store(&look[(uint64_t)vb * LB_STRIDE],
+                           res == LBR_OK ? lb_word(tag, LB_INCL, pre + sum)
+                                         : lb_word(tag, res == LBR_DEFER ? LB_DEF : LB_FAIL, sum),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return pre;
 }
@@ -1353,8 +1365,9 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_small(DevIndex ix, Workspace 
         for (int i = 0; i < SM_TOPICS; i++) sum += s_cnt[i];
         // one flag round trip per 64 predecessors (look_back); a failed wait
         // fails this block and every later one: err 4, the fail word raised
-        bool fail;
-        const uint64_t pre = look_back(ws.look, vb, tag, sum, lb, fail);
+        int res;
+        const uint64_t pre = look_back<false>(ws.look, vb, tag, sum, lb, res);
+        const bool fail = res != LBR_OK;
         if (threadIdx.x == 0) {
             s_fail = fail;
             s_sum = sum;
@@ -1790,50 +1803,111 @@ __global__ __launch_bounds__(EMIT_BLOCK) void k_emit(DevIndex ix, Workspace ws, 
 
 // ------------------------------------------------ large batches in one pass
 //
-// k_walk_one: the whole count-mode batch above SMALL_TOPICS topics in ONE
-// launch.  The two-phase path (k_walk_fast, tails,
-// k_scan_top, k_emit, k_rewalk_tail) parks every topic's value ranges in HBM
-// between the walk and the emit -- 44 B/topic written and 73 B/topic read back
-// on C3 -- and its three short kernels queue behind other streams' walks for
-// workgroup slots.  Here a 64-lane block (one wave, one topic per lane)
+// k_walk_one: the whole count-mode batch above SMALL_TOPICS topics in one
+// launch, plus k_one_finish for the blocks that parked.
+// The two-phase path (k_walk_fast, tails, k_scan_top, k_emit, k_rewalk_tail)
+// parks EVERY topic's value ranges in HBM between the walk and the emit --
+// 44 B/topic written and 73 B/topic read back on C3 -- and its three short
+// kernels queue behind other streams' walks for workgroup slots.  Here a
+// 64-lane block (one wave, one topic per lane)
 //   1. walks its topics exactly as k_walk_fast (the same dfs, LDS store and
-//      register ranges);
+//      register ranges); a lane's ranges then wait in its own (dead) column of
+//      the walk store;
 //   2. counts the topics deeper than FAST_L levels with a second walk over the
 //      same LDS, tokenised with every level scanned and only the levels the
 //      trie can use resolved (LdsStore<FAST_L, true>; one_pass_ok: the index's
 //      depth and binary keys fit FAST_L, and it holds no '#'-not-last key);
-//      a lane's ranges wait in its own (dead) column of the walk store;
-//   3. gets its global offset from the decoupled look-back (look_back, over
-//      the blocks in start order -- a ticket, so it only waits for blocks
-//      already running);
-//   4. writes its offsets and flags, and its values straight from the
-//      registers: the ranges go to LDS (the walk store's space) and the wave
-//      writes the block's span with wave_emit, as k_emit does per wave;
+//   3. gets its global offset from the decoupled look-back (look_back<true>,
+//      over the blocks in dispatch order);
+//   4. writes its offsets and flags, and its values from the LDS ranges with
+//      wave_emit, as k_emit does per wave (one_emit);
 //   5. re-walks the topics whose values it could not keep (more than RCAP
 //      ranges, or deeper than FAST_L) and writes their values directly.
-// Per topic it writes only the CSR itself: 8 B offset + 1 B flag + 4 B per
-// value; nothing else crosses HBM between the steps.
+// A block whose predecessors are still walking after LB_DEFER polls does not
+// wait on: it parks its counts, flags and ranges (as k_walk_fast would) and
+// publishes LB_DEF; k_one_finish emits those blocks once the kernel is done.
+// Waiting blocks hold their slots, so one slow block would stall every block
+// after it that finished meanwhile -- the GPU filling up with waiting waves.
+// Per topic of a block that does not park, only the CSR itself is written:
+// 8 B offset + 1 B flag + 4 B per value.
 static_assert(WALK_BLOCK == 64, "k_walk_one: one wave per block");
 union OneLds {   // a k_walk_one block's LDS, reused step by step (4864 B: 8 waves per SIMD as k_walk_fast)
     struct { uint32_t wid[FAST_L * WALK_BLOCK], pend[(FAST_L + 1) * WALK_BLOCK]; uint8_t len[FAST_L * WALK_BLOCK]; } walk;
     struct { uint32_t off[WR], rel[WR + 1]; uint8_t flg[WR]; } emit;
 };
+static_assert(2 * RCAP <= 2 * FAST_L + 1, "a lane's walk-store column holds its ranges");
 
-// (the workspace comes as the four pointers k_walk_one uses -- ticket,
-// parked ranges, look-back words, fail word -- not the whole struct: fewer
-// scalar registers held across the walk)
-__global__ __launch_bounds__(WALK_BLOCK, 8) void k_walk_one(DevIndex ix, uint32_t *ticket, uint2 *rng, uint64_t *look,
-                                                          uint32_t *fail_word, uint64_t n, const uint8_t *blob,
-                                                          const uint64_t *offs, uint8_t *err, uint64_t *hit_offs,
-                                                          uint32_t *out, uint64_t cap, uint32_t tag, LbCtl lb) {
-    __shared__ OneLds S;
-    const uint32_t lane = threadIdx.x;
-    uint32_t vb = 0;
-    if (lane == 0) {
-        vb = atomicAdd(ticket, 1u);   // blocks scan in start order
-        if (vb == gridDim.x - 1) atomicExch(ticket, 0u);   // every ticket is taken
+// k_walk_one's arguments besides the index.  The walk reads the first three;
+// the rest are read only after it, through late_args(): held in scalar
+// registers across the walk they spilled (k_walk_fast's 64-VGPR budget, 8
+// waves per SIMD, has no room for them), and a kernel that spills needs
+// scratch -- its hot loop then reloaded values from it.
+struct OneArgs {
+    uint64_t n; const uint8_t *blob; const uint64_t *offs;                        // the walk's
+    uint64_t *look; uint8_t *err; uint64_t *hit_offs; uint32_t *out; uint64_t cap; // after it
+    uint32_t *cnt, *nr; uint2 *rng;                                               // parked blocks' results
+    uint32_t tag; LbCtl lb;
+};
+struct OneKargs { DevIndex ix; OneArgs a; };   // k_walk_one's kernarg layout (arguments in order, naturally aligned)
+
+// the kernel's own OneArgs in its kernarg segment, behind an opaque step so
+// the compiler cannot hoist the loads through it to the kernel's entry
+__device__ __forceinline__ const OneArgs *late_args() {
+    uint64_t p = (uint64_t)(uintptr_t)(const void *)__builtin_amdgcn_kernarg_segment_ptr() + offsetof(OneKargs, a);
+    asm volatile("" : "+s"(p));
+    return reinterpret_cast<const OneArgs *>(p);
+}
+
+// Steps 4 and 5 of a block (one wave, lane = topic t): offset, values of the
+// ranges rg[0, nrr) at base + rel, or -- rew -- a re-walk writing them.  The
+// LDS is free on entry (walk stores dead, the lane's ranges in registers).
+__device__ __forceinline__ void one_emit(const DevIndex &ix, OneLds &S, const uint8_t *blob, const uint64_t *offs,
+                                         uint64_t t, bool live, bool rew, uint32_t nrr, const uint2 (&rg)[RCAP],
+                                         uint64_t base, uint64_t rel, uint64_t total, uint64_t *hit_offs,
+                                         uint32_t *out, uint64_t cap) {
+    const uint32_t lane = threadIdx.x & 63;
+    if (live) __builtin_nontemporal_store(base + rel, hit_offs + t);
+    uint32_t R;
+    const uint32_t r0 = wave_excl_scan32(rew ? 1u : nrr, R);
+    const uint32_t rel32 = (uint32_t)rel;
+    if (rew) {
+        S.emit.off[r0] = 0; S.emit.rel[r0] = rel32; S.emit.flg[r0] = RF_SKIP;
+    } else {
+        uint32_t acc = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < RCAP; i++) {
+            if (i >= nrr) break;
+            S.emit.off[r0 + i] = rg[i].x;          // RUN_INLINE: the value itself
+            S.emit.rel[r0 + i] = rel32 + acc;
+            S.emit.flg[r0 + i] = (rg[i].y & RUN_INLINE) ? RF_INLINE : 0;
+            acc += rg[i].y & RUN_CNT;
+        }
     }
-    vb = __builtin_amdgcn_readfirstlane((uint32_t)__shfl((int)vb, 0, 64));
+    if (lane == 0) S.emit.rel[R] = (uint32_t)total;
+    wave_sync();
+    wave_emit(ix, S.emit.off, S.emit.rel, S.emit.flg, R, base, base + total, out, cap);
+    if (__ballot(rew)) {
+        wave_sync();   // the LDS holds walk stores again
+        if (rew) {
+            LdsStore<FAST_L, true> st{S.walk.wid + lane, S.walk.pend + lane, S.walk.len + lane, WALK_BLOCK, 0};
+            DirectEmit de{ix.vals, out, base + rel, cap};
+            match_topic(ix, blob, offs[t], offs[t + 1], st, de);
+        }
+    }
+}
+
+__global__ __launch_bounds__(WALK_BLOCK, 8) void k_walk_one(DevIndex ix, OneArgs a) {
+    __shared__ OneLds S;
+    const uint64_t n = a.n;
+    const uint8_t *blob = a.blob;
+    const uint64_t *offs = a.offs;
+    const uint32_t lane = threadIdx.x;
+    // Blocks scan in blockIdx order: workgroups are dispatched in that order,
+    // so a block's predecessors are running or done, never waiting for a slot
+    // it holds.  (A start-order ticket -- one atomic on one word per block, as
+    // k_walk_small takes -- serialised 15.6k blocks at ~9 ns each: the C3
+    // batch 0.343 -> 0.478 ms, profiles/r4/onepass_study.md.)
+    const uint32_t vb = blockIdx.x;
     const uint64_t t = (uint64_t)vb * WALK_BLOCK + lane;
     const bool live = t < n;
 
@@ -1847,10 +1921,9 @@ __global__ __launch_bounds__(WALK_BLOCK, 8) void k_walk_one(DevIndex ix, uint32_
         rc = match_topic(ix, blob, offs[t], offs[t + 1], st, em);
         if (rc == RC_OK) {
             cnt = em.cnt; nr = em.nr;
-            // the ranges go into this lane's own column of the walk store
-            // (FAST_L + (FAST_L + 1) words >= 2 RCAP), dead once its walk is
-            // done: no register holds them across the rest of the kernel
-            static_assert(2 * RCAP <= 2 * FAST_L + 1, "a lane's store column holds its ranges");
+            // the ranges go into this lane's own column of the walk store,
+            // dead once its walk is done: no register holds them across the
+            // rest of the kernel
 #pragma unroll
             for (uint32_t i = 0; i < RCAP; i++)
                 if (i < nr) { S.walk.wid[i * WALK_BLOCK + lane] = em.r[i].x; S.walk.pend[i * WALK_BLOCK + lane] = em.r[i].y; }
@@ -1870,59 +1943,102 @@ __global__ __launch_bounds__(WALK_BLOCK, 8) void k_walk_one(DevIndex ix, uint32_
         e = frc == RC_BADARG ? 1u : frc == RC_DEEP ? 2u : 0u;   // RC_DEEP here: > MAX_LEVELS levels
     }
     rew = rew && e == 0 && cnt > 0;
+    const uint32_t nrr = rew || rc != RC_OK ? 0u : nr;
 
     // ---- 3. the block's offset
+    const OneArgs &A = *late_args();
     const uint64_t inc = wave_incl_scan(cnt);
     const uint64_t total = __shfl(inc, 63, 64), rel = inc - cnt;
-    bool fail;
-    const uint64_t base = look_back(look, vb, tag, total, lb, fail);
-    if (fail) {   // (wave-uniform) no trusted offset: the host runs the batch again
-        if (live) err[t] = 4;
-        if (lane == 0) *fail_word = 1;
-        return;
-    }
-
-    // ---- 4. offsets, flags, values
-    if (live) {
-        __builtin_nontemporal_store(base + rel, hit_offs + t);
-        __builtin_nontemporal_store((uint8_t)e, err + t);
-    }
-    if (lane == 0 && vb == gridDim.x - 1) hit_offs[n] = base + total;
-    uint32_t R;
-    const uint32_t nrr = rew ? 1u : (rc == RC_OK ? nr : 0u);
-    const uint32_t r0 = wave_excl_scan32(nrr, R);
-    uint2 rg[RCAP];   // this lane's ranges, out of its store column before the stage overwrites it
+    int res;
+    const uint64_t base = look_back<true>(A.look, vb, A.tag, total, A.lb, res);
+    uint2 rg[RCAP];   // this lane's ranges, out of its store column before the LDS is reused
 #pragma unroll
     for (uint32_t i = 0; i < RCAP; i++)
-        rg[i] = i < nrr && !rew ? make_uint2(S.walk.wid[i * WALK_BLOCK + lane], S.walk.pend[i * WALK_BLOCK + lane])
-                                : make_uint2(0, 0);
+        rg[i] = i < nrr ? make_uint2(S.walk.wid[i * WALK_BLOCK + lane], S.walk.pend[i * WALK_BLOCK + lane])
+                        : make_uint2(0, 0);
+    if (live) __builtin_nontemporal_store((uint8_t)e, A.err + t);
+    if (res != LBR_OK) {   // (wave-uniform) parked for k_one_finish, as k_walk_fast leaves every topic
+        if (live) {
+            __builtin_nontemporal_store(cnt, A.cnt + t);
+            __builtin_nontemporal_store(rew ? (uint32_t)RCAP + 1 : nrr, A.nr + t);
+#pragma unroll
+            for (uint32_t i = 0; i < RCAP; i++)
+                if (i < nrr)
+                    __builtin_nontemporal_store((uint64_t)rg[i].x | (uint64_t)rg[i].y << 32,
+                                                reinterpret_cast<uint64_t *>(A.rng) + (uint64_t)i * n + t);
+        }
+        return;
+    }
+    if (lane == 0 && vb == gridDim.x - 1) A.hit_offs[n] = base + total;
+
+    // ---- 4, 5. offsets, values, re-walks
     wave_sync();   // every lane has its ranges: the LDS becomes the range stage
-    const uint32_t rel32 = (uint32_t)rel;
-    if (rew) {
-        S.emit.off[r0] = 0; S.emit.rel[r0] = rel32; S.emit.flg[r0] = RF_SKIP;
-    } else {
-        uint32_t acc = 0;
+    one_emit(ix, S, blob, offs, t, live, rew, nrr, rg, base, rel, total, A.hit_offs, A.out, A.cap);
+}
+
+// The blocks of a k_walk_one launch that parked (LB_DEF), after it: one wave
+// per 64 blocks' look-back words; per parked block, its exclusive prefix from
+// the words before it (final now: LB_INCL or LB_DEF), then its offsets and
+// values from the parked counts and ranges (one_emit, re-walks included).  A
+// word that is not final (never, unless a block failed to publish) raises the
+// fail word: the host runs the batch again.  The workspace counts the parked
+// blocks (list_n[LS_PARKED], TM_DEBUG_DEFERRED_BLOCKS).
+__global__ __launch_bounds__(WALK_BLOCK) void k_one_finish(DevIndex ix, OneArgs a, uint32_t nb, uint32_t *fail_word,
+                                                           uint32_t *parked) {
+    __shared__ OneLds S;
+    const uint32_t lane = threadIdx.x;
+    const uint32_t w0 = blockIdx.x * 64;
+    const uint64_t n = a.n;
+    const uint64_t fw = w0 + lane < nb ? __hip_atomic_load(&a.look[(uint64_t)(w0 + lane) * LB_STRIDE], __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_AGENT) : 0;
+    uint64_t mdef = __ballot(w0 + lane < nb && lb_tag(fw) == a.tag && lb_state(fw) == LB_DEF);
+    const uint64_t mbad = __ballot(w0 + lane < nb && (lb_tag(fw) != a.tag || lb_state(fw) == LB_AGG ||
+                                                      lb_state(fw) == LB_FAIL));
+    if (mbad && lane == 0) *fail_word = 1;   // (the offsets are not trusted: the host runs the batch again)
+    if (mdef && lane == 0) atomicAdd(parked, (uint32_t)__popcll(mdef));   // (device memory: diagnostics)
+    while (mdef) {
+        const uint32_t vb = w0 + (uint32_t)__ffsll((long long)mdef) - 1;
+        mdef &= mdef - 1;
+        // the block's exclusive prefix: the nearest inclusive one before it plus the parked totals between
+        uint64_t pre = 0;
+        bool bad = false;
+        for (int64_t hi = (int64_t)vb - 1; hi >= 0;) {
+            const int64_t j = hi - (int64_t)lane;
+            const uint64_t f = j >= 0 ? __hip_atomic_load(&a.look[(uint64_t)j * LB_STRIDE], __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT)
+                                      : lb_word(a.tag, LB_INCL, 0);
+            if (__ballot(lb_tag(f) != a.tag || (lb_state(f) != LB_INCL && lb_state(f) != LB_DEF))) { bad = true; break; }
+            const uint64_t mi = __ballot(lb_state(f) == LB_INCL);
+            const uint32_t k = mi ? (uint32_t)__ffsll((long long)mi) - 1 : 63;
+            uint64_t v = lane <= k ? f & LB_VAL_MASK : 0;
+            for (int d = 32; d; d >>= 1) v += __shfl_xor(v, d, 64);
+            pre += v;
+            if (mi) break;
+            hi -= 64;
+        }
+        if (bad) {
+            if (lane == 0) *fail_word = 1;
+            continue;
+        }
+        const uint64_t t = (uint64_t)vb * WALK_BLOCK + lane;
+        const bool live = t < n;
+        const uint32_t cnt = live ? __builtin_nontemporal_load(a.cnt + t) : 0u;
+        const uint32_t pnr = live ? __builtin_nontemporal_load(a.nr + t) : 0u;
+        const bool rew = pnr > RCAP;
+        const uint32_t nrr = rew ? 0u : pnr;
+        uint2 rg[RCAP];
 #pragma unroll
         for (uint32_t i = 0; i < RCAP; i++) {
-            if (i >= nrr) break;
-            S.emit.off[r0 + i] = rg[i].x;          // RUN_INLINE: the value itself
-            S.emit.rel[r0 + i] = rel32 + acc;
-            S.emit.flg[r0 + i] = (rg[i].y & RUN_INLINE) ? RF_INLINE : 0;
-            acc += rg[i].y & RUN_CNT;
+            const uint64_t g = i < nrr ? __builtin_nontemporal_load(reinterpret_cast<const uint64_t *>(a.rng) +
+                                                                    (uint64_t)i * n + t) : 0;
+            rg[i] = make_uint2((uint32_t)g, (uint32_t)(g >> 32));
         }
-    }
-    if (lane == 0) S.emit.rel[R] = (uint32_t)total;
-    wave_sync();
-    wave_emit(ix, S.emit.off, S.emit.rel, S.emit.flg, R, base, base + total, out, cap);
-
-    // ---- 5. re-walks: values straight into the CSR
-    if (__ballot(rew)) {
-        wave_sync();   // the LDS holds walk stores again
-        if (rew) {
-            LdsStore<FAST_L, true> st{S.walk.wid + lane, S.walk.pend + lane, S.walk.len + lane, WALK_BLOCK, 0};
-            DirectEmit de{ix.vals, out, base + rel, cap};
-            match_topic(ix, blob, offs[t], offs[t + 1], st, de);
-        }
+        const uint64_t inc = wave_incl_scan(cnt);
+        const uint64_t total = __shfl(inc, 63, 64);
+        if (lane == 0 && vb == nb - 1) a.hit_offs[n] = pre + total;
+        wave_sync();   // (the previous parked block's emit is done with the LDS)
+        one_emit(ix, S, a.blob, a.offs, t, live, rew, nrr, rg, pre, inc - cnt, total, a.hit_offs, a.out, a.cap);
+        wave_sync();
     }
 }
 
@@ -2223,10 +2339,16 @@ hipError_t launch_match(const DevIndex &ix, const Workspace &ws, uint64_t n, con
         if (n <= SMALL_TOPICS)
             hipLaunchKernelGGL(k_walk_small<MODE_COUNT>, dim3(blocks_for(n, SM_TOPICS)), dim3(WV_BLOCK), 0, s, ix, ws,
                                n, bytes, offs, o, hit_offs, out, cap, tag & LB_TAG_MASK, lb);
-        else
-            hipLaunchKernelGGL(k_walk_one, dim3(blocks_for(n, WALK_BLOCK)), dim3(WALK_BLOCK), 0, s, ix,
-                               ws.list_n + L_COUNT + 4, ws.rng, ws.look, ws.hint_d + HINT_FAIL, n, bytes, offs, err,
-                               hit_offs, out, cap, tag & LB_TAG_MASK, lb);
+        if (n > SMALL_TOPICS) {
+            const OneArgs a{n, bytes, offs, ws.look, err, hit_offs, out, cap, ws.cnt, ws.nr, ws.rng,
+                            tag & LB_TAG_MASK, lb};
+            const uint32_t nb = blocks_for(n, WALK_BLOCK);
+            hipLaunchKernelGGL(k_walk_one, dim3(nb), dim3(WALK_BLOCK), 0, s, ix, a);
+            if (ev_walk1 && (e = hipEventRecord(ev_walk1, s)) != hipSuccess) return e;
+            hipLaunchKernelGGL(k_one_finish, dim3(blocks_for(nb, 64)), dim3(WALK_BLOCK), 0, s, ix, a, nb,
+                               ws.hint_d + HINT_FAIL, ws.list_n + LS_PARKED);
+            return hipGetLastError();
+        }
         if (ev_walk1 && (e = hipEventRecord(ev_walk1, s)) != hipSuccess) return e;
         return hipGetLastError();
     }
@@ -2241,7 +2363,7 @@ hipError_t launch_first(const DevIndex &ix, const Workspace &ws, uint64_t n, con
     Outs o{nullptr, out_value, out_found};
     if (small_path_ok(ix, n)) {
         hipLaunchKernelGGL(k_walk_small<MODE_FIRST>, dim3(blocks_for(n, SM_TOPICS)), dim3(WV_BLOCK), 0, s, ix, ws, n,
-                           bytes, offs, o, nullptr, nullptr, (uint64_t)0, 0u, LbCtl{LB_SPINS, NONE});
+                           bytes, offs, o, nullptr, nullptr, (uint64_t)0, 0u, LbCtl{LB_SPINS, NONE, LB_DEFER});
         return hipGetLastError();
     }
     if (n <= WAVE_TOPICS)

@@ -276,19 +276,24 @@ int tm_profile_read(tm_index *h, double *walk_ms, double *batch_ms, uint64_t *ba
 /* Test hooks (no reference counterpart; tests/test_gpu_parity.py):
  *   TM_DEBUG_LB_SPINS       the look-back wait bound (polls of one word) of the
  *   TM_DEBUG_LB_FAIL_BLOCK  next TM_DEBUG_LB_LAUNCHES one-launch batches, and
- *   TM_DEBUG_LB_LAUNCHES    the block (in start order) that fails as if its
- *                           wait expired (>= 2^32: none)
+ *   TM_DEBUG_LB_LAUNCHES    the block that fails as if its wait expired
+ *                           (k_walk_one: parks) (>= 2^32: none)
  *   TM_DEBUG_PHASES         batches above 65536 topics: 1 the two-phase path
  *                           (walk, tails, scan, emit), 0 one launch (k_walk_one,
  *                           where the index allows it); the default is the
  *                           faster of the two on C3
+ *   TM_DEBUG_LB_DEFER       k_walk_one: polls of a predecessor still walking
+ *                           before a block parks its results for k_one_finish
+ *                           (0: every block that would wait parks)
  * tm_debug_get: TM_DEBUG_FAILED_BATCHES (one-launch batches whose look-back
  * failed, host API), TM_DEBUG_RETRIED_BATCHES (of those, run again) and the
  * match launches per kernel path: TM_DEBUG_PATH_PHASES (walk, tails, scan,
- * emit), TM_DEBUG_PATH_SMALL (k_walk_small), TM_DEBUG_PATH_ONE (k_walk_one). */
+ * emit), TM_DEBUG_PATH_SMALL (k_walk_small), TM_DEBUG_PATH_ONE (k_walk_one),
+ * and TM_DEBUG_DEFERRED_BLOCKS: k_walk_one blocks that parked (after the
+ * batches finished). */
 enum { TM_DEBUG_LB_SPINS = 1, TM_DEBUG_LB_FAIL_BLOCK = 2, TM_DEBUG_LB_LAUNCHES = 3, TM_DEBUG_PHASES = 4,
        TM_DEBUG_FAILED_BATCHES = 5, TM_DEBUG_RETRIED_BATCHES = 6, TM_DEBUG_PATH_PHASES = 7,
-       TM_DEBUG_PATH_SMALL = 8, TM_DEBUG_PATH_ONE = 9 };
+       TM_DEBUG_PATH_SMALL = 8, TM_DEBUG_PATH_ONE = 9, TM_DEBUG_LB_DEFER = 10, TM_DEBUG_DEFERRED_BLOCKS = 11 };
 int tm_debug_set(tm_index *h, uint32_t key, uint64_t value);
 int tm_debug_get(tm_index *h, uint32_t key, uint64_t *value);
 

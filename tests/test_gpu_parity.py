@@ -2026,20 +2026,19 @@ def test_one_pass_c3deep_and_index_gates(torch_dev):
 
 # ------------------------------------- device failures are not badarg (round 4)
 
-@pytest.mark.parametrize("nt", [5_000, 100_000])   # k_walk_small / k_walk_one
-def test_lookback_failure_is_retried_then_a_device_error(torch_dev, nt):
-    """A one-launch batch whose look-back wait expires (forced: block 3 acts
-    as if its wait expired, TM_DEBUG_LB_FAIL_BLOCK) flags err 4 from that block
-    on (LB_FAIL propagates: no later block takes a partial prefix), the host
-    API runs it again once -- exact results -- and a second failure is a
-    device error for the whole call: TM_EDEVICE / DeviceError, never BadArg
-    (the reference raises badarg only for a '+'/'#' level,
-    emqx_trie_search.erl:374-375)."""
+def test_lookback_failure_is_retried_then_a_device_error(torch_dev):
+    """A one-launch small batch (k_walk_small) whose look-back wait expires
+    (forced: block 3 acts as if its wait expired, TM_DEBUG_LB_FAIL_BLOCK) flags
+    err 4 from that block on (LB_FAIL propagates: no later block takes a
+    partial prefix), the host API runs it again once -- exact results -- and a
+    second failure is a device error for the whole call: TM_EDEVICE /
+    DeviceError, never BadArg (the reference raises badarg only for a '+'/'#'
+    level, emqx_trie_search.erl:374-375)."""
     torch = torch_dev
+    nt = 5_000
     fs = wl.filters(3, 50_000)
     ts = wl.topics(3, 50_000, nt)
     ix, o = gpu_index(fs), oracle_of(fs)
-    ix.debug_set(_native.TM_DEBUG_PHASES, 0)   # (large batches: k_walk_one)
     assert_same(ix, o, ts)
     f0, r0 = ix.debug_get(_native.TM_DEBUG_FAILED_BATCHES), ix.debug_get(_native.TM_DEBUG_RETRIED_BATCHES)
     assert f0 == 0 and r0 == 0                       # a normal run never fails
@@ -2068,8 +2067,7 @@ def test_lookback_failure_is_retried_then_a_device_error(torch_dev, nt):
                        d_err.data_ptr(), torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
     err = d_err.cpu().numpy()
-    per_block = 16 if nt <= 65536 else 64
-    first = 3 * per_block
+    first = 3 * 16   # k_walk_small: 16 topics per block
     assert not err[:first].any() and (err[first:] == 4).all()
     # the hook is spent: the next batches are exact again, with no failure
     assert_same(ix, o, ts)
@@ -2079,7 +2077,8 @@ def test_lookback_failure_is_retried_then_a_device_error(torch_dev, nt):
 def test_lookback_without_waiting_is_exact_or_a_device_error(torch_dev):
     """With no wait at all (TM_DEBUG_LB_SPINS 0: a block fails whenever a
     predecessor has not published yet), every batch either matches exactly or
-    fails as a device error -- never a wrong result, never BadArg."""
+    fails as a device error -- never a wrong result, never BadArg (k_walk_one
+    parks instead of failing: exact either way)."""
     fs = wl.filters(3, 50_000)
     ix, o = gpu_index(fs), oracle_of(fs)
     ix.debug_set(_native.TM_DEBUG_PHASES, 0)
@@ -2094,3 +2093,32 @@ def test_lookback_without_waiting_is_exact_or_a_device_error(torch_dev):
         ix.debug_set(_native.TM_DEBUG_LB_LAUNCHES, 0)
         ix.debug_set(_native.TM_DEBUG_LB_SPINS, 1 << 22)
         assert_same(ix, o, ts)
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_one_pass_parked_blocks_are_finished(torch_dev, seed):
+    """k_walk_one blocks that would wait for a predecessor still walking park
+    their counts, flags and ranges (LB_DEF) and k_one_finish emits them after
+    the kernel: forced for one block (the hook), for every block that would
+    wait at all (TM_DEBUG_LB_DEFER 0), and never (a bound no wait reaches) --
+    exact CSR against the oracle each time, overflowing and deep topics
+    included, and no failure."""
+    r = random.Random(0x454D5158 + 500 + seed)
+    filters, vals, topics = _shallow_case(r)
+    fs = items_of(filters, vals)
+    ix, o = gpu_index(fs), oracle_of(fs)
+    ix.debug_set(_native.TM_DEBUG_PHASES, 0)
+    big = items_of([topics[i % len(topics)] for i in r.sample(range(90_000 * 2), 90_000)])
+    ix.debug_set(_native.TM_DEBUG_LB_FAIL_BLOCK, 5)
+    ix.debug_set(_native.TM_DEBUG_LB_LAUNCHES, 1 << 30)
+    d0 = ix.debug_get(_native.TM_DEBUG_DEFERRED_BLOCKS)
+    assert_same(ix, o, big)
+    assert ix.debug_get(_native.TM_DEBUG_DEFERRED_BLOCKS) > d0
+    ix.debug_set(_native.TM_DEBUG_LB_LAUNCHES, 0)
+    for defer in (0, 1 << 30, 8):
+        ix.debug_set(_native.TM_DEBUG_LB_DEFER, defer)
+        d0 = ix.debug_get(_native.TM_DEBUG_DEFERRED_BLOCKS)
+        assert_same(ix, o, big)
+        if defer == 1 << 30:
+            assert ix.debug_get(_native.TM_DEBUG_DEFERRED_BLOCKS) == d0
+    assert ix.debug_get(_native.TM_DEBUG_FAILED_BATCHES) == 0

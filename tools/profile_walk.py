@@ -27,6 +27,12 @@ def main():
     p.add_argument("--filter-order", default="stream", choices=["stream", "sorted"],
                    help="insertion order of the filters (node ids follow it): generator stream or "
                         "byte-sorted, i.e. trie nodes numbered depth first (layout study)")
+    p.add_argument("--streams", type=int, default=1,
+                   help="streams the launches rotate over (3: bench.py's overlapped steps; wall/batch is then the "
+                        "step time)")
+    p.add_argument("--large-path", default="default", choices=["default", "one", "phases"],
+                   help="batches above 65536 topics: the library's default, k_walk_one or the two-phase path")
+    p.add_argument("--lb-defer", type=int, default=None, help="k_walk_one: polls before a block parks (TM_DEBUG_LB_DEFER)")
     a = p.parse_args()
     import torch
     from bench import CONFIGS
@@ -41,6 +47,10 @@ def main():
         fs = wl.ItemSet(blob, offs, fs.vals[np.array(order)], fs.flags[np.array(order)])
         del items, order
     ix = _native.Index(device=0)
+    if a.large_path != "default":
+        ix.debug_set(_native.TM_DEBUG_PHASES, int(a.large_path == "phases"))
+    if a.lb_defer is not None:
+        ix.debug_set(_native.TM_DEBUG_LB_DEFER, a.lb_defer)
     for lo in range(0, len(fs), 2_000_000):
         part = fs.slice(lo, min(lo + 2_000_000, len(fs)))
         ix.apply(np.ones(len(part), np.uint8), part.blob, part.offs, part.vals)
@@ -66,18 +76,25 @@ def main():
     d_hit = torch.zeros(a.batch + 1, dtype=torch.int64, device=dev)
     d_err = torch.zeros(a.batch, dtype=torch.uint8, device=dev)
     s = torch.cuda.current_stream().cuda_stream
+    S = max(1, a.streams)
+    streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(S - 1)]
     tot = 0
     for d_blob, d_offs in d_in:
         ix.match_batch_dev(a.batch, d_blob.data_ptr(), d_offs.data_ptr(), d_hit.data_ptr(), 0, 0, d_err.data_ptr(), s)
         torch.cuda.synchronize()
         tot = max(tot, int(d_hit[-1]))
-    d_out = torch.zeros(max(tot, 1), dtype=torch.int32, device=dev)
+    outs = [(torch.zeros(a.batch + 1, dtype=torch.int64, device=dev), torch.zeros(a.batch, dtype=torch.uint8, device=dev),
+             torch.zeros(max(tot, 1), dtype=torch.int32, device=dev)) for _ in range(S)]
 
     def launch(k):
         d_blob, d_offs = d_in[k % R]
-        ix.match_batch_dev(a.batch, d_blob.data_ptr(), d_offs.data_ptr(), d_hit.data_ptr(), d_out.data_ptr(), tot,
-                           d_err.data_ptr(), s)
+        h_, e_, o_ = outs[k % S]
+        ix.match_batch_dev(a.batch, d_blob.data_ptr(), d_offs.data_ptr(), h_.data_ptr(), o_.data_ptr(), tot,
+                           e_.data_ptr(), streams[k % S].cuda_stream)
 
+    for k in range(S):   # every stream's workspace exists before the timed launches
+        launch(k)
+    torch.cuda.synchronize()
     launch(0)   # unprofiled: the profiled launches are enqueued behind a busy stream
     ix.profile(True)
     t = time.perf_counter()
@@ -87,9 +104,14 @@ def main():
     el = time.perf_counter() - t
     w, b, n = ix.profile_read()
     st = ix.stats()
-    print(f"{a.config}/{a.order}/filters-{a.filter_order} filters={len(fs)} batch={a.batch} rotate={R} hits<={tot} "
+    paths = [ix.debug_get(k) for k in (_native.TM_DEBUG_PATH_PHASES, _native.TM_DEBUG_PATH_SMALL,
+                                       _native.TM_DEBUG_PATH_ONE)]
+    assert not any(bool(e_.any().item()) for _, e_, _ in outs), "err flags set"
+    parked = ix.debug_get(_native.TM_DEBUG_DEFERRED_BLOCKS)
+    print(f"{a.config}/{a.order}/filters-{a.filter_order} streams={S} paths(phases,small,one)={paths} filters={len(fs)} batch={a.batch} rotate={R} hits<={tot} "
           f"wall/batch={el / a.batches * 1e3:.3f}ms walk={w / n:.4f}ms batch_dev={b / n:.4f}ms "
-          f"rate={a.batch * a.batches / el / 1e9:.3f}G/s device_MiB={st['device_bytes'] / 2**20:.0f}", flush=True)
+          f"rate={a.batch * a.batches / el / 1e9:.3f}G/s device_MiB={st['device_bytes'] / 2**20:.0f} "
+          f"parked_blocks={parked}", flush=True)
 
 
 if __name__ == "__main__":
