@@ -394,24 +394,31 @@ def main():
         if a.concurrency > 0:
             conc = []
             # (threads, deltas per ms from one more thread): without churn, then with
-            for nth, churn in ((a.concurrency, 0), (a.concurrency, 256), (2 * a.concurrency, 256)):
+            # (threads, deltas per ms from one more thread, mode): without churn, then with; mode 4: the
+            # u32-offset API the NIF calls (tm_match_batch32_ex), 0: the u64 one
+            for nth, churn, mode in ((a.concurrency, 0, 0), (a.concurrency, 0, 4), (a.concurrency, 256, 4),
+                                     (2 * a.concurrency, 256, 4)):
                 lb = min(4096, B)
                 sub = ts.slice(0, nth * lb)
                 hh, _, _ = ix.match_batch(sub.blob, sub.offs)
                 cap = int(np.diff(hh.astype(np.int64)).reshape(nth, lb).sum(axis=1).max()) + 65536
                 out = (ctypes.c_double * 6)()
-                rc = hb.tmb_callers(ix._h, nth, lb, _native._ptr(sub.blob), _native._ptr(sub.offs), cap, 1.0, churn,
-                                    out)
+                rc = hb.tmb_callers_ex(ix._h, nth, lb, _native._ptr(sub.blob), _native._ptr(sub.offs), cap, 1.0, churn,
+                                       mode, out)
                 assert rc == 0, rc
                 conc.append({"threads": nth, "topics_per_batch": lb, "batches": int(out[0]),
                              "topics_per_s": round(out[1], 1), "p50_ms": round(out[2], 4), "p99_ms": round(out[3], 4),
-                             "deltas_per_s": round(out[4], 1),
+                             "deltas_per_s": round(out[4], 1), "offsets": "u32" if mode == 4 else "u64",
                              "callers": "native threads, tm_host_alloc buffers each (in place)"})
         if B >= 65536:
             allt = wl.concat(tsets)
             out = (ctypes.c_double * 5)()
             iters = 24
             rc = hb.tmb_pipeline(ix._h, local, _native._ptr(allt.blob), _native._ptr(allt.offs), B, R, 3, iters, out)
+            assert rc == 0, rc
+            out32 = (ctypes.c_double * 5)()   # the same with u32 offsets both ways (tm_match_batch32_dev)
+            rc = hb.tmb_pipeline_ex(ix._h, local, _native._ptr(allt.blob), _native._ptr(allt.offs), B, R, 3, iters, 1,
+                                    out32)
             assert rc == 0, rc
             h2d, d2h = out[2], out[3]
             hostfed = {"topics_per_s": round(out[0], 1), "ms_per_batch": round(out[1], 4), "batch": B,
@@ -431,6 +438,13 @@ def main():
             if per > 0:
                 hostfed["pcie_bound_topics_per_s"] = round(B / per, 1)
                 hostfed["frac_of_pcie_bound"] = round(out[0] / (B / per), 3)
+            per32 = max(out32[2] / (pc[0] * 1e9), out32[3] / (pc[1] * 1e9)) if pc[0] > 0 and pc[1] > 0 else 0.0
+            hostfed["u32_offsets"] = {"topics_per_s": round(out32[0], 1), "ms_per_batch": round(out32[1], 4),
+                                      "h2d_MB_per_batch": round(out32[2] / 1e6, 2),
+                                      "d2h_MB_per_batch": round(out32[3] / 1e6, 2),
+                                      "pcie_bound_topics_per_s": round(B / per32, 1) if per32 else None,
+                                      "frac_of_pcie_bound": round(out32[0] / (B / per32), 3) if per32 else None,
+                                      "note": "tm_match_batch32_dev: u32 topic and hit offsets over PCIe"}
     if world > 1 and lat_native:
         # the slowest rank's percentiles (max over ranks); the caller and
         # host-fed legs are rank 0's (each rank drives its own GPU alike)
@@ -646,6 +660,8 @@ def host_bench_lib():
     lib.tmb_callers.argtypes = [vp, ctypes.c_int, u64, vp, vp, u64, ctypes.c_double, ctypes.c_int, dp]
     lib.tmb_callers_ex.argtypes = [vp, ctypes.c_int, u64, vp, vp, u64, ctypes.c_double, ctypes.c_int, ctypes.c_int, dp]
     lib.tmb_pipeline.argtypes = [vp, ctypes.c_int, vp, vp, u64, ctypes.c_int, ctypes.c_int, ctypes.c_int, dp]
+    lib.tmb_pipeline_ex.argtypes = [vp, ctypes.c_int, vp, vp, u64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                    ctypes.c_int, dp]
     lib.tmb_pcie.argtypes = [ctypes.c_int, u64, ctypes.c_int, ctypes.c_int, dp]
     lib.tmb_bind.argtypes = [vp]
     from emqx_amd import _native

@@ -13,7 +13,7 @@ void tmn_pool_init(tmn_pool *p, tm_index *h) {
 }
 
 static void set_free(tm_index *h, tmn_set *s) {
-    tmn_buf *all[] = {&s->blob, &s->offs, &s->hit, &s->vals, &s->err, &s->uniq};
+    tmn_buf *all[] = {&s->blob, &s->offs, &s->hit, &s->vals, &s->err, &s->uniq, &s->offs64};
     for (unsigned i = 0; i < sizeof all / sizeof all[0]; i++)
         if (all[i]->p) tm_host_free(h, all[i]->p);
     free(s);
@@ -59,21 +59,22 @@ void *tmn_get(tm_index *h, tmn_buf *b, uint64_t need) {
 int tmn_pack(tmn_set *s, tm_index *h, uint32_t n, const uint8_t *const *topics, const uint64_t *lens) {
     uint64_t tot = 0;
     for (uint32_t i = 0; i < n; i++) tot += lens[i];
+    if (tot > 0xFFFFFFFFull) return TM_EINVAL;
     uint8_t *blob = tmn_get(h, &s->blob, tot + 16);
-    uint64_t *offs = tmn_get(h, &s->offs, 8ull * (n + 1));
+    uint32_t *offs = tmn_get(h, &s->offs, 4ull * (n + 1));
     if (!blob || !offs) return TM_ENOMEM;
     tot = 0;
     for (uint32_t i = 0; i < n; i++) {
-        offs[i] = tot;
+        offs[i] = (uint32_t)tot;
         if (lens[i]) memcpy(blob + tot, topics[i], lens[i]);
         tot += lens[i];
     }
-    offs[n] = tot;
+    offs[n] = (uint32_t)tot;
     return TM_OK;
 }
 
 int tmn_match(tmn_set *s, tm_index *h, uint32_t n, uint32_t order) {
-    uint64_t *hit = tmn_get(h, &s->hit, 8ull * (n + 1));
+    uint32_t *hit = tmn_get(h, &s->hit, 4ull * (n + 1));
     uint8_t *err = tmn_get(h, &s->err, (uint64_t)n + 1);
     uint32_t *uniq = order == TM_ORDER_UNIQUE ? tmn_get(h, &s->uniq, 4ull * n + 4) : NULL;
     /* capacity: what the set already holds, at least TMN_IDS_PER_TOPIC ids per topic */
@@ -82,13 +83,13 @@ int tmn_match(tmn_set *s, tm_index *h, uint32_t n, uint32_t order) {
     uint32_t *vals = tmn_get(h, &s->vals, 4 * cap);
     if (!hit || !err || !vals || (order == TM_ORDER_UNIQUE && !uniq)) return TM_ENOMEM;
     cap = s->vals.cap / 4;
-    int rc = tm_match_batch_ex(h, n, s->blob.p, s->offs.p, hit, vals, cap, err, order, uniq);
+    int rc = tm_match_batch32_ex(h, n, s->blob.p, s->offs.p, hit, vals, cap, err, order, uniq);
     /* TM_ECAP: the offsets are valid, so rerun with room for every id (again
        if concurrent inserts grew the total in between; a few times at most) */
     for (int tries = 0; rc == TM_ECAP && tries < 4; tries++) {
         s->reruns++;
         vals = tmn_get(h, &s->vals, 4 * hit[n]);
-        rc = vals ? tm_match_batch_ex(h, n, s->blob.p, s->offs.p, hit, vals, s->vals.cap / 4, err, order, uniq)
+        rc = vals ? tm_match_batch32_ex(h, n, s->blob.p, s->offs.p, hit, vals, s->vals.cap / 4, err, order, uniq)
                   : TM_ENOMEM;
     }
     /* err flag 4 (a batch the device failed; the library runs it again and
@@ -102,12 +103,15 @@ int tmn_match(tmn_set *s, tm_index *h, uint32_t n, uint32_t order) {
 int tmn_first(tmn_set *s, tm_index *h, uint32_t n) {
     uint32_t *val = tmn_get(h, &s->vals, 4ull * n + 4);
     uint8_t *found = tmn_get(h, &s->err, (uint64_t)n + 1);
-    if (!val || !found) return TM_ENOMEM;
-    return tm_first_batch(h, n, s->blob.p, s->offs.p, val, found);
+    uint64_t *o64 = tmn_get(h, &s->offs64, 8ull * (n + 1));
+    if (!val || !found || !o64) return TM_ENOMEM;
+    const uint32_t *o32 = s->offs.p;
+    for (uint32_t i = 0; i <= n; i++) o64[i] = o32[i];   /* tm_first_batch takes u64 offsets */
+    return tm_first_batch(h, n, s->blob.p, o64, val, found);
 }
 
 int tmn_row(const tmn_set *s, uint32_t n, uint32_t order, uint32_t i, uint64_t *b, uint64_t *e) {
-    const uint64_t *hit = s->hit.p;
+    const uint32_t *hit = s->hit.p;
     const uint8_t *err = s->err.p;
     (void)n;
     *b = *e = 0;

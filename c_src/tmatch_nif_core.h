@@ -29,7 +29,8 @@ extern "C" {
 typedef struct { void *p; uint64_t cap; } tmn_buf;
 
 typedef struct tmn_set {         /* one caller's batch buffers (tm_host_alloc: the batch runs in place) */
-    tmn_buf blob, offs, hit, vals, err, uniq;
+    tmn_buf blob, offs, hit, vals, err, uniq;   /* offs, hit: u32 (tm_match_batch32_ex) */
+    tmn_buf offs64;                              /* tm_first_batch's u64 offsets */
     uint64_t reruns;             /* batches rerun after TM_ECAP (diagnostics) */
     struct tmn_set *next;
 } tmn_set;
@@ -50,10 +51,13 @@ void tmn_give(tmn_pool *p, tmn_set *s);  /* back to the pool, or freed beyond TM
 void *tmn_get(tm_index *h, tmn_buf *b, uint64_t need);
 
 /* Topic i is topics[i][0 .. lens[i]).  Packs them into the set's pinned blob
- * (16-byte aligned, as the in-place path needs) and offsets. */
+ * (16-byte aligned, as the in-place path needs) and u32 offsets (TM_EINVAL if
+ * the topics exceed 2^32 bytes: never for a broker micro-batch). */
 int tmn_pack(tmn_set *s, tm_index *h, uint32_t n, const uint8_t *const *topics, const uint64_t *lens);
 
-/* matches/3 for the packed batch in `order` (TM_ORDER_*): sizes the value
+/* matches/3 for the packed batch in `order` (TM_ORDER_*) through
+ * tm_match_batch32_ex -- u32 offsets in and out, half the offset bytes of the
+ * in-place batch over PCIe each way: sizes the value
  * buffer from what the set already holds (>= TMN_IDS_PER_TOPIC per topic), and
  * on TM_ECAP (offsets valid, values truncated) grows it to the exact total
  * and runs the batch again.  TM_EDEVICE: the device failed the batch (the

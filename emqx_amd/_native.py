@@ -25,7 +25,8 @@ EXPORTS = ("tm_create", "tm_destroy", "tm_apply_deltas", "tm_sync", "tm_match_ba
            "tm_last_error", "tm_abi_version", "tm_merge_shards", "tm_host_alloc", "tm_host_free",
            "tm_stream_release", "tm_match_batch_ex", "tm_match_batch_dev_ex", "tm_sort_segments",
            "tm_matches_filter", "tm_apply_deltas_ex", "tm_read_begin", "tm_read_end", "tm_epoch",
-           "tm_create_replicas", "tm_replica_stats", "tm_debug_set", "tm_debug_get")
+           "tm_create_replicas", "tm_replica_stats", "tm_debug_set", "tm_debug_get", "tm_match_batch32_ex",
+           "tm_match_batch32_dev")
 TM_DEBUG_LB_SPINS, TM_DEBUG_LB_FAIL_BLOCK, TM_DEBUG_LB_LAUNCHES, TM_DEBUG_PHASES = 1, 2, 3, 4
 TM_DEBUG_FAILED_BATCHES, TM_DEBUG_RETRIED_BATCHES = 5, 6
 TM_DEBUG_PATH_PHASES, TM_DEBUG_PATH_SMALL, TM_DEBUG_PATH_ONE = 7, 8, 9
@@ -101,6 +102,8 @@ def load_library(path: Path | None = None):
         "tm_epoch": (i32, [vp, C.POINTER(u64), C.POINTER(u64)]),
         "tm_create_replicas": (i32, [C.POINTER(tm_options), C.POINTER(C.c_int32), u32, C.POINTER(vp)]),
         "tm_replica_stats": (i32, [vp, u32, C.POINTER(u64), C.POINTER(C.c_int32)]),
+        "tm_match_batch32_ex": (i32, [vp, u64, vp, vp, vp, vp, u64, vp, u32, vp]),
+        "tm_match_batch32_dev": (i32, [vp, u64, vp, vp, vp, vp, u64, vp, vp]),
         "tm_debug_set": (i32, [vp, u32, u64]),
         "tm_debug_get": (i32, [vp, u32, C.POINTER(u64)]),
     }
@@ -277,6 +280,24 @@ class Index:
                 continue
             self._check(rc)
             return hit, out[: int(hit[n])], err[:n]
+
+    def match_batch32(self, blob: np.ndarray, offs: np.ndarray, out, order: int = TM_ORDER_TRAVERSAL,
+                      unique_counts: np.ndarray | None = None):
+        """tm_match_batch32_ex: u32 topic offsets in, u32 hit offsets out.
+        out = (hit u32[>= n+1], values u32[cap], err u8[>= n]); in place when
+        every buffer comes from host_array() (a NIF's pooled buffers).  Raises
+        TmError(TM_ECAP) when the values do not fit (hit offsets valid)."""
+        n = len(offs) - 1
+        hit, vals, err = out
+        if offs.dtype != np.uint32 or hit.dtype != np.uint32 or len(hit) < n + 1 or len(err) < n:
+            raise ValueError("match_batch32: u32 offsets and large enough outputs expected")
+        self._check(self._lib.tm_match_batch32_ex(self._h, n, _ptr(blob), _ptr(offs), _ptr(hit), _ptr(vals), len(vals),
+                                                  _ptr(err), order, _ptr(unique_counts)))
+        return hit[: n + 1], vals[: int(hit[n])], err[:n]
+
+    def match_batch32_dev(self, n: int, d_blob: int, d_offs: int, d_hit: int, d_out: int, cap: int, d_err: int,
+                          stream: int | None = None):
+        self._check(self._lib.tm_match_batch32_dev(self._h, n, d_blob, d_offs, d_hit, d_out, cap, d_err, stream))
 
     def first_batch(self, blob: np.ndarray, offs: np.ndarray):
         """-> (value u32[n], found u8[n]: 1 hit, 0 none, 2 badarg, 3 > 65536 levels)."""

@@ -37,6 +37,10 @@ int (*match_batch_dev)(tm_index *, uint64_t, const uint8_t *, const uint64_t *, 
 int (*apply_deltas)(tm_index *, uint64_t, const uint8_t *, const uint8_t *, const uint64_t *, const uint32_t *,
                     const uint8_t *);
 int (*stream_release)(tm_index *, void *);
+int (*match_batch32)(tm_index *, uint64_t, const uint8_t *, const uint32_t *, uint32_t *, uint32_t *, uint64_t,
+                     uint8_t *, uint32_t, uint32_t *);
+int (*match_batch32_dev)(tm_index *, uint64_t, const uint8_t *, const uint32_t *, uint32_t *, uint32_t *, uint64_t,
+                         uint8_t *, void *);
 }  // namespace api
 
 namespace {
@@ -54,16 +58,19 @@ struct Caller {
     tm_index *h;
     uint64_t n, cap;
     uint8_t *blob = nullptr; uint64_t *offs = nullptr, *hit = nullptr; uint32_t *vals = nullptr; uint8_t *err = nullptr;
+    uint32_t *offs32 = nullptr, *hit32 = nullptr;   // mode 4: tm_match_batch32_ex (u32 offsets)
     int init(tm_index *ix, uint64_t nt, const uint8_t *tb, const uint64_t *to, uint64_t first, uint64_t cap_) {
         h = ix; n = nt; cap = cap_;
         const uint64_t b0 = to[first], nb = to[first + nt] - b0;
         int rc;
         if ((rc = api::host_alloc(h, nb + 16, (void **)&blob)) || (rc = api::host_alloc(h, 8 * (nt + 1), (void **)&offs)) ||
             (rc = api::host_alloc(h, 8 * (nt + 1), (void **)&hit)) || (rc = api::host_alloc(h, 4 * cap, (void **)&vals)) ||
-            (rc = api::host_alloc(h, nt + 1, (void **)&err)))
+            (rc = api::host_alloc(h, nt + 1, (void **)&err)) || (rc = api::host_alloc(h, 4 * (nt + 1), (void **)&offs32)) ||
+            (rc = api::host_alloc(h, 4 * (nt + 1), (void **)&hit32)))
             return rc;
         memcpy(blob, tb + b0, nb);
         for (uint64_t i = 0; i <= nt; i++) offs[i] = to[first + i] - b0;
+        for (uint64_t i = 0; i <= nt; i++) offs32[i] = (uint32_t)offs[i];
         return TM_OK;
     }
     // device mode: the same batch copied into HBM once, run through the device
@@ -88,6 +95,7 @@ struct Caller {
         return hipHostGetDevicePointer(&d, hp, 0) == hipSuccess ? static_cast<T *>(d) : nullptr;
     }
     int run() {
+        if (mode == 4) return api::match_batch32(h, n, blob, offs32, hit32, vals, cap, err, TM_ORDER_TRAVERSAL, nullptr);
         if (!s) return api::match_batch(h, n, blob, offs, hit, vals, cap, err);
         const bool hin = mode == 3, hout = mode == 2;
         int rc = api::match_batch_dev(h, n, hin ? mapped(blob) : dblob, hin ? mapped(offs) : doffs,
@@ -97,7 +105,8 @@ struct Caller {
         return hipStreamSynchronize(s) == hipSuccess ? TM_OK : TM_EDEVICE;
     }
     void fini() {
-        for (void *p : {(void *)blob, (void *)offs, (void *)hit, (void *)vals, (void *)err}) if (p) api::host_free(h, p);
+        for (void *p : {(void *)blob, (void *)offs, (void *)hit, (void *)vals, (void *)err, (void *)offs32, (void *)hit32})
+            if (p) api::host_free(h, p);
         if (s) {
             for (void *p : {(void *)dblob, (void *)doffs, (void *)dhit, (void *)dvals, (void *)derr}) if (p) (void)hipFree(p);
             api::stream_release(h, s);
@@ -118,8 +127,10 @@ int tmb_bind(void *lib) {
     api::match_batch_dev = reinterpret_cast<decltype(api::match_batch_dev)>(dlsym(lib, "tm_match_batch_dev"));
     api::apply_deltas = reinterpret_cast<decltype(api::apply_deltas)>(dlsym(lib, "tm_apply_deltas"));
     api::stream_release = reinterpret_cast<decltype(api::stream_release)>(dlsym(lib, "tm_stream_release"));
+    api::match_batch32 = reinterpret_cast<decltype(api::match_batch32)>(dlsym(lib, "tm_match_batch32_ex"));
+    api::match_batch32_dev = reinterpret_cast<decltype(api::match_batch32_dev)>(dlsym(lib, "tm_match_batch32_dev"));
     return api::host_alloc && api::host_free && api::match_batch && api::match_batch_dev && api::apply_deltas &&
-                   api::stream_release ? 0 : -1;
+                   api::stream_release && api::match_batch32 && api::match_batch32_dev ? 0 : -1;
 }
 
 // out: [p50_ms, p99_ms, mean_ms]
@@ -149,7 +160,8 @@ int tmb_single(tm_index *h, uint64_t n, const uint8_t *tb, const uint64_t *to, u
 // caller's batch lives in HBM and goes through tm_match_batch_dev on its own
 // stream (what the device can take without the PCIe leg of in-place batches);
 // 2: inputs in HBM, outputs written into the mapped host buffers; 3: inputs
-// read from the mapped host buffers, outputs in HBM.
+// read from the mapped host buffers, outputs in HBM; 4: in place with u32
+// offsets (tm_match_batch32_ex, what the NIF calls).
 // out: [batches, topics_per_s, p50_ms, p99_ms, deltas_per_s, seconds]
 int tmb_callers_ex(tm_index *h, int nthreads, uint64_t n, const uint8_t *tb, const uint64_t *to, uint64_t cap,
                    double seconds, int churn_ops, int device_buffers, double *out) {
@@ -157,7 +169,7 @@ int tmb_callers_ex(tm_index *h, int nthreads, uint64_t n, const uint8_t *tb, con
     for (int k = 0; k < nthreads; k++) {
         int rc = cs[k].init(h, n, tb, to, (uint64_t)k * n, cap);
         if (rc) return rc;
-        if (device_buffers && (rc = cs[k].to_device())) return rc;
+        if (device_buffers && device_buffers != 4 && (rc = cs[k].to_device())) return rc;
         cs[k].mode = device_buffers;
         if ((rc = cs[k].run())) return rc;   // warm: lane, workspace
     }
@@ -230,22 +242,34 @@ int tmb_callers(tm_index *h, int nthreads, uint64_t n, const uint8_t *tb, const 
 // values into pinned host buffers of that stream; before a stream's buffers
 // are reused the host waits for its previous batch.
 // out: [topics_per_s, ms_per_batch, h2d_bytes_per_batch, d2h_bytes_per_batch, seconds]
-int tmb_pipeline(tm_index *h, int device, const uint8_t *tb, const uint64_t *to, uint64_t n, int R, int nstreams,
-                 int iters, double *out) {
+// u32 != 0: the same with 32-bit offsets both ways (tm_match_batch32_dev):
+// 4 B per topic less over PCIe in each direction.
+int tmb_pipeline_ex(tm_index *h, int device, const uint8_t *tb, const uint64_t *to, uint64_t n, int R, int nstreams,
+                    int iters, int u32, double *out) {
     if (hipSetDevice(device) != hipSuccess) return TM_EDEVICE;
     struct HostBatch { uint8_t *p; uint64_t bytes, total; };
     std::vector<HostBatch> hb(R);
     uint64_t maxb = 0;
+    const uint64_t ow = u32 ? 4 : 8;   // offset width
+    const uint64_t boff = ((n + 1) * ow + 15) & ~15ull;
     for (int k = 0; k < R; k++) {
         const uint64_t b0 = to[(uint64_t)k * n], nb = to[(uint64_t)(k + 1) * n] - b0;
-        const uint64_t boff = ((n + 1) * 8 + 15) & ~15ull;
         hb[k].bytes = boff + nb;
         if (hipHostMalloc(&hb[k].p, hb[k].bytes + 16, hipHostMallocDefault) != hipSuccess) return TM_ENOMEM;
-        uint64_t *o = reinterpret_cast<uint64_t *>(hb[k].p);
-        for (uint64_t i = 0; i <= n; i++) o[i] = to[(uint64_t)k * n + i] - b0;
+        for (uint64_t i = 0; i <= n; i++) {
+            const uint64_t v = to[(uint64_t)k * n + i] - b0;
+            if (u32) reinterpret_cast<uint32_t *>(hb[k].p)[i] = (uint32_t)v;
+            else reinterpret_cast<uint64_t *>(hb[k].p)[i] = v;
+        }
         memcpy(hb[k].p + boff, tb + b0, nb);
         maxb = std::max(maxb, hb[k].bytes);
     }
+    auto match = [&](uint8_t *d_in, void *d_hit, uint32_t *d_vals, uint64_t cap, uint8_t *d_err, hipStream_t s) {
+        return u32 ? api::match_batch32_dev(h, n, d_in + boff, reinterpret_cast<uint32_t *>(d_in),
+                                            static_cast<uint32_t *>(d_hit), d_vals, cap, d_err, s)
+                   : api::match_batch_dev(h, n, d_in + boff, reinterpret_cast<uint64_t *>(d_in),
+                                          static_cast<uint64_t *>(d_hit), d_vals, cap, d_err, s);
+    };
     struct Lane { hipStream_t s; hipEvent_t done; uint8_t *d_in; uint64_t *d_hit; uint32_t *d_vals; uint8_t *d_err;
                   uint64_t *h_hit; uint32_t *h_vals; bool busy; };
     std::vector<Lane> ls(nstreams);
@@ -262,14 +286,12 @@ int tmb_pipeline(tm_index *h, int device, const uint8_t *tb, const uint64_t *to,
     {
         Lane &l = ls[0];
         for (int k = 0; k < R; k++) {
-            const uint64_t boff = ((n + 1) * 8 + 15) & ~15ull;
             hipMemcpyAsync(l.d_in, hb[k].p, hb[k].bytes, hipMemcpyHostToDevice, l.s);
-            int rc = api::match_batch_dev(h, n, l.d_in + boff, reinterpret_cast<uint64_t *>(l.d_in), l.d_hit, nullptr, 0,
-                                        l.d_err, l.s);
+            int rc = match(l.d_in, l.d_hit, nullptr, 0, l.d_err, l.s);
             if (rc) return rc;
-            hipMemcpyAsync(l.h_hit, l.d_hit, 8 * (n + 1), hipMemcpyDeviceToHost, l.s);
+            hipMemcpyAsync(l.h_hit, l.d_hit, ow * (n + 1), hipMemcpyDeviceToHost, l.s);
             hipStreamSynchronize(l.s);
-            hb[k].total = l.h_hit[n];
+            hb[k].total = u32 ? reinterpret_cast<uint32_t *>(l.h_hit)[n] : l.h_hit[n];
             cap = std::max(cap, hb[k].total);
         }
     }
@@ -280,17 +302,15 @@ int tmb_pipeline(tm_index *h, int device, const uint8_t *tb, const uint64_t *to,
     double h2d = 0, d2h = 0;
     auto issue = [&](int k, Lane &l) -> int {
         const HostBatch &b = hb[k % R];
-        const uint64_t boff = ((n + 1) * 8 + 15) & ~15ull;
         if (hipMemcpyAsync(l.d_in, b.p, b.bytes, hipMemcpyHostToDevice, l.s) != hipSuccess) return TM_EDEVICE;
-        int rc = api::match_batch_dev(h, n, l.d_in + boff, reinterpret_cast<uint64_t *>(l.d_in), l.d_hit, l.d_vals, cap,
-                                    l.d_err, l.s);
+        int rc = match(l.d_in, l.d_hit, l.d_vals, cap, l.d_err, l.s);
         if (rc) return rc;
-        if (hipMemcpyAsync(l.h_hit, l.d_hit, 8 * (n + 1), hipMemcpyDeviceToHost, l.s) != hipSuccess ||
+        if (hipMemcpyAsync(l.h_hit, l.d_hit, ow * (n + 1), hipMemcpyDeviceToHost, l.s) != hipSuccess ||
             hipMemcpyAsync(l.h_vals, l.d_vals, 4 * b.total, hipMemcpyDeviceToHost, l.s) != hipSuccess ||
             hipEventRecord(l.done, l.s) != hipSuccess)
             return TM_EDEVICE;
         h2d += b.bytes;
-        d2h += 8.0 * (n + 1) + 4.0 * b.total;
+        d2h += (double)ow * (n + 1) + 4.0 * b.total;
         l.busy = true;
         return TM_OK;
     };
@@ -320,6 +340,11 @@ int tmb_pipeline(tm_index *h, int device, const uint8_t *tb, const uint64_t *to,
     out[3] = d2h / iters;
     out[4] = el;
     return TM_OK;
+}
+
+int tmb_pipeline(tm_index *h, int device, const uint8_t *tb, const uint64_t *to, uint64_t n, int R, int nstreams,
+                 int iters, double *out) {
+    return tmb_pipeline_ex(h, device, tb, to, n, R, nstreams, iters, 0, out);
 }
 
 // The PCIe ceiling the host-fed pipeline runs against: pinned-host <-> HBM

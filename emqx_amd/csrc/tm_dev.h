@@ -137,6 +137,13 @@ hipError_t launch_match(const DevIndex &ix, const Workspace &ws, uint64_t n, con
                         const uint64_t *offs, uint64_t *hit_offs, uint8_t *err, uint32_t *out, uint64_t cap,
                         uint32_t tag, LbCtl lb, bool phases, hipStream_t s, hipEvent_t ev_walk0 = nullptr,
                         hipEvent_t ev_walk1 = nullptr, int *path = nullptr);
+// The one-launch small batch with 32-bit offsets in and out (hipErrorInvalidValue
+// if small_path_ok refuses the batch), and the 32 <-> 64-bit offset copies
+hipError_t launch_match32(const DevIndex &ix, const Workspace &ws, uint64_t n, const uint8_t *bytes,
+                          const uint32_t *offs, uint32_t *hit_offs, uint8_t *err, uint32_t *out, uint64_t cap,
+                          uint32_t tag, LbCtl lb, hipStream_t s);
+hipError_t launch_offs_widen(const uint32_t *in, uint64_t *out, uint64_t m, hipStream_t s);
+hipError_t launch_offs_narrow(const uint64_t *in, uint32_t *out, uint64_t m, hipStream_t s);
 hipError_t launch_first(const DevIndex &ix, const Workspace &ws, uint64_t n, const uint8_t *bytes,
                         const uint64_t *offs, uint32_t *out_value, uint8_t *out_found, hipStream_t s);
 // filter-sharded merge of allgathered per-shard CSR hit lists (k_merge_shards)

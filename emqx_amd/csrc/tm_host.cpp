@@ -110,6 +110,7 @@ struct Lane {
     uint8_t *d_res = nullptr; uint64_t d_res_cap = 0;
     uint32_t *pin_vals = nullptr, *pin_vals_dev = nullptr; uint64_t pin_vals_cap = 0;
     uint32_t *d_vals = nullptr; uint64_t d_vals_cap = 0;   // sorted output: values sorted in HBM first
+    uint64_t *d_o64 = nullptr, *d_h64 = nullptr; uint64_t d_o64_cap = 0, d_h64_cap = 0;   // 32-bit device API: widened offsets
 };
 
 // Patch log: a ring of the last PATCH_RING patches (numbered 1, 2, ... in the
@@ -1392,7 +1393,7 @@ void free_workspace(Workspace &w) {
 
 void free_lane(Lane &l) {
     free_workspace(l.w);
-    void *dv[] = {l.d_in, l.d_res, l.d_vals};
+    void *dv[] = {l.d_in, l.d_res, l.d_vals, l.d_o64, l.d_h64};
     for (void *p : dv) if (p) (void)hipFree(p);
     void *pins[] = {l.pin_in, l.pin_out, l.pin_vals};
     for (void *p : pins) if (p) (void)hipHostFree(p);
@@ -1611,7 +1612,7 @@ int drain_lanes(tm_index *ix) {
 
 extern "C" {
 
-uint32_t tm_abi_version(void) { return (1u << 16) | 6u; }
+uint32_t tm_abi_version(void) { return (1u << 16) | 7u; }
 
 const char *tm_last_error(tm_index *) { return g_last_error.c_str(); }
 
@@ -2123,6 +2124,112 @@ int tm_match_batch_ex(tm_index *ix, uint64_t n, const uint8_t *tb, const uint64_
 int tm_match_batch(tm_index *ix, uint64_t n, const uint8_t *tb, const uint64_t *to, uint64_t *out_hit,
                    uint32_t *out_vals, uint64_t cap, uint8_t *out_err) {
     return tm_match_batch_ex(ix, n, tb, to, out_hit, out_vals, cap, out_err, TM_ORDER_TRAVERSAL, nullptr);
+}
+
+// 32-bit offsets (include/tmatch.h).  An in-place batch the one-launch small
+// kernel takes runs on 32-bit offsets end to end (k_walk_small<.., uint32_t>):
+// half the offset bytes cross PCIe in each direction.  Any other batch is
+// widened on the host, matched as tm_match_batch_ex, and narrowed.
+int tm_match_batch32_ex(tm_index *ix, uint64_t n, const uint8_t *tb, const uint32_t *to, uint32_t *out_hit,
+                        uint32_t *out_vals, uint64_t cap, uint8_t *out_err, uint32_t order, uint32_t *out_unique) {
+    if (!ix) return fail(nullptr, TM_EINVAL, "tm_match_batch32: null handle");
+    if (!to || !out_hit || (n && !tb && to[n] != to[0])) return fail(ix, TM_EINVAL, "tm_match_batch32: null buffer");
+    if (n >= 0xFFFFFFFFull) return fail(ix, TM_EINVAL, "tm_match_batch32: batch too large");
+    if (order > TM_ORDER_UNIQUE) return fail(ix, TM_EINVAL, "tm_match_batch32: bad order");
+    if (cap > 0xFFFFFFFFull) cap = 0xFFFFFFFFull;   // (a 32-bit offset addresses no more)
+    if (n && n <= ZC_TOPICS && order == TM_ORDER_TRAVERSAL && ((uintptr_t)tb & 15) == 0) {
+        std::unique_lock<std::mutex> g(ix->mu);
+        const uint64_t nbytes = to[n];
+        uint8_t *db = nbytes ? pinned_dev(ix, tb, nbytes) : nullptr;
+        uint8_t *dof = pinned_dev(ix, to, (n + 1) * 4);
+        uint8_t *dh = pinned_dev(ix, out_hit, (n + 1) * 4);
+        uint8_t *dv = out_vals ? pinned_dev(ix, out_vals, cap * 4) : nullptr;
+        uint8_t *de = out_err ? pinned_dev(ix, out_err, n) : nullptr;
+        if ((db || !nbytes) && dof && dh && (dv || !out_vals) && (de || !out_err)) {
+            LaneLease lease{ix, g};
+            int rc;
+            if ((rc = host_lane(ix, g, lease.ln))) return rc;
+            Lane &ln = *lease.ln;
+            const hipStream_t s = ln.s;
+            if ((rc = sync_locked(ix, ln.r, s))) return rc;
+            if ((rc = ensure_ws(ix, n, ln))) return rc;
+            if (small_path_ok(dev_view(ix, ln.r), n)) {
+                ix->rep[ln.r].batches++;
+                if (!de && (rc = stage_out(ix, ln, n, n, de))) return rc;   // flags nobody reads still need a home
+                for (int tries = 0;; tries++) {
+                    const DevIndex d = dev_view(ix, ln.r);
+                    uint32_t tag;
+                    if ((rc = next_tag(ix, ln, s, tag))) return rc;
+                    HIPCHK(ix, launch_match32(d, ln.w, n, db ? db : dof, reinterpret_cast<const uint32_t *>(dof),
+                                              reinterpret_cast<uint32_t *>(dh), de, reinterpret_cast<uint32_t *>(dv),
+                                              dv ? cap : 0, tag, next_lb(ix), s));
+                    ix->path_batches[PATH_SMALL]++;
+                    if ((rc = batch_done(ix, ln))) return rc;
+                    g.unlock();
+                    HIPCHK(ix, hipStreamSynchronize(s));
+                    if (!batch_failed(ix, ln)) break;
+                    if ((rc = retry_or_fail(ix, g, ln, tries))) return rc;
+                }
+                return (out_vals && out_hit[n] > cap) ? TM_ECAP : TM_OK;
+            }
+        }
+    }
+    // widened: the 64-bit path, then the offsets narrowed
+    std::vector<uint64_t> o64, h64;
+    try {
+        o64.assign(to, to + n + 1);
+        h64.resize(n + 1);
+    } catch (const std::bad_alloc &) {
+        return fail(ix, TM_ENOMEM, "tm_match_batch32: out of host memory");
+    }
+    const int rc = tm_match_batch_ex(ix, n, tb, o64.data(), h64.data(), out_vals, cap, out_err, order, out_unique);
+    if (rc != TM_OK && rc != TM_ECAP) return rc;
+    if (h64[n] > 0xFFFFFFFFull) return fail(ix, TM_EINVAL, "tm_match_batch32: more than 2^32 - 1 values");
+    for (uint64_t i = 0; i <= n; i++) out_hit[i] = (uint32_t)h64[i];
+    return rc;
+}
+
+int tm_match_batch32_dev(tm_index *ix, uint64_t n, const uint8_t *bytes, const uint32_t *offs, uint32_t *hit_offs,
+                         uint32_t *out, uint64_t cap, uint8_t *err, void *stream) {
+    if (!ix) return fail(nullptr, TM_EINVAL, "tm_match_batch32_dev: null handle");
+    if (!hit_offs || (n && (!offs || !bytes || !err))) return fail(ix, TM_EINVAL, "tm_match_batch32_dev: null buffer");
+    if (n >= 0xFFFFFFFFull) return fail(ix, TM_EINVAL, "tm_match_batch32_dev: batch too large");
+    if (cap > 0xFFFFFFFFull) cap = 0xFFFFFFFFull;
+    std::lock_guard<std::mutex> g(ix->mu);
+    hipStream_t s = pick_stream(ix, stream);
+    int rc, grp = 0;
+    Lane *ln;
+    if ((rc = dev_group(ix, grp))) return rc;
+    if ((rc = collect_patch(ix))) return rc;
+    const int r = pick_copy(ix, grp, nullptr);
+    ix->rep[r].last_use = ++ix->tick;
+    ix->rep[r].batches++;
+    if ((rc = dev_lane(ix, s, r, ln))) return rc;
+    if ((rc = sync_locked(ix, ln->r, s))) return rc;
+    if ((rc = ensure_ws(ix, n, *ln))) return rc;
+    const DevIndex d = dev_view(ix, ln->r);
+    tm_index::ProfEv ev;
+    if ((rc = prof_begin(ix, ev, s))) return rc;
+    uint32_t tag;
+    if ((rc = next_tag(ix, *ln, s, tag))) return rc;
+    if (small_path_ok(d, n)) {
+        if (ev.w0) HIPCHK(ix, hipEventRecord(ev.w0, s));
+        HIPCHK(ix, launch_match32(d, ln->w, n, bytes, offs, hit_offs, err, out, out ? cap : 0, tag, next_lb(ix), s));
+        if (ev.w1) HIPCHK(ix, hipEventRecord(ev.w1, s));
+        ix->path_batches[PATH_SMALL]++;
+    } else {
+        // widened into the lane's scratch, matched, narrowed into the caller's offsets
+        if ((rc = grow_dev(ix, s, ln->d_o64, ln->d_o64_cap, n + 1))) return rc;
+        if ((rc = grow_dev(ix, s, ln->d_h64, ln->d_h64_cap, n + 1))) return rc;
+        HIPCHK(ix, launch_offs_widen(offs, ln->d_o64, n + 1, s));
+        int path = PATH_PHASES;
+        HIPCHK(ix, launch_match(d, ln->w, n, bytes, ln->d_o64, ln->d_h64, err, out, out ? cap : 0, tag, next_lb(ix),
+                                ix->dbg_phases, s, ev.w0, ev.w1, &path));
+        ix->path_batches[path]++;
+        HIPCHK(ix, launch_offs_narrow(ln->d_h64, hit_offs, n + 1, s));
+    }
+    if ((rc = batch_done(ix, *ln))) return rc;
+    return prof_end(ix, ev, s);
 }
 
 int tm_first_batch(tm_index *ix, uint64_t n, const uint8_t *tb, const uint64_t *to, uint32_t *out_value,

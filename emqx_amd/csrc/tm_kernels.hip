@@ -1129,9 +1129,12 @@ bool one_pass_ok(const DevIndex &ix) {
     return !ix.hdesc && ix.depth + 2 <= (uint32_t)FAST_L && ix.xlen_max <= (uint32_t)FAST_L;
 }
 
-template <int MODE>
+// OT: the offsets' type, in and out -- uint64_t (tm_match_batch*), or uint32_t
+// (tm_match_batch32*: half the offset bytes of an in-place host batch cross
+// PCIe in each direction)
+template <int MODE, class OT>
 __global__ __launch_bounds__(WV_BLOCK) void k_walk_small(DevIndex ix, Workspace ws, uint64_t n, const uint8_t *blob,
-                                                         const uint64_t *offs, Outs o, uint64_t *hit_offs,
+                                                         const OT *offs, Outs o, OT *hit_offs,
                                                          uint32_t *out, uint64_t cap, uint32_t tag, LbCtl lb) {
     constexpr int W = WAVE_W;
     constexpr uint32_t G = 64 / W;                        // topics per wave
@@ -1374,7 +1377,7 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_small(DevIndex ix, Workspace 
             s_base = pre;
             if (fail) ws.hint_d[HINT_FAIL] = 1;
             if (vb == gridDim.x - 1) {
-                if (!fail) hit_offs[n] = pre + sum;
+                if (!fail) hit_offs[n] = (OT)(pre + sum);
                 ws.list_n[L_COUNT + 4] = 0;   // every ticket is taken
             }
         }
@@ -1384,7 +1387,7 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_small(DevIndex ix, Workspace 
     if (threadIdx.x < SM_TOPICS && (uint64_t)vb * SM_TOPICS + threadIdx.x < n) {
         uint64_t p = s_base;
         for (uint32_t i = 0; i < threadIdx.x; i++) p += s_cnt[i];
-        hit_offs[(uint64_t)vb * SM_TOPICS + threadIdx.x] = p;
+        hit_offs[(uint64_t)vb * SM_TOPICS + threadIdx.x] = (OT)p;
         o.err[(uint64_t)vb * SM_TOPICS + threadIdx.x] = s_fail ? 4 : s_err[threadIdx.x];
     }
     if (s_fail) return;   // (block-uniform)
@@ -2337,8 +2340,8 @@ hipError_t launch_match(const DevIndex &ix, const Workspace &ws, uint64_t n, con
         Outs o{err, nullptr, nullptr};
         if (ev_walk0 && (e = hipEventRecord(ev_walk0, s)) != hipSuccess) return e;
         if (n <= SMALL_TOPICS)
-            hipLaunchKernelGGL(k_walk_small<MODE_COUNT>, dim3(blocks_for(n, SM_TOPICS)), dim3(WV_BLOCK), 0, s, ix, ws,
-                               n, bytes, offs, o, hit_offs, out, cap, tag & LB_TAG_MASK, lb);
+            hipLaunchKernelGGL((k_walk_small<MODE_COUNT, uint64_t>), dim3(blocks_for(n, SM_TOPICS)), dim3(WV_BLOCK), 0,
+                               s, ix, ws, n, bytes, offs, o, hit_offs, out, cap, tag & LB_TAG_MASK, lb);
         if (n > SMALL_TOPICS) {
             const OneArgs a{n, bytes, offs, ws.look, err, hit_offs, out, cap, ws.cnt, ws.nr, ws.rng,
                             tag & LB_TAG_MASK, lb};
@@ -2357,13 +2360,44 @@ hipError_t launch_match(const DevIndex &ix, const Workspace &ws, uint64_t n, con
     return launch_match_phase2(ix, ws, n, bytes, offs, hit_offs, out, cap, s);
 }
 
+hipError_t launch_match32(const DevIndex &ix, const Workspace &ws, uint64_t n, const uint8_t *bytes,
+                          const uint32_t *offs, uint32_t *hit_offs, uint8_t *err, uint32_t *out, uint64_t cap,
+                          uint32_t tag, LbCtl lb, hipStream_t s) {
+    if (!small_path_ok(ix, n)) return hipErrorInvalidValue;   // (the caller converts instead)
+    Outs o{err, nullptr, nullptr};
+    hipLaunchKernelGGL((k_walk_small<MODE_COUNT, uint32_t>), dim3(blocks_for(n, SM_TOPICS)), dim3(WV_BLOCK), 0, s, ix,
+                       ws, n, bytes, offs, o, hit_offs, out, cap, tag & LB_TAG_MASK, lb);
+    return hipGetLastError();
+}
+
+// 32-bit offsets <-> the 64-bit ones every other kernel takes (tm_match_batch32_dev
+// on a batch the one-launch small kernel does not take)
+__global__ __launch_bounds__(256) void k_offs_widen(const uint32_t *in, uint64_t *out, uint64_t m) {
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < m; i += (uint64_t)gridDim.x * 256) out[i] = in[i];
+}
+__global__ __launch_bounds__(256) void k_offs_narrow(const uint64_t *in, uint32_t *out, uint64_t m) {
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < m; i += (uint64_t)gridDim.x * 256)
+        out[i] = in[i] > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)in[i];
+}
+
+hipError_t launch_offs_widen(const uint32_t *in, uint64_t *out, uint64_t m, hipStream_t s) {
+    const uint32_t g = blocks_for(m, 256) < 4096 ? blocks_for(m, 256) : 4096;
+    hipLaunchKernelGGL(k_offs_widen, dim3(g), dim3(256), 0, s, in, out, m);
+    return hipGetLastError();
+}
+hipError_t launch_offs_narrow(const uint64_t *in, uint32_t *out, uint64_t m, hipStream_t s) {
+    const uint32_t g = blocks_for(m, 256) < 4096 ? blocks_for(m, 256) : 4096;
+    hipLaunchKernelGGL(k_offs_narrow, dim3(g), dim3(256), 0, s, in, out, m);
+    return hipGetLastError();
+}
+
 hipError_t launch_first(const DevIndex &ix, const Workspace &ws, uint64_t n, const uint8_t *bytes,
                         const uint64_t *offs, uint32_t *out_value, uint8_t *out_found, hipStream_t s) {
     if (!n) return hipSuccess;
     Outs o{nullptr, out_value, out_found};
     if (small_path_ok(ix, n)) {
-        hipLaunchKernelGGL(k_walk_small<MODE_FIRST>, dim3(blocks_for(n, SM_TOPICS)), dim3(WV_BLOCK), 0, s, ix, ws, n,
-                           bytes, offs, o, nullptr, nullptr, (uint64_t)0, 0u, LbCtl{LB_SPINS, NONE, LB_DEFER});
+        hipLaunchKernelGGL((k_walk_small<MODE_FIRST, uint64_t>), dim3(blocks_for(n, SM_TOPICS)), dim3(WV_BLOCK), 0, s,
+                           ix, ws, n, bytes, offs, o, nullptr, nullptr, (uint64_t)0, 0u, LbCtl{LB_SPINS, NONE, LB_DEFER});
         return hipGetLastError();
     }
     if (n <= WAVE_TOPICS)

@@ -124,6 +124,34 @@ class Router:
         else:
             raise TypeError(f"not a route table record: {rec!r}")
 
+    def on_table_events(self, events):
+        """A run of replicated table events -- everything the mirror's event
+        process drained from its mailbox (src/emqx_router_gpu.erl) -- shipped
+        to the device as ONE delta batch (emqx_topic_index_gpu:table_events/2).
+        A node-down cleanup reaches the mirror this way: mria's match_delete
+        on both tables (emqx_router.erl:535-550) produces a delete event per
+        route, and the mirror never writes the mria-managed table itself."""
+        for ev in events:
+            self.on_table_event(ev)
+        self._filters.flush()
+
+    def attach(self, route_rows, filter_rows, batch_size: int = 1000) -> int:
+        """Boot from existing route tables (emqx_router_gpu:attach/1 over
+        ?ROUTE_TAB_FILTERS; the bag's rows as well, since its topics are binary
+        keys of the same device index): route_rows are Route(topic, dest) in
+        bag insertion order, filter_rows RouteIdx(entry) in key order; at most
+        batch_size keys per tm_apply_deltas.  Returns the device calls made."""
+        def rows():
+            for r in route_rows:
+                dests = self._bag.setdefault(bytes(r.topic), {})
+                if r.dest not in dests:
+                    self._seq += 1
+                    dests[r.dest] = self._seq
+                    yield make_key(bytes(r.topic), r.dest), []
+            for r in filter_rows:
+                yield r.entry, []
+        return self._filters.attach(rows(), batch_size)
+
     def cleanup_routes(self, node):
         """cleanup_routes/1 (emqx_router.erl:535-578): drop every route whose
         destination lives on `node` (a dead node), wildcard and exact alike."""

@@ -135,6 +135,24 @@ class Tab:
                 self._keys[kid] = None
                 self._released.append(kid)
 
+    def attach(self, rows, batch_size: int = 1000) -> int:
+        """Boot the device mirror from an existing table (emqx_topic_index_gpu:
+        attach/2): rows are (Key, Record) in the table's key order, loaded in
+        batches of at most batch_size keys, one tm_apply_deltas per batch (the
+        Erlang module counts the batch as it fills: linear in the rows).
+        Returns the device calls made."""
+        calls, k = 0, 0
+        for key, rec in rows:
+            self.insert_key(key, rec)
+            k += 1
+            if k >= batch_size:
+                self.flush()
+                calls, k = calls + 1, 0
+        if k:
+            self.flush()
+            calls += 1
+        return calls
+
     def size(self) -> int:
         return len(self._records)
 

@@ -196,6 +196,25 @@ int tm_match_batch_ex(tm_index *h, uint64_t n, const uint8_t *topic_bytes, const
                       uint64_t *out_hit_offsets, uint32_t *out_values, uint64_t cap, uint8_t *out_err,
                       uint32_t order, uint32_t *out_unique);
 
+/* tm_match_batch_ex with 32-bit offsets: topic_offsets[n+1] and
+ * out_hit_offsets[n+1] are u32 (a batch's topic bytes and its values must each
+ * stay below 2^32 -- a NIF micro-batch always does).  An in-place batch of up
+ * to 65536 topics (see tm_host_alloc) in TM_ORDER_TRAVERSAL then moves half
+ * the offset bytes over PCIe in each direction; any other batch is widened to
+ * tm_match_batch_ex on the host.  cap is clamped to 2^32 - 1; TM_EINVAL if the
+ * values exceed that.  (No reference counterpart: the NIF's own buffers.) */
+int tm_match_batch32_ex(tm_index *h, uint64_t n, const uint8_t *topic_bytes, const uint32_t *topic_offsets,
+                        uint32_t *out_hit_offsets, uint32_t *out_values, uint64_t cap, uint8_t *out_err,
+                        uint32_t order, uint32_t *out_unique);
+
+/* tm_match_batch_dev with 32-bit offsets (traversal order): a batch of up to
+ * 65536 topics reads and writes them as they are; a larger one is widened
+ * into the stream's scratch, matched and narrowed on the device (two small
+ * copy kernels).  For host-fed pipelines: 4 B per topic less each way. */
+int tm_match_batch32_dev(tm_index *h, uint64_t n, const uint8_t *d_topic_bytes, const uint32_t *d_topic_offsets,
+                         uint32_t *d_out_hit_offsets, uint32_t *d_out_values, uint64_t cap, uint8_t *d_out_err,
+                         void *stream);
+
 /* Pinned host buffers, mapped into the index's device.  A NIF keeps its
  * per-scheduler batch buffers here: when every buffer given to tm_match_batch
  * (topic bytes -- 16-byte aligned --, offsets, hit offsets, values and err if

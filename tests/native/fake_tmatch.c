@@ -55,6 +55,16 @@ int tm_match_batch_ex(tm_index *h, uint64_t n, const uint8_t *tb, const uint64_t
     return hit[n] > cap ? TM_ECAP : TM_OK;
 }
 
+int tm_match_batch32_ex(tm_index *h, uint64_t n, const uint8_t *tb, const uint32_t *to, uint32_t *hit,
+                        uint32_t *vals, uint64_t cap, uint8_t *err, uint32_t order, uint32_t *uniq) {
+    uint64_t *o64 = malloc(8 * (n + 1)), *h64 = malloc(8 * (n + 1));
+    for (uint64_t i = 0; i <= n; i++) o64[i] = to[i];
+    const int rc = tm_match_batch_ex(h, n, tb, o64, h64, vals, cap, err, order, uniq);
+    for (uint64_t i = 0; i <= n; i++) hit[i] = (uint32_t)h64[i];
+    free(o64); free(h64);
+    return rc;
+}
+
 int tm_first_batch(tm_index *h, uint64_t n, const uint8_t *tb, const uint64_t *to, uint32_t *val, uint8_t *found) {
     (void)h;
     n_first++;

@@ -2122,3 +2122,100 @@ def test_one_pass_parked_blocks_are_finished(torch_dev, seed):
         if defer == 1 << 30:
             assert ix.debug_get(_native.TM_DEBUG_DEFERRED_BLOCKS) == d0
     assert ix.debug_get(_native.TM_DEBUG_FAILED_BATCHES) == 0
+
+
+def test_router_boot_1m_routes_and_node_down_cleanup(torch_dev):
+    """The deployment's boot and node-down paths at size:
+    1M routes of an existing table set (C3-shaped filters; exact topics in the
+    bag, wildcard ones in the index, destinations on four nodes and shared
+    groups) booted into the device mirror in batches of at most 1000 keys,
+    then one node's routes deleted as mria's match_delete would replicate
+    them -- delete table events, drained 1000 at a time (emqx_router.erl:
+    535-550, src/emqx_router_gpu.erl).  match_routes equals the CPU model +
+    oracle (harness.RouterModel) after each."""
+    from emqx_amd.trie_search import filter as tfilter
+    nodes = ["n1", "n2", "n3", (b"grp", "n2"), (b"grp", "n4")]
+    fs = wl.filters(3, 1_000_000)
+    model = RouterModel()
+    route_rows, filter_rows, routes, seen = [], [], [], set()
+    for i in range(len(fs)):
+        t, d = fs.item(i), nodes[i % len(nodes)]
+        if (t, d) in seen:
+            continue
+        seen.add((t, d))
+        routes.append((t, d))
+        model.add(t, d)
+        if tfilter(t) is not False:
+            filter_rows.append(rt.RouteIdx(ti.make_key(t, d)))
+        else:
+            route_rows.append(rt.Route(t, d))
+    filter_rows.sort(key=lambda r: ti.key_order(r.entry))
+    r = rt.Router(node="n1")
+    calls = r.attach(route_rows, filter_rows, batch_size=1000)
+    assert calls == (len(route_rows) + len(filter_rows) + 999) // 1000
+    assert r._filters.stats()["n_keys"] == len(route_rows) + len(filter_rows)
+    ts = wl.topics(3, 1_000_000, 4_000)
+    topics = [ts.item(i) for i in range(len(ts))]
+    topics += [routes[i][0] for i in range(0, len(routes), 997) if tfilter(routes[i][0]) is False][:500]
+    assert r.match_routes_batch(topics) == model.expected(topics)
+    # node n2 goes down: every route whose destination lives there, as delete events
+    dead = [(t, d) for t, d in routes if rt.get_dest_node(d) == "n2"]
+    events = [("delete", rt.RouteIdx(ti.make_key(t, d)) if tfilter(t) is not False else rt.Route(t, d))
+              for t, d in dead]
+    for k in range(0, len(events), 1000):
+        r.on_table_events(events[k:k + 1000])
+    for t, d in dead:
+        model.delete(t, d)
+    got = r.match_routes_batch(topics)
+    assert got == model.expected(topics)
+    assert all(rt.get_dest_node(x.dest) != "n2" for rs in got for x in rs)
+    assert r._filters.stats()["n_keys"] == len(routes) - len(dead)
+
+
+@pytest.mark.parametrize("nt", [1, 3000, 65536, 70_000])
+def test_u32_offsets_api_equals_u64(torch_dev, nt):
+    """tm_match_batch32_ex / tm_match_batch32_dev: u32 topic
+    offsets in, u32 hit offsets out -- in place from tm_host_alloc buffers (the
+    one-launch kernel on 32-bit offsets, up to 65536 topics), staged host
+    buffers, and device buffers (widened and narrowed on the device above
+    65536) -- identical to the u64 API and the oracle; TM_ECAP with valid
+    offsets when the values do not fit."""
+    torch = torch_dev
+    fs = wl.filters(3, 100_000)
+    ts = wl.topics(3, 100_000, nt)
+    ix, o = gpu_index(fs), oracle_of(fs)
+    hit, vals = assert_same(ix, o, ts)
+    o32 = ts.offs.astype(np.uint32)
+    # in place: every buffer from tm_host_alloc
+    pb = ix.host_array(len(ts.blob) + 16, np.uint8)
+    pb[: len(ts.blob)] = ts.blob
+    po = ix.host_array(nt + 1, np.uint32)
+    po[:] = o32
+    ph, pv, pe = ix.host_array(nt + 1, np.uint32), ix.host_array(int(hit[-1]) + 16, np.uint32), ix.host_array(nt, np.uint8)
+    p0 = _paths(ix)
+    h2, v2, e2 = ix.match_batch32(pb, po, (ph, pv, pe))
+    assert np.array_equal(h2.astype(np.uint64), hit) and np.array_equal(v2, vals) and not e2.any()
+    if nt <= 65536:
+        assert _paths(ix)[1] > p0[1]   # the 32-bit one-launch kernel
+    # staged (ordinary numpy buffers)
+    h3, v3, e3 = np.zeros(nt + 1, np.uint32), np.zeros(int(hit[-1]) + 16, np.uint32), np.zeros(nt, np.uint8)
+    ix.match_batch32(ts.blob, o32, (h3, v3, e3))
+    assert np.array_equal(h3[: nt + 1].astype(np.uint64), hit) and np.array_equal(v3[: int(hit[-1])], vals)
+    # capacity too small: TM_ECAP, offsets still valid
+    small = np.zeros(max(int(hit[-1]) // 2, 1), np.uint32)
+    h4 = np.zeros(nt + 1, np.uint32)
+    if int(hit[-1]) > 1:
+        with pytest.raises(_native.TmError) as ex:
+            ix.match_batch32(ts.blob, o32, (h4, small, np.zeros(nt, np.uint8)))
+        assert ex.value.code == _native.TM_ECAP and np.array_equal(h4.astype(np.uint64), hit)
+    # device API
+    d_blob, d_offs = torch.from_numpy(ts.blob.copy()).cuda(), torch.from_numpy(o32.view(np.int32)).cuda()
+    d_hit = torch.zeros(nt + 1, dtype=torch.int32, device="cuda")
+    d_err = torch.zeros(nt, dtype=torch.uint8, device="cuda")
+    d_out = torch.zeros(int(hit[-1]) + 1, dtype=torch.int32, device="cuda")
+    ix.match_batch32_dev(nt, d_blob.data_ptr(), d_offs.data_ptr(), d_hit.data_ptr(), d_out.data_ptr(),
+                         int(hit[-1]) + 1, d_err.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert np.array_equal(d_hit.cpu().numpy().view(np.uint32).astype(np.uint64), hit)
+    assert np.array_equal(d_out.cpu().numpy().view(np.uint32)[: int(hit[-1])], vals)
+    assert not d_err.cpu().numpy().any()
