@@ -100,6 +100,11 @@ def parse():
     p.add_argument("--concurrency", type=int, default=8,
                    help="native caller threads of the concurrent-caller leg (and twice as many; 0 = skip)")
     p.add_argument("--frontier-sample", type=int, default=20_000)
+    p.add_argument("--replicas", type=int, default=0,
+                   help="replica-topology leg: one process, one tm_create_replicas index (one host image) over N "
+                        "device entries, native feeder threads submitting in-place host batches while a syncer thread "
+                        "applies deltas (the NIF's deployment, INTEGRATION.md 5); with fewer GPUs than N the entries "
+                        "repeat the local device -- a rehearsal, not scaling")
     p.add_argument("--large-path", default="default", choices=["default", "one", "phases"],
                    help="batches above 65536 topics: the library's default, k_walk_one (one launch) or the "
                         "two-phase path (TM_DEBUG_PHASES)")
@@ -456,6 +461,7 @@ def main():
         lat_native = {k: {"p50_ms": v[2 * i], "p99_ms": v[2 * i + 1], "mean_ms": lat_native[k]["mean_ms"]}
                       for i, k in enumerate(keys)}
     lat_pinned = lat_native
+    replicas = replica_leg(a, fs, ix, ts, local) if a.replicas > 0 and rank == 0 else None
 
     if rank != 0:
         if world > 1:
@@ -629,6 +635,8 @@ def main():
                   "kernel_source_hash": source_hash()},
     }
     res.update(res_extra)
+    if replicas is not None:
+        res["replicas"] = replicas
     if dchunks:
         res["deltas_per_step"] = a.deltas / every
         res["delta_batch"] = {"deltas": a.deltas, "every_steps": every}
@@ -648,6 +656,56 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def replica_leg(a, fs, ix, ts, local):
+    """One EMQX node's deployment (emqx_router.erl:133-162:
+    one replicated route table per node): ONE host image compiled once, N
+    device replicas (tm_create_replicas), host-API batches spread over them by
+    the library, one syncer thread's tm_apply_deltas reaching every replica.
+    Feeder threads submit in-place 64k-topic batches (tm_host_alloc buffers,
+    u32 offsets: what the NIF's dirty schedulers do), with and without churn;
+    per-replica batch counts from tm_replica_stats.  Its parity: the replica
+    index's lists on a sample equal the primary index's (which the oracle
+    sample checks) element for element."""
+    import torch
+    from emqx_amd import _native
+    ngpu = torch.cuda.device_count()
+    devices = [d % ngpu for d in range(a.replicas)] if ngpu >= a.replicas else [local] * a.replicas
+    t = time.time()
+    rx = _native.Index(devices=devices, hint_keys=len(fs))
+    for lo in range(0, len(fs), 2_000_000):
+        part = fs.slice(lo, min(lo + 2_000_000, len(fs)))
+        rx.apply(np.ones(len(part), np.uint8), part.blob, part.offs, part.vals)
+    t_build = time.time() - t
+    sub = ts.slice(0, min(len(ts), 20_000))
+    h0, v0, e0 = ix.match_batch(sub.blob, sub.offs)
+    h1, v1, e1 = rx.match_batch(sub.blob, sub.offs)
+    exact = bool(np.array_equal(h0, h1) and np.array_equal(v0, v1) and np.array_equal(e0, e1))
+    hb = host_bench_lib()
+    legs = []
+    lb = min(65536, len(ts) // max(1, 2 * a.replicas))
+    for nth, churn in ((2 * a.replicas, 0), (2 * a.replicas, 256)):
+        s2 = ts.slice(0, nth * lb)
+        hh, _, _ = rx.match_batch(s2.blob, s2.offs)
+        cap = int(np.diff(hh.astype(np.int64)).reshape(nth, lb).sum(axis=1).max()) + 65536
+        before = [rx.replica_stats(r)[0] for r in range(a.replicas)]
+        out = (ctypes.c_double * 6)()
+        rc = hb.tmb_callers_ex(rx._h, nth, lb, _native._ptr(s2.blob), _native._ptr(s2.offs), cap, 2.0, churn, 4, out)
+        assert rc == 0, rc
+        per = [rx.replica_stats(r)[0] - before[r] for r in range(a.replicas)]
+        legs.append({"feeder_threads": nth, "topics_per_batch": lb, "topics_per_s": round(out[1], 1),
+                     "p50_ms": round(out[2], 4), "p99_ms": round(out[3], 4), "deltas_per_s": round(out[4], 1),
+                     "batches_per_replica": per})
+    st = rx.stats()
+    rx.close()
+    return {"replicas": a.replicas, "devices": devices,
+            "rehearsal": len(set(devices)) < a.replicas,
+            "note": ("replicas sharing a GPU: the control flow and balance of the one-process deployment, not "
+                     "scaling" if len(set(devices)) < a.replicas else "one replica per GPU"),
+            "build_s": round(t_build, 1), "device_MiB_per_replica": round(st["device_bytes"] / 2**20, 1),
+            "parity_sample": {"topics": len(sub), "equal_to_primary_index": exact},
+            "legs": legs}
 
 
 def host_bench_lib():

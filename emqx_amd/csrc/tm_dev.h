@@ -85,7 +85,7 @@ struct Workspace {
     uint32_t *lists;      // [(L_COUNT + 1) * n] topic lists (the last one: long segments to sort)
     uint32_t *list_n;     // [L_COUNT] list lengths, [L_COUNT] reset ticket, [L_COUNT + 1] scan ticket,
                           // [L_COUNT + 2] long-segment count, [L_COUNT + 3] its reset ticket,
-                          // [L_COUNT + 4] the one-launch path's block ticket (zero between batches),
+                          // [L_COUNT + 4] unused (was the one-launch path's start ticket),
                           // [LS_PARKED] k_walk_one blocks parked so far (diagnostics)
     uint64_t *blk;        // [n / TILE + 2] tile hit totals -> exclusive tile prefixes (zero between batches)
     uint32_t *deep_wid;   // [DEEP_LANES * MAX_LEVELS]

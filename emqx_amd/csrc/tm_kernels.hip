@@ -1092,8 +1092,8 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_wave(DevIndex ix, Workspace w
 // '#'-not-last cut) is walked by the group's first lane with an LDS store of
 // MID_L levels (small_path_ok: the index never needs more); the block's 16
 // hit counts get their global offset from a single-pass decoupled look-back
-// scan over the blocks in the order they started (a ticket, so a block only
-// ever waits for blocks already running); then each group puts its values in
+// scan over the blocks in dispatch order (a block only ever waits for blocks
+// already running); then each group puts its values in
 // the block's LDS span, written out as one contiguous run (or, for a block
 // whose values do not fit or that holds a lane-walked topic, straight into the
 // CSR).  The caller's buffers may be host memory (in-place host batches): the
@@ -1151,7 +1151,7 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_small(DevIndex ix, Workspace 
     __shared__ uint8_t s_mlen[SM_TOPICS][MID_L];
     __shared__ uint64_t s_cnt[SM_TOPICS];
     __shared__ uint64_t s_base;
-    __shared__ uint32_t s_vb, s_fail;
+    __shared__ uint32_t s_fail;
     constexpr uint32_t TBQ = SM_TB / 16 + 1;              // 16-B chunks of a topic staged in LDS
     constexpr uint32_t TBQ_ALL = SM_TOPICS * TBQ;
     // topic bytes in LDS: the block's whole byte span in one cooperative round
@@ -1164,9 +1164,10 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_small(DevIndex ix, Workspace 
     // (in place batches: a few whole PCIe writes instead of one per group)
     __shared__ uint32_t s_vals[SM_VSTAGE];
     __shared__ uint64_t s_sum;
-    if (threadIdx.x == 0) s_vb = atomicAdd(&ws.list_n[L_COUNT + 4], 1u);   // blocks scan in start order
-    __syncthreads();
-    const uint32_t vb = s_vb;
+    // blocks scan in blockIdx order: workgroups are dispatched in that order,
+    // so a block's predecessors are running or done (a start-order ticket, one
+    // atomic on one word per block, serialised the blocks: k_walk_one's study)
+    const uint32_t vb = blockIdx.x;
     // the block's SM_TOPICS + 1 topic offsets, read once by one wave (the
     // caller's buffers may be host memory: one coalesced read, not one per group)
     if (threadIdx.x <= SM_TOPICS && (uint64_t)vb * SM_TOPICS + threadIdx.x <= n)
@@ -1352,7 +1353,6 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_small(DevIndex ix, Workspace 
                 o.first_found[t] = badarg ? 2 : (nh ? 1 : 0);
             }
         }
-        if (threadIdx.x == 0 && vb == gridDim.x - 1) ws.list_n[L_COUNT + 4] = 0;   // every ticket is taken
         return;
     }
 
@@ -1376,10 +1376,7 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_small(DevIndex ix, Workspace 
             s_sum = sum;
             s_base = pre;
             if (fail) ws.hint_d[HINT_FAIL] = 1;
-            if (vb == gridDim.x - 1) {
-                if (!fail) hit_offs[n] = (OT)(pre + sum);
-                ws.list_n[L_COUNT + 4] = 0;   // every ticket is taken
-            }
+            if (vb == gridDim.x - 1 && !fail) hit_offs[n] = (OT)(pre + sum);
         }
     }
     __syncthreads();
@@ -1907,9 +1904,9 @@ __global__ __launch_bounds__(WALK_BLOCK, 8) void k_walk_one(DevIndex ix, OneArgs
     const uint32_t lane = threadIdx.x;
     // Blocks scan in blockIdx order: workgroups are dispatched in that order,
     // so a block's predecessors are running or done, never waiting for a slot
-    // it holds.  (A start-order ticket -- one atomic on one word per block, as
-    // k_walk_small takes -- serialised 15.6k blocks at ~9 ns each: the C3
-    // batch 0.343 -> 0.478 ms, profiles/r4/onepass_study.md.)
+    // it holds.  (A start-order ticket -- one atomic on one word per block --
+    // serialised 15.6k blocks at ~9 ns each: the C3 batch 0.343 -> 0.478 ms,
+    // profiles/r4/onepass_study.md.)
     const uint32_t vb = blockIdx.x;
     const uint64_t t = (uint64_t)vb * WALK_BLOCK + lane;
     const bool live = t < n;
