@@ -7,7 +7,8 @@ TAG=$1; shift
 OUT=gpurun_out/var_$TAG
 mkdir -p $OUT
 timeout -k 10 400 python3 -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread \
-  -k "one_pass or lookback or parked or u32 or boot_1m" > $OUT/tests.log 2>&1
+  -k "one_pass or lookback or parked or u32 or boot_1m" > $OUT/tests.log 2>&1 || {
+  rc=$?; echo "tests rc=$rc" >> $OUT/timing.txt; [ $rc -eq 1 ] || exit $rc; }
 for st in 1 3; do
   echo "== product phases streams=$st" >> $OUT/timing.txt
   timeout -k 10 120 python3 -u tools/profile_walk.py --large-path phases --streams $st "$@" 2>&1 | grep -v amdgpu.ids >> $OUT/timing.txt
