@@ -65,15 +65,17 @@ def build_tmatch(force: bool = False) -> Path:
     return LIB_TMATCH
 
 
-def build_variant(name: str, kernel_src: str | None = None, force: bool = False) -> Path:
+def build_variant(name: str, kernel_src: str | None = None, force: bool = False,
+                  host_src: str | None = None) -> Path:
     """An experimental build of libtmatch (perf studies: tools/gpu_variants.sh
     loads it through TM_LIB).  `kernel_src` replaces tm_kernels.hip with a
     study copy (e.g. under emqx_amd/study/, not tracked), so experiments never
-    put switches into the product source.  Not the product library."""
+    put switches into the product source; `host_src` likewise tm_host.cpp.
+    Not the product library."""
     out = PKG / "variants" / f"libtmatch_{name}.so"
     out.parent.mkdir(exist_ok=True)
     kern = Path(kernel_src) if kernel_src else CSRC / "tm_kernels.hip"
-    srcs = [CSRC / "tm_host.cpp", kern]
+    srcs = [Path(host_src) if host_src else CSRC / "tm_host.cpp", kern]
     deps = srcs + [CSRC / "tm_layout.h", CSRC / "tm_dev.h", ROOT / "include" / "tmatch.h"]
     if force or _stale(out, deps):
         _run(["hipcc", "-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-shared", "-Wall",

@@ -85,7 +85,7 @@ struct Workspace {
     uint32_t *lists;      // [(L_COUNT + 1) * n] topic lists (the last one: long segments to sort)
     uint32_t *list_n;     // [L_COUNT] list lengths, [L_COUNT] reset ticket, [L_COUNT + 1] scan ticket,
                           // [L_COUNT + 2] long-segment count, [L_COUNT + 3] its reset ticket,
-                          // [L_COUNT + 4] unused (was the one-launch path's start ticket),
+                          // [LS_NPARK] k_walk_one blocks parked in this batch (k_one_scan -> k_one_finish),
                           // [LS_PARKED] k_walk_one blocks parked so far (diagnostics)
     uint64_t *blk;        // [n / TILE + 2] tile hit totals -> exclusive tile prefixes (zero between batches)
     uint32_t *deep_wid;   // [DEEP_LANES * MAX_LEVELS]
@@ -102,7 +102,8 @@ struct Workspace {
 };
 
 constexpr int TILE = 256;    // topics per walk block = per scan tile = per emit block
-constexpr int LS_PARKED = L_COUNT + 5;    // Workspace::list_n word: k_walk_one blocks that parked, so far (diagnostics)
+constexpr int LS_NPARK = L_COUNT + 4;     // Workspace::list_n word: k_walk_one blocks parked in this batch
+constexpr int LS_PARKED = L_COUNT + 5;   // Workspace::list_n word: k_walk_one blocks that parked, so far (diagnostics)
 constexpr int LIST_SLOTS = L_COUNT + 6;   // Workspace::list_n entries
 constexpr int HINT_FAIL = L_COUNT + 1;    // Workspace::hint_* word of the fail flag
 constexpr int HINT_WORDS = L_COUNT + 2;

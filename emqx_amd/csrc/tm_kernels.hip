@@ -1825,7 +1825,8 @@ __global__ __launch_bounds__(EMIT_BLOCK) void k_emit(DevIndex ix, Workspace ws, 
 //      ranges, or deeper than FAST_L) and writes their values directly.
 // A block whose predecessors are still walking after LB_DEFER polls does not
 // wait on: it parks its counts, flags and ranges (as k_walk_fast would) and
-// publishes LB_DEF; k_one_finish emits those blocks once the kernel is done.
+// publishes LB_DEF; after the kernel, k_one_scan gives the parked blocks their
+// prefixes (and writes hit_offs[n]) and k_one_finish emits them.
 // Waiting blocks hold their slots, so one slow block would stall every block
 // after it that finished meanwhile -- the GPU filling up with waiting waves.
 // Per topic of a block that does not park, only the CSR itself is written:
@@ -1969,57 +1970,120 @@ __global__ __launch_bounds__(WALK_BLOCK, 8) void k_walk_one(DevIndex ix, OneArgs
         }
         return;
     }
-    if (lane == 0 && vb == gridDim.x - 1) A.hit_offs[n] = base + total;
-
     // ---- 4, 5. offsets, values, re-walks
     wave_sync();   // every lane has its ranges: the LDS becomes the range stage
     one_emit(ix, S, blob, offs, t, live, rew, nrr, rg, base, rel, total, A.hit_offs, A.out, A.cap);
 }
 
-// The blocks of a k_walk_one launch that parked (LB_DEF), after it: one wave
-// per 64 blocks' look-back words; per parked block, its exclusive prefix from
-// the words before it (final now: LB_INCL or LB_DEF), then its offsets and
-// values from the parked counts and ranges (one_emit, re-walks included).  A
-// word that is not final (never, unless a block failed to publish) raises the
-// fail word: the host runs the batch again.  The workspace counts the parked
-// blocks (list_n[LS_PARKED], TM_DEBUG_DEFERRED_BLOCKS).
-__global__ __launch_bounds__(WALK_BLOCK) void k_one_finish(DevIndex ix, OneArgs a, uint32_t nb, uint32_t *fail_word,
-                                                           uint32_t *parked) {
+// After k_walk_one every look word is final: LB_INCL (the block's inclusive
+// prefix) or LB_DEF (a parked block's own total).  One block of 1024 threads
+// (thread j: a contiguous run of words, as k_scan_top) runs a segmented scan
+// over them -- an LB_INCL word restarts the sum at its value -- and gives each
+// parked block its exclusive prefix, written back into its word (LB_DEF, value
+// = the prefix), and a place in the list of parked blocks, in block order
+// (plist, count in list_n[LS_NPARK]); hit_offs[n] = the grand total.  A word
+// that is not final (never, unless a block failed to publish) raises the fail
+// word: the host runs the batch again.  (The first finisher looked back from
+// each parked block over the words before it, one wave per 64 blocks, serially:
+// with most blocks parked that was O(nb^2 / 64) loads and 0.9 ms per C3 batch.)
+constexpr uint32_t SCAN_U = 8;
+__global__ __launch_bounds__(1024) void k_one_scan(uint64_t *look, uint32_t nb, uint32_t tag, uint32_t *plist,
+                                                   uint32_t *list_n, uint64_t *hit_offs, uint64_t n,
+                                                   uint32_t *fail_word) {
+    __shared__ uint64_t s_v[16];
+    __shared__ uint32_t s_f[16], s_c[16];
+    const uint32_t per = (nb + 1023) / 1024;
+    const uint32_t b0 = threadIdx.x * per < nb ? threadIdx.x * per : nb, b1 = b0 + per < nb ? b0 + per : nb;
+    // the run's aggregate: f = it holds an LB_INCL word, v = the sum from its
+    // last LB_INCL word on (or from its start), c = its parked blocks
+    // (plain loads, SCAN_U at a time: k_walk_one has ended, its words are
+    // visible; one dependent load after another took 75 us for 15.6k words)
+    uint32_t f = 0, c = 0, bad = 0;
+    uint64_t v = 0;
+    for (uint32_t i0 = b0; i0 < b1; i0 += SCAN_U) {
+        uint64_t w[SCAN_U];
+#pragma unroll
+        for (uint32_t u = 0; u < SCAN_U; u++) w[u] = i0 + u < b1 ? look[(uint64_t)(i0 + u) * LB_STRIDE] : 0;
+#pragma unroll
+        for (uint32_t u = 0; u < SCAN_U; u++) {
+            if (i0 + u >= b1) break;
+            const uint32_t st = lb_tag(w[u]) == tag ? lb_state(w[u]) : 0u;
+            if (st == LB_INCL) { f = 1; v = w[u] & LB_VAL_MASK; }
+            else if (st == LB_DEF) { v += w[u] & LB_VAL_MASK; c++; }
+            else bad = 1;
+        }
+    }
+    if (__syncthreads_or(bad)) {
+        if (threadIdx.x == 0) { *fail_word = 1; list_n[LS_NPARK] = 0; }
+        return;
+    }
+    // segmented inclusive scan over the threads: (f1, v1) then (f2, v2) = f2 ? (1, v2) : (f1, v1 + v2)
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint32_t sf = f, sc = c;
+    uint64_t sv = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t of = __shfl_up(sf, d, 64), oc = __shfl_up(sc, d, 64);
+        const uint64_t ov = __shfl_up(sv, d, 64);
+        if (lane >= d) {
+            if (!sf) sv += ov;
+            sf |= of;
+            sc += oc;
+        }
+    }
+    if (lane == 63) { s_f[wv] = sf; s_v[wv] = sv; s_c[wv] = sc; }
+    __syncthreads();
+    uint32_t pf = 0, pc = 0, tc = 0;   // the waves before this one, combined
+    uint64_t pv = 0;
+    for (int k = 0; k < 16; k++) {
+        if (k < wv) { pv = s_f[k] ? s_v[k] : pv + s_v[k]; pf |= s_f[k]; pc += s_c[k]; }
+        tc += s_c[k];
+    }
+    // this thread's exclusive prefix: the waves before, then the lanes before
+    uint32_t ef = __shfl_up(sf, 1, 64), ec = __shfl_up(sc, 1, 64);
+    uint64_t ev = __shfl_up(sv, 1, 64);
+    if (lane == 0) { ef = 0; ec = 0; ev = 0; }
+    uint64_t run = ef ? ev : pv + ev;
+    uint32_t k = pc + ec;
+    (void)pf;
+    for (uint32_t i0 = b0; i0 < b1; i0 += SCAN_U) {
+        uint64_t w[SCAN_U];
+#pragma unroll
+        for (uint32_t u = 0; u < SCAN_U; u++) w[u] = i0 + u < b1 ? look[(uint64_t)(i0 + u) * LB_STRIDE] : 0;
+#pragma unroll
+        for (uint32_t u = 0; u < SCAN_U; u++) {
+            if (i0 + u >= b1) break;
+            if (lb_state(w[u]) == LB_INCL) {
+                run = w[u] & LB_VAL_MASK;
+            } else {
+                look[(uint64_t)(i0 + u) * LB_STRIDE] = lb_word(tag, LB_DEF, run);
+                plist[k++] = i0 + u;
+                run += w[u] & LB_VAL_MASK;
+            }
+        }
+    }
+    if (threadIdx.x == 1023) {   // (its run ends at nb: run = the grand total)
+        hit_offs[n] = run;
+        list_n[LS_NPARK] = tc;
+        list_n[LS_PARKED] += tc;   // (diagnostics: TM_DEBUG_DEFERRED_BLOCKS)
+    }
+}
+
+// The parked blocks of a k_walk_one launch, after k_one_scan: a grid of up
+// to FIN_GRID one-wave blocks takes them from the list in turn; per block, its
+// offsets and values from the parked counts and ranges and the prefix
+// k_one_scan left in its word (one_emit, re-walks included).
+constexpr uint32_t FIN_GRID = 65536;   // (4096: 57 us for 15.6k parked C3 blocks -- 4 waves per SIMD hide too little)
+__global__ __launch_bounds__(WALK_BLOCK) void k_one_finish(DevIndex ix, OneArgs a, const uint32_t *plist,
+                                                           const uint32_t *list_n) {
     __shared__ OneLds S;
     const uint32_t lane = threadIdx.x;
-    const uint32_t w0 = blockIdx.x * 64;
     const uint64_t n = a.n;
-    const uint64_t fw = w0 + lane < nb ? __hip_atomic_load(&a.look[(uint64_t)(w0 + lane) * LB_STRIDE], __ATOMIC_RELAXED,
-                                                           __HIP_MEMORY_SCOPE_AGENT) : 0;
-    uint64_t mdef = __ballot(w0 + lane < nb && lb_tag(fw) == a.tag && lb_state(fw) == LB_DEF);
-    const uint64_t mbad = __ballot(w0 + lane < nb && (lb_tag(fw) != a.tag || lb_state(fw) == LB_AGG ||
-                                                      lb_state(fw) == LB_FAIL));
-    if (mbad && lane == 0) *fail_word = 1;   // (the offsets are not trusted: the host runs the batch again)
-    if (mdef && lane == 0) atomicAdd(parked, (uint32_t)__popcll(mdef));   // (device memory: diagnostics)
-    while (mdef) {
-        const uint32_t vb = w0 + (uint32_t)__ffsll((long long)mdef) - 1;
-        mdef &= mdef - 1;
-        // the block's exclusive prefix: the nearest inclusive one before it plus the parked totals between
-        uint64_t pre = 0;
-        bool bad = false;
-        for (int64_t hi = (int64_t)vb - 1; hi >= 0;) {
-            const int64_t j = hi - (int64_t)lane;
-            const uint64_t f = j >= 0 ? __hip_atomic_load(&a.look[(uint64_t)j * LB_STRIDE], __ATOMIC_RELAXED,
-                                                          __HIP_MEMORY_SCOPE_AGENT)
-                                      : lb_word(a.tag, LB_INCL, 0);
-            if (__ballot(lb_tag(f) != a.tag || (lb_state(f) != LB_INCL && lb_state(f) != LB_DEF))) { bad = true; break; }
-            const uint64_t mi = __ballot(lb_state(f) == LB_INCL);
-            const uint32_t k = mi ? (uint32_t)__ffsll((long long)mi) - 1 : 63;
-            uint64_t v = lane <= k ? f & LB_VAL_MASK : 0;
-            for (int d = 32; d; d >>= 1) v += __shfl_xor(v, d, 64);
-            pre += v;
-            if (mi) break;
-            hi -= 64;
-        }
-        if (bad) {
-            if (lane == 0) *fail_word = 1;
-            continue;
-        }
+    const uint32_t np = list_n[LS_NPARK];
+    for (uint32_t i = blockIdx.x; i < np; i += gridDim.x) {
+        const uint32_t vb = plist[i];
+        const uint64_t pre = __hip_atomic_load(&a.look[(uint64_t)vb * LB_STRIDE], __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT) & LB_VAL_MASK;
         const uint64_t t = (uint64_t)vb * WALK_BLOCK + lane;
         const bool live = t < n;
         const uint32_t cnt = live ? __builtin_nontemporal_load(a.cnt + t) : 0u;
@@ -2028,14 +2092,13 @@ __global__ __launch_bounds__(WALK_BLOCK) void k_one_finish(DevIndex ix, OneArgs 
         const uint32_t nrr = rew ? 0u : pnr;
         uint2 rg[RCAP];
 #pragma unroll
-        for (uint32_t i = 0; i < RCAP; i++) {
-            const uint64_t g = i < nrr ? __builtin_nontemporal_load(reinterpret_cast<const uint64_t *>(a.rng) +
-                                                                    (uint64_t)i * n + t) : 0;
-            rg[i] = make_uint2((uint32_t)g, (uint32_t)(g >> 32));
+        for (uint32_t r = 0; r < RCAP; r++) {
+            const uint64_t g = r < nrr ? __builtin_nontemporal_load(reinterpret_cast<const uint64_t *>(a.rng) +
+                                                                    (uint64_t)r * n + t) : 0;
+            rg[r] = make_uint2((uint32_t)g, (uint32_t)(g >> 32));
         }
         const uint64_t inc = wave_incl_scan(cnt);
         const uint64_t total = __shfl(inc, 63, 64);
-        if (lane == 0 && vb == nb - 1) a.hit_offs[n] = pre + total;
         wave_sync();   // (the previous parked block's emit is done with the LDS)
         one_emit(ix, S, a.blob, a.offs, t, live, rew, nrr, rg, pre, inc - cnt, total, a.hit_offs, a.out, a.cap);
         wave_sync();
@@ -2345,8 +2408,10 @@ hipError_t launch_match(const DevIndex &ix, const Workspace &ws, uint64_t n, con
             const uint32_t nb = blocks_for(n, WALK_BLOCK);
             hipLaunchKernelGGL(k_walk_one, dim3(nb), dim3(WALK_BLOCK), 0, s, ix, a);
             if (ev_walk1 && (e = hipEventRecord(ev_walk1, s)) != hipSuccess) return e;
-            hipLaunchKernelGGL(k_one_finish, dim3(blocks_for(nb, 64)), dim3(WALK_BLOCK), 0, s, ix, a, nb,
-                               ws.hint_d + HINT_FAIL, ws.list_n + LS_PARKED);
+            hipLaunchKernelGGL(k_one_scan, dim3(1), dim3(1024), 0, s, ws.look, nb, tag & LB_TAG_MASK, ws.lists,
+                               ws.list_n, hit_offs, n, ws.hint_d + HINT_FAIL);
+            hipLaunchKernelGGL(k_one_finish, dim3(nb < FIN_GRID ? nb : FIN_GRID), dim3(WALK_BLOCK), 0, s, ix, a,
+                               ws.lists, ws.list_n);
             return hipGetLastError();
         }
         if (ev_walk1 && (e = hipEventRecord(ev_walk1, s)) != hipSuccess) return e;
