@@ -88,6 +88,11 @@ def parse():
                         "default 3, and 1 for c5 with one copy of the tables: a churn step's patch then waits "
                         "for every batch in flight, so its steps cannot overlap and a second stream only adds "
                         "cross-stream waits (0.41 vs 0.54-0.64 ms per step measured in round 2)")
+    p.add_argument("--split", type=int, default=1,
+                   help="sub-batches per step: each step's batch goes to the streams as this many contiguous "
+                        "sub-batches (each its own CSR, as that many concurrent NIF batches), so the timed "
+                        "region ends one sub-batch's latency after the last launch instead of one whole "
+                        "overlapped batch's")
     p.add_argument("--copies", type=int, default=1,
                    help="copies of the tables on the GPU (tm_options.copies): a batch after a delta runs on a "
                         "copy no batch is reading (measured: no gain on c5 or churned callers, DESIGN.md 3)")
@@ -235,6 +240,9 @@ def main():
     nstreams = 1 if filter_sharded else max(1, a.streams if a.streams is not None else
                                             (1 if a.config == "c5" and copies == 1 else 3))
     streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(nstreams - 1)]
+    split = 1 if (filter_sharded or a.config == "c5") else max(1, min(a.split, nstreams))
+    sub = -(-B // split)
+    parts = [(j * sub, min(sub, B - j * sub)) for j in range(split)]   # (first topic, topics) of each sub-batch
     outs = [{"hit": torch.zeros(B + 1, dtype=torch.int64, device=dev),
              "err": torch.zeros(B, dtype=torch.uint8, device=dev),
              "out": torch.zeros(1, dtype=torch.int32, device=dev)} for _ in range(nstreams)]
@@ -256,6 +264,12 @@ def main():
         kstep[0] += 1
         o = outs[k % nstreams]
         d_blob, d_offs = d_in[k % R]
+        if split > 1:   # sub-batch j on stream j, into its own CSR
+            for j, (lo, n) in enumerate(parts):
+                o = outs[j]
+                ix.match_batch_dev(n, d_blob.data_ptr(), d_offs.data_ptr() + 8 * lo, o["hit"].data_ptr(),
+                                   o["out"].data_ptr(), cap, o["err"].data_ptr(), streams[j].cuda_stream)
+            return None
         sid = streams[k % nstreams].cuda_stream
         if dchunks and k % every == 0:
             d = dchunks[dpos[0]]
@@ -280,6 +294,9 @@ def main():
         torch.cuda.synchronize()
         batch_hits.append(int(outs[0]["hit"][-1].item()))
         total_hits = max(total_hits, batch_hits[-1])
+        if split > 1:   # each sub-batch's CSR is offset from 0: its own capacity is its own hits
+            hv = outs[0]["hit"]
+            total_hits = max(total_hits, max(int(hv[lo + n].item()) - int(hv[lo].item()) for lo, n in parts))
         if xch is not None:
             xch.size_from(outs[0]["hit"])   # per-peer exchange capacity: setup, not the data path
     slack = a.deltas * (a.steps + a.warmup) * 64 if dchunks else 0   # churn may add hits
@@ -316,11 +333,15 @@ def main():
     if xch is not None:   # the on-device high-water mark: did any timed batch overflow the capacity?
         assert xch.check(), "filter-sharded exchange capacity overflowed during the timed steps"
     last_k = kstep[0] - 1
-    last = outs[last_k % nstreams]
     last_batch = last_k % R
-    d_hit, d_out = last["hit"], last["out"]
-    last_hits = int(d_hit[-1].item())
-    assert last_hits <= cap
+    # the last timed step's CSR(s): (first topic, topics, output set) per sub-batch
+    last_parts = ([(lo, n, outs[j]) for j, (lo, n) in enumerate(parts)] if split > 1
+                  else [(0, B, outs[last_k % nstreams])])
+    last_hits = 0
+    for lo, n, o in last_parts:
+        h = int(o["hit"][n].item())
+        assert h <= cap
+        last_hits += h
     merged_total = int(merged[0][-1].item()) if merged is not None else None
     merged_topics = merged[0].numel() - 1 if merged is not None else None
     # The walk kernel alone: two passes over the R batches, back to back on
@@ -492,8 +513,8 @@ def main():
         o.prepare()
         log(f"oracle built in {time.time() - t:.1f}s")
         # the last timed step's output of this rank (its own shard's lists for c4)
-        host_hit = d_hit.cpu().numpy().view(np.uint64)
-        host_out = d_out.cpu().numpy().view(np.uint32)
+        host_parts = [(lo, n, o["hit"][: n + 1].cpu().numpy().view(np.uint64), o["out"].cpu().numpy().view(np.uint32))
+                      for lo, n, o in last_parts]
         rng = np.random.default_rng(0x454D5158)
         idx = np.sort(rng.choice(B, ns, replace=False))
         lts = tsets[last_batch]
@@ -501,7 +522,8 @@ def main():
         cnt, _, ohit, ovals = o.match_batch(sblob, soffs, nthreads=cpu_threads)
         mism = 0
         for j, i in enumerate(idx):
-            g = host_out[int(host_hit[i]):int(host_hit[i + 1])]
+            lo, _, host_hit, host_out = next(p for p in host_parts if p[0] <= i < p[0] + p[1])
+            g = host_out[int(host_hit[i - lo]):int(host_hit[i - lo + 1])]
             e = ovals[int(ohit[j]):int(ohit[j + 1])]
             mism += int(not np.array_equal(g, e))
         # algorithmic bytes per launch of the timed kernel (SURVEY.md 8d per
@@ -596,7 +618,8 @@ def main():
         "data": "synthetic (emqx_amd/csrc/workload.cpp, seed 0x454D5158+cfg)",
         "config": {"workload": f"{a.config}: {desc}", "filters": nf if (filter_sharded or level0) else len(fs),
                    "topics_per_gpu_step": B, "global_batch": topics_per_step, "parallelism": par,
-                   "streams": nstreams, "distinct_batches": R, "table_copies": copies},
+                   "streams": nstreams, "sub_batches_per_step": split, "distinct_batches": R,
+                   "table_copies": copies},
         "roofline": {"bound": "hbm", "achieved": None if achieved is None else round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": None if achieved is None else round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
@@ -613,8 +636,9 @@ def main():
                      "effective": {"kernel_avg_ms_overlapped": round(walk_avg_ms, 4),
                                    "walk_GBps_per_step": None if walk_bytes is None
                                    else round(walk_bytes / (ms_per_step * 1e-3) / 1e9, 1),
-                                   "note": f"the timed region's walks, overlapping the other {nstreams - 1} streams' "
-                                           f"kernels; GBps_per_step = algorithmic bytes / ms_per_step"}},
+                                   "note": f"the timed region's walks ({'per sub-batch, ' if split > 1 else ''}"
+                                           f"overlapping the other {nstreams - 1} streams' kernels); "
+                                           f"GBps_per_step = algorithmic bytes / ms_per_step"}},
         "checks": {"walk_isolated_le_ms_per_step": bool(iso_ms <= ms_per_step)},
         "cpu_baseline": cpu,
         "matched_ids_per_s": round(last_hits * (1 if filter_sharded else world) * a.steps / el_max, 1),
