@@ -242,11 +242,20 @@ int tmb_callers(tm_index *h, int nthreads, uint64_t n, const uint8_t *tb, const 
 // values into pinned host buffers of that stream; before a stream's buffers
 // are reused the host waits for its previous batch.
 // out: [topics_per_s, ms_per_batch, h2d_bytes_per_batch, d2h_bytes_per_batch, seconds]
-// u32 != 0: the same with 32-bit offsets both ways (tm_match_batch32_dev):
-// 4 B per topic less over PCIe in each direction.
+// u32 bit 0: the same with 32-bit offsets both ways (tm_match_batch32_dev):
+// 4 B per topic less over PCIe in each direction.  Bit 1: every H2D on one
+// upload stream and every D2H on one download stream, joined to the batches'
+// compute streams by events (the arrangement tmb_pcie measures both directions
+// at once with), instead of each batch's copies on its own stream.
 int tmb_pipeline_ex(tm_index *h, int device, const uint8_t *tb, const uint64_t *to, uint64_t n, int R, int nstreams,
                     int iters, int u32, double *out) {
     if (hipSetDevice(device) != hipSuccess) return TM_EDEVICE;
+    const bool sep = (u32 & 2) != 0;
+    u32 &= 1;
+    hipStream_t up = nullptr, down = nullptr;
+    if (sep && (hipStreamCreateWithFlags(&up, hipStreamNonBlocking) != hipSuccess ||
+                hipStreamCreateWithFlags(&down, hipStreamNonBlocking) != hipSuccess))
+        return TM_EDEVICE;
     struct HostBatch { uint8_t *p; uint64_t bytes, total; };
     std::vector<HostBatch> hb(R);
     uint64_t maxb = 0;
@@ -270,13 +279,15 @@ int tmb_pipeline_ex(tm_index *h, int device, const uint8_t *tb, const uint64_t *
                    : api::match_batch_dev(h, n, d_in + boff, reinterpret_cast<uint64_t *>(d_in),
                                           static_cast<uint64_t *>(d_hit), d_vals, cap, d_err, s);
     };
-    struct Lane { hipStream_t s; hipEvent_t done; uint8_t *d_in; uint64_t *d_hit; uint32_t *d_vals; uint8_t *d_err;
-                  uint64_t *h_hit; uint32_t *h_vals; bool busy; };
+    struct Lane { hipStream_t s; hipEvent_t done, e_in, e_out; uint8_t *d_in; uint64_t *d_hit; uint32_t *d_vals;
+                  uint8_t *d_err; uint64_t *h_hit; uint32_t *h_vals; bool busy; };
     std::vector<Lane> ls(nstreams);
     uint64_t cap = 0;
     for (auto &l : ls) {
         if (hipStreamCreateWithFlags(&l.s, hipStreamNonBlocking) != hipSuccess ||
             hipEventCreateWithFlags(&l.done, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&l.e_in, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&l.e_out, hipEventDisableTiming) != hipSuccess ||
             hipMalloc(&l.d_in, maxb + 16) != hipSuccess || hipMalloc(&l.d_hit, 8 * (n + 1)) != hipSuccess ||
             hipMalloc(&l.d_err, n + 1) != hipSuccess || hipHostMalloc(&l.h_hit, 8 * (n + 1), hipHostMallocDefault) != hipSuccess)
             return TM_EDEVICE;
@@ -302,19 +313,28 @@ int tmb_pipeline_ex(tm_index *h, int device, const uint8_t *tb, const uint64_t *
     double h2d = 0, d2h = 0;
     auto issue = [&](int k, Lane &l) -> int {
         const HostBatch &b = hb[k % R];
-        if (hipMemcpyAsync(l.d_in, b.p, b.bytes, hipMemcpyHostToDevice, l.s) != hipSuccess) return TM_EDEVICE;
+        hipStream_t si = sep ? up : l.s, so = sep ? down : l.s;
+        if (hipMemcpyAsync(l.d_in, b.p, b.bytes, hipMemcpyHostToDevice, si) != hipSuccess) return TM_EDEVICE;
+        if (sep && (hipEventRecord(l.e_in, up) != hipSuccess || hipStreamWaitEvent(l.s, l.e_in, 0) != hipSuccess))
+            return TM_EDEVICE;
         int rc = match(l.d_in, l.d_hit, l.d_vals, cap, l.d_err, l.s);
         if (rc) return rc;
-        if (hipMemcpyAsync(l.h_hit, l.d_hit, ow * (n + 1), hipMemcpyDeviceToHost, l.s) != hipSuccess ||
-            hipMemcpyAsync(l.h_vals, l.d_vals, 4 * b.total, hipMemcpyDeviceToHost, l.s) != hipSuccess ||
-            hipEventRecord(l.done, l.s) != hipSuccess)
+        if (sep && (hipEventRecord(l.e_out, l.s) != hipSuccess || hipStreamWaitEvent(down, l.e_out, 0) != hipSuccess))
+            return TM_EDEVICE;
+        if (hipMemcpyAsync(l.h_hit, l.d_hit, ow * (n + 1), hipMemcpyDeviceToHost, so) != hipSuccess ||
+            hipMemcpyAsync(l.h_vals, l.d_vals, 4 * b.total, hipMemcpyDeviceToHost, so) != hipSuccess ||
+            hipEventRecord(l.done, so) != hipSuccess)
             return TM_EDEVICE;
         h2d += b.bytes;
         d2h += (double)ow * (n + 1) + 4.0 * b.total;
         l.busy = true;
         return TM_OK;
     };
-    for (int k = 0; k < nstreams; k++) issue(k, ls[k]);   // warm
+    for (int k = 0; k < 4 * nstreams; k++) {   // warm (the first rounds run slower)
+        Lane &l = ls[k % nstreams];
+        if (l.busy && hipEventSynchronize(l.done) != hipSuccess) return TM_EDEVICE;
+        if (int rc = issue(k, l)) return rc;
+    }
     for (auto &l : ls) { hipEventSynchronize(l.done); l.busy = false; }
     h2d = d2h = 0;
     const double t0 = now_s();
@@ -331,8 +351,10 @@ int tmb_pipeline_ex(tm_index *h, int device, const uint8_t *tb, const uint64_t *
         api::stream_release(h, l.s);
         hipFree(l.d_in); hipFree(l.d_hit); hipFree(l.d_vals); hipFree(l.d_err);
         hipHostFree(l.h_hit); hipHostFree(l.h_vals);
-        hipEventDestroy(l.done); hipStreamDestroy(l.s);
+        hipEventDestroy(l.done); hipEventDestroy(l.e_in); hipEventDestroy(l.e_out); hipStreamDestroy(l.s);
     }
+    if (up) hipStreamDestroy(up);
+    if (down) hipStreamDestroy(down);
     for (auto &b : hb) hipHostFree(b.p);
     out[0] = iters * (double)n / el;
     out[1] = el / iters * 1e3;
