@@ -132,6 +132,7 @@ int tmn_ticket_begin(tmn_ticket *t, tm_index *h) {
     if (pthread_mutex_init(&t->mu, NULL)) return TM_ENOMEM;
     int rc = tm_read_begin(h, &t->ticket);
     t->open = rc == TM_OK;
+    if (rc != TM_OK) pthread_mutex_destroy(&t->mu);   /* a failed begin leaves nothing to end or destroy */
     return rc;
 }
 

@@ -91,7 +91,7 @@ typedef struct {
     pthread_mutex_t mu;
 } tmn_ticket;
 
-int tmn_ticket_begin(tmn_ticket *t, tm_index *h);   /* TM_OK: registered, open */
+int tmn_ticket_begin(tmn_ticket *t, tm_index *h);   /* TM_OK: registered, open; else nothing to end or destroy */
 void tmn_ticket_end(tmn_ticket *t);                 /* idempotent */
 void tmn_ticket_destroy(tmn_ticket *t);             /* ends it if still open */
 
