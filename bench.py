@@ -310,22 +310,25 @@ def main():
 
     ix.profile(True)
     ix.profile_read(reset=True)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
     apply_s[0] = 0.0
     # the host loop stands in for the NIF's C caller: keep Python's cyclic
     # collector out of the timed region (a full collection stalled the GPU
-    # ~7 ms at a time in c5 traces, where each step waits for its deltas)
+    # ~7 ms at a time in c5 traces, where each step waits for its deltas) --
+    # collected before the barrier, so the ranks leave it together
     gc.collect()
     gc.freeze()
     gc.disable()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
     t0 = time.perf_counter()
+    t0_wall = time.time()
     merged = None
     for _ in range(a.steps):
         merged = step(cap)
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
+    log(f"[rank {rank}] timed region {t0_wall:.6f} .. {t0_wall + el:.6f} (wall clock)")
     gc.enable()
     if world > 1:
         dist.barrier()
