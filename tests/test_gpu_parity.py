@@ -1888,6 +1888,7 @@ def test_replicas_share_one_host_image(torch_dev):
         dev_bytes = x.stats()["device_bytes"]
         x.close()
         return rss, dev_bytes
+    build([0, 0])   # one-time runtime allocations (a second replica's streams, pinned pools) land here
     one, db1 = build([0])
     two, db2 = build([0, 0])
     print(f"host RSS growth: 1 replica {one / 2**20:.0f} MiB, 2 replicas {two / 2**20:.0f} MiB "
