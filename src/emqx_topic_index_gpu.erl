@@ -46,6 +46,8 @@
 -define(KIND_BINARY, 0).
 -define(KIND_WORDS, 1).
 -define(KIND_EMPTY, 2).
+%% Deltas accumulate as {DeviceDeltas, ReleasedKids}, both prepended.
+-define(NOACC, {[], []}).
 
 %%--------------------------------------------------------------------
 %% Tables
@@ -71,7 +73,7 @@ new(Options) ->
 
 %% Put a device mirror next to an existing index table (e.g. the router's
 %% ?ROUTE_TAB_FILTERS, emqx_router.erl:148-160) and load its keys in batches:
-%% boot from ETS.  Records are taken to be the last element of each row.
+%% boot from ETS (keys only: ets:first/next walk the table's keys).
 -spec attach(ets:table(), pos_integer()) -> gtab().
 attach(Tab, BatchSize) ->
     attach(Tab, BatchSize, -1).
@@ -96,9 +98,6 @@ mirror(Tab, Devices) ->
     Quar = ets:new(emqx_topic_index_quar, [ordered_set, public]),
     Free = ets:new(emqx_topic_index_free, [set, public]),
     #gtab{tab = Tab, kids = Kids, quar = Quar, free = Free, ref = Ref}.
-
-%% Deltas accumulate as {DeviceDeltas, ReleasedKids}, both prepended.
--define(NOACC, {[], []}).
 
 %% Rows are walked in key order; every BatchSize keys ship as one device call.
 %% The batch is counted as it fills (K): a length/1 guard per key made each
