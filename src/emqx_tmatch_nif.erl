@@ -3,6 +3,8 @@
 -module(emqx_tmatch_nif).
 
 -export([new/1, apply/2, match_batch/3, first_batch/2, read_begin/1, read_end/2, epoch/1, stats/1]).
+%% apply/2 is the NIF's name (c_src/emqx_tmatch_nif.c); callers always qualify it
+-compile({no_auto_import, [apply/2]}).
 -on_load(init/0).
 
 -type ref() :: reference().
