@@ -31,6 +31,7 @@ TM_DEBUG_LB_SPINS, TM_DEBUG_LB_FAIL_BLOCK, TM_DEBUG_LB_LAUNCHES, TM_DEBUG_PHASES
 TM_DEBUG_FAILED_BATCHES, TM_DEBUG_RETRIED_BATCHES = 5, 6
 TM_DEBUG_PATH_PHASES, TM_DEBUG_PATH_SMALL, TM_DEBUG_PATH_ONE = 7, 8, 9
 TM_DEBUG_LB_DEFER, TM_DEBUG_DEFERRED_BLOCKS = 10, 11
+TM_DEBUG_COMBINE, TM_DEBUG_COMBINED_LAUNCHES, TM_DEBUG_COMBINED_BATCHES = 12, 13, 14
 
 
 class NativeUnavailable(RuntimeError):

@@ -140,6 +140,19 @@ hipError_t launch_match(const DevIndex &ix, const Workspace &ws, uint64_t n, con
                         hipEvent_t ev_walk1 = nullptr, int *path = nullptr);
 // The one-launch small batch with 32-bit offsets in and out (hipErrorInvalidValue
 // if small_path_ok refuses the batch), and the 32 <-> 64-bit offset copies
+// Several host batches in ONE k_walk_small launch (the host's combiner,
+// tm_host.cpp small_combined): segment k owns the launch's blocks
+// [block0, next block0), its own inputs and outputs and its own look-back
+// region; a launch holds at most SMALL_SEGS segments of at most SMALL_TOPICS
+// topics together.  Offsets are uint64_t or uint32_t for the whole launch.
+constexpr int SMALL_SEGS = 16;
+struct SmallSeg {
+    const uint8_t *blob; const void *offs; void *hit; uint8_t *err; uint32_t *out;
+    uint64_t cap; uint32_t n, block0;
+};
+struct SmallSegs { uint32_t count, pad; SmallSeg s[SMALL_SEGS]; };
+hipError_t launch_small_segs(const DevIndex &ix, const Workspace &ws, const SmallSegs &sg, bool u32, uint32_t tag,
+                             LbCtl lb, hipStream_t s);
 hipError_t launch_match32(const DevIndex &ix, const Workspace &ws, uint64_t n, const uint8_t *bytes,
                           const uint32_t *offs, uint32_t *hit_offs, uint8_t *err, uint32_t *out, uint64_t cap,
                           uint32_t tag, LbCtl lb, hipStream_t s);

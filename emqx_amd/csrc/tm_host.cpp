@@ -18,6 +18,7 @@
 #include <cstdio>
 #include <cstring>
 #include <condition_variable>
+#include <deque>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -150,6 +151,9 @@ constexpr bool LARGE_PHASES_DEFAULT = true;
 constexpr int MAX_HOST_LANES = 16;   // concurrent host-API batches in flight, per replica
 constexpr int MAX_DEV_LANES = 16;    // device-API streams with a workspace kept
 
+// concurrent combined launches of small host batches (tm_index::cmb_leaders)
+constexpr int CMB_LEADERS = 4;   // (2 / 3 / 6 measured: profiles/r4/combiner/)
+
 struct tm_index {
     // Two locks (order: mu, then img).  `mu` covers the device side: lanes,
     // the patch log, the replicas, pinned buffers, profiling.  `img` covers
@@ -250,6 +254,16 @@ struct tm_index {
     bool dbg_phases = LARGE_PHASES_DEFAULT;
     std::atomic<uint64_t> failed_batches{0}, retried_batches{0};   // one-launch look-back failures seen / retried
     std::atomic<uint64_t> path_batches[PATH_COUNT] = {};             // match launches per kernel path
+    // The host-batch combiner (small_combined): small in-place 32-bit batches
+    // of concurrent callers queue here; up to cmb_leaders callers at a time
+    // each take what is queued and run it as ONE k_walk_small launch
+    // (TM_DEBUG_COMBINE: 0 = every batch its own launch)
+    std::mutex cmb_mu;
+    std::condition_variable cmb_cv;
+    std::deque<struct SmallReq *> cmb_q;
+    int cmb_running = 0;
+    int cmb_leaders = CMB_LEADERS;
+    std::atomic<uint64_t> cmb_launches{0}, cmb_batches{0};
 };
 
 namespace {
@@ -1974,6 +1988,91 @@ static int retry_or_fail(tm_index *ix, std::unique_lock<std::mutex> &g, Lane &ln
     return sync_locked(ix, ln.r, ln.s);
 }
 
+// ---- the host-batch combiner (32-bit in-place batches, the NIF's calls)
+//
+// Concurrent callers' small batches run better as fewer, larger launches: a
+// lone 4k batch keeps the GPU ~26 us for fixed costs a 64k batch pays once
+// (host to host: 4k 0.040 ms, 64k 0.19 ms), and 8 callers' kernels do not
+// overlap beyond ~3 at a time.  A caller queues its batch;
+// while fewer than cmb_leaders launches are running it takes the lead: it
+// takes the queued batches (in order, up to SMALL_SEGS of them and
+// ZC_TOPICS topics), runs them as ONE k_walk_small launch with a segment
+// table (each segment its own inputs, outputs and look-back region), and
+// marks them done; others wait on the condition variable.  A lone caller
+// leads its own batch at once: its latency is the single-batch path's.
+struct SmallReq {
+    uint64_t n;
+    const uint8_t *db; const uint8_t *dof; uint8_t *dh; uint8_t *de; uint8_t *dv;
+    uint64_t cap;
+    int rc = TM_OK;
+    bool done = false;
+};
+constexpr int CMB_LEGACY = 1;   // (not a TM_ code) the index no longer allows the one-launch path
+
+static int run_small_group(tm_index *ix, const std::vector<SmallReq *> &grp) {
+    uint64_t total = 0;
+    for (auto *r : grp) total += r->n;
+    std::unique_lock<std::mutex> g(ix->mu);
+    LaneLease lease{ix, g};
+    int rc;
+    if ((rc = host_lane(ix, g, lease.ln))) return rc;
+    Lane &ln = *lease.ln;
+    const hipStream_t s = ln.s;
+    if ((rc = sync_locked(ix, ln.r, s))) return rc;
+    if ((rc = ensure_ws(ix, total + (uint64_t)SMALL_SEGS * SM_TOPICS, ln))) return rc;
+    if (!small_path_ok(dev_view(ix, ln.r), total)) return CMB_LEGACY;
+    ix->rep[ln.r].batches++;
+    SmallSegs sg{};
+    sg.count = (uint32_t)grp.size();
+    for (size_t k = 0; k < grp.size(); k++) {
+        const SmallReq &r = *grp[k];
+        sg.s[k] = SmallSeg{r.db ? r.db : r.dof, r.dof, r.dh, r.de, reinterpret_cast<uint32_t *>(r.dv),
+                           r.dv ? r.cap : 0, (uint32_t)r.n, 0};
+    }
+    for (int tries = 0;; tries++) {
+        const DevIndex d = dev_view(ix, ln.r);
+        uint32_t tag;
+        if ((rc = next_tag(ix, ln, s, tag))) return rc;
+        HIPCHK(ix, launch_small_segs(d, ln.w, sg, true, tag, next_lb(ix), s));
+        ix->path_batches[PATH_SMALL]++;
+        ix->cmb_launches++;
+        ix->cmb_batches += grp.size();
+        if ((rc = batch_done(ix, ln))) return rc;
+        g.unlock();
+        HIPCHK(ix, hipStreamSynchronize(s));
+        if (!batch_failed(ix, ln)) break;
+        if ((rc = retry_or_fail(ix, g, ln, tries))) return rc;
+    }
+    return TM_OK;
+}
+
+static int small_combined(tm_index *ix, SmallReq &rq) {
+    std::unique_lock<std::mutex> lk(ix->cmb_mu);
+    ix->cmb_q.push_back(&rq);
+    while (!rq.done) {
+        if (ix->cmb_running < std::max(ix->cmb_leaders, 1) && !ix->cmb_q.empty()) {
+            std::vector<SmallReq *> grp;
+            uint64_t total = 0;
+            while (!ix->cmb_q.empty() && grp.size() < (size_t)SMALL_SEGS &&
+                   total + ix->cmb_q.front()->n <= ZC_TOPICS) {
+                total += ix->cmb_q.front()->n;
+                grp.push_back(ix->cmb_q.front());
+                ix->cmb_q.pop_front();
+            }
+            ix->cmb_running++;
+            lk.unlock();
+            const int rc = run_small_group(ix, grp);
+            lk.lock();
+            for (auto *r : grp) { r->rc = rc; r->done = true; }
+            ix->cmb_running--;
+            ix->cmb_cv.notify_all();
+            continue;
+        }
+        ix->cmb_cv.wait(lk);
+    }
+    return rq.rc;
+}
+
 // Host-API batches hold the index lock only to ship pending patches, pick up
 // the index's current device view and queue the kernels on the caller's lane;
 // they wait for the GPU and copy results out without it, so concurrent callers
@@ -2146,6 +2245,17 @@ int tm_match_batch32_ex(tm_index *ix, uint64_t n, const uint8_t *tb, const uint3
         uint8_t *dv = out_vals ? pinned_dev(ix, out_vals, cap * 4) : nullptr;
         uint8_t *de = out_err ? pinned_dev(ix, out_err, n) : nullptr;
         if ((db || !nbytes) && dof && dh && (dv || !out_vals) && (de || !out_err)) {
+            if (ix->cmb_leaders > 0 && de) {   // through the combiner (the flags have a home)
+                g.unlock();
+                SmallReq rq;
+                rq.n = n; rq.db = db; rq.dof = dof; rq.dh = dh; rq.de = de; rq.dv = dv; rq.cap = dv ? cap : 0;
+                const int rc = small_combined(ix, rq);
+                if (rc != CMB_LEGACY) {
+                    if (rc) return rc;
+                    return (out_vals && out_hit[n] > cap) ? TM_ECAP : TM_OK;
+                }
+                g.lock();
+            }
             LaneLease lease{ix, g};
             int rc;
             if ((rc = host_lane(ix, g, lease.ln))) return rc;
@@ -2323,6 +2433,11 @@ int tm_debug_set(tm_index *ix, uint32_t key, uint64_t value) {
     case TM_DEBUG_LB_FAIL_BLOCK: ix->dbg_lb.fail_block = value > 0xFFFFFFFFull ? NONE : (uint32_t)value; break;
     case TM_DEBUG_LB_LAUNCHES: ix->dbg_lb_launches = value; break;
     case TM_DEBUG_PHASES: ix->dbg_phases = value != 0; break;
+    case TM_DEBUG_COMBINE: {
+        std::lock_guard<std::mutex> c(ix->cmb_mu);
+        ix->cmb_leaders = value > 16 ? 16 : (int)value;
+        break;
+    }
     case TM_DEBUG_LB_DEFER:
         ix->lb_defer = value > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)value;
         ix->dbg_lb.defer = ix->lb_defer;
@@ -2340,6 +2455,8 @@ int tm_debug_get(tm_index *ix, uint32_t key, uint64_t *value) {
     case TM_DEBUG_PATH_PHASES: *value = ix->path_batches[PATH_PHASES].load(); break;
     case TM_DEBUG_PATH_SMALL: *value = ix->path_batches[PATH_SMALL].load(); break;
     case TM_DEBUG_PATH_ONE: *value = ix->path_batches[PATH_ONE].load(); break;
+    case TM_DEBUG_COMBINED_LAUNCHES: *value = ix->cmb_launches.load(); break;
+    case TM_DEBUG_COMBINED_BATCHES: *value = ix->cmb_batches.load(); break;
     case TM_DEBUG_DEFERRED_BLOCKS: {   // every lane's counter, after its batches (device memory: copied back)
         std::lock_guard<std::mutex> g(ix->mu);
         uint64_t v = 0;

@@ -1132,10 +1132,32 @@ bool one_pass_ok(const DevIndex &ix) {
 // OT: the offsets' type, in and out -- uint64_t (tm_match_batch*), or uint32_t
 // (tm_match_batch32*: half the offset bytes of an in-place host batch cross
 // PCIe in each direction)
+// sg.count > 0 (count mode): the launch carries several host batches
+// (SmallSegs); each block finds its segment and works on it as a launch of
+// that batch alone would -- its own block index, look-back region and last block.
 template <int MODE, class OT>
-__global__ __launch_bounds__(WV_BLOCK) void k_walk_small(DevIndex ix, Workspace ws, uint64_t n, const uint8_t *blob,
-                                                         const OT *offs, Outs o, OT *hit_offs,
-                                                         uint32_t *out, uint64_t cap, uint32_t tag, LbCtl lb) {
+__global__ __launch_bounds__(WV_BLOCK) void k_walk_small(DevIndex ix, Workspace ws, uint64_t n_, const uint8_t *blob_,
+                                                         const OT *offs_, Outs o, OT *hit_offs_,
+                                                         uint32_t *out_, uint64_t cap_, uint32_t tag, LbCtl lb,
+                                                         SmallSegs sg) {
+    uint64_t n = n_, cap = cap_;
+    const uint8_t *blob = blob_;
+    const OT *offs = offs_;
+    OT *hit_offs = hit_offs_;
+    uint32_t *out = out_;
+    uint32_t vb = blockIdx.x, nblk = gridDim.x, sb0 = 0;   // sb0: the segment's first block
+    if (MODE == MODE_COUNT && sg.count) {
+        uint32_t k = 0;
+        while (k + 1 < sg.count && blockIdx.x >= sg.s[k + 1].block0) k++;
+        const SmallSeg &S = sg.s[k];
+        n = S.n; cap = S.cap; blob = S.blob;
+        offs = static_cast<const OT *>(S.offs);
+        hit_offs = static_cast<OT *>(S.hit);
+        out = S.out; o.err = S.err;
+        sb0 = S.block0;
+        nblk = (k + 1 < sg.count ? sg.s[k + 1].block0 : gridDim.x) - sb0;
+        vb = blockIdx.x - sb0;
+    }
     constexpr int W = WAVE_W;
     constexpr uint32_t G = 64 / W;                        // topics per wave
     constexpr uint32_t MAXL = W < 31 ? W : 31;
@@ -1167,7 +1189,6 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_small(DevIndex ix, Workspace 
     // blocks scan in blockIdx order: workgroups are dispatched in that order,
     // so a block's predecessors are running or done (a start-order ticket, one
     // atomic on one word per block, serialised the blocks: k_walk_one's study)
-    const uint32_t vb = blockIdx.x;
     // the block's SM_TOPICS + 1 topic offsets, read once by one wave (the
     // caller's buffers may be host memory: one coalesced read, not one per group)
     if (threadIdx.x <= SM_TOPICS && (uint64_t)vb * SM_TOPICS + threadIdx.x <= n)
@@ -1369,14 +1390,14 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_small(DevIndex ix, Workspace 
         // one flag round trip per 64 predecessors (look_back); a failed wait
         // fails this block and every later one: err 4, the fail word raised
         int res;
-        const uint64_t pre = look_back<false>(ws.look, vb, tag, sum, lb, res);
+        const uint64_t pre = look_back<false>(ws.look + (uint64_t)sb0 * LB_STRIDE, vb, tag, sum, lb, res);
         const bool fail = res != LBR_OK;
         if (threadIdx.x == 0) {
             s_fail = fail;
             s_sum = sum;
             s_base = pre;
             if (fail) ws.hint_d[HINT_FAIL] = 1;
-            if (vb == gridDim.x - 1 && !fail) hit_offs[n] = (OT)(pre + sum);
+            if (vb == nblk - 1 && !fail) hit_offs[n] = (OT)(pre + sum);
         }
     }
     __syncthreads();
@@ -2401,7 +2422,7 @@ hipError_t launch_match(const DevIndex &ix, const Workspace &ws, uint64_t n, con
         if (ev_walk0 && (e = hipEventRecord(ev_walk0, s)) != hipSuccess) return e;
         if (n <= SMALL_TOPICS)
             hipLaunchKernelGGL((k_walk_small<MODE_COUNT, uint64_t>), dim3(blocks_for(n, SM_TOPICS)), dim3(WV_BLOCK), 0,
-                               s, ix, ws, n, bytes, offs, o, hit_offs, out, cap, tag & LB_TAG_MASK, lb);
+                               s, ix, ws, n, bytes, offs, o, hit_offs, out, cap, tag & LB_TAG_MASK, lb, SmallSegs{});
         if (n > SMALL_TOPICS) {
             const OneArgs a{n, bytes, offs, ws.look, err, hit_offs, out, cap, ws.cnt, ws.nr, ws.rng,
                             tag & LB_TAG_MASK, lb};
@@ -2428,7 +2449,30 @@ hipError_t launch_match32(const DevIndex &ix, const Workspace &ws, uint64_t n, c
     if (!small_path_ok(ix, n)) return hipErrorInvalidValue;   // (the caller converts instead)
     Outs o{err, nullptr, nullptr};
     hipLaunchKernelGGL((k_walk_small<MODE_COUNT, uint32_t>), dim3(blocks_for(n, SM_TOPICS)), dim3(WV_BLOCK), 0, s, ix,
-                       ws, n, bytes, offs, o, hit_offs, out, cap, tag & LB_TAG_MASK, lb);
+                       ws, n, bytes, offs, o, hit_offs, out, cap, tag & LB_TAG_MASK, lb, SmallSegs{});
+    return hipGetLastError();
+}
+
+// the combiner's launch: sg's segments (block0 filled here) in one grid
+hipError_t launch_small_segs(const DevIndex &ix, const Workspace &ws, const SmallSegs &sg0, bool u32, uint32_t tag,
+                             LbCtl lb, hipStream_t s) {
+    SmallSegs sg = sg0;
+    uint32_t blocks = 0;
+    for (uint32_t k = 0; k < sg.count; k++) {
+        if (!sg.s[k].n) return hipErrorInvalidValue;
+        sg.s[k].block0 = blocks;
+        blocks += blocks_for(sg.s[k].n, SM_TOPICS);
+    }
+    if (!sg.count || sg.count > (uint32_t)SMALL_SEGS) return hipErrorInvalidValue;
+    Outs o{sg.s[0].err, nullptr, nullptr};
+    if (u32)
+        hipLaunchKernelGGL((k_walk_small<MODE_COUNT, uint32_t>), dim3(blocks), dim3(WV_BLOCK), 0, s, ix, ws,
+                           (uint64_t)sg.s[0].n, sg.s[0].blob, static_cast<const uint32_t *>(sg.s[0].offs), o,
+                           static_cast<uint32_t *>(sg.s[0].hit), sg.s[0].out, sg.s[0].cap, tag & LB_TAG_MASK, lb, sg);
+    else
+        hipLaunchKernelGGL((k_walk_small<MODE_COUNT, uint64_t>), dim3(blocks), dim3(WV_BLOCK), 0, s, ix, ws,
+                           (uint64_t)sg.s[0].n, sg.s[0].blob, static_cast<const uint64_t *>(sg.s[0].offs), o,
+                           static_cast<uint64_t *>(sg.s[0].hit), sg.s[0].out, sg.s[0].cap, tag & LB_TAG_MASK, lb, sg);
     return hipGetLastError();
 }
 
@@ -2459,7 +2503,8 @@ hipError_t launch_first(const DevIndex &ix, const Workspace &ws, uint64_t n, con
     Outs o{nullptr, out_value, out_found};
     if (small_path_ok(ix, n)) {
         hipLaunchKernelGGL((k_walk_small<MODE_FIRST, uint64_t>), dim3(blocks_for(n, SM_TOPICS)), dim3(WV_BLOCK), 0, s,
-                           ix, ws, n, bytes, offs, o, nullptr, nullptr, (uint64_t)0, 0u, LbCtl{LB_SPINS, NONE, LB_DEFER});
+                           ix, ws, n, bytes, offs, o, nullptr, nullptr, (uint64_t)0, 0u, LbCtl{LB_SPINS, NONE, LB_DEFER},
+                           SmallSegs{});
         return hipGetLastError();
     }
     if (n <= WAVE_TOPICS)

@@ -304,15 +304,20 @@ int tm_profile_read(tm_index *h, double *walk_ms, double *batch_ms, uint64_t *ba
  *   TM_DEBUG_LB_DEFER       k_walk_one: polls of a predecessor still walking
  *                           before a block parks its results for k_one_finish
  *                           (0: every block that would wait parks)
+ *   TM_DEBUG_COMBINE        concurrent combined launches of small 32-bit
+ *                           in-place host batches (tm_match_batch32_ex): 0 =
+ *                           every batch its own launch (default 4)
  * tm_debug_get: TM_DEBUG_FAILED_BATCHES (one-launch batches whose look-back
  * failed, host API), TM_DEBUG_RETRIED_BATCHES (of those, run again) and the
  * match launches per kernel path: TM_DEBUG_PATH_PHASES (walk, tails, scan,
  * emit), TM_DEBUG_PATH_SMALL (k_walk_small), TM_DEBUG_PATH_ONE (k_walk_one),
- * and TM_DEBUG_DEFERRED_BLOCKS: k_walk_one blocks that parked (after the
- * batches finished). */
+ * TM_DEBUG_DEFERRED_BLOCKS: k_walk_one blocks that parked (after the
+ * batches finished), and TM_DEBUG_COMBINED_LAUNCHES / _BATCHES: the
+ * combiner's launches and the host batches they carried. */
 enum { TM_DEBUG_LB_SPINS = 1, TM_DEBUG_LB_FAIL_BLOCK = 2, TM_DEBUG_LB_LAUNCHES = 3, TM_DEBUG_PHASES = 4,
        TM_DEBUG_FAILED_BATCHES = 5, TM_DEBUG_RETRIED_BATCHES = 6, TM_DEBUG_PATH_PHASES = 7,
-       TM_DEBUG_PATH_SMALL = 8, TM_DEBUG_PATH_ONE = 9, TM_DEBUG_LB_DEFER = 10, TM_DEBUG_DEFERRED_BLOCKS = 11 };
+       TM_DEBUG_PATH_SMALL = 8, TM_DEBUG_PATH_ONE = 9, TM_DEBUG_LB_DEFER = 10, TM_DEBUG_DEFERRED_BLOCKS = 11,
+       TM_DEBUG_COMBINE = 12, TM_DEBUG_COMBINED_LAUNCHES = 13, TM_DEBUG_COMBINED_BATCHES = 14 };
 int tm_debug_set(tm_index *h, uint32_t key, uint64_t value);
 int tm_debug_get(tm_index *h, uint32_t key, uint64_t *value);
 

@@ -2173,6 +2173,83 @@ def test_router_boot_1m_routes_and_node_down_cleanup(torch_dev):
     assert r._filters.stats()["n_keys"] == len(routes) - len(dead)
 
 
+def test_combined_small_batches_equal_single_launches(torch_dev):
+    """The host-batch combiner (tm_host.cpp small_combined): concurrent callers'
+    in-place 32-bit batches of 1 to 20k topics run as shared k_walk_small
+    launches with a segment table -- each caller's hit offsets, values and
+    flags identical to its batch run alone (combiner off) and to the oracle;
+    a badarg topic stays in its own slot; a forced look-back failure reruns
+    the whole launch once (every caller still exact)."""
+    import threading
+    fs = wl.filters(3, 200_000)
+    ix, o = gpu_index(fs), oracle_of(fs)
+    sizes = [1, 7, 100, 640, 3000, 4096, 9000, 20_000]
+    sets = []
+    for k, nt in enumerate(sizes):
+        ts = wl.topics(3, 200_000, nt, first=k * 50_000)
+        items = [ts.item(i) for i in range(nt)]
+        if nt >= 100:
+            items[nt // 2] = b"bad/+/topic"   # badarg in its own slot
+        blob, offs = _native.pack_strings(items)
+        pb = ix.host_array(len(blob) + 16, np.uint8)
+        pb[: len(blob)] = blob
+        po = ix.host_array(nt + 1, np.uint32)
+        po[:] = offs.astype(np.uint32)
+        cap = 64 * nt + 64
+        outs = [(ix.host_array(nt + 1, np.uint32), ix.host_array(cap, np.uint32), ix.host_array(nt, np.uint8))
+                for _ in range(2)]
+        sets.append((pb, po, outs, items))
+    # alone: combiner off, then the oracle
+    ix.debug_set(_native.TM_DEBUG_COMBINE, 0)
+    ref = []
+    for pb, po, outs, items in sets:
+        h, v, e = ix.match_batch32(pb, po, outs[0])
+        ref.append((h.copy(), v.copy(), e.copy()))
+        bl, of = _native.pack_strings(items)
+        oc, _, ohit, ovals = o.match_batch(bl, of)
+        for i in range(len(items)):
+            if e[i]:
+                assert b"+" in items[i] or b"#" in items[i]
+                continue
+            assert np.array_equal(v[h[i]:h[i + 1]], ovals[int(ohit[i]):int(ohit[i + 1])])
+    ix.debug_set(_native.TM_DEBUG_COMBINE, 3)
+    l0 = ix.debug_get(_native.TM_DEBUG_COMBINED_LAUNCHES)
+    b0 = ix.debug_get(_native.TM_DEBUG_COMBINED_BATCHES)
+    errors = []
+
+    def caller(k, rounds):
+        pb, po, outs, _ = sets[k]
+        try:
+            for _ in range(rounds):
+                h, v, e = ix.match_batch32(pb, po, outs[1])
+                rh, rv, re_ = ref[k]
+                if not (np.array_equal(h, rh) and np.array_equal(v, rv) and np.array_equal(e, re_)):
+                    errors.append(k)
+                    return
+        except Exception as ex:   # noqa: BLE001 -- reported below
+            errors.append((k, repr(ex)))
+
+    def run(rounds):
+        th = [threading.Thread(target=caller, args=(k, rounds)) for k in range(len(sets))]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+
+    run(40)
+    assert not errors, errors
+    launches = ix.debug_get(_native.TM_DEBUG_COMBINED_LAUNCHES) - l0
+    batches = ix.debug_get(_native.TM_DEBUG_COMBINED_BATCHES) - b0
+    assert batches == 40 * len(sets) and launches < batches, (launches, batches)   # some launches carried several
+    # a forced look-back failure in the next combined launch: rerun, exact
+    f0 = ix.debug_get(_native.TM_DEBUG_FAILED_BATCHES)
+    ix.debug_set(_native.TM_DEBUG_LB_FAIL_BLOCK, 0)   # (block 0 of every segment)
+    ix.debug_set(_native.TM_DEBUG_LB_LAUNCHES, 1)
+    run(3)
+    assert not errors, errors
+    assert ix.debug_get(_native.TM_DEBUG_FAILED_BATCHES) == f0 + 1
+
+
 @pytest.mark.parametrize("nt", [1, 3000, 65536, 70_000])
 def test_u32_offsets_api_equals_u64(torch_dev, nt):
     """tm_match_batch32_ex / tm_match_batch32_dev: u32 topic
