@@ -262,7 +262,7 @@ struct tm_index {
     std::condition_variable cmb_cv;
     std::deque<struct SmallReq *> cmb_q;
     int cmb_running = 0;
-    int cmb_leaders = CMB_LEADERS;
+    std::atomic<int> cmb_leaders{CMB_LEADERS};
     std::atomic<uint64_t> cmb_launches{0}, cmb_batches{0};
 };
 
@@ -2050,7 +2050,7 @@ static int small_combined(tm_index *ix, SmallReq &rq) {
     std::unique_lock<std::mutex> lk(ix->cmb_mu);
     ix->cmb_q.push_back(&rq);
     while (!rq.done) {
-        if (ix->cmb_running < std::max(ix->cmb_leaders, 1) && !ix->cmb_q.empty()) {
+        if (ix->cmb_running < std::max(ix->cmb_leaders.load(), 1) && !ix->cmb_q.empty()) {
             std::vector<SmallReq *> grp;
             uint64_t total = 0;
             while (!ix->cmb_q.empty() && grp.size() < (size_t)SMALL_SEGS &&
@@ -2433,11 +2433,7 @@ int tm_debug_set(tm_index *ix, uint32_t key, uint64_t value) {
     case TM_DEBUG_LB_FAIL_BLOCK: ix->dbg_lb.fail_block = value > 0xFFFFFFFFull ? NONE : (uint32_t)value; break;
     case TM_DEBUG_LB_LAUNCHES: ix->dbg_lb_launches = value; break;
     case TM_DEBUG_PHASES: ix->dbg_phases = value != 0; break;
-    case TM_DEBUG_COMBINE: {
-        std::lock_guard<std::mutex> c(ix->cmb_mu);
-        ix->cmb_leaders = value > 16 ? 16 : (int)value;
-        break;
-    }
+    case TM_DEBUG_COMBINE: ix->cmb_leaders = value > 16 ? 16 : (int)value; break;
     case TM_DEBUG_LB_DEFER:
         ix->lb_defer = value > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)value;
         ix->dbg_lb.defer = ix->lb_defer;
