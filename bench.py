@@ -110,9 +110,10 @@ def parse():
                         "device entries, native feeder threads submitting in-place host batches while a syncer thread "
                         "applies deltas (the NIF's deployment, INTEGRATION.md 5); with fewer GPUs than N the entries "
                         "repeat the local device -- a rehearsal, not scaling")
-    p.add_argument("--large-path", default="default", choices=["default", "one", "phases"],
-                   help="batches above 65536 topics: the library's default, k_walk_one (one launch) or the "
-                        "two-phase path (TM_DEBUG_PHASES)")
+    p.add_argument("--small-kernel", default="auto", choices=["auto", "wave", "lane"],
+                   help="the one-launch kernel of batches <= 65536 topics (latency and concurrent-caller legs): "
+                        "the library's default, k_walk_small (16 lanes per topic) or k_walk_lane "
+                        "(TM_DEBUG_SMALL_KERNEL)")
     return p.parse_args()
 
 
@@ -199,8 +200,8 @@ def main():
     t = time.time()
     copies = a.copies
     ix = _native.Index(device=local, hint_keys=len(fs), copies=copies)
-    if a.large_path != "default":
-        ix.debug_set(_native.TM_DEBUG_PHASES, int(a.large_path == "phases"))
+    if a.small_kernel != "auto":
+        ix.debug_set(_native.TM_DEBUG_SMALL_KERNEL, {"wave": _native.SMALL_WAVE, "lane": _native.SMALL_LANE}[a.small_kernel])
     chunk = 2_000_000
     for lo in range(0, len(fs), chunk):
         part = fs.slice(lo, min(lo + chunk, len(fs)))
@@ -370,20 +371,20 @@ def main():
     iso_launch(*d_in[0])
     ix.profile(True)
     paths0 = [ix.debug_get(k) for k in (_native.TM_DEBUG_PATH_PHASES, _native.TM_DEBUG_PATH_SMALL,
-                                        _native.TM_DEBUG_PATH_ONE)]
+                                        _native.TM_DEBUG_PATH_LANE)]
     for _ in range(iso_passes):
         for d_blob, d_offs in d_in:
             iso_launch(d_blob, d_offs)
     torch.cuda.synchronize()
     iso_walk_ms, iso_batch_ms, iso_nb = ix.profile_read(reset=True)
     ix.profile(False)
-    # the kernel the events bracketed: k_walk_one (the whole batch in one launch:
-    # walk, look-back scan and emit), k_walk_small, or k_walk_fast (the walk of
-    # the two-phase path)
+    # the kernel the events bracketed: k_walk_fast (the walk of the two-phase
+    # path), or for a batch of <= 65536 topics the one-launch k_walk_small /
+    # k_walk_lane (walk, look-back scan and emit)
     paths1 = [ix.debug_get(k) for k in (_native.TM_DEBUG_PATH_PHASES, _native.TM_DEBUG_PATH_SMALL,
-                                        _native.TM_DEBUG_PATH_ONE)]
+                                        _native.TM_DEBUG_PATH_LANE)]
     path = max(range(3), key=lambda i: paths1[i] - paths0[i])
-    kernel = ("k_walk_fast", "k_walk_small", "k_walk_one")[path]
+    kernel = ("k_walk_fast", "k_walk_small", "k_walk_lane")[path]
     one_launch = path != 0
     el_t = torch.tensor([el], dtype=torch.float64, device=cdev)
     if world > 1:
@@ -432,12 +433,18 @@ def main():
                 hh, _, _ = ix.match_batch(sub.blob, sub.offs)
                 cap = int(np.diff(hh.astype(np.int64)).reshape(nth, lb).sum(axis=1).max()) + 65536
                 out = (ctypes.c_double * 6)()
+                fr0 = [ix.debug_get(k) for k in (_native.TM_DEBUG_FAILED_BATCHES, _native.TM_DEBUG_RETRIED_BATCHES)]
                 rc = hb.tmb_callers_ex(ix._h, nth, lb, _native._ptr(sub.blob), _native._ptr(sub.offs), cap, 1.0, churn,
                                        mode, out)
                 assert rc == 0, rc
+                fr1 = [ix.debug_get(k) for k in (_native.TM_DEBUG_FAILED_BATCHES, _native.TM_DEBUG_RETRIED_BATCHES)]
                 conc.append({"threads": nth, "topics_per_batch": lb, "batches": int(out[0]),
                              "topics_per_s": round(out[1], 1), "p50_ms": round(out[2], 4), "p99_ms": round(out[3], 4),
                              "deltas_per_s": round(out[4], 1), "offsets": "u32" if mode == 4 else "u64",
+                             # one-launch batches whose look-back wait expired (err 4; each is run
+                             # again once, a second failure is TM_EDEVICE): forward progress under
+                             # concurrent launches, measured
+                             "failed_batches": fr1[0] - fr0[0], "retried_batches": fr1[1] - fr0[1],
                              "callers": "native threads, tm_host_alloc buffers each (in place)"})
         if B >= 65536:
             allt = wl.concat(tsets)
@@ -723,13 +730,16 @@ def replica_leg(a, fs, ix, ts, local):
         hh, _, _ = rx.match_batch(s2.blob, s2.offs)
         cap = int(np.diff(hh.astype(np.int64)).reshape(nth, lb).sum(axis=1).max()) + 65536
         before = [rx.replica_stats(r)[0] for r in range(a.replicas)]
+        fr0 = [rx.debug_get(k) for k in (_native.TM_DEBUG_FAILED_BATCHES, _native.TM_DEBUG_RETRIED_BATCHES)]
         out = (ctypes.c_double * 6)()
         rc = hb.tmb_callers_ex(rx._h, nth, lb, _native._ptr(s2.blob), _native._ptr(s2.offs), cap, 2.0, churn, 4, out)
         assert rc == 0, rc
+        fr1 = [rx.debug_get(k) for k in (_native.TM_DEBUG_FAILED_BATCHES, _native.TM_DEBUG_RETRIED_BATCHES)]
         per = [rx.replica_stats(r)[0] - before[r] for r in range(a.replicas)]
         legs.append({"feeder_threads": nth, "topics_per_batch": lb, "topics_per_s": round(out[1], 1),
                      "p50_ms": round(out[2], 4), "p99_ms": round(out[3], 4), "deltas_per_s": round(out[4], 1),
-                     "batches_per_replica": per})
+                     "batches_per_replica": per, "failed_batches": fr1[0] - fr0[0],
+                     "retried_batches": fr1[1] - fr0[1]})
     st = rx.stats()
     rx.close()
     return {"replicas": a.replicas, "devices": devices,

@@ -29,9 +29,11 @@ EXPORTS = ("tm_create", "tm_destroy", "tm_apply_deltas", "tm_sync", "tm_match_ba
            "tm_match_batch32_dev")
 TM_DEBUG_LB_SPINS, TM_DEBUG_LB_FAIL_BLOCK, TM_DEBUG_LB_LAUNCHES, TM_DEBUG_PHASES = 1, 2, 3, 4
 TM_DEBUG_FAILED_BATCHES, TM_DEBUG_RETRIED_BATCHES = 5, 6
-TM_DEBUG_PATH_PHASES, TM_DEBUG_PATH_SMALL, TM_DEBUG_PATH_ONE = 7, 8, 9
-TM_DEBUG_LB_DEFER, TM_DEBUG_DEFERRED_BLOCKS = 10, 11
+TM_DEBUG_PATH_PHASES, TM_DEBUG_PATH_SMALL, TM_DEBUG_PATH_LANE = 7, 8, 9
+TM_DEBUG_SMALL_KERNEL = 10
+SMALL_AUTO, SMALL_WAVE, SMALL_LANE = 0, 1, 2
 TM_DEBUG_COMBINE, TM_DEBUG_COMBINED_LAUNCHES, TM_DEBUG_COMBINED_BATCHES = 12, 13, 14
+TM_DEBUG_WIDE_NODES, TM_DEBUG_DENSE_WIDE = 15, 16
 
 
 class NativeUnavailable(RuntimeError):

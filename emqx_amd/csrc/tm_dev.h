@@ -41,15 +41,14 @@ constexpr int DEEP_LANES = 64;   // lanes of the global-scratch (deep / overflow
 enum { L_MID = 0, L_DEEP = 1, L_OVF_MID = 2, L_OVF_DEEP = 3, L_COUNT = 4 };
 
 // Per-batch device scratch (grow-only, owned by the index).
-// The one-launch kernels' (k_walk_small, k_walk_one) look-back word of a
+// The one-launch kernels' (k_walk_small, k_walk_lane) look-back word of a
 // block: launch tag (19 bits), state (LB_AGG: its own hit total; LB_INCL: the
 // total of it and every block before it; LB_FAIL: its wait expired, or a
-// predecessor's did -- every later block fails too; LB_DEF: its own total, the
-// block parked its results and left, k_one_finish emits them) and the value
-// (42 bits) in ONE 64-bit word, so a reader gets state and value from one
-// coherent load (no acquire / release: those write back and invalidate the
-// whole L2 of the XCD, under every kernel running there)
-enum : uint32_t { LB_AGG = 1, LB_INCL = 2, LB_FAIL = 3, LB_DEF = 4 };
+// predecessor's did -- every later block fails too) and the value (42 bits)
+// in ONE 64-bit word, so a reader gets state and value from one coherent load
+// (no acquire / release: those write back and invalidate the whole L2 of the
+// XCD, under every kernel running there)
+enum : uint32_t { LB_AGG = 1, LB_INCL = 2, LB_FAIL = 3 };
 constexpr uint32_t LB_TAG_BITS = 19, LB_TAG_MASK = (1u << LB_TAG_BITS) - 1;
 constexpr uint64_t LB_VAL_MASK = (1ull << 42) - 1;
 __host__ __device__ constexpr uint64_t lb_word(uint32_t tag, uint32_t st, uint64_t v) {
@@ -58,25 +57,21 @@ __host__ __device__ constexpr uint64_t lb_word(uint32_t tag, uint32_t st, uint64
 __host__ __device__ constexpr uint32_t lb_tag(uint64_t w) { return (uint32_t)(w >> 45); }
 __host__ __device__ constexpr uint32_t lb_state(uint64_t w) { return (uint32_t)(w >> 42) & 7u; }
 
-// The look-back's bounded wait.  A block waits only for blocks that took their
-// start ticket before it (so they are running and publish soon); the bound
-// keeps a lost publication (e.g. a predecessor's waves preempted for long) from
-// leaving a spinning grid behind: past it the block and every later one flag
-// their topics err 4 and raise the workspace's fail word, and the host API
-// runs the batch again (tm_host.cpp retry_or_fail).
+// The look-back's bounded wait.  A block waits only for blocks that started
+// before it (so they are running and publish soon); the bound keeps a lost
+// publication (e.g. a predecessor's waves preempted for long) from leaving a
+// spinning grid behind: past it the block and every later one flag their
+// topics err 4 and raise the workspace's fail word, and the host API runs the
+// batch again (tm_host.cpp retry_or_fail).
 constexpr uint32_t LB_SPINS = 1u << 22;   // polls of one predecessor word (LB_SLEEP apart: >= 0.1 s)
 constexpr uint32_t LB_SLEEP = 1;          // s_sleep between polls of a word not yet published (x 64 clocks)
 constexpr uint32_t LB_STRIDE = 1;         // 8-B words between consecutive blocks' look-back words
-// k_walk_one: polls of a predecessor still walking before the block parks its
-// results (LB_DEF) instead of holding its slot: one slow block would otherwise
-// stall every block after it that finished meanwhile (a convoy filling the GPU
-// with waiting waves)
-constexpr uint32_t LB_DEFER = 8;
 struct LbCtl {
     uint32_t spins;        // the bound (LB_SPINS; tm_debug_set can lower it)
-    uint32_t fail_block;   // test hook: this block acts as if its wait expired (k_walk_one: parks) (NONE: off)
-    uint32_t defer;        // k_walk_one: LB_DEFER (tm_debug_set can change it)
+    uint32_t fail_block;   // test hook: this block acts as if its wait expired (NONE: off)
 };
+
+constexpr int SMALL_SEGS = 16;   // host batches one combined small launch can carry (SmallSegs)
 
 struct Workspace {
     uint32_t *cnt;        // [n] hits per topic
@@ -85,13 +80,12 @@ struct Workspace {
     uint32_t *lists;      // [(L_COUNT + 1) * n] topic lists (the last one: long segments to sort)
     uint32_t *list_n;     // [L_COUNT] list lengths, [L_COUNT] reset ticket, [L_COUNT + 1] scan ticket,
                           // [L_COUNT + 2] long-segment count, [L_COUNT + 3] its reset ticket,
-                          // [LS_NPARK] k_walk_one blocks parked in this batch (k_one_scan -> k_one_finish),
-                          // [LS_PARKED] k_walk_one blocks parked so far (diagnostics)
+                          // [LS_TICK + k] k_walk_lane's start-order ticket of segment k (zero between launches)
     uint64_t *blk;        // [n / TILE + 2] tile hit totals -> exclusive tile prefixes (zero between batches)
     uint32_t *deep_wid;   // [DEEP_LANES * MAX_LEVELS]
     uint2 *deep_stk;      // [DEEP_LANES * (MAX_LEVELS + 1)]
     uint8_t *deep_plus;   // [DEEP_LANES * MAX_LEVELS] '+' levels of each deep lane's path
-    uint64_t *look;       // [(n / SM_TOPICS + 4) * LB_STRIDE] one-launch path: per block, one look-back word (lb_word)
+    uint64_t *look;       // [(n / SM_TOPICS + 4) * LB_STRIDE] one-launch kernels: per block, one look-back word (lb_word)
     // list lengths of the last count-mode batch that finished here ([0, L_COUNT))
     // and its topic count ([L_COUNT]; 0: none yet), written by the device into
     // mapped host memory: the next batch sizes its tail grids from them;
@@ -102,9 +96,8 @@ struct Workspace {
 };
 
 constexpr int TILE = 256;    // topics per walk block = per scan tile = per emit block
-constexpr int LS_NPARK = L_COUNT + 4;     // Workspace::list_n word: k_walk_one blocks parked in this batch
-constexpr int LS_PARKED = L_COUNT + 5;   // Workspace::list_n word: k_walk_one blocks that parked, so far (diagnostics)
-constexpr int LIST_SLOTS = L_COUNT + 6;   // Workspace::list_n entries
+constexpr int LS_TICK = L_COUNT + 4;      // Workspace::list_n words: k_walk_lane's tickets, one per segment
+constexpr int LIST_SLOTS = LS_TICK + SMALL_SEGS;   // Workspace::list_n entries
 constexpr int HINT_FAIL = L_COUNT + 1;    // Workspace::hint_* word of the fail flag
 constexpr int HINT_WORDS = L_COUNT + 2;
 constexpr int SM_TOPICS = 16;             // topics per block of the one-launch small-batch path
@@ -123,39 +116,43 @@ hipError_t launch_match_phase1(const DevIndex &ix, const Workspace &ws, uint64_t
 hipError_t launch_match_phase2(const DevIndex &ix, const Workspace &ws, uint64_t n, const uint8_t *bytes,
                                const uint64_t *offs, uint64_t *hit_offs, uint32_t *out, uint64_t cap,
                                hipStream_t s);
-// The whole batch in ONE launch when the index allows it: k_walk_small up to
-// SMALL_TOPICS topics (one_launch_ok: its depth fits the fallback store),
-// k_walk_one above (one_pass_ok: a shallow index without '#'-not-last keys);
-// the two phases otherwise (or when `phases` forces them: tests of that
-// path).  `tag` must differ between consecutive launches on one workspace (the
-// one-launch look-back scan tells its own blocks' words from older ones by it).  A one-launch batch whose
-// look-back failed flags its topics err 4 and sets ws.hint_h[HINT_FAIL].
+// The whole batch in ONE launch when the index allows it: up to SMALL_TOPICS
+// topics (small_path_ok: the fallback store of k_walk_small holds the
+// index's depth) on k_walk_lane (one lane per topic, lane_path_ok: a shallow
+// index without '#'-not-last keys) or k_walk_small (16 lanes per topic); the
+// two phases otherwise (or when `phases` forces them: tests of that path).
+// `tag` must differ between consecutive launches on one workspace (the
+// one-launch look-back scan tells its own blocks' words from older ones by
+// it).  A one-launch batch whose look-back failed flags its topics err 4 and
+// sets ws.hint_h[HINT_FAIL].
 bool small_path_ok(const DevIndex &ix, uint64_t n);
 bool one_launch_ok(const DevIndex &ix);
-bool one_pass_ok(const DevIndex &ix);   // k_walk_one's condition (large batches)
-enum { PATH_PHASES = 0, PATH_SMALL = 1, PATH_ONE = 2, PATH_COUNT = 3 };   // *path of launch_match
+bool lane_path_ok(const DevIndex &ix);   // k_walk_lane's condition
+enum { SMALL_AUTO = 0, SMALL_WAVE = 1, SMALL_LANE = 2 };   // which one-launch kernel (small_kind)
+bool small_lane(const DevIndex &ix, int small_kind);
+enum { PATH_PHASES = 0, PATH_SMALL = 1, PATH_LANE = 2, PATH_COUNT = 3 };   // *path of launch_match
 hipError_t launch_match(const DevIndex &ix, const Workspace &ws, uint64_t n, const uint8_t *bytes,
                         const uint64_t *offs, uint64_t *hit_offs, uint8_t *err, uint32_t *out, uint64_t cap,
-                        uint32_t tag, LbCtl lb, bool phases, hipStream_t s, hipEvent_t ev_walk0 = nullptr,
-                        hipEvent_t ev_walk1 = nullptr, int *path = nullptr);
-// The one-launch small batch with 32-bit offsets in and out (hipErrorInvalidValue
-// if small_path_ok refuses the batch), and the 32 <-> 64-bit offset copies
-// Several host batches in ONE k_walk_small launch (the host's combiner,
+                        uint32_t tag, LbCtl lb, bool phases, int small_kind, hipStream_t s,
+                        hipEvent_t ev_walk0 = nullptr, hipEvent_t ev_walk1 = nullptr, int *path = nullptr);
+// Several host batches in ONE one-launch small kernel (the host's combiner,
 // tm_host.cpp small_combined): segment k owns the launch's blocks
-// [block0, next block0), its own inputs and outputs and its own look-back
-// region; a launch holds at most SMALL_SEGS segments of at most SMALL_TOPICS
-// topics together.  Offsets are uint64_t or uint32_t for the whole launch.
-constexpr int SMALL_SEGS = 16;
+// [block0, next block0), its own inputs and outputs, its own look-back region
+// and (k_walk_lane) its own ticket word; a launch holds at most SMALL_SEGS
+// segments of at most SMALL_TOPICS topics together.  Offsets are uint64_t or
+// uint32_t for the whole launch.
 struct SmallSeg {
     const uint8_t *blob; const void *offs; void *hit; uint8_t *err; uint32_t *out;
     uint64_t cap; uint32_t n, block0;
 };
 struct SmallSegs { uint32_t count, pad; SmallSeg s[SMALL_SEGS]; };
 hipError_t launch_small_segs(const DevIndex &ix, const Workspace &ws, const SmallSegs &sg, bool u32, uint32_t tag,
-                             LbCtl lb, hipStream_t s);
+                             LbCtl lb, int small_kind, hipStream_t s, int *path = nullptr);
+// The one-launch small batch with 32-bit offsets in and out (hipErrorInvalidValue
+// if small_path_ok refuses the batch), and the 32 <-> 64-bit offset copies
 hipError_t launch_match32(const DevIndex &ix, const Workspace &ws, uint64_t n, const uint8_t *bytes,
                           const uint32_t *offs, uint32_t *hit_offs, uint8_t *err, uint32_t *out, uint64_t cap,
-                          uint32_t tag, LbCtl lb, hipStream_t s);
+                          uint32_t tag, LbCtl lb, int small_kind, hipStream_t s, int *path = nullptr);
 hipError_t launch_offs_widen(const uint32_t *in, uint64_t *out, uint64_t m, hipStream_t s);
 hipError_t launch_offs_narrow(const uint64_t *in, uint32_t *out, uint64_t m, hipStream_t s);
 hipError_t launch_first(const DevIndex &ix, const Workspace &ws, uint64_t n, const uint8_t *bytes,

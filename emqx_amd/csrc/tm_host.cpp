@@ -23,6 +23,7 @@
 #include <mutex>
 #include <string>
 #include <map>
+#include <unordered_map>
 #include <unordered_set>
 #include <set>
 #include <vector>
@@ -143,10 +144,6 @@ struct Replica {
     uint64_t batches = 0;                     // host-API batches served (tm_replica_stats)
 };
 
-// Large batches (> 65536 topics) on an index one_pass_ok accepts: the two-phase
-// path (true) or k_walk_one (false) by default; TM_DEBUG_PHASES switches it
-// per index (which one is faster on C3, measured)
-constexpr bool LARGE_PHASES_DEFAULT = true;
 
 constexpr int MAX_HOST_LANES = 16;   // concurrent host-API batches in flight, per replica
 constexpr int MAX_DEV_LANES = 16;    // device-API streams with a workspace kept
@@ -186,6 +183,12 @@ struct tm_index {
     Mirror<uint32_t> wseq; uint64_t wseq_dead = 0;   // words of erased long exact keys
     Mirror<uint32_t> wbits; uint32_t wb_words = 0;   // wide nodes' child bitmaps, wb_words words each
     std::vector<uint32_t> free_wbits; std::set<uint32_t> wide;
+    // literal edges per (level, wid) and distinct edge words per level: a wide
+    // node whose children cover most of its level's words probes its child
+    // table directly (its line's bitmap pointer NONE, wide_dense)
+    std::unordered_map<uint64_t, uint32_t> lvl_edges;
+    std::vector<uint32_t> lvl_distinct;
+    bool dense_dirty = false;
 
     // levels a walk must resolve (DevIndex::depth / xlen_*): live nodes per
     // depth and live exact keys per level count
@@ -248,10 +251,10 @@ struct tm_index {
     // test hooks (tm_debug_set, under mu): the look-back control of the next
     // dbg_lb_launches one-launch batches, and the two-phase path forced for
     // large batches
-    LbCtl dbg_lb{LB_SPINS, NONE, LB_DEFER};
+    LbCtl dbg_lb{LB_SPINS, NONE};
     uint64_t dbg_lb_launches = 0;
-    uint32_t lb_defer = LB_DEFER;   // k_walk_one's polls before a block parks (TM_DEBUG_LB_DEFER)
-    bool dbg_phases = LARGE_PHASES_DEFAULT;
+    bool dbg_phases = false;        // TM_DEBUG_PHASES: small batches on the two-phase path too (tests)
+    int small_kind = SMALL_AUTO;    // TM_DEBUG_SMALL_KERNEL: which one-launch kernel takes small batches
     std::atomic<uint64_t> failed_batches{0}, retried_batches{0};   // one-launch look-back failures seen / retried
     std::atomic<uint64_t> path_batches[PATH_COUNT] = {};             // match launches per kernel path
     // The host-batch combiner (small_combined): small in-place 32-bit batches
@@ -594,8 +597,9 @@ void wide_fill(tm_index *ix, uint32_t node) {
         if (w != NONE) ix->wbits.h[bm + (w >> 5)] |= 1u << (w & 31);
     }
     ix->wbits.touch(bm, ix->wb_words);
-    n.kw[2] = bm;
+    n.kw[2] = bm;   // (wide_dense may point a dense node's line away from it again)
     ix->nodes.touch(node);
+    ix->dense_dirty = true;
 }
 
 uint32_t wide_alloc(tm_index *ix) {
@@ -733,11 +737,56 @@ void to_table(tm_index *ix, uint32_t node, uint32_t cap) {
         set_bloom(m, c.wid);
     }
     m.kw[0] = off; m.kw[1] = cap - 1;
-    if (ix->aux[node].bm != NONE) m.kw[2] = ix->aux[node].bm;   // wide: the bitmap, not the Bloom
+    if (ix->aux[node].bm != NONE) {   // wide: the bitmap, not the Bloom (wide_dense decides again)
+        m.kw[2] = ix->aux[node].bm;
+        ix->dense_dirty = true;
+    }
+}
+
+// A literal edge with word `wid` appears at / leaves level `lvl`.
+void lvl_edge(tm_index *ix, uint32_t lvl, uint32_t wid, bool add) {
+    const uint64_t k = (uint64_t)lvl << 32 | wid;
+    if (ix->lvl_distinct.size() <= lvl) ix->lvl_distinct.resize(lvl + 1, 0);
+    if (add) {
+        if (ix->lvl_edges[k]++ == 0) { ix->lvl_distinct[lvl]++; ix->dense_dirty |= !ix->wide.empty(); }
+    } else {
+        auto it = ix->lvl_edges.find(k);
+        if (it != ix->lvl_edges.end() && --it->second == 0) {
+            ix->lvl_edges.erase(it);
+            ix->lvl_distinct[lvl]--;
+            ix->dense_dirty |= !ix->wide.empty();
+        }
+    }
+}
+
+// Dense wide nodes.  A wide node's bitmap line answers "may w be a child?"
+// before its child table is probed: one more L2 request in the chain of every
+// visit, worth it only where the answer is often no.  C3's level-1 nodes and
+// the root's '+' child have (nearly) every word of their level as a child, so
+// their bitmap is pure overhead on almost every topic; there the line's
+// bitmap pointer is NONE and the walk probes the table at once.  Dense: the
+// node's children are at least DENSE_NUM/DENSE_DEN of the distinct words
+// that appear as literal edges at its children's level anywhere in the trie
+// (the words a topic reaching it is likely to carry there).  Re-evaluated for
+// every wide node when an edge count changed, before the next patch.
+constexpr uint64_t DENSE_NUM = 3, DENSE_DEN = 5;
+void wide_dense(tm_index *ix) {
+    if (!ix->dense_dirty) return;
+    ix->dense_dirty = false;
+    for (uint32_t node : ix->wide) {
+        Node &n = ix->nodes.h[node];
+        const uint32_t lvl = ix->aux[node].depth;
+        const uint64_t distinct = lvl < ix->lvl_distinct.size() ? ix->lvl_distinct[lvl] : 0;
+        const bool dense = (uint64_t)nlit_of(n) * DENSE_DEN >= distinct * DENSE_NUM;
+        const uint32_t want = dense ? NONE : ix->aux[node].bm;
+        if (n.kw[2] != want) { n.kw[2] = want; ix->nodes.touch(node); }
+    }
 }
 
 void child_add(tm_index *ix, uint32_t node, uint32_t wid, uint32_t child) {
     ix->nlinks++;
+    lvl_edge(ix, ix->aux[node].depth, wid, true);
+    if (ix->aux[node].bm != NONE) ix->dense_dirty = true;
     Node *n = &ix->nodes.h[node];
     if (nlit_of(*n) < KINL) {
         for (uint32_t k = 0; k < KINL; k++)
@@ -758,6 +807,8 @@ void child_add(tm_index *ix, uint32_t node, uint32_t wid, uint32_t child) {
 
 void child_remove(tm_index *ix, uint32_t node, uint32_t wid) {
     ix->nlinks--;
+    lvl_edge(ix, ix->aux[node].depth, wid, false);
+    if (ix->aux[node].bm != NONE) ix->dense_dirty = true;
     Node &n = ix->nodes.h[node];
     if (nlit_of(n) <= KINL) {
         for (uint32_t k = 0; k < KINL; k++)
@@ -1186,7 +1237,7 @@ int next_tag(tm_index *ix, Lane &ln, hipStream_t s, uint32_t &tag) {
 // the look-back control of the next launch (caller holds ix->mu): the
 // default bound, or the test hook's for the next dbg_lb_launches launches
 LbCtl next_lb(tm_index *ix) {
-    if (!ix->dbg_lb_launches) return LbCtl{LB_SPINS, NONE, ix->lb_defer};
+    if (!ix->dbg_lb_launches) return LbCtl{LB_SPINS, NONE};
     ix->dbg_lb_launches--;
     return ix->dbg_lb;
 }
@@ -1626,7 +1677,7 @@ int drain_lanes(tm_index *ix) {
 
 extern "C" {
 
-uint32_t tm_abi_version(void) { return (1u << 16) | 7u; }
+uint32_t tm_abi_version(void) { return (1u << 16) | 8u; }
 
 const char *tm_last_error(tm_index *) { return g_last_error.c_str(); }
 
@@ -1735,6 +1786,7 @@ int tm_apply_deltas_ex(tm_index *ix, uint64_t n, const uint8_t *ops, const uint8
             key_op(ix, ops[i] == TM_OP_INSERT, fb + fo[i], (uint32_t)(fo[i + 1] - fo[i]), values[i],
                    key_flags ? key_flags[i] : 0, w, wids);
         reclaim(ix);
+        wide_dense(ix);
     } catch (const std::bad_alloc &) {
         return fail(ix, TM_ENOMEM, "tm_apply_deltas: out of host memory");
     }
@@ -1818,7 +1870,7 @@ int tm_match_batch_dev_ex(tm_index *ix, uint64_t n, const uint8_t *bytes, const 
     // (asynchronous: a failed look-back reaches the caller as err 4 flags, include/tmatch.h)
     int path = PATH_PHASES;
     HIPCHK(ix, launch_match(d, ln->w, n, bytes, offs, hit_offs, err, out, out ? cap : 0, tag, next_lb(ix),
-                            ix->dbg_phases, s, ev.w0, ev.w1, &path));
+                            ix->dbg_phases, ix->small_kind, s, ev.w0, ev.w1, &path));
     ix->path_batches[path]++;
     if (order != TM_ORDER_TRAVERSAL && out)
         HIPCHK(ix, launch_sort_segments(ln->w, n, hit_offs, out, cap, order == TM_ORDER_UNIQUE, ucnt, s));
@@ -2033,8 +2085,9 @@ static int run_small_group(tm_index *ix, const std::vector<SmallReq *> &grp) {
         const DevIndex d = dev_view(ix, ln.r);
         uint32_t tag;
         if ((rc = next_tag(ix, ln, s, tag))) return rc;
-        HIPCHK(ix, launch_small_segs(d, ln.w, sg, true, tag, next_lb(ix), s));
-        ix->path_batches[PATH_SMALL]++;
+        int path = PATH_SMALL;
+        HIPCHK(ix, launch_small_segs(d, ln.w, sg, true, tag, next_lb(ix), ix->small_kind, s, &path));
+        ix->path_batches[path]++;
         ix->cmb_launches++;
         ix->cmb_batches += grp.size();
         if ((rc = batch_done(ix, ln))) return rc;
@@ -2125,7 +2178,8 @@ int tm_match_batch_ex(tm_index *ix, uint64_t n, const uint8_t *tb, const uint64_
                 if (int rc = next_tag(ix, ln, s, tag)) return rc;
                 int path = PATH_PHASES;
                 HIPCHK(ix, launch_match(d, ln.w, n, dbytes, reinterpret_cast<const uint64_t *>(dof), dhit, de, vdst,
-                                        dv ? cap : 0, tag, next_lb(ix), ix->dbg_phases, s, nullptr, nullptr, &path));
+                                        dv ? cap : 0, tag, next_lb(ix), ix->dbg_phases, ix->small_kind, s, nullptr,
+                                        nullptr, &path));
                 ix->path_batches[path]++;
                 if (sorted && dv) {
                     HIPCHK(ix, launch_sort_segments(ln.w, n, dhit, vdst, cap, unique, reinterpret_cast<uint32_t *>(du), s));
@@ -2178,7 +2232,7 @@ int tm_match_batch_ex(tm_index *ix, uint64_t n, const uint8_t *tb, const uint64_
         if (int rc = next_tag(ix, ln, s, tag)) return rc;
         int path = PATH_PHASES;
         HIPCHK(ix, launch_match(d, ln.w, n, dbytes, doffs, dhit, derr, vdst, ln.pin_vals_cap, tag, next_lb(ix),
-                                ix->dbg_phases, s, nullptr, nullptr, &path));
+                                ix->dbg_phases, ix->small_kind, s, nullptr, nullptr, &path));
         ix->path_batches[path]++;
         if (sorted) {
             HIPCHK(ix, launch_sort_segments(ln.w, n, dhit, vdst, ln.pin_vals_cap, unique, dunq, s));
@@ -2270,10 +2324,11 @@ int tm_match_batch32_ex(tm_index *ix, uint64_t n, const uint8_t *tb, const uint3
                     const DevIndex d = dev_view(ix, ln.r);
                     uint32_t tag;
                     if ((rc = next_tag(ix, ln, s, tag))) return rc;
+                    int path = PATH_SMALL;
                     HIPCHK(ix, launch_match32(d, ln.w, n, db ? db : dof, reinterpret_cast<const uint32_t *>(dof),
                                               reinterpret_cast<uint32_t *>(dh), de, reinterpret_cast<uint32_t *>(dv),
-                                              dv ? cap : 0, tag, next_lb(ix), s));
-                    ix->path_batches[PATH_SMALL]++;
+                                              dv ? cap : 0, tag, next_lb(ix), ix->small_kind, s, &path));
+                    ix->path_batches[path]++;
                     if ((rc = batch_done(ix, ln))) return rc;
                     g.unlock();
                     HIPCHK(ix, hipStreamSynchronize(s));
@@ -2324,9 +2379,11 @@ int tm_match_batch32_dev(tm_index *ix, uint64_t n, const uint8_t *bytes, const u
     if ((rc = next_tag(ix, *ln, s, tag))) return rc;
     if (small_path_ok(d, n)) {
         if (ev.w0) HIPCHK(ix, hipEventRecord(ev.w0, s));
-        HIPCHK(ix, launch_match32(d, ln->w, n, bytes, offs, hit_offs, err, out, out ? cap : 0, tag, next_lb(ix), s));
+        int path = PATH_SMALL;
+        HIPCHK(ix, launch_match32(d, ln->w, n, bytes, offs, hit_offs, err, out, out ? cap : 0, tag, next_lb(ix),
+                                  ix->small_kind, s, &path));
         if (ev.w1) HIPCHK(ix, hipEventRecord(ev.w1, s));
-        ix->path_batches[PATH_SMALL]++;
+        ix->path_batches[path]++;
     } else {
         // widened into the lane's scratch, matched, narrowed into the caller's offsets
         if ((rc = grow_dev(ix, s, ln->d_o64, ln->d_o64_cap, n + 1))) return rc;
@@ -2334,7 +2391,7 @@ int tm_match_batch32_dev(tm_index *ix, uint64_t n, const uint8_t *bytes, const u
         HIPCHK(ix, launch_offs_widen(offs, ln->d_o64, n + 1, s));
         int path = PATH_PHASES;
         HIPCHK(ix, launch_match(d, ln->w, n, bytes, ln->d_o64, ln->d_h64, err, out, out ? cap : 0, tag, next_lb(ix),
-                                ix->dbg_phases, s, ev.w0, ev.w1, &path));
+                                ix->dbg_phases, ix->small_kind, s, ev.w0, ev.w1, &path));
         ix->path_batches[path]++;
         HIPCHK(ix, launch_offs_narrow(ln->d_h64, hit_offs, n + 1, s));
     }
@@ -2434,9 +2491,9 @@ int tm_debug_set(tm_index *ix, uint32_t key, uint64_t value) {
     case TM_DEBUG_LB_LAUNCHES: ix->dbg_lb_launches = value; break;
     case TM_DEBUG_PHASES: ix->dbg_phases = value != 0; break;
     case TM_DEBUG_COMBINE: ix->cmb_leaders = value > 16 ? 16 : (int)value; break;
-    case TM_DEBUG_LB_DEFER:
-        ix->lb_defer = value > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)value;
-        ix->dbg_lb.defer = ix->lb_defer;
+    case TM_DEBUG_SMALL_KERNEL:
+        if (value > SMALL_LANE) return fail(ix, TM_EINVAL, "tm_debug_set: TM_DEBUG_SMALL_KERNEL is 0, 1 or 2");
+        ix->small_kind = (int)value;
         break;
     default: return fail(ix, TM_EINVAL, "tm_debug_set: unknown key");
     }
@@ -2450,20 +2507,14 @@ int tm_debug_get(tm_index *ix, uint32_t key, uint64_t *value) {
     case TM_DEBUG_RETRIED_BATCHES: *value = ix->retried_batches.load(); break;
     case TM_DEBUG_PATH_PHASES: *value = ix->path_batches[PATH_PHASES].load(); break;
     case TM_DEBUG_PATH_SMALL: *value = ix->path_batches[PATH_SMALL].load(); break;
-    case TM_DEBUG_PATH_ONE: *value = ix->path_batches[PATH_ONE].load(); break;
+    case TM_DEBUG_PATH_LANE: *value = ix->path_batches[PATH_LANE].load(); break;
     case TM_DEBUG_COMBINED_LAUNCHES: *value = ix->cmb_launches.load(); break;
     case TM_DEBUG_COMBINED_BATCHES: *value = ix->cmb_batches.load(); break;
-    case TM_DEBUG_DEFERRED_BLOCKS: {   // every lane's counter, after its batches (device memory: copied back)
-        std::lock_guard<std::mutex> g(ix->mu);
+    case TM_DEBUG_WIDE_NODES:
+    case TM_DEBUG_DENSE_WIDE: {   // wide nodes / those of them that probe their table without the bitmap
+        std::lock_guard<std::mutex> g(ix->img);
         uint64_t v = 0;
-        for (auto &l : ix->lanes) {
-            if (!l->w.list_n) continue;
-            uint32_t c = 0;
-            HIPCHK(ix, hipSetDevice(ix->rep[l->r].device));
-            if (l->used) HIPCHK(ix, hipEventSynchronize(l->done));
-            HIPCHK(ix, hipMemcpy(&c, l->w.list_n + LS_PARKED, 4, hipMemcpyDeviceToHost));
-            v += c;
-        }
+        for (uint32_t node : ix->wide) v += key == TM_DEBUG_WIDE_NODES || ix->nodes.h[node].kw[2] == NONE;
         *value = v;
         break;
     }

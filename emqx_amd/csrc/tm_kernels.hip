@@ -47,12 +47,15 @@ __device__ __forceinline__ uint32_t bloom_bit(const uint4 &n2, const uint4 &n3, 
 }
 
 // may a table-mode node (line words n1, n2, n3) have a literal child for word
-// w?  Wide nodes answer exactly from their bitmap (an L2-resident line), the
-// others from the 192-bit Bloom in the line
+// w?  Wide nodes answer exactly from their bitmap (an L2-resident line) --
+// unless the node is dense (its line's bitmap pointer NONE: nearly every word
+// of its level is a child, tm_host.cpp wide_dense), where the answer is
+// almost always yes and the table is probed at once -- the others from the
+// 192-bit Bloom in the line
 __device__ __forceinline__ uint32_t child_maybe(const DevIndex &ix, const uint4 &n1, const uint4 &n2, const uint4 &n3,
                                                 uint32_t w, uint32_t h) {
     if ((n1.y & NLIT_MASK) >= WIDE_LIT)
-        return w < ix.wcap ? (ix.wbits[n2.z + (w >> 5)] >> (w & 31)) & 1u : 0u;
+        return n2.z == NONE ? 1u : w < ix.wcap ? (ix.wbits[n2.z + (w >> 5)] >> (w & 31)) & 1u : 0u;
     return bloom_bit(n2, n3, child_bit(h));
 }
 
@@ -100,28 +103,63 @@ struct WordAcc {
     }
 };
 
-__device__ bool bytes_eq(const uint8_t *a, const uint8_t *b, uint32_t n) {
-    for (uint32_t i = 0; i < n; i++) if (a[i] != b[i]) return false;
+// Where a walk reads its topic's bytes (offsets are the batch's own):
+//  - GlobalSrc: the batch in global memory (HBM, or mapped host memory for
+//    in-place host batches), or any byte pointer;
+//  - StagedSrc: the block's byte span copied into LDS by coalesced loads
+//    (k_walk_lane), read at offset p - b0 from the LDS array itself -- never
+//    through a pointer rebased below it.  (The round-4 stage1 study formed
+//    `s_stage - B0`: the compiler did that arithmetic on the 32-bit LDS
+//    address, which wraps for B0 above the array's LDS offset, then cast it to
+//    a flat pointer whose 64-bit add of the topic offset carried into the
+//    aperture bits: HSA_STATUS_ERROR_MEMORY_APERTURE_VIOLATION on every block
+//    with B0 > 0x1300, so 1- and 64-topic batches (one block, B0 = 0) passed
+//    and the 1,024-topic batch faulted -- DESIGN.md 8.)  When the span does not
+//    fit (`staged` false, block-uniform) the lanes read global memory.
+struct GlobalSrc {
+    const uint8_t *g;
+    __device__ __forceinline__ uint4 ld16(uint64_t p) const { return ld4_once(g + p); }
+    __device__ __forceinline__ uint32_t byte(uint64_t p) const { return g[p]; }
+};
+struct StagedSrc {
+    const uint8_t *g;
+    const uint4 *lds;
+    uint64_t b0;
+    bool staged;
+    __device__ __forceinline__ uint4 ld16(uint64_t p) const {
+        return staged ? lds[(uint32_t)(p - b0) >> 4] : ld4_once(g + p);
+    }
+    __device__ __forceinline__ uint32_t byte(uint64_t p) const {
+        return staged ? reinterpret_cast<const uint8_t *>(lds)[(uint32_t)(p - b0)] : g[p];
+    }
+};
+
+template <class Src>
+__device__ bool bytes_eq(const uint8_t *a, const Src &src, uint64_t b, uint32_t n) {
+    for (uint32_t i = 0; i < n; i++) if (a[i] != src.byte(b + i)) return false;
     return true;
 }
 
-__device__ __forceinline__ uint64_t word_hash_dev(const WordAcc &w, const uint8_t *blob) {
+template <class Src>
+__device__ __forceinline__ uint64_t word_hash_dev(const WordAcc &w, const Src &src) {
     if (w.len <= VINL) return word_hash_short(w.b0, w.b1, w.len);
     uint64_t h = FNV_OFF;   // FNV-1a, as the host's word_hash (tm_host.cpp)
-    for (uint32_t i = 0; i < w.len; i++) h = (h ^ blob[w.start + i]) * FNV_PRIME;
+    for (uint32_t i = 0; i < w.len; i++) h = (h ^ src.byte(w.start + i)) * FNV_PRIME;
     return word_hash_finish(h, w.len);
 }
 
-// continue a vocab probe sequence from `slot` (exact: tag, then bytes)
+// continue a vocab probe sequence from `slot` (exact: tag, then bytes: the
+// word at `start` of src when it is longer than VINL)
+template <class Src>
 __device__ uint32_t vocab_probe(const DevIndex &ix, uint32_t slot, uint32_t tag, uint32_t len, uint32_t b0,
-                                uint32_t b1, const uint8_t *bytes) {
+                                uint32_t b1, const Src &src, uint64_t start) {
     for (;;) {
         const uint4 e = ld4(ix.vocab + slot);   // tag, wid, b0, b1
         if (e.y == NONE) return NONE;
         if (e.x == tag) {
             if (len <= VINL) {
                 if (e.z == b0 && e.w == b1) return e.y;
-            } else if (e.w == len && bytes_eq(ix.wpool + e.z, bytes, len)) {
+            } else if (e.w == len && bytes_eq(ix.wpool + e.z, src, start, len)) {
                 return e.y;
             }
         }
@@ -129,10 +167,21 @@ __device__ uint32_t vocab_probe(const DevIndex &ix, uint32_t slot, uint32_t tag,
     }
 }
 
+// the same for a word of <= VINL bytes (tag, then its packed bytes)
+__device__ uint32_t vocab_probe_short(const DevIndex &ix, uint32_t slot, uint32_t tag, uint32_t b0, uint32_t b1) {
+    for (;;) {
+        const uint4 e = ld4(ix.vocab + slot);   // tag, wid, b0, b1
+        if (e.y == NONE) return NONE;
+        if (e.x == tag && e.z == b0 && e.w == b1) return e.y;
+        slot = (slot + 1) & ix.vmask;
+    }
+}
+
 // vocab: word -> wid, exact by construction (hash tag, then length and bytes)
-__device__ uint32_t vocab_find(const DevIndex &ix, const WordAcc &w, const uint8_t *blob) {
-    const uint64_t h = word_hash_dev(w, blob);
-    return vocab_probe(ix, (uint32_t)h & ix.vmask, vocab_tag(h, w.len), w.len, w.b0, w.b1, blob + w.start);
+template <class Src>
+__device__ uint32_t vocab_find(const DevIndex &ix, const WordAcc &w, const Src &src) {
+    const uint64_t h = word_hash_dev(w, src);
+    return vocab_probe(ix, (uint32_t)h & ix.vmask, vocab_tag(h, w.len), w.len, w.b0, w.b1, src, w.start);
 }
 
 // literal child in a node's private table (table mode, nlit > KINL), with the
@@ -158,10 +207,10 @@ __device__ __forceinline__ uint32_t ctab_find(const DevIndex &ix, uint32_t off, 
 // main walk's store does not: a topic that meets such a cut is handed to the
 // tail lists (DFS_REROUTE), keeping k_walk_fast within its register budget.
 //
-// LITE (k_walk_one's second look at a topic deeper than FAST_L): the main
+// LITE (k_walk_lane's second look at a topic deeper than FAST_L): the main
 // walk's FAST_L levels, but tokenised like the deeper stores -- every level
 // scanned (count, badarg), only the levels a walk can use resolved
-// (need_levels) -- which one_pass_ok guarantees fit FAST_L.
+// (need_levels) -- which lane_path_ok guarantees fit FAST_L.
 template <int ML, bool LITE = false>
 struct LdsStore {
     static constexpr uint32_t maxl = ML;
@@ -248,12 +297,14 @@ constexpr uint32_t VGROUP = 6;
 
 // '/' bytes in [p, end), p 16-byte aligned: four 16-byte loads in flight per
 // round trip, bytes compared a word at a time
-__device__ __noinline__ uint32_t count_slashes(const uint8_t *blob, uint64_t p, uint64_t end) {
+template <class Src>
+__device__ __noinline__ uint32_t count_slashes(const Src src, uint64_t p, uint64_t end) {   // (by value: a reference to a
+                                                                                            // temporary put it in scratch)
     uint32_t n = 0;
     for (; p < end; p += 64) {
         uint4 v[4];
 #pragma unroll
-        for (int c = 0; c < 4; c++) v[c] = p + 16 * c < end ? ld4_once(blob + p + 16 * c) : make_uint4(0, 0, 0, 0);
+        for (int c = 0; c < 4; c++) v[c] = p + 16 * c < end ? src.ld16(p + 16 * c) : make_uint4(0, 0, 0, 0);
 #pragma unroll
         for (int c = 0; c < 4; c++) {
             const uint32_t w[4] = {v[c].x, v[c].y, v[c].z, v[c].w};
@@ -282,8 +333,8 @@ __device__ __noinline__ uint32_t count_slashes(const uint8_t *blob, uint64_t p, 
 // Then the vocab probes of up to VGROUP levels are issued together, so a topic's
 // words cost one memory round trip instead of one per level, and the lanes of a
 // wave no longer serialise on the byte position where each of their words ends.
-template <class S>
-__device__ int tokenize(const DevIndex &ix, const uint8_t *blob, uint64_t beg, uint64_t end, S &st,
+template <class S, class Src>
+__device__ int tokenize(const DevIndex &ix, const Src &src, uint64_t beg, uint64_t end, S &st,
                         uint32_t &L, bool &dollar, uint64_t &xh, bool &all_found) {
     uint64_t longmask = 0;   // levels resolved before the deferred probes
     all_found = true; dollar = false; xh = FNV_OFF;
@@ -291,8 +342,8 @@ __device__ int tokenize(const DevIndex &ix, const uint8_t *blob, uint64_t beg, u
     // aligned 16-byte loads (the first two issued together): a chunk shares its 16-byte granule with a valid
     // byte, so it never crosses a page the caller does not own
     const uint4 z = make_uint4(0, 0, 0, 0);
-    const uint4 c0 = p0 < end ? ld4_once(blob + p0) : z;
-    const uint4 c1 = p0 + 16 < end ? ld4_once(blob + p0 + 16) : z;
+    const uint4 c0 = p0 < end ? src.ld16(p0) : z;
+    const uint4 c1 = p0 + 16 < end ? src.ld16(p0 + 16) : z;
     if constexpr (S::deferred) {
         // The scan keeps only (first 8 bytes, length) per word and parks them in
         // the level's LDS slots when a '/' ends it; the checks (badarg, depth,
@@ -325,9 +376,9 @@ __device__ int tokenize(const DevIndex &ix, const uint8_t *blob, uint64_t beg, u
             uint4 v;
             if constexpr (NEED) {
                 v = ra; ra = rb;
-                rb = p + 32 < end ? ld4_once(blob + p + 32) : z;
+                rb = p + 32 < end ? src.ld16(p + 32) : z;
             } else {
-                v = ci == 0 ? c0 : ci == 1 ? c1 : ld4_once(blob + p);
+                v = ci == 0 ? c0 : ci == 1 ? c1 : src.ld16(p);
             }
             const uint32_t k0 = p < beg ? (uint32_t)(beg - p) : 0;
             const uint32_t k1 = end - p < 16 ? (uint32_t)(end - p) : 16;
@@ -354,7 +405,7 @@ __device__ int tokenize(const DevIndex &ix, const uint8_t *blob, uint64_t beg, u
             // the rest is not scanned: a long topic made its whole wave wait
             const bool any = ix.xlen_max <= S::maxl && ix.depth + 2 <= (uint32_t)MID_L &&
                              end - beg < (uint64_t)MAX_LEVELS;
-            L = any ? lev + 1 : lev + 1 + count_slashes(blob, p, end);
+            L = any ? lev + 1 : lev + 1 + count_slashes(src, p, end);
             return RC_DEEP;
         }
         park();
@@ -373,11 +424,11 @@ __device__ int tokenize(const DevIndex &ix, const uint8_t *blob, uint64_t beg, u
             L |= Lw << 24;   // Lw rides in L's top byte until the probes are done
         }
         // base_init (:160-163): the first level starts with '$'
-        dollar = st.word_len(0) == 255 ? blob[beg] == '$' : st.word_len(0) >= 1 && (st.word_b0(0) & 0xFFu) == '$';
+        dollar = st.word_len(0) == 255 ? src.byte(beg) == '$' : st.word_len(0) >= 1 && (st.word_b0(0) & 0xFFu) == '$';
         for (uint32_t l = 0; l < (S::need ? L >> 24 : L); l++) {
             if (st.word_len(l) != 255) continue;
             WordAcc w; w.reset(beg + st.word_b1(l)); w.len = st.word_b0(l);
-            st.set_wid(l, vocab_find(ix, w, blob));
+            st.set_wid(l, vocab_find(ix, w, src));
             longmask |= 1ull << l;
         }
     } else {
@@ -387,13 +438,13 @@ __device__ int tokenize(const DevIndex &ix, const uint8_t *blob, uint64_t beg, u
             if (w.len == 1 && (w.b0 == '+' || w.b0 == '#')) return RC_BADARG;
             if (lev >= S::maxl) return RC_DEEP;
             if (lev == 0 && w.len >= 1 && (w.b0 & 0xFF) == '$') dollar = true;
-            st.set_wid(lev, vocab_find(ix, w, blob));
+            st.set_wid(lev, vocab_find(ix, w, src));
             lev++;
             return RC_OK;
         };
         uint32_t ci = 0;
         for (uint64_t p = p0; p < end; p += 16, ci++) {
-            const uint4 v = ci == 0 ? c0 : ci == 1 ? c1 : ld4_once(blob + p);
+            const uint4 v = ci == 0 ? c0 : ci == 1 ? c1 : src.ld16(p);
             const uint32_t k0 = p < beg ? (uint32_t)(beg - p) : 0;
             const uint32_t k1 = end - p < 16 ? (uint32_t)(end - p) : 16;
             for (uint32_t k = k0; k < k1; k++) {
@@ -442,7 +493,7 @@ __device__ int tokenize(const DevIndex &ix, const uint8_t *blob, uint64_t beg, u
                     if (wid == NONE - 1) {   // rare at load <= 1/2: walk the probe sequence on
                         const uint32_t len = st.word_len(l);
                         const uint64_t h = word_hash_short(b0, b1, len);
-                        wid = vocab_probe(ix, ((uint32_t)h + 1) & ix.vmask, tg[k], len, b0, b1, nullptr);
+                        wid = vocab_probe_short(ix, ((uint32_t)h + 1) & ix.vmask, tg[k], b0, b1);
                     }
                     st.set_wid(l, wid);
                 }
@@ -633,11 +684,11 @@ struct FirstEmit {          // match/2: stop at the first hit
     }
 };
 
-template <class S, class EM>
-__device__ __forceinline__ int match_topic(const DevIndex &ix, const uint8_t *blob, uint64_t beg, uint64_t end, S &st, EM &em,
-                            uint32_t *levels = nullptr) {
+template <class S, class EM, class Src>
+__device__ __forceinline__ int match_topic(const DevIndex &ix, const Src &src, uint64_t beg, uint64_t end, S &st,
+                                           EM &em, uint32_t *levels = nullptr) {
     uint32_t L = 0; bool dollar, allf; uint64_t xh;
-    int rc = tokenize(ix, blob, beg, end, st, L, dollar, xh, allf);
+    int rc = tokenize(ix, src, beg, end, st, L, dollar, xh, allf);
     if (levels) *levels = L;   // RC_DEEP: the topic's level count (the tail list's choice)
     if (rc) return rc;
     st.reset();
@@ -700,7 +751,7 @@ __device__ int run_topic(const DevIndex &ix, const Workspace &ws, uint64_t n, co
         RangeEmit em;
         em.cnt = 0; em.nr = 0;
         uint32_t levels;
-        int rc = match_topic(ix, blob, beg, end, st, em, &levels);
+        int rc = match_topic(ix, GlobalSrc{blob}, beg, end, st, em, &levels);
         // more levels than the global scratch holds (> 65536: longer than any
         // MQTT topic, emqx_mqtt.hrl:44): flagged err 2, no hits
         const bool toolong = rc == RC_DEEP && S::maxl == MAX_LEVELS;
@@ -720,7 +771,7 @@ __device__ int run_topic(const DevIndex &ix, const Workspace &ws, uint64_t n, co
     } else {
         FirstEmit em{ix.vals, 0, false};
         uint32_t levels;
-        int rc = match_topic(ix, blob, beg, end, st, em, &levels);
+        int rc = match_topic(ix, GlobalSrc{blob}, beg, end, st, em, &levels);
         const bool toolong = rc == RC_DEEP && S::maxl == MAX_LEVELS;
         if (rc == RC_DEEP && !toolong) { *hits = levels; return rc; }
         o.first_val[t] = toolong ? 0 : em.v;
@@ -745,31 +796,25 @@ __device__ __forceinline__ uint64_t wave_incl_scan(uint64_t v) {
 // Decoupled look-back of the one-launch kernels, by one whole wave: block vb
 // publishes its own total `sum` (LB_AGG), reads its predecessors' words 64 at
 // a time (lane k: block hi - k) back to the nearest inclusive prefix, summing
-// the totals in between (LB_AGG / LB_DEF), publishes its own inclusive prefix
-// and returns its exclusive one (in every lane).  A predecessor dispatched
-// before vb is running or done, so it publishes soon; the wait for one word is
-// still bounded:
-//  - k_walk_small (DEFER false): past lb.spins polls -- or when a predecessor
-//    failed, or vb is the test hook's lb.fail_block -- the result is LBR_FAIL
-//    and vb publishes LB_FAIL, which every later block meets and propagates:
-//    nothing after a failed block is trusted, the caller flags its topics err
-//    4 and raises the workspace's fail word (a failed block used to
-//    publish a partial prefix its successors took as correct);
-//  - k_walk_one (DEFER true): past lb.defer polls of a predecessor still
-//    walking (or for the hook's block) the result is LBR_DEFER: vb publishes
-//    LB_DEF with its own total -- later blocks sum it like LB_AGG -- parks its
-//    results and leaves; k_one_finish, after the kernel, emits them.
-enum { LBR_OK = 0, LBR_FAIL = 1, LBR_DEFER = 2 };
-template <bool DEFER>
+// the totals in between, publishes its own inclusive prefix and returns its
+// exclusive one (in every lane).  A predecessor started before vb (dispatch
+// order for k_walk_small, the start-order ticket for k_walk_lane), so it
+// publishes soon; the wait for one word is still bounded: past lb.spins polls
+// -- or when a predecessor failed, or vb is the test hook's lb.fail_block --
+// the result is LBR_FAIL and vb publishes LB_FAIL, which every later block
+// meets and propagates: nothing after a failed block is trusted, the caller
+// flags its topics err 4 and raises the workspace's fail word (a
+// failed block used to publish a partial prefix its successors took as
+// correct).
+enum { LBR_OK = 0, LBR_FAIL = 1 };
 __device__ __forceinline__ uint64_t look_back(uint64_t *look, uint32_t vb, uint32_t tag, uint64_t sum, const LbCtl &lb,
                                               int &res) {
     const uint32_t lane = threadIdx.x & 63;
     uint64_t pre = 0;
-    res = vb == lb.fail_block ? (DEFER ? LBR_DEFER : LBR_FAIL) : LBR_OK;
+    res = vb == lb.fail_block ? LBR_FAIL : LBR_OK;
     if (res == LBR_OK && vb > 0 && lane == 0)
         __hip_atomic_store(&look[(uint64_t)vb * LB_STRIDE], lb_word(tag, LB_AGG, sum), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
-    const uint32_t bound = DEFER ? lb.defer : lb.spins;
     uint32_t spins = 0;
     for (int64_t hi = (int64_t)vb - 1; hi >= 0 && res == LBR_OK;) {
         const int64_t j = hi - (int64_t)lane;
@@ -777,11 +822,10 @@ __device__ __forceinline__ uint64_t look_back(uint64_t *look, uint32_t vb, uint3
         if (j >= 0)
             for (;;) {
                 f = __hip_atomic_load(&look[(uint64_t)j * LB_STRIDE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (lb_tag(f) == tag || ++spins > bound) break;
+                if (lb_tag(f) == tag || ++spins > lb.spins) break;
                 __builtin_amdgcn_s_sleep(LB_SLEEP);
             }
-        if (__ballot(lb_tag(f) == tag && lb_state(f) == LB_FAIL)) { res = LBR_FAIL; break; }
-        if (__ballot(lb_tag(f) != tag)) { res = DEFER ? LBR_DEFER : LBR_FAIL; break; }
+        if (__ballot(lb_tag(f) != tag || lb_state(f) == LB_FAIL)) { res = LBR_FAIL; break; }
         const uint64_t mi = __ballot(lb_state(f) == LB_INCL);
         const uint32_t k = mi ? (uint32_t)__ffsll((long long)mi) - 1 : 63;   // nearest inclusive prefix
         uint64_t v = lane <= k ? f & LB_VAL_MASK : 0;
@@ -792,8 +836,7 @@ __device__ __forceinline__ uint64_t look_back(uint64_t *look, uint32_t vb, uint3
     }
     if (lane == 0)
         __hip_atomic_store(&look[(uint64_t)vb * LB_STRIDE],
-                           res == LBR_OK ? lb_word(tag, LB_INCL, pre + sum)
-                                         : lb_word(tag, res == LBR_DEFER ? LB_DEF : LB_FAIL, sum),
+                           res == LBR_OK ? lb_word(tag, LB_INCL, pre + sum) : lb_word(tag, LB_FAIL, sum),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return pre;
 }
@@ -965,7 +1008,7 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_wave(DevIndex ix, Workspace w
     const bool bad = mine && wl == 1 && (w.b0 == '+' || w.b0 == '#');
     const bool badarg = grp.ballot(bad) != 0;
     const bool dollar = grp.bcast(mine && wl >= 1 && (w.b0 & 0xFFu) == '$' ? 1u : 0u, 0) != 0;
-    uint32_t wid = mine && !badarg ? vocab_find(ix, w, blob) : NONE;
+    uint32_t wid = mine && !badarg ? vocab_find(ix, w, GlobalSrc{blob}) : NONE;
     const bool allf = grp.ballot(mine && wid == NONE) == 0;
     uint64_t xh = FNV_OFF;
     for (uint32_t l = 0; l < L; l++) xh = seq_hash_step(xh, grp.bcast(wid, l));
@@ -1121,14 +1164,6 @@ bool one_launch_ok(const DevIndex &ix) {
 
 bool small_path_ok(const DevIndex &ix, uint64_t n) { return n && n <= SMALL_TOPICS && one_launch_ok(ix); }
 
-// k_walk_one walks every topic with FAST_L-level stores: a topic deeper than
-// that needs only the levels down to the trie's depth (+2 look-ahead) when no
-// binary key is longer than FAST_L levels, and its main store makes no
-// '#'-not-last cut (the deeper stores' job)
-bool one_pass_ok(const DevIndex &ix) {
-    return !ix.hdesc && ix.depth + 2 <= (uint32_t)FAST_L && ix.xlen_max <= (uint32_t)FAST_L;
-}
-
 // OT: the offsets' type, in and out -- uint64_t (tm_match_batch*), or uint32_t
 // (tm_match_batch32*: half the offset bytes of an in-place host batch cross
 // PCIe in each direction)
@@ -1188,7 +1223,8 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_small(DevIndex ix, Workspace 
     __shared__ uint64_t s_sum;
     // blocks scan in blockIdx order: workgroups are dispatched in that order,
     // so a block's predecessors are running or done (a start-order ticket, one
-    // atomic on one word per block, serialised the blocks: k_walk_one's study)
+    // atomic on one word per block, serialised the blocks of a 64k batch:
+    // 4,096 tickets; k_walk_lane, 64 topics per block, takes one)
     // the block's SM_TOPICS + 1 topic offsets, read once by one wave (the
     // caller's buffers may be host memory: one coalesced read, not one per group)
     if (threadIdx.x <= SM_TOPICS && (uint64_t)vb * SM_TOPICS + threadIdx.x <= n)
@@ -1251,7 +1287,7 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_small(DevIndex ix, Workspace 
     const bool bad = mine && wl == 1 && (w.b0 == '+' || w.b0 == '#');
     const bool badarg = grp.ballot(bad) != 0;
     const bool dollar = grp.bcast(mine && wl >= 1 && (w.b0 & 0xFFu) == '$' ? 1u : 0u, 0) != 0;
-    uint32_t wid = mine && !badarg ? vocab_find(ix, w, tb) : NONE;   // (long words: bytes from LDS)
+    uint32_t wid = mine && !badarg ? vocab_find(ix, w, GlobalSrc{tb}) : NONE;   // (long words: bytes from LDS)
     const bool allf = grp.ballot(mine && wid == NONE) == 0;
     uint64_t xh = FNV_OFF;
     for (uint32_t l = 0; l < L && !fb; l++) xh = seq_hash_step(xh, grp.bcast(wid, l));
@@ -1357,11 +1393,11 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_small(DevIndex ix, Workspace 
     if (fb && gl == 0) {
         if (MODE == MODE_COUNT) {
             CountEmit em{0};
-            frc = match_topic(ix, blob, beg, end, st, em);
+            frc = match_topic(ix, GlobalSrc{blob}, beg, end, st, em);
             total = frc == RC_OK ? em.cnt : 0;
         } else {
             FirstEmit em{ix.vals, 0, false};
-            frc = match_topic(ix, blob, beg, end, st, em);
+            frc = match_topic(ix, GlobalSrc{blob}, beg, end, st, em);
             o.first_val[t] = frc == RC_OK ? em.v : 0;
             o.first_found[t] = frc == RC_BADARG ? 2 : frc == RC_DEEP ? 3 : (em.found ? 1 : 0);
         }
@@ -1390,7 +1426,7 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_small(DevIndex ix, Workspace 
         // one flag round trip per 64 predecessors (look_back); a failed wait
         // fails this block and every later one: err 4, the fail word raised
         int res;
-        const uint64_t pre = look_back<false>(ws.look + (uint64_t)sb0 * LB_STRIDE, vb, tag, sum, lb, res);
+        const uint64_t pre = look_back(ws.look + (uint64_t)sb0 * LB_STRIDE, vb, tag, sum, lb, res);
         const bool fail = res != LBR_OK;
         if (threadIdx.x == 0) {
             s_fail = fail;
@@ -1425,7 +1461,7 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_small(DevIndex ix, Workspace 
     if (live && fb) {
         if (gl == 0 && frc == RC_OK) {   // (never with stage)
             DirectEmit em{ix.vals, out, pos, cap};
-            match_topic(ix, blob, beg, end, st, em);
+            match_topic(ix, GlobalSrc{blob}, beg, end, st, em);
         }
     } else if (live) {
         uint32_t *roff = s_roff[wv] + base, *rcnt = s_rcnt[wv] + base;
@@ -1562,7 +1598,7 @@ template <class S>
 __device__ void rewalk(const DevIndex &ix, const uint8_t *blob, const uint64_t *offs, uint64_t t,
                        const uint64_t *hit_offs, uint32_t *out, uint64_t cap, S &st) {
     DirectEmit em{ix.vals, out, hit_offs[t], cap};
-    match_topic(ix, blob, offs[t], offs[t + 1], st, em);
+    match_topic(ix, GlobalSrc{blob}, offs[t], offs[t + 1], st, em);
 }
 
 __global__ __launch_bounds__(MID_BLOCK) void k_rewalk_tail(DevIndex ix, Workspace ws, uint64_t n, const uint8_t *blob,
@@ -1627,7 +1663,7 @@ constexpr uint8_t RF_INLINE = 1, RF_SKIP = 2;   // s_flg: a one-value run kept i
 // s_off = the range's value offset (RF_INLINE: the value itself), s_rel = its
 // first position relative to base (s_rel[R] = endp - base), s_flg (RF_SKIP: a
 // re-walked topic's positions, written by its re-walk).  Shared by k_emit
-// (ranges read back from the walk's range lists) and k_walk_one (ranges
+// (ranges read back from the walk's range lists) and k_walk_lane (ranges
 // straight from the walk's registers).
 __device__ __forceinline__ void wave_emit(const DevIndex &ix, const uint32_t *s_off, const uint32_t *s_rel,
                                           const uint8_t *s_flg, uint32_t R, uint64_t base, uint64_t endp,
@@ -1822,75 +1858,153 @@ __global__ __launch_bounds__(EMIT_BLOCK) void k_emit(DevIndex ix, Workspace ws, 
     wave_emit(ix, s_off[wv], s_rel[wv], s_flg[wv], R, base, endp, out, cap);
 }
 
-// ------------------------------------------------ large batches in one pass
+// ------------------------------------------ small batches, one lane per topic
 //
-// k_walk_one: the whole count-mode batch above SMALL_TOPICS topics in one
-// launch, plus k_one_finish for the blocks that parked.
-// The two-phase path (k_walk_fast, tails, k_scan_top, k_emit, k_rewalk_tail)
-// parks EVERY topic's value ranges in HBM between the walk and the emit --
-// 44 B/topic written and 73 B/topic read back on C3 -- and its three short
-// kernels queue behind other streams' walks for workgroup slots.  Here a
-// 64-lane block (one wave, one topic per lane)
-//   1. walks its topics exactly as k_walk_fast (the same dfs, LDS store and
-//      register ranges); a lane's ranges then wait in its own (dead) column of
-//      the walk store;
-//   2. counts the topics deeper than FAST_L levels with a second walk over the
-//      same LDS, tokenised with every level scanned and only the levels the
-//      trie can use resolved (LdsStore<FAST_L, true>; one_pass_ok: the index's
-//      depth and binary keys fit FAST_L, and it holds no '#'-not-last key);
-//   3. gets its global offset from the decoupled look-back (look_back<true>,
-//      over the blocks in dispatch order);
-//   4. writes its offsets and flags, and its values from the LDS ranges with
-//      wave_emit, as k_emit does per wave (one_emit);
-//   5. re-walks the topics whose values it could not keep (more than RCAP
-//      ranges, or deeper than FAST_L) and writes their values directly.
-// A block whose predecessors are still walking after LB_DEFER polls does not
-// wait on: it parks its counts, flags and ranges (as k_walk_fast would) and
-// publishes LB_DEF; after the kernel, k_one_scan gives the parked blocks their
-// prefixes (and writes hit_offs[n]) and k_one_finish emits them.
-// Waiting blocks hold their slots, so one slow block would stall every block
-// after it that finished meanwhile -- the GPU filling up with waiting waves.
-// Per topic of a block that does not park, only the CSR itself is written:
-// 8 B offset + 1 B flag + 4 B per value.
-static_assert(WALK_BLOCK == 64, "k_walk_one: one wave per block");
-union OneLds {   // a k_walk_one block's LDS, reused step by step (4864 B: 8 waves per SIMD as k_walk_fast)
-    struct { uint32_t wid[FAST_L * WALK_BLOCK], pend[(FAST_L + 1) * WALK_BLOCK]; uint8_t len[FAST_L * WALK_BLOCK]; } walk;
+// k_walk_lane: a count-mode batch of <= SMALL_TOPICS topics in ONE launch,
+// one lane per topic -- the throughput shape for the NIF's concurrent small
+// batches.  k_walk_small spends 16 lanes on a topic whose
+// frontier averages 2.4 states: it issues ~8x the instructions per topic of a
+// lane walk (a 4k C3 batch: ~2.9M) and tops out near 3.4e8 topics/s however
+// the batches arrive.  One 64-lane block (one wave, 64 topics):
+//   1. takes a start-order ticket (vb, per segment): every block with a lower
+//      ticket has started, so the look-back below only ever waits for blocks
+//      that are running -- forward progress by construction, whatever other
+//      launches hold the GPU's slots (64 topics per ticket,
+//      so a 4k batch takes 64 atomics on one word);
+//   2. reads its 65 topic offsets and stages its whole topic byte span in LDS
+//      with one round of coalesced 16-B loads (in-place host batches: one PCIe
+//      burst per block instead of a round trip per lane and chunk -- the
+//      round-4 lane walk without it was 2x slower); a span
+//      longer than LANE_TBQ chunks is read from global memory instead;
+//   3. walks each topic from there (StagedSrc) exactly as k_walk_fast does
+//      (dfs, LDS store, ranges in registers, parked in the lane's own store
+//      column); a topic deeper than FAST_L levels is counted by a second walk
+//      whose store resolves only need_levels() (lane_path_ok: the index's
+//      depth and binary keys fit FAST_L and it holds no '#'-not-last key);
+//   4. gets its global offset from the decoupled look-back over the blocks in
+//      ticket order (bounded wait: a failure flags err 4, the host reruns);
+//   5. writes its offsets and flags (64 coalesced stores each), then its
+//      values from the LDS ranges (wave_emit: 16-B stores, 1 KiB per
+//      instruction); topics with more than RCAP ranges, or deeper than
+//      FAST_L, re-walk and write theirs directly.
+// Several host batches in one launch (SmallSegs, the combiner): as k_walk_small.
+constexpr int LANE_BLOCK = 64;
+constexpr uint32_t LANE_TBQ = 256;   // 16-B chunks of topic bytes a block stages (4 KiB: 64 B per topic)
+static_assert(LANE_BLOCK == 64, "k_walk_lane: one wave per block");
+union LaneLds {   // a k_walk_lane block's LDS, reused step by step
+    struct { uint32_t wid[FAST_L * LANE_BLOCK], pend[(FAST_L + 1) * LANE_BLOCK]; uint8_t len[FAST_L * LANE_BLOCK]; } walk;
     struct { uint32_t off[WR], rel[WR + 1]; uint8_t flg[WR]; } emit;
 };
 static_assert(2 * RCAP <= 2 * FAST_L + 1, "a lane's walk-store column holds its ranges");
 
-// k_walk_one's arguments besides the index.  The walk reads the first three;
-// the rest are read only after it, through late_args(): held in scalar
-// registers across the walk they spilled (k_walk_fast's 64-VGPR budget, 8
-// waves per SIMD, has no room for them), and a kernel that spills needs
-// scratch -- its hot loop then reloaded values from it.
-struct OneArgs {
-    uint64_t n; const uint8_t *blob; const uint64_t *offs;                        // the walk's
-    uint64_t *look; uint8_t *err; uint64_t *hit_offs; uint32_t *out; uint64_t cap; // after it
-    uint32_t *cnt, *nr; uint2 *rng;                                               // parked blocks' results
-    uint32_t tag; LbCtl lb;
-};
-struct OneKargs { DevIndex ix; OneArgs a; };   // k_walk_one's kernarg layout (arguments in order, naturally aligned)
-
-// the kernel's own OneArgs in its kernarg segment, behind an opaque step so
-// the compiler cannot hoist the loads through it to the kernel's entry
-__device__ __forceinline__ const OneArgs *late_args() {
-    uint64_t p = (uint64_t)(uintptr_t)(const void *)__builtin_amdgcn_kernarg_segment_ptr() + offsetof(OneKargs, a);
-    asm volatile("" : "+s"(p));
-    return reinterpret_cast<const OneArgs *>(p);
+bool lane_path_ok(const DevIndex &ix) {
+    return !ix.hdesc && ix.depth + 2 <= (uint32_t)FAST_L && ix.xlen_max <= (uint32_t)FAST_L;
 }
 
-// Steps 4 and 5 of a block (one wave, lane = topic t): offset, values of the
-// ranges rg[0, nrr) at base + rel, or -- rew -- a re-walk writing them.  The
-// LDS is free on entry (walk stores dead, the lane's ranges in registers).
-__device__ __forceinline__ void one_emit(const DevIndex &ix, OneLds &S, const uint8_t *blob, const uint64_t *offs,
-                                         uint64_t t, bool live, bool rew, uint32_t nrr, const uint2 (&rg)[RCAP],
-                                         uint64_t base, uint64_t rel, uint64_t total, uint64_t *hit_offs,
-                                         uint32_t *out, uint64_t cap) {
-    const uint32_t lane = threadIdx.x & 63;
-    if (live) __builtin_nontemporal_store(base + rel, hit_offs + t);
+template <class OT>
+__global__ __launch_bounds__(LANE_BLOCK) void k_walk_lane(DevIndex ix, Workspace ws, uint64_t n_, const uint8_t *blob_,
+                                                          const OT *offs_, uint8_t *err_, OT *hit_offs_, uint32_t *out_,
+                                                          uint64_t cap_, uint32_t tag, LbCtl lb, SmallSegs sg) {
+    __shared__ LaneLds S;
+    __shared__ uint4 s_tb[LANE_TBQ];
+    __shared__ uint64_t s_off[LANE_BLOCK + 1];
+    const uint32_t lane = threadIdx.x;
+    uint64_t n = n_, cap = cap_;
+    const uint8_t *blob = blob_;
+    const OT *offs = offs_;
+    OT *hit_offs = hit_offs_;
+    uint32_t *out = out_;
+    uint8_t *err = err_;
+    uint32_t seg = 0, nblk = gridDim.x, sb0 = 0;
+    if (sg.count) {
+        while (seg + 1 < sg.count && blockIdx.x >= sg.s[seg + 1].block0) seg++;
+        const SmallSeg &G = sg.s[seg];
+        n = G.n; cap = G.cap; blob = G.blob; out = G.out; err = G.err;
+        offs = static_cast<const OT *>(G.offs);
+        hit_offs = static_cast<OT *>(G.hit);
+        sb0 = G.block0;
+        nblk = (seg + 1 < sg.count ? sg.s[seg + 1].block0 : gridDim.x) - sb0;
+    }
+    // ---- 1. the start-order ticket (the segment's last ticket resets the
+    // word for the next launch on this workspace: every block has its ticket)
+    uint32_t tk = 0;
+    if (lane == 0) {
+        tk = atomicAdd(&ws.list_n[LS_TICK + seg], 1u);
+        if (tk == nblk - 1) atomicExch(&ws.list_n[LS_TICK + seg], 0u);
+    }
+    const uint32_t vb = __builtin_amdgcn_readfirstlane(tk);
+    const uint64_t t0 = (uint64_t)vb * LANE_BLOCK, t = t0 + lane;
+    const bool live = t < n;
+    const uint32_t nt = n - t0 < (uint64_t)LANE_BLOCK ? (uint32_t)(n - t0) : (uint32_t)LANE_BLOCK;
+
+    // ---- 2. offsets and the byte span into LDS
+    if (lane <= nt) s_off[lane] = offs[t0 + lane];
+    if (lane == 0 && nt == LANE_BLOCK) s_off[LANE_BLOCK] = offs[t0 + LANE_BLOCK];
+    wave_sync();
+    const uint64_t beg = live ? s_off[lane] : 0, end = live ? s_off[lane + 1] : 0;
+    const uint64_t B0 = s_off[0] & ~15ull;
+    const uint64_t nq = (s_off[nt] - B0 + 15) >> 4;
+    const bool staged = nq <= LANE_TBQ;   // (block-uniform)
+    if (staged) {
+        // aligned chunks share their granule with a valid byte: no page the caller does not own
+        for (uint32_t c = lane; c < nq; c += LANE_BLOCK) s_tb[c] = ld4_once(blob + B0 + 16ull * c);
+        wave_sync();
+    }
+    const StagedSrc src{blob, s_tb, B0, staged};
+
+    // ---- 3. the walk (k_walk_fast's), ranges parked in the lane's store column
+    uint32_t cnt = 0, nr = 0, e = 0;
+    int rc = RC_OK;
+    if (live) {
+        RangeEmit em;
+        em.cnt = 0; em.nr = 0;
+        LdsStore<FAST_L> st{S.walk.wid + lane, S.walk.pend + lane, S.walk.len + lane, LANE_BLOCK, 0};
+        rc = match_topic(ix, src, beg, end, st, em);
+        if (rc == RC_OK) {
+            cnt = em.cnt; nr = em.nr;
+#pragma unroll
+            for (uint32_t i = 0; i < RCAP; i++)
+                if (i < nr) { S.walk.wid[i * LANE_BLOCK + lane] = em.r[i].x; S.walk.pend[i * LANE_BLOCK + lane] = em.r[i].y; }
+        }
+        e = rc == RC_BADARG ? 1u : 0u;
+    }
+    const bool deep = rc == RC_DEEP;
+    bool rew = deep || nr > RCAP;   // values written by a re-walk (step 5)
+    if (deep) {   // (rare: C3 has none) counted in the lane's own column, levels beyond the trie only scanned
+        LdsStore<FAST_L, true> st{S.walk.wid + lane, S.walk.pend + lane, S.walk.len + lane, LANE_BLOCK, 0};
+        CountEmit ce{0};
+        const int frc = match_topic(ix, src, beg, end, st, ce);
+        cnt = frc == RC_OK ? (uint32_t)ce.cnt : 0u;
+        e = frc == RC_BADARG ? 1u : frc == RC_DEEP ? 2u : 0u;   // RC_DEEP here: > MAX_LEVELS levels
+    }
+    rew = rew && e == 0 && cnt > 0;
+    const uint32_t nrr = rew || rc != RC_OK ? 0u : nr;
+
+    // ---- 4. the block's offset
+    const uint64_t inc = wave_incl_scan(cnt);
+    const uint64_t total = __shfl(inc, 63, 64), rel = inc - cnt;
+    int res;
+    const uint64_t base = look_back(ws.look + (uint64_t)sb0 * LB_STRIDE, vb, tag, total, lb, res);
+    const bool fail = res != LBR_OK;   // (wave-uniform)
+    uint2 rg[RCAP];   // the lane's ranges, out of its store column before the LDS is reused
+#pragma unroll
+    for (uint32_t i = 0; i < RCAP; i++)
+        rg[i] = i < nrr ? make_uint2(S.walk.wid[i * LANE_BLOCK + lane], S.walk.pend[i * LANE_BLOCK + lane])
+                        : make_uint2(0, 0);
+    if (live) {
+        hit_offs[t] = (OT)(base + rel);
+        err[t] = fail ? 4 : (uint8_t)e;
+    }
+    if (fail) {
+        if (lane == 0) ws.hint_d[HINT_FAIL] = 1;
+        return;
+    }
+    if (lane == 0 && vb == nblk - 1) hit_offs[n] = (OT)(base + total);
+
+    // ---- 5. values
     uint32_t R;
     const uint32_t r0 = wave_excl_scan32(rew ? 1u : nrr, R);
+    wave_sync();   // every lane has its ranges: the LDS becomes the range stage
     const uint32_t rel32 = (uint32_t)rel;
     if (rew) {
         S.emit.off[r0] = 0; S.emit.rel[r0] = rel32; S.emit.flg[r0] = RF_SKIP;
@@ -1911,218 +2025,10 @@ __device__ __forceinline__ void one_emit(const DevIndex &ix, OneLds &S, const ui
     if (__ballot(rew)) {
         wave_sync();   // the LDS holds walk stores again
         if (rew) {
-            LdsStore<FAST_L, true> st{S.walk.wid + lane, S.walk.pend + lane, S.walk.len + lane, WALK_BLOCK, 0};
+            LdsStore<FAST_L, true> st{S.walk.wid + lane, S.walk.pend + lane, S.walk.len + lane, LANE_BLOCK, 0};
             DirectEmit de{ix.vals, out, base + rel, cap};
-            match_topic(ix, blob, offs[t], offs[t + 1], st, de);
+            match_topic(ix, src, beg, end, st, de);
         }
-    }
-}
-
-__global__ __launch_bounds__(WALK_BLOCK, 8) void k_walk_one(DevIndex ix, OneArgs a) {
-    __shared__ OneLds S;
-    const uint64_t n = a.n;
-    const uint8_t *blob = a.blob;
-    const uint64_t *offs = a.offs;
-    const uint32_t lane = threadIdx.x;
-    // Blocks scan in blockIdx order: workgroups are dispatched in that order,
-    // so a block's predecessors are running or done, never waiting for a slot
-    // it holds.  (A start-order ticket -- one atomic on one word per block --
-    // serialised 15.6k blocks at ~9 ns each: the C3 batch 0.343 -> 0.478 ms,
-    // profiles/r4/onepass_study.md.)
-    const uint32_t vb = blockIdx.x;
-    const uint64_t t = (uint64_t)vb * WALK_BLOCK + lane;
-    const bool live = t < n;
-
-    // ---- 1. the walk (k_walk_fast's)
-    uint32_t cnt = 0, nr = 0, e = 0;
-    int rc = RC_OK;
-    if (live) {
-        RangeEmit em;
-        em.cnt = 0; em.nr = 0;
-        LdsStore<FAST_L> st{S.walk.wid + lane, S.walk.pend + lane, S.walk.len + lane, WALK_BLOCK, 0};
-        rc = match_topic(ix, blob, offs[t], offs[t + 1], st, em);
-        if (rc == RC_OK) {
-            cnt = em.cnt; nr = em.nr;
-            // the ranges go into this lane's own column of the walk store,
-            // dead once its walk is done: no register holds them across the
-            // rest of the kernel
-#pragma unroll
-            for (uint32_t i = 0; i < RCAP; i++)
-                if (i < nr) { S.walk.wid[i * WALK_BLOCK + lane] = em.r[i].x; S.walk.pend[i * WALK_BLOCK + lane] = em.r[i].y; }
-        }
-        e = rc == RC_BADARG ? 1u : 0u;
-    }
-    const bool deep = rc == RC_DEEP;
-    bool rew = deep || nr > RCAP;   // values written by a re-walk (step 5)
-
-    // ---- 2. topics deeper than the main store: counted by a second walk in
-    // their own store columns (the other lanes' columns hold their ranges)
-    if (deep) {   // (rare: C3 has none, C3deep ~6 per block)
-        LdsStore<FAST_L, true> st{S.walk.wid + lane, S.walk.pend + lane, S.walk.len + lane, WALK_BLOCK, 0};
-        CountEmit ce{0};
-        const int frc = match_topic(ix, blob, offs[t], offs[t + 1], st, ce);
-        cnt = frc == RC_OK ? (uint32_t)ce.cnt : 0u;
-        e = frc == RC_BADARG ? 1u : frc == RC_DEEP ? 2u : 0u;   // RC_DEEP here: > MAX_LEVELS levels
-    }
-    rew = rew && e == 0 && cnt > 0;
-    const uint32_t nrr = rew || rc != RC_OK ? 0u : nr;
-
-    // ---- 3. the block's offset
-    const OneArgs &A = *late_args();
-    const uint64_t inc = wave_incl_scan(cnt);
-    const uint64_t total = __shfl(inc, 63, 64), rel = inc - cnt;
-    int res;
-    const uint64_t base = look_back<true>(A.look, vb, A.tag, total, A.lb, res);
-    uint2 rg[RCAP];   // this lane's ranges, out of its store column before the LDS is reused
-#pragma unroll
-    for (uint32_t i = 0; i < RCAP; i++)
-        rg[i] = i < nrr ? make_uint2(S.walk.wid[i * WALK_BLOCK + lane], S.walk.pend[i * WALK_BLOCK + lane])
-                        : make_uint2(0, 0);
-    if (live) __builtin_nontemporal_store((uint8_t)e, A.err + t);
-    if (res != LBR_OK) {   // (wave-uniform) parked for k_one_finish, as k_walk_fast leaves every topic
-        if (live) {
-            __builtin_nontemporal_store(cnt, A.cnt + t);
-            __builtin_nontemporal_store(rew ? (uint32_t)RCAP + 1 : nrr, A.nr + t);
-#pragma unroll
-            for (uint32_t i = 0; i < RCAP; i++)
-                if (i < nrr)
-                    __builtin_nontemporal_store((uint64_t)rg[i].x | (uint64_t)rg[i].y << 32,
-                                                reinterpret_cast<uint64_t *>(A.rng) + (uint64_t)i * n + t);
-        }
-        return;
-    }
-    // ---- 4, 5. offsets, values, re-walks
-    wave_sync();   // every lane has its ranges: the LDS becomes the range stage
-    one_emit(ix, S, blob, offs, t, live, rew, nrr, rg, base, rel, total, A.hit_offs, A.out, A.cap);
-}
-
-// After k_walk_one every look word is final: LB_INCL (the block's inclusive
-// prefix) or LB_DEF (a parked block's own total).  One block of 1024 threads
-// (thread j: a contiguous run of words, as k_scan_top) runs a segmented scan
-// over them -- an LB_INCL word restarts the sum at its value -- and gives each
-// parked block its exclusive prefix, written back into its word (LB_DEF, value
-// = the prefix), and a place in the list of parked blocks, in block order
-// (plist, count in list_n[LS_NPARK]); hit_offs[n] = the grand total.  A word
-// that is not final (never, unless a block failed to publish) raises the fail
-// word: the host runs the batch again.  (The first finisher looked back from
-// each parked block over the words before it, one wave per 64 blocks, serially:
-// with most blocks parked that was O(nb^2 / 64) loads and 0.9 ms per C3 batch.)
-constexpr uint32_t SCAN_U = 8;
-__global__ __launch_bounds__(1024) void k_one_scan(uint64_t *look, uint32_t nb, uint32_t tag, uint32_t *plist,
-                                                   uint32_t *list_n, uint64_t *hit_offs, uint64_t n,
-                                                   uint32_t *fail_word) {
-    __shared__ uint64_t s_v[16];
-    __shared__ uint32_t s_f[16], s_c[16];
-    const uint32_t per = (nb + 1023) / 1024;
-    const uint32_t b0 = threadIdx.x * per < nb ? threadIdx.x * per : nb, b1 = b0 + per < nb ? b0 + per : nb;
-    // the run's aggregate: f = it holds an LB_INCL word, v = the sum from its
-    // last LB_INCL word on (or from its start), c = its parked blocks
-    // (plain loads, SCAN_U at a time: k_walk_one has ended, its words are
-    // visible; one dependent load after another took 75 us for 15.6k words)
-    uint32_t f = 0, c = 0, bad = 0;
-    uint64_t v = 0;
-    for (uint32_t i0 = b0; i0 < b1; i0 += SCAN_U) {
-        uint64_t w[SCAN_U];
-#pragma unroll
-        for (uint32_t u = 0; u < SCAN_U; u++) w[u] = i0 + u < b1 ? look[(uint64_t)(i0 + u) * LB_STRIDE] : 0;
-#pragma unroll
-        for (uint32_t u = 0; u < SCAN_U; u++) {
-            if (i0 + u >= b1) break;
-            const uint32_t st = lb_tag(w[u]) == tag ? lb_state(w[u]) : 0u;
-            if (st == LB_INCL) { f = 1; v = w[u] & LB_VAL_MASK; }
-            else if (st == LB_DEF) { v += w[u] & LB_VAL_MASK; c++; }
-            else bad = 1;
-        }
-    }
-    if (__syncthreads_or(bad)) {
-        if (threadIdx.x == 0) { *fail_word = 1; list_n[LS_NPARK] = 0; }
-        return;
-    }
-    // segmented inclusive scan over the threads: (f1, v1) then (f2, v2) = f2 ? (1, v2) : (f1, v1 + v2)
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    uint32_t sf = f, sc = c;
-    uint64_t sv = v;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t of = __shfl_up(sf, d, 64), oc = __shfl_up(sc, d, 64);
-        const uint64_t ov = __shfl_up(sv, d, 64);
-        if (lane >= d) {
-            if (!sf) sv += ov;
-            sf |= of;
-            sc += oc;
-        }
-    }
-    if (lane == 63) { s_f[wv] = sf; s_v[wv] = sv; s_c[wv] = sc; }
-    __syncthreads();
-    uint32_t pf = 0, pc = 0, tc = 0;   // the waves before this one, combined
-    uint64_t pv = 0;
-    for (int k = 0; k < 16; k++) {
-        if (k < wv) { pv = s_f[k] ? s_v[k] : pv + s_v[k]; pf |= s_f[k]; pc += s_c[k]; }
-        tc += s_c[k];
-    }
-    // this thread's exclusive prefix: the waves before, then the lanes before
-    uint32_t ef = __shfl_up(sf, 1, 64), ec = __shfl_up(sc, 1, 64);
-    uint64_t ev = __shfl_up(sv, 1, 64);
-    if (lane == 0) { ef = 0; ec = 0; ev = 0; }
-    uint64_t run = ef ? ev : pv + ev;
-    uint32_t k = pc + ec;
-    (void)pf;
-    for (uint32_t i0 = b0; i0 < b1; i0 += SCAN_U) {
-        uint64_t w[SCAN_U];
-#pragma unroll
-        for (uint32_t u = 0; u < SCAN_U; u++) w[u] = i0 + u < b1 ? look[(uint64_t)(i0 + u) * LB_STRIDE] : 0;
-#pragma unroll
-        for (uint32_t u = 0; u < SCAN_U; u++) {
-            if (i0 + u >= b1) break;
-            if (lb_state(w[u]) == LB_INCL) {
-                run = w[u] & LB_VAL_MASK;
-            } else {
-                look[(uint64_t)(i0 + u) * LB_STRIDE] = lb_word(tag, LB_DEF, run);
-                plist[k++] = i0 + u;
-                run += w[u] & LB_VAL_MASK;
-            }
-        }
-    }
-    if (threadIdx.x == 1023) {   // (its run ends at nb: run = the grand total)
-        hit_offs[n] = run;
-        list_n[LS_NPARK] = tc;
-        list_n[LS_PARKED] += tc;   // (diagnostics: TM_DEBUG_DEFERRED_BLOCKS)
-    }
-}
-
-// The parked blocks of a k_walk_one launch, after k_one_scan: a grid of up
-// to FIN_GRID one-wave blocks takes them from the list in turn; per block, its
-// offsets and values from the parked counts and ranges and the prefix
-// k_one_scan left in its word (one_emit, re-walks included).
-constexpr uint32_t FIN_GRID = 65536;   // (4096: 57 us for 15.6k parked C3 blocks -- 4 waves per SIMD hide too little)
-__global__ __launch_bounds__(WALK_BLOCK) void k_one_finish(DevIndex ix, OneArgs a, const uint32_t *plist,
-                                                           const uint32_t *list_n) {
-    __shared__ OneLds S;
-    const uint32_t lane = threadIdx.x;
-    const uint64_t n = a.n;
-    const uint32_t np = list_n[LS_NPARK];
-    for (uint32_t i = blockIdx.x; i < np; i += gridDim.x) {
-        const uint32_t vb = plist[i];
-        const uint64_t pre = __hip_atomic_load(&a.look[(uint64_t)vb * LB_STRIDE], __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT) & LB_VAL_MASK;
-        const uint64_t t = (uint64_t)vb * WALK_BLOCK + lane;
-        const bool live = t < n;
-        const uint32_t cnt = live ? __builtin_nontemporal_load(a.cnt + t) : 0u;
-        const uint32_t pnr = live ? __builtin_nontemporal_load(a.nr + t) : 0u;
-        const bool rew = pnr > RCAP;
-        const uint32_t nrr = rew ? 0u : pnr;
-        uint2 rg[RCAP];
-#pragma unroll
-        for (uint32_t r = 0; r < RCAP; r++) {
-            const uint64_t g = r < nrr ? __builtin_nontemporal_load(reinterpret_cast<const uint64_t *>(a.rng) +
-                                                                    (uint64_t)r * n + t) : 0;
-            rg[r] = make_uint2((uint32_t)g, (uint32_t)(g >> 32));
-        }
-        const uint64_t inc = wave_incl_scan(cnt);
-        const uint64_t total = __shfl(inc, 63, 64);
-        wave_sync();   // (the previous parked block's emit is done with the LDS)
-        one_emit(ix, S, a.blob, a.offs, t, live, rew, nrr, rg, pre, inc - cnt, total, a.hit_offs, a.out, a.cap);
-        wave_sync();
     }
 }
 
@@ -2410,34 +2316,31 @@ hipError_t launch_match_phase2(const DevIndex &ix, const Workspace &ws, uint64_t
     return hipGetLastError();
 }
 
+// k_walk_lane where the index allows it (lane_path_ok) unless k_walk_small is
+// asked for; SMALL_LANE on an index the lane walk cannot take: k_walk_small
+bool small_lane(const DevIndex &ix, int kind) { return kind != SMALL_WAVE && lane_path_ok(ix); }
+
 hipError_t launch_match(const DevIndex &ix, const Workspace &ws, uint64_t n, const uint8_t *bytes,
                         const uint64_t *offs, uint64_t *hit_offs, uint8_t *err, uint32_t *out, uint64_t cap,
-                        uint32_t tag, LbCtl lb, bool phases, hipStream_t s, hipEvent_t ev_walk0,
+                        uint32_t tag, LbCtl lb, bool phases, int small_kind, hipStream_t s, hipEvent_t ev_walk0,
                         hipEvent_t ev_walk1, int *path) {
-    const bool one = n && (n <= SMALL_TOPICS ? one_launch_ok(ix) : !phases && one_pass_ok(ix));
-    if (path) *path = !one ? PATH_PHASES : n <= SMALL_TOPICS ? PATH_SMALL : PATH_ONE;
-    if (one) {
+    if (n && !phases && small_path_ok(ix, n)) {
+        const bool lane = small_lane(ix, small_kind);
+        if (path) *path = lane ? PATH_LANE : PATH_SMALL;
         hipError_t e;
-        Outs o{err, nullptr, nullptr};
         if (ev_walk0 && (e = hipEventRecord(ev_walk0, s)) != hipSuccess) return e;
-        if (n <= SMALL_TOPICS)
+        if (lane) {
+            hipLaunchKernelGGL((k_walk_lane<uint64_t>), dim3(blocks_for(n, LANE_BLOCK)), dim3(LANE_BLOCK), 0, s, ix, ws,
+                               n, bytes, offs, err, hit_offs, out, cap, tag & LB_TAG_MASK, lb, SmallSegs{});
+        } else {
+            Outs o{err, nullptr, nullptr};
             hipLaunchKernelGGL((k_walk_small<MODE_COUNT, uint64_t>), dim3(blocks_for(n, SM_TOPICS)), dim3(WV_BLOCK), 0,
                                s, ix, ws, n, bytes, offs, o, hit_offs, out, cap, tag & LB_TAG_MASK, lb, SmallSegs{});
-        if (n > SMALL_TOPICS) {
-            const OneArgs a{n, bytes, offs, ws.look, err, hit_offs, out, cap, ws.cnt, ws.nr, ws.rng,
-                            tag & LB_TAG_MASK, lb};
-            const uint32_t nb = blocks_for(n, WALK_BLOCK);
-            hipLaunchKernelGGL(k_walk_one, dim3(nb), dim3(WALK_BLOCK), 0, s, ix, a);
-            if (ev_walk1 && (e = hipEventRecord(ev_walk1, s)) != hipSuccess) return e;
-            hipLaunchKernelGGL(k_one_scan, dim3(1), dim3(1024), 0, s, ws.look, nb, tag & LB_TAG_MASK, ws.lists,
-                               ws.list_n, hit_offs, n, ws.hint_d + HINT_FAIL);
-            hipLaunchKernelGGL(k_one_finish, dim3(nb < FIN_GRID ? nb : FIN_GRID), dim3(WALK_BLOCK), 0, s, ix, a,
-                               ws.lists, ws.list_n);
-            return hipGetLastError();
         }
         if (ev_walk1 && (e = hipEventRecord(ev_walk1, s)) != hipSuccess) return e;
         return hipGetLastError();
     }
+    if (path) *path = PATH_PHASES;
     hipError_t e = launch_match_phase1(ix, ws, n, bytes, offs, hit_offs, err, s, ev_walk0, ev_walk1);
     if (e != hipSuccess) return e;
     return launch_match_phase2(ix, ws, n, bytes, offs, hit_offs, out, cap, s);
@@ -2445,34 +2348,54 @@ hipError_t launch_match(const DevIndex &ix, const Workspace &ws, uint64_t n, con
 
 hipError_t launch_match32(const DevIndex &ix, const Workspace &ws, uint64_t n, const uint8_t *bytes,
                           const uint32_t *offs, uint32_t *hit_offs, uint8_t *err, uint32_t *out, uint64_t cap,
-                          uint32_t tag, LbCtl lb, hipStream_t s) {
+                          uint32_t tag, LbCtl lb, int small_kind, hipStream_t s, int *path) {
     if (!small_path_ok(ix, n)) return hipErrorInvalidValue;   // (the caller converts instead)
-    Outs o{err, nullptr, nullptr};
-    hipLaunchKernelGGL((k_walk_small<MODE_COUNT, uint32_t>), dim3(blocks_for(n, SM_TOPICS)), dim3(WV_BLOCK), 0, s, ix,
-                       ws, n, bytes, offs, o, hit_offs, out, cap, tag & LB_TAG_MASK, lb, SmallSegs{});
+    const bool lane = small_lane(ix, small_kind);
+    if (path) *path = lane ? PATH_LANE : PATH_SMALL;
+    if (lane) {
+        hipLaunchKernelGGL((k_walk_lane<uint32_t>), dim3(blocks_for(n, LANE_BLOCK)), dim3(LANE_BLOCK), 0, s, ix, ws, n,
+                           bytes, offs, err, hit_offs, out, cap, tag & LB_TAG_MASK, lb, SmallSegs{});
+    } else {
+        Outs o{err, nullptr, nullptr};
+        hipLaunchKernelGGL((k_walk_small<MODE_COUNT, uint32_t>), dim3(blocks_for(n, SM_TOPICS)), dim3(WV_BLOCK), 0, s,
+                           ix, ws, n, bytes, offs, o, hit_offs, out, cap, tag & LB_TAG_MASK, lb, SmallSegs{});
+    }
     return hipGetLastError();
 }
 
 // the combiner's launch: sg's segments (block0 filled here) in one grid
 hipError_t launch_small_segs(const DevIndex &ix, const Workspace &ws, const SmallSegs &sg0, bool u32, uint32_t tag,
-                             LbCtl lb, hipStream_t s) {
+                             LbCtl lb, int small_kind, hipStream_t s, int *path) {
     SmallSegs sg = sg0;
+    const bool lane = small_lane(ix, small_kind);
+    const uint32_t per = lane ? LANE_BLOCK : SM_TOPICS;
     uint32_t blocks = 0;
     for (uint32_t k = 0; k < sg.count; k++) {
         if (!sg.s[k].n) return hipErrorInvalidValue;
         sg.s[k].block0 = blocks;
-        blocks += blocks_for(sg.s[k].n, SM_TOPICS);
+        blocks += blocks_for(sg.s[k].n, per);
     }
     if (!sg.count || sg.count > (uint32_t)SMALL_SEGS) return hipErrorInvalidValue;
-    Outs o{sg.s[0].err, nullptr, nullptr};
-    if (u32)
+    if (path) *path = lane ? PATH_LANE : PATH_SMALL;
+    const SmallSeg &F = sg.s[0];
+    Outs o{F.err, nullptr, nullptr};
+    const uint32_t tg = tag & LB_TAG_MASK;
+    if (lane && u32)
+        hipLaunchKernelGGL((k_walk_lane<uint32_t>), dim3(blocks), dim3(LANE_BLOCK), 0, s, ix, ws, (uint64_t)F.n, F.blob,
+                           static_cast<const uint32_t *>(F.offs), F.err, static_cast<uint32_t *>(F.hit), F.out, F.cap,
+                           tg, lb, sg);
+    else if (lane)
+        hipLaunchKernelGGL((k_walk_lane<uint64_t>), dim3(blocks), dim3(LANE_BLOCK), 0, s, ix, ws, (uint64_t)F.n, F.blob,
+                           static_cast<const uint64_t *>(F.offs), F.err, static_cast<uint64_t *>(F.hit), F.out, F.cap,
+                           tg, lb, sg);
+    else if (u32)
         hipLaunchKernelGGL((k_walk_small<MODE_COUNT, uint32_t>), dim3(blocks), dim3(WV_BLOCK), 0, s, ix, ws,
-                           (uint64_t)sg.s[0].n, sg.s[0].blob, static_cast<const uint32_t *>(sg.s[0].offs), o,
-                           static_cast<uint32_t *>(sg.s[0].hit), sg.s[0].out, sg.s[0].cap, tag & LB_TAG_MASK, lb, sg);
+                           (uint64_t)F.n, F.blob, static_cast<const uint32_t *>(F.offs), o,
+                           static_cast<uint32_t *>(F.hit), F.out, F.cap, tg, lb, sg);
     else
         hipLaunchKernelGGL((k_walk_small<MODE_COUNT, uint64_t>), dim3(blocks), dim3(WV_BLOCK), 0, s, ix, ws,
-                           (uint64_t)sg.s[0].n, sg.s[0].blob, static_cast<const uint64_t *>(sg.s[0].offs), o,
-                           static_cast<uint64_t *>(sg.s[0].hit), sg.s[0].out, sg.s[0].cap, tag & LB_TAG_MASK, lb, sg);
+                           (uint64_t)F.n, F.blob, static_cast<const uint64_t *>(F.offs), o,
+                           static_cast<uint64_t *>(F.hit), F.out, F.cap, tg, lb, sg);
     return hipGetLastError();
 }
 
@@ -2503,7 +2426,7 @@ hipError_t launch_first(const DevIndex &ix, const Workspace &ws, uint64_t n, con
     Outs o{nullptr, out_value, out_found};
     if (small_path_ok(ix, n)) {
         hipLaunchKernelGGL((k_walk_small<MODE_FIRST, uint64_t>), dim3(blocks_for(n, SM_TOPICS)), dim3(WV_BLOCK), 0, s,
-                           ix, ws, n, bytes, offs, o, nullptr, nullptr, (uint64_t)0, 0u, LbCtl{LB_SPINS, NONE, LB_DEFER},
+                           ix, ws, n, bytes, offs, o, nullptr, nullptr, (uint64_t)0, 0u, LbCtl{LB_SPINS, NONE},
                            SmallSegs{});
         return hipGetLastError();
     }

@@ -58,7 +58,9 @@ constexpr uint32_t KINL = 4;     // literal children kept inside the node's line
 
 // A table-mode node with at least WIDE_LIT literal children (its 192-bit Bloom
 // would be saturated: every probe passes it) keeps an exact bitmap over the
-// whole wid space instead, in the `wbits` pool (kw[2] = its word offset).
+// whole wid space instead, in the `wbits` pool (kw[2] = its word offset; NONE
+// for a dense wide node, whose children are most of its level's words: the
+// walk then probes its child table without asking the bitmap first).
 // The few such nodes are the widest of the upper trie -- C3: the level-1
 // nodes and the (w0,+) / (+,+) level-2 nodes -- so their bitmaps stay in L2
 // and a probe for a word the node has no child for costs an L2 hit instead of

@@ -285,7 +285,7 @@ int tm_merge_shards(uint32_t world, uint64_t n, const uint64_t *d_shard_hit_offs
                     void *stream);
 
 /* Diagnostics.  While enabled, every match batch records HIP events on its
- * stream around the main walk kernel (k_walk_one / k_walk_small for a
+ * stream around the main walk kernel (k_walk_lane / k_walk_small for a
  * one-launch batch, k_walk_fast for a two-phase one) and around the whole batch;
  * tm_profile_read() resolves them and returns the accumulated device times
  * (milliseconds) and the number of batches since the last reset. */
@@ -296,28 +296,32 @@ int tm_profile_read(tm_index *h, double *walk_ms, double *batch_ms, uint64_t *ba
  *   TM_DEBUG_LB_SPINS       the look-back wait bound (polls of one word) of the
  *   TM_DEBUG_LB_FAIL_BLOCK  next TM_DEBUG_LB_LAUNCHES one-launch batches, and
  *   TM_DEBUG_LB_LAUNCHES    the block that fails as if its wait expired
- *                           (k_walk_one: parks) (>= 2^32: none)
- *   TM_DEBUG_PHASES         batches above 65536 topics: 1 the two-phase path
- *                           (walk, tails, scan, emit), 0 one launch (k_walk_one,
- *                           where the index allows it); the default is the
- *                           faster of the two on C3
- *   TM_DEBUG_LB_DEFER       k_walk_one: polls of a predecessor still walking
- *                           before a block parks its results for k_one_finish
- *                           (0: every block that would wait parks)
+ *                           (>= 2^32: none)
+ *   TM_DEBUG_PHASES         1: batches of <= 65536 topics take the two-phase
+ *                           path too (walk, tails, scan, emit); 0 (default):
+ *                           one launch where the index allows it
+ *   TM_DEBUG_SMALL_KERNEL   the one-launch kernel of small batches: 0 (default)
+ *                           k_walk_lane (one lane per topic) where the index
+ *                           allows it, else k_walk_small; 1 k_walk_small (16
+ *                           lanes per topic); 2 k_walk_lane where allowed
  *   TM_DEBUG_COMBINE        concurrent combined launches of small 32-bit
  *                           in-place host batches (tm_match_batch32_ex): 0 =
  *                           every batch its own launch (default 4)
  * tm_debug_get: TM_DEBUG_FAILED_BATCHES (one-launch batches whose look-back
  * failed, host API), TM_DEBUG_RETRIED_BATCHES (of those, run again) and the
  * match launches per kernel path: TM_DEBUG_PATH_PHASES (walk, tails, scan,
- * emit), TM_DEBUG_PATH_SMALL (k_walk_small), TM_DEBUG_PATH_ONE (k_walk_one),
- * TM_DEBUG_DEFERRED_BLOCKS: k_walk_one blocks that parked (after the
- * batches finished), and TM_DEBUG_COMBINED_LAUNCHES / _BATCHES: the
- * combiner's launches and the host batches they carried. */
+ * emit), TM_DEBUG_PATH_SMALL (k_walk_small), TM_DEBUG_PATH_LANE
+ * (k_walk_lane), TM_DEBUG_COMBINED_LAUNCHES / _BATCHES: the combiner's
+ * launches and the host batches they carried, and TM_DEBUG_WIDE_NODES /
+ * TM_DEBUG_DENSE_WIDE: trie nodes with a child bitmap, and those of them
+ * dense enough that the walk probes their child table without it.  (Keys
+ * 9-11 named the round-4 one-pass kernel's hooks; 9 and 10 now name these,
+ * 11 is retired.) */
 enum { TM_DEBUG_LB_SPINS = 1, TM_DEBUG_LB_FAIL_BLOCK = 2, TM_DEBUG_LB_LAUNCHES = 3, TM_DEBUG_PHASES = 4,
        TM_DEBUG_FAILED_BATCHES = 5, TM_DEBUG_RETRIED_BATCHES = 6, TM_DEBUG_PATH_PHASES = 7,
-       TM_DEBUG_PATH_SMALL = 8, TM_DEBUG_PATH_ONE = 9, TM_DEBUG_LB_DEFER = 10, TM_DEBUG_DEFERRED_BLOCKS = 11,
-       TM_DEBUG_COMBINE = 12, TM_DEBUG_COMBINED_LAUNCHES = 13, TM_DEBUG_COMBINED_BATCHES = 14 };
+       TM_DEBUG_PATH_SMALL = 8, TM_DEBUG_PATH_LANE = 9, TM_DEBUG_SMALL_KERNEL = 10,
+       TM_DEBUG_COMBINE = 12, TM_DEBUG_COMBINED_LAUNCHES = 13, TM_DEBUG_COMBINED_BATCHES = 14,
+       TM_DEBUG_WIDE_NODES = 15, TM_DEBUG_DENSE_WIDE = 16 };
 int tm_debug_set(tm_index *h, uint32_t key, uint64_t value);
 int tm_debug_get(tm_index *h, uint32_t key, uint64_t *value);
 

@@ -12,6 +12,9 @@
 #                             passes (one rocprofv3 --pmc run per group)
 #   walk[:<args>]             tools/profile_walk.py <args> (isolated walk timing)
 #   py:<name>:<script args>   python3 -u <script args> -> <name>.txt
+#   export:<VAR>=<value>      set an environment variable for the steps after it
+#                             (e.g. TM_LIB=emqx_amd/variants/libtmatch_<study>.so)
+#   unset:<VAR>
 # Output: gpurun_out/<tag>/
 set -e
 TAG=$1; shift
@@ -62,6 +65,8 @@ for step in "$@"; do
         timeout -k 10 -s KILL 120 rocprofv3 --pmc $pmc -d "$OUT/prof/pmc$i" -o run --output-format csv -- \
           python3 -u tools/profile_walk.py ${rest//,/ } > "$OUT/prof/pmc$i.log" 2>&1
       done ;;
+    export) export "$rest"; echo "  $rest" ;;
+    unset) unset "$rest" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

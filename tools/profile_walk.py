@@ -30,9 +30,9 @@ def main():
     p.add_argument("--streams", type=int, default=1,
                    help="streams the launches rotate over (3: bench.py's overlapped steps; wall/batch is then the "
                         "step time)")
-    p.add_argument("--large-path", default="default", choices=["default", "one", "phases"],
-                   help="batches above 65536 topics: the library's default, k_walk_one or the two-phase path")
-    p.add_argument("--lb-defer", type=int, default=None, help="k_walk_one: polls before a block parks (TM_DEBUG_LB_DEFER)")
+    p.add_argument("--small-kernel", default="auto", choices=["auto", "wave", "lane"],
+                   help="batches <= 65536 topics: the library's default, k_walk_small or k_walk_lane")
+    p.add_argument("--phases", action="store_true", help="every batch on the two-phase path (TM_DEBUG_PHASES)")
     a = p.parse_args()
     import torch
     from bench import CONFIGS
@@ -47,13 +47,15 @@ def main():
         fs = wl.ItemSet(blob, offs, fs.vals[np.array(order)], fs.flags[np.array(order)])
         del items, order
     ix = _native.Index(device=0)
-    if a.large_path != "default":
-        ix.debug_set(_native.TM_DEBUG_PHASES, int(a.large_path == "phases"))
-    if a.lb_defer is not None:
-        ix.debug_set(_native.TM_DEBUG_LB_DEFER, a.lb_defer)
+    if a.small_kernel != "auto":
+        ix.debug_set(_native.TM_DEBUG_SMALL_KERNEL, {"wave": _native.SMALL_WAVE, "lane": _native.SMALL_LANE}[a.small_kernel])
+    if a.phases:
+        ix.debug_set(_native.TM_DEBUG_PHASES, 1)
     for lo in range(0, len(fs), 2_000_000):
         part = fs.slice(lo, min(lo + 2_000_000, len(fs)))
         ix.apply(np.ones(len(part), np.uint8), part.blob, part.offs, part.vals)
+    print(f"wide nodes {ix.debug_get(_native.TM_DEBUG_WIDE_NODES)}, dense {ix.debug_get(_native.TM_DEBUG_DENSE_WIDE)}",
+          flush=True)
     dev = torch.device("cuda:0")
     R = max(1, a.rotate)
     d_in = []
@@ -105,13 +107,11 @@ def main():
     w, b, n = ix.profile_read()
     st = ix.stats()
     paths = [ix.debug_get(k) for k in (_native.TM_DEBUG_PATH_PHASES, _native.TM_DEBUG_PATH_SMALL,
-                                       _native.TM_DEBUG_PATH_ONE)]
+                                       _native.TM_DEBUG_PATH_LANE)]
     assert not any(bool(e_.any().item()) for _, e_, _ in outs), "err flags set"
-    parked = ix.debug_get(_native.TM_DEBUG_DEFERRED_BLOCKS)
-    print(f"{a.config}/{a.order}/filters-{a.filter_order} streams={S} paths(phases,small,one)={paths} filters={len(fs)} batch={a.batch} rotate={R} hits<={tot} "
+    print(f"{a.config}/{a.order}/filters-{a.filter_order} streams={S} paths(phases,small,lane)={paths} filters={len(fs)} batch={a.batch} rotate={R} hits<={tot} "
           f"wall/batch={el / a.batches * 1e3:.3f}ms walk={w / n:.4f}ms batch_dev={b / n:.4f}ms "
-          f"rate={a.batch * a.batches / el / 1e9:.3f}G/s device_MiB={st['device_bytes'] / 2**20:.0f} "
-          f"parked_blocks={parked}", flush=True)
+          f"rate={a.batch * a.batches / el / 1e9:.3f}G/s device_MiB={st['device_bytes'] / 2**20:.0f}", flush=True)
 
 
 if __name__ == "__main__":
