@@ -110,7 +110,7 @@ def parse():
                         "device entries, native feeder threads submitting in-place host batches while a syncer thread "
                         "applies deltas (the NIF's deployment, INTEGRATION.md 5); with fewer GPUs than N the entries "
                         "repeat the local device -- a rehearsal, not scaling")
-    p.add_argument("--small-kernel", default="auto", choices=["auto", "wave", "lane"],
+    p.add_argument("--small-kernel", default="auto", choices=["auto", "wave", "wave8", "lane"],
                    help="the one-launch kernel of batches <= 65536 topics (latency and concurrent-caller legs): "
                         "the library's default, k_walk_small (16 lanes per topic) or k_walk_lane "
                         "(TM_DEBUG_SMALL_KERNEL)")
@@ -201,7 +201,8 @@ def main():
     copies = a.copies
     ix = _native.Index(device=local, hint_keys=len(fs), copies=copies)
     if a.small_kernel != "auto":
-        ix.debug_set(_native.TM_DEBUG_SMALL_KERNEL, {"wave": _native.SMALL_WAVE, "lane": _native.SMALL_LANE}[a.small_kernel])
+        ix.debug_set(_native.TM_DEBUG_SMALL_KERNEL, {"wave": _native.SMALL_WAVE, "wave8": _native.SMALL_WAVE8,
+                                                     "lane": _native.SMALL_LANE}[a.small_kernel])
     chunk = 2_000_000
     for lo in range(0, len(fs), chunk):
         part = fs.slice(lo, min(lo + chunk, len(fs)))

@@ -31,7 +31,7 @@ TM_DEBUG_LB_SPINS, TM_DEBUG_LB_FAIL_BLOCK, TM_DEBUG_LB_LAUNCHES, TM_DEBUG_PHASES
 TM_DEBUG_FAILED_BATCHES, TM_DEBUG_RETRIED_BATCHES = 5, 6
 TM_DEBUG_PATH_PHASES, TM_DEBUG_PATH_SMALL, TM_DEBUG_PATH_LANE = 7, 8, 9
 TM_DEBUG_SMALL_KERNEL = 10
-SMALL_AUTO, SMALL_WAVE, SMALL_LANE = 0, 1, 2
+SMALL_AUTO, SMALL_WAVE, SMALL_LANE, SMALL_WAVE8 = 0, 1, 2, 3
 TM_DEBUG_COMBINE, TM_DEBUG_COMBINED_LAUNCHES, TM_DEBUG_COMBINED_BATCHES = 12, 13, 14
 TM_DEBUG_WIDE_NODES, TM_DEBUG_DENSE_WIDE = 15, 16
 

@@ -67,7 +67,7 @@ def build_tmatch(force: bool = False) -> Path:
 
 def build_variant(name: str, kernel_src: str | None = None, force: bool = False,
                   host_src: str | None = None) -> Path:
-    """An experimental build of libtmatch (perf studies: tools/gpu_variants.sh
+    """An experimental build of libtmatch (perf studies: tools/gpu.sh export:TM_LIB=...
     loads it through TM_LIB).  `kernel_src` replaces tm_kernels.hip with a
     study copy (e.g. under emqx_amd/study/, not tracked), so experiments never
     put switches into the product source; `host_src` likewise tm_host.cpp.

@@ -128,7 +128,9 @@ hipError_t launch_match_phase2(const DevIndex &ix, const Workspace &ws, uint64_t
 bool small_path_ok(const DevIndex &ix, uint64_t n);
 bool one_launch_ok(const DevIndex &ix);
 bool lane_path_ok(const DevIndex &ix);   // k_walk_lane's condition
-enum { SMALL_AUTO = 0, SMALL_WAVE = 1, SMALL_LANE = 2 };   // which one-launch kernel (small_kind)
+// which one-launch kernel (small_kind): the default, k_walk_small with 16 /
+// 8 lanes per topic, k_walk_lane (one lane per topic, where lane_path_ok)
+enum { SMALL_AUTO = 0, SMALL_WAVE = 1, SMALL_LANE = 2, SMALL_WAVE8 = 3 };
 bool small_lane(const DevIndex &ix, int small_kind);
 enum { PATH_PHASES = 0, PATH_SMALL = 1, PATH_LANE = 2, PATH_COUNT = 3 };   // *path of launch_match
 hipError_t launch_match(const DevIndex &ix, const Workspace &ws, uint64_t n, const uint8_t *bytes,

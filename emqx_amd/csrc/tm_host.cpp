@@ -2492,7 +2492,7 @@ int tm_debug_set(tm_index *ix, uint32_t key, uint64_t value) {
     case TM_DEBUG_PHASES: ix->dbg_phases = value != 0; break;
     case TM_DEBUG_COMBINE: ix->cmb_leaders = value > 16 ? 16 : (int)value; break;
     case TM_DEBUG_SMALL_KERNEL:
-        if (value > SMALL_LANE) return fail(ix, TM_EINVAL, "tm_debug_set: TM_DEBUG_SMALL_KERNEL is 0, 1 or 2");
+        if (value > SMALL_WAVE8) return fail(ix, TM_EINVAL, "tm_debug_set: TM_DEBUG_SMALL_KERNEL is 0 to 3");
         ix->small_kind = (int)value;
         break;
     default: return fail(ix, TM_EINVAL, "tm_debug_set: unknown key");

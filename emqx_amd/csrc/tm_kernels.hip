@@ -1170,7 +1170,21 @@ bool small_path_ok(const DevIndex &ix, uint64_t n) { return n && n <= SMALL_TOPI
 // sg.count > 0 (count mode): the launch carries several host batches
 // (SmallSegs); each block finds its segment and works on it as a launch of
 // that batch alone would -- its own block index, look-back region and last block.
-template <int MODE, class OT>
+// W: lanes per topic -- 16 (four topics per wave), or 8 (eight: twice the
+// topics per wave slot for concurrent callers, whose launches together fill
+// every slot of the GPU; levels and frontier states per topic <= 8, else the
+// lane walk).  A group keeps up to HC hit ranges (C3: 8.4 per topic).
+template <int W>
+struct SmallShape {
+    static constexpr uint32_t G = 64 / W;                          // topics per wave
+    static constexpr uint32_t ST = WV_WAVES * G;                   // topics per block
+    static constexpr uint32_t MAXL = W < 31 ? W : 31;              // levels a group takes
+    static constexpr uint32_t HC = W < 16 ? 16 : W;                // hit ranges a group keeps
+    static constexpr uint32_t TBQ = (W >= 16 ? SM_TB : SM_TB / 2) / 16 + 1;   // 16-B chunks of a topic staged
+};
+static_assert(SmallShape<16>::ST == SM_TOPICS, "SM_TOPICS: the most blocks a small batch launches per topic");
+
+template <int MODE, class OT, int W>
 __global__ __launch_bounds__(WV_BLOCK) void k_walk_small(DevIndex ix, Workspace ws, uint64_t n_, const uint8_t *blob_,
                                                          const OT *offs_, Outs o, OT *hit_offs_,
                                                          uint32_t *out_, uint64_t cap_, uint32_t tag, LbCtl lb,
@@ -1193,30 +1207,28 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_small(DevIndex ix, Workspace 
         nblk = (k + 1 < sg.count ? sg.s[k + 1].block0 : gridDim.x) - sb0;
         vb = blockIdx.x - sb0;
     }
-    constexpr int W = WAVE_W;
-    constexpr uint32_t G = 64 / W;                        // topics per wave
-    constexpr uint32_t MAXL = W < 31 ? W : 31;
-    static_assert(WV_WAVES * G == SM_TOPICS, "a block is SM_TOPICS topics");
+    using SH = SmallShape<W>;
+    constexpr uint32_t G = SH::G, ST = SH::ST, MAXL = SH::MAXL, HC = SH::HC;
     __shared__ uint32_t s_slash[WV_WAVES][64];
     __shared__ uint32_t s_node[WV_WAVES][64];
     __shared__ uint64_t s_code[WV_WAVES][64];
-    __shared__ uint64_t s_hcode[WV_WAVES][64];
-    __shared__ uint32_t s_hoff[WV_WAVES][64], s_hcnt[WV_WAVES][64];
-    __shared__ uint32_t s_roff[WV_WAVES][64], s_rcnt[WV_WAVES][64];   // hits by rank
-    __shared__ uint64_t s_rpos[WV_WAVES][64];
-    __shared__ uint32_t s_mwid[SM_TOPICS][MID_L], s_mpend[SM_TOPICS][MID_L + 1];   // fallback lane-walk stores
-    __shared__ uint8_t s_mlen[SM_TOPICS][MID_L];
-    __shared__ uint64_t s_cnt[SM_TOPICS];
+    __shared__ uint64_t s_hcode[WV_WAVES][G * HC];
+    __shared__ uint32_t s_hoff[WV_WAVES][G * HC], s_hcnt[WV_WAVES][G * HC];
+    __shared__ uint32_t s_roff[WV_WAVES][G * HC], s_rcnt[WV_WAVES][G * HC];   // hits by rank
+    __shared__ uint64_t s_rpos[WV_WAVES][G * HC];
+    __shared__ uint32_t s_mwid[ST][MID_L], s_mpend[ST][MID_L + 1];   // fallback lane-walk stores
+    __shared__ uint8_t s_mlen[ST][MID_L];
+    __shared__ uint64_t s_cnt[ST];
     __shared__ uint64_t s_base;
     __shared__ uint32_t s_fail;
-    constexpr uint32_t TBQ = SM_TB / 16 + 1;              // 16-B chunks of a topic staged in LDS
-    constexpr uint32_t TBQ_ALL = SM_TOPICS * TBQ;
+    constexpr uint32_t TBQ = SH::TBQ;                     // 16-B chunks of a topic staged in LDS
+    constexpr uint32_t TBQ_ALL = ST * TBQ;
     // topic bytes in LDS: the block's whole byte span in one cooperative round
     // of 16-B loads when it fits (each chunk read once -- consecutive topics
     // share the chunk at their boundary), else one row per topic
     __shared__ uint4 s_tb[TBQ_ALL];
-    __shared__ uint64_t s_off[SM_TOPICS + 1];
-    __shared__ uint8_t s_err[SM_TOPICS], s_fbk[SM_TOPICS];
+    __shared__ uint64_t s_off[ST + 1];
+    __shared__ uint8_t s_err[ST], s_fbk[ST];
     // the block's values staged in LDS and written as one contiguous span
     // (in place batches: a few whole PCIe writes instead of one per group)
     __shared__ uint32_t s_vals[SM_VSTAGE];
@@ -1225,29 +1237,30 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_small(DevIndex ix, Workspace 
     // so a block's predecessors are running or done (a start-order ticket, one
     // atomic on one word per block, serialised the blocks of a 64k batch:
     // 4,096 tickets; k_walk_lane, 64 topics per block, takes one)
-    // the block's SM_TOPICS + 1 topic offsets, read once by one wave (the
-    // caller's buffers may be host memory: one coalesced read, not one per group)
-    if (threadIdx.x <= SM_TOPICS && (uint64_t)vb * SM_TOPICS + threadIdx.x <= n)
-        s_off[threadIdx.x] = offs[(uint64_t)vb * SM_TOPICS + threadIdx.x];
+    // the block's ST + 1 topic offsets, read once by one wave (the caller's
+    // buffers may be host memory: one coalesced read, not one per group)
+    if (threadIdx.x <= ST && (uint64_t)vb * ST + threadIdx.x <= n)
+        s_off[threadIdx.x] = offs[(uint64_t)vb * ST + threadIdx.x];
     __syncthreads();
     const Group<W> grp;
     const uint32_t wv = threadIdx.x >> 6, gl = grp.gl, base = grp.g * W;
     const uint32_t gi = wv * G + grp.g;                   // topic slot in the block
-    const uint64_t t = (uint64_t)vb * SM_TOPICS + gi;
+    const uint64_t t = (uint64_t)vb * ST + gi;
     const bool live = t < n;
-    uint32_t *sl_ = s_slash[wv] + base, *sn_ = s_node[wv] + base, *hoff = s_hoff[wv] + base, *hcnt = s_hcnt[wv] + base;
-    uint64_t *sc_ = s_code[wv] + base, *hcode = s_hcode[wv] + base;
+    const uint32_t hbase = grp.g * HC;
+    uint32_t *sl_ = s_slash[wv] + base, *sn_ = s_node[wv] + base, *hoff = s_hoff[wv] + hbase, *hcnt = s_hcnt[wv] + hbase;
+    uint64_t *sc_ = s_code[wv] + base, *hcode = s_hcode[wv] + hbase;
     const uint64_t beg = live ? s_off[gi] : 0, end = live ? s_off[gi + 1] : 0, len = end - beg;
 
     // ---- the topic into LDS: one round of 16-B loads by the group's lanes
     // (the caller's buffers may be host memory read over PCIe: every byte
     // read from there would be a round trip).  Aligned chunks share their
     // granule with a valid byte, so they never touch a page the caller does
-    // not own.  A topic longer than SM_TB bytes goes to the lane walk.
+    // not own.  A topic longer than its row (TBQ chunks) goes to the lane walk.
     const uint64_t a0 = beg & ~15ull;
     const uint32_t nq = live ? (uint32_t)((end - a0 + 15) >> 4) : 0;
     bool fb = nq > TBQ;   // the group's first lane walks this topic (lane walk, global reads)
-    const uint32_t nt = (uint64_t)vb * SM_TOPICS + SM_TOPICS <= n ? SM_TOPICS : (uint32_t)(n - (uint64_t)vb * SM_TOPICS);
+    const uint32_t nt = (uint64_t)vb * ST + ST <= n ? ST : (uint32_t)(n - (uint64_t)vb * ST);
     const uint64_t B0 = s_off[0] & ~15ull;
     const uint64_t nqb = (s_off[nt] - B0 + 15) >> 4;
     const bool span = nqb <= TBQ_ALL;                     // (block-uniform)
@@ -1302,7 +1315,7 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_small(DevIndex ix, Workspace 
         const uint64_t m = grp.ballot(h);
         if (h) {
             const uint32_t k = nh + grp.rank(m);
-            if (k < W) { hcode[k] = c; hoff[k] = off; hcnt[k] = cnt; }
+            if (k < HC) { hcode[k] = c; hoff[k] = off; hcnt[k] = cnt; }
         }
         nh += (uint32_t)__popcll(m);
     };
@@ -1373,24 +1386,19 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_small(DevIndex ix, Workspace 
         }
         add_hits(gl == 0 && xcnt, ~0ull, xoff, xcnt);
     }
-    fb |= live && nh > W;
+    fb |= live && nh > HC;
 
-    // ---- rank the hits by path code (traversal order)
+    // ---- the hits' total (every lane); their ranks by path code below
     wave_sync();
-    const bool hv = live && !fb && gl < nh;
-    const uint64_t my = hv ? hcode[gl] : 0;
-    uint32_t rank = 0;
     uint64_t total = 0;
     if (live && !fb)
-        for (uint32_t j = 0; j < nh; j++) {
-            rank += hcode[j] < my;
-            total += hcnt[j] & RUN_CNT;
-        }
+        for (uint32_t j = 0; j < nh; j++) total += hcnt[j] & RUN_CNT;
 
     // ---- topics the group could not take: its first lane walks them (LDS store of MID_L levels)
     LdsStore<MID_L> st{s_mwid[gi], s_mpend[gi], s_mlen[gi], 1, 0};
     int frc = RC_OK;
-    if (fb && gl == 0) {
+    const bool walker = fb && gl == 0;
+    if (walker) {
         if (MODE == MODE_COUNT) {
             CountEmit em{0};
             frc = match_topic(ix, GlobalSrc{blob}, beg, end, st, em);
@@ -1404,7 +1412,11 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_small(DevIndex ix, Workspace 
     }
     if (MODE == MODE_FIRST) {
         if (live && !fb) {
-            if (hv && rank == 0) o.first_val[t] = (hcnt[gl] & RUN_INLINE) ? hoff[gl] : ix.vals[hoff[gl]];
+            for (uint32_t h = gl; h < nh; h += W) {   // the hit ranked first
+                uint32_t rank = 0;
+                for (uint32_t j = 0; j < nh; j++) rank += hcode[j] < hcode[h];
+                if (!rank) o.first_val[t] = (hcnt[h] & RUN_INLINE) ? hoff[h] : ix.vals[hoff[h]];
+            }
             if (gl == 0) {
                 if (!nh) o.first_val[t] = 0;
                 o.first_found[t] = badarg ? 2 : (nh ? 1 : 0);
@@ -1413,7 +1425,7 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_small(DevIndex ix, Workspace 
         return;
     }
 
-    // ---- the block's offset: exclusive scan of its 16 counts + decoupled look-back
+    // ---- the block's offset: exclusive scan of its ST counts + decoupled look-back
     if (gl == 0) {
         s_cnt[gi] = live ? total : 0;
         s_err[gi] = fb ? (frc == RC_BADARG ? 1 : frc == RC_DEEP ? 2 : 0) : badarg;
@@ -1422,7 +1434,7 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_small(DevIndex ix, Workspace 
     __syncthreads();
     if (wv == 0) {
         uint64_t sum = 0;
-        for (int i = 0; i < SM_TOPICS; i++) sum += s_cnt[i];
+        for (uint32_t i = 0; i < ST; i++) sum += s_cnt[i];
         // one flag round trip per 64 predecessors (look_back); a failed wait
         // fails this block and every later one: err 4, the fail word raised
         int res;
@@ -1437,18 +1449,18 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_small(DevIndex ix, Workspace 
         }
     }
     __syncthreads();
-    // the block's hit offsets and flags: lanes 0..15 of wave 0, one coalesced store each
-    if (threadIdx.x < SM_TOPICS && (uint64_t)vb * SM_TOPICS + threadIdx.x < n) {
+    // the block's hit offsets and flags: lanes 0..ST-1 of wave 0, one coalesced store each
+    if (threadIdx.x < ST && (uint64_t)vb * ST + threadIdx.x < n) {
         uint64_t p = s_base;
         for (uint32_t i = 0; i < threadIdx.x; i++) p += s_cnt[i];
-        hit_offs[(uint64_t)vb * SM_TOPICS + threadIdx.x] = (OT)p;
-        o.err[(uint64_t)vb * SM_TOPICS + threadIdx.x] = s_fail ? 4 : s_err[threadIdx.x];
+        hit_offs[(uint64_t)vb * ST + threadIdx.x] = (OT)p;
+        o.err[(uint64_t)vb * ST + threadIdx.x] = s_fail ? 4 : s_err[threadIdx.x];
     }
     if (s_fail) return;   // (block-uniform)
     // stage the block's values in LDS when they fit and no topic of the block
     // took the lane walk (which writes its values itself)
     bool stage = s_sum <= SM_VSTAGE;
-    for (uint32_t i = 0; i < SM_TOPICS; i++) stage &= !s_fbk[i];
+    for (uint32_t i = 0; i < ST; i++) stage &= !s_fbk[i];
     const uint64_t b0 = s_base;
     uint64_t pos = b0;
     for (uint32_t i = 0; i < gi; i++) pos += s_cnt[i];
@@ -1458,22 +1470,25 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_small(DevIndex ix, Workspace 
     };
 
     // ---- the values
-    if (live && fb) {
-        if (gl == 0 && frc == RC_OK) {   // (never with stage)
-            DirectEmit em{ix.vals, out, pos, cap};
-            match_topic(ix, GlobalSrc{blob}, beg, end, st, em);
-        }
-    } else if (live) {
-        uint32_t *roff = s_roff[wv] + base, *rcnt = s_rcnt[wv] + base;
-        uint64_t *rpos = s_rpos[wv] + base;
-        if (hv) {
+    if (walker && frc == RC_OK) {   // (never with stage)
+        DirectEmit em{ix.vals, out, pos, cap};
+        match_topic(ix, GlobalSrc{blob}, beg, end, st, em);
+    }
+    if (live && !fb) {
+        uint32_t *roff = s_roff[wv] + hbase, *rcnt = s_rcnt[wv] + hbase;
+        uint64_t *rpos = s_rpos[wv] + hbase;
+        for (uint32_t h = gl; h < nh; h += W) {
+            const uint64_t my = hcode[h];
+            uint32_t rank = 0;
             uint64_t before = 0;   // values of the hits ranked before this one
-            for (uint32_t j = 0; j < nh; j++) if (hcode[j] < my) before += hcnt[j] & RUN_CNT;
-            roff[rank] = hoff[gl]; rcnt[rank] = hcnt[gl]; rpos[rank] = pos + before;
+            for (uint32_t j = 0; j < nh; j++)
+                if (hcode[j] < my) { rank++; before += hcnt[j] & RUN_CNT; }
+            roff[rank] = hoff[h]; rcnt[rank] = hcnt[h]; rpos[rank] = pos + before;
         }
         wave_sync();
         // single-value runs (C3: almost every hit): lane r writes the one ranked r
-        if (gl < nh && (rcnt[gl] & RUN_INLINE)) put(rpos[gl], roff[gl]);
+        for (uint32_t r = gl; r < nh; r += W)
+            if (rcnt[r] & RUN_INLINE) put(rpos[r], roff[r]);
         for (uint32_t r = 0; r < nh; r++) {
             const uint32_t ro = roff[r], rc = rcnt[r];
             const uint64_t P = rpos[r];
@@ -2316,27 +2331,47 @@ hipError_t launch_match_phase2(const DevIndex &ix, const Workspace &ws, uint64_t
     return hipGetLastError();
 }
 
-// k_walk_lane where the index allows it (lane_path_ok) unless k_walk_small is
-// asked for; SMALL_LANE on an index the lane walk cannot take: k_walk_small
-bool small_lane(const DevIndex &ix, int kind) { return kind != SMALL_WAVE && lane_path_ok(ix); }
+// The one-launch kernel of a small batch (small_kind): k_walk_small with 16
+// or 8 lanes per topic, or k_walk_lane (one lane per topic) where the index
+// allows it (lane_path_ok; else k_walk_small's 16 lanes).
+struct SmallPick { bool lane; int w; };
+static SmallPick small_pick(const DevIndex &ix, int kind) {
+    if (kind == SMALL_LANE && lane_path_ok(ix)) return {true, 0};
+    return {false, kind == SMALL_WAVE8 ? 8 : 16};
+}
+bool small_lane(const DevIndex &ix, int kind) { return small_pick(ix, kind).lane; }
+static uint32_t small_topics_per_block(const SmallPick &k) {
+    return k.lane ? LANE_BLOCK : k.w == 8 ? SmallShape<8>::ST : SmallShape<16>::ST;
+}
+
+template <class OT>
+static void launch_small_kernel(const SmallPick &k, uint32_t blocks, const DevIndex &ix, const Workspace &ws,
+                                uint64_t n, const uint8_t *bytes, const OT *offs, uint8_t *err, OT *hit_offs,
+                                uint32_t *out, uint64_t cap, uint32_t tag, LbCtl lb, const SmallSegs &sg,
+                                hipStream_t s) {
+    Outs o{err, nullptr, nullptr};
+    if (k.lane)
+        hipLaunchKernelGGL((k_walk_lane<OT>), dim3(blocks), dim3(LANE_BLOCK), 0, s, ix, ws, n, bytes, offs, err,
+                           hit_offs, out, cap, tag, lb, sg);
+    else if (k.w == 8)
+        hipLaunchKernelGGL((k_walk_small<MODE_COUNT, OT, 8>), dim3(blocks), dim3(WV_BLOCK), 0, s, ix, ws, n, bytes,
+                           offs, o, hit_offs, out, cap, tag, lb, sg);
+    else
+        hipLaunchKernelGGL((k_walk_small<MODE_COUNT, OT, 16>), dim3(blocks), dim3(WV_BLOCK), 0, s, ix, ws, n, bytes,
+                           offs, o, hit_offs, out, cap, tag, lb, sg);
+}
 
 hipError_t launch_match(const DevIndex &ix, const Workspace &ws, uint64_t n, const uint8_t *bytes,
                         const uint64_t *offs, uint64_t *hit_offs, uint8_t *err, uint32_t *out, uint64_t cap,
                         uint32_t tag, LbCtl lb, bool phases, int small_kind, hipStream_t s, hipEvent_t ev_walk0,
                         hipEvent_t ev_walk1, int *path) {
     if (n && !phases && small_path_ok(ix, n)) {
-        const bool lane = small_lane(ix, small_kind);
-        if (path) *path = lane ? PATH_LANE : PATH_SMALL;
+        const SmallPick k = small_pick(ix, small_kind);
+        if (path) *path = k.lane ? PATH_LANE : PATH_SMALL;
         hipError_t e;
         if (ev_walk0 && (e = hipEventRecord(ev_walk0, s)) != hipSuccess) return e;
-        if (lane) {
-            hipLaunchKernelGGL((k_walk_lane<uint64_t>), dim3(blocks_for(n, LANE_BLOCK)), dim3(LANE_BLOCK), 0, s, ix, ws,
-                               n, bytes, offs, err, hit_offs, out, cap, tag & LB_TAG_MASK, lb, SmallSegs{});
-        } else {
-            Outs o{err, nullptr, nullptr};
-            hipLaunchKernelGGL((k_walk_small<MODE_COUNT, uint64_t>), dim3(blocks_for(n, SM_TOPICS)), dim3(WV_BLOCK), 0,
-                               s, ix, ws, n, bytes, offs, o, hit_offs, out, cap, tag & LB_TAG_MASK, lb, SmallSegs{});
-        }
+        launch_small_kernel<uint64_t>(k, blocks_for(n, small_topics_per_block(k)), ix, ws, n, bytes, offs, err,
+                                      hit_offs, out, cap, tag & LB_TAG_MASK, lb, SmallSegs{}, s);
         if (ev_walk1 && (e = hipEventRecord(ev_walk1, s)) != hipSuccess) return e;
         return hipGetLastError();
     }
@@ -2350,16 +2385,10 @@ hipError_t launch_match32(const DevIndex &ix, const Workspace &ws, uint64_t n, c
                           const uint32_t *offs, uint32_t *hit_offs, uint8_t *err, uint32_t *out, uint64_t cap,
                           uint32_t tag, LbCtl lb, int small_kind, hipStream_t s, int *path) {
     if (!small_path_ok(ix, n)) return hipErrorInvalidValue;   // (the caller converts instead)
-    const bool lane = small_lane(ix, small_kind);
-    if (path) *path = lane ? PATH_LANE : PATH_SMALL;
-    if (lane) {
-        hipLaunchKernelGGL((k_walk_lane<uint32_t>), dim3(blocks_for(n, LANE_BLOCK)), dim3(LANE_BLOCK), 0, s, ix, ws, n,
-                           bytes, offs, err, hit_offs, out, cap, tag & LB_TAG_MASK, lb, SmallSegs{});
-    } else {
-        Outs o{err, nullptr, nullptr};
-        hipLaunchKernelGGL((k_walk_small<MODE_COUNT, uint32_t>), dim3(blocks_for(n, SM_TOPICS)), dim3(WV_BLOCK), 0, s,
-                           ix, ws, n, bytes, offs, o, hit_offs, out, cap, tag & LB_TAG_MASK, lb, SmallSegs{});
-    }
+    const SmallPick k = small_pick(ix, small_kind);
+    if (path) *path = k.lane ? PATH_LANE : PATH_SMALL;
+    launch_small_kernel<uint32_t>(k, blocks_for(n, small_topics_per_block(k)), ix, ws, n, bytes, offs, err, hit_offs,
+                                  out, cap, tag & LB_TAG_MASK, lb, SmallSegs{}, s);
     return hipGetLastError();
 }
 
@@ -2367,35 +2396,24 @@ hipError_t launch_match32(const DevIndex &ix, const Workspace &ws, uint64_t n, c
 hipError_t launch_small_segs(const DevIndex &ix, const Workspace &ws, const SmallSegs &sg0, bool u32, uint32_t tag,
                              LbCtl lb, int small_kind, hipStream_t s, int *path) {
     SmallSegs sg = sg0;
-    const bool lane = small_lane(ix, small_kind);
-    const uint32_t per = lane ? LANE_BLOCK : SM_TOPICS;
+    const SmallPick k = small_pick(ix, small_kind);
+    const uint32_t per = small_topics_per_block(k);
     uint32_t blocks = 0;
-    for (uint32_t k = 0; k < sg.count; k++) {
-        if (!sg.s[k].n) return hipErrorInvalidValue;
-        sg.s[k].block0 = blocks;
-        blocks += blocks_for(sg.s[k].n, per);
+    for (uint32_t q = 0; q < sg.count; q++) {
+        if (!sg.s[q].n) return hipErrorInvalidValue;
+        sg.s[q].block0 = blocks;
+        blocks += blocks_for(sg.s[q].n, per);
     }
     if (!sg.count || sg.count > (uint32_t)SMALL_SEGS) return hipErrorInvalidValue;
-    if (path) *path = lane ? PATH_LANE : PATH_SMALL;
+    if (path) *path = k.lane ? PATH_LANE : PATH_SMALL;
     const SmallSeg &F = sg.s[0];
-    Outs o{F.err, nullptr, nullptr};
     const uint32_t tg = tag & LB_TAG_MASK;
-    if (lane && u32)
-        hipLaunchKernelGGL((k_walk_lane<uint32_t>), dim3(blocks), dim3(LANE_BLOCK), 0, s, ix, ws, (uint64_t)F.n, F.blob,
-                           static_cast<const uint32_t *>(F.offs), F.err, static_cast<uint32_t *>(F.hit), F.out, F.cap,
-                           tg, lb, sg);
-    else if (lane)
-        hipLaunchKernelGGL((k_walk_lane<uint64_t>), dim3(blocks), dim3(LANE_BLOCK), 0, s, ix, ws, (uint64_t)F.n, F.blob,
-                           static_cast<const uint64_t *>(F.offs), F.err, static_cast<uint64_t *>(F.hit), F.out, F.cap,
-                           tg, lb, sg);
-    else if (u32)
-        hipLaunchKernelGGL((k_walk_small<MODE_COUNT, uint32_t>), dim3(blocks), dim3(WV_BLOCK), 0, s, ix, ws,
-                           (uint64_t)F.n, F.blob, static_cast<const uint32_t *>(F.offs), o,
-                           static_cast<uint32_t *>(F.hit), F.out, F.cap, tg, lb, sg);
+    if (u32)
+        launch_small_kernel<uint32_t>(k, blocks, ix, ws, F.n, F.blob, static_cast<const uint32_t *>(F.offs), F.err,
+                                      static_cast<uint32_t *>(F.hit), F.out, F.cap, tg, lb, sg, s);
     else
-        hipLaunchKernelGGL((k_walk_small<MODE_COUNT, uint64_t>), dim3(blocks), dim3(WV_BLOCK), 0, s, ix, ws,
-                           (uint64_t)F.n, F.blob, static_cast<const uint64_t *>(F.offs), o,
-                           static_cast<uint64_t *>(F.hit), F.out, F.cap, tg, lb, sg);
+        launch_small_kernel<uint64_t>(k, blocks, ix, ws, F.n, F.blob, static_cast<const uint64_t *>(F.offs), F.err,
+                                      static_cast<uint64_t *>(F.hit), F.out, F.cap, tg, lb, sg, s);
     return hipGetLastError();
 }
 
@@ -2425,7 +2443,7 @@ hipError_t launch_first(const DevIndex &ix, const Workspace &ws, uint64_t n, con
     if (!n) return hipSuccess;
     Outs o{nullptr, out_value, out_found};
     if (small_path_ok(ix, n)) {
-        hipLaunchKernelGGL((k_walk_small<MODE_FIRST, uint64_t>), dim3(blocks_for(n, SM_TOPICS)), dim3(WV_BLOCK), 0, s,
+        hipLaunchKernelGGL((k_walk_small<MODE_FIRST, uint64_t, 16>), dim3(blocks_for(n, SM_TOPICS)), dim3(WV_BLOCK), 0, s,
                            ix, ws, n, bytes, offs, o, nullptr, nullptr, (uint64_t)0, 0u, LbCtl{LB_SPINS, NONE},
                            SmallSegs{});
         return hipGetLastError();

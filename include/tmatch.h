@@ -300,10 +300,11 @@ int tm_profile_read(tm_index *h, double *walk_ms, double *batch_ms, uint64_t *ba
  *   TM_DEBUG_PHASES         1: batches of <= 65536 topics take the two-phase
  *                           path too (walk, tails, scan, emit); 0 (default):
  *                           one launch where the index allows it
- *   TM_DEBUG_SMALL_KERNEL   the one-launch kernel of small batches: 0 (default)
- *                           k_walk_lane (one lane per topic) where the index
- *                           allows it, else k_walk_small; 1 k_walk_small (16
- *                           lanes per topic); 2 k_walk_lane where allowed
+ *   TM_DEBUG_SMALL_KERNEL   the one-launch kernel of small batches: 0 the
+ *                           default; 1 k_walk_small with 16
+ *                           lanes per topic; 2 k_walk_lane (one lane per
+ *                           topic) where the index allows it; 3 k_walk_small
+ *                           with 8 lanes per topic
  *   TM_DEBUG_COMBINE        concurrent combined launches of small 32-bit
  *                           in-place host batches (tm_match_batch32_ex): 0 =
  *                           every batch its own launch (default 4)

@@ -24,6 +24,11 @@ def torch_dev():
     return torch
 
 
+def _small_kind(kind: str) -> int:
+    """TM_DEBUG_SMALL_KERNEL value of a small-batch kernel name"""
+    return {"lane": _native.SMALL_LANE, "wave": _native.SMALL_WAVE, "wave8": _native.SMALL_WAVE8}[kind]
+
+
 def gpu_index(items: wl.ItemSet | None = None, flags=None) -> _native.Index:
     ix = _native.Index()
     if items is not None and len(items):
@@ -1235,7 +1240,7 @@ def test_concurrent_callers_see_consistent_snapshots(torch_dev, copies):
           f"p50 {np.percentile(lat, 50):.3f} ms p99 {np.percentile(lat, 99):.3f} ms")
 
 
-@pytest.mark.parametrize("kind", ["lane", "wave"])
+@pytest.mark.parametrize("kind", ["lane", "wave", "wave8"])
 def test_combined_callers_with_deltas_see_snapshots_and_never_fail(torch_dev, kind):
     """The NIF's production path under load:
     16 host threads submit in-place 32-bit batches (tm_match_batch32_ex on
@@ -1253,7 +1258,7 @@ def test_combined_callers_with_deltas_see_snapshots_and_never_fail(torch_dev, ki
     fs = wl.filters(1, nf)
     ix = _native.Index()
     ix.debug_set(_native.TM_DEBUG_COMBINE, 4)
-    ix.debug_set(_native.TM_DEBUG_SMALL_KERNEL, _native.SMALL_LANE if kind == "lane" else _native.SMALL_WAVE)
+    ix.debug_set(_native.TM_DEBUG_SMALL_KERNEL, _small_kind(kind))
     ix.apply(np.ones(len(fs), np.uint8), fs.blob, fs.offs, fs.vals)
     o = oracle_of(fs)
     r = random.Random(0x454D5158 + 99)
@@ -2138,10 +2143,11 @@ def _shallow_case(r, nt=700):
 
 
 def _all_kernels(ix, ts):
-    """the batch on k_walk_lane (default), k_walk_small and the two-phase path:
-    -> (hit, vals, err) of each, and the paths they took"""
+    """the batch on k_walk_lane, k_walk_small with 16 and 8 lanes per topic and
+    the two-phase path: -> (hit, vals, err) of each, and the paths they took"""
     out = []
-    for kind, phases in ((_native.SMALL_AUTO, 0), (_native.SMALL_WAVE, 0), (_native.SMALL_AUTO, 1)):
+    for kind, phases in ((_native.SMALL_LANE, 0), (_native.SMALL_WAVE, 0), (_native.SMALL_WAVE8, 0),
+                         (_native.SMALL_AUTO, 1)):
         ix.debug_set(_native.TM_DEBUG_SMALL_KERNEL, kind)
         ix.debug_set(_native.TM_DEBUG_PHASES, phases)
         p0 = _paths(ix)
@@ -2157,7 +2163,8 @@ def test_lane_walk_vs_oracle_and_the_other_kernels(torch_dev, seed):
     lane per topic, the block's topic bytes staged in LDS, a start-order
     ticket, look-back, emit): exact CSR against the oracle
     and bit-identical to k_walk_small and to the two-phase path forced on the
-    same batch -- topics deeper than the main store, badarg beyond it, more
+    same batch, and k_walk_small with 8 lanes per topic (fallbacks: more
+    than 8 levels or frontier states) -- topics deeper than the main store, badarg beyond it, more
     than 65536 levels, more than RCAP ranges, multi-value runs -- at batch
     sizes around a block's 64 topics and up to 65536; after deletes and
     re-inserts too; host, device and 32-bit APIs."""
@@ -2171,7 +2178,7 @@ def test_lane_walk_vs_oracle_and_the_other_kernels(torch_dev, seed):
         ts = items_of([topics[i % len(topics)] for i in r.sample(range(2 * n + 7), n)])
         runs = _all_kernels(ix, ts)
         # (a first run may be repeated to size the values buffer: capacity reruns)
-        assert [tuple(x > 0 for x in p) for _, p in runs] == [(0, 0, 1), (0, 1, 0), (1, 0, 0)], \
+        assert [tuple(x > 0 for x in p) for _, p in runs] == [(0, 0, 1), (0, 1, 0), (0, 1, 0), (1, 0, 0)], \
             [p for _, p in runs]
         (hit, v1, e1), _ = runs[0]
         assert_same(ix, o, ts)
@@ -2279,7 +2286,7 @@ def test_lane_walk_c3deep_and_index_gates(torch_dev):
 
 # ------------------------------------- device failures are not badarg (round 4)
 
-@pytest.mark.parametrize("kind", ["lane", "wave"])
+@pytest.mark.parametrize("kind", ["lane", "wave", "wave8"])
 def test_lookback_failure_is_retried_then_a_device_error(torch_dev, kind):
     """A one-launch small batch (k_walk_lane or k_walk_small) whose look-back
     wait expires (forced: block 3 acts as if its wait expired,
@@ -2294,7 +2301,7 @@ def test_lookback_failure_is_retried_then_a_device_error(torch_dev, kind):
     fs = wl.filters(3, 50_000)
     ts = wl.topics(3, 50_000, nt)
     ix, o = gpu_index(fs), oracle_of(fs)
-    ix.debug_set(_native.TM_DEBUG_SMALL_KERNEL, _native.SMALL_LANE if kind == "lane" else _native.SMALL_WAVE)
+    ix.debug_set(_native.TM_DEBUG_SMALL_KERNEL, _small_kind(kind))
     p0 = _paths(ix)
     assert_same(ix, o, ts)
     assert _paths(ix)[2 if kind == "lane" else 1] > p0[2 if kind == "lane" else 1]
@@ -2325,21 +2332,21 @@ def test_lookback_failure_is_retried_then_a_device_error(torch_dev, kind):
                        d_err.data_ptr(), torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
     err = d_err.cpu().numpy()
-    first = 3 * (64 if kind == "lane" else 16)   # topics per block (k_walk_lane: in ticket order)
+    first = 3 * {"lane": 64, "wave": 16, "wave8": 32}[kind]   # topics per block (k_walk_lane: in ticket order)
     assert not err[:first].any() and (err[first:] == 4).all()
     # the hook is spent: the next batches are exact again, with no failure
     assert_same(ix, o, ts)
     assert ix.debug_get(_native.TM_DEBUG_FAILED_BATCHES) == 5
 
 
-@pytest.mark.parametrize("kind", ["lane", "wave"])
+@pytest.mark.parametrize("kind", ["lane", "wave", "wave8"])
 def test_lookback_without_waiting_is_exact_or_a_device_error(torch_dev, kind):
     """With no wait at all (TM_DEBUG_LB_SPINS 0: a block fails whenever a
     predecessor has not published yet), every batch either matches exactly or
     fails as a device error -- never a wrong result, never BadArg."""
     fs = wl.filters(3, 50_000)
     ix, o = gpu_index(fs), oracle_of(fs)
-    ix.debug_set(_native.TM_DEBUG_SMALL_KERNEL, _native.SMALL_LANE if kind == "lane" else _native.SMALL_WAVE)
+    ix.debug_set(_native.TM_DEBUG_SMALL_KERNEL, _small_kind(kind))
     for nt in (3_000, 30_000, 65_536):
         ts = wl.topics(3, 50_000, nt)
         ix.debug_set(_native.TM_DEBUG_LB_SPINS, 0)
@@ -2402,7 +2409,7 @@ def test_router_boot_1m_routes_and_node_down_cleanup(torch_dev):
     assert r.mirror_keys() == len(filter_rows) - sum(1 for t, _ in dead if tfilter(t) is not False)
 
 
-@pytest.mark.parametrize("kind", ["lane", "wave"])
+@pytest.mark.parametrize("kind", ["lane", "wave", "wave8"])
 def test_combined_small_batches_equal_single_launches(torch_dev, kind):
     """The host-batch combiner (tm_host.cpp small_combined): concurrent callers'
     in-place 32-bit batches of 1 to 20k topics run as shared k_walk_lane (or
@@ -2413,7 +2420,7 @@ def test_combined_small_batches_equal_single_launches(torch_dev, kind):
     import threading
     fs = wl.filters(3, 200_000)
     ix, o = gpu_index(fs), oracle_of(fs)
-    ix.debug_set(_native.TM_DEBUG_SMALL_KERNEL, _native.SMALL_LANE if kind == "lane" else _native.SMALL_WAVE)
+    ix.debug_set(_native.TM_DEBUG_SMALL_KERNEL, _small_kind(kind))
     sizes = [1, 7, 100, 640, 3000, 4096, 9000, 20_000]
     sets = []
     for k, nt in enumerate(sizes):

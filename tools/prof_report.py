@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Turn one tools/gpu_prof.sh output directory into the committed evidence
+"""Turn one tools/gpu.sh `prof` output directory (gpurun_out/<tag>/prof) into the committed evidence
 under profiles/:
 
   profiles/<round>_<tag>.md            kernel-trace summary per kernel and grid
