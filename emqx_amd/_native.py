@@ -16,7 +16,7 @@ from .build import LIB_TMATCH
 
 TM_OK, TM_EINVAL, TM_ENOMEM, TM_EDEVICE, TM_ECAP = 0, -1, -2, -3, -4
 TM_OP_DELETE, TM_OP_INSERT = 0, 1
-TM_KEY_BINARY, TM_KEY_WORDS, TM_KEY_EMPTY_LIST = 0, 1, 2
+TM_KEY_BINARY, TM_KEY_WORDS, TM_KEY_EMPTY_LIST, TM_KEY_ESCAPED = 0, 1, 2, 4
 TM_ORDER_TRAVERSAL, TM_ORDER_SORTED, TM_ORDER_UNIQUE = 0, 1, 2
 
 # every symbol include/tmatch.h declares (tests check the export table)
@@ -26,7 +26,7 @@ EXPORTS = ("tm_create", "tm_destroy", "tm_apply_deltas", "tm_sync", "tm_match_ba
            "tm_stream_release", "tm_match_batch_ex", "tm_match_batch_dev_ex", "tm_sort_segments",
            "tm_matches_filter", "tm_apply_deltas_ex", "tm_read_begin", "tm_read_end", "tm_epoch",
            "tm_create_replicas", "tm_replica_stats", "tm_debug_set", "tm_debug_get", "tm_match_batch32_ex",
-           "tm_match_batch32_dev")
+           "tm_match_batch32_dev", "tm_matches_filter_ex")
 TM_DEBUG_LB_SPINS, TM_DEBUG_LB_FAIL_BLOCK, TM_DEBUG_LB_LAUNCHES, TM_DEBUG_PHASES = 1, 2, 3, 4
 TM_DEBUG_FAILED_BATCHES, TM_DEBUG_RETRIED_BATCHES = 5, 6
 TM_DEBUG_PATH_PHASES, TM_DEBUG_PATH_SMALL, TM_DEBUG_PATH_LANE = 7, 8, 9
@@ -87,6 +87,7 @@ def load_library(path: Path | None = None):
         "tm_match_batch_dev": (i32, [vp, u64, vp, vp, vp, vp, u64, vp, vp]),
         "tm_first_batch": (i32, [vp, u64, vp, vp, vp, vp]),
         "tm_matches_filter": (i32, [vp, u64, vp, vp, vp, vp, u64, vp]),
+        "tm_matches_filter_ex": (i32, [vp, u64, vp, vp, vp, vp, vp, u64, vp]),
         "tm_stats": (i32, [vp, C.POINTER(tm_stats_t)]),
         "tm_profile_enable": (i32, [vp, i32]),
         "tm_profile_read": (i32, [vp, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(u64), i32]),
@@ -312,18 +313,22 @@ class Index:
         self._check(self._lib.tm_first_batch(self._h, n, _ptr(blob), _ptr(offs), _ptr(val), _ptr(found)))
         return val[:n], found[:n]
 
-    def matches_filter_batch(self, blob: np.ndarray, offs: np.ndarray):
-        """matches_filter/3 for n subscription filters on the device (tm_matches_filter):
+    def matches_filter_batch(self, blob: np.ndarray, offs: np.ndarray, flags: np.ndarray | None = None):
+        """matches_filter/3 for n subscription filters on the device (tm_matches_filter_ex;
+        flags: TM_KEY_ESCAPED per filter given as an escaped word list, or None):
         -> (hit_offsets u64[n+1], values u32 in traversal order, err u8[n])."""
         n = len(offs) - 1
         blob = np.ascontiguousarray(blob, dtype=np.uint8)
         offs = np.ascontiguousarray(offs, dtype=np.uint64)
+        if flags is not None:
+            flags = np.ascontiguousarray(flags, dtype=np.uint8)
         hit = np.zeros(n + 1, dtype=np.uint64)
         err = np.zeros(max(n, 1), dtype=np.uint8)
         cap = 1024
         while True:
             out = np.zeros(max(cap, 1), dtype=np.uint32)
-            rc = self._lib.tm_matches_filter(self._h, n, _ptr(blob), _ptr(offs), _ptr(hit), _ptr(out), cap, _ptr(err))
+            rc = self._lib.tm_matches_filter_ex(self._h, n, _ptr(blob), _ptr(offs), _ptr(flags), _ptr(hit), _ptr(out),
+                                                cap, _ptr(err))
             if rc == TM_ECAP and int(hit[n]) > cap:
                 cap = int(hit[n])
                 continue

@@ -1013,8 +1013,88 @@ void mf_log(tm_index *ix, bool ins, const std::string &key) {
 }
 
 // one insert (ins = true) or delete of the key make_key(Filter, V)
+// An escaped word list (TM_KEY_WORDS | TM_KEY_ESCAPED): words split on '/',
+// "\x" = the byte x; a word written "\+" / "\#" is a binary word, a bare
+// "+" / "#" the wildcard.  -> (word bytes, wildcard?) per word.
+void esc_words(const uint8_t *f, uint32_t len, std::vector<std::pair<std::string, bool>> &out) {
+    out.clear();
+    std::string cur;
+    bool esc_any = false;
+    auto push = [&]() {
+        const bool wild = !esc_any && cur.size() == 1 && (cur[0] == '+' || cur[0] == '#');
+        out.emplace_back(cur, wild);
+        cur.clear();
+        esc_any = false;
+    };
+    for (uint32_t i = 0; i < len; i++) {
+        if (f[i] == '\\' && i + 1 < len) { cur.push_back((char)f[++i]); esc_any = true; }
+        else if (f[i] == '/') push();
+        else cur.push_back((char)f[i]);
+    }
+    push();
+}
+
+// the canonical escaped form of a word list ('/' and '\' escaped, binary
+// "+" / "#" as "\+" / "\#")
+std::string esc_join(const std::vector<std::pair<std::string, bool>> &w) {
+    std::string o;
+    for (size_t i = 0; i < w.size(); i++) {
+        if (i) o.push_back('/');
+        if (w[i].second) { o += w[i].first; continue; }
+        if (w[i].first == "+" || w[i].first == "#") { o.push_back('\\'); o += w[i].first; continue; }
+        for (char c : w[i].first) {
+            if (c == '/' || c == '\\') o.push_back('\\');
+            o.push_back(c);
+        }
+    }
+    return o;
+}
+
+// a binary word no topic level can equal: "+" / "#" (a level exactly that is
+// badarg) or one holding a '/'
+bool word_never(const std::pair<std::string, bool> &w) {
+    return !w.second && (w.first == "+" || w.first == "#" || w.first.find('/') != std::string::npos);
+}
+
+void word_key_op(tm_index *ix, bool ins, const std::vector<WordRef> &w, uint32_t v, const std::string &dk,
+                 bool dead_done);
+
 void key_op(tm_index *ix, bool ins, const uint8_t *f, uint32_t len, uint32_t v, uint8_t flags,
             std::vector<WordRef> &w, std::vector<uint32_t> &wids) {
+    if ((flags & TM_KEY_ESCAPED) && !(flags & TM_KEY_EMPTY_LIST)) {
+        std::vector<std::pair<std::string, bool>> ew;
+        esc_words(f, len, ew);
+        bool never = false;
+        for (auto &x : ew) never |= word_never(x);
+        if (!never) {   // plain words after all: the TM_KEY_WORDS key of the joined bytes
+            std::string plain;
+            for (size_t i = 0; i < ew.size(); i++) { if (i) plain.push_back('/'); plain += ew[i].first; }
+            key_op(ix, ins, reinterpret_cast<const uint8_t *>(plain.data()), (uint32_t)plain.size(), v,
+                   TM_KEY_WORDS, w, wids);
+            return;
+        }
+        // never matches a topic: a key of the table for matches_filter/3 only --
+        // but a '#' atom before its last word still steers the ordered walk at
+        // the node of the words before it, if those are plain (NLIT_HDESC)
+        const std::string canon = esc_join(ew);
+        const std::string dk = dead_key(reinterpret_cast<const uint8_t *>(canon.data()), (uint32_t)canon.size(), v,
+                                        TM_KEY_WORDS | TM_KEY_ESCAPED);
+        if (ix->mf.log_on) mf_log(ix, ins, dk);
+        if (ins ? !ix->dead.insert(dk).second : !ix->dead.erase(dk)) return;   // present / absent: no-op
+        size_t hpos = ew.size();
+        for (size_t i = 0; i + 1 < ew.size(); i++)
+            if (ew[i].second && ew[i].first == "#") { hpos = i; break; }
+        bool plain_prefix = hpos < ew.size();
+        for (size_t i = 0; i < hpos && plain_prefix; i++) plain_prefix = !word_never(ew[i]);
+        if (!plain_prefix) return;
+        std::vector<WordRef> pw;   // the prefix, the '#', and a stand-in for the rest (only the prefix is walked)
+        for (size_t i = 0; i <= hpos; i++)
+            pw.push_back({reinterpret_cast<const uint8_t *>(ew[i].first.data()), (uint32_t)ew[i].first.size(),
+                          ew[i].second ? (ew[i].first == "+" ? 1 : 2) : 0});
+        pw.push_back({nullptr, 0, 0});
+        word_key_op(ix, ins, pw, v, dk, true);
+        return;
+    }
     if (flags & TM_KEY_EMPTY_LIST) {   // [] never matches a topic (topics have >= 1 level)
         auto k = dead_key(nullptr, 0, v, TM_KEY_EMPTY_LIST);
         if (ins) ix->dead.insert(k); else ix->dead.erase(k);
@@ -1071,7 +1151,15 @@ void key_op(tm_index *ix, bool ins, const uint8_t *f, uint32_t len, uint32_t v, 
         ix->exact.touch(s);
         return;
     }
-    if (ix->mf.log_on) mf_log(ix, ins, dead_key(f, len, v, TM_KEY_WORDS));
+    word_key_op(ix, ins, w, v, dead_key(f, len, v, TM_KEY_WORDS), false);
+}
+
+// A word-list key (its words w; dk: its dead-key string, the identity
+// matches_filter/3 and the never-matching set know it by; dead_done: the
+// caller already logged it and entered it in that set).
+void word_key_op(tm_index *ix, bool ins, const std::vector<WordRef> &w, uint32_t v, const std::string &dk,
+                 bool dead_done) {
+    if (ix->mf.log_on && !dead_done) mf_log(ix, ins, dk);
     // word-list key.  '#' anywhere but last never matches (compare/3 has no
     // clause for it, emqx_trie_search.erl:282-290 vs :341-348; emqx_topic.erl:110),
     // but the key still steers the reference's walk at the node P of its
@@ -1079,10 +1167,9 @@ void key_op(tm_index *ix, bool ins, const uint8_t *f, uint32_t len, uint32_t v, 
     size_t hpos = w.size();
     for (size_t i = 0; i + 1 < w.size(); i++)
         if (w[i].kind == 2) { hpos = i; break; }
-    if (hpos < w.size()) {
+    if (hpos < w.size() && !dead_done) {
         // (a wildcard filter is a word list whatever the flag: one key)
-        auto k = dead_key(f, len, v, TM_KEY_WORDS);
-        if (ins ? !ix->dead.insert(k).second : !ix->dead.erase(k)) return;   // present / absent: no-op
+        if (ins ? !ix->dead.insert(dk).second : !ix->dead.erase(dk)) return;   // present / absent: no-op
     }
     const bool hash_term = hpos == w.size() && w.back().kind == 2;
     const size_t end = hpos < w.size() ? hpos : hash_term ? w.size() - 1 : w.size();
@@ -2538,12 +2625,21 @@ void mf_words_of(const uint8_t *p, uint32_t n, std::vector<std::string> &out) {
 
 // rank of a word: '#' 0, '+' 1, a binary word 3 + 2 i if it is words[i], else
 // 2 + 2 i (i = the words before it): term order (atoms < binaries, bytes)
-uint32_t mf_rank(const std::vector<std::string> &words, const std::string &w) {
-    if (w == "#") return 0;
-    if (w == "+") return 1;
+uint32_t mf_rank(const std::vector<std::string> &words, const std::string &w, bool wild) {
+    if (wild) return w == "#" ? 0 : 1;
     const auto it = std::lower_bound(words.begin(), words.end(), w);
     const uint32_t i = (uint32_t)(it - words.begin());
     return it != words.end() && *it == w ? 3 + 2 * i : 2 + 2 * i;
+}
+
+// the words of a key (or query) in bytes + flags form: escaped word lists
+// decoded, else split on '/' with bare "+" / "#" the wildcards
+void mf_key_words(const uint8_t *p, uint32_t n, uint8_t flags, std::vector<std::pair<std::string, bool>> &out) {
+    if (flags & TM_KEY_ESCAPED) { esc_words(p, n, out); return; }
+    std::vector<std::string> ws;
+    mf_words_of(p, n, ws);
+    out.clear();
+    for (auto &x : ws) out.emplace_back(x, x == "+" || x == "#");
 }
 
 void mf_free_keys(tm_index::MfState &m) {
@@ -2622,12 +2718,13 @@ void mf_snapshot(tm_index *ix) {
 // the device's term-ordered key arrays from m.keys (caller holds m.mu only)
 int mf_upload(tm_index *ix) {
     auto &m = ix->mf;
-    std::vector<std::string> dw, sorted;
+    std::vector<std::pair<std::string, bool>> dw;
+    std::vector<std::string> sorted;
     std::unordered_set<std::string> distinct;
     for (const std::string &k : m.keys) {
         if ((uint8_t)k[0] & TM_KEY_EMPTY_LIST) continue;
-        mf_words_of(reinterpret_cast<const uint8_t *>(k.data()) + 5, (uint32_t)k.size() - 5, dw);
-        for (auto &x : dw) if (x != "+" && x != "#") distinct.insert(x);
+        mf_key_words(reinterpret_cast<const uint8_t *>(k.data()) + 5, (uint32_t)k.size() - 5, (uint8_t)k[0], dw);
+        for (auto &x : dw) if (!x.second) distinct.insert(x.first);
     }
     sorted.assign(distinct.begin(), distinct.end());
     std::sort(sorted.begin(), sorted.end());
@@ -2640,8 +2737,8 @@ int mf_upload(tm_index *ix) {
         memcpy(&v, k.data() + 1, 4);
         const uint64_t off = pool.size();
         if (!((uint8_t)k[0] & TM_KEY_EMPTY_LIST)) {
-            mf_words_of(reinterpret_cast<const uint8_t *>(k.data()) + 5, (uint32_t)k.size() - 5, dw);
-            for (auto &x : dw) pool.push_back(mf_rank(sorted, x));
+            mf_key_words(reinterpret_cast<const uint8_t *>(k.data()) + 5, (uint32_t)k.size() - 5, (uint8_t)k[0], dw);
+            for (auto &x : dw) pool.push_back(mf_rank(sorted, x.first, x.second));
         }
         keys.push_back(K{off, (uint32_t)(pool.size() - off), v});
     }
@@ -2727,6 +2824,11 @@ extern "C" {
 
 int tm_matches_filter(tm_index *ix, uint64_t n, const uint8_t *fb, const uint64_t *fo, uint64_t *out_hit_offsets,
                       uint32_t *out_values, uint64_t cap, uint8_t *out_err) {
+    return tm_matches_filter_ex(ix, n, fb, fo, nullptr, out_hit_offsets, out_values, cap, out_err);
+}
+
+int tm_matches_filter_ex(tm_index *ix, uint64_t n, const uint8_t *fb, const uint64_t *fo, const uint8_t *ff,
+                         uint64_t *out_hit_offsets, uint32_t *out_values, uint64_t cap, uint8_t *out_err) {
     if (!ix) return fail(nullptr, TM_EINVAL, "tm_matches_filter: null handle");
     if (!fo || !out_hit_offsets || !out_err || (n && !fb && fo[n] != fo[0]) || (cap && !out_values))
         return fail(ix, TM_EINVAL, "tm_matches_filter: null buffer");
@@ -2739,11 +2841,11 @@ int tm_matches_filter(tm_index *ix, uint64_t n, const uint8_t *fb, const uint64_
     if ((rc = mf_refresh(ix))) return rc;
     // queries: filter_words/1 (:359-366) -> ranks; base_init on a '$' first word
     std::vector<uint32_t> qoff(n + 1, 0), qr, qbase(n, NONE);
-    std::vector<std::string> w;
+    std::vector<std::pair<std::string, bool>> w;
     for (uint64_t i = 0; i < n; i++) {
-        mf_words_of(fb + fo[i], (uint32_t)(fo[i + 1] - fo[i]), w);
-        for (auto &x : w) qr.push_back(mf_rank(m.words, x));
-        if (!w[0].empty() && w[0][0] == '$' && w[0] != "+" && w[0] != "#") qbase[i] = mf_rank(m.words, w[0]);
+        mf_key_words(fb + fo[i], (uint32_t)(fo[i + 1] - fo[i]), ff ? ff[i] : 0, w);
+        for (auto &x : w) qr.push_back(mf_rank(m.words, x.first, x.second));
+        if (!w[0].second && !w[0].first.empty() && w[0].first[0] == '$') qbase[i] = mf_rank(m.words, w[0].first, false);
         qoff[i + 1] = (uint32_t)qr.size();
     }
     const uint64_t qwords = (n + 1) + qr.size() + n + n;   // offsets, ranks, bases, counts

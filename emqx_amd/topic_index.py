@@ -39,7 +39,7 @@ import numpy as np
 
 from . import _native
 from .trie_search import (BadArg, HASH, PLUS, filter_words, get_id, get_topic, key_order,  # noqa: F401
-                          make_key, search_filter, term_key, topic_words)
+                          make_key, term_key, topic_words)
 
 
 class Tab:
@@ -53,7 +53,6 @@ class Tab:
         self._free: list[int] = []      # u32s no reader can still return
         self._released: list[int] = []  # freed by deletes not yet shipped
         self._quarantine = deque()      # (epoch of the delete, u32): reusable once the safe epoch reaches it
-        self._dead: set = set()         # keys that can never match (kept host-side only)
         self._ops: list = []            # pending (op, filter_bytes, kid, flags)
         self._lock = threading.Lock()   # pending deltas and u32 bookkeeping (writer side)
         self._sorted = None             # (keys, order keys) in term order, for matches_filter/3
@@ -61,31 +60,16 @@ class Tab:
     # -- key <-> device encoding
     @staticmethod
     def _encode(key):
-        """-> (filter bytes, flags) for tm_apply_deltas, or None for a key no topic can match."""
+        """-> (filter bytes, flags) for tm_apply_deltas (include/tmatch.h "Keys")."""
         f = key[0]
         if not isinstance(f, tuple):
             return bytes(f), _native.TM_KEY_BINARY
         if len(f) == 0:
             return b"", _native.TM_KEY_EMPTY_LIST
-        parts = []
-        for w in f:
-            if w == PLUS or w == HASH:
-                parts.append(w.encode())
-            elif isinstance(w, (bytes, bytearray)):
-                w = bytes(w)
-                # a binary word "+"/"#" or one containing '/' never equals a topic level
-                if w in (b"+", b"#") or b"/" in w:
-                    return None
-                parts.append(w)
-            else:
-                raise TypeError(f"bad filter word {w!r}")
-        return b"/".join(parts), _native.TM_KEY_WORDS
+        return encode_words(f)
 
     def _queue(self, op, key, kid):
         enc = self._encode(key)
-        if enc is None:
-            (self._dead.add if op else self._dead.discard)(key)
-            return
         self._ops.append((op, enc[0], kid, enc[1]))
 
     def flush(self):
@@ -327,25 +311,53 @@ def matches_filter(filter_, tab: Tab, opts=()):
     Its result depends on where the ordered walk stops (a stored key below the
     query at a query '+' ends the whole search), which the trie walk has no
     notion of, so the device runs the reference's walk itself over the keys in
-    term order (tm_matches_filter).  Keys the device does not hold (binary
-    words '+'/'#' or words containing '/', kept host-side) take their place in
-    that order too: a table holding any, or a word-list query, runs the same
-    walk on the host over the table's ordered key set.  Callers are
+    term order (tm_matches_filter_ex) -- every key of the table, those no topic
+    can match included (binary words '+'/'#' or holding a '/': the escaped
+    key form), and a query given as a word list in the same form.  Callers are
     control-plane (durable-storage stream discovery,
     emqx_ds_new_streams.erl:325)."""
-    if not tab._dead and isinstance(filter_, (bytes, bytearray)):
-        ticket = tab.read_begin()
-        try:
-            tab.flush()
-            blob, offs = _native.pack_strings([bytes(filter_)])
-            _, vals, err = tab._index.matches_filter_batch(blob, offs)
-            if len(err) and err[0]:   # the device walk hit its step bound: no silent truncation
-                raise RuntimeError(f"matches_filter: device walk exceeded its step bound for {bytes(filter_)!r}")
-            return _finish(tab.decode(vals), opts)
-        finally:
-            tab.read_end(ticket)
-    keys, order = tab.sorted_keys()
-    return _finish(search_filter(keys, order, filter_words(filter_)), opts)
+    if isinstance(filter_, (bytes, bytearray)):
+        q, qf = bytes(filter_), 0
+    else:
+        q, qf = encode_words(tuple(filter_words(filter_)))
+    ticket = tab.read_begin()
+    try:
+        tab.flush()
+        blob, offs = _native.pack_strings([q])
+        _, vals, err = tab._index.matches_filter_batch(blob, offs, np.array([qf], np.uint8))
+        if len(err) and err[0]:   # the device walk hit its step bound: no silent truncation
+            raise RuntimeError(f"matches_filter: device walk exceeded its step bound for {filter_!r}")
+        return _finish(tab.decode(vals), opts)
+    finally:
+        tab.read_end(ticket)
+
+
+def encode_words(words):
+    """A word list -> (bytes, flags) in the C ABI's key form: '/'-joined
+    (TM_KEY_WORDS), or -- when a binary word holds a '/' or equals "+" / "#",
+    which no topic level can equal -- the escaped form (TM_KEY_WORDS |
+    TM_KEY_ESCAPED: "\\/" a '/', "\\\\" a '\\', "\\+" / "\\#" the binary
+    words, bare "+" / "#" the wildcards).  The library keeps such a key for
+    matches_filter/3 only; it never matches a topic."""
+    plain, esc, escaped = [], [], False
+    for w in words:
+        if w == PLUS or w == HASH:
+            plain.append(w.encode())
+            esc.append(w.encode())
+        elif isinstance(w, (bytes, bytearray)):
+            w = bytes(w)
+            if w in (b"+", b"#"):
+                escaped = True
+                esc.append(b"\\" + w)
+            else:
+                escaped |= b"/" in w
+                esc.append(w.replace(b"\\", b"\\\\").replace(b"/", b"\\/"))
+            plain.append(w)
+        else:
+            raise TypeError(f"bad filter word {w!r}")
+    if escaped:
+        return b"/".join(esc), _native.TM_KEY_WORDS | _native.TM_KEY_ESCAPED
+    return b"/".join(plain), _native.TM_KEY_WORDS
 
 
 def get_record(key, tab: Tab):

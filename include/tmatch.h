@@ -38,8 +38,16 @@
  * Key form follows make_key/2: a binary filter with a '+'/'#' level is a word
  * list; a binary without one is a binary key; TM_KEY_WORDS forces the
  * word-list form (make_key(Words, ID) with a list); TM_KEY_EMPTY_LIST is the
- * word list [] (which has no byte form).  Inserting an existing key and
- * deleting a missing key are no-ops (ETS set semantics, emqx_topic_index.erl:58-62).
+ * word list [] (which has no byte form).  TM_KEY_WORDS | TM_KEY_ESCAPED is
+ * a word list whose binary words may hold any bytes: words are separated by
+ * '/', and inside a word "\/" stands for a '/' byte and "\\" for a '\';
+ * a word written "\+" or "\#" is the binary word <<"+">> / <<"#">>, where
+ * a bare "+" / "#" is the wildcard ('+' / '#' atoms).  A key with such a
+ * word can never match a publish topic (a topic level is never "+" or "#",
+ * never holds a '/'), but it is one of the table's keys for matches_filter/3
+ * (tm_matches_filter), where it takes its place in Erlang term order.
+ * Inserting an existing key and deleting a missing key are no-ops (ETS set
+ * semantics, emqx_topic_index.erl:58-62).
  *
  * Output.  For each topic the matching values are written in TRAVERSAL order:
  * ascending Erlang term order of the keys {Filter, {Value}} -- word-list keys
@@ -81,7 +89,7 @@ enum {
 };
 
 enum { TM_OP_DELETE = 0, TM_OP_INSERT = 1 };
-enum { TM_KEY_BINARY = 0, TM_KEY_WORDS = 1, TM_KEY_EMPTY_LIST = 2 };
+enum { TM_KEY_BINARY = 0, TM_KEY_WORDS = 1, TM_KEY_EMPTY_LIST = 2, TM_KEY_ESCAPED = 4 };
 
 typedef struct {
     int32_t device;          /* HIP device ordinal; -1 = current device        */
@@ -270,6 +278,13 @@ int tm_first_batch(tm_index *h, uint64_t n, const uint8_t *topic_bytes, const ui
  * walk exceeded its step bound (never for a valid filter). */
 int tm_matches_filter(tm_index *h, uint64_t n, const uint8_t *filter_bytes, const uint64_t *filter_offsets,
                       uint64_t *out_hit_offsets, uint32_t *out_values, uint64_t cap, uint8_t *out_err);
+/* The same with a flags byte per filter (may be NULL: all plain):
+ * TM_KEY_ESCAPED marks a filter given as an escaped word list (the key form
+ * above) -- matches_filter(Words, Tab, Opts) with binary words that hold a
+ * '/' or equal "+" / "#". */
+int tm_matches_filter_ex(tm_index *h, uint64_t n, const uint8_t *filter_bytes, const uint64_t *filter_offsets,
+                         const uint8_t *filter_flags, uint64_t *out_hit_offsets, uint32_t *out_values, uint64_t cap,
+                         uint8_t *out_err);
 
 int tm_stats(tm_index *h, tm_stats_t *out);
 

@@ -141,3 +141,79 @@ def frontier(o: "Oracle", blob, offs, nthreads: int = 8):
 def spec_match(topic: bytes, flt: bytes, words_form: bool = False) -> bool:
     """emqx_topic:match/2 restated (brute-force oracle)."""
     return bool(load().orc_spec_match(topic, len(topic), flt, len(flt), int(words_form)))
+
+
+# ------------------------------------------------------------ matches_filter
+#
+# The reference's ordered matches_filter/3 walk restated in Python over a
+# sorted key list (emqx_trie_search.erl:186-253 with the filter clauses of
+# compare/3, :260-348): a second, independent restatement next to
+# tm_oracle.c's orc_matches_filter, for tests/test_matches_filter_cpu.py.  The
+# product runs this walk on the device only (tm_matches_filter_ex).
+
+from emqx_amd.trie_search import HASH, PLUS, term_key  # noqa: E402
+
+FULL, PREFIX, LOWER = "match_full", "match_prefix", "lower"
+
+
+def compare_filter(f, w):
+    """compare/3 (emqx_trie_search.erl:260-348) with a FILTER query `w`: the
+    filter clauses (:291-300) come before the stored-'+' clause, so a query '+'
+    passes any stored word over without turning a later 'lower' into a seek.
+    -> FULL / PREFIX / LOWER / seek position (int)."""
+    if not isinstance(f, tuple):
+        return LOWER                                         # :260-261 binary key
+    lastplus = -1
+    i = 0
+    while True:
+        if i == len(f):
+            return FULL if i == len(w) else PREFIX           # :262-281
+        if f[i] == HASH and i == len(f) - 1:
+            return FULL                                      # :282-290
+        if i < len(w) and w[i] == HASH and i == len(w) - 1:
+            return FULL                                      # :292-293
+        if i == len(w):
+            break                                            # :333-340 lower
+        if w[i] == PLUS:
+            i += 1                                           # :294-300
+            continue
+        if f[i] == PLUS:
+            lastplus = i                                     # :302-320
+            i += 1
+            continue
+        a, b = term_key(f[i]), term_key(w[i])
+        if a == b:
+            i += 1                                           # :321-324
+            continue
+        if a > b:
+            break                                            # :325-332 lower
+        return i                                             # :341-348 seek
+    return lastplus if lastplus >= 0 else LOWER
+
+
+def _base_order(prefix):
+    """order key of base(Prefix) = {Prefix, {}}: before every {Prefix, {ID}}"""
+    return ((8, tuple(term_key(x) for x in prefix)), (-1,))
+
+
+def search_filter(keys, order, words):
+    """matches_filter's ordered search (emqx_trie_search.erl:186-253, no
+    match_topics phase) over `keys` sorted in term order (`order[i]` =
+    key_order(keys[i])).  -> matching keys in traversal order."""
+    import bisect
+    base = (words[0],) if words and isinstance(words[0], bytes) and words[0][:1] == b"$" else ()   # :160-163
+    cur = bisect.bisect_right(order, _base_order(base))
+    out = []
+    while cur < len(keys):
+        k = keys[cur]
+        r = compare_filter(k[0], words)
+        if r == FULL:
+            out.append(k)
+            cur = bisect.bisect_right(order, order[cur])
+        elif r == PREFIX:
+            cur = bisect.bisect_right(order, order[cur])
+        elif r == LOWER:
+            break
+        else:
+            cur = bisect.bisect_right(order, _base_order(tuple(k[0][:r]) + (words[r],)))   # seek/3 :255-258
+    return out

@@ -1442,6 +1442,82 @@ def test_readers_never_decode_a_reused_value(torch_dev):
           f"{len(tab._keys)} values for {len(stable) + inserted} keys")
 
 
+def test_matches_filter_keys_no_topic_can_match(torch_dev):
+    """Word-list keys with binary words no topic level can equal -- <<"+">>,
+    <<"#">>, words holding a '/' (make_key(Words, ID) with such binaries; the
+    rule engine indexes unvalidated FROM topics, emqx_rule_engine.erl:534-540)
+    -- reach the library in the escaped key form and take their place in
+    matches_filter/3's term-ordered walk on the device, for byte and word-list
+    queries (escaped words included), equal to the Python restatement of the
+    reference's walk (oracle/pyoracle.py search_filter) over the same key set;
+    deletes and re-inserts included.  They never match a topic, except that a
+    '#' atom before the last word steers the ordered walk at its plain prefix
+    as a plain '#'-not-last key does (NLIT_HDESC)."""
+    from pyoracle import search_filter
+    from emqx_amd.trie_search import HASH, PLUS, filter_words, key_order
+    r = random.Random(0x454D5158 + 77)
+    plain = [b"a", b"b", b"c", b"$s", b""]
+    odd = [b"+", b"#", b"a/b", b"/", b"x/", b"\\", b"c\\/d"]
+
+    def word(odd_p):
+        c = r.random()
+        if c < 0.2:
+            return PLUS
+        if c < 0.3:
+            return HASH
+        return r.choice(odd) if r.random() < odd_p else r.choice(plain)
+
+    for seed in range(4):
+        tab = ti.new()
+        keys = []
+        for i in range(400):
+            ws = tuple(word(0.25) for _ in range(r.randint(1, 4)))
+            k = ti.make_key(ws, i)
+            keys.append(k)
+            ti.insert(ws, i, None, tab)
+        for i in range(400, 460):   # binary keys and []
+            f = b"/".join(r.choice(plain) for _ in range(r.randint(1, 3)))
+            keys.append(ti.make_key(f, i))
+            ti.insert(f, i, None, tab)
+        ti.insert((), 999, None, tab)
+        keys.append(ti.make_key((), 999))
+
+        def expect(q):
+            live = sorted(set(tab.keys()), key=key_order)
+            return ti._finish(search_filter(live, [key_order(k) for k in live], filter_words(q)), [])
+
+        queries = [b"/".join(r.choice(plain + [b"+"]) for _ in range(r.randint(1, 4))) for _ in range(60)]
+        queries += [b"#", b"a/#", b"+/+", b"$s/+", b"a/+/#"]
+        queries += [tuple(word(0.3) for _ in range(r.randint(1, 4))) for _ in range(60)]   # word lists
+        for q in queries:
+            if not isinstance(q, bytes) and HASH in q[:-1]:
+                continue   # (filter_words of a list: the caller's words as given; '#' only last in a filter)
+            assert ti.matches_filter(q, tab) == expect(q), (seed, q)
+        # deletes, then the same keys back
+        gone = r.sample(keys, 150)
+        for k in gone:
+            ti.delete(k[0], k[1][0], tab)
+        for q in queries[:40]:
+            assert ti.matches_filter(q, tab) == expect(q), (seed, "after deletes", q)
+        for k in gone:
+            ti.insert(k[0], k[1][0], None, tab)
+        for q in queries[:40]:
+            assert ti.matches_filter(q, tab) == expect(q), (seed, "after re-inserts", q)
+    # topic matching: the escaped keys never match; one with a '#' atom before
+    # its last word cuts the walk at its plain prefix like 'a/#/z' would
+    filters = [b"a/+", b"a/b/c", b"+/+/+", b"a/#", b"#"]
+    fs = items_of(filters)
+    ix = gpu_index(fs)
+    e = ti.encode_words((b"a", HASH, b"x/y"))
+    ix.apply(np.ones(2, np.uint8), *_native.pack_strings([e[0], b"q\\/r/+"]), np.array([100, 101], np.uint32),
+             np.array([e[1], e[1]], np.uint8))
+    o = oracle_of(items_of(filters + [b"a/#/z"], list(range(len(filters))) + [100]),
+                  np.array([0] * len(filters) + [1], np.uint8))
+    ts = items_of([b"a", b"a/b", b"a/b/c", b"q/r/s", b"q", b"x/y/z", b"a//"])
+    assert_same(ix, o, ts)
+    assert ix.stats()["n_dead_keys"] == 2
+
+
 def test_matches_filter_does_not_stall_matching(torch_dev):
     """tm_matches_filter builds its term-ordered keys from a snapshot taken in
     slices of ~100 us under the index lock plus a log of key ops, and sorts /
@@ -2185,6 +2261,7 @@ def test_lane_walk_vs_oracle_and_the_other_kernels(torch_dev, seed):
         for (h, v, e), _ in runs[1:]:
             assert np.array_equal(hit, h) and np.array_equal(v1, v) and np.array_equal(e1, e)
     assert np.diff(hit.astype(np.int64)).max() > 8 * 2        # some topic beyond RCAP ranges
+    ix.debug_set(_native.TM_DEBUG_SMALL_KERNEL, _native.SMALL_LANE)   # the lane walk from here on
     # device API on a torch stream
     d_blob, d_offs = torch.from_numpy(ts.blob).cuda(), torch.from_numpy(ts.offs.view(np.int64)).cuda()
     d_hit = torch.zeros(len(ts) + 1, dtype=torch.int64, device="cuda")
@@ -2235,6 +2312,7 @@ def test_lane_walk_long_topics_read_global_memory(torch_dev):
                for _ in range(3_000)] + [b"#", b"w1/#", b"+/+/#"]
     fs = items_of(filters)
     ix, o = gpu_index(fs), oracle_of(fs)
+    ix.debug_set(_native.TM_DEBUG_SMALL_KERNEL, _native.SMALL_LANE)
     topics = []
     for i in range(5_000):
         blk = (i // 64) % 3   # blocks of short topics, of ~180-byte topics, and mixed
@@ -2265,6 +2343,7 @@ def test_lane_walk_c3deep_and_index_gates(torch_dev):
     fs = wl.filters(3, 200_000)
     ts = wl.topics(30, 200_000, 60_000)
     ix, o = gpu_index(fs), oracle_of(fs)
+    ix.debug_set(_native.TM_DEBUG_SMALL_KERNEL, _native.SMALL_LANE)
     p0 = _paths(ix)
     assert_same(ix, o, ts)
     assert _paths(ix)[2] > p0[2]

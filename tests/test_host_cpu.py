@@ -41,11 +41,17 @@ def test_finish_orders_like_reference():
     assert _finish(keys, [])[0] == make_key(b"a/b/c", 4)
 
 
-def test_encode_dead_word_lists():
-    assert Tab._encode(((b"a/b", PLUS), (1,))) is None
-    assert Tab._encode(((b"+",), (1,))) is None
+def test_encode_word_lists_no_topic_can_match():
+    """Binary words no topic level can equal ('+' / '#' as binaries, words
+    holding a '/') take the escaped key form (include/tmatch.h "Keys"): the
+    library keeps them for matches_filter/3 only."""
+    esc = 1 | 4   # TM_KEY_WORDS | TM_KEY_ESCAPED
+    assert Tab._encode(((b"a/b", PLUS), (1,))) == (b"a\\/b/+", esc)
+    assert Tab._encode(((b"+",), (1,))) == (b"\\+", esc)
+    assert Tab._encode(((b"x\\y", b"#", HASH), (1,))) == (b"x\\\\y/\\#/#", esc)
     assert Tab._encode(((), (1,))) == (b"", 2)
     assert Tab._encode(((b"a", PLUS), (1,))) == (b"a/+", 1)
+    assert Tab._encode(((b"a\\b", PLUS), (1,))) == (b"a\\b/+", 1)   # a backslash alone: no escape needed
 
 
 def test_workload_deterministic_and_sharded():

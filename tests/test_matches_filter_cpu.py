@@ -1,6 +1,6 @@
 """matches_filter/3 (emqx_trie_search.erl:186-189 + the filter clauses of
 compare/3, :291-300): the Python mirror's ordered search
-(emqx_amd.trie_search.search_filter, which emqx_amd.topic_index.matches_filter
+(oracle/pyoracle.py search_filter, the Python restatement the device walk
 runs over a table's ordered key set) against the C oracle's independent
 restatement (oracle/tm_oracle.c orc_matches_filter, a sorted array with its own
 term-order comparator), plus known answers worked out from the reference's
@@ -11,8 +11,8 @@ import random
 
 import pytest
 
-from emqx_amd.trie_search import filter_words, get_id, key_order, make_key, search_filter
-from pyoracle import Oracle
+from emqx_amd.trie_search import filter_words, get_id, key_order, make_key
+from pyoracle import Oracle, search_filter
 
 
 def _index(filters, words_form=()):
