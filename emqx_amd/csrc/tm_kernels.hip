@@ -1174,6 +1174,9 @@ bool small_path_ok(const DevIndex &ix, uint64_t n) { return n && n <= SMALL_TOPI
 // topics per wave slot for concurrent callers, whose launches together fill
 // every slot of the GPU; levels and frontier states per topic <= 8, else the
 // lane walk).  A group keeps up to HC hit ranges (C3: 8.4 per topic).
+// LITE: the fallback lane walk's store holds FAST_L levels and resolves only
+// need_levels() (as k_walk_lane's; lane_path_ok indexes: shallow, no
+// '#'-not-last key) instead of MID_L: 76 instead of 292 B of LDS per topic.
 template <int W>
 struct SmallShape {
     static constexpr uint32_t G = 64 / W;                          // topics per wave
@@ -1184,7 +1187,7 @@ struct SmallShape {
 };
 static_assert(SmallShape<16>::ST == SM_TOPICS, "SM_TOPICS: the most blocks a small batch launches per topic");
 
-template <int MODE, class OT, int W>
+template <int MODE, class OT, int W, bool LITE>
 __global__ __launch_bounds__(WV_BLOCK) void k_walk_small(DevIndex ix, Workspace ws, uint64_t n_, const uint8_t *blob_,
                                                          const OT *offs_, Outs o, OT *hit_offs_,
                                                          uint32_t *out_, uint64_t cap_, uint32_t tag, LbCtl lb,
@@ -1212,12 +1215,14 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_small(DevIndex ix, Workspace 
     __shared__ uint32_t s_slash[WV_WAVES][64];
     __shared__ uint32_t s_node[WV_WAVES][64];
     __shared__ uint64_t s_code[WV_WAVES][64];
+    // a group's hits (path code, value run) -- by rank once they are ranked
+    // (then the code's slot holds the hit's first output position)
     __shared__ uint64_t s_hcode[WV_WAVES][G * HC];
     __shared__ uint32_t s_hoff[WV_WAVES][G * HC], s_hcnt[WV_WAVES][G * HC];
-    __shared__ uint32_t s_roff[WV_WAVES][G * HC], s_rcnt[WV_WAVES][G * HC];   // hits by rank
-    __shared__ uint64_t s_rpos[WV_WAVES][G * HC];
-    __shared__ uint32_t s_mwid[ST][MID_L], s_mpend[ST][MID_L + 1];   // fallback lane-walk stores
-    __shared__ uint8_t s_mlen[ST][MID_L];
+    constexpr uint32_t FBL = LITE ? FAST_L : MID_L;       // levels of the fallback lane walk's store
+    using FbStore = LdsStore<FBL, LITE>;
+    __shared__ uint32_t s_mwid[ST][FBL], s_mpend[ST][FBL + 1];   // fallback lane-walk stores
+    __shared__ uint8_t s_mlen[ST][FBL];
     __shared__ uint64_t s_cnt[ST];
     __shared__ uint64_t s_base;
     __shared__ uint32_t s_fail;
@@ -1394,8 +1399,8 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_small(DevIndex ix, Workspace 
     if (live && !fb)
         for (uint32_t j = 0; j < nh; j++) total += hcnt[j] & RUN_CNT;
 
-    // ---- topics the group could not take: its first lane walks them (LDS store of MID_L levels)
-    LdsStore<MID_L> st{s_mwid[gi], s_mpend[gi], s_mlen[gi], 1, 0};
+    // ---- topics the group could not take: its first lane walks them (LDS store of FBL levels)
+    FbStore st{s_mwid[gi], s_mpend[gi], s_mlen[gi], 1, 0};
     int frc = RC_OK;
     const bool walker = fb && gl == 0;
     if (walker) {
@@ -1475,16 +1480,30 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_small(DevIndex ix, Workspace 
         match_topic(ix, GlobalSrc{blob}, beg, end, st, em);
     }
     if (live && !fb) {
-        uint32_t *roff = s_roff[wv] + hbase, *rcnt = s_rcnt[wv] + hbase;
-        uint64_t *rpos = s_rpos[wv] + hbase;
-        for (uint32_t h = gl; h < nh; h += W) {
-            const uint64_t my = hcode[h];
-            uint32_t rank = 0;
-            uint64_t before = 0;   // values of the hits ranked before this one
-            for (uint32_t j = 0; j < nh; j++)
-                if (hcode[j] < my) { rank++; before += hcnt[j] & RUN_CNT; }
-            roff[rank] = hoff[h]; rcnt[rank] = hcnt[h]; rpos[rank] = pos + before;
+        // each lane ranks its hits (HC / W of them) in registers, then writes
+        // them back in rank order: run in hoff / hcnt, first position in hcode
+        constexpr uint32_t HPL = HC / W;
+        uint32_t rk[HPL], ro[HPL], rc[HPL];
+        uint64_t rp[HPL];
+#pragma unroll
+        for (uint32_t q = 0; q < HPL; q++) {
+            const uint32_t h = gl + q * W;
+            rk[q] = NONE; ro[q] = rc[q] = 0; rp[q] = 0;
+            if (h < nh) {
+                const uint64_t my = hcode[h];
+                uint32_t rank = 0;
+                uint64_t before = 0;   // values of the hits ranked before this one
+                for (uint32_t j = 0; j < nh; j++)
+                    if (hcode[j] < my) { rank++; before += hcnt[j] & RUN_CNT; }
+                rk[q] = rank; ro[q] = hoff[h]; rc[q] = hcnt[h]; rp[q] = pos + before;
+            }
         }
+        wave_sync();   // every hit read before the slots take them by rank
+#pragma unroll
+        for (uint32_t q = 0; q < HPL; q++)
+            if (rk[q] != NONE) { hoff[rk[q]] = ro[q]; hcnt[rk[q]] = rc[q]; hcode[rk[q]] = rp[q]; }
+        const uint32_t *roff = hoff, *rcnt = hcnt;
+        const uint64_t *rpos = hcode;
         wave_sync();
         // single-value runs (C3: almost every hit): lane r writes the one ranked r
         for (uint32_t r = gl; r < nh; r += W)
@@ -2334,12 +2353,20 @@ hipError_t launch_match_phase2(const DevIndex &ix, const Workspace &ws, uint64_t
 // The one-launch kernel of a small batch (small_kind): k_walk_small with 16
 // or 8 lanes per topic, or k_walk_lane (one lane per topic) where the index
 // allows it (lane_path_ok; else k_walk_small's 16 lanes).
+// The default (SMALL_AUTO): 8 lanes per topic for a launch of >= SMALL_W8_MIN
+// topics or of several host batches (the combiner's) -- throughput, twice the
+// topics per wave slot -- and 16 for a lone smaller batch (latency: a topic's
+// levels tokenised in half the ballot rounds).  8 lanes per topic run only on
+// a lane_path_ok index (the LITE fallback store); elsewhere 16.
+constexpr uint64_t SMALL_W8_MIN = 8192;
 struct SmallPick { bool lane; int w; };
-static SmallPick small_pick(const DevIndex &ix, int kind) {
-    if (kind == SMALL_LANE && lane_path_ok(ix)) return {true, 0};
-    return {false, kind == SMALL_WAVE8 ? 8 : 16};
+static SmallPick small_pick(const DevIndex &ix, int kind, uint64_t n, uint32_t segs) {
+    const bool lite = lane_path_ok(ix);
+    if (kind == SMALL_LANE && lite) return {true, 0};
+    const bool w8 = kind == SMALL_WAVE8 || (kind == SMALL_AUTO && (n >= SMALL_W8_MIN || segs > 1));
+    return {false, w8 && lite ? 8 : 16};
 }
-bool small_lane(const DevIndex &ix, int kind) { return small_pick(ix, kind).lane; }
+bool small_lane(const DevIndex &ix, int kind) { return small_pick(ix, kind, 0, 1).lane; }
 static uint32_t small_topics_per_block(const SmallPick &k) {
     return k.lane ? LANE_BLOCK : k.w == 8 ? SmallShape<8>::ST : SmallShape<16>::ST;
 }
@@ -2354,11 +2381,11 @@ static void launch_small_kernel(const SmallPick &k, uint32_t blocks, const DevIn
         hipLaunchKernelGGL((k_walk_lane<OT>), dim3(blocks), dim3(LANE_BLOCK), 0, s, ix, ws, n, bytes, offs, err,
                            hit_offs, out, cap, tag, lb, sg);
     else if (k.w == 8)
-        hipLaunchKernelGGL((k_walk_small<MODE_COUNT, OT, 8>), dim3(blocks), dim3(WV_BLOCK), 0, s, ix, ws, n, bytes,
-                           offs, o, hit_offs, out, cap, tag, lb, sg);
+        hipLaunchKernelGGL((k_walk_small<MODE_COUNT, OT, 8, true>), dim3(blocks), dim3(WV_BLOCK), 0, s, ix, ws, n,
+                           bytes, offs, o, hit_offs, out, cap, tag, lb, sg);
     else
-        hipLaunchKernelGGL((k_walk_small<MODE_COUNT, OT, 16>), dim3(blocks), dim3(WV_BLOCK), 0, s, ix, ws, n, bytes,
-                           offs, o, hit_offs, out, cap, tag, lb, sg);
+        hipLaunchKernelGGL((k_walk_small<MODE_COUNT, OT, 16, false>), dim3(blocks), dim3(WV_BLOCK), 0, s, ix, ws, n,
+                           bytes, offs, o, hit_offs, out, cap, tag, lb, sg);
 }
 
 hipError_t launch_match(const DevIndex &ix, const Workspace &ws, uint64_t n, const uint8_t *bytes,
@@ -2366,7 +2393,7 @@ hipError_t launch_match(const DevIndex &ix, const Workspace &ws, uint64_t n, con
                         uint32_t tag, LbCtl lb, bool phases, int small_kind, hipStream_t s, hipEvent_t ev_walk0,
                         hipEvent_t ev_walk1, int *path) {
     if (n && !phases && small_path_ok(ix, n)) {
-        const SmallPick k = small_pick(ix, small_kind);
+        const SmallPick k = small_pick(ix, small_kind, n, 1);
         if (path) *path = k.lane ? PATH_LANE : PATH_SMALL;
         hipError_t e;
         if (ev_walk0 && (e = hipEventRecord(ev_walk0, s)) != hipSuccess) return e;
@@ -2385,7 +2412,7 @@ hipError_t launch_match32(const DevIndex &ix, const Workspace &ws, uint64_t n, c
                           const uint32_t *offs, uint32_t *hit_offs, uint8_t *err, uint32_t *out, uint64_t cap,
                           uint32_t tag, LbCtl lb, int small_kind, hipStream_t s, int *path) {
     if (!small_path_ok(ix, n)) return hipErrorInvalidValue;   // (the caller converts instead)
-    const SmallPick k = small_pick(ix, small_kind);
+    const SmallPick k = small_pick(ix, small_kind, n, 1);
     if (path) *path = k.lane ? PATH_LANE : PATH_SMALL;
     launch_small_kernel<uint32_t>(k, blocks_for(n, small_topics_per_block(k)), ix, ws, n, bytes, offs, err, hit_offs,
                                   out, cap, tag & LB_TAG_MASK, lb, SmallSegs{}, s);
@@ -2396,7 +2423,9 @@ hipError_t launch_match32(const DevIndex &ix, const Workspace &ws, uint64_t n, c
 hipError_t launch_small_segs(const DevIndex &ix, const Workspace &ws, const SmallSegs &sg0, bool u32, uint32_t tag,
                              LbCtl lb, int small_kind, hipStream_t s, int *path) {
     SmallSegs sg = sg0;
-    const SmallPick k = small_pick(ix, small_kind);
+    uint64_t total = 0;
+    for (uint32_t q = 0; q < sg.count; q++) total += sg.s[q].n;
+    const SmallPick k = small_pick(ix, small_kind, total, sg.count);
     const uint32_t per = small_topics_per_block(k);
     uint32_t blocks = 0;
     for (uint32_t q = 0; q < sg.count; q++) {
@@ -2443,7 +2472,7 @@ hipError_t launch_first(const DevIndex &ix, const Workspace &ws, uint64_t n, con
     if (!n) return hipSuccess;
     Outs o{nullptr, out_value, out_found};
     if (small_path_ok(ix, n)) {
-        hipLaunchKernelGGL((k_walk_small<MODE_FIRST, uint64_t, 16>), dim3(blocks_for(n, SM_TOPICS)), dim3(WV_BLOCK), 0, s,
+        hipLaunchKernelGGL((k_walk_small<MODE_FIRST, uint64_t, 16, false>), dim3(blocks_for(n, SM_TOPICS)), dim3(WV_BLOCK), 0, s,
                            ix, ws, n, bytes, offs, o, nullptr, nullptr, (uint64_t)0, 0u, LbCtl{LB_SPINS, NONE},
                            SmallSegs{});
         return hipGetLastError();

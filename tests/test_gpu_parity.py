@@ -2553,11 +2553,14 @@ def test_combined_small_batches_equal_single_launches(torch_dev, kind):
         for t in th:
             t.join()
 
-    run(40)
+    run(40)   # up to 3 leaders: whether callers queue depends on kernel speed
+    ix.debug_set(_native.TM_DEBUG_COMBINE, 1)
+    run(20)   # one leader: 7 callers queue behind every launch
+    ix.debug_set(_native.TM_DEBUG_COMBINE, 3)
     assert not errors, errors
     launches = ix.debug_get(_native.TM_DEBUG_COMBINED_LAUNCHES) - l0
     batches = ix.debug_get(_native.TM_DEBUG_COMBINED_BATCHES) - b0
-    assert batches == 40 * len(sets) and launches < batches, (launches, batches)   # some launches carried several
+    assert batches == 60 * len(sets) and launches < batches, (launches, batches)   # some launches carried several
     # a forced look-back failure in the next combined launch: rerun, exact
     f0 = ix.debug_get(_native.TM_DEBUG_FAILED_BATCHES)
     ix.debug_set(_native.TM_DEBUG_LB_FAIL_BLOCK, 0)   # (block 0 of every segment)
