@@ -81,7 +81,8 @@ struct Workspace {
     uint32_t *list_n;     // [L_COUNT] list lengths, [L_COUNT] reset ticket, [L_COUNT + 1] scan ticket,
                           // [L_COUNT + 2] long-segment count, [L_COUNT + 3] its reset ticket,
                           // [LS_TICK + k] k_walk_lane's start-order ticket of segment k (zero between launches)
-    uint64_t *blk;        // [n / TILE + 2] tile hit totals -> exclusive tile prefixes (zero between batches)
+    uint64_t *blk;        // [n / TILE + 4] tile hit totals (zero between batches)
+    uint64_t *sup;        // [n / (TILE * SUP) + 4] superblock hit totals (zero between batches; in blk's allocation)
     uint32_t *deep_wid;   // [DEEP_LANES * MAX_LEVELS]
     uint2 *deep_stk;      // [DEEP_LANES * (MAX_LEVELS + 1)]
     uint8_t *deep_plus;   // [DEEP_LANES * MAX_LEVELS] '+' levels of each deep lane's path
@@ -96,6 +97,7 @@ struct Workspace {
 };
 
 constexpr int TILE = 256;    // topics per walk block = per scan tile = per emit block
+constexpr int SUP = 64;      // tiles per superblock (Workspace::sup)
 constexpr int LS_TICK = L_COUNT + 4;      // Workspace::list_n words: k_walk_lane's tickets, one per segment
 constexpr int LIST_SLOTS = LS_TICK + SMALL_SEGS;   // Workspace::list_n entries
 constexpr int HINT_FAIL = L_COUNT + 1;    // Workspace::hint_* word of the fail flag

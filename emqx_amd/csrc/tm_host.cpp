@@ -1690,8 +1690,10 @@ int ensure_ws(tm_index *ix, uint64_t n, Lane &ln) {
     HIPCHK(ix, hipMalloc(&w.nr, c * 4));
     HIPCHK(ix, hipMalloc(&w.rng, c * RCAP * 8));
     HIPCHK(ix, hipMalloc(&w.lists, c * (L_COUNT + 1) * 4));
-    HIPCHK(ix, hipMalloc(&w.blk, (c / TILE + 4) * 8));
-    HIPCHK(ix, hipMemsetAsync(w.blk, 0, (c / TILE + 4) * 8, ln.s));   // zero between batches (k_emit)
+    const uint64_t nblk = c / TILE + 4, nsup = c / ((uint64_t)TILE * SUP) + 4;
+    HIPCHK(ix, hipMalloc(&w.blk, (nblk + nsup) * 8));
+    HIPCHK(ix, hipMemsetAsync(w.blk, 0, (nblk + nsup) * 8, ln.s));   // zero between batches (k_rewalk_tail)
+    w.sup = w.blk + nblk;
     HIPCHK(ix, hipMalloc(&w.look, (c / SM_TOPICS + 4) * 8 * LB_STRIDE));
     HIPCHK(ix, hipMemsetAsync(w.look, 0, (c / SM_TOPICS + 4) * 8 * LB_STRIDE, ln.s));   // no launch tag is 0
     w.cap_n = c;

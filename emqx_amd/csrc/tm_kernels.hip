@@ -867,12 +867,23 @@ __device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t &total,
     return pre + inc - v;
 }
 
+// a walk's hits into its topic's tile total (phase 1).  (Adding them into
+// the superblock total here as well cost the walk 19 us per 1M C3 topics:
+// 256 walk blocks' atomics on each superblock word.)
+__device__ __forceinline__ void add_tile_total(const Workspace &ws, uint64_t t, uint64_t v) {
+    atomicAdd((unsigned long long *)&ws.blk[t / TILE], (unsigned long long)v);
+}
+
 // ----------------------------------------------------------------- kernels
 //
-// Per batch: phase 1 = k_walk_fast, k_walk_tail, k_scan_top; phase 2 =
-// k_emit, k_rewalk_tail.  Tiles of TILE = 256 topics line up across kernels:
-// the walk writes each tile's hit total into ws.blk, k_scan_top turns those
-// into tile prefixes, k_emit finishes the scan inside its tile.
+// Per batch: phase 1 = k_walk_fast, k_walk_tail; phase 2 = k_emit,
+// k_rewalk_tail.  Tiles of TILE = 256 topics line up across kernels: the walks
+// add each tile's hit total into ws.blk, the last k_walk_tail block sums each
+// superblock's (SUP tiles) into ws.sup; a k_emit block sums the superblock
+// totals before its own and the tile totals before it inside its superblock
+// (one load per lane, no scan kernel and no waiting: every total is final
+// when k_emit starts), then scans inside its tile; k_rewalk_tail, the batch's
+// last kernel, zeroes both.
 
 // a walk block is a scan tile, or a part of one (tile totals added
 // atomically); 64 vs 256 threads: walk 0.2553 vs 0.2631 ms per 1M C3 topics
@@ -904,11 +915,7 @@ __global__ __launch_bounds__(WALK_BLOCK, 8) void k_walk_fast(DevIndex ix, Worksp
     if (MODE == MODE_COUNT) {
         uint64_t total;
         block_excl_scan(hits, total, s_w);
-        if (WALK_BLOCK == TILE) {
-            if (threadIdx.x == 0) ws.blk[blockIdx.x] = total;
-        } else if (threadIdx.x == 0 && total) {
-            atomicAdd((unsigned long long *)&ws.blk[((uint64_t)blockIdx.x * WALK_BLOCK) / TILE], (unsigned long long)total);
-        }
+        if (threadIdx.x == 0 && total) add_tile_total(ws, (uint64_t)blockIdx.x * WALK_BLOCK, total);
     }
 }
 
@@ -1113,7 +1120,7 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_wave(DevIndex ix, Workspace w
             ws.cnt[t] = total;
             ws.nr[t] = nh;
             o.err[t] = badarg;
-            if (total) atomicAdd((unsigned long long *)&ws.blk[t / TILE], (unsigned long long)total);
+            if (total) add_tile_total(ws, t, total);
             if (nh > RCAP) list_push(ws, n, L_OVF_MID, (uint32_t)t);
         }
     } else {
@@ -1401,16 +1408,21 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_small(DevIndex ix, Workspace 
 
     // ---- topics the group could not take: its first lane walks them (LDS store of FBL levels)
     FbStore st{s_mwid[gi], s_mpend[gi], s_mlen[gi], 1, 0};
+    // its bytes from the LDS copy above (the block's span, or the topic's row),
+    // not from the caller's buffer: for an in-place batch every byte the walk
+    // read from there was a PCIe round trip on the launch's critical path (the
+    // block's count waits for it, and every later block for the block's count)
+    const StagedSrc fsrc{blob, span ? s_tb : s_tb + gi * TBQ, span ? B0 : a0, span || nq <= TBQ};
     int frc = RC_OK;
     const bool walker = fb && gl == 0;
     if (walker) {
         if (MODE == MODE_COUNT) {
             CountEmit em{0};
-            frc = match_topic(ix, GlobalSrc{blob}, beg, end, st, em);
+            frc = match_topic(ix, fsrc, beg, end, st, em);
             total = frc == RC_OK ? em.cnt : 0;
         } else {
             FirstEmit em{ix.vals, 0, false};
-            frc = match_topic(ix, GlobalSrc{blob}, beg, end, st, em);
+            frc = match_topic(ix, fsrc, beg, end, st, em);
             o.first_val[t] = frc == RC_OK ? em.v : 0;
             o.first_found[t] = frc == RC_BADARG ? 2 : frc == RC_DEEP ? 3 : (em.found ? 1 : 0);
         }
@@ -1477,7 +1489,7 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_small(DevIndex ix, Workspace 
     // ---- the values
     if (walker && frc == RC_OK) {   // (never with stage)
         DirectEmit em{ix.vals, out, pos, cap};
-        match_topic(ix, GlobalSrc{blob}, beg, end, st, em);
+        match_topic(ix, fsrc, beg, end, st, em);
     }
     if (live && !fb) {
         // each lane ranks its hits (HC / W of them) in registers, then writes
@@ -1570,14 +1582,10 @@ __device__ __forceinline__ void reset_lists_if_last(const Workspace &ws, uint32_
 
 // topics deeper than FAST_L: blocks < MID_GRID take the MID list (LDS frontier,
 // <= MID_L levels), the rest take the DEEP list (global scratch, any depth)
-//
-// scan_hit != null (count mode, small batches): the grid's last block also
-// turns the nb tile totals into exclusive tile prefixes and writes the grand
-// total to scan_hit[n] -- k_scan_top's job, without its own launch.
 template <int MODE>
 __global__ __launch_bounds__(MID_BLOCK) void k_walk_tail(DevIndex ix, Workspace ws, uint64_t n,
                                                          const uint8_t *blob, const uint64_t *offs, Outs o,
-                                                         uint64_t nb, uint64_t *scan_hit, uint32_t mid_grid) {
+                                                         uint32_t mid_grid) {
     __shared__ uint32_t s_wid[MID_L * MID_BLOCK];
     __shared__ uint32_t s_pend[(MID_L + 1) * MID_BLOCK];
     __shared__ uint8_t s_len[MID_L * MID_BLOCK];
@@ -1588,7 +1596,7 @@ __global__ __launch_bounds__(MID_BLOCK) void k_walk_tail(DevIndex ix, Workspace 
         LdsStore<MID_L> st{s_wid + threadIdx.x, s_pend + threadIdx.x, s_len + threadIdx.x, MID_BLOCK, 0};
         for (uint32_t i = blockIdx.x * MID_BLOCK + threadIdx.x; i < cnt; i += mid_grid * MID_BLOCK) {
             run_topic<MODE>(ix, ws, n, blob, offs, lst[i], st, o, &hits);
-            if (MODE == MODE_COUNT && hits) atomicAdd((unsigned long long *)&ws.blk[lst[i] / TILE], hits);
+            if (MODE == MODE_COUNT && hits) add_tile_total(ws, lst[i], hits);
         }
     } else {
         const uint32_t lane = (blockIdx.x - mid_grid) * 64 + threadIdx.x;   // < DEEP_LANES
@@ -1598,11 +1606,14 @@ __global__ __launch_bounds__(MID_BLOCK) void k_walk_tail(DevIndex ix, Workspace 
                        ws.deep_plus + (uint64_t)lane * MAX_LEVELS, 0};
         for (uint32_t i = lane; i < cnt; i += DEEP_LANES) {
             run_topic<MODE>(ix, ws, n, blob, offs, lst[i], st, o, &hits);
-            if (MODE == MODE_COUNT && hits) atomicAdd((unsigned long long *)&ws.blk[lst[i] / TILE], hits);
+            if (MODE == MODE_COUNT && hits) add_tile_total(ws, lst[i], hits);
         }
     }
     if (MODE == MODE_FIRST) reset_lists_if_last(ws);   // count mode: k_rewalk_tail resets
-    if (MODE == MODE_COUNT && scan_hit) {
+    if (MODE == MODE_COUNT) {
+        // the grid's last block: the superblock totals from the (now final)
+        // tile totals -- a lane per superblock, its SUP totals in SUP / 2
+        // independent 16-B loads (the tail of blk past nb is zero)
         __shared__ uint32_t s_last;
         __syncthreads();
         if (threadIdx.x == 0) {
@@ -1612,18 +1623,23 @@ __global__ __launch_bounds__(MID_BLOCK) void k_walk_tail(DevIndex ix, Workspace 
         __syncthreads();
         if (!s_last) return;
         __threadfence();
-        uint64_t carry = 0;
-        for (uint64_t b0 = 0; b0 < nb; b0 += MID_BLOCK) {
-            const uint64_t i = b0 + threadIdx.x;
-            const uint64_t v = i < nb ? __hip_atomic_load(&ws.blk[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
-            const uint64_t inc = wave_incl_scan(v);
-            if (i < nb) ws.blk[i] = carry + inc - v;
-            carry += __shfl(inc, 63, 64);
+        const uint64_t nb = (n + TILE - 1) / TILE, ns = (nb + SUP - 1) / SUP;
+        for (uint64_t sb = threadIdx.x; sb < ns; sb += MID_BLOCK) {
+            typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+            const u64x2 *q = reinterpret_cast<const u64x2 *>(ws.blk + sb * SUP);
+            u64x2 x[SUP / 2];
+#pragma unroll
+            for (int i = 0; i < SUP / 2; i++) x[i] = __builtin_nontemporal_load(q + i);
+            uint64_t v = 0;
+#pragma unroll
+            for (int i = 0; i < SUP / 2; i++) {
+                const uint64_t i0 = sb * SUP + 2 * i;
+                if (i0 < nb) v += x[i].x;
+                if (i0 + 1 < nb) v += x[i].y;
+            }
+            ws.sup[sb] = v;
         }
-        if (threadIdx.x == 0) {
-            scan_hit[n] = carry;
-            atomicExch(&ws.list_n[L_COUNT + 1], 0u);
-        }
+        if (threadIdx.x == 0) atomicExch(&ws.list_n[L_COUNT + 1], 0u);
     }
 }
 
@@ -1641,6 +1657,11 @@ __global__ __launch_bounds__(MID_BLOCK) void k_rewalk_tail(DevIndex ix, Workspac
     __shared__ uint32_t s_wid[MID_L * MID_BLOCK];
     __shared__ uint32_t s_pend[(MID_L + 1) * MID_BLOCK];
     __shared__ uint8_t s_len[MID_L * MID_BLOCK];
+    {   // every k_emit block has read the totals: zero them for the next batch
+        const uint64_t nb = (n + TILE - 1) / TILE, ns = (nb + SUP - 1) / SUP;
+        for (uint64_t i = (uint64_t)blockIdx.x * MID_BLOCK + threadIdx.x; i < nb + ns; i += (uint64_t)gridDim.x * MID_BLOCK)
+            if (i < nb) ws.blk[i] = 0; else ws.sup[i - nb] = 0;
+    }
     if (blockIdx.x < mid_grid) {
         const uint32_t cnt = ws.list_n[L_OVF_MID];
         const uint32_t *lst = ws.lists + (uint64_t)L_OVF_MID * n;
@@ -1657,30 +1678,6 @@ __global__ __launch_bounds__(MID_BLOCK) void k_rewalk_tail(DevIndex ix, Workspac
             rewalk(ix, blob, offs, lst[i], hit_offs, out, cap, st);
     }
     reset_lists_if_last(ws, n < 0xFFFFFFFFull ? (uint32_t)n : 0xFFFFFFFFu);
-}
-
-// tile totals -> exclusive tile prefixes; hit_offs[n] = grand total
-__global__ __launch_bounds__(1024) void k_scan_top(uint64_t *blk, uint64_t nb, uint64_t *hit_offs, uint64_t n) {
-    // one block: thread j owns a contiguous run of ceil(nb / 1024) tiles (one
-    // pass over the totals instead of nb / 256 dependent block scans)
-    __shared__ uint64_t s_w[16];
-    const uint64_t per = (nb + 1023) / 1024;
-    const uint64_t b0 = threadIdx.x * per, b1 = b0 + per < nb ? b0 + per : nb;
-    uint64_t sum = 0;
-    for (uint64_t i = b0; i < b1; i++) sum += blk[i];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const uint64_t inc = wave_incl_scan(sum);
-    if (lane == 63) s_w[wv] = inc;
-    __syncthreads();
-    uint64_t pre = 0, total = 0;
-    for (int k = 0; k < 16; k++) { if (k < wv) pre += s_w[k]; total += s_w[k]; }
-    uint64_t run = pre + inc - sum;
-    for (uint64_t i = b0; i < b1; i++) {
-        const uint64_t v = blk[i];
-        blk[i] = run;
-        run += v;
-    }
-    if (threadIdx.x == 0) hit_offs[n] = total;
 }
 
 // ------------------------------------------------------------------- emit
@@ -1838,6 +1835,7 @@ __global__ __launch_bounds__(EMIT_BLOCK) void k_emit(DevIndex ix, Workspace ws, 
     __shared__ uint8_t s_flg[EMIT_WAVES][WR];
     __shared__ uint64_t s_w[4];
     __shared__ uint64_t s_end[EMIT_WAVES];
+    __shared__ uint64_t s_pre;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint64_t t = (uint64_t)blockIdx.x * EMIT_BLOCK + threadIdx.x;
     const bool valid = t < n;
@@ -1854,15 +1852,24 @@ __global__ __launch_bounds__(EMIT_BLOCK) void k_emit(DevIndex ix, Workspace ws, 
 #pragma unroll
     for (int i = 0; i < RCAP; i++)
         gr[i] = (uint32_t)i < nr ? __builtin_nontemporal_load(reinterpret_cast<const uint64_t *>(ws.rng) + (uint64_t)i * n + t) : 0;
+    // the tile's prefix: the superblocks before this one, then the tiles
+    // before this one in its superblock (wave 0; <= 64 of each per lane round)
+    if (wv == 0) {
+        const uint64_t b = blockIdx.x, sb = b / SUP;
+        uint64_t v = 0;
+        for (uint64_t i = lane; i < sb; i += 64) v += ws.sup[i];
+        if (sb * SUP + lane < b) v += ws.blk[sb * SUP + lane];
+        v = wave_incl_scan(v);
+        if (lane == 63) s_pre = v;
+    }
     uint64_t total;
-    const uint64_t my = ws.blk[blockIdx.x] + block_excl_scan(c, total, s_w);
+    const uint64_t ex = block_excl_scan(c, total, s_w);   // (its barrier publishes s_pre)
+    const uint64_t my = s_pre + ex;
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) hit_offs[n] = s_pre + total;   // the grand total
     // the GPU never reads the offsets (or the err flags) back: non-temporal
     if (valid) __builtin_nontemporal_store(my, hit_offs + t);
     if (lane == 63) s_end[wv] = my + c;
     __syncthreads();
-    // every thread has read its tile prefix: leave the tile total zero for the
-    // next batch (the wave walk adds into it)
-    if (threadIdx.x == 0) ws.blk[blockIdx.x] = 0;
     const uint64_t t0 = t - lane;
     if (t0 >= n) return;   // whole wave leaves; only wave-level sync below
     const uint64_t base = __shfl(my, 0, 64);
@@ -2317,9 +2324,8 @@ hipError_t launch_match_phase1(const DevIndex &ix, const Workspace &ws, uint64_t
                                hipEvent_t ev_walk0, hipEvent_t ev_walk1) {
     hipError_t e;
     Outs o{err, nullptr, nullptr};
-    const uint32_t nb = blocks_for(n, TILE);
-    // tile totals are zero between batches (k_emit leaves them so): the wave
-    // walk adds its topics' hits into them, the lane walk overwrites them
+    // tile and superblock totals are zero between batches (k_rewalk_tail
+    // leaves them so): the walks add their topics' hits into them
     const bool wave = n && n <= WAVE_TOPICS;
     if (n) {
         if (ev_walk0 && (e = hipEventRecord(ev_walk0, s)) != hipSuccess) return e;
@@ -2330,20 +2336,19 @@ hipError_t launch_match_phase1(const DevIndex &ix, const Workspace &ws, uint64_t
             hipLaunchKernelGGL(k_walk_fast<MODE_COUNT>, dim3(blocks_for(n, WALK_BLOCK)), dim3(WALK_BLOCK), 0, s, ix, ws,
                                n, bytes, offs, o);
         if (ev_walk1 && (e = hipEventRecord(ev_walk1, s)) != hipSuccess) return e;
-        // small batches: the tail kernel's last block also scans the (few) tile totals
         const uint32_t mg = tail_blocks(ws, n, L_MID, wave ? MID_GRID : MID_GRID_BIG);
         hipLaunchKernelGGL(k_walk_tail<MODE_COUNT>, dim3(mg + DEEP_LANES / 64), dim3(MID_BLOCK), 0, s, ix, ws, n,
-                           bytes, offs, o, (uint64_t)nb, wave ? hit_offs : nullptr, mg);
+                           bytes, offs, o, mg);
     }
-    if (!wave) hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(1024), 0, s, ws.blk, (uint64_t)nb, hit_offs, n);
     return hipGetLastError();
 }
 
 hipError_t launch_match_phase2(const DevIndex &ix, const Workspace &ws, uint64_t n, const uint8_t *bytes,
                                const uint64_t *offs, uint64_t *hit_offs, uint32_t *out, uint64_t cap,
                                hipStream_t s) {
-    if (!n) return hipSuccess;
-    hipLaunchKernelGGL(k_emit, dim3(blocks_for(n, TILE)), dim3(EMIT_BLOCK), 0, s, ix, ws, n, hit_offs, out, cap);
+    // (an empty batch: one k_emit block writes hit_offs[0] = 0)
+    hipLaunchKernelGGL(k_emit, dim3(n ? blocks_for(n, TILE) : 1), dim3(EMIT_BLOCK), 0, s, ix, ws, n, hit_offs, out, cap);
+    if (!n) return hipGetLastError();
     const uint32_t mg = tail_blocks(ws, n, L_OVF_MID, MID_GRID);
     hipLaunchKernelGGL(k_rewalk_tail, dim3(mg + DEEP_LANES / 64), dim3(MID_BLOCK), 0, s, ix, ws, n, bytes, offs,
                        hit_offs, out, cap, mg);
@@ -2484,7 +2489,7 @@ hipError_t launch_first(const DevIndex &ix, const Workspace &ws, uint64_t n, con
         hipLaunchKernelGGL(k_walk_fast<MODE_FIRST>, dim3(blocks_for(n, WALK_BLOCK)), dim3(WALK_BLOCK), 0, s,
                            ix, ws, n, bytes, offs, o);
     hipLaunchKernelGGL(k_walk_tail<MODE_FIRST>, dim3(MID_GRID + DEEP_LANES / 64), dim3(MID_BLOCK), 0, s, ix, ws, n, bytes, offs, o,
-                       (uint64_t)0, nullptr, (uint32_t)MID_GRID);
+                       (uint32_t)MID_GRID);
     return hipGetLastError();
 }
 
