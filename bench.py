@@ -422,13 +422,27 @@ def main():
                                a.latency_batches * 5, out)
             assert rc == 0, rc
             lat_native[str(lb)] = {"p50_ms": round(out[0], 4), "p99_ms": round(out[1], 4), "mean_ms": round(out[2], 4)}
+        # the NIF's entry point (u32 offsets) with the inputs in TM_ALLOC_VRAM
+        # memory the caller writes before every batch (the copy is timed)
+        lb = min(4096, B)
+        sub = ts.slice(0, lb)
+        hh, _, _ = ix.match_batch(sub.blob, sub.offs)
+        out = (ctypes.c_double * 3)()
+        rc = hb.tmb_single_ex(ix._h, lb, _native._ptr(sub.blob), _native._ptr(sub.offs), int(hh[-1]) + 4096,
+                              a.latency_batches * 5, 5, out)
+        assert rc == 0, rc
+        lat_native[f"{lb}_u32_vram_inputs"] = {"p50_ms": round(out[0], 4), "p99_ms": round(out[1], 4),
+                                               "mean_ms": round(out[2], 4)}
         if a.concurrency > 0:
             conc = []
             # (threads, deltas per ms from one more thread): without churn, then with
             # (threads, deltas per ms from one more thread, mode): without churn, then with; mode 4: the
             # u32-offset API the NIF calls (tm_match_batch32_ex), 0: the u64 one
+            # mode 5: mode 4 with the inputs in TM_ALLOC_VRAM memory, written by each caller before
+            # every batch (as a NIF packs its micro-batch): no PCIe read on the kernel's path
             for nth, churn, mode in ((a.concurrency, 0, 0), (a.concurrency, 0, 4), (a.concurrency, 256, 4),
-                                     (2 * a.concurrency, 256, 4)):
+                                     (2 * a.concurrency, 256, 4), (a.concurrency, 0, 5), (a.concurrency, 256, 5),
+                                     (2 * a.concurrency, 256, 5)):
                 lb = min(4096, B)
                 sub = ts.slice(0, nth * lb)
                 hh, _, _ = ix.match_batch(sub.blob, sub.offs)
@@ -441,11 +455,12 @@ def main():
                 fr1 = [ix.debug_get(k) for k in (_native.TM_DEBUG_FAILED_BATCHES, _native.TM_DEBUG_RETRIED_BATCHES)]
                 conc.append({"threads": nth, "topics_per_batch": lb, "batches": int(out[0]),
                              "topics_per_s": round(out[1], 1), "p50_ms": round(out[2], 4), "p99_ms": round(out[3], 4),
-                             "deltas_per_s": round(out[4], 1), "offsets": "u32" if mode == 4 else "u64",
+                             "deltas_per_s": round(out[4], 1), "offsets": "u32" if mode >= 4 else "u64",
                              # one-launch batches whose look-back wait expired (err 4; each is run
                              # again once, a second failure is TM_EDEVICE): forward progress under
                              # concurrent launches, measured
                              "failed_batches": fr1[0] - fr0[0], "retried_batches": fr1[1] - fr0[1],
+                             "inputs": "vram (written per batch)" if mode == 5 else "host",
                              "callers": "native threads, tm_host_alloc buffers each (in place)"})
         if B >= 65536:
             allt = wl.concat(tsets)
@@ -759,6 +774,7 @@ def host_bench_lib():
     lib = ctypes.CDLL(str(LIB_BENCH))
     vp, u64, dp = ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_double)
     lib.tmb_single.argtypes = [vp, u64, vp, vp, u64, ctypes.c_int, dp]
+    lib.tmb_single_ex.argtypes = [vp, u64, vp, vp, u64, ctypes.c_int, ctypes.c_int, dp]
     lib.tmb_callers.argtypes = [vp, ctypes.c_int, u64, vp, vp, u64, ctypes.c_double, ctypes.c_int, dp]
     lib.tmb_callers_ex.argtypes = [vp, ctypes.c_int, u64, vp, vp, u64, ctypes.c_double, ctypes.c_int, ctypes.c_int, dp]
     lib.tmb_pipeline.argtypes = [vp, ctypes.c_int, vp, vp, u64, ctypes.c_int, ctypes.c_int, ctypes.c_int, dp]

@@ -26,7 +26,8 @@ EXPORTS = ("tm_create", "tm_destroy", "tm_apply_deltas", "tm_sync", "tm_match_ba
            "tm_stream_release", "tm_match_batch_ex", "tm_match_batch_dev_ex", "tm_sort_segments",
            "tm_matches_filter", "tm_apply_deltas_ex", "tm_read_begin", "tm_read_end", "tm_epoch",
            "tm_create_replicas", "tm_replica_stats", "tm_debug_set", "tm_debug_get", "tm_match_batch32_ex",
-           "tm_match_batch32_dev", "tm_matches_filter_ex")
+           "tm_match_batch32_dev", "tm_matches_filter_ex", "tm_host_alloc_ex")
+TM_ALLOC_VRAM = 1
 TM_DEBUG_LB_SPINS, TM_DEBUG_LB_FAIL_BLOCK, TM_DEBUG_LB_LAUNCHES, TM_DEBUG_PHASES = 1, 2, 3, 4
 TM_DEBUG_FAILED_BATCHES, TM_DEBUG_RETRIED_BATCHES = 5, 6
 TM_DEBUG_PATH_PHASES, TM_DEBUG_PATH_SMALL, TM_DEBUG_PATH_LANE = 7, 8, 9
@@ -96,6 +97,7 @@ def load_library(path: Path | None = None):
         "tm_merge_shards": (i32, [u32, u64, vp, vp, u64, vp, vp, u64, vp]),
         "tm_host_alloc": (i32, [vp, u64, C.POINTER(vp)]),
         "tm_host_free": (i32, [vp, vp]),
+        "tm_host_alloc_ex": (i32, [vp, u64, u32, C.POINTER(vp)]),
         "tm_stream_release": (i32, [vp, vp]),
         "tm_match_batch_ex": (i32, [vp, u64, vp, vp, vp, vp, u64, vp, u32, vp]),
         "tm_match_batch_dev_ex": (i32, [vp, u64, vp, vp, vp, vp, u64, vp, u32, vp, vp]),
@@ -224,15 +226,17 @@ class Index:
         self._check(self._lib.tm_sync(self._h, stream))
 
     # ---- pinned host buffers (tm_host_alloc)
-    def host_array(self, n: int, dtype) -> np.ndarray:
+    def host_array(self, n: int, dtype, vram: bool = False) -> np.ndarray:
         """A numpy array in pinned host memory mapped into the device.  Batches
         whose buffers (topics 16-byte aligned, offsets, outputs) all come from
         here run in place, without staging copies (include/tmatch.h).  Valid
-        until host_free() or close()."""
+        until host_free() or close().  vram: device memory mapped into the host
+        (TM_ALLOC_VRAM) for a batch's inputs -- write it, never read it back
+        (each host read is an uncached PCIe round trip)."""
         dtype = np.dtype(dtype)
         nbytes = max(int(n), 1) * dtype.itemsize
         p = C.c_void_p()
-        self._check(self._lib.tm_host_alloc(self._h, nbytes, C.byref(p)))
+        self._check(self._lib.tm_host_alloc_ex(self._h, nbytes, TM_ALLOC_VRAM if vram else 0, C.byref(p)))
         buf = (C.c_uint8 * nbytes).from_address(p.value)
         a = np.frombuffer(buf, dtype=dtype, count=max(int(n), 1))
         if not hasattr(self, "_pinned"):

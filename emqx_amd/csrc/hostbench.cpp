@@ -31,6 +31,7 @@
 namespace api {
 int (*host_alloc)(tm_index *, uint64_t, void **);
 int (*host_free)(tm_index *, void *);
+int (*host_alloc_ex)(tm_index *, uint64_t, uint32_t, void **);   // optional (ABI 1.9)
 int (*match_batch)(tm_index *, uint64_t, const uint8_t *, const uint64_t *, uint64_t *, uint32_t *, uint64_t, uint8_t *);
 int (*match_batch_dev)(tm_index *, uint64_t, const uint8_t *, const uint64_t *, uint64_t *, uint32_t *, uint64_t,
                        uint8_t *, void *);
@@ -59,6 +60,18 @@ struct Caller {
     uint64_t n, cap;
     uint8_t *blob = nullptr; uint64_t *offs = nullptr, *hit = nullptr; uint32_t *vals = nullptr; uint8_t *err = nullptr;
     uint32_t *offs32 = nullptr, *hit32 = nullptr;   // mode 4: tm_match_batch32_ex (u32 offsets)
+    // mode 5: mode 4 with the inputs in TM_ALLOC_VRAM memory, written by the
+    // caller before every batch (as a NIF packs each micro-batch)
+    uint8_t *vblob = nullptr; uint32_t *voffs32 = nullptr; uint64_t nbytes = 0;
+    int to_vram() {
+        nbytes = offs[n];
+        int rc;
+        if (!api::host_alloc_ex) return TM_EINVAL;
+        if ((rc = api::host_alloc_ex(h, nbytes + 16, TM_ALLOC_VRAM, (void **)&vblob)) ||
+            (rc = api::host_alloc_ex(h, 4 * (n + 1), TM_ALLOC_VRAM, (void **)&voffs32)))
+            return rc;
+        return TM_OK;
+    }
     int init(tm_index *ix, uint64_t nt, const uint8_t *tb, const uint64_t *to, uint64_t first, uint64_t cap_) {
         h = ix; n = nt; cap = cap_;
         const uint64_t b0 = to[first], nb = to[first + nt] - b0;
@@ -96,6 +109,11 @@ struct Caller {
     }
     int run() {
         if (mode == 4) return api::match_batch32(h, n, blob, offs32, hit32, vals, cap, err, TM_ORDER_TRAVERSAL, nullptr);
+        if (mode == 5) {
+            memcpy(vblob, blob, nbytes);
+            memcpy(voffs32, offs32, 4 * (n + 1));
+            return api::match_batch32(h, n, vblob, voffs32, hit32, vals, cap, err, TM_ORDER_TRAVERSAL, nullptr);
+        }
         if (!s) return api::match_batch(h, n, blob, offs, hit, vals, cap, err);
         const bool hin = mode == 3, hout = mode == 2;
         int rc = api::match_batch_dev(h, n, hin ? mapped(blob) : dblob, hin ? mapped(offs) : doffs,
@@ -105,7 +123,8 @@ struct Caller {
         return hipStreamSynchronize(s) == hipSuccess ? TM_OK : TM_EDEVICE;
     }
     void fini() {
-        for (void *p : {(void *)blob, (void *)offs, (void *)hit, (void *)vals, (void *)err, (void *)offs32, (void *)hit32})
+        for (void *p : {(void *)blob, (void *)offs, (void *)hit, (void *)vals, (void *)err, (void *)offs32, (void *)hit32,
+                        (void *)vblob, (void *)voffs32})
             if (p) api::host_free(h, p);
         if (s) {
             for (void *p : {(void *)dblob, (void *)doffs, (void *)dhit, (void *)dvals, (void *)derr}) if (p) (void)hipFree(p);
@@ -123,6 +142,7 @@ extern "C" {
 int tmb_bind(void *lib) {
     api::host_alloc = reinterpret_cast<decltype(api::host_alloc)>(dlsym(lib, "tm_host_alloc"));
     api::host_free = reinterpret_cast<decltype(api::host_free)>(dlsym(lib, "tm_host_free"));
+    api::host_alloc_ex = reinterpret_cast<decltype(api::host_alloc_ex)>(dlsym(lib, "tm_host_alloc_ex"));
     api::match_batch = reinterpret_cast<decltype(api::match_batch)>(dlsym(lib, "tm_match_batch"));
     api::match_batch_dev = reinterpret_cast<decltype(api::match_batch_dev)>(dlsym(lib, "tm_match_batch_dev"));
     api::apply_deltas = reinterpret_cast<decltype(api::apply_deltas)>(dlsym(lib, "tm_apply_deltas"));
@@ -134,10 +154,15 @@ int tmb_bind(void *lib) {
 }
 
 // out: [p50_ms, p99_ms, mean_ms]
-int tmb_single(tm_index *h, uint64_t n, const uint8_t *tb, const uint64_t *to, uint64_t cap, int iters, double *out) {
+// mode: as tmb_callers_ex (0: in place, u64 offsets; 4: u32; 5: u32 with the
+// inputs in TM_ALLOC_VRAM memory written before every batch)
+int tmb_single_ex(tm_index *h, uint64_t n, const uint8_t *tb, const uint64_t *to, uint64_t cap, int iters, int mode,
+                  double *out) {
     Caller c;
     int rc = c.init(h, n, tb, to, 0, cap);
     if (rc) return rc;
+    if (mode == 5 && (rc = c.to_vram())) return rc;
+    c.mode = mode ? mode : 1;
     std::vector<double> lat;
     for (int k = 0; k < iters + 3 && !rc; k++) {
         const double t0 = now_s();
@@ -154,6 +179,10 @@ int tmb_single(tm_index *h, uint64_t n, const uint8_t *tb, const uint64_t *to, u
     return TM_OK;
 }
 
+int tmb_single(tm_index *h, uint64_t n, const uint8_t *tb, const uint64_t *to, uint64_t cap, int iters, double *out) {
+    return tmb_single_ex(h, n, tb, to, cap, iters, 0, out);
+}
+
 // nthreads callers, each with batches of n topics (caller k takes topics
 // [k n, (k + 1) n) of the set, which must hold nthreads * n); one churn thread
 // applies `churn_ops` deltas per millisecond (0: none).  device_buffers: each
@@ -161,7 +190,8 @@ int tmb_single(tm_index *h, uint64_t n, const uint8_t *tb, const uint64_t *to, u
 // stream (what the device can take without the PCIe leg of in-place batches);
 // 2: inputs in HBM, outputs written into the mapped host buffers; 3: inputs
 // read from the mapped host buffers, outputs in HBM; 4: in place with u32
-// offsets (tm_match_batch32_ex, what the NIF calls).
+// offsets (tm_match_batch32_ex, what the NIF calls); 5: mode 4 with the inputs
+// in TM_ALLOC_VRAM memory the caller writes before every batch.
 // out: [batches, topics_per_s, p50_ms, p99_ms, deltas_per_s, seconds]
 int tmb_callers_ex(tm_index *h, int nthreads, uint64_t n, const uint8_t *tb, const uint64_t *to, uint64_t cap,
                    double seconds, int churn_ops, int device_buffers, double *out) {
@@ -169,7 +199,8 @@ int tmb_callers_ex(tm_index *h, int nthreads, uint64_t n, const uint8_t *tb, con
     for (int k = 0; k < nthreads; k++) {
         int rc = cs[k].init(h, n, tb, to, (uint64_t)k * n, cap);
         if (rc) return rc;
-        if (device_buffers && device_buffers != 4 && (rc = cs[k].to_device())) return rc;
+        if (device_buffers == 5 && (rc = cs[k].to_vram())) return rc;
+        if (device_buffers && device_buffers < 4 && (rc = cs[k].to_device())) return rc;
         cs[k].mode = device_buffers;
         if ((rc = cs[k].run())) return rc;   // warm: lane, workspace
     }

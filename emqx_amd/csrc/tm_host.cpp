@@ -229,8 +229,9 @@ struct tm_index {
     std::vector<std::unique_ptr<Lane>> lanes;
     uint64_t tick = 0;
 
-    // caller buffers from tm_host_alloc (host address -> size, device address)
-    struct Pinned { uint8_t *host, *dev; uint64_t size; };
+    // caller buffers from tm_host_alloc (host address -> size, device address;
+    // vram: TM_ALLOC_VRAM device memory, the same address on both sides)
+    struct Pinned { uint8_t *host, *dev; uint64_t size; bool vram; };
     std::vector<Pinned> pinned;
 
     // reader epochs (tm_read_begin / tm_read_end / tm_epoch): the epoch
@@ -1766,7 +1767,7 @@ int drain_lanes(tm_index *ix) {
 
 extern "C" {
 
-uint32_t tm_abi_version(void) { return (1u << 16) | 8u; }
+uint32_t tm_abi_version(void) { return (1u << 16) | 9u; }
 
 const char *tm_last_error(tm_index *) { return g_last_error.c_str(); }
 
@@ -1849,7 +1850,7 @@ int tm_destroy(tm_index *ix) {
     for (void *p : {(void *)ix->mf.q, (void *)ix->mf.err, (void *)ix->mf.hit, (void *)ix->mf.out}) if (p) (void)hipFree(p);
     if (ix->mf.s) (void)hipStreamDestroy(ix->mf.s);
     for (auto &p : ix->patch) if (p.pin) (void)hipHostFree(p.pin);
-    for (auto &b : ix->pinned) (void)hipHostFree(b.host);
+    for (auto &b : ix->pinned) (void)(b.vram ? hipFree(b.host) : hipHostFree(b.host));
     for (auto *v : {&ix->prof_pending, &ix->prof_free})
         for (auto &ev : *v) {
             (void)hipSetDevice(ev.device);
@@ -2078,20 +2079,35 @@ static uint8_t *pinned_dev(tm_index *ix, const void *p, uint64_t bytes) {
     return nullptr;
 }
 
-int tm_host_alloc(tm_index *ix, uint64_t bytes, void **out) {
+int tm_host_alloc_ex(tm_index *ix, uint64_t bytes, uint32_t flags, void **out) {
     if (!ix || !out) return fail(ix, TM_EINVAL, "tm_host_alloc: null argument");
     *out = nullptr;
+    if (flags & ~TM_ALLOC_VRAM) return fail(ix, TM_EINVAL, "tm_host_alloc_ex: unknown flags");
     std::lock_guard<std::mutex> g(ix->mu);
     HIPCHK(ix, hipSetDevice(ix->rep[0].device));
     void *h = nullptr, *d = nullptr;
+    if (flags & TM_ALLOC_VRAM) {
+        // a replica on another device would read it over the fabric: one device only
+        for (int r = 1; r < ix->nrep; r++)
+            if (ix->rep[r].device != ix->rep[0].device)
+                return fail(ix, TM_EINVAL, "tm_host_alloc_ex: TM_ALLOC_VRAM needs a one-device index");
+        // fine-grained: the host maps it through the BAR (same virtual address)
+        if (hipExtMallocWithFlags(&d, bytes ? bytes : 1, hipDeviceMallocFinegrained) != hipSuccess || !d)
+            return fail(ix, TM_ENOMEM, "tm_host_alloc_ex: fine-grained device allocation failed");
+        ix->pinned.push_back({static_cast<uint8_t *>(d), static_cast<uint8_t *>(d), bytes, true});
+        *out = d;
+        return TM_OK;
+    }
     // portable: every replica's device reads it in place (one virtual address on ROCm)
     if (hipHostMalloc(&h, bytes ? bytes : 1, hipHostMallocMapped | hipHostMallocPortable) != hipSuccess || !h)
         return fail(ix, TM_ENOMEM, "tm_host_alloc: hipHostMalloc failed");
     HIPCHK(ix, hipHostGetDevicePointer(&d, h, 0));
-    ix->pinned.push_back({static_cast<uint8_t *>(h), static_cast<uint8_t *>(d), bytes});
+    ix->pinned.push_back({static_cast<uint8_t *>(h), static_cast<uint8_t *>(d), bytes, false});
     *out = h;
     return TM_OK;
 }
+
+int tm_host_alloc(tm_index *ix, uint64_t bytes, void **out) { return tm_host_alloc_ex(ix, bytes, 0, out); }
 
 int tm_host_free(tm_index *ix, void *p) {
     if (!ix) return fail(nullptr, TM_EINVAL, "tm_host_free: null handle");
@@ -2101,7 +2117,8 @@ int tm_host_free(tm_index *ix, void *p) {
         if (ix->pinned[i].host != p) continue;
         int rc = drain_lanes(ix);   // no batch may still read or write it
         if (rc) return rc;
-        HIPCHK(ix, hipHostFree(p));
+        if (ix->pinned[i].vram) HIPCHK(ix, hipFree(p));
+        else HIPCHK(ix, hipHostFree(p));
         ix->pinned.erase(ix->pinned.begin() + i);
         return TM_OK;
     }

@@ -1612,30 +1612,30 @@ __global__ __launch_bounds__(MID_BLOCK) void k_walk_tail(DevIndex ix, Workspace 
     if (MODE == MODE_FIRST) reset_lists_if_last(ws);   // count mode: k_rewalk_tail resets
     if (MODE == MODE_COUNT) {
         // the grid's last block: the superblock totals from the (now final)
-        // tile totals -- a lane per superblock, its SUP totals in SUP / 2
-        // independent 16-B loads (the tail of blk past nb is zero)
+        // tile totals.  The tile totals are written only by device-scope
+        // atomics, which are performed coherently across the XCDs: each block
+        // drains its own (s_waitcnt) before its ticket, and the last block
+        // reads them with agent-scope (sc1) loads -- no L2 write-back per
+        // block (an agent-scope release, __threadfence, in every block cost
+        // C3deep's tail 68 us: 159 -> 227 us, profiles/r5/scan/).
         __shared__ uint32_t s_last;
+        __builtin_amdgcn_s_waitcnt(0);
         __syncthreads();
-        if (threadIdx.x == 0) {
-            __threadfence();   // this block's tile additions before its ticket
-            s_last = atomicAdd(&ws.list_n[L_COUNT + 1], 1u) == gridDim.x - 1;
-        }
+        if (threadIdx.x == 0) s_last = atomicAdd(&ws.list_n[L_COUNT + 1], 1u) == gridDim.x - 1;
         __syncthreads();
         if (!s_last) return;
-        __threadfence();
         const uint64_t nb = (n + TILE - 1) / TILE, ns = (nb + SUP - 1) / SUP;
-        for (uint64_t sb = threadIdx.x; sb < ns; sb += MID_BLOCK) {
-            typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
-            const u64x2 *q = reinterpret_cast<const u64x2 *>(ws.blk + sb * SUP);
-            u64x2 x[SUP / 2];
-#pragma unroll
-            for (int i = 0; i < SUP / 2; i++) x[i] = __builtin_nontemporal_load(q + i);
+        for (uint64_t sb = threadIdx.x; sb < ns; sb += MID_BLOCK) {   // a lane per superblock
+            const uint64_t t0 = sb * SUP, t1 = t0 + SUP < nb ? t0 + SUP : nb;
             uint64_t v = 0;
+#pragma unroll 1
+            for (uint64_t c = t0; c < t1; c += 8) {   // 8 loads in flight
+                uint64_t x[8];
 #pragma unroll
-            for (int i = 0; i < SUP / 2; i++) {
-                const uint64_t i0 = sb * SUP + 2 * i;
-                if (i0 < nb) v += x[i].x;
-                if (i0 + 1 < nb) v += x[i].y;
+                for (int i = 0; i < 8; i++)
+                    x[i] = c + i < t1 ? __hip_atomic_load(&ws.blk[c + i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+#pragma unroll
+                for (int i = 0; i < 8; i++) v += x[i];
             }
             ws.sup[sb] = v;
         }

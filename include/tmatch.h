@@ -234,6 +234,19 @@ int tm_match_batch32_dev(tm_index *h, uint64_t n, const uint8_t *d_topic_bytes, 
 int tm_host_alloc(tm_index *h, uint64_t bytes, void **out);
 int tm_host_free(tm_index *h, void *p);
 
+/* tm_host_alloc with flags.  TM_ALLOC_VRAM: device memory of the index's GPU
+ * (fine-grained HBM) mapped into the host's address space through the PCIe
+ * BAR, for a batch's INPUTS (topic bytes, offsets): the host writes it with
+ * ordinary stores (write-combined: ~37 GB/s for a 4k-topic batch's 140 KB,
+ * tools/study/bar_probe.hip), and an in-place batch's kernel then reads HBM --
+ * no PCIe read on its critical path.  Host READS of it are uncached PCIe reads
+ * (~0.6 us each): write it, never read it back.  Outputs stay in tm_host_alloc
+ * memory.  Only on an index with one device (TM_EINVAL for replicas); freed by
+ * tm_host_free.  flags 0 = tm_host_alloc.  (No reference counterpart: the
+ * NIF's own buffers.) */
+#define TM_ALLOC_VRAM 1u
+int tm_host_alloc_ex(tm_index *h, uint64_t bytes, uint32_t flags, void **out);
+
 /* Device-resident batch: every pointer is device memory; asynchronous on
  * `stream` (hipStream_t; NULL = HIP's default stream, which PyTorch's default
  * stream handle 0 also names).  d_out_hit_offsets has

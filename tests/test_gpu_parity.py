@@ -2570,6 +2570,86 @@ def test_combined_small_batches_equal_single_launches(torch_dev, kind):
     assert ix.debug_get(_native.TM_DEBUG_FAILED_BATCHES) == f0 + 1
 
 
+def test_vram_inputs_equal_host_buffers(torch_dev):
+    """TM_ALLOC_VRAM (include/tmatch.h tm_host_alloc_ex): a batch whose topic
+    bytes and offsets live in device memory mapped into the host -- written by
+    the host, never read back by this test -- runs in place on the NIF's u32
+    entry point, alone and through the combiner (concurrent callers, deltas in
+    between), with offsets, values and flags identical to the same batch in
+    tm_host_alloc memory, which the oracle checks.  Freed by tm_host_free."""
+    import threading
+    fs = wl.filters(3, 200_000)
+    ix, o = gpu_index(fs), oracle_of(fs)
+    sets = []
+    for k, nt in enumerate([1, 100, 4096, 9000, 65536]):
+        ts = wl.topics(3, 200_000, nt, first=k * 70_000)
+        items = [ts.item(i) for i in range(nt)]
+        if nt >= 100:
+            items[nt // 3] = b"x/#/y"   # badarg in its own slot
+        blob, offs = _native.pack_strings(items)
+        vb = ix.host_array(len(blob) + 16, np.uint8, vram=True)
+        vb[: len(blob)] = blob
+        vo = ix.host_array(nt + 1, np.uint32, vram=True)
+        vo[:] = offs.astype(np.uint32)
+        hb = ix.host_array(len(blob) + 16, np.uint8)
+        hb[: len(blob)] = blob
+        ho = ix.host_array(nt + 1, np.uint32)
+        ho[:] = offs.astype(np.uint32)
+        cap = 64 * nt + 64
+        outs = [(ix.host_array(nt + 1, np.uint32), ix.host_array(cap, np.uint32), ix.host_array(nt, np.uint8))
+                for _ in range(2)]
+        sets.append((vb, vo, hb, ho, outs, items, blob, offs))
+    ref = []
+    for vb, vo, hb, ho, outs, items, blob, offs in sets:
+        h, v, e = ix.match_batch32(hb, ho, outs[0])
+        ref.append((h.copy(), v.copy(), e.copy()))
+        oc, _, ohit, ovals = o.match_batch(blob, offs)
+        for i in range(len(items)):
+            if e[i]:
+                assert b"+" in items[i] or b"#" in items[i]
+                continue
+            assert np.array_equal(v[h[i]:h[i + 1]], ovals[int(ohit[i]):int(ohit[i + 1])])
+        h2, v2, e2 = ix.match_batch32(vb, vo, outs[1])   # alone
+        assert np.array_equal(h2, h) and np.array_equal(v2, v) and np.array_equal(e2, e)
+    errors = []
+
+    def caller(k):
+        vb, vo, _, _, outs, _, _, _ = sets[k]
+        try:
+            for _ in range(20):
+                h, v, e = ix.match_batch32(vb, vo, outs[1])
+                rh, rv, re_ = ref[k]
+                if not (np.array_equal(h, rh) and np.array_equal(v, rv) and np.array_equal(e, re_)):
+                    errors.append(k)
+                    return
+        except Exception as ex:   # noqa: BLE001 -- reported below
+            errors.append((k, repr(ex)))
+
+    ix.debug_set(_native.TM_DEBUG_COMBINE, 1)
+    l0 = ix.debug_get(_native.TM_DEBUG_COMBINED_LAUNCHES)
+    b0 = ix.debug_get(_native.TM_DEBUG_COMBINED_BATCHES)
+    th = [threading.Thread(target=caller, args=(k,)) for k in range(len(sets))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    ix.debug_set(_native.TM_DEBUG_COMBINE, 4)
+    assert not errors, errors
+    assert ix.debug_get(_native.TM_DEBUG_COMBINED_BATCHES) - b0 == 20 * len(sets)
+    assert ix.debug_get(_native.TM_DEBUG_COMBINED_LAUNCHES) - l0 < 20 * len(sets)
+    # a delta between two batches: the VRAM batch sees it as the host one does
+    new = b"/".join(bytes(w) for w in sets[2][5][0].split(b"/")[:2]) + b"/#"
+    ix.apply(np.ones(1, np.uint8), *_native.pack_strings([new]), np.array([0xABCDEF], np.uint32))
+    vb, vo, hb, ho, outs, _, _, _ = sets[2]
+    h, v, e = ix.match_batch32(hb, ho, outs[0])
+    h = h.copy(); v = v.copy(); e = e.copy()
+    assert 0xABCDEF in v
+    h2, v2, e2 = ix.match_batch32(vb, vo, outs[1])
+    assert np.array_equal(h2, h) and np.array_equal(v2, v) and np.array_equal(e2, e)
+    for a_ in (vb, vo):
+        ix.host_free(a_)
+
+
 @pytest.mark.parametrize("nt", [1, 3000, 65536, 70_000])
 def test_u32_offsets_api_equals_u64(torch_dev, nt):
     """tm_match_batch32_ex / tm_match_batch32_dev: u32 topic
