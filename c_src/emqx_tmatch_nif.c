@@ -133,6 +133,10 @@ static ERL_NIF_TERM nif_new(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[])
     int rc = nd ? tm_create_replicas(&o, devs, nd, &r->h) : tm_create(&o, &r->h);
     if (rc != TM_OK) { r->h = NULL; enif_release_resource(r); return err_term(env, rc); }
     tmn_pool_init(&r->pool, r->h);
+    /* one device: batch inputs in HBM the host writes through the BAR, so the
+       in-place kernel reads no host memory (tm_host_alloc_ex; a set falls back
+       to pinned host memory if the allocation fails) */
+    if (!nd) r->pool.in_flags = TM_ALLOC_VRAM;
     ERL_NIF_TERM t = enif_make_resource(env, r);
     enif_release_resource(r);
     return enif_make_tuple2(env, A_OK, t);

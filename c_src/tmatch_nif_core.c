@@ -35,7 +35,7 @@ tmn_set *tmn_take(tmn_pool *p) {
     if (s) { p->pool = s->next; p->npool--; }
     pthread_mutex_unlock(&p->mu);
     if (!s) s = calloc(1, sizeof *s);
-    if (s) s->next = NULL;
+    if (s) { s->next = NULL; s->in_flags = p->in_flags; }
     return s;
 }
 
@@ -47,22 +47,42 @@ void tmn_give(tmn_pool *p, tmn_set *s) {
     if (s) set_free(p->h, s);
 }
 
-void *tmn_get(tm_index *h, tmn_buf *b, uint64_t need) {
-    if (need <= b->cap && b->p) return b->p;
+void *tmn_get_ex(tm_index *h, tmn_buf *b, uint64_t need, uint32_t flags) {
+    if (need <= b->cap && b->p && b->flags == flags) return b->p;
     if (b->p) tm_host_free(h, b->p);
     b->p = NULL;
     b->cap = need + need / 2 + 4096;
-    if (tm_host_alloc(h, b->cap, &b->p) != TM_OK) { b->p = NULL; b->cap = 0; }
+    b->flags = flags;
+    if (flags && tm_host_alloc_ex(h, b->cap, flags, &b->p) != TM_OK) { b->p = NULL; b->flags = 0; }
+    if (!b->p && tm_host_alloc(h, b->cap, &b->p) != TM_OK) { b->p = NULL; b->cap = 0; }
     return b->p;
 }
+
+void *tmn_get(tm_index *h, tmn_buf *b, uint64_t need) { return tmn_get_ex(h, b, need, 0); }
 
 int tmn_pack(tmn_set *s, tm_index *h, uint32_t n, const uint8_t *const *topics, const uint64_t *lens) {
     uint64_t tot = 0;
     for (uint32_t i = 0; i < n; i++) tot += lens[i];
     if (tot > 0xFFFFFFFFull) return TM_EINVAL;
-    uint8_t *blob = tmn_get(h, &s->blob, tot + 16);
-    uint32_t *offs = tmn_get(h, &s->offs, 4ull * (n + 1));
+    uint8_t *blob = tmn_get_ex(h, &s->blob, tot + 16, s->in_flags);
+    uint32_t *offs = tmn_get_ex(h, &s->offs, 4ull * (n + 1), s->in_flags);
     if (!blob || !offs) return TM_ENOMEM;
+    if (s->offs.flags) {
+        /* device memory: written once, in order, never read back (each host
+           read would be a PCIe round trip); the u64 offsets tm_first_batch
+           takes are kept on the host beside them */
+        uint64_t *o64 = tmn_get(h, &s->offs64, 8ull * (n + 1));
+        if (!o64) return TM_ENOMEM;
+        tot = 0;
+        for (uint32_t i = 0; i < n; i++) {
+            o64[i] = tot;
+            if (lens[i]) memcpy(blob + tot, topics[i], lens[i]);
+            tot += lens[i];
+        }
+        o64[n] = tot;
+        for (uint32_t i = 0; i <= n; i++) offs[i] = (uint32_t)o64[i];
+        return TM_OK;
+    }
     tot = 0;
     for (uint32_t i = 0; i < n; i++) {
         offs[i] = (uint32_t)tot;
@@ -105,8 +125,10 @@ int tmn_first(tmn_set *s, tm_index *h, uint32_t n) {
     uint8_t *found = tmn_get(h, &s->err, (uint64_t)n + 1);
     uint64_t *o64 = tmn_get(h, &s->offs64, 8ull * (n + 1));
     if (!val || !found || !o64) return TM_ENOMEM;
-    const uint32_t *o32 = s->offs.p;
-    for (uint32_t i = 0; i <= n; i++) o64[i] = o32[i];   /* tm_first_batch takes u64 offsets */
+    if (!s->offs.flags) {   /* (device-memory offsets: tmn_pack filled o64 already) */
+        const uint32_t *o32 = s->offs.p;
+        for (uint32_t i = 0; i <= n; i++) o64[i] = o32[i];   /* tm_first_batch takes u64 offsets */
+    }
     return tm_first_batch(h, n, s->blob.p, o64, val, found);
 }
 

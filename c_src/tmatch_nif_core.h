@@ -26,11 +26,12 @@ extern "C" {
 #define TMN_POOL_MAX 64          /* sets kept; more concurrent callers allocate and free their own */
 #define TMN_IDS_PER_TOPIC 16     /* first capacity guess: values per topic */
 
-typedef struct { void *p; uint64_t cap; } tmn_buf;
+typedef struct { void *p; uint64_t cap; uint32_t flags; } tmn_buf;   /* flags: what p is (TM_ALLOC_VRAM or 0) */
 
 typedef struct tmn_set {         /* one caller's batch buffers (tm_host_alloc: the batch runs in place) */
     tmn_buf blob, offs, hit, vals, err, uniq;   /* offs, hit: u32 (tm_match_batch32_ex) */
     tmn_buf offs64;                              /* tm_first_batch's u64 offsets */
+    uint32_t in_flags;           /* the pool's input placement (tmn_pool.in_flags) */
     uint64_t reruns;             /* batches rerun after TM_ECAP (diagnostics) */
     struct tmn_set *next;
 } tmn_set;
@@ -40,6 +41,11 @@ typedef struct {
     pthread_mutex_t mu;          /* guards pool / npool only: held for a few instructions */
     tmn_set *pool;
     int npool;
+    /* TM_ALLOC_VRAM: pack the topics and offsets into device memory the host
+       writes through the BAR (tm_host_alloc_ex), so the in-place kernel reads
+       HBM; never read back by the host.  0: pinned host memory.  Set once,
+       before the first tmn_take (the NIF: for a one-device index). */
+    uint32_t in_flags;
 } tmn_pool;
 
 void tmn_pool_init(tmn_pool *p, tm_index *h);
@@ -49,6 +55,9 @@ void tmn_give(tmn_pool *p, tmn_set *s);  /* back to the pool, or freed beyond TM
 
 /* grow-only pinned buffer (contents are not kept across a grow); NULL on failure */
 void *tmn_get(tm_index *h, tmn_buf *b, uint64_t need);
+/* the same in memory of kind `flags` (TM_ALLOC_VRAM), or pinned host memory if
+   that allocation fails (b->flags says which it got) */
+void *tmn_get_ex(tm_index *h, tmn_buf *b, uint64_t need, uint32_t flags);
 
 /* Topic i is topics[i][0 .. lens[i]).  Packs them into the set's pinned blob
  * (16-byte aligned, as the in-place path needs) and u32 offsets (TM_EINVAL if

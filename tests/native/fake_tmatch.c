@@ -24,6 +24,21 @@ int tm_host_alloc(tm_index *h, uint64_t bytes, void **out) {
     return TM_OK;
 }
 
+/* TM_ALLOC_VRAM: host memory here, counted apart; fake_vram_fail(1) makes
+   such allocations fail (the NIF core then falls back to tm_host_alloc) */
+static long n_vram;
+static int vram_fail;
+int tm_host_alloc_ex(tm_index *h, uint64_t bytes, uint32_t flags, void **out) {
+    if (!flags) return tm_host_alloc(h, bytes, out);
+    if (vram_fail) { *out = NULL; return TM_ENOMEM; }
+    int rc = tm_host_alloc(h, bytes, out);
+    if (rc == TM_OK) n_vram++;
+    return rc;
+}
+long fake_vram_count(void) { return n_vram; }
+void fake_vram_fail(int f) { vram_fail = f; }
+void fake_pool_set_inputs(tmn_pool *p, uint32_t flags) { p->in_flags = flags; }
+
 int tm_host_free(tm_index *h, void *p) {
     (void)h;
     free(p);

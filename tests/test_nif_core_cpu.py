@@ -84,6 +84,37 @@ def test_rows_and_badarg(core):
     core.fake_pool_free(pool)
 
 
+def test_vram_inputs_same_rows_and_host_fallback(core):
+    """A one-device NIF packs its inputs into TM_ALLOC_VRAM memory
+    (tmn_pool.in_flags): topics and u32 offsets written once, in order, the
+    u64 offsets for tm_first_batch kept on the host (the core never reads
+    device memory back).  Rows equal the host-buffer ones; when the device
+    allocation fails the set falls back to pinned host memory."""
+    core.fake_vram_count.restype = C.c_long
+    core.fake_pool_set_inputs.argtypes = [C.c_void_p, C.c_uint32]
+    core.fake_vram_fail.argtypes = [C.c_int]
+    topics = [b"ab", b"+x", b"", b"xyz"]
+    for fail in (0, 1):
+        core.fake_vram_fail(fail)
+        pool = core.fake_pool_new()
+        core.fake_pool_set_inputs(pool, 1)   # TM_ALLOC_VRAM
+        s = core.tmn_take(pool)
+        v0 = core.fake_vram_count()
+        assert pack(core, s, topics) == TM_OK
+        assert core.fake_vram_count() - v0 == (0 if fail else 2)   # blob + offsets
+        assert core.tmn_match(s, H, len(topics), TRAVERSAL) == TM_OK
+        assert rows(core, s, 4, TRAVERSAL) == [[0, 1], 1, [], [3000, 3001, 3002]]
+        assert core.tmn_first(s, H, len(topics)) == TM_OK
+        found = []
+        for i in range(4):
+            v = C.c_uint32()
+            found.append((core.tmn_first_row(s, i, C.byref(v)), v.value))
+        assert found == [(1, 0), (2, 0), (0, 0), (1, 3000)]
+        core.tmn_give(pool, s)
+        core.fake_pool_free(pool)
+    core.fake_vram_fail(0)
+
+
 def test_ecap_grows_the_set_and_reruns_once(core):
     """More values than the first guess (TMN_IDS_PER_TOPIC per topic + 1024):
     the batch is rerun once with room for the exact total, and the grown
