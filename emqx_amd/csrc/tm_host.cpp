@@ -103,6 +103,7 @@ struct Lane {
     hipEvent_t done = nullptr;   // after the lane's last batch: later patches wait for it
     uint64_t tick = 0;        // last use (LRU of device-API lanes)
     uint32_t tag = 0;         // launches on this workspace (the one-launch path's look-back tag)
+    uint64_t waited = 0;      // the replica's patch (seq) this lane's stream last waited for
     Workspace w{};
     // host-API staging: mapped pinned buffers (*_dev = their device
     // addresses) and the HBM copies used for batches above ZC_TOPICS
@@ -1678,8 +1679,12 @@ int ensure_ws(tm_index *ix, uint64_t n, Lane &ln) {
         std::memset(w.hint_h, 0, HINT_WORDS * 4);
         HIPCHK(ix, hipHostGetDevicePointer(reinterpret_cast<void **>(&w.hint_d), w.hint_h, 0));
     }
-    // the batch must see every patch shipped so far, whichever stream it went on
-    if (ix->rep[ln.r].last_patch) HIPCHK(ix, hipStreamWaitEvent(ln.s, ix->rep[ln.r].last_patch, 0));
+    // the batch must see every patch shipped so far, whichever stream it went
+    // on (once per patch: later batches on the lane's stream are behind it)
+    if (ix->rep[ln.r].last_patch && ln.waited != ix->rep[ln.r].applied) {
+        HIPCHK(ix, hipStreamWaitEvent(ln.s, ix->rep[ln.r].last_patch, 0));
+        ln.waited = ix->rep[ln.r].applied;
+    }
     if (n <= w.cap_n && w.cnt) return TM_OK;
     HIPCHK(ix, hipStreamSynchronize(ln.s));
     if (w.cnt) {
@@ -2397,8 +2402,8 @@ int tm_match_batch32_ex(tm_index *ix, uint64_t n, const uint8_t *tb, const uint3
     if (order > TM_ORDER_UNIQUE) return fail(ix, TM_EINVAL, "tm_match_batch32: bad order");
     if (cap > 0xFFFFFFFFull) cap = 0xFFFFFFFFull;   // (a 32-bit offset addresses no more)
     if (n && n <= ZC_TOPICS && order == TM_ORDER_TRAVERSAL && ((uintptr_t)tb & 15) == 0) {
+        const uint64_t nbytes = to[n];   // (before the lock: in TM_ALLOC_VRAM memory a host read is a PCIe round trip)
         std::unique_lock<std::mutex> g(ix->mu);
-        const uint64_t nbytes = to[n];
         uint8_t *db = nbytes ? pinned_dev(ix, tb, nbytes) : nullptr;
         uint8_t *dof = pinned_dev(ix, to, (n + 1) * 4);
         uint8_t *dh = pinned_dev(ix, out_hit, (n + 1) * 4);
