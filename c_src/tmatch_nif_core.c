@@ -34,8 +34,8 @@ tmn_set *tmn_take(tmn_pool *p) {
     tmn_set *s = p->pool;
     if (s) { p->pool = s->next; p->npool--; }
     pthread_mutex_unlock(&p->mu);
-    if (!s) s = calloc(1, sizeof *s);
-    if (s) { s->next = NULL; s->in_flags = p->in_flags; }
+    if (!s && (s = calloc(1, sizeof *s))) s->in_flags = p->in_flags;   /* (a pooled set keeps its own: 0 after a failed device allocation) */
+    if (s) s->next = NULL;
     return s;
 }
 
@@ -67,6 +67,9 @@ int tmn_pack(tmn_set *s, tm_index *h, uint32_t n, const uint8_t *const *topics, 
     uint8_t *blob = tmn_get_ex(h, &s->blob, tot + 16, s->in_flags);
     uint32_t *offs = tmn_get_ex(h, &s->offs, 4ull * (n + 1), s->in_flags);
     if (!blob || !offs) return TM_ENOMEM;
+    /* a device allocation that failed is not retried batch after batch (each
+       retry would free a host buffer, which waits for the index's batches) */
+    if (s->in_flags && (s->blob.flags != s->in_flags || s->offs.flags != s->in_flags)) s->in_flags = 0;
     if (s->offs.flags) {
         /* device memory: written once, in order, never read back (each host
            read would be a PCIe round trip); the u64 offsets tm_first_batch
