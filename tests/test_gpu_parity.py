@@ -2646,6 +2646,18 @@ def test_vram_inputs_equal_host_buffers(torch_dev):
     assert 0xABCDEF in v
     h2, v2, e2 = ix.match_batch32(vb, vo, outs[1])
     assert np.array_equal(h2, h) and np.array_equal(v2, v) and np.array_equal(e2, e)
+    # match/2 (tm_first_batch) the way the NIF runs it (tmn_first): topic bytes
+    # in device memory, u64 offsets and the outputs in pinned host memory
+    vb, vo, hb, ho, outs, items, blob, offs = sets[2]
+    nt = len(items)
+    o64 = ix.host_array(nt + 1, np.uint64)
+    o64[:] = offs
+    val = ix.host_array(nt, np.uint32)
+    found = ix.host_array(nt, np.uint8)
+    ix._check(ix._lib.tm_first_batch(ix._h, nt, _native._ptr(vb), _native._ptr(o64), _native._ptr(val),
+                                     _native._ptr(found)))
+    rv, rf = ix.first_batch(blob, offs)
+    assert np.array_equal(val, rv) and np.array_equal(found, rf)
     for a_ in (vb, vo):
         ix.host_free(a_)
 
