@@ -85,17 +85,20 @@ def parse():
                         "the router syncer's batch size, emqx_router_syncer.erl's <= 1000 ops per run_batch)")
     p.add_argument("--streams", type=int, default=None,
                    help="HIP streams the steps rotate over (batch k+1's walk overlaps batch k's scan/emit); "
-                        "default 3, and 1 for c5 with one copy of the tables: a churn step's patch then waits "
+                        "default 3; for c5 one per table copy up to 2 (with one copy a churn step's patch waits "
                         "for every batch in flight, so its steps cannot overlap and a second stream only adds "
-                        "cross-stream waits (0.41 vs 0.54-0.64 ms per step measured in round 2)")
+                        "cross-stream waits: 0.41 vs 0.54-0.64 ms per step measured in round 2)")
     p.add_argument("--split", type=int, default=1,
                    help="sub-batches per step: each step's batch goes to the streams as this many contiguous "
                         "sub-batches (each its own CSR, as that many concurrent NIF batches), so the timed "
                         "region ends one sub-batch's latency after the last launch instead of one whole "
                         "overlapped batch's")
-    p.add_argument("--copies", type=int, default=1,
+    p.add_argument("--copies", type=int, default=None,
                    help="copies of the tables on the GPU (tm_options.copies): a batch after a delta runs on a "
-                        "copy no batch is reading (measured: no gain on c5 or churned callers, DESIGN.md 3)")
+                        "copy no batch is reading.  Default 1, and 2 for c5 on two streams: each step's patch "
+                        "goes to the copy the step before did not read, so consecutive churn steps overlap "
+                        "(round 5: 3.30e9 vs 2.89e9 with one copy on one stream; 2 copies on 3 streams 1.65e9, "
+                        "3 on 3 2.44e9, profiles/r5/c5/)")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     p.add_argument("--cpu-threads", type=int, default=None,
                    help="CPU baseline threads (default: the CPUs this process may use)")
@@ -198,7 +201,7 @@ def main():
     log(f"[rank {rank}] generated {len(fs)} filters in {t_gen:.1f}s")
 
     t = time.time()
-    copies = a.copies
+    copies = a.copies if a.copies is not None else (2 if a.config == "c5" else 1)
     ix = _native.Index(device=local, hint_keys=len(fs), copies=copies)
     if a.small_kernel != "auto":
         ix.debug_set(_native.TM_DEBUG_SMALL_KERNEL, {"wave": _native.SMALL_WAVE, "wave8": _native.SMALL_WAVE8,
@@ -240,7 +243,7 @@ def main():
     # step k+1's walk overlaps step k's scan / emit (the library keeps one
     # workspace per stream and orders index patches across streams)
     nstreams = 1 if filter_sharded else max(1, a.streams if a.streams is not None else
-                                            (1 if a.config == "c5" and copies == 1 else 3))
+                                            (copies if a.config == "c5" and copies <= 2 else 3))
     streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(nstreams - 1)]
     split = 1 if (filter_sharded or a.config == "c5") else max(1, min(a.split, nstreams))
     sub = -(-B // split)
