@@ -29,12 +29,13 @@ def main():
     p.add_argument("--kinds", default="auto,wave,wave8")
     p.add_argument("--churn", type=int, default=0)
     p.add_argument("--seconds", type=float, default=1.0)
+    p.add_argument("--copies", type=int, default=1, help="tm_options.copies of the index")
     a = p.parse_args()
     from bench import CONFIGS, host_bench_lib
     from emqx_amd import _native, workload as wl
     gen, _, _ = CONFIGS["c3"]
     fs = wl.filters(gen, a.filters)
-    ix = _native.Index(device=0)
+    ix = _native.Index(device=0, copies=a.copies)
     for lo in range(0, len(fs), 2_000_000):
         part = fs.slice(lo, min(lo + 2_000_000, len(fs)))
         ix.apply(np.ones(len(part), np.uint8), part.blob, part.offs, part.vals)
@@ -61,7 +62,7 @@ def main():
                     assert rc == 0, rc
                     launches = ix.debug_get(_native.TM_DEBUG_COMBINED_LAUNCHES) - l0
                     batches = ix.debug_get(_native.TM_DEBUG_COMBINED_BATCHES) - b0
-                    print(json.dumps({"threads": nth, "mode": mode, "kind": kind, "leaders": lead,
+                    print(json.dumps({"threads": nth, "mode": mode, "kind": kind, "leaders": lead, "copies": a.copies, "churn": a.churn,
                                       "topics_per_s": round(out[1]), "p50_ms": round(out[2], 4),
                                       "p99_ms": round(out[3], 4), "deltas_per_s": round(out[4]),
                                       "batches_per_launch": round(batches / launches, 2) if launches else None,
