@@ -26,7 +26,8 @@ def torch_dev():
 
 def _small_kind(kind: str) -> int:
     """TM_DEBUG_SMALL_KERNEL value of a small-batch kernel name"""
-    return {"lane": _native.SMALL_LANE, "wave": _native.SMALL_WAVE, "wave8": _native.SMALL_WAVE8}[kind]
+    return {"auto": _native.SMALL_AUTO, "lane": _native.SMALL_LANE, "wave": _native.SMALL_WAVE,
+            "wave8": _native.SMALL_WAVE8}[kind]
 
 
 def gpu_index(items: wl.ItemSet | None = None, flags=None) -> _native.Index:
@@ -1240,8 +1241,8 @@ def test_concurrent_callers_see_consistent_snapshots(torch_dev, copies):
           f"p50 {np.percentile(lat, 50):.3f} ms p99 {np.percentile(lat, 99):.3f} ms")
 
 
-@pytest.mark.parametrize("kind", ["lane", "wave", "wave8"])
-def test_combined_callers_with_deltas_see_snapshots_and_never_fail(torch_dev, kind):
+@pytest.mark.parametrize("kind,copies", [("lane", 1), ("wave", 1), ("wave8", 1), ("auto", 2)])
+def test_combined_callers_with_deltas_see_snapshots_and_never_fail(torch_dev, kind, copies):
     """The NIF's production path under load:
     16 host threads submit in-place 32-bit batches (tm_match_batch32_ex on
     host_array buffers, what the NIF's dirty schedulers do) through the
@@ -1251,12 +1252,14 @@ def test_combined_callers_with_deltas_see_snapshots_and_never_fail(torch_dev, ki
     batch equals the oracle after exactly the epochs its probe topic saw, a
     thread never goes back in time, and no batch's look-back wait expired:
     TM_DEBUG_FAILED_BATCHES and _RETRIED_BATCHES stay 0 (the readers of the
-    reference's read_concurrency table never fail, emqx_topic_index.erl:41-48)."""
+    reference's read_concurrency table never fail, emqx_topic_index.erl:41-48).
+    copies 2: the configuration INTEGRATION recommends under churn (a batch
+    after a delta runs on the table copy no batch is reading)."""
     import threading
     import time
     nf, nthreads, lb, epochs = 10_000, 16, 4096, 16
     fs = wl.filters(1, nf)
-    ix = _native.Index()
+    ix = _native.Index(copies=copies)
     ix.debug_set(_native.TM_DEBUG_COMBINE, 4)
     ix.debug_set(_native.TM_DEBUG_SMALL_KERNEL, _small_kind(kind))
     ix.apply(np.ones(len(fs), np.uint8), fs.blob, fs.offs, fs.vals)
