@@ -85,13 +85,18 @@ def event_key(event):
     return None
 
 
+ROUTER_COPIES = 2   # src/emqx_router_gpu.erl ?COPIES
+
+
 class Router:
     def __init__(self, node="node", device: int = -1, mirror=None):
         self.node = node
         self._bag: dict[bytes, dict] = {}        # emqx_route: Topic -> {Dest: seq} (insertion order)
         self._seq = 0
         self._filters: dict = {}                 # emqx_route_filters: Key -> RouteIdx
-        self._mirror = mirror if mirror is not None else ti.Tab(device=device)   # device mirror of emqx_route_filters
+        # device mirror of emqx_route_filters: two copies of the tables, as
+        # emqx_router_gpu attaches it (?COPIES: the router takes the churn)
+        self._mirror = mirror if mirror is not None else ti.Tab(device=device, copies=ROUTER_COPIES)
         self._mailbox: list = []                 # table events not yet drained by the event process
         self.mirror_calls = 0                    # tm_apply_deltas calls made for the mirror
 

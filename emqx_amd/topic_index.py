@@ -45,8 +45,12 @@ from .trie_search import (BadArg, HASH, PLUS, filter_words, get_id, get_topic, k
 class Tab:
     """An index table: records + the device-resident mirror of its keys."""
 
-    def __init__(self, device: int = -1, hint_keys: int = 0, index=None):
-        self._index = index if index is not None else _native.Index(device=device, hint_keys=hint_keys)
+    def __init__(self, device: int = -1, hint_keys: int = 0, index=None, copies: int = 1):
+        """copies: copies of the tables on the device (tm_options.copies; new/1's
+        {copies, N}): under churn a batch after a delta runs on a copy no batch
+        is reading."""
+        self._index = index if index is not None else _native.Index(device=device, hint_keys=hint_keys,
+                                                                    copies=copies)
         self._records: dict = {}        # key -> record        (the ETS rows)
         self._kid: dict = {}            # key -> u32 value on the device
         self._keys: list = []           # u32 -> key (None: deleted)

@@ -38,6 +38,11 @@
 
 -define(PT_KEY, {?MODULE, mirror}).
 -define(BOOT_BATCH, 100000).
+%% copies of the route tables per device: the router's mirror takes the
+%% cluster's subscribe/unsubscribe churn, and with two copies a publish batch
+%% after a delta runs on the copy no batch is reading (DESIGN.md 8 item 2:
+%% churned callers +10-19 %, C5 3.30e9 vs 2.89e9 topic matches/s)
+-define(COPIES, 2).
 -define(MAX_EVENTS, 10000).
 
 %% Boot: mirror the existing ?ROUTE_TAB_FILTERS (emqx_router.erl:148-160) on the
@@ -46,7 +51,7 @@
 %% start_link(Devices).
 -spec attach([integer()]) -> ok.
 attach(Devices) ->
-    G = emqx_topic_index_gpu:attach(?ROUTE_TAB_FILTERS, ?BOOT_BATCH, Devices),
+    G = emqx_topic_index_gpu:attach(?ROUTE_TAB_FILTERS, ?BOOT_BATCH, {Devices, ?COPIES}),
     persistent_term:put(?PT_KEY, G),
     ok.
 

@@ -79,8 +79,9 @@ attach(Tab, BatchSize) ->
     attach(Tab, BatchSize, -1).
 
 %% Devices: -1 (the default device), a device, or a list of devices (one
-%% replica each, one host image -- SURVEY.md 8e topic-sharded mode in one node).
--spec attach(ets:table(), pos_integer(), integer() | [integer()]) -> gtab().
+%% replica each, one host image -- SURVEY.md 8e topic-sharded mode in one node),
+%% or {Devices, Copies} (Copies copies of the tables per device).
+-spec attach(ets:table(), pos_integer(), integer() | [integer()] | {integer() | [integer()], pos_integer()}) -> gtab().
 attach(Tab, BatchSize, Devices) ->
     G = mirror(Tab, Devices),
     ets:safe_fixtable(Tab, true),
