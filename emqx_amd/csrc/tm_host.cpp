@@ -1828,8 +1828,30 @@ int tm_replica_stats(tm_index *ix, uint32_t r, uint64_t *batches, int32_t *devic
 
 namespace { void mf_free_keys(tm_index::MfState &m); }
 
+// TM_HOST_TIMING=1 (diagnostics): where a combined launch's host time goes,
+// summed over the process and printed by tm_destroy
+struct CmbTiming {
+    std::atomic<uint64_t> groups{0}, reqs{0};
+    std::atomic<uint64_t> lock_ns{0}, setup_ns{0}, launch_ns{0}, sync_ns{0}, release_ns{0}, done_ns{0}, req_ns{0};
+};
+static CmbTiming g_cmbt;
+static const bool g_cmb_timing = getenv("TM_HOST_TIMING") != nullptr;
+static inline uint64_t ns_now() {
+    return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+        std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 int tm_destroy(tm_index *ix) {
     if (!ix) return TM_EINVAL;
+    if (g_cmb_timing && g_cmbt.groups) {
+        const double g = (double)g_cmbt.groups, us = 1e-3;
+        fprintf(stderr, "tm combiner: %lu launches, %lu requests (%.2f per launch); per launch us: lock %.1f "
+                        "setup %.1f launch %.1f sync %.1f lane-release %.1f mark-done %.1f; per request %.1f us\n",
+                (unsigned long)g_cmbt.groups.load(), (unsigned long)g_cmbt.reqs.load(), g_cmbt.reqs / g,
+                g_cmbt.lock_ns * us / g, g_cmbt.setup_ns * us / g, g_cmbt.launch_ns * us / g, g_cmbt.sync_ns * us / g,
+                g_cmbt.release_ns * us / g, g_cmbt.done_ns * us / g,
+                g_cmbt.req_ns * us / std::max<double>(1.0, (double)g_cmbt.reqs));
+    }
     for (int r = 0; r < ix->nrep; r++) {
         (void)hipSetDevice(ix->rep[r].device);
         (void)hipDeviceSynchronize();
@@ -2172,10 +2194,13 @@ struct SmallReq {
 };
 constexpr int CMB_LEGACY = 1;   // (not a TM_ code) the index no longer allows the one-launch path
 
-static int run_small_group(tm_index *ix, const std::vector<SmallReq *> &grp) {
+
+static int run_small_group(tm_index *ix, const std::vector<SmallReq *> &grp, uint64_t *t_sync_end) {
     uint64_t total = 0;
     for (auto *r : grp) total += r->n;
+    const uint64_t ta = g_cmb_timing ? ns_now() : 0;
     std::unique_lock<std::mutex> g(ix->mu);
+    const uint64_t tb = g_cmb_timing ? ns_now() : 0;
     LaneLease lease{ix, g};
     int rc;
     if ((rc = host_lane(ix, g, lease.ln))) return rc;
@@ -2192,6 +2217,7 @@ static int run_small_group(tm_index *ix, const std::vector<SmallReq *> &grp) {
         sg.s[k] = SmallSeg{r.db ? r.db : r.dof, r.dof, r.dh, r.de, reinterpret_cast<uint32_t *>(r.dv),
                            r.dv ? r.cap : 0, (uint32_t)r.n, 0};
     }
+    const uint64_t tc = g_cmb_timing ? ns_now() : 0;
     for (int tries = 0;; tries++) {
         const DevIndex d = dev_view(ix, ln.r);
         uint32_t tag;
@@ -2203,7 +2229,14 @@ static int run_small_group(tm_index *ix, const std::vector<SmallReq *> &grp) {
         ix->cmb_batches += grp.size();
         if ((rc = batch_done(ix, ln))) return rc;
         g.unlock();
+        const uint64_t td = g_cmb_timing ? ns_now() : 0;
         HIPCHK(ix, hipStreamSynchronize(s));
+        if (g_cmb_timing) {
+            const uint64_t te = ns_now();
+            g_cmbt.groups++;
+            g_cmbt.lock_ns += tb - ta; g_cmbt.setup_ns += tc - tb; g_cmbt.launch_ns += td - tc; g_cmbt.sync_ns += te - td;
+            *t_sync_end = te;
+        }
         if (!batch_failed(ix, ln)) break;
         if ((rc = retry_or_fail(ix, g, ln, tries))) return rc;
     }
@@ -2211,6 +2244,11 @@ static int run_small_group(tm_index *ix, const std::vector<SmallReq *> &grp) {
 }
 
 static int small_combined(tm_index *ix, SmallReq &rq) {
+    const uint64_t t_in = g_cmb_timing ? ns_now() : 0;
+    struct ReqTime {   // (on every return path)
+        uint64_t t;
+        ~ReqTime() { if (g_cmb_timing) { g_cmbt.reqs++; g_cmbt.req_ns += ns_now() - t; } }
+    } rt{t_in};
     std::unique_lock<std::mutex> lk(ix->cmb_mu);
     ix->cmb_q.push_back(&rq);
     while (!rq.done) {
@@ -2225,8 +2263,14 @@ static int small_combined(tm_index *ix, SmallReq &rq) {
             }
             ix->cmb_running++;
             lk.unlock();
-            const int rc = run_small_group(ix, grp);
+            uint64_t t_sync_end = 0;
+            const int rc = run_small_group(ix, grp, &t_sync_end);   // (the lane is released on return)
+            const uint64_t t_rel = g_cmb_timing ? ns_now() : 0;
             lk.lock();
+            if (g_cmb_timing && t_sync_end) {
+                g_cmbt.release_ns += t_rel - t_sync_end;
+                g_cmbt.done_ns += ns_now() - t_rel;
+            }
             for (auto *r : grp) { r->rc = rc; r->done = true; }
             ix->cmb_running--;
             ix->cmb_cv.notify_all();
