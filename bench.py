@@ -105,6 +105,8 @@ def parse():
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-parity", action="store_true")
     p.add_argument("--latency-batches", type=int, default=20)
+    p.add_argument("--combine-leaders", type=int, default=None,
+                   help="concurrent combined launches of the callers' legs (TM_DEBUG_COMBINE; default: the library's)")
     p.add_argument("--concurrency", type=int, default=8,
                    help="native caller threads of the concurrent-caller leg (and twice as many; 0 = skip)")
     p.add_argument("--frontier-sample", type=int, default=20_000)
@@ -438,7 +440,8 @@ def main():
                                                "mean_ms": round(out[2], 4)}
         if a.concurrency > 0:
             conc = []
-            # (threads, deltas per ms from one more thread): without churn, then with
+            if a.combine_leaders is not None:
+                ix.debug_set(_native.TM_DEBUG_COMBINE, a.combine_leaders)
             # (threads, deltas per ms from one more thread, mode): without churn, then with; mode 4: the
             # u32-offset API the NIF calls (tm_match_batch32_ex), 0: the u64 one
             # mode 5: mode 4 with the inputs in TM_ALLOC_VRAM memory, written by each caller before
@@ -464,6 +467,7 @@ def main():
                              # concurrent launches, measured
                              "failed_batches": fr1[0] - fr0[0], "retried_batches": fr1[1] - fr0[1],
                              "inputs": "vram (written per batch)" if mode == 5 else "host",
+                             "combine_leaders": ix.debug_get(_native.TM_DEBUG_COMBINE) if mode >= 4 else None,
                              "callers": "native threads, tm_host_alloc buffers each (in place)"})
         if B >= 65536:
             allt = wl.concat(tsets)

@@ -150,7 +150,7 @@ constexpr int MAX_HOST_LANES = 16;   // concurrent host-API batches in flight, p
 constexpr int MAX_DEV_LANES = 16;    // device-API streams with a workspace kept
 
 // concurrent combined launches of small host batches (tm_index::cmb_leaders)
-constexpr int CMB_LEADERS = 4;   // (2 / 3 / 6 measured: profiles/r4/combiner/)
+constexpr int CMB_LEADERS = 4;   // (2 / 3 / 6 measured: profiles/r4/combiner/; round 5: 2 / 3, profiles/r5/conc/leaders_*)
 
 struct tm_index {
     // Two locks (order: mu, then img).  `mu` covers the device side: lanes,
@@ -2663,6 +2663,7 @@ int tm_debug_get(tm_index *ix, uint32_t key, uint64_t *value) {
     case TM_DEBUG_PATH_PHASES: *value = ix->path_batches[PATH_PHASES].load(); break;
     case TM_DEBUG_PATH_SMALL: *value = ix->path_batches[PATH_SMALL].load(); break;
     case TM_DEBUG_PATH_LANE: *value = ix->path_batches[PATH_LANE].load(); break;
+    case TM_DEBUG_COMBINE: *value = (uint64_t)ix->cmb_leaders.load(); break;
     case TM_DEBUG_COMBINED_LAUNCHES: *value = ix->cmb_launches.load(); break;
     case TM_DEBUG_COMBINED_BATCHES: *value = ix->cmb_batches.load(); break;
     case TM_DEBUG_WIDE_NODES:

@@ -336,7 +336,7 @@ int tm_profile_read(tm_index *h, double *walk_ms, double *batch_ms, uint64_t *ba
  *   TM_DEBUG_COMBINE        concurrent combined launches of small 32-bit
  *                           in-place host batches (tm_match_batch32_ex): 0 =
  *                           every batch its own launch (default 4)
- * tm_debug_get: TM_DEBUG_FAILED_BATCHES (one-launch batches whose look-back
+ * tm_debug_get: TM_DEBUG_COMBINE (the current setting), TM_DEBUG_FAILED_BATCHES (one-launch batches whose look-back
  * failed, host API), TM_DEBUG_RETRIED_BATCHES (of those, run again) and the
  * match launches per kernel path: TM_DEBUG_PATH_PHASES (walk, tails, scan,
  * emit), TM_DEBUG_PATH_SMALL (k_walk_small), TM_DEBUG_PATH_LANE

@@ -1241,12 +1241,13 @@ def test_concurrent_callers_see_consistent_snapshots(torch_dev, copies):
           f"p50 {np.percentile(lat, 50):.3f} ms p99 {np.percentile(lat, 99):.3f} ms")
 
 
-@pytest.mark.parametrize("kind,copies", [("lane", 1), ("wave", 1), ("wave8", 1), ("auto", 2)])
-def test_combined_callers_with_deltas_see_snapshots_and_never_fail(torch_dev, kind, copies):
+@pytest.mark.parametrize("kind,copies,leaders", [("lane", 1, 4), ("wave", 1, 4), ("wave8", 1, 4), ("auto", 2, None),
+                                                 ("auto", 2, 2)])
+def test_combined_callers_with_deltas_see_snapshots_and_never_fail(torch_dev, kind, copies, leaders):
     """The NIF's production path under load:
     16 host threads submit in-place 32-bit batches (tm_match_batch32_ex on
     host_array buffers, what the NIF's dirty schedulers do) through the
-    host-batch combiner at 4 leaders -- shared k_walk_lane (or k_walk_small)
+    host-batch combiner at 4 leaders (the default; and at 2) -- shared k_walk_lane (or k_walk_small)
     launches with a segment table -- while the main thread applies 16 delta
     epochs.  Every
     batch equals the oracle after exactly the epochs its probe topic saw, a
@@ -1260,7 +1261,9 @@ def test_combined_callers_with_deltas_see_snapshots_and_never_fail(torch_dev, ki
     nf, nthreads, lb, epochs = 10_000, 16, 4096, 16
     fs = wl.filters(1, nf)
     ix = _native.Index(copies=copies)
-    ix.debug_set(_native.TM_DEBUG_COMBINE, 4)
+    if leaders is not None:
+        ix.debug_set(_native.TM_DEBUG_COMBINE, leaders)
+    assert ix.debug_get(_native.TM_DEBUG_COMBINE) == (leaders or 4)
     ix.debug_set(_native.TM_DEBUG_SMALL_KERNEL, _small_kind(kind))
     ix.apply(np.ones(len(fs), np.uint8), fs.blob, fs.offs, fs.vals)
     o = oracle_of(fs)
@@ -2628,6 +2631,7 @@ def test_vram_inputs_equal_host_buffers(torch_dev):
         except Exception as ex:   # noqa: BLE001 -- reported below
             errors.append((k, repr(ex)))
 
+    lead0 = ix.debug_get(_native.TM_DEBUG_COMBINE)
     ix.debug_set(_native.TM_DEBUG_COMBINE, 1)
     l0 = ix.debug_get(_native.TM_DEBUG_COMBINED_LAUNCHES)
     b0 = ix.debug_get(_native.TM_DEBUG_COMBINED_BATCHES)
@@ -2636,7 +2640,7 @@ def test_vram_inputs_equal_host_buffers(torch_dev):
         t.start()
     for t in th:
         t.join()
-    ix.debug_set(_native.TM_DEBUG_COMBINE, 4)
+    ix.debug_set(_native.TM_DEBUG_COMBINE, lead0)
     assert not errors, errors
     assert ix.debug_get(_native.TM_DEBUG_COMBINED_BATCHES) - b0 == 20 * len(sets)
     assert ix.debug_get(_native.TM_DEBUG_COMBINED_LAUNCHES) - l0 < 20 * len(sets)

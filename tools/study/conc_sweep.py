@@ -30,6 +30,7 @@ def main():
     p.add_argument("--churn", type=int, default=0)
     p.add_argument("--seconds", type=float, default=1.0)
     p.add_argument("--copies", type=int, default=1, help="tm_options.copies of the index")
+    p.add_argument("--repeat", type=int, default=1, help="passes over the whole sweep (interleaved A/B)")
     a = p.parse_args()
     from bench import CONFIGS, host_bench_lib
     from emqx_amd import _native, workload as wl
@@ -43,31 +44,33 @@ def main():
     kinds = {"auto": _native.SMALL_AUTO, "wave": _native.SMALL_WAVE, "wave8": _native.SMALL_WAVE8,
              "lane": _native.SMALL_LANE}
     lb = 4096
-    for nth in map(int, a.threads.replace("+", ",").split(",")):
-        ts = wl.topics(gen, a.filters, nth * lb)
-        hh, _, _ = ix.match_batch(ts.blob, ts.offs)
-        cap = int(np.diff(hh.astype(np.int64)).reshape(nth, lb).sum(axis=1).max()) + 65536
-        for mode in map(int, a.modes.replace("+", ",").split(",")):
-            for kind in a.kinds.replace("+", ",").split(","):
-                ix.debug_set(_native.TM_DEBUG_SMALL_KERNEL, kinds[kind])
-                for lead in (map(int, a.leaders.replace("+", ",").split(",")) if mode == 4 else [0]):
-                    if mode == 4:
-                        ix.debug_set(_native.TM_DEBUG_COMBINE, lead)
-                    l0 = ix.debug_get(_native.TM_DEBUG_COMBINED_LAUNCHES)
-                    b0 = ix.debug_get(_native.TM_DEBUG_COMBINED_BATCHES)
-                    f0 = ix.debug_get(_native.TM_DEBUG_FAILED_BATCHES)
-                    out = (ctypes.c_double * 6)()
-                    rc = hb.tmb_callers_ex(ix._h, nth, lb, _native._ptr(ts.blob), _native._ptr(ts.offs), cap,
-                                           a.seconds, a.churn, mode, out)
-                    assert rc == 0, rc
-                    launches = ix.debug_get(_native.TM_DEBUG_COMBINED_LAUNCHES) - l0
-                    batches = ix.debug_get(_native.TM_DEBUG_COMBINED_BATCHES) - b0
-                    print(json.dumps({"threads": nth, "mode": mode, "kind": kind, "leaders": lead, "copies": a.copies, "churn": a.churn,
-                                      "topics_per_s": round(out[1]), "p50_ms": round(out[2], 4),
-                                      "p99_ms": round(out[3], 4), "deltas_per_s": round(out[4]),
-                                      "batches_per_launch": round(batches / launches, 2) if launches else None,
-                                      "failed": ix.debug_get(_native.TM_DEBUG_FAILED_BATCHES) - f0}), flush=True)
-    ix.debug_set(_native.TM_DEBUG_COMBINE, 4)
+    lead0 = ix.debug_get(_native.TM_DEBUG_COMBINE)
+    for rep in range(a.repeat):
+        for nth in map(int, a.threads.replace("+", ",").split(",")):
+            ts = wl.topics(gen, a.filters, nth * lb)
+            hh, _, _ = ix.match_batch(ts.blob, ts.offs)
+            cap = int(np.diff(hh.astype(np.int64)).reshape(nth, lb).sum(axis=1).max()) + 65536
+            for mode in map(int, a.modes.replace("+", ",").split(",")):
+                for kind in a.kinds.replace("+", ",").split(","):
+                    ix.debug_set(_native.TM_DEBUG_SMALL_KERNEL, kinds[kind])
+                    for lead in (map(int, a.leaders.replace("+", ",").split(",")) if mode in (4, 5) else [0]):
+                        if mode in (4, 5):
+                            ix.debug_set(_native.TM_DEBUG_COMBINE, lead)
+                        l0 = ix.debug_get(_native.TM_DEBUG_COMBINED_LAUNCHES)
+                        b0 = ix.debug_get(_native.TM_DEBUG_COMBINED_BATCHES)
+                        f0 = ix.debug_get(_native.TM_DEBUG_FAILED_BATCHES)
+                        out = (ctypes.c_double * 6)()
+                        rc = hb.tmb_callers_ex(ix._h, nth, lb, _native._ptr(ts.blob), _native._ptr(ts.offs), cap,
+                                               a.seconds, a.churn, mode, out)
+                        assert rc == 0, rc
+                        launches = ix.debug_get(_native.TM_DEBUG_COMBINED_LAUNCHES) - l0
+                        batches = ix.debug_get(_native.TM_DEBUG_COMBINED_BATCHES) - b0
+                        print(json.dumps({"rep": rep, "threads": nth, "mode": mode, "kind": kind, "leaders": lead, "copies": a.copies, "churn": a.churn,
+                                          "topics_per_s": round(out[1]), "p50_ms": round(out[2], 4),
+                                          "p99_ms": round(out[3], 4), "deltas_per_s": round(out[4]),
+                                          "batches_per_launch": round(batches / launches, 2) if launches else None,
+                                          "failed": ix.debug_get(_native.TM_DEBUG_FAILED_BATCHES) - f0}), flush=True)
+    ix.debug_set(_native.TM_DEBUG_COMBINE, lead0)
 
 
 if __name__ == "__main__":
