@@ -98,7 +98,8 @@ def parse():
                         "copy no batch is reading.  Default 1, and 2 for c5 on two streams: each step's patch "
                         "goes to the copy the step before did not read, so consecutive churn steps overlap "
                         "(round 5: 3.30e9 vs 2.89e9 with one copy on one stream; 2 copies on 3 streams 1.65e9, "
-                        "3 on 3 2.44e9, profiles/r5/c5/)")
+                        "3 on 3 2.44e9, profiles/r5/c5/; with stream-aware copies 3 on 3 2.80-2.87e9, 2 on 2 "
+                        "3.32-3.36e9, profiles/r5/c5_stream_copies/)")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     p.add_argument("--cpu-threads", type=int, default=None,
                    help="CPU baseline threads (default: the CPUs this process may use)")

@@ -1491,10 +1491,31 @@ int sync_locked(tm_index *ix, int r0, hipStream_t s) {
 // churn one copy stays hot), else one no batch is reading (it takes the
 // patch without waiting), else the least recently used one.  busy (host
 // lanes per replica) excludes copies whose host lanes are all in use.
-int pick_copy(tm_index *ix, int g, const int *busy) {
+// A device-API batch names its stream s: then a copy whose unfinished
+// readers all run on s counts as idle too (the patch is ordered behind them
+// by the stream itself, no cross-stream wait), preferring the copy s read
+// last, so with as many copies as streams each stream keeps to its own copy
+// under churn.
+int pick_copy(tm_index *ix, int g, const int *busy, hipStream_t s = nullptr, bool by_stream = false) {
     auto ok = [&](int r) { return ix->rep[r].group == g && (!busy || busy[r] < MAX_HOST_LANES); };
     for (int r = 0; r < ix->nrep; r++)
         if (ok(r) && ix->rep[r].applied == ix->patch_seq) return r;
+    if (by_stream) {
+        int pick = -1;
+        uint64_t pick_tick = 0;
+        for (int r = 0; r < ix->nrep; r++) {
+            if (!ok(r)) continue;
+            bool free_here = true;
+            uint64_t mine = 0;   // when stream s last read copy r (0: never)
+            for (auto &l : ix->lanes) {
+                if (l->r != r || !l->used) continue;
+                if (l->s == s) { mine = std::max<uint64_t>(mine, l->tick); continue; }
+                if (hipEventQuery(l->done) == hipErrorNotReady) { free_here = false; break; }
+            }
+            if (free_here && (pick < 0 || mine > pick_tick)) { pick = r; pick_tick = mine; }
+        }
+        if (pick >= 0) return pick;
+    }
     for (int r = 0; r < ix->nrep; r++) {
         if (!ok(r)) continue;
         bool idle = true;
@@ -1973,7 +1994,7 @@ int tm_match_batch_dev_ex(tm_index *ix, uint64_t n, const uint8_t *bytes, const 
     Lane *ln;
     if ((rc = dev_group(ix, grp))) return rc;
     if ((rc = collect_patch(ix))) return rc;
-    const int r = pick_copy(ix, grp, nullptr);
+    const int r = pick_copy(ix, grp, nullptr, s, true);
     ix->rep[r].last_use = ++ix->tick;
     ix->rep[r].batches++;
     if ((rc = dev_lane(ix, s, r, ln))) return rc;
@@ -2521,7 +2542,7 @@ int tm_match_batch32_dev(tm_index *ix, uint64_t n, const uint8_t *bytes, const u
     Lane *ln;
     if ((rc = dev_group(ix, grp))) return rc;
     if ((rc = collect_patch(ix))) return rc;
-    const int r = pick_copy(ix, grp, nullptr);
+    const int r = pick_copy(ix, grp, nullptr, s, true);
     ix->rep[r].last_use = ++ix->tick;
     ix->rep[r].batches++;
     if ((rc = dev_lane(ix, s, r, ln))) return rc;
