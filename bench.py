@@ -106,6 +106,8 @@ def parse():
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-parity", action="store_true")
     p.add_argument("--latency-batches", type=int, default=20)
+    p.add_argument("--pool-streams", action="store_true",
+                   help="run the steps on streams from torch's pool only (default: the current stream and pool ones)")
     p.add_argument("--combine-leaders", type=int, default=None,
                    help="concurrent combined launches of the callers' legs (TM_DEBUG_COMBINE; default: the library's)")
     p.add_argument("--concurrency", type=int, default=8,
@@ -247,7 +249,10 @@ def main():
     # workspace per stream and orders index patches across streams)
     nstreams = 1 if filter_sharded else max(1, a.streams if a.streams is not None else
                                             (copies if a.config == "c5" and copies <= 2 else 3))
-    streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(nstreams - 1)]
+    if a.pool_streams:   # every step on a stream of torch's pool, none on the default stream
+        streams = [torch.cuda.Stream() for _ in range(nstreams)]
+    else:
+        streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(nstreams - 1)]
     split = 1 if (filter_sharded or a.config == "c5") else max(1, min(a.split, nstreams))
     sub = -(-B // split)
     parts = [(j * sub, min(sub, B - j * sub)) for j in range(split)]   # (first topic, topics) of each sub-batch
@@ -789,6 +794,8 @@ def host_bench_lib():
     lib.tmb_pipeline_ex.argtypes = [vp, ctypes.c_int, vp, vp, u64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                     ctypes.c_int, dp]
     lib.tmb_pcie.argtypes = [ctypes.c_int, u64, ctypes.c_int, ctypes.c_int, dp]
+    lib.tmb_noise_start.argtypes = [ctypes.c_int, ctypes.c_int]
+    lib.tmb_noise_stop.argtypes = [dp]
     lib.tmb_bind.argtypes = [vp]
     from emqx_amd import _native
     assert lib.tmb_bind(ctypes.c_void_p(_native.load_library()._handle)) == 0   # the libtmatch this process uses

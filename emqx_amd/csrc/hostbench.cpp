@@ -400,6 +400,49 @@ int tmb_pipeline(tm_index *h, int device, const uint8_t *tb, const uint64_t *to,
     return tmb_pipeline_ex(h, device, tb, to, n, R, nstreams, iters, 0, out);
 }
 
+// Launch noise (a study, tools/profile_walk.py --noise native): a thread that
+// enqueues 4-byte hipMemsetAsync fills (one small kernel dispatch each) on a
+// stream of its own as fast as the queue takes them, until tmb_noise_stop.
+// Does another stream's dispatch rate slow a running walk?
+static std::atomic<bool> g_noise_run{false};
+static std::thread g_noise_th;
+static std::atomic<uint64_t> g_noise_n{0};
+static double g_noise_t0 = 0;
+
+int tmb_noise_start(int device, int mode) {   // mode 0: 4-byte fills; 1: event records (no kernel)
+    if (g_noise_run.exchange(true)) return TM_EINVAL;
+    g_noise_n = 0;
+    g_noise_t0 = now_s();
+    g_noise_th = std::thread([device, mode] {
+        if (hipSetDevice(device) != hipSuccess) return;
+        hipStream_t s = nullptr;
+        uint32_t *d = nullptr;
+        hipEvent_t ev = nullptr;
+        if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess || hipMalloc(&d, 64) != hipSuccess ||
+            hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess)
+            return;
+        while (g_noise_run.load(std::memory_order_relaxed)) {
+            for (int k = 0; k < 64; k++) {
+                if (mode == 1) (void)hipEventRecord(ev, s);
+                else (void)hipMemsetAsync(d, 0, 4, s);
+            }
+            (void)hipStreamSynchronize(s);
+            g_noise_n += 64;
+        }
+        (void)hipEventDestroy(ev);
+        (void)hipStreamDestroy(s);
+        (void)hipFree(d);
+    });
+    return TM_OK;
+}
+
+int tmb_noise_stop(double *per_s) {
+    if (!g_noise_run.exchange(false)) return TM_EINVAL;
+    g_noise_th.join();
+    *per_s = (double)g_noise_n.load() / (now_s() - g_noise_t0);
+    return TM_OK;
+}
+
 // The PCIe ceiling the host-fed pipeline runs against: pinned-host <-> HBM
 // copies of `bytes` in `chunks` pieces, H2D alone, D2H alone, and both
 // directions at once on two streams.  out: [h2d_GBps, d2h_GBps, both_h2d_GBps, both_d2h_GBps]

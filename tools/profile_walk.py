@@ -33,6 +33,11 @@ def main():
     p.add_argument("--small-kernel", default="auto", choices=["auto", "wave", "wave8", "lane"],
                    help="batches <= 65536 topics: the library's default, k_walk_small or k_walk_lane")
     p.add_argument("--phases", action="store_true", help="every batch on the two-phase path (TM_DEBUG_PHASES)")
+    p.add_argument("--noise", default="none", choices=["none", "launch", "host", "native", "events"],
+                   help="during the timed launches, a thread that launches one-element kernels on a stream of its "
+                        "own as fast as it can (launch; native: a C++ thread enqueueing 4-byte fills, libtmbench; events: event records, no kernel), "
+                        "or spins on the host only (host): does another stream's "
+                        "launch rate slow the walk (kernel-boundary cache maintenance)?")
     a = p.parse_args()
     import torch
     from bench import CONFIGS
@@ -99,12 +104,41 @@ def main():
         launch(k)
     torch.cuda.synchronize()
     launch(0)   # unprofiled: the profiled launches are enqueued behind a busy stream
+    import threading
+    stop, nlaunch = threading.Event(), [0]
+
+    def noise():
+        ns = torch.cuda.Stream()
+        x = torch.zeros(1, device=dev)
+        with torch.cuda.stream(ns):
+            while not stop.is_set():
+                if a.noise == "launch":
+                    x.add_(1)
+                nlaunch[0] += 1
+
+    th = threading.Thread(target=noise) if a.noise in ("launch", "host") else None
+    hb = None
+    if a.noise in ("native", "events"):
+        import ctypes
+        from bench import host_bench_lib
+        hb = host_bench_lib()
+        assert hb.tmb_noise_start(0, 1 if a.noise == "events" else 0) == 0
     ix.profile(True)
     t = time.perf_counter()
+    if th:
+        th.start()
     for k in range(a.batches):
         launch(k)
     torch.cuda.synchronize()
     el = time.perf_counter() - t
+    if th:
+        stop.set()
+        th.join()
+        print(f"noise={a.noise}: {nlaunch[0] / el:.0f} loop iterations/s on the other thread", flush=True)
+    if hb is not None:
+        rate = ctypes.c_double()
+        assert hb.tmb_noise_stop(ctypes.byref(rate)) == 0
+        print(f"noise={a.noise}: {rate.value:.0f} operations/s on the other stream", flush=True)
     w, b, n = ix.profile_read()
     st = ix.stats()
     paths = [ix.debug_get(k) for k in (_native.TM_DEBUG_PATH_PHASES, _native.TM_DEBUG_PATH_SMALL,
