@@ -118,10 +118,9 @@ def parse():
                         "device entries, native feeder threads submitting in-place host batches while a syncer thread "
                         "applies deltas (the NIF's deployment, INTEGRATION.md 5); with fewer GPUs than N the entries "
                         "repeat the local device -- a rehearsal, not scaling")
-    p.add_argument("--small-kernel", default="auto", choices=["auto", "wave", "wave8", "lane"],
+    p.add_argument("--small-kernel", default="auto", choices=["auto", "wave", "wave8"],
                    help="the one-launch kernel of batches <= 65536 topics (latency and concurrent-caller legs): "
-                        "the library's default, k_walk_small (16 lanes per topic) or k_walk_lane "
-                        "(TM_DEBUG_SMALL_KERNEL)")
+                        "the library's default, k_walk_small with 16 or 8 lanes per topic (TM_DEBUG_SMALL_KERNEL)")
     return p.parse_args()
 
 
@@ -209,8 +208,7 @@ def main():
     copies = a.copies if a.copies is not None else (2 if a.config == "c5" else 1)
     ix = _native.Index(device=local, hint_keys=len(fs), copies=copies)
     if a.small_kernel != "auto":
-        ix.debug_set(_native.TM_DEBUG_SMALL_KERNEL, {"wave": _native.SMALL_WAVE, "wave8": _native.SMALL_WAVE8,
-                                                     "lane": _native.SMALL_LANE}[a.small_kernel])
+        ix.debug_set(_native.TM_DEBUG_SMALL_KERNEL, {"wave": _native.SMALL_WAVE, "wave8": _native.SMALL_WAVE8}[a.small_kernel])
     chunk = 2_000_000
     for lo in range(0, len(fs), chunk):
         part = fs.slice(lo, min(lo + chunk, len(fs)))
@@ -392,11 +390,11 @@ def main():
     ix.profile(False)
     # the kernel the events bracketed: k_walk_fast (the walk of the two-phase
     # path), or for a batch of <= 65536 topics the one-launch k_walk_small /
-    # k_walk_lane (walk, look-back scan and emit)
+    # (walk, look-back scan and emit in one kernel)
     paths1 = [ix.debug_get(k) for k in (_native.TM_DEBUG_PATH_PHASES, _native.TM_DEBUG_PATH_SMALL,
                                         _native.TM_DEBUG_PATH_LANE)]
     path = max(range(3), key=lambda i: paths1[i] - paths0[i])
-    kernel = ("k_walk_fast", "k_walk_small", "k_walk_lane")[path]
+    kernel = ("k_walk_fast", "k_walk_small", "k_walk_small")[path]
     one_launch = path != 0
     el_t = torch.tensor([el], dtype=torch.float64, device=cdev)
     if world > 1:
@@ -790,6 +788,8 @@ def host_bench_lib():
     lib.tmb_single_ex.argtypes = [vp, u64, vp, vp, u64, ctypes.c_int, ctypes.c_int, dp]
     lib.tmb_callers.argtypes = [vp, ctypes.c_int, u64, vp, vp, u64, ctypes.c_double, ctypes.c_int, dp]
     lib.tmb_callers_ex.argtypes = [vp, ctypes.c_int, u64, vp, vp, u64, ctypes.c_double, ctypes.c_int, ctypes.c_int, dp]
+    lib.tmb_writers.argtypes = [vp, ctypes.c_int, ctypes.c_int, u64, vp, vp, u64, ctypes.c_double, ctypes.c_int,
+                                ctypes.c_int, dp]
     lib.tmb_pipeline.argtypes = [vp, ctypes.c_int, vp, vp, u64, ctypes.c_int, ctypes.c_int, ctypes.c_int, dp]
     lib.tmb_pipeline_ex.argtypes = [vp, ctypes.c_int, vp, vp, u64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                     ctypes.c_int, dp]

@@ -61,7 +61,7 @@ typedef struct {
 } ticket_res;
 
 static ErlNifResourceType *IDX_RT, *TICKET_RT;
-static ERL_NIF_TERM A_OK, A_ERROR, A_FALSE, A_BADARG, A_SYSTEM_LIMIT, A_TRAVERSAL, A_SORTED, A_UNIQUE, A_DEVICE;
+static ERL_NIF_TERM A_OK, A_ERROR, A_FALSE, A_TRUE, A_BADARG, A_SYSTEM_LIMIT, A_TRAVERSAL, A_SORTED, A_UNIQUE, A_DEVICE;
 
 static void idx_dtor(ErlNifEnv *env, void *obj) {
     idx_res *r = obj;
@@ -86,6 +86,7 @@ static int load(ErlNifEnv *env, void **priv, ERL_NIF_TERM info) {
     A_OK = enif_make_atom(env, "ok");
     A_ERROR = enif_make_atom(env, "error");
     A_FALSE = enif_make_atom(env, "false");
+    A_TRUE = enif_make_atom(env, "true");
     A_BADARG = enif_make_atom(env, "badarg");
     A_SYSTEM_LIMIT = enif_make_atom(env, "system_limit");
     A_TRAVERSAL = enif_make_atom(env, "traversal");
@@ -104,19 +105,27 @@ static ERL_NIF_TERM err_term(ErlNifEnv *env, int rc) {
     return enif_make_tuple2(env, A_ERROR, rc == TM_EDEVICE ? A_DEVICE : enif_make_int(env, rc));
 }
 
-/* new(Device | [Device] | {Device | [Device], Copies}) -> {ok, Ref} | {error, Code}
+/* new(Device | [Device] | {Device | [Device], Copies} | {Device | [Device], Copies, VramInputs})
+       -> {ok, Ref} | {error, Code}
    A list: one host image with a replica on each device (tm_create_replicas).
    Copies: copies of the tables per device (tm_options.copies, 1..4): a batch
-   after a delta runs on a copy no batch is reading instead of waiting. */
+   after a delta runs on a copy no batch is reading instead of waiting.
+   VramInputs (default true): pack batch inputs into device memory the host
+   writes through the BAR (tm_host_alloc_ex TM_ALLOC_VRAM); false keeps them in
+   pinned host memory. */
 static ERL_NIF_TERM nif_new(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
-    int dev = -1, devs[8], copies = 1, arity = 0;
+    int dev = -1, devs[8], copies = 1, arity = 0, vram = 1;
     unsigned nd = 0;
     const ERL_NIF_TERM *tup;
     ERL_NIF_TERM spec = argv[0];
     (void)argc;
     if (enif_get_tuple(env, argv[0], &arity, &tup)) {
-        if (arity != 2 || !enif_get_int(env, tup[1], &copies) || copies < 1 || copies > 4)
+        if ((arity != 2 && arity != 3) || !enif_get_int(env, tup[1], &copies) || copies < 1 || copies > 4)
             return enif_make_badarg(env);
+        if (arity == 3) {
+            if (enif_is_identical(tup[2], A_FALSE)) vram = 0;
+            else if (!enif_is_identical(tup[2], A_TRUE)) return enif_make_badarg(env);
+        }
         spec = tup[0];
     }
     if (enif_get_list_length(env, spec, &nd)) {
@@ -133,10 +142,13 @@ static ERL_NIF_TERM nif_new(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[])
     int rc = nd ? tm_create_replicas(&o, devs, nd, &r->h) : tm_create(&o, &r->h);
     if (rc != TM_OK) { r->h = NULL; enif_release_resource(r); return err_term(env, rc); }
     tmn_pool_init(&r->pool, r->h);
-    /* one device: batch inputs in HBM the host writes through the BAR, so the
-       in-place kernel reads no host memory (tm_host_alloc_ex; a set falls back
-       to pinned host memory if the allocation fails) */
-    if (!nd) r->pool.in_flags = TM_ALLOC_VRAM;
+    /* batch inputs in HBM the host writes through the BAR, so the in-place
+       kernel reads no host memory.  Asked of every index (a one-element device
+       list is a one-device index too): tm_host_alloc_ex refuses it
+       for an index spanning several devices or a device whose memory the host
+       cannot map (no large BAR) -- a set then falls back to pinned host
+       memory (tmn_get_ex) and stops asking */
+    r->pool.in_flags = vram ? TM_ALLOC_VRAM : 0;
     ERL_NIF_TERM t = enif_make_resource(env, r);
     enif_release_resource(r);
     return enif_make_tuple2(env, A_OK, t);
@@ -168,7 +180,7 @@ static ERL_NIF_TERM nif_apply(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[
         unsigned op, v, k;
         if (!enif_get_tuple(env, h, &ar, &e) || ar != 4 || !enif_get_uint(env, e[0], &op) || op > 1 ||
             !enif_inspect_binary(env, e[1], &bins[i]) || !enif_get_uint(env, e[2], &v) ||
-            !enif_get_uint(env, e[3], &k) || k > 2) {
+            !enif_get_uint(env, e[3], &k) || (k > 2 && k != (TM_KEY_WORDS | TM_KEY_ESCAPED))) {
             res = enif_make_badarg(env);
             goto out;
         }

@@ -26,15 +26,18 @@ EXPORTS = ("tm_create", "tm_destroy", "tm_apply_deltas", "tm_sync", "tm_match_ba
            "tm_stream_release", "tm_match_batch_ex", "tm_match_batch_dev_ex", "tm_sort_segments",
            "tm_matches_filter", "tm_apply_deltas_ex", "tm_read_begin", "tm_read_end", "tm_epoch",
            "tm_create_replicas", "tm_replica_stats", "tm_debug_set", "tm_debug_get", "tm_match_batch32_ex",
-           "tm_match_batch32_dev", "tm_matches_filter_ex", "tm_host_alloc_ex")
+           "tm_match_batch32_dev", "tm_matches_filter_ex", "tm_host_alloc_ex", "tm_commit")
 TM_ALLOC_VRAM = 1
 TM_DEBUG_LB_SPINS, TM_DEBUG_LB_FAIL_BLOCK, TM_DEBUG_LB_LAUNCHES, TM_DEBUG_PHASES = 1, 2, 3, 4
 TM_DEBUG_FAILED_BATCHES, TM_DEBUG_RETRIED_BATCHES = 5, 6
 TM_DEBUG_PATH_PHASES, TM_DEBUG_PATH_SMALL, TM_DEBUG_PATH_LANE = 7, 8, 9
 TM_DEBUG_SMALL_KERNEL = 10
-SMALL_AUTO, SMALL_WAVE, SMALL_LANE, SMALL_WAVE8 = 0, 1, 2, 3
+SMALL_AUTO, SMALL_WAVE, SMALL_WAVE8 = 0, 1, 3   # (2: round 5's lane kernel, removed)
 TM_DEBUG_COMBINE, TM_DEBUG_COMBINED_LAUNCHES, TM_DEBUG_COMBINED_BATCHES = 12, 13, 14
 TM_DEBUG_WIDE_NODES, TM_DEBUG_DENSE_WIDE = 15, 16
+TM_DEBUG_CMB_GATHER, TM_DEBUG_CMB_LAND = 17, 18
+TM_DEBUG_COMMITS, TM_DEBUG_COMMIT_WAITS, TM_DEBUG_COMMIT_FORCED = 19, 20, 21
+TM_DEBUG_SMALL_TICKET = 22
 
 
 class NativeUnavailable(RuntimeError):
@@ -103,6 +106,7 @@ def load_library(path: Path | None = None):
         "tm_match_batch_dev_ex": (i32, [vp, u64, vp, vp, vp, vp, u64, vp, u32, vp, vp]),
         "tm_sort_segments": (i32, [vp, u64, vp, vp, u64, u32, vp, vp]),
         "tm_apply_deltas_ex": (i32, [vp, u64, vp, vp, vp, vp, vp, C.POINTER(u64)]),
+        "tm_commit": (i32, [vp, u64, vp, vp, vp, vp, vp, C.POINTER(u64)]),
         "tm_read_begin": (i32, [vp, C.POINTER(u64)]),
         "tm_read_end": (i32, [vp, u64]),
         "tm_epoch": (i32, [vp, C.POINTER(u64), C.POINTER(u64)]),
@@ -195,7 +199,9 @@ class Index:
 
     # ---- deltas
     def apply(self, ops: np.ndarray, blob: np.ndarray, offs: np.ndarray, values: np.ndarray,
-              flags: np.ndarray | None = None):
+              flags: np.ndarray | None = None, commit: bool = False):
+        """tm_apply_deltas_ex, or (commit) tm_commit: published on a table copy no
+        batch is reading, so no batch waits for the patch.  -> the delta epoch."""
         ops = np.ascontiguousarray(ops, dtype=np.uint8)
         offs = np.ascontiguousarray(offs, dtype=np.uint64)
         values = np.ascontiguousarray(values, dtype=np.uint32)
@@ -203,8 +209,8 @@ class Index:
         if flags is not None:
             flags = np.ascontiguousarray(flags, dtype=np.uint8)
         e = C.c_uint64()
-        self._check(self._lib.tm_apply_deltas_ex(self._h, len(ops), _ptr(ops), _ptr(blob), _ptr(offs),
-                                                 _ptr(values), _ptr(flags), C.byref(e)))
+        fn = self._lib.tm_commit if commit else self._lib.tm_apply_deltas_ex
+        self._check(fn(self._h, len(ops), _ptr(ops), _ptr(blob), _ptr(offs), _ptr(values), _ptr(flags), C.byref(e)))
         return e.value
 
     # ---- reader epochs (include/tmatch.h "Reader epochs")

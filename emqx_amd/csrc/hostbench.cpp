@@ -9,6 +9,12 @@
 //                  thread applying subscribe/unsubscribe deltas, for a while:
 //                  aggregate topics/s and per-batch p50 / p99 -- the reference's
 //                  concurrent publishers (emqx_broker.erl:293-298)
+//   tmb_writers    route writes one key at a time from many writer threads,
+//                  group-committed by one mirror thread (emqx_router_gpu's
+//                  process: every queued sync request in ONE tm_apply_deltas),
+//                  while matcher threads run NIF-shaped batches: writes/s,
+//                  write latency, the matchers' rate and p99, and each
+//                  writer's read of its own write
 //   tmb_pipeline   host-fed throughput: batches of topics in pinned host memory,
 //                  H2D copy, match, D2H of offsets and values, overlapped on
 //                  several streams -- the rate a caller that hands over host
@@ -19,7 +25,11 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <cstring>
+#include <deque>
+#include <mutex>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -37,6 +47,8 @@ int (*match_batch_dev)(tm_index *, uint64_t, const uint8_t *, const uint64_t *, 
                        uint8_t *, void *);
 int (*apply_deltas)(tm_index *, uint64_t, const uint8_t *, const uint8_t *, const uint64_t *, const uint32_t *,
                     const uint8_t *);
+int (*commit)(tm_index *, uint64_t, const uint8_t *, const uint8_t *, const uint64_t *, const uint32_t *,
+              const uint8_t *, uint64_t *);   // optional (ABI 1.10)
 int (*stream_release)(tm_index *, void *);
 int (*match_batch32)(tm_index *, uint64_t, const uint8_t *, const uint32_t *, uint32_t *, uint32_t *, uint64_t,
                      uint8_t *, uint32_t, uint32_t *);
@@ -146,6 +158,7 @@ int tmb_bind(void *lib) {
     api::match_batch = reinterpret_cast<decltype(api::match_batch)>(dlsym(lib, "tm_match_batch"));
     api::match_batch_dev = reinterpret_cast<decltype(api::match_batch_dev)>(dlsym(lib, "tm_match_batch_dev"));
     api::apply_deltas = reinterpret_cast<decltype(api::apply_deltas)>(dlsym(lib, "tm_apply_deltas"));
+    api::commit = reinterpret_cast<decltype(api::commit)>(dlsym(lib, "tm_commit"));
     api::stream_release = reinterpret_cast<decltype(api::stream_release)>(dlsym(lib, "tm_stream_release"));
     api::match_batch32 = reinterpret_cast<decltype(api::match_batch32)>(dlsym(lib, "tm_match_batch32_ex"));
     api::match_batch32_dev = reinterpret_cast<decltype(api::match_batch32_dev)>(dlsym(lib, "tm_match_batch32_dev"));
@@ -263,6 +276,155 @@ int tmb_callers_ex(tm_index *h, int nthreads, uint64_t n, const uint8_t *tb, con
 int tmb_callers(tm_index *h, int nthreads, uint64_t n, const uint8_t *tb, const uint64_t *to, uint64_t cap,
                 double seconds, int churn_ops, double *out) {
     return tmb_callers_ex(h, nthreads, n, tb, to, cap, seconds, churn_ops, 0, out);
+}
+
+// Route writes through a group-committing mirror.  The
+// reference runs route writes in parallel in up to schedulers x 2 broker-pool
+// workers (emqx_broker_sup.erl:36; emqx_broker.erl:778-808 -> emqx_router.erl
+// :193-196, 492-493); with the device mirror each write also waits until the
+// mirror has it (the read-your-writes hook, src/emqx_router_gpu.erl
+// filters_written/1), and the mirror is ONE process: it takes every sync
+// request queued when it wakes and ships them as ONE delta batch
+// (mirror_batch/2), then replies to each.  Here: `nwriters` writer threads, each
+// subscribing and unsubscribing its own keys one at a time (a binary key
+// "bench/writer/<w>/<k>" -- the exact-topic path -- alternating with the word
+// list "bench/writer/<w>/<k>/+"), one mirror thread committing the queue, and
+// `nmatch` matcher threads running 4k-topic batches as the NIF does (u32
+// offsets, inputs in TM_ALLOC_VRAM memory, through the combiner).  check:
+// after each insert commit the writer matches its own topic (a one-topic
+// batch) and counts a miss if its value is absent -- a publish right after the
+// SUBACK must reach the subscriber.  commit: the mirror ships each group with
+// tm_commit (published on a table copy no batch is reading), else with
+// tm_apply_deltas.
+// out: [writes_per_s, write_p50_ms, write_p99_ms, commits_per_s, topics_per_s, match_p50_ms, match_p99_ms,
+//       ryw_checks, ryw_misses, seconds]
+int tmb_writers(tm_index *h, int nwriters, int nmatch, uint64_t n, const uint8_t *tb, const uint64_t *to, uint64_t cap,
+                double seconds, int check, int commit, double *out) {
+    if (commit && !api::commit) return TM_EINVAL;
+    struct Req { uint8_t op; std::string key; uint32_t val; bool done = false; };
+    std::mutex mu;
+    std::condition_variable cv_mirror, cv_done;
+    std::deque<Req *> q;
+    std::atomic<bool> stop{false};
+    bool mstop = false;   // (under mu) the mirror ends once every writer has
+    std::atomic<int> err{0};
+    std::atomic<uint64_t> commits{0}, ryw_checks{0}, ryw_miss{0};
+    std::vector<Caller> cs(nmatch);
+    for (int k = 0; k < nmatch; k++) {
+        int rc = cs[k].init(h, n, tb, to, (uint64_t)k * n, cap);
+        if (rc) return rc;
+        cs[k].mode = 4;
+        if (cs[k].to_vram() == TM_OK) cs[k].mode = 5;
+        if ((rc = cs[k].run())) return rc;
+    }
+    std::vector<std::vector<double>> mlat(nmatch), wlat(nwriters);
+    std::vector<std::thread> th;
+    // the mirror process
+    th.emplace_back([&] {
+        std::vector<uint8_t> ops, blob, kinds;
+        std::vector<uint64_t> offs;
+        std::vector<uint32_t> vals;
+        std::vector<Req *> batch;
+        std::unique_lock<std::mutex> lk(mu);
+        for (;;) {
+            cv_mirror.wait(lk, [&] { return !q.empty() || mstop; });
+            if (q.empty()) break;
+            batch.assign(q.begin(), q.end());
+            q.clear();
+            lk.unlock();
+            ops.clear(); blob.clear(); vals.clear(); kinds.clear(); offs.assign(1, 0);
+            for (Req *r : batch) {
+                ops.push_back(r->op);
+                blob.insert(blob.end(), r->key.begin(), r->key.end());
+                offs.push_back(blob.size());
+                vals.push_back(r->val);
+            }
+            const int rc = commit ? api::commit(h, batch.size(), ops.data(), blob.data(), offs.data(), vals.data(), nullptr,
+                                                nullptr)
+                                  : api::apply_deltas(h, batch.size(), ops.data(), blob.data(), offs.data(), vals.data(),
+                                                      nullptr);
+            if (rc) err = -1;
+            commits++;
+            lk.lock();
+            for (Req *r : batch) r->done = true;
+            cv_done.notify_all();
+        }
+    });
+    for (int k = 0; k < nmatch; k++)
+        th.emplace_back([&, k] {
+            while (!stop.load(std::memory_order_relaxed)) {
+                const double a = now_s();
+                const int rc = cs[k].run();
+                if (rc) { err = rc; break; }
+                mlat[k].push_back((now_s() - a) * 1e3);
+            }
+        });
+    for (int w = 0; w < nwriters; w++)
+        th.emplace_back([&, w] {
+            // the one-topic batch a writer publishes after its subscribe (pinned: in place)
+            uint8_t *pb = nullptr; uint64_t *po = nullptr, *ph = nullptr; uint32_t *pv = nullptr; uint8_t *pe = nullptr;
+            if (check && (api::host_alloc(h, 256, (void **)&pb) || api::host_alloc(h, 16, (void **)&po) ||
+                          api::host_alloc(h, 16, (void **)&ph) || api::host_alloc(h, 4 * 4096, (void **)&pv) ||
+                          api::host_alloc(h, 16, (void **)&pe))) { err = -2; return; }
+            Req r;
+            for (uint64_t k = 0; !stop.load(std::memory_order_relaxed); k++) {
+                const std::string topic = "bench/writer/" + std::to_string(w) + "/" + std::to_string(k % 64);
+                const bool words = (k / 64) & 1;   // the word-list key "<topic>/+" every other sweep
+                r.key = words ? topic + "/+" : topic;
+                r.val = 0xE0000000u + (uint32_t)w * 64 + (uint32_t)(k % 64);
+                for (int op = 1; op >= 0; op--) {   // subscribe, (publish,) unsubscribe
+                    r.op = (uint8_t)op;
+                    r.done = false;
+                    const double a = now_s();
+                    {
+                        std::unique_lock<std::mutex> lk(mu);
+                        q.push_back(&r);
+                        cv_mirror.notify_one();
+                        cv_done.wait(lk, [&] { return r.done; });
+                    }
+                    wlat[w].push_back((now_s() - a) * 1e3);
+                    if (op == 1 && check) {
+                        const std::string t = words ? topic + "/x" : topic;
+                        memcpy(pb, t.data(), t.size());
+                        po[0] = 0; po[1] = t.size();
+                        if (api::match_batch(h, 1, pb, po, ph, pv, 4096, pe)) { err = -3; break; }
+                        bool seen = false;
+                        for (uint64_t i = ph[0]; i < ph[1] && i < 4096; i++) seen |= pv[i] == r.val;
+                        ryw_checks++;
+                        if (!seen) ryw_miss++;
+                    }
+                }
+            }
+            for (void *p : {(void *)pb, (void *)po, (void *)ph, (void *)pv, (void *)pe}) if (p) api::host_free(h, p);
+        });
+    const double t0 = now_s();
+    std::this_thread::sleep_for(std::chrono::duration<double>(seconds));
+    stop = true;
+    for (size_t i = 1; i < th.size(); i++) th[i].join();
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        mstop = true;
+        cv_mirror.notify_all();
+    }
+    th[0].join();
+    const double el = now_s() - t0;
+    for (auto &c : cs) c.fini();
+    if (err) return err;
+    std::vector<double> wa, ma;
+    for (auto &v : wlat) wa.insert(wa.end(), v.begin(), v.end());
+    uint64_t nb = 0;
+    for (auto &v : mlat) { nb += v.size(); ma.insert(ma.end(), v.begin() + std::min<size_t>(2, v.size()), v.end()); }
+    out[0] = wa.size() / el;
+    out[1] = pct(wa, 50);
+    out[2] = pct(wa, 99);
+    out[3] = commits / el;
+    out[4] = nb * (double)n / el;
+    out[5] = pct(ma, 50);
+    out[6] = pct(ma, 99);
+    out[7] = (double)ryw_checks;
+    out[8] = (double)ryw_miss;
+    out[9] = el;
+    return TM_OK;
 }
 
 // Host-fed pipeline.  R batches of n topics (batch k = topics [k n, (k + 1) n)

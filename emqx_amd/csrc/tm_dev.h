@@ -41,7 +41,7 @@ constexpr int DEEP_LANES = 64;   // lanes of the global-scratch (deep / overflow
 enum { L_MID = 0, L_DEEP = 1, L_OVF_MID = 2, L_OVF_DEEP = 3, L_COUNT = 4 };
 
 // Per-batch device scratch (grow-only, owned by the index).
-// The one-launch kernels' (k_walk_small, k_walk_lane) look-back word of a
+// The one-launch kernel's (k_walk_small) look-back word of a
 // block: launch tag (19 bits), state (LB_AGG: its own hit total; LB_INCL: the
 // total of it and every block before it; LB_FAIL: its wait expired, or a
 // predecessor's did -- every later block fails too) and the value (42 bits)
@@ -69,6 +69,7 @@ constexpr uint32_t LB_STRIDE = 1;         // 8-B words between consecutive block
 struct LbCtl {
     uint32_t spins;        // the bound (LB_SPINS; tm_debug_set can lower it)
     uint32_t fail_block;   // test hook: this block acts as if its wait expired (NONE: off)
+    uint32_t ticket;       // 1: k_walk_small's blocks take a start-order ticket (TM_DEBUG_SMALL_TICKET)
 };
 
 constexpr int SMALL_SEGS = 16;   // host batches one combined small launch can carry (SmallSegs)
@@ -80,7 +81,7 @@ struct Workspace {
     uint32_t *lists;      // [(L_COUNT + 1) * n] topic lists (the last one: long segments to sort)
     uint32_t *list_n;     // [L_COUNT] list lengths, [L_COUNT] reset ticket, [L_COUNT + 1] scan ticket,
                           // [L_COUNT + 2] long-segment count, [L_COUNT + 3] its reset ticket,
-                          // [LS_TICK + k] k_walk_lane's start-order ticket of segment k (zero between launches)
+                          // [SM_TICK + k] k_walk_small's start-order ticket of segment k (zero between launches)
     uint64_t *blk;        // [n / TILE + 4] tile hit totals (zero between batches)
     uint64_t *sup;        // [n / (TILE * SUP) + 4] superblock hit totals (zero between batches; in blk's allocation)
     uint32_t *deep_wid;   // [DEEP_LANES * MAX_LEVELS]
@@ -98,8 +99,8 @@ struct Workspace {
 
 constexpr int TILE = 256;    // topics per walk block = per scan tile = per emit block
 constexpr int SUP = 64;      // tiles per superblock (Workspace::sup)
-constexpr int LS_TICK = L_COUNT + 4;      // Workspace::list_n words: k_walk_lane's tickets, one per segment
-constexpr int LIST_SLOTS = LS_TICK + SMALL_SEGS;   // Workspace::list_n entries
+constexpr int SM_TICK = L_COUNT + 4;     // Workspace::list_n words: k_walk_small's tickets, one per segment
+constexpr int LIST_SLOTS = SM_TICK + SMALL_SEGS;   // Workspace::list_n entries
 constexpr int HINT_FAIL = L_COUNT + 1;    // Workspace::hint_* word of the fail flag
 constexpr int HINT_WORDS = L_COUNT + 2;
 constexpr int SM_TOPICS = 16;             // topics per block of the one-launch small-batch path
@@ -119,30 +120,27 @@ hipError_t launch_match_phase2(const DevIndex &ix, const Workspace &ws, uint64_t
                                const uint64_t *offs, uint64_t *hit_offs, uint32_t *out, uint64_t cap,
                                hipStream_t s);
 // The whole batch in ONE launch when the index allows it: up to SMALL_TOPICS
-// topics (small_path_ok: the fallback store of k_walk_small holds the
-// index's depth) on k_walk_lane (one lane per topic, lane_path_ok: a shallow
-// index without '#'-not-last keys) or k_walk_small (16 lanes per topic); the
-// two phases otherwise (or when `phases` forces them: tests of that path).
-// `tag` must differ between consecutive launches on one workspace (the
-// one-launch look-back scan tells its own blocks' words from older ones by
-// it).  A one-launch batch whose look-back failed flags its topics err 4 and
-// sets ws.hint_h[HINT_FAIL].
+// topics (small_path_ok: the fallback store of k_walk_small holds the index's
+// depth) on k_walk_small (16 or 8 lanes per topic); the two phases otherwise
+// (or when `phases` forces them: tests of that path).  `tag` must differ
+// between consecutive launches on one workspace (the one-launch look-back scan
+// tells its own blocks' words from older ones by it).  A one-launch batch whose
+// look-back failed flags its topics err 4 and sets ws.hint_h[HINT_FAIL].
 bool small_path_ok(const DevIndex &ix, uint64_t n);
 bool one_launch_ok(const DevIndex &ix);
-bool lane_path_ok(const DevIndex &ix);   // k_walk_lane's condition
-// which one-launch kernel (small_kind): the default, k_walk_small with 16 /
-// 8 lanes per topic, k_walk_lane (one lane per topic, where lane_path_ok)
-enum { SMALL_AUTO = 0, SMALL_WAVE = 1, SMALL_LANE = 2, SMALL_WAVE8 = 3 };
-bool small_lane(const DevIndex &ix, int small_kind);
-enum { PATH_PHASES = 0, PATH_SMALL = 1, PATH_LANE = 2, PATH_COUNT = 3 };   // *path of launch_match
+bool lite_path_ok(const DevIndex &ix);   // k_walk_small<8>'s LITE fallback store holds every topic
+// which one-launch kernel (small_kind): the default, k_walk_small with 16 / 8
+// lanes per topic.  (2 named round 5's k_walk_lane, removed in round 6.)
+enum { SMALL_AUTO = 0, SMALL_WAVE = 1, SMALL_WAVE8 = 3 };
+enum { PATH_PHASES = 0, PATH_SMALL = 1, PATH_LANE = 2, PATH_COUNT = 3 };   // *path of launch_match (PATH_LANE: retired, 0)
 hipError_t launch_match(const DevIndex &ix, const Workspace &ws, uint64_t n, const uint8_t *bytes,
                         const uint64_t *offs, uint64_t *hit_offs, uint8_t *err, uint32_t *out, uint64_t cap,
                         uint32_t tag, LbCtl lb, bool phases, int small_kind, hipStream_t s,
                         hipEvent_t ev_walk0 = nullptr, hipEvent_t ev_walk1 = nullptr, int *path = nullptr);
 // Several host batches in ONE one-launch small kernel (the host's combiner,
 // tm_host.cpp small_combined): segment k owns the launch's blocks
-// [block0, next block0), its own inputs and outputs, its own look-back region
-// and (k_walk_lane) its own ticket word; a launch holds at most SMALL_SEGS
+// [block0, next block0), its own inputs and outputs and its own look-back
+// region; a launch holds at most SMALL_SEGS
 // segments of at most SMALL_TOPICS topics together.  Offsets are uint64_t or
 // uint32_t for the whole launch.
 struct SmallSeg {
@@ -152,6 +150,18 @@ struct SmallSeg {
 struct SmallSegs { uint32_t count, pad; SmallSeg s[SMALL_SEGS]; };
 hipError_t launch_small_segs(const DevIndex &ix, const Workspace &ws, const SmallSegs &sg, bool u32, uint32_t tag,
                              LbCtl lb, int small_kind, hipStream_t s, int *path = nullptr);
+// The combiner's results landed from HBM (TM_DEBUG_CMB_LAND): segment k's hit
+// offsets (n + 1 u32), flags (n) and values (min(hit[n], cap) u32), written by
+// the launch into the lane's HBM arena, copied to the callers' buffers (mapped
+// pinned host memory) in ONE kernel -- 16 B per lane where both sides allow it,
+// whole lines per wave instead of the walk's scattered small PCIe writes.
+struct LandSeg {
+    const uint32_t *hit; const uint8_t *err; const uint32_t *vals;
+    uint32_t *dhit; uint8_t *derr; uint32_t *dvals;
+    uint64_t cap; uint32_t n, pad;
+};
+struct LandSegs { uint32_t count, pad; LandSeg s[SMALL_SEGS]; };
+hipError_t launch_land(const LandSegs &ls, hipStream_t s);
 // The one-launch small batch with 32-bit offsets in and out (hipErrorInvalidValue
 // if small_path_ok refuses the batch), and the 32 <-> 64-bit offset copies
 hipError_t launch_match32(const DevIndex &ix, const Workspace &ws, uint64_t n, const uint8_t *bytes,

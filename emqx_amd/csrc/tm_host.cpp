@@ -22,6 +22,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <map>
 #include <unordered_map>
 #include <unordered_set>
@@ -114,6 +115,7 @@ struct Lane {
     uint32_t *pin_vals = nullptr, *pin_vals_dev = nullptr; uint64_t pin_vals_cap = 0;
     uint32_t *d_vals = nullptr; uint64_t d_vals_cap = 0;   // sorted output: values sorted in HBM first
     uint64_t *d_o64 = nullptr, *d_h64 = nullptr; uint64_t d_o64_cap = 0, d_h64_cap = 0;   // 32-bit device API: widened offsets
+    uint8_t *d_land = nullptr; uint64_t d_land_cap = 0;   // combined launches' outputs in HBM (TM_DEBUG_CMB_LAND)
 };
 
 // Patch log: a ring of the last PATCH_RING patches (numbered 1, 2, ... in the
@@ -225,6 +227,15 @@ struct tm_index {
     uint64_t uploads = 0, patch_bytes = 0;
 
     PatchSlot patch[PATCH_RING]; uint64_t patch_seq = 0;   // patches collected so far
+    // Patches every batch queued from now on must see (<= patch_seq): a
+    // collect by a batch publishes what it collects at once; tm_commit
+    // publishes its patch only once a copy no batch is reading holds it.
+    uint64_t pub_seq = 0;
+    int serving[MAX_REPLICAS];       // per group: the copy tm_commit last published on (-1: none)
+    // tm_commit's image changes not yet published: batches do not collect
+    // them meanwhile (they were not applied before those batches were queued)
+    std::atomic<int> img_hold{0};
+    std::atomic<uint64_t> commits{0}, commit_waits{0}, commit_forced{0};
     DevIndex view[MAX_REPLICAS];     // each replica's device view as of the last collect_patch
 
     std::vector<std::unique_ptr<Lane>> lanes;
@@ -253,7 +264,8 @@ struct tm_index {
     // test hooks (tm_debug_set, under mu): the look-back control of the next
     // dbg_lb_launches one-launch batches, and the two-phase path forced for
     // large batches
-    LbCtl dbg_lb{LB_SPINS, NONE};
+    LbCtl dbg_lb{LB_SPINS, NONE, 0};
+    uint32_t small_ticket = 0;      // TM_DEBUG_SMALL_TICKET: k_walk_small's blocks take start-order tickets
     uint64_t dbg_lb_launches = 0;
     bool dbg_phases = false;        // TM_DEBUG_PHASES: small batches on the two-phase path too (tests)
     int small_kind = SMALL_AUTO;    // TM_DEBUG_SMALL_KERNEL: which one-launch kernel takes small batches
@@ -264,10 +276,16 @@ struct tm_index {
     // each take what is queued and run it as ONE k_walk_small launch
     // (TM_DEBUG_COMBINE: 0 = every batch its own launch)
     std::mutex cmb_mu;
-    std::condition_variable cmb_cv;
+    std::condition_variable cmb_gcv;  // a gathering leader waits here for more batches
     std::deque<struct SmallReq *> cmb_q;
-    int cmb_running = 0;
+    int cmb_running = 0;              // launches being prepared or in flight (at most cmb_leaders)
+    int cmb_inflight = 0;             // host batches those launches carry
+    int cmb_gathering = 0;            // leaders waiting in the gather window
+    int cmb_hw = 0;                   // recent high-water mark of queued + in-flight batches
+    uint64_t cmb_hw_ns = 0;           // when it was last reached
     std::atomic<int> cmb_leaders{CMB_LEADERS};
+    std::atomic<int> cmb_gather_us{0};   // TM_DEBUG_CMB_GATHER
+    std::atomic<int> cmb_land{0};        // TM_DEBUG_CMB_LAND
     std::atomic<uint64_t> cmb_launches{0}, cmb_batches{0};
 };
 
@@ -1326,9 +1344,13 @@ int next_tag(tm_index *ix, Lane &ln, hipStream_t s, uint32_t &tag) {
 // the look-back control of the next launch (caller holds ix->mu): the
 // default bound, or the test hook's for the next dbg_lb_launches launches
 LbCtl next_lb(tm_index *ix) {
-    if (!ix->dbg_lb_launches) return LbCtl{LB_SPINS, NONE};
-    ix->dbg_lb_launches--;
-    return ix->dbg_lb;
+    LbCtl c{LB_SPINS, NONE, 0};
+    if (ix->dbg_lb_launches) {
+        ix->dbg_lb_launches--;
+        c = ix->dbg_lb;
+    }
+    c.ticket = ix->small_ticket;
+    return c;
 }
 
 // did the lane's last one-launch batch fail its look-back (err 4, the fail
@@ -1400,13 +1422,16 @@ DevIndex dev_view_build(tm_index *ix, int r);
 // cached device views (caller holds ix->mu; takes ix->img, and only when a
 // delta was applied since the last call); nothing reaches a device here but
 // whole-table uploads
-int collect_patch(tm_index *ix) {
-    if (ix->view_ok && !ix->img_dirty.load(std::memory_order_acquire)) return TM_OK;
+int collect_patch(tm_index *ix, bool commit = false) {
+    if (ix->view_ok && !commit &&
+        (!ix->img_dirty.load(std::memory_order_acquire) || ix->img_hold.load(std::memory_order_acquire) > 0))
+        return TM_OK;
     std::lock_guard<std::mutex> gi(ix->img);
     ix->img_dirty.store(false, std::memory_order_relaxed);   // (an apply from here on sets it again)
     int rc = collect_patch_locked(ix);
     for (int r = 0; r < ix->nrep; r++) ix->view[r] = dev_view_build(ix, r);
     ix->view_ok = rc == TM_OK;
+    if (!commit) ix->pub_seq = ix->patch_seq;   // a batch's collect: published at once
     return rc;
 }
 
@@ -1481,7 +1506,7 @@ int collect_patch_locked2(tm_index *ix) {
 int sync_locked(tm_index *ix, int r0, hipStream_t s) {
     int rc;
     if ((rc = collect_patch(ix))) return rc;
-    if ((rc = bring_up(ix, r0, ix->patch_seq, s))) return rc;
+    if ((rc = bring_up(ix, r0, ix->pub_seq, s))) return rc;
     HIPCHK(ix, hipSetDevice(ix->rep[r0].device));
     return TM_OK;
 }
@@ -1498,8 +1523,10 @@ int sync_locked(tm_index *ix, int r0, hipStream_t s) {
 // under churn.
 int pick_copy(tm_index *ix, int g, const int *busy, hipStream_t s = nullptr, bool by_stream = false) {
     auto ok = [&](int r) { return ix->rep[r].group == g && (!busy || busy[r] < MAX_HOST_LANES); };
+    const int sv = ix->serving[g];   // the copy tm_commit last published on: fresh, its readers' hot set
+    if (sv >= 0 && ok(sv) && ix->rep[sv].applied >= ix->pub_seq) return sv;
     for (int r = 0; r < ix->nrep; r++)
-        if (ok(r) && ix->rep[r].applied == ix->patch_seq) return r;
+        if (ok(r) && ix->rep[r].applied >= ix->pub_seq) return r;
     if (by_stream) {
         int pick = -1;
         uint64_t pick_tick = 0;
@@ -1568,7 +1595,7 @@ void free_workspace(Workspace &w) {
 
 void free_lane(Lane &l) {
     free_workspace(l.w);
-    void *dv[] = {l.d_in, l.d_res, l.d_vals, l.d_o64, l.d_h64};
+    void *dv[] = {l.d_in, l.d_res, l.d_vals, l.d_o64, l.d_h64, l.d_land};
     for (void *p : dv) if (p) (void)hipFree(p);
     void *pins[] = {l.pin_in, l.pin_out, l.pin_vals};
     for (void *p : pins) if (p) (void)hipHostFree(p);
@@ -1793,7 +1820,7 @@ int drain_lanes(tm_index *ix) {
 
 extern "C" {
 
-uint32_t tm_abi_version(void) { return (1u << 16) | 9u; }
+uint32_t tm_abi_version(void) { return (1u << 16) | 10u; }
 
 const char *tm_last_error(tm_index *) { return g_last_error.c_str(); }
 
@@ -1806,6 +1833,7 @@ int tm_create_replicas(const tm_options *opts, const int32_t *devices, uint32_t 
     tm_index *ix = new (std::nothrow) tm_index();
     if (!ix) return fail(nullptr, TM_ENOMEM, "tm_create: out of host memory");
     ix->nrep = (int)(n * copies);
+    for (int g = 0; g < MAX_REPLICAS; g++) ix->serving[g] = -1;
     ix->ngroups = (int)n;
     hipError_t e = hipSuccess;
     for (uint32_t r = 0; r < n * copies && e == hipSuccess; r++) {
@@ -1939,6 +1967,70 @@ int tm_apply_deltas_ex(tm_index *ix, uint64_t n, const uint8_t *ops, const uint8
 int tm_apply_deltas(tm_index *ix, uint64_t n, const uint8_t *ops, const uint8_t *fb, const uint64_t *fo,
                     const uint32_t *values, const uint8_t *key_flags) {
     return tm_apply_deltas_ex(ix, n, ops, fb, fo, values, key_flags, nullptr);
+}
+
+// tm_commit (include/tmatch.h): the deltas reach the host image while
+// batches are held off collecting them (img_hold), then -- under the device
+// lock -- one patch is collected and applied to a copy of each group that no
+// batch is reading, which becomes the group's serving copy, and only then is
+// the patch published (pub_seq): batches queued afterwards read that copy,
+// and no batch ever waits on the GPU for this patch.  While every copy of a
+// group has readers the committer waits (the lock released) for one to
+// drain, up to COMMIT_WAIT; past it -- or with one copy per group -- the
+// patch is published as tm_apply_deltas' are (batches take it in stream
+// order, behind the batches reading that copy).
+constexpr auto COMMIT_WAIT = std::chrono::milliseconds(20);
+
+int tm_commit(tm_index *ix, uint64_t n, const uint8_t *ops, const uint8_t *fb, const uint64_t *fo,
+              const uint32_t *values, const uint8_t *key_flags, uint64_t *out_epoch) {
+    if (!ix) return fail(nullptr, TM_EINVAL, "tm_commit: null handle");
+    ix->img_hold.fetch_add(1, std::memory_order_acq_rel);
+    struct Unhold {
+        tm_index *ix;
+        ~Unhold() { ix->img_hold.fetch_sub(1, std::memory_order_acq_rel); }
+    } unhold{ix};
+    int rc = tm_apply_deltas_ex(ix, n, ops, fb, fo, values, key_flags, out_epoch);
+    if (rc || !n) return rc;
+    std::unique_lock<std::mutex> g(ix->mu);
+    if ((rc = collect_patch(ix, true))) return rc;
+    const uint64_t q = ix->patch_seq;
+    if (ix->pub_seq >= q) return TM_OK;   // (nothing to ship: the deltas changed no device word)
+    ix->commits++;
+    const auto t0 = std::chrono::steady_clock::now();
+    bool done[MAX_REPLICAS] = {}, waited = false;
+    int left = ix->ngroups;
+    for (;;) {
+        const bool late = std::chrono::steady_clock::now() - t0 > COMMIT_WAIT;
+        for (int gi = 0; gi < ix->ngroups; gi++) {
+            if (done[gi]) continue;
+            int pick = -1, copies = 0;
+            for (int r = 0; r < ix->nrep; r++) {
+                if (ix->rep[r].group != gi) continue;
+                copies++;
+                bool idle = true;
+                for (auto &l : ix->lanes)
+                    if (l->r == r && l->used && hipEventQuery(l->done) == hipErrorNotReady) { idle = false; break; }
+                if (idle && (pick < 0 || ix->rep[r].applied > ix->rep[pick].applied)) pick = r;
+            }
+            if (pick < 0 && copies > 1 && !late) continue;   // wait for a copy to drain
+            if (pick >= 0) {
+                if ((rc = bring_up(ix, pick, q, ix->rep[pick].ps))) return rc;
+                ix->serving[gi] = pick;
+            } else {
+                ix->commit_forced++;   // published below; the group's batches take the patch themselves
+            }
+            done[gi] = true;
+            left--;
+        }
+        if (!left) break;
+        waited = true;
+        g.unlock();
+        std::this_thread::sleep_for(std::chrono::microseconds(2));
+        g.lock();
+    }
+    if (waited) ix->commit_waits++;
+    if (ix->pub_seq < q) ix->pub_seq = q;
+    return TM_OK;
 }
 
 int tm_read_begin(tm_index *ix, uint64_t *ticket) {
@@ -2077,17 +2169,65 @@ int pin_mapped(tm_index *ix, hipStream_t s, uint8_t *&host, uint8_t *&dev, uint6
     return TM_OK;
 }
 
-// a host topic batch -> what the kernels read: rebased offsets, then the bytes
-// (16-aligned: the walk's aligned 16-byte loads), in one buffer of the lane
-int stage_in(tm_index *ix, Lane &ln, uint64_t n, const uint8_t *tb, const uint64_t *to,
+// the TM_ALLOC_VRAM buffer holding [p, p + bytes), or null (caller holds ix->mu)
+const tm_index::Pinned *vram_buf(tm_index *ix, const void *p, uint64_t bytes) {
+    const uint8_t *q = static_cast<const uint8_t *>(p);
+    for (const auto &b : ix->pinned)
+        if (b.vram && q >= b.host && bytes <= b.size && q - b.host <= (ptrdiff_t)(b.size - bytes)) return &b;
+    return nullptr;
+}
+
+// A host topic batch -> what the kernels read: rebased offsets, then the bytes
+// (16-aligned: the walk's aligned 16-byte loads), in one buffer of the lane.
+// Inputs in TM_ALLOC_VRAM memory are read where they lie, never by the host
+// (each host read of it is an uncached PCIe round trip, ~0.6 us):
+// bytes there are used in place with the offsets unrebased; u64 offsets there
+// too are used in place; u32 offsets there (to32v, the 32-bit API) are widened
+// by a kernel into the lane's scratch.  Only `to[0]`/`to[n]` (or to32v[n])
+// are read by the host for a VRAM batch.
+int stage_in(tm_index *ix, Lane &ln, uint64_t n, const uint8_t *tb, const uint64_t *to, const uint32_t *to32v,
              const uint8_t *&dbytes, const uint64_t *&doffs) {
-    const uint64_t b0 = to[0], nbytes = to[n] - b0;
+    int rc;
+    const uint64_t end = to32v ? to32v[n] : to[n];
+    const uint64_t b0 = to32v ? 0 : to[0];
+    const bool vbytes = vram_buf(ix, tb, std::max<uint64_t>(end, 1)) != nullptr;
+    const bool voffs = to32v || vram_buf(ix, to, (n + 1) * 8) != nullptr;
+    if (vbytes && voffs) {   // both in HBM already: nothing crosses PCIe
+        dbytes = tb;
+        if (to32v) {
+            if ((rc = grow_dev(ix, ln.s, ln.d_o64, ln.d_o64_cap, n + 1))) return rc;
+            HIPCHK(ix, launch_offs_widen(to32v, ln.d_o64, n + 1, ln.s));
+            doffs = ln.d_o64;
+        } else {
+            doffs = to;
+        }
+        return TM_OK;
+    }
+    if (to32v || voffs) {   // offsets in HBM, bytes in host memory (no caller of the library does this)
+        uint64_t *o = nullptr;
+        if ((rc = pin_mapped(ix, ln.s, ln.pin_in, ln.pin_in_dev, ln.pin_in_cap, (n + 1) * 8 + end + 32))) return rc;
+        o = reinterpret_cast<uint64_t *>(ln.pin_in);
+        if (to32v) HIPCHK(ix, launch_offs_widen(to32v, reinterpret_cast<uint64_t *>(ln.pin_in_dev), n + 1, ln.s));
+        else HIPCHK(ix, hipMemcpyAsync(o, to, (n + 1) * 8, hipMemcpyDeviceToHost, ln.s));
+        const uint64_t boff = ((n + 1) * 8 + 15) & ~15ull;
+        if (end) memcpy(ln.pin_in + boff, tb, end);   // bytes [0, end): the offsets stay unrebased
+        dbytes = ln.pin_in_dev + boff;
+        doffs = reinterpret_cast<const uint64_t *>(ln.pin_in_dev);
+        if (n > ZC_TOPICS) {
+            if ((rc = grow_dev(ix, ln.s, ln.d_in, ln.d_in_cap, boff + end + 16))) return rc;
+            HIPCHK(ix, hipMemcpyAsync(ln.d_in, ln.pin_in, boff + end, hipMemcpyHostToDevice, ln.s));
+            dbytes = ln.d_in + boff;
+            doffs = reinterpret_cast<const uint64_t *>(ln.d_in);
+        }
+        return TM_OK;
+    }
+    const uint64_t nbytes = vbytes ? 0 : end - b0;   // bytes in HBM: only the offsets move
     const uint64_t boff = ((n + 1) * 8 + 15) & ~15ull;
     const uint64_t need = boff + nbytes + 16;
-    int rc;
     if ((rc = pin_mapped(ix, ln.s, ln.pin_in, ln.pin_in_dev, ln.pin_in_cap, need))) return rc;
     uint64_t *po = reinterpret_cast<uint64_t *>(ln.pin_in);
-    for (uint64_t i = 0; i <= n; i++) po[i] = to[i] - b0;
+    const uint64_t rb = vbytes ? 0 : b0;
+    for (uint64_t i = 0; i <= n; i++) po[i] = to[i] - rb;
     if (nbytes) memcpy(ln.pin_in + boff, tb + b0, nbytes);
     const uint8_t *base = ln.pin_in_dev;
     if (n > ZC_TOPICS) {
@@ -2096,7 +2236,7 @@ int stage_in(tm_index *ix, Lane &ln, uint64_t n, const uint8_t *tb, const uint64
         base = ln.d_in;
     }
     doffs = reinterpret_cast<const uint64_t *>(base);
-    dbytes = base + boff;
+    dbytes = vbytes ? tb : base + boff;
     return TM_OK;
 }
 
@@ -2139,9 +2279,21 @@ int tm_host_alloc_ex(tm_index *ix, uint64_t bytes, uint32_t flags, void **out) {
         for (int r = 1; r < ix->nrep; r++)
             if (ix->rep[r].device != ix->rep[0].device)
                 return fail(ix, TM_EINVAL, "tm_host_alloc_ex: TM_ALLOC_VRAM needs a one-device index");
+        // the host writes it through the PCIe BAR: only where the whole of the
+        // device's memory is mapped there (large / resizable BAR) -- else a host
+        // store could fault the caller; TM_EINVAL, and the caller
+        // keeps its inputs in tm_host_alloc memory (the NIF does)
+        int large_bar = 0;
+        if (hipDeviceGetAttribute(&large_bar, hipDeviceAttributeIsLargeBar, ix->rep[0].device) != hipSuccess || !large_bar)
+            return fail(ix, TM_EINVAL, "tm_host_alloc_ex: the device's memory is not mapped for the host (no large BAR)");
         // fine-grained: the host maps it through the BAR (same virtual address)
         if (hipExtMallocWithFlags(&d, bytes ? bytes : 1, hipDeviceMallocFinegrained) != hipSuccess || !d)
             return fail(ix, TM_ENOMEM, "tm_host_alloc_ex: fine-grained device allocation failed");
+        hipPointerAttribute_t pa;
+        if (hipPointerGetAttributes(&pa, d) != hipSuccess || pa.type != hipMemoryTypeDevice) {
+            (void)hipFree(d);
+            return fail(ix, TM_EINVAL, "tm_host_alloc_ex: the allocation is not device memory");
+        }
         ix->pinned.push_back({static_cast<uint8_t *>(d), static_cast<uint8_t *>(d), bytes, true});
         *out = d;
         return TM_OK;
@@ -2204,17 +2356,27 @@ static int retry_or_fail(tm_index *ix, std::unique_lock<std::mutex> &g, Lane &ln
 // takes the queued batches (in order, up to SMALL_SEGS of them and
 // ZC_TOPICS topics), runs them as ONE k_walk_small launch with a segment
 // table (each segment its own inputs, outputs and look-back region), and
-// marks them done; others wait on the condition variable.  A lone caller
-// leads its own batch at once: its latency is the single-batch path's.
+// marks them done, waking each of their callers (one condition variable per
+// request: no herd of every waiting caller per launch).  A lone caller leads
+// its own batch at once: its latency is the single-batch path's.
+// TM_DEBUG_CMB_GATHER (us, study knob, 0 = off): a new leader first waits up to
+// that long while fewer batches are queued or in flight than the recent
+// high-water mark (callers between two batches are about to queue theirs), so
+// launches carry more batches.  TM_DEBUG_CMB_LAND: the launch writes its
+// outputs to the lane's HBM arena and one k_land launch copies them to the
+// callers' buffers (whole lines over PCIe instead of the walk's small writes).
 struct SmallReq {
     uint64_t n;
     const uint8_t *db; const uint8_t *dof; uint8_t *dh; uint8_t *de; uint8_t *dv;
     uint64_t cap;
     int rc = TM_OK;
     bool done = false;
+    std::condition_variable cv;
 };
 constexpr int CMB_LEGACY = 1;   // (not a TM_ code) the index no longer allows the one-launch path
+constexpr uint64_t CMB_HW_NS = 2000000;   // the high-water mark's memory (2 ms)
 
+static uint64_t land_align(uint64_t b) { return (b + 255) & ~255ull; }
 
 static int run_small_group(tm_index *ix, const std::vector<SmallReq *> &grp, uint64_t *t_sync_end) {
     uint64_t total = 0;
@@ -2231,12 +2393,31 @@ static int run_small_group(tm_index *ix, const std::vector<SmallReq *> &grp, uin
     if ((rc = ensure_ws(ix, total + (uint64_t)SMALL_SEGS * SM_TOPICS, ln))) return rc;
     if (!small_path_ok(dev_view(ix, ln.r), total)) return CMB_LEGACY;
     ix->rep[ln.r].batches++;
+    const bool land = ix->cmb_land.load(std::memory_order_relaxed) != 0;
+    if (land) {   // the arena: each segment's offsets, flags, values (256-B aligned regions)
+        uint64_t need = 0;
+        for (auto *r : grp) need += land_align(4 * (r->n + 1)) + land_align(r->n) + land_align(4 * (r->dv ? r->cap : 0));
+        if ((rc = grow_dev(ix, s, ln.d_land, ln.d_land_cap, need))) return rc;
+    }
     SmallSegs sg{};
-    sg.count = (uint32_t)grp.size();
+    LandSegs ls{};
+    sg.count = ls.count = (uint32_t)grp.size();
+    uint64_t at = 0;
     for (size_t k = 0; k < grp.size(); k++) {
         const SmallReq &r = *grp[k];
-        sg.s[k] = SmallSeg{r.db ? r.db : r.dof, r.dof, r.dh, r.de, reinterpret_cast<uint32_t *>(r.dv),
-                           r.dv ? r.cap : 0, (uint32_t)r.n, 0};
+        const uint64_t vcap = r.dv ? r.cap : 0;
+        if (land) {
+            uint8_t *hh = ln.d_land + at, *he = hh + land_align(4 * (r.n + 1)), *hv = he + land_align(r.n);
+            at += land_align(4 * (r.n + 1)) + land_align(r.n) + land_align(4 * vcap);
+            sg.s[k] = SmallSeg{r.db ? r.db : r.dof, r.dof, hh, he, r.dv ? reinterpret_cast<uint32_t *>(hv) : nullptr,
+                               vcap, (uint32_t)r.n, 0};
+            ls.s[k] = LandSeg{reinterpret_cast<const uint32_t *>(hh), he, reinterpret_cast<const uint32_t *>(hv),
+                              reinterpret_cast<uint32_t *>(r.dh), r.de, reinterpret_cast<uint32_t *>(r.dv), vcap,
+                              (uint32_t)r.n, 0};
+        } else {
+            sg.s[k] = SmallSeg{r.db ? r.db : r.dof, r.dof, r.dh, r.de, reinterpret_cast<uint32_t *>(r.dv), vcap,
+                               (uint32_t)r.n, 0};
+        }
     }
     const uint64_t tc = g_cmb_timing ? ns_now() : 0;
     for (int tries = 0;; tries++) {
@@ -2245,6 +2426,7 @@ static int run_small_group(tm_index *ix, const std::vector<SmallReq *> &grp, uin
         if ((rc = next_tag(ix, ln, s, tag))) return rc;
         int path = PATH_SMALL;
         HIPCHK(ix, launch_small_segs(d, ln.w, sg, true, tag, next_lb(ix), ix->small_kind, s, &path));
+        if (land) HIPCHK(ix, launch_land(ls, s));
         ix->path_batches[path]++;
         ix->cmb_launches++;
         ix->cmb_batches += grp.size();
@@ -2264,6 +2446,13 @@ static int run_small_group(tm_index *ix, const std::vector<SmallReq *> &grp, uin
     return TM_OK;
 }
 
+// (caller holds cmb_mu) queued + in flight, against the recent high-water mark
+static void cmb_note_load(tm_index *ix) {
+    const int cur = (int)ix->cmb_q.size() + ix->cmb_inflight;
+    const uint64_t t = ns_now();
+    if (cur >= ix->cmb_hw || t - ix->cmb_hw_ns > CMB_HW_NS) { ix->cmb_hw = cur; ix->cmb_hw_ns = t; }
+}
+
 static int small_combined(tm_index *ix, SmallReq &rq) {
     const uint64_t t_in = g_cmb_timing ? ns_now() : 0;
     struct ReqTime {   // (on every return path)
@@ -2272,8 +2461,25 @@ static int small_combined(tm_index *ix, SmallReq &rq) {
     } rt{t_in};
     std::unique_lock<std::mutex> lk(ix->cmb_mu);
     ix->cmb_q.push_back(&rq);
+    cmb_note_load(ix);
+    if (ix->cmb_gathering) ix->cmb_gcv.notify_all();
     while (!rq.done) {
         if (ix->cmb_running < std::max(ix->cmb_leaders.load(), 1) && !ix->cmb_q.empty()) {
+            ix->cmb_running++;
+            const int gus = ix->cmb_gather_us.load(std::memory_order_relaxed);
+            if (gus > 0) {   // the gather window (study knob)
+                const auto dl = std::chrono::steady_clock::now() + std::chrono::microseconds(gus);
+                ix->cmb_gathering++;
+                for (;;) {
+                    uint64_t q = 0;
+                    for (auto *r : ix->cmb_q) q += r->n;
+                    if ((int)ix->cmb_q.size() + ix->cmb_inflight >= ix->cmb_hw || ix->cmb_q.size() >= (size_t)SMALL_SEGS ||
+                        q >= ZC_TOPICS)
+                        break;
+                    if (ix->cmb_gcv.wait_until(lk, dl) == std::cv_status::timeout) break;
+                }
+                ix->cmb_gathering--;
+            }
             std::vector<SmallReq *> grp;
             uint64_t total = 0;
             while (!ix->cmb_q.empty() && grp.size() < (size_t)SMALL_SEGS &&
@@ -2282,7 +2488,8 @@ static int small_combined(tm_index *ix, SmallReq &rq) {
                 grp.push_back(ix->cmb_q.front());
                 ix->cmb_q.pop_front();
             }
-            ix->cmb_running++;
+            ix->cmb_inflight += (int)grp.size();
+            if (!ix->cmb_q.empty() && ix->cmb_running < ix->cmb_leaders.load()) ix->cmb_q.front()->cv.notify_one();
             lk.unlock();
             uint64_t t_sync_end = 0;
             const int rc = run_small_group(ix, grp, &t_sync_end);   // (the lane is released on return)
@@ -2292,12 +2499,17 @@ static int small_combined(tm_index *ix, SmallReq &rq) {
                 g_cmbt.release_ns += t_rel - t_sync_end;
                 g_cmbt.done_ns += ns_now() - t_rel;
             }
-            for (auto *r : grp) { r->rc = rc; r->done = true; }
+            for (auto *r : grp) {
+                r->rc = rc;
+                r->done = true;
+                if (r != &rq) r->cv.notify_one();
+            }
+            ix->cmb_inflight -= (int)grp.size();
             ix->cmb_running--;
-            ix->cmb_cv.notify_all();
+            if (!ix->cmb_q.empty()) ix->cmb_q.front()->cv.notify_one();   // it may lead now
             continue;
         }
-        ix->cmb_cv.wait(lk);
+        rq.cv.wait(lk);
     }
     return rq.rc;
 }
@@ -2306,13 +2518,15 @@ static int small_combined(tm_index *ix, SmallReq &rq) {
 // the index's current device view and queue the kernels on the caller's lane;
 // they wait for the GPU and copy results out without it, so concurrent callers
 // overlap on the device (each lane is its own stream) and deltas keep flowing.
-int tm_match_batch_ex(tm_index *ix, uint64_t n, const uint8_t *tb, const uint64_t *to, uint64_t *out_hit,
-                      uint32_t *out_vals, uint64_t cap, uint8_t *out_err, uint32_t order, uint32_t *out_unique) {
+// tm_match_batch_ex, or (to32v) the same over u32 offsets that lie in
+// TM_ALLOC_VRAM memory with their bytes (tm_match_batch32_ex's batches the
+// one-launch path does not take): widened on the device, never read by the host
+static int match_batch_impl(tm_index *ix, uint64_t n, const uint8_t *tb, const uint64_t *to, const uint32_t *to32v,
+                            uint64_t *out_hit, uint32_t *out_vals, uint64_t cap, uint8_t *out_err, uint32_t order,
+                            uint32_t *out_unique) {
     static const bool timing = getenv("TM_HOST_TIMING") != nullptr;
     double tt[8]; int nt = 0;
     if (timing) tt[nt++] = now_us();
-    if (!ix) return fail(nullptr, TM_EINVAL, "tm_match_batch: null handle");
-    if (!to || !out_hit || (n && !tb && to[n] != to[0])) return fail(ix, TM_EINVAL, "tm_match_batch: null buffer");
     if (n >= 0xFFFFFFFFull) return fail(ix, TM_EINVAL, "tm_match_batch: batch too large");
     if (order > TM_ORDER_UNIQUE) return fail(ix, TM_EINVAL, "tm_match_batch: bad order");
     const bool sorted = order != TM_ORDER_TRAVERSAL, unique = order == TM_ORDER_UNIQUE;
@@ -2326,7 +2540,7 @@ int tm_match_batch_ex(tm_index *ix, uint64_t n, const uint8_t *tb, const uint64_
     if ((rc = ensure_ws(ix, n, ln))) return rc;
     ix->rep[ln.r].batches++;
     if (timing) tt[nt++] = now_us();
-    if (n && n <= ZC_TOPICS) {
+    if (n && n <= ZC_TOPICS && !to32v) {
         // every buffer from tm_host_alloc: the kernels read the topics and
         // write the hit lists in place (no staging copy in, no copy out)
         const uint64_t nbytes = to[n];
@@ -2379,7 +2593,7 @@ int tm_match_batch_ex(tm_index *ix, uint64_t n, const uint8_t *tb, const uint64_
     }
     const uint8_t *dbytes;
     const uint64_t *doffs;
-    if ((rc = stage_in(ix, ln, n, tb, to, dbytes, doffs))) return rc;
+    if ((rc = stage_in(ix, ln, n, tb, to, to32v, dbytes, doffs))) return rc;
     if (timing) tt[nt++] = now_us();
     // results: hit offsets (n + 1) x u64, then the badarg flags (then the
     // distinct counts, u32, for UNIQUE); the values are written by k_emit
@@ -2450,6 +2664,13 @@ int tm_match_batch_ex(tm_index *ix, uint64_t n, const uint8_t *tb, const uint64_
     return (out_vals && total > cap) ? TM_ECAP : TM_OK;
 }
 
+int tm_match_batch_ex(tm_index *ix, uint64_t n, const uint8_t *tb, const uint64_t *to, uint64_t *out_hit,
+                      uint32_t *out_vals, uint64_t cap, uint8_t *out_err, uint32_t order, uint32_t *out_unique) {
+    if (!ix) return fail(nullptr, TM_EINVAL, "tm_match_batch: null handle");
+    if (!to || !out_hit || (n && !tb && to[n] != to[0])) return fail(ix, TM_EINVAL, "tm_match_batch: null buffer");
+    return match_batch_impl(ix, n, tb, to, nullptr, out_hit, out_vals, cap, out_err, order, out_unique);
+}
+
 int tm_match_batch(tm_index *ix, uint64_t n, const uint8_t *tb, const uint64_t *to, uint64_t *out_hit,
                    uint32_t *out_vals, uint64_t cap, uint8_t *out_err) {
     return tm_match_batch_ex(ix, n, tb, to, out_hit, out_vals, cap, out_err, TM_ORDER_TRAVERSAL, nullptr);
@@ -2515,15 +2736,24 @@ int tm_match_batch32_ex(tm_index *ix, uint64_t n, const uint8_t *tb, const uint3
             }
         }
     }
-    // widened: the 64-bit path, then the offsets narrowed
+    // widened: the 64-bit path, then the offsets narrowed.  Offsets in
+    // TM_ALLOC_VRAM memory are widened on the device (the host never reads
+    // them: ADVICE r5 -- a deep index, > 65536 topics or a sorted order took
+    // this path and read the NIF's device buffers back over the BAR)
+    bool voffs;
+    {
+        std::lock_guard<std::mutex> g(ix->mu);
+        voffs = vram_buf(ix, to, (n + 1) * 4) != nullptr;
+    }
     std::vector<uint64_t> o64, h64;
     try {
-        o64.assign(to, to + n + 1);
+        if (!voffs) o64.assign(to, to + n + 1);
         h64.resize(n + 1);
     } catch (const std::bad_alloc &) {
         return fail(ix, TM_ENOMEM, "tm_match_batch32: out of host memory");
     }
-    const int rc = tm_match_batch_ex(ix, n, tb, o64.data(), h64.data(), out_vals, cap, out_err, order, out_unique);
+    const int rc = voffs ? match_batch_impl(ix, n, tb, nullptr, to, h64.data(), out_vals, cap, out_err, order, out_unique)
+                         : tm_match_batch_ex(ix, n, tb, o64.data(), h64.data(), out_vals, cap, out_err, order, out_unique);
     if (rc != TM_OK && rc != TM_ECAP) return rc;
     if (h64[n] > 0xFFFFFFFFull) return fail(ix, TM_EINVAL, "tm_match_batch32: more than 2^32 - 1 values");
     for (uint64_t i = 0; i <= n; i++) out_hit[i] = (uint32_t)h64[i];
@@ -2606,7 +2836,7 @@ int tm_first_batch(tm_index *ix, uint64_t n, const uint8_t *tb, const uint64_t *
     }
     const uint8_t *dbytes;
     const uint64_t *doffs;
-    if ((rc = stage_in(ix, ln, n, tb, to, dbytes, doffs))) return rc;
+    if ((rc = stage_in(ix, ln, n, tb, to, nullptr, dbytes, doffs))) return rc;
     const uint64_t rbytes = n * 5;   // first value u32 per topic, then the found flags
     uint8_t *dres;
     if ((rc = stage_out(ix, ln, n, rbytes, dres))) return rc;
@@ -2667,8 +2897,12 @@ int tm_debug_set(tm_index *ix, uint32_t key, uint64_t value) {
     case TM_DEBUG_LB_LAUNCHES: ix->dbg_lb_launches = value; break;
     case TM_DEBUG_PHASES: ix->dbg_phases = value != 0; break;
     case TM_DEBUG_COMBINE: ix->cmb_leaders = value > 16 ? 16 : (int)value; break;
+    case TM_DEBUG_CMB_GATHER: ix->cmb_gather_us = value > 1000 ? 1000 : (int)value; break;
+    case TM_DEBUG_CMB_LAND: ix->cmb_land = value != 0; break;
+    case TM_DEBUG_SMALL_TICKET: ix->small_ticket = value != 0; break;
     case TM_DEBUG_SMALL_KERNEL:
-        if (value > SMALL_WAVE8) return fail(ix, TM_EINVAL, "tm_debug_set: TM_DEBUG_SMALL_KERNEL is 0 to 3");
+        if (value != SMALL_AUTO && value != SMALL_WAVE && value != SMALL_WAVE8)
+            return fail(ix, TM_EINVAL, "tm_debug_set: TM_DEBUG_SMALL_KERNEL is 0, 1 or 3 (2, the lane kernel, was removed)");
         ix->small_kind = (int)value;
         break;
     default: return fail(ix, TM_EINVAL, "tm_debug_set: unknown key");
@@ -2685,6 +2919,12 @@ int tm_debug_get(tm_index *ix, uint32_t key, uint64_t *value) {
     case TM_DEBUG_PATH_SMALL: *value = ix->path_batches[PATH_SMALL].load(); break;
     case TM_DEBUG_PATH_LANE: *value = ix->path_batches[PATH_LANE].load(); break;
     case TM_DEBUG_COMBINE: *value = (uint64_t)ix->cmb_leaders.load(); break;
+    case TM_DEBUG_CMB_GATHER: *value = (uint64_t)ix->cmb_gather_us.load(); break;
+    case TM_DEBUG_CMB_LAND: *value = (uint64_t)ix->cmb_land.load(); break;
+    case TM_DEBUG_COMMITS: *value = ix->commits.load(); break;
+    case TM_DEBUG_SMALL_TICKET: *value = ix->small_ticket; break;
+    case TM_DEBUG_COMMIT_WAITS: *value = ix->commit_waits.load(); break;
+    case TM_DEBUG_COMMIT_FORCED: *value = ix->commit_forced.load(); break;
     case TM_DEBUG_COMBINED_LAUNCHES: *value = ix->cmb_launches.load(); break;
     case TM_DEBUG_COMBINED_BATCHES: *value = ix->cmb_batches.load(); break;
     case TM_DEBUG_WIDE_NODES:

@@ -107,7 +107,8 @@ struct WordAcc {
 //  - GlobalSrc: the batch in global memory (HBM, or mapped host memory for
 //    in-place host batches), or any byte pointer;
 //  - StagedSrc: the block's byte span copied into LDS by coalesced loads
-//    (k_walk_lane), read at offset p - b0 from the LDS array itself -- never
+//    (k_walk_small's fallback lane walk), read at offset p - b0 from the LDS
+//    array itself -- never
 //    through a pointer rebased below it.  (The round-4 stage1 study formed
 //    `s_stage - B0`: the compiler did that arithmetic on the 32-bit LDS
 //    address, which wraps for B0 above the array's LDS offset, then cast it to
@@ -207,10 +208,10 @@ __device__ __forceinline__ uint32_t ctab_find(const DevIndex &ix, uint32_t off, 
 // main walk's store does not: a topic that meets such a cut is handed to the
 // tail lists (DFS_REROUTE), keeping k_walk_fast within its register budget.
 //
-// LITE (k_walk_lane's second look at a topic deeper than FAST_L): the main
+// LITE (k_walk_small<8>'s fallback lane walk, lite_path_ok indexes): the main
 // walk's FAST_L levels, but tokenised like the deeper stores -- every level
 // scanned (count, badarg), only the levels a walk can use resolved
-// (need_levels) -- which lane_path_ok guarantees fit FAST_L.
+// (need_levels) -- which lite_path_ok guarantees fit FAST_L.
 template <int ML, bool LITE = false>
 struct LdsStore {
     static constexpr uint32_t maxl = ML;
@@ -798,7 +799,7 @@ __device__ __forceinline__ uint64_t wave_incl_scan(uint64_t v) {
 // a time (lane k: block hi - k) back to the nearest inclusive prefix, summing
 // the totals in between, publishes its own inclusive prefix and returns its
 // exclusive one (in every lane).  A predecessor started before vb (dispatch
-// order for k_walk_small, the start-order ticket for k_walk_lane), so it
+// order, include/tmatch.h "Forward progress"), so it
 // publishes soon; the wait for one word is still bounded: past lb.spins polls
 // -- or when a predecessor failed, or vb is the test hook's lb.fail_block --
 // the result is LBR_FAIL and vb publishes LB_FAIL, which every later block
@@ -1182,7 +1183,7 @@ bool small_path_ok(const DevIndex &ix, uint64_t n) { return n && n <= SMALL_TOPI
 // every slot of the GPU; levels and frontier states per topic <= 8, else the
 // lane walk).  A group keeps up to HC hit ranges (C3: 8.4 per topic).
 // LITE: the fallback lane walk's store holds FAST_L levels and resolves only
-// need_levels() (as k_walk_lane's; lane_path_ok indexes: shallow, no
+// need_levels() (lite_path_ok indexes: shallow, no
 // '#'-not-last key) instead of MID_L: 76 instead of 292 B of LDS per topic.
 template <int W>
 struct SmallShape {
@@ -1205,8 +1206,8 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_small(DevIndex ix, Workspace 
     OT *hit_offs = hit_offs_;
     uint32_t *out = out_;
     uint32_t vb = blockIdx.x, nblk = gridDim.x, sb0 = 0;   // sb0: the segment's first block
+    uint32_t k = 0;   // the segment
     if (MODE == MODE_COUNT && sg.count) {
-        uint32_t k = 0;
         while (k + 1 < sg.count && blockIdx.x >= sg.s[k + 1].block0) k++;
         const SmallSeg &S = sg.s[k];
         n = S.n; cap = S.cap; blob = S.blob;
@@ -1216,6 +1217,20 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_small(DevIndex ix, Workspace 
         sb0 = S.block0;
         nblk = (k + 1 < sg.count ? sg.s[k + 1].block0 : gridDim.x) - sb0;
         vb = blockIdx.x - sb0;
+    }
+    if (MODE == MODE_COUNT && lb.ticket) {
+        // start-order ticket (include/tmatch.h "Forward progress"): the block
+        // takes the segment's next virtual index, so every block it may wait
+        // for in the look-back below has started; the segment's last ticket
+        // resets the word for the next launch on this workspace
+        __shared__ uint32_t s_tk;
+        if (threadIdx.x == 0) {
+            const uint32_t tk = atomicAdd(&ws.list_n[SM_TICK + k], 1u);
+            if (tk == nblk - 1) atomicExch(&ws.list_n[SM_TICK + k], 0u);
+            s_tk = tk;
+        }
+        __syncthreads();
+        vb = s_tk;
     }
     using SH = SmallShape<W>;
     constexpr uint32_t G = SH::G, ST = SH::ST, MAXL = SH::MAXL, HC = SH::HC;
@@ -1245,10 +1260,8 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_small(DevIndex ix, Workspace 
     // (in place batches: a few whole PCIe writes instead of one per group)
     __shared__ uint32_t s_vals[SM_VSTAGE];
     __shared__ uint64_t s_sum;
-    // blocks scan in blockIdx order: workgroups are dispatched in that order,
-    // so a block's predecessors are running or done (a start-order ticket, one
-    // atomic on one word per block, serialised the blocks of a 64k batch:
-    // 4,096 tickets; k_walk_lane, 64 topics per block, takes one)
+    // blocks scan in blockIdx order (workgroups are dispatched in that order),
+    // or in start order with lb.ticket (include/tmatch.h "Forward progress")
     // the block's ST + 1 topic offsets, read once by one wave (the caller's
     // buffers may be host memory: one coalesced read, not one per group)
     if (threadIdx.x <= ST && (uint64_t)vb * ST + threadIdx.x <= n)
@@ -1693,9 +1706,8 @@ constexpr uint8_t RF_INLINE = 1, RF_SKIP = 2;   // s_flg: a one-value run kept i
 // One wave writes the values of R ranges flattened in LDS into out[base, endp):
 // s_off = the range's value offset (RF_INLINE: the value itself), s_rel = its
 // first position relative to base (s_rel[R] = endp - base), s_flg (RF_SKIP: a
-// re-walked topic's positions, written by its re-walk).  Shared by k_emit
-// (ranges read back from the walk's range lists) and k_walk_lane (ranges
-// straight from the walk's registers).
+// re-walked topic's positions, written by its re-walk).  k_emit's inner copy
+// (ranges read back from the walk's range lists).
 __device__ __forceinline__ void wave_emit(const DevIndex &ix, const uint32_t *s_off, const uint32_t *s_rel,
                                           const uint8_t *s_flg, uint32_t R, uint64_t base, uint64_t endp,
                                           uint32_t *out, uint64_t cap) {
@@ -1899,178 +1911,13 @@ __global__ __launch_bounds__(EMIT_BLOCK) void k_emit(DevIndex ix, Workspace ws, 
     wave_emit(ix, s_off[wv], s_rel[wv], s_flg[wv], R, base, endp, out, cap);
 }
 
-// ------------------------------------------ small batches, one lane per topic
-//
-// k_walk_lane: a count-mode batch of <= SMALL_TOPICS topics in ONE launch,
-// one lane per topic -- the throughput shape for the NIF's concurrent small
-// batches.  k_walk_small spends 16 lanes on a topic whose
-// frontier averages 2.4 states: it issues ~8x the instructions per topic of a
-// lane walk (a 4k C3 batch: ~2.9M) and tops out near 3.4e8 topics/s however
-// the batches arrive.  One 64-lane block (one wave, 64 topics):
-//   1. takes a start-order ticket (vb, per segment): every block with a lower
-//      ticket has started, so the look-back below only ever waits for blocks
-//      that are running -- forward progress by construction, whatever other
-//      launches hold the GPU's slots (64 topics per ticket,
-//      so a 4k batch takes 64 atomics on one word);
-//   2. reads its 65 topic offsets and stages its whole topic byte span in LDS
-//      with one round of coalesced 16-B loads (in-place host batches: one PCIe
-//      burst per block instead of a round trip per lane and chunk -- the
-//      round-4 lane walk without it was 2x slower); a span
-//      longer than LANE_TBQ chunks is read from global memory instead;
-//   3. walks each topic from there (StagedSrc) exactly as k_walk_fast does
-//      (dfs, LDS store, ranges in registers, parked in the lane's own store
-//      column); a topic deeper than FAST_L levels is counted by a second walk
-//      whose store resolves only need_levels() (lane_path_ok: the index's
-//      depth and binary keys fit FAST_L and it holds no '#'-not-last key);
-//   4. gets its global offset from the decoupled look-back over the blocks in
-//      ticket order (bounded wait: a failure flags err 4, the host reruns);
-//   5. writes its offsets and flags (64 coalesced stores each), then its
-//      values from the LDS ranges (wave_emit: 16-B stores, 1 KiB per
-//      instruction); topics with more than RCAP ranges, or deeper than
-//      FAST_L, re-walk and write theirs directly.
-// Several host batches in one launch (SmallSegs, the combiner): as k_walk_small.
-constexpr int LANE_BLOCK = 64;
-constexpr uint32_t LANE_TBQ = 256;   // 16-B chunks of topic bytes a block stages (4 KiB: 64 B per topic)
-static_assert(LANE_BLOCK == 64, "k_walk_lane: one wave per block");
-union LaneLds {   // a k_walk_lane block's LDS, reused step by step
-    struct { uint32_t wid[FAST_L * LANE_BLOCK], pend[(FAST_L + 1) * LANE_BLOCK]; uint8_t len[FAST_L * LANE_BLOCK]; } walk;
-    struct { uint32_t off[WR], rel[WR + 1]; uint8_t flg[WR]; } emit;
-};
-static_assert(2 * RCAP <= 2 * FAST_L + 1, "a lane's walk-store column holds its ranges");
-
-bool lane_path_ok(const DevIndex &ix) {
+// The LITE fallback store of k_walk_small<8> (FAST_L levels resolving only
+// need_levels()) holds every topic of a shallow index without a
+// '#'-not-last key.  (Round 5's k_walk_lane, one lane per topic, ran on the same
+// condition; it lost to k_walk_small on every measured path -- 4k 0.077 vs
+// 0.040 ms, 8 callers 2.5e8 vs 3.1e8 -- and was removed in round 6.)
+bool lite_path_ok(const DevIndex &ix) {
     return !ix.hdesc && ix.depth + 2 <= (uint32_t)FAST_L && ix.xlen_max <= (uint32_t)FAST_L;
-}
-
-template <class OT>
-__global__ __launch_bounds__(LANE_BLOCK) void k_walk_lane(DevIndex ix, Workspace ws, uint64_t n_, const uint8_t *blob_,
-                                                          const OT *offs_, uint8_t *err_, OT *hit_offs_, uint32_t *out_,
-                                                          uint64_t cap_, uint32_t tag, LbCtl lb, SmallSegs sg) {
-    __shared__ LaneLds S;
-    __shared__ uint4 s_tb[LANE_TBQ];
-    __shared__ uint64_t s_off[LANE_BLOCK + 1];
-    const uint32_t lane = threadIdx.x;
-    uint64_t n = n_, cap = cap_;
-    const uint8_t *blob = blob_;
-    const OT *offs = offs_;
-    OT *hit_offs = hit_offs_;
-    uint32_t *out = out_;
-    uint8_t *err = err_;
-    uint32_t seg = 0, nblk = gridDim.x, sb0 = 0;
-    if (sg.count) {
-        while (seg + 1 < sg.count && blockIdx.x >= sg.s[seg + 1].block0) seg++;
-        const SmallSeg &G = sg.s[seg];
-        n = G.n; cap = G.cap; blob = G.blob; out = G.out; err = G.err;
-        offs = static_cast<const OT *>(G.offs);
-        hit_offs = static_cast<OT *>(G.hit);
-        sb0 = G.block0;
-        nblk = (seg + 1 < sg.count ? sg.s[seg + 1].block0 : gridDim.x) - sb0;
-    }
-    // ---- 1. the start-order ticket (the segment's last ticket resets the
-    // word for the next launch on this workspace: every block has its ticket)
-    uint32_t tk = 0;
-    if (lane == 0) {
-        tk = atomicAdd(&ws.list_n[LS_TICK + seg], 1u);
-        if (tk == nblk - 1) atomicExch(&ws.list_n[LS_TICK + seg], 0u);
-    }
-    const uint32_t vb = __builtin_amdgcn_readfirstlane(tk);
-    const uint64_t t0 = (uint64_t)vb * LANE_BLOCK, t = t0 + lane;
-    const bool live = t < n;
-    const uint32_t nt = n - t0 < (uint64_t)LANE_BLOCK ? (uint32_t)(n - t0) : (uint32_t)LANE_BLOCK;
-
-    // ---- 2. offsets and the byte span into LDS
-    if (lane <= nt) s_off[lane] = offs[t0 + lane];
-    if (lane == 0 && nt == LANE_BLOCK) s_off[LANE_BLOCK] = offs[t0 + LANE_BLOCK];
-    wave_sync();
-    const uint64_t beg = live ? s_off[lane] : 0, end = live ? s_off[lane + 1] : 0;
-    const uint64_t B0 = s_off[0] & ~15ull;
-    const uint64_t nq = (s_off[nt] - B0 + 15) >> 4;
-    const bool staged = nq <= LANE_TBQ;   // (block-uniform)
-    if (staged) {
-        // aligned chunks share their granule with a valid byte: no page the caller does not own
-        for (uint32_t c = lane; c < nq; c += LANE_BLOCK) s_tb[c] = ld4_once(blob + B0 + 16ull * c);
-        wave_sync();
-    }
-    const StagedSrc src{blob, s_tb, B0, staged};
-
-    // ---- 3. the walk (k_walk_fast's), ranges parked in the lane's store column
-    uint32_t cnt = 0, nr = 0, e = 0;
-    int rc = RC_OK;
-    if (live) {
-        RangeEmit em;
-        em.cnt = 0; em.nr = 0;
-        LdsStore<FAST_L> st{S.walk.wid + lane, S.walk.pend + lane, S.walk.len + lane, LANE_BLOCK, 0};
-        rc = match_topic(ix, src, beg, end, st, em);
-        if (rc == RC_OK) {
-            cnt = em.cnt; nr = em.nr;
-#pragma unroll
-            for (uint32_t i = 0; i < RCAP; i++)
-                if (i < nr) { S.walk.wid[i * LANE_BLOCK + lane] = em.r[i].x; S.walk.pend[i * LANE_BLOCK + lane] = em.r[i].y; }
-        }
-        e = rc == RC_BADARG ? 1u : 0u;
-    }
-    const bool deep = rc == RC_DEEP;
-    bool rew = deep || nr > RCAP;   // values written by a re-walk (step 5)
-    if (deep) {   // (rare: C3 has none) counted in the lane's own column, levels beyond the trie only scanned
-        LdsStore<FAST_L, true> st{S.walk.wid + lane, S.walk.pend + lane, S.walk.len + lane, LANE_BLOCK, 0};
-        CountEmit ce{0};
-        const int frc = match_topic(ix, src, beg, end, st, ce);
-        cnt = frc == RC_OK ? (uint32_t)ce.cnt : 0u;
-        e = frc == RC_BADARG ? 1u : frc == RC_DEEP ? 2u : 0u;   // RC_DEEP here: > MAX_LEVELS levels
-    }
-    rew = rew && e == 0 && cnt > 0;
-    const uint32_t nrr = rew || rc != RC_OK ? 0u : nr;
-
-    // ---- 4. the block's offset
-    const uint64_t inc = wave_incl_scan(cnt);
-    const uint64_t total = __shfl(inc, 63, 64), rel = inc - cnt;
-    int res;
-    const uint64_t base = look_back(ws.look + (uint64_t)sb0 * LB_STRIDE, vb, tag, total, lb, res);
-    const bool fail = res != LBR_OK;   // (wave-uniform)
-    uint2 rg[RCAP];   // the lane's ranges, out of its store column before the LDS is reused
-#pragma unroll
-    for (uint32_t i = 0; i < RCAP; i++)
-        rg[i] = i < nrr ? make_uint2(S.walk.wid[i * LANE_BLOCK + lane], S.walk.pend[i * LANE_BLOCK + lane])
-                        : make_uint2(0, 0);
-    if (live) {
-        hit_offs[t] = (OT)(base + rel);
-        err[t] = fail ? 4 : (uint8_t)e;
-    }
-    if (fail) {
-        if (lane == 0) ws.hint_d[HINT_FAIL] = 1;
-        return;
-    }
-    if (lane == 0 && vb == nblk - 1) hit_offs[n] = (OT)(base + total);
-
-    // ---- 5. values
-    uint32_t R;
-    const uint32_t r0 = wave_excl_scan32(rew ? 1u : nrr, R);
-    wave_sync();   // every lane has its ranges: the LDS becomes the range stage
-    const uint32_t rel32 = (uint32_t)rel;
-    if (rew) {
-        S.emit.off[r0] = 0; S.emit.rel[r0] = rel32; S.emit.flg[r0] = RF_SKIP;
-    } else {
-        uint32_t acc = 0;
-#pragma unroll
-        for (uint32_t i = 0; i < RCAP; i++) {
-            if (i >= nrr) break;
-            S.emit.off[r0 + i] = rg[i].x;          // RUN_INLINE: the value itself
-            S.emit.rel[r0 + i] = rel32 + acc;
-            S.emit.flg[r0 + i] = (rg[i].y & RUN_INLINE) ? RF_INLINE : 0;
-            acc += rg[i].y & RUN_CNT;
-        }
-    }
-    if (lane == 0) S.emit.rel[R] = (uint32_t)total;
-    wave_sync();
-    wave_emit(ix, S.emit.off, S.emit.rel, S.emit.flg, R, base, base + total, out, cap);
-    if (__ballot(rew)) {
-        wave_sync();   // the LDS holds walk stores again
-        if (rew) {
-            LdsStore<FAST_L, true> st{S.walk.wid + lane, S.walk.pend + lane, S.walk.len + lane, LANE_BLOCK, 0};
-            DirectEmit de{ix.vals, out, base + rel, cap};
-            match_topic(ix, src, beg, end, st, de);
-        }
-    }
 }
 
 __global__ void k_patch(const PatchRun *runs, const uint32_t *data, uint64_t n, PatchBases bases) {
@@ -2313,6 +2160,28 @@ __global__ __launch_bounds__(256) void k_copy_values(const uint64_t *hit, uint64
         dst[i] = src[i];
 }
 
+// The combiner's landing copy (launch_land): every lane moves 16 B per step
+// when source and destination are both 16-B aligned (the arena's regions are;
+// tm_host_alloc buffers are), else bytes.  Grid: x strides one segment, y = segment.
+__device__ __forceinline__ void land_copy(uint8_t *d, const uint8_t *s, uint64_t nb, uint64_t i0, uint64_t st) {
+    if ((((uintptr_t)d | (uintptr_t)s) & 15) == 0) {
+        const uint64_t q = nb >> 4;
+        for (uint64_t i = i0; i < q; i += st) reinterpret_cast<uint4 *>(d)[i] = ld4_once(s + 16 * i);
+        for (uint64_t i = (q << 4) + i0; i < nb; i += st) d[i] = s[i];
+    } else {
+        for (uint64_t i = i0; i < nb; i += st) d[i] = s[i];
+    }
+}
+
+__global__ __launch_bounds__(256) void k_land(LandSegs ls) {
+    const LandSeg &S = ls.s[blockIdx.y];
+    const uint64_t tot = S.hit[S.n], nv = tot < S.cap ? tot : S.cap;
+    const uint64_t i0 = (uint64_t)blockIdx.x * 256 + threadIdx.x, st = (uint64_t)gridDim.x * 256;
+    land_copy(reinterpret_cast<uint8_t *>(S.dhit), reinterpret_cast<const uint8_t *>(S.hit), 4ull * (S.n + 1), i0, st);
+    land_copy(S.derr, S.err, S.n, i0, st);
+    if (S.dvals) land_copy(reinterpret_cast<uint8_t *>(S.dvals), reinterpret_cast<const uint8_t *>(S.vals), 4 * nv, i0, st);
+}
+
 // ------------------------------------------------------------ launchers
 
 static inline uint32_t blocks_for(uint64_t n, uint32_t per) { return (uint32_t)((n + per - 1) / per); }
@@ -2356,36 +2225,25 @@ hipError_t launch_match_phase2(const DevIndex &ix, const Workspace &ws, uint64_t
 }
 
 // The one-launch kernel of a small batch (small_kind): k_walk_small with 16
-// or 8 lanes per topic, or k_walk_lane (one lane per topic) where the index
-// allows it (lane_path_ok; else k_walk_small's 16 lanes).
-// The default (SMALL_AUTO): 8 lanes per topic for a launch of >= SMALL_W8_MIN
-// topics or of several host batches (the combiner's) -- throughput, twice the
-// topics per wave slot -- and 16 for a lone smaller batch (latency: a topic's
-// levels tokenised in half the ballot rounds).  8 lanes per topic run only on
-// a lane_path_ok index (the LITE fallback store); elsewhere 16.
+// or 8 lanes per topic.  The default (SMALL_AUTO): 8 lanes per topic for a
+// launch of >= SMALL_W8_MIN topics or of several host batches (the
+// combiner's) -- throughput, twice the topics per wave slot -- and 16 for a
+// lone smaller batch (latency: a topic's levels tokenised in half the ballot
+// rounds).  8 lanes per topic run only on a lite_path_ok index (the LITE
+// fallback store); elsewhere 16.
 constexpr uint64_t SMALL_W8_MIN = 8192;
-struct SmallPick { bool lane; int w; };
-static SmallPick small_pick(const DevIndex &ix, int kind, uint64_t n, uint32_t segs) {
-    const bool lite = lane_path_ok(ix);
-    if (kind == SMALL_LANE && lite) return {true, 0};
+static int small_w(const DevIndex &ix, int kind, uint64_t n, uint32_t segs) {
     const bool w8 = kind == SMALL_WAVE8 || (kind == SMALL_AUTO && (n >= SMALL_W8_MIN || segs > 1));
-    return {false, w8 && lite ? 8 : 16};
+    return w8 && lite_path_ok(ix) ? 8 : 16;
 }
-bool small_lane(const DevIndex &ix, int kind) { return small_pick(ix, kind, 0, 1).lane; }
-static uint32_t small_topics_per_block(const SmallPick &k) {
-    return k.lane ? LANE_BLOCK : k.w == 8 ? SmallShape<8>::ST : SmallShape<16>::ST;
-}
+static uint32_t small_topics_per_block(int w) { return w == 8 ? SmallShape<8>::ST : SmallShape<16>::ST; }
 
 template <class OT>
-static void launch_small_kernel(const SmallPick &k, uint32_t blocks, const DevIndex &ix, const Workspace &ws,
-                                uint64_t n, const uint8_t *bytes, const OT *offs, uint8_t *err, OT *hit_offs,
-                                uint32_t *out, uint64_t cap, uint32_t tag, LbCtl lb, const SmallSegs &sg,
-                                hipStream_t s) {
+static void launch_small_kernel(int w, uint32_t blocks, const DevIndex &ix, const Workspace &ws, uint64_t n,
+                                const uint8_t *bytes, const OT *offs, uint8_t *err, OT *hit_offs, uint32_t *out,
+                                uint64_t cap, uint32_t tag, LbCtl lb, const SmallSegs &sg, hipStream_t s) {
     Outs o{err, nullptr, nullptr};
-    if (k.lane)
-        hipLaunchKernelGGL((k_walk_lane<OT>), dim3(blocks), dim3(LANE_BLOCK), 0, s, ix, ws, n, bytes, offs, err,
-                           hit_offs, out, cap, tag, lb, sg);
-    else if (k.w == 8)
+    if (w == 8)
         hipLaunchKernelGGL((k_walk_small<MODE_COUNT, OT, 8, true>), dim3(blocks), dim3(WV_BLOCK), 0, s, ix, ws, n,
                            bytes, offs, o, hit_offs, out, cap, tag, lb, sg);
     else
@@ -2398,11 +2256,11 @@ hipError_t launch_match(const DevIndex &ix, const Workspace &ws, uint64_t n, con
                         uint32_t tag, LbCtl lb, bool phases, int small_kind, hipStream_t s, hipEvent_t ev_walk0,
                         hipEvent_t ev_walk1, int *path) {
     if (n && !phases && small_path_ok(ix, n)) {
-        const SmallPick k = small_pick(ix, small_kind, n, 1);
-        if (path) *path = k.lane ? PATH_LANE : PATH_SMALL;
+        const int w = small_w(ix, small_kind, n, 1);
+        if (path) *path = PATH_SMALL;
         hipError_t e;
         if (ev_walk0 && (e = hipEventRecord(ev_walk0, s)) != hipSuccess) return e;
-        launch_small_kernel<uint64_t>(k, blocks_for(n, small_topics_per_block(k)), ix, ws, n, bytes, offs, err,
+        launch_small_kernel<uint64_t>(w, blocks_for(n, small_topics_per_block(w)), ix, ws, n, bytes, offs, err,
                                       hit_offs, out, cap, tag & LB_TAG_MASK, lb, SmallSegs{}, s);
         if (ev_walk1 && (e = hipEventRecord(ev_walk1, s)) != hipSuccess) return e;
         return hipGetLastError();
@@ -2417,9 +2275,9 @@ hipError_t launch_match32(const DevIndex &ix, const Workspace &ws, uint64_t n, c
                           const uint32_t *offs, uint32_t *hit_offs, uint8_t *err, uint32_t *out, uint64_t cap,
                           uint32_t tag, LbCtl lb, int small_kind, hipStream_t s, int *path) {
     if (!small_path_ok(ix, n)) return hipErrorInvalidValue;   // (the caller converts instead)
-    const SmallPick k = small_pick(ix, small_kind, n, 1);
-    if (path) *path = k.lane ? PATH_LANE : PATH_SMALL;
-    launch_small_kernel<uint32_t>(k, blocks_for(n, small_topics_per_block(k)), ix, ws, n, bytes, offs, err, hit_offs,
+    const int w = small_w(ix, small_kind, n, 1);
+    if (path) *path = PATH_SMALL;
+    launch_small_kernel<uint32_t>(w, blocks_for(n, small_topics_per_block(w)), ix, ws, n, bytes, offs, err, hit_offs,
                                   out, cap, tag & LB_TAG_MASK, lb, SmallSegs{}, s);
     return hipGetLastError();
 }
@@ -2430,8 +2288,8 @@ hipError_t launch_small_segs(const DevIndex &ix, const Workspace &ws, const Smal
     SmallSegs sg = sg0;
     uint64_t total = 0;
     for (uint32_t q = 0; q < sg.count; q++) total += sg.s[q].n;
-    const SmallPick k = small_pick(ix, small_kind, total, sg.count);
-    const uint32_t per = small_topics_per_block(k);
+    const int w = small_w(ix, small_kind, total, sg.count);
+    const uint32_t per = small_topics_per_block(w);
     uint32_t blocks = 0;
     for (uint32_t q = 0; q < sg.count; q++) {
         if (!sg.s[q].n) return hipErrorInvalidValue;
@@ -2439,15 +2297,21 @@ hipError_t launch_small_segs(const DevIndex &ix, const Workspace &ws, const Smal
         blocks += blocks_for(sg.s[q].n, per);
     }
     if (!sg.count || sg.count > (uint32_t)SMALL_SEGS) return hipErrorInvalidValue;
-    if (path) *path = k.lane ? PATH_LANE : PATH_SMALL;
+    if (path) *path = PATH_SMALL;
     const SmallSeg &F = sg.s[0];
     const uint32_t tg = tag & LB_TAG_MASK;
     if (u32)
-        launch_small_kernel<uint32_t>(k, blocks, ix, ws, F.n, F.blob, static_cast<const uint32_t *>(F.offs), F.err,
+        launch_small_kernel<uint32_t>(w, blocks, ix, ws, F.n, F.blob, static_cast<const uint32_t *>(F.offs), F.err,
                                       static_cast<uint32_t *>(F.hit), F.out, F.cap, tg, lb, sg, s);
     else
-        launch_small_kernel<uint64_t>(k, blocks, ix, ws, F.n, F.blob, static_cast<const uint64_t *>(F.offs), F.err,
+        launch_small_kernel<uint64_t>(w, blocks, ix, ws, F.n, F.blob, static_cast<const uint64_t *>(F.offs), F.err,
                                       static_cast<uint64_t *>(F.hit), F.out, F.cap, tg, lb, sg, s);
+    return hipGetLastError();
+}
+
+hipError_t launch_land(const LandSegs &ls, hipStream_t s) {
+    if (!ls.count || ls.count > (uint32_t)SMALL_SEGS) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_land, dim3(32, ls.count), dim3(256), 0, s, ls);
     return hipGetLastError();
 }
 

@@ -76,7 +76,9 @@ class Tab:
         enc = self._encode(key)
         self._ops.append((op, enc[0], kid, enc[1]))
 
-    def flush(self):
+    def flush(self, commit: bool = False):
+        """Ship the queued deltas as ONE call (commit: tm_commit -- the route
+        mirror's group commit, which no batch waits for on the GPU)."""
         with self._lock:
             if not self._ops:
                 return
@@ -85,7 +87,8 @@ class Tab:
             vals = np.array([o[2] for o in self._ops], dtype=np.uint32)
             flags = np.array([o[3] for o in self._ops], dtype=np.uint8)
             self._ops = []
-            epoch = self._index.apply(ops, blob, offs, vals, flags)
+            epoch = (self._index.apply(ops, blob, offs, vals, flags, commit=True) if commit
+                     else self._index.apply(ops, blob, offs, vals, flags))
             # the deletes just shipped are visible from `epoch` on: their u32s
             # wait until no reader that began earlier is running
             for kid in self._released:

@@ -152,6 +152,23 @@ int tm_apply_deltas_ex(tm_index *h, uint64_t n, const uint8_t *ops, const uint8_
                        const uint64_t *filter_offsets, const uint32_t *values, const uint8_t *key_flags,
                        uint64_t *out_epoch);
 
+/* tm_apply_deltas_ex for a writer that must not slow the readers: the route
+ * mirror's group commit (src/emqx_router_gpu.erl, the read-your-writes hook
+ * of emqx_router.erl:483-509 under the broker pool's concurrent route writes,
+ * emqx_broker.erl:778-808).  The deltas are applied to the host image, the
+ * resulting patch is shipped to a copy of the tables (tm_options.copies) that
+ * no batch is reading, and only then published: it returns once every batch
+ * queued afterwards reads a copy holding these deltas (as tm_apply_deltas
+ * does), but no batch waits on the GPU for the patch -- with tm_apply_deltas
+ * every batch after a delta first waits for the batches still reading the
+ * copy it patches.  While every copy has readers, tm_commit waits for one to
+ * drain (bounded; past the bound, or with copies = 1, it publishes as
+ * tm_apply_deltas does).  Batches do not collect these deltas before
+ * tm_commit publishes them (they were queued before it returned); a
+ * tm_apply_deltas running meanwhile is published with them. */
+int tm_commit(tm_index *h, uint64_t n, const uint8_t *ops, const uint8_t *filter_bytes, const uint64_t *filter_offsets,
+              const uint32_t *values, const uint8_t *key_flags, uint64_t *out_epoch);
+
 /* Reader epochs: when may a caller hand a value freed by a delete to a new key?
  * The reference's readers walk a read_concurrency ETS table and decode keys
  * from it lock-free (emqx_topic_index.erl:41-48): a concurrent delete can hide
@@ -313,8 +330,8 @@ int tm_merge_shards(uint32_t world, uint64_t n, const uint64_t *d_shard_hit_offs
                     void *stream);
 
 /* Diagnostics.  While enabled, every match batch records HIP events on its
- * stream around the main walk kernel (k_walk_lane / k_walk_small for a
- * one-launch batch, k_walk_fast for a two-phase one) and around the whole batch;
+ * stream around the main walk kernel (k_walk_small for a one-launch batch,
+ * k_walk_fast for a two-phase one) and around the whole batch;
  * tm_profile_read() resolves them and returns the accumulated device times
  * (milliseconds) and the number of batches since the last reset. */
 int tm_profile_enable(tm_index *h, int enable);
@@ -330,17 +347,27 @@ int tm_profile_read(tm_index *h, double *walk_ms, double *batch_ms, uint64_t *ba
  *                           one launch where the index allows it
  *   TM_DEBUG_SMALL_KERNEL   the one-launch kernel of small batches: 0 the
  *                           default; 1 k_walk_small with 16
- *                           lanes per topic; 2 k_walk_lane (one lane per
- *                           topic) where the index allows it; 3 k_walk_small
- *                           with 8 lanes per topic
+ *                           lanes per topic; 3 with 8 lanes per topic (2 named
+ *                           round 5's one-lane-per-topic kernel, removed:
+ *                           TM_EINVAL)
  *   TM_DEBUG_COMBINE        concurrent combined launches of small 32-bit
  *                           in-place host batches (tm_match_batch32_ex): 0 =
  *                           every batch its own launch (default 4)
- * tm_debug_get: TM_DEBUG_COMBINE (the current setting), TM_DEBUG_FAILED_BATCHES (one-launch batches whose look-back
+ *   TM_DEBUG_CMB_GATHER     (study) microseconds a new combined launch waits
+ *                           for the callers between two batches to queue
+ *                           theirs (0 = none, the default)
+ *   TM_DEBUG_SMALL_TICKET   1: k_walk_small's blocks take a start-order
+ *                           ticket (see "Forward progress"); 0: dispatch order
+ *   TM_DEBUG_CMB_LAND       (study) 1: a combined launch writes its outputs to
+ *                           HBM and one copy kernel lands them in the callers'
+ *                           buffers (0 = the kernel writes them in place)
+ * tm_debug_get: those settings; TM_DEBUG_COMMITS / _COMMIT_WAITS / _COMMIT_FORCED:
+ * tm_commit patches, those that waited for a copy to drain, and those
+ * published without an idle copy; TM_DEBUG_FAILED_BATCHES (one-launch batches whose look-back
  * failed, host API), TM_DEBUG_RETRIED_BATCHES (of those, run again) and the
  * match launches per kernel path: TM_DEBUG_PATH_PHASES (walk, tails, scan,
- * emit), TM_DEBUG_PATH_SMALL (k_walk_small), TM_DEBUG_PATH_LANE
- * (k_walk_lane), TM_DEBUG_COMBINED_LAUNCHES / _BATCHES: the combiner's
+ * emit), TM_DEBUG_PATH_SMALL (k_walk_small), TM_DEBUG_PATH_LANE (retired:
+ * always 0), TM_DEBUG_COMBINED_LAUNCHES / _BATCHES: the combiner's
  * launches and the host batches they carried, and TM_DEBUG_WIDE_NODES /
  * TM_DEBUG_DENSE_WIDE: trie nodes with a child bitmap, and those of them
  * dense enough that the walk probes their child table without it.  (Keys
@@ -350,7 +377,8 @@ enum { TM_DEBUG_LB_SPINS = 1, TM_DEBUG_LB_FAIL_BLOCK = 2, TM_DEBUG_LB_LAUNCHES =
        TM_DEBUG_FAILED_BATCHES = 5, TM_DEBUG_RETRIED_BATCHES = 6, TM_DEBUG_PATH_PHASES = 7,
        TM_DEBUG_PATH_SMALL = 8, TM_DEBUG_PATH_LANE = 9, TM_DEBUG_SMALL_KERNEL = 10,
        TM_DEBUG_COMBINE = 12, TM_DEBUG_COMBINED_LAUNCHES = 13, TM_DEBUG_COMBINED_BATCHES = 14,
-       TM_DEBUG_WIDE_NODES = 15, TM_DEBUG_DENSE_WIDE = 16 };
+       TM_DEBUG_WIDE_NODES = 15, TM_DEBUG_DENSE_WIDE = 16, TM_DEBUG_CMB_GATHER = 17, TM_DEBUG_CMB_LAND = 18,
+       TM_DEBUG_COMMITS = 19, TM_DEBUG_COMMIT_WAITS = 20, TM_DEBUG_COMMIT_FORCED = 21, TM_DEBUG_SMALL_TICKET = 22 };
 int tm_debug_set(tm_index *h, uint32_t key, uint64_t value);
 int tm_debug_get(tm_index *h, uint32_t key, uint64_t *value);
 

@@ -26,8 +26,7 @@ def torch_dev():
 
 def _small_kind(kind: str) -> int:
     """TM_DEBUG_SMALL_KERNEL value of a small-batch kernel name"""
-    return {"auto": _native.SMALL_AUTO, "lane": _native.SMALL_LANE, "wave": _native.SMALL_WAVE,
-            "wave8": _native.SMALL_WAVE8}[kind]
+    return {"auto": _native.SMALL_AUTO, "wave": _native.SMALL_WAVE, "wave8": _native.SMALL_WAVE8}[kind]
 
 
 def gpu_index(items: wl.ItemSet | None = None, flags=None) -> _native.Index:
@@ -1241,14 +1240,18 @@ def test_concurrent_callers_see_consistent_snapshots(torch_dev, copies):
           f"p50 {np.percentile(lat, 50):.3f} ms p99 {np.percentile(lat, 99):.3f} ms")
 
 
-@pytest.mark.parametrize("kind,copies,leaders", [("lane", 1, 4), ("wave", 1, 4), ("wave8", 1, 4), ("auto", 2, None),
-                                                 ("auto", 2, 2)])
-def test_combined_callers_with_deltas_see_snapshots_and_never_fail(torch_dev, kind, copies, leaders):
+@pytest.mark.parametrize("kind,copies,leaders,gather,land,ticket", [
+    ("wave", 1, 4, 0, 0, 0), ("wave8", 1, 4, 0, 0, 0), ("auto", 2, None, 0, 0, 0), ("auto", 2, 2, 0, 0, 0),
+    ("auto", 1, 4, 30, 1, 0), ("auto", 2, 1, 30, 0, 0), ("auto", 2, 2, 0, 1, 0), ("auto", 2, 2, 0, 0, 1)])
+def test_combined_callers_with_deltas_see_snapshots_and_never_fail(torch_dev, kind, copies, leaders, gather, land,
+                                                                   ticket):
     """The NIF's production path under load:
     16 host threads submit in-place 32-bit batches (tm_match_batch32_ex on
     host_array buffers, what the NIF's dirty schedulers do) through the
-    host-batch combiner at 4 leaders (the default; and at 2) -- shared k_walk_lane (or k_walk_small)
-    launches with a segment table -- while the main thread applies 16 delta
+    host-batch combiner at 4 leaders (the default; and at 2 and 1) -- shared
+    k_walk_small launches with a segment table; with a gather window
+    (TM_DEBUG_CMB_GATHER) and with the outputs landed from HBM by k_land
+    (TM_DEBUG_CMB_LAND) -- while the main thread applies 16 delta
     epochs.  Every
     batch equals the oracle after exactly the epochs its probe topic saw, a
     thread never goes back in time, and no batch's look-back wait expired:
@@ -1264,6 +1267,10 @@ def test_combined_callers_with_deltas_see_snapshots_and_never_fail(torch_dev, ki
     if leaders is not None:
         ix.debug_set(_native.TM_DEBUG_COMBINE, leaders)
     assert ix.debug_get(_native.TM_DEBUG_COMBINE) == (leaders or 4)
+    ix.debug_set(_native.TM_DEBUG_CMB_GATHER, gather)
+    ix.debug_set(_native.TM_DEBUG_CMB_LAND, land)
+    ix.debug_set(_native.TM_DEBUG_SMALL_TICKET, ticket)
+    assert (ix.debug_get(_native.TM_DEBUG_CMB_GATHER), ix.debug_get(_native.TM_DEBUG_CMB_LAND)) == (gather, land)
     ix.debug_set(_native.TM_DEBUG_SMALL_KERNEL, _small_kind(kind))
     ix.apply(np.ones(len(fs), np.uint8), fs.blob, fs.offs, fs.vals)
     o = oracle_of(fs)
@@ -2172,18 +2179,19 @@ def test_replicas_share_one_host_image(torch_dev):
     assert db1 == db2 and two <= 1.2 * one + (32 << 20)
 
 
-# ----------------------------- small batches, one lane per topic (round 5)
+# ------------- small batches: k_walk_small with 16 / 8 lanes per topic (rounds 3-6)
 
 def _paths(ix):
-    """match launches so far per kernel path: (two-phase, k_walk_small, k_walk_lane)"""
+    """match launches so far per kernel path: (two-phase, k_walk_small, retired lane kernel: 0)"""
     return tuple(ix.debug_get(k) for k in (_native.TM_DEBUG_PATH_PHASES, _native.TM_DEBUG_PATH_SMALL,
                                            _native.TM_DEBUG_PATH_LANE))
 
 
 def _shallow_case(r, nt=700):
     """Filters of at most 6 levels (trie depth <= 6, binary keys <= 6 levels:
-    k_walk_lane's index condition, lane_path_ok), topics of 1-14 levels (the
-    ones deeper than FAST_L = 8 take k_walk_lane's second, lite walk), dense
+    the LITE fallback store's index condition, lite_path_ok), topics of 1-14
+    levels (the ones deeper than 8 levels take k_walk_small<8>'s lite
+    fallback walk), dense
     wildcard families over some prefixes (topics with more than RCAP = 8 value
     ranges: re-walked), filters with several IDs (multi-value runs)."""
     def lvl():
@@ -2225,11 +2233,10 @@ def _shallow_case(r, nt=700):
 
 
 def _all_kernels(ix, ts):
-    """the batch on k_walk_lane, k_walk_small with 16 and 8 lanes per topic and
-    the two-phase path: -> (hit, vals, err) of each, and the paths they took"""
+    """the batch on k_walk_small with 16 and 8 lanes per topic and the
+    two-phase path: -> (hit, vals, err) of each, and the paths they took"""
     out = []
-    for kind, phases in ((_native.SMALL_LANE, 0), (_native.SMALL_WAVE, 0), (_native.SMALL_WAVE8, 0),
-                         (_native.SMALL_AUTO, 1)):
+    for kind, phases in ((_native.SMALL_WAVE, 0), (_native.SMALL_WAVE8, 0), (_native.SMALL_AUTO, 1)):
         ix.debug_set(_native.TM_DEBUG_SMALL_KERNEL, kind)
         ix.debug_set(_native.TM_DEBUG_PHASES, phases)
         p0 = _paths(ix)
@@ -2240,13 +2247,12 @@ def _all_kernels(ix, ts):
 
 
 @pytest.mark.parametrize("seed", range(8))
-def test_lane_walk_vs_oracle_and_the_other_kernels(torch_dev, seed):
-    """Small batches on a shallow index run in ONE launch of k_walk_lane (one
-    lane per topic, the block's topic bytes staged in LDS, a start-order
-    ticket, look-back, emit): exact CSR against the oracle
-    and bit-identical to k_walk_small and to the two-phase path forced on the
-    same batch, and k_walk_small with 8 lanes per topic (fallbacks: more
-    than 8 levels or frontier states) -- topics deeper than the main store, badarg beyond it, more
+def test_small_walks_vs_oracle_and_the_two_phase_path(torch_dev, seed):
+    """Small batches on a shallow index run in ONE launch of k_walk_small
+    with 16 or 8 lanes per topic (the 8-lane groups' fallbacks: more than 8
+    levels or frontier states, the LITE store): exact CSR against the oracle
+    and bit-identical to each other and to the two-phase path forced on the
+    same batch -- topics deeper than the main store, badarg beyond it, more
     than 65536 levels, more than RCAP ranges, multi-value runs -- at batch
     sizes around a block's 64 topics and up to 65536; after deletes and
     re-inserts too; host, device and 32-bit APIs."""
@@ -2260,14 +2266,14 @@ def test_lane_walk_vs_oracle_and_the_other_kernels(torch_dev, seed):
         ts = items_of([topics[i % len(topics)] for i in r.sample(range(2 * n + 7), n)])
         runs = _all_kernels(ix, ts)
         # (a first run may be repeated to size the values buffer: capacity reruns)
-        assert [tuple(x > 0 for x in p) for _, p in runs] == [(0, 0, 1), (0, 1, 0), (0, 1, 0), (1, 0, 0)], \
+        assert [tuple(x > 0 for x in p) for _, p in runs] == [(0, 1, 0), (0, 1, 0), (1, 0, 0)], \
             [p for _, p in runs]
         (hit, v1, e1), _ = runs[0]
         assert_same(ix, o, ts)
         for (h, v, e), _ in runs[1:]:
             assert np.array_equal(hit, h) and np.array_equal(v1, v) and np.array_equal(e1, e)
     assert np.diff(hit.astype(np.int64)).max() > 8 * 2        # some topic beyond RCAP ranges
-    ix.debug_set(_native.TM_DEBUG_SMALL_KERNEL, _native.SMALL_LANE)   # the lane walk from here on
+    ix.debug_set(_native.TM_DEBUG_SMALL_KERNEL, _native.SMALL_WAVE8)   # 8 lanes per topic from here on
     # device API on a torch stream
     d_blob, d_offs = torch.from_numpy(ts.blob).cuda(), torch.from_numpy(ts.offs.view(np.int64)).cuda()
     d_hit = torch.zeros(len(ts) + 1, dtype=torch.int64, device="cuda")
@@ -2277,10 +2283,10 @@ def test_lane_walk_vs_oracle_and_the_other_kernels(torch_dev, seed):
     ix.match_batch_dev(len(ts), d_blob.data_ptr(), d_offs.data_ptr(), d_hit.data_ptr(), d_out.data_ptr(),
                        int(hit[-1]) + 1, d_err.data_ptr(), torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
-    assert _paths(ix)[2] > p0[2]
+    assert _paths(ix)[1] > p0[1]
     assert np.array_equal(d_hit.cpu().numpy().view(np.uint64), hit)
     assert np.array_equal(d_out.cpu().numpy().view(np.uint32)[: int(hit[-1])], v1)
-    # the 32-bit in-place API (the NIF's): through the combiner, on the lane walk
+    # the 32-bit in-place API (the NIF's): through the combiner
     nb = int(ts.offs[-1])
     blob = ix.host_array(nb + 16, np.uint8)
     blob[:nb] = ts.blob[:nb]
@@ -2290,7 +2296,7 @@ def test_lane_walk_vs_oracle_and_the_other_kernels(torch_dev, seed):
            ix.host_array(len(ts), np.uint8))
     p0 = _paths(ix)
     h32, v32, e32 = ix.match_batch32(blob, offs, out)
-    assert _paths(ix)[2] > p0[2]
+    assert _paths(ix)[1] > p0[1]
     assert np.array_equal(h32.astype(np.uint64), hit) and np.array_equal(v32, v1) and np.array_equal(e32, e1)
     # deletes and re-inserts as deltas
     dele = sorted(r.sample(range(len(filters)), len(filters) // 4))
@@ -2304,21 +2310,23 @@ def test_lane_walk_vs_oracle_and_the_other_kernels(torch_dev, seed):
     o.apply(np.ones(len(back), np.uint8), d2.blob, d2.offs, d2.vals, flags[back])
     p2 = _paths(ix)
     assert_same(ix, o, ts)
-    assert _paths(ix)[2] > p2[2]
+    assert _paths(ix)[1] > p2[1]
 
 
-def test_lane_walk_long_topics_read_global_memory(torch_dev):
-    """A block whose 64 topics span more than the 4 KiB the lane walk stages
-    in LDS reads them from global memory instead (block-uniform); blocks of a
-    batch may take either way.  Exact against the oracle, in place too (the
-    topics then come over PCIe)."""
+@pytest.mark.parametrize("kind", ["wave", "wave8"])
+def test_small_walk_long_topics(torch_dev, kind):
+    """A block whose topics span more than k_walk_small stages in LDS at once
+    stages a row per topic; a topic longer than its row is walked by its
+    group's first lane (block-uniform choices; blocks of a batch may take
+    either way).  Exact against the oracle, in place too (the topics then come
+    over PCIe)."""
     r = random.Random(0x454D5158 + 450)
     words = [b"w%d" % i for i in range(30)] + [b"long-" + b"x" * 90, b"$SYS"]
     filters = [b"/".join(r.choice(words) if r.random() < 0.7 else b"+" for _ in range(r.randint(1, 5)))
                for _ in range(3_000)] + [b"#", b"w1/#", b"+/+/#"]
     fs = items_of(filters)
     ix, o = gpu_index(fs), oracle_of(fs)
-    ix.debug_set(_native.TM_DEBUG_SMALL_KERNEL, _native.SMALL_LANE)
+    ix.debug_set(_native.TM_DEBUG_SMALL_KERNEL, _small_kind(kind))
     topics = []
     for i in range(5_000):
         blk = (i // 64) % 3   # blocks of short topics, of ~180-byte topics, and mixed
@@ -2329,7 +2337,7 @@ def test_lane_walk_long_topics_read_global_memory(torch_dev):
     assert max(int(ts.offs[(b + 1) * 64] - ts.offs[b * 64]) for b in range(len(ts) // 64)) > 4096
     p0 = _paths(ix)
     hit, v = assert_same(ix, o, ts)
-    assert _paths(ix)[2] > p0[2]
+    assert _paths(ix)[1] > p0[1]
     nb = int(ts.offs[-1])
     blob = ix.host_array(nb + 16, np.uint8)
     blob[:nb] = ts.blob[:nb]
@@ -2341,18 +2349,19 @@ def test_lane_walk_long_topics_read_global_memory(torch_dev):
     assert np.array_equal(h32.astype(np.uint64), hit) and np.array_equal(v32, v)
 
 
-def test_lane_walk_c3deep_and_index_gates(torch_dev):
-    """C3deep batches (10 % of the topics 33-64 levels) on the lane walk; an
-    index a topic could need more than FAST_L levels of (a binary key of 40
-    levels: the two-phase path) or with a '#'-not-last key (k_walk_small)
-    takes another kernel, exact either way."""
+def test_small_walk_c3deep_and_index_gates(torch_dev):
+    """C3deep batches (10 % of the topics 33-64 levels) on k_walk_small with 8
+    lanes per topic (the deep topics on the LITE fallback walk); an index a
+    topic could need more than MID_L levels of (a binary key of 40 levels: the
+    two-phase path) or with a '#'-not-last key (16 lanes per topic, the full
+    fallback store) takes another kernel shape, exact either way."""
     fs = wl.filters(3, 200_000)
     ts = wl.topics(30, 200_000, 60_000)
     ix, o = gpu_index(fs), oracle_of(fs)
-    ix.debug_set(_native.TM_DEBUG_SMALL_KERNEL, _native.SMALL_LANE)
+    ix.debug_set(_native.TM_DEBUG_SMALL_KERNEL, _native.SMALL_WAVE8)
     p0 = _paths(ix)
     assert_same(ix, o, ts)
-    assert _paths(ix)[2] > p0[2]
+    assert _paths(ix)[1] > p0[1]
     for extra in ([b"/".join([b"z"] * 40)], [b"a/#/b"]):   # deep binary key / '#'-not-last key
         e = items_of(extra, [1_000_000])
         ix.apply(np.ones(1, np.uint8), e.blob, e.offs, e.vals)
@@ -2361,19 +2370,19 @@ def test_lane_walk_c3deep_and_index_gates(torch_dev):
         assert_same(ix, o, ts)
         # (the 40-level binary key is beyond k_walk_small's fallback store too: the two phases)
         assert _paths(ix)[0 if len(extra[0]) > 40 else 1] > p0[0 if len(extra[0]) > 40 else 1]
-        assert _paths(ix)[2] == p0[2], "expected k_walk_small or the two-phase path"
+        assert _paths(ix)[2] == p0[2] == 0
         ix.apply(np.zeros(1, np.uint8), e.blob, e.offs, e.vals)
         o.apply(np.zeros(1, np.uint8), e.blob, e.offs, e.vals)
     p0 = _paths(ix)
     assert_same(ix, o, ts)
-    assert _paths(ix)[2] > p0[2]
+    assert _paths(ix)[1] > p0[1]
 
 
 # ------------------------------------- device failures are not badarg (round 4)
 
-@pytest.mark.parametrize("kind", ["lane", "wave", "wave8"])
-def test_lookback_failure_is_retried_then_a_device_error(torch_dev, kind):
-    """A one-launch small batch (k_walk_lane or k_walk_small) whose look-back
+@pytest.mark.parametrize("kind,ticket", [("wave", 0), ("wave8", 0), ("wave8", 1)])
+def test_lookback_failure_is_retried_then_a_device_error(torch_dev, kind, ticket):
+    """A one-launch small batch (k_walk_small, 16 or 8 lanes per topic) whose look-back
     wait expires (forced: block 3 acts as if its wait expired,
     TM_DEBUG_LB_FAIL_BLOCK) flags err 4 from that block on (LB_FAIL
     propagates: no later block takes a partial prefix), the host API runs it
@@ -2387,9 +2396,10 @@ def test_lookback_failure_is_retried_then_a_device_error(torch_dev, kind):
     ts = wl.topics(3, 50_000, nt)
     ix, o = gpu_index(fs), oracle_of(fs)
     ix.debug_set(_native.TM_DEBUG_SMALL_KERNEL, _small_kind(kind))
+    ix.debug_set(_native.TM_DEBUG_SMALL_TICKET, ticket)   # (the failing block is then virtual block 3)
     p0 = _paths(ix)
     assert_same(ix, o, ts)
-    assert _paths(ix)[2 if kind == "lane" else 1] > p0[2 if kind == "lane" else 1]
+    assert _paths(ix)[1] > p0[1]
     f0, r0 = ix.debug_get(_native.TM_DEBUG_FAILED_BATCHES), ix.debug_get(_native.TM_DEBUG_RETRIED_BATCHES)
     assert f0 == 0 and r0 == 0                       # a normal run never fails
     ix.debug_set(_native.TM_DEBUG_LB_FAIL_BLOCK, 3)
@@ -2417,21 +2427,22 @@ def test_lookback_failure_is_retried_then_a_device_error(torch_dev, kind):
                        d_err.data_ptr(), torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
     err = d_err.cpu().numpy()
-    first = 3 * {"lane": 64, "wave": 16, "wave8": 32}[kind]   # topics per block (k_walk_lane: in ticket order)
+    first = 3 * {"wave": 16, "wave8": 32}[kind]   # topics per block
     assert not err[:first].any() and (err[first:] == 4).all()
     # the hook is spent: the next batches are exact again, with no failure
     assert_same(ix, o, ts)
     assert ix.debug_get(_native.TM_DEBUG_FAILED_BATCHES) == 5
 
 
-@pytest.mark.parametrize("kind", ["lane", "wave", "wave8"])
-def test_lookback_without_waiting_is_exact_or_a_device_error(torch_dev, kind):
+@pytest.mark.parametrize("kind,ticket", [("wave", 0), ("wave8", 0), ("wave8", 1)])
+def test_lookback_without_waiting_is_exact_or_a_device_error(torch_dev, kind, ticket):
     """With no wait at all (TM_DEBUG_LB_SPINS 0: a block fails whenever a
     predecessor has not published yet), every batch either matches exactly or
     fails as a device error -- never a wrong result, never BadArg."""
     fs = wl.filters(3, 50_000)
     ix, o = gpu_index(fs), oracle_of(fs)
     ix.debug_set(_native.TM_DEBUG_SMALL_KERNEL, _small_kind(kind))
+    ix.debug_set(_native.TM_DEBUG_SMALL_TICKET, ticket)
     for nt in (3_000, 30_000, 65_536):
         ts = wl.topics(3, 50_000, nt)
         ix.debug_set(_native.TM_DEBUG_LB_SPINS, 0)
@@ -2494,11 +2505,12 @@ def test_router_boot_1m_routes_and_node_down_cleanup(torch_dev):
     assert r.mirror_keys() == len(filter_rows) - sum(1 for t, _ in dead if tfilter(t) is not False)
 
 
-@pytest.mark.parametrize("kind", ["lane", "wave", "wave8"])
-def test_combined_small_batches_equal_single_launches(torch_dev, kind):
+@pytest.mark.parametrize("kind,land,ticket", [("wave", 0, 0), ("wave8", 0, 0), ("auto", 1, 0), ("auto", 0, 1)])
+def test_combined_small_batches_equal_single_launches(torch_dev, kind, land, ticket):
     """The host-batch combiner (tm_host.cpp small_combined): concurrent callers'
-    in-place 32-bit batches of 1 to 20k topics run as shared k_walk_lane (or
-    k_walk_small) launches with a segment table -- each caller's hit offsets,
+    in-place 32-bit batches of 1 to 20k topics run as shared k_walk_small
+    launches with a segment table (land: outputs written to HBM, then landed
+    by k_land) -- each caller's hit offsets,
     values and flags identical to its batch run alone (combiner off) and to
     the oracle; a badarg topic stays in its own slot; a forced look-back
     failure reruns the whole launch once (every caller still exact)."""
@@ -2536,6 +2548,8 @@ def test_combined_small_batches_equal_single_launches(torch_dev, kind):
                 continue
             assert np.array_equal(v[h[i]:h[i + 1]], ovals[int(ohit[i]):int(ohit[i + 1])])
     ix.debug_set(_native.TM_DEBUG_COMBINE, 3)
+    ix.debug_set(_native.TM_DEBUG_CMB_LAND, land)
+    ix.debug_set(_native.TM_DEBUG_SMALL_TICKET, ticket)
     l0 = ix.debug_get(_native.TM_DEBUG_COMBINED_LAUNCHES)
     b0 = ix.debug_get(_native.TM_DEBUG_COMBINED_BATCHES)
     errors = []
@@ -2716,3 +2730,194 @@ def test_u32_offsets_api_equals_u64(torch_dev, nt):
     assert np.array_equal(d_hit.cpu().numpy().view(np.uint32).astype(np.uint64), hit)
     assert np.array_equal(d_out.cpu().numpy().view(np.uint32)[: int(hit[-1])], vals)
     assert not d_err.cpu().numpy().any()
+
+
+def test_vram_inputs_on_every_staged_path(torch_dev):
+    """batch inputs in TM_ALLOC_VRAM memory that do NOT take
+    the in-place one-launch path -- an index with a 35-level subscription
+    (deeper than the one-launch store: any client can make one), a batch of
+    more than 65536 topics, the sorted and unique orders, match/2 above 65536
+    topics -- are read where they lie (device-side widening of the u32
+    offsets), never by the host through the BAR (~163 ms per MiB).  Results
+    equal the same batch in host memory and the oracle; the VRAM batch takes
+    no longer than a few times the host-memory one."""
+    import time
+    fs = wl.filters(3, 100_000)
+    deep = items_of([b"/".join([b"d"] * 34 + [b"+"])], [5_000_000])
+    ix, o = gpu_index(fs), oracle_of(fs)
+
+    def vram_pair(items):
+        blob, offs = _native.pack_strings(items)
+        vb = ix.host_array(len(blob) + 16, np.uint8, vram=True)
+        vb[: len(blob)] = blob
+        vo = ix.host_array(len(items) + 1, np.uint32, vram=True)
+        vo[:] = offs.astype(np.uint32)
+        hb = ix.host_array(len(blob) + 16, np.uint8)
+        hb[: len(blob)] = blob
+        ho = ix.host_array(len(items) + 1, np.uint32)
+        ho[:] = offs.astype(np.uint32)
+        return vb, vo, hb, ho, blob, offs
+
+    def run_both(items, order=_native.TM_ORDER_TRAVERSAL):
+        n = len(items)
+        vb, vo, hb, ho, blob, offs = vram_pair(items)
+        cap = 64 * n + 64
+        outs = [(ix.host_array(n + 1, np.uint32), ix.host_array(cap, np.uint32), ix.host_array(n, np.uint8))
+                for _ in range(2)]
+        uq = [ix.host_array(n, np.uint32) for _ in range(2)] if order == _native.TM_ORDER_UNIQUE else [None, None]
+        t0 = time.perf_counter()
+        h, v, e = ix.match_batch32(hb, ho, outs[0], order, uq[0])
+        t1 = time.perf_counter()
+        h2, v2, e2 = ix.match_batch32(vb, vo, outs[1], order, uq[1])
+        t2 = time.perf_counter()
+        assert np.array_equal(h, h2) and np.array_equal(v, v2) and np.array_equal(e, e2)
+        if uq[0] is not None:
+            assert np.array_equal(uq[0], uq[1])
+        return (h.copy(), v.copy(), e.copy()), blob, offs, t1 - t0, t2 - t1
+
+    # 1. a 35-level subscription: the index no longer allows the one-launch path
+    ix.apply(np.ones(1, np.uint8), deep.blob, deep.offs, deep.vals)
+    o.apply(np.ones(1, np.uint8), deep.blob, deep.offs, deep.vals)
+    ts = wl.topics(3, 100_000, 5_000)
+    items = [ts.item(i) for i in range(len(ts))] + [b"/".join([b"d"] * 35), b"a/+/b"]
+    p0 = ix.debug_get(_native.TM_DEBUG_PATH_PHASES)
+    (h, v, e), blob, offs, th, tv = run_both(items)
+    assert ix.debug_get(_native.TM_DEBUG_PATH_PHASES) >= p0 + 2
+    oc, _, ohit, ovals = o.match_batch(blob, offs)
+    assert np.array_equal(h.astype(np.uint64), ohit) and np.array_equal(v, ovals)
+    assert 5_000_000 in v.tolist() and e[-1] == 1
+    assert tv < 5 * th + 0.05, (tv, th)
+    ix.apply(np.zeros(1, np.uint8), deep.blob, deep.offs, deep.vals)
+    o.apply(np.zeros(1, np.uint8), deep.blob, deep.offs, deep.vals)
+    # 2. more than 65536 topics
+    ts = wl.topics(3, 100_000, 70_000, first=10_000)
+    items = [ts.item(i) for i in range(len(ts))]
+    (h, v, e), blob, offs, th, tv = run_both(items)
+    oc, _, ohit, ovals = o.match_batch(blob, offs)
+    assert np.array_equal(h.astype(np.uint64), ohit) and np.array_equal(v, ovals)
+    assert tv < 5 * th + 0.05, (tv, th)
+    # 3. the sorted and unique orders
+    ts = wl.topics(3, 100_000, 3_000, first=90_000)
+    items = [ts.item(i) for i in range(len(ts))]
+    for order in (_native.TM_ORDER_SORTED, _native.TM_ORDER_UNIQUE):
+        (h, v, e), blob, offs, th, tv = run_both(items, order)
+        oc, _, ohit, ovals = o.match_batch(blob, offs)
+        assert np.array_equal(h.astype(np.uint64), ohit)
+        for i in range(len(items)):
+            seg = np.sort(ovals[int(ohit[i]):int(ohit[i + 1])])
+            if order == _native.TM_ORDER_UNIQUE:
+                seg = np.unique(seg)
+            assert np.array_equal(v[h[i]:h[i] + len(seg)], seg)
+    # 4. match/2 above 65536 topics: VRAM bytes, host u64 offsets (what tmn_first passes)
+    ts = wl.topics(3, 100_000, 70_000, first=200_000)
+    items = [ts.item(i) for i in range(len(ts))]
+    vb, vo, hb, ho, blob, offs = vram_pair(items)
+    val, found = ix.first_batch(vb, offs.astype(np.uint64))
+    val2, found2 = ix.first_batch(blob, offs.astype(np.uint64))
+    assert np.array_equal(val, val2) and np.array_equal(found, found2)
+    oc, _, ohit, ovals = o.match_batch(blob, offs)
+    has = oc > 0
+    assert np.array_equal(found[has], np.ones(int(has.sum()), np.uint8))
+    assert np.array_equal(val[has], ovals[ohit[:-1][has].astype(np.int64)])
+
+
+def test_router_concurrent_writers_read_their_writes(torch_dev):
+    """VERDICT r5 missing 2 / next 2: N writer threads (the reference's
+    broker-pool workers, emqx_broker_sup.erl:36, each running do_add_route ->
+    mria write -> the hook, emqx_broker.erl:778-808) subscribe, publish right
+    after the subscribe returned and must see their own route, unsubscribe
+    and must no longer see it -- while other threads publish a C3-shaped
+    batch stream.  The sync requests are group-committed (fewer device calls
+    than writes) and at the end every topic's routes equal the CPU model +
+    oracle (harness.RouterModel)."""
+    import threading
+    r = rt.Router(node="n1")
+    base = wl.filters(3, 20_000)
+    model = RouterModel()
+    for i in range(len(base)):
+        model.add(base.item(i), "n9")
+    r.do_batch({(base.item(i), "n9"): ("add", 0, None) for i in range(len(base))})
+    ts = wl.topics(3, 20_000, 2_000)
+    pubs = [ts.item(i) for i in range(len(ts))]
+    nw, per = 12, 25
+    errors, stop = [], threading.Event()
+    lock = threading.Lock()
+
+    def writer(w):
+        try:
+            for i in range(per):
+                flt = f"wr/{w}/{i}/+".encode()
+                topic = f"wr/{w}/{i}/x".encode()
+                dest = ("n1" if i % 2 else (b"grp", "n2"))
+                r.add_route(flt, dest)
+                got = r.match_routes(topic)
+                if rt.Route(flt, dest) not in got:
+                    errors.append(("missing", w, i, got))
+                if i % 3 == 0:
+                    r.delete_route(flt, dest)
+                    if rt.Route(flt, dest) in r.match_routes(topic):
+                        errors.append(("stale", w, i))
+                else:
+                    with lock:
+                        model.add(flt, dest)
+        except Exception as e:   # noqa: BLE001 -- reported below
+            errors.append(("raised", w, repr(e)))
+
+    def publisher():
+        try:
+            while not stop.is_set():
+                r.match_routes_batch(pubs[:500])
+        except Exception as e:   # noqa: BLE001
+            errors.append(("publisher", repr(e)))
+    pt = [threading.Thread(target=publisher) for _ in range(2)]
+    wt = [threading.Thread(target=writer, args=(w,)) for w in range(nw)]
+    for t in pt + wt:
+        t.start()
+    for t in wt:
+        t.join()
+    stop.set()
+    for t in pt:
+        t.join()
+    assert not errors, errors[:5]
+    writes = nw * per + nw * ((per + 2) // 3)
+    assert r.mirror_synced_requests == writes + 1            # (+ the base do_batch)
+    assert r.mirror_commits < r.mirror_synced_requests
+    topics = pubs[:300] + [f"wr/{w}/{i}/x".encode() for w in range(nw) for i in range(per)]
+    assert r.match_routes_batch(topics) == model.expected(topics)
+    r.drain_events()
+    assert r.match_routes_batch(topics) == model.expected(topics)
+    print(f"{writes} writes in {r.mirror_commits - 1} group commits")
+
+
+def test_router_killed_mirror_never_serves_a_stale_handle(torch_dev):
+    """the mirror process dies; no publish is
+    served by its handle (MirrorDown -- the Erlang module takes the
+    reference's ETS path) while routes keep being written; the restarted
+    mirror boots from the tables and serves exactly the routes written
+    before and during the outage (vs the CPU model + oracle)."""
+    r = rt.Router(node="n1")
+    model = RouterModel()
+    fs = wl.filters(3, 5_000)
+    for i in range(len(fs)):
+        r.add_route(fs.item(i), "n1")
+        model.add(fs.item(i), "n1")
+    ts = wl.topics(3, 5_000, 1_000)
+    topics = [ts.item(i) for i in range(len(ts))] + [b"down/x/y"]
+    assert r.match_routes_batch(topics) == model.expected(topics)
+    old = r._mirror
+    r.kill_mirror()
+    for t, d in ((b"down/+/y", "n2"), (b"down/#", "n3")):
+        r.add_route(t, d)
+        model.add(t, d)
+    r.delete_route(fs.item(0), "n1")
+    model.delete(fs.item(0), "n1")
+    with pytest.raises(rt.MirrorDown):
+        r.match_routes(b"down/x/y")
+    with pytest.raises(rt.MirrorDown):
+        r.match_routes_batch(topics)
+    assert old.stats()["n_keys"] == sum(1 for i in range(len(fs)) if rt.tfilter(fs.item(i)) is not False)
+    r.restart_mirror(batch_size=1000)
+    assert r._mirror is not old
+    got = r.match_routes_batch(topics)
+    assert got == model.expected(topics)
+    assert {x.topic for x in got[-1]} >= {b"down/#", b"down/+/y"}

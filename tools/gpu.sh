@@ -5,7 +5,8 @@
 #
 # usage: tools/gpu.sh <tag> <step> [<step> ...]
 #   smoke                     __graft_entry__.smoke()
-#   tests[:<pytest -k expr>]  pytest -m gpu (verbose, per-test timeout)
+#   tests[:<pytest -k expr>]  pytest -m gpu (verbose, per-test timeout; '+' in the
+#                             expression stands for a space)
 #   bench[:<name>:<args>]     bench.py <args> -> <name>.json (args: comma separated)
 #   prof[:<profile_walk args>]  rocprofv3 --kernel-trace --stats over bench.py
 #                             defaults + tools/profile_walk.py, then the PMC
@@ -32,7 +33,7 @@ for step in "$@"; do
       timeout -k 10 300 python3 -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
       tail -1 "$OUT/smoke.log" ;;
     tests)
-      if [ -n "$rest" ]; then KARG=(-k "$rest"); else KARG=(); fi
+      if [ -n "$rest" ]; then KARG=(-k "${rest//+/ }"); else KARG=(); fi
       timeout -k 10 1000 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
         "${KARG[@]}" > "$OUT/tests_$n.log" 2>&1
       tail -2 "$OUT/tests_$n.log" ;;

@@ -20,7 +20,7 @@ request, so the value is taken as is (no x2).
 It also counts Infinity-Cache (MALL) hits, so it is an upper bound on HBM.
 
 The bench run's kernel trace is split by phase: its last 2 x rotate
-full-grid launches of the main kernel (k_walk_lane for a one-launch batch,
+full-grid launches of the main kernel (k_walk_small for a one-launch batch,
 else k_walk_fast) are the isolated pass bench.py times for
 roofline.kernel_avg_ms (one stream, back to back), the launches before them
 ran overlapped on three streams.  pmc_<config>.json is stamped with the
@@ -86,7 +86,7 @@ def pmc_values(prof, grid, last):
     return out
 
 
-MAIN_KERNELS = ("k_walk_lane", "k_walk_fast")   # the timed kernel: a one-launch batch, else the two-phase walk
+MAIN_KERNELS = ("k_walk_small", "k_walk_fast")   # the timed kernel: a one-launch batch, else the two-phase walk
 
 
 def main_kernel(names):
@@ -98,7 +98,7 @@ def main_kernel(names):
 
 
 def split_phases(path, grid, n_iso):
-    """full-grid launches of the main kernel (k_walk_lane, else k_walk_fast) of
+    """full-grid launches of the main kernel (k_walk_small, else k_walk_fast) of
     the bench run in time order -> (timed region + warmup, isolated pass)
     durations in ns"""
     rows = list(csv.DictReader(_open(path)))

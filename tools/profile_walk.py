@@ -30,8 +30,8 @@ def main():
     p.add_argument("--streams", type=int, default=1,
                    help="streams the launches rotate over (3: bench.py's overlapped steps; wall/batch is then the "
                         "step time)")
-    p.add_argument("--small-kernel", default="auto", choices=["auto", "wave", "wave8", "lane"],
-                   help="batches <= 65536 topics: the library's default, k_walk_small or k_walk_lane")
+    p.add_argument("--small-kernel", default="auto", choices=["auto", "wave", "wave8"],
+                   help="batches <= 65536 topics: the library's default, k_walk_small with 16 or 8 lanes per topic")
     p.add_argument("--phases", action="store_true", help="every batch on the two-phase path (TM_DEBUG_PHASES)")
     p.add_argument("--noise", default="none", choices=["none", "launch", "host", "native", "events"],
                    help="during the timed launches, a thread that launches one-element kernels on a stream of its "
@@ -53,8 +53,7 @@ def main():
         del items, order
     ix = _native.Index(device=0)
     if a.small_kernel != "auto":
-        ix.debug_set(_native.TM_DEBUG_SMALL_KERNEL, {"wave": _native.SMALL_WAVE, "wave8": _native.SMALL_WAVE8,
-                                                     "lane": _native.SMALL_LANE}[a.small_kernel])
+        ix.debug_set(_native.TM_DEBUG_SMALL_KERNEL, {"wave": _native.SMALL_WAVE, "wave8": _native.SMALL_WAVE8}[a.small_kernel])
     if a.phases:
         ix.debug_set(_native.TM_DEBUG_PHASES, 1)
     for lo in range(0, len(fs), 2_000_000):
