@@ -113,6 +113,11 @@ def parse():
     p.add_argument("--concurrency", type=int, default=8,
                    help="native caller threads of the concurrent-caller leg (and twice as many; 0 = skip)")
     p.add_argument("--frontier-sample", type=int, default=20_000)
+    p.add_argument("--route-writers", type=int, default=16,
+                   help="route-write leg: writer threads issuing one-key subscribe/unsubscribe writes through a "
+                        "group-committing mirror thread (tm_commit) while --concurrency matcher threads run NIF-shaped "
+                        "batches, on a second index of the same filters with --writes-copies table copies (0 = skip)")
+    p.add_argument("--writes-copies", type=int, default=3)
     p.add_argument("--replicas", type=int, default=0,
                    help="replica-topology leg: one process, one tm_create_replicas index (one host image) over N "
                         "device entries, native feeder threads submitting in-place host batches while a syncer thread "
@@ -526,6 +531,8 @@ def main():
                       for i, k in enumerate(keys)}
     lat_pinned = lat_native
     replicas = replica_leg(a, fs, ix, ts, local) if a.replicas > 0 and rank == 0 else None
+    writes = (route_write_leg(a, fs, ts, local) if a.route_writers > 0 and a.concurrency > 0 and rank == 0
+              and not filter_sharded and not level0 and a.config in ("c3", "c1") else None)
 
     if rank != 0:
         if world > 1:
@@ -704,6 +711,8 @@ def main():
     res.update(res_extra)
     if replicas is not None:
         res["replicas"] = replicas
+    if writes is not None:
+        res["route_writes"] = writes
     if dchunks:
         res["deltas_per_step"] = a.deltas / every
         res["delta_batch"] = {"deltas": a.deltas, "every_steps": every}
@@ -776,6 +785,57 @@ def replica_leg(a, fs, ix, ts, local):
             "build_s": round(t_build, 1), "device_MiB_per_replica": round(st["device_bytes"] / 2**20, 1),
             "parity_sample": {"topics": len(sub), "equal_to_primary_index": exact},
             "legs": legs}
+
+
+def route_write_leg(a, fs, ts, local):
+    """Route writes under publish load (the reference's
+    broker pool runs do_add_route in up to schedulers x 2 workers,
+    emqx_broker_sup.erl:36, emqx_broker.erl:778-808): `--route-writers`
+    threads each subscribe and unsubscribe one key at a time and wait for the
+    mirror to hold it (the read-your-writes hook); ONE mirror thread takes every
+    queued request into ONE tm_commit (src/emqx_router_gpu.erl's group commit),
+    published on a table copy no publish batch is reading; meanwhile
+    --concurrency matcher threads run 4k-topic batches the NIF's way (u32
+    offsets, inputs in TM_ALLOC_VRAM memory, the combiner).  After each
+    subscribe the writer publishes its own topic and must see its route
+    (ryw_misses counts the failures).  The same with tm_apply_deltas as the
+    commit (every publish batch after a write first waits for the batches
+    reading the copy it patches) for comparison.  On a second index of the
+    same filters with --writes-copies copies of the tables."""
+    from emqx_amd import _native
+    t = time.time()
+    wx = _native.Index(device=local, hint_keys=len(fs), copies=a.writes_copies)
+    for lo in range(0, len(fs), 2_000_000):
+        part = fs.slice(lo, min(lo + 2_000_000, len(fs)))
+        wx.apply(np.ones(len(part), np.uint8), part.blob, part.offs, part.vals)
+    t_build = time.time() - t
+    hb = host_bench_lib()
+    lb, nm = 4096, a.concurrency
+    sub = ts.slice(0, nm * lb)
+    hh, _, _ = wx.match_batch(sub.blob, sub.offs)
+    cap = int(np.diff(hh.astype(np.int64)).reshape(nm, lb).sum(axis=1).max()) + 65536
+    legs = []
+    for commit in (1, 0):
+        keys = (_native.TM_DEBUG_COMMITS, _native.TM_DEBUG_COMMIT_WAITS, _native.TM_DEBUG_COMMIT_FORCED,
+                _native.TM_DEBUG_FAILED_BATCHES)
+        c0 = [wx.debug_get(k) for k in keys]
+        out = (ctypes.c_double * 10)()
+        rc = hb.tmb_writers(wx._h, a.route_writers, nm, lb, _native._ptr(sub.blob), _native._ptr(sub.offs), cap, 2.0,
+                            1, commit, out)
+        assert rc == 0, rc
+        c1 = [wx.debug_get(k) for k in keys]
+        legs.append({"commit": "tm_commit" if commit else "tm_apply_deltas",
+                     "writes_per_s": round(out[0], 1), "write_p50_ms": round(out[1], 4),
+                     "write_p99_ms": round(out[2], 4), "group_commits_per_s": round(out[3], 1),
+                     "matcher_topics_per_s": round(out[4], 1), "matcher_p50_ms": round(out[5], 4),
+                     "matcher_p99_ms": round(out[6], 4), "ryw_checks": int(out[7]), "ryw_misses": int(out[8]),
+                     "commits_waiting_for_a_copy": c1[1] - c0[1], "commits_forced": c1[2] - c0[2],
+                     "failed_batches": c1[3] - c0[3]})
+    wx.close()
+    return {"writers": a.route_writers, "matchers": nm, "topics_per_batch": lb, "table_copies": a.writes_copies,
+            "build_s": round(t_build, 1), "legs": legs,
+            "keys": "writer w: 'bench/writer/<w>/<k>' (binary key) and '<that>/+' (word list) alternately, "
+                    "subscribed then unsubscribed"}
 
 
 def host_bench_lib():

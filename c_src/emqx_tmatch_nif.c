@@ -155,11 +155,13 @@ static ERL_NIF_TERM nif_new(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[])
 }
 
 /* apply(Ref, [{Op, FilterBin, U32, Kind}]) -> {ok, Epoch} | {error, Code}
-   One router-syncer batch (emqx_router_syncer.erl:297-356) = one call. */
-static ERL_NIF_TERM nif_apply(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
+   One router-syncer batch (emqx_router_syncer.erl:297-356) = one call.
+   commit(Ref, Deltas): the same through tm_commit -- published on a table copy
+   no publish batch is reading (the route mirror's group commit,
+   src/emqx_router_gpu.erl) */
+static ERL_NIF_TERM apply_deltas(ErlNifEnv *env, const ERL_NIF_TERM argv[], int commit) {
     idx_res *r;
     unsigned n;
-    (void)argc;
     if (!enif_get_resource(env, argv[0], IDX_RT, (void **)&r) || !enif_get_list_length(env, argv[1], &n))
         return enif_make_badarg(env);
     uint64_t epoch = 0;
@@ -189,12 +191,23 @@ static ERL_NIF_TERM nif_apply(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[
     offs[n] = tot;
     blob = enif_alloc(tot + 1);
     for (unsigned i = 0; i < n; i++) memcpy(blob + offs[i], bins[i].data, bins[i].size);
-    int rc = tm_apply_deltas_ex(r->h, n, ops, blob, offs, vals, kinds, &epoch);   /* thread safe, no NIF lock */
+    int rc = commit ? tm_commit(r->h, n, ops, blob, offs, vals, kinds, &epoch)   /* thread safe, no NIF lock */
+                    : tm_apply_deltas_ex(r->h, n, ops, blob, offs, vals, kinds, &epoch);
     res = rc == TM_OK ? enif_make_tuple2(env, A_OK, enif_make_uint64(env, epoch)) : err_term(env, rc);
 out:
     enif_free(ops); enif_free(kinds); enif_free(vals); enif_free(offs); enif_free(bins);
     if (blob) enif_free(blob);
     return res;
+}
+
+static ERL_NIF_TERM nif_apply(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
+    (void)argc;
+    return apply_deltas(env, argv, 0);
+}
+
+static ERL_NIF_TERM nif_commit(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
+    (void)argc;
+    return apply_deltas(env, argv, 1);
 }
 
 /* the topic list's binaries (views into the caller's terms, valid during the call) */
@@ -351,6 +364,7 @@ static ERL_NIF_TERM nif_stats(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[
 static ErlNifFunc funcs[] = {
     {"new", 1, nif_new, ERL_NIF_DIRTY_JOB_IO_BOUND},
     {"apply", 2, nif_apply, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"commit", 2, nif_commit, ERL_NIF_DIRTY_JOB_IO_BOUND},   /* (may wait for a table copy to drain) */
     {"match_batch", 3, nif_match_batch, ERL_NIF_DIRTY_JOB_IO_BOUND},
     {"first_batch", 2, nif_first_batch, ERL_NIF_DIRTY_JOB_IO_BOUND},
     {"read_begin", 1, nif_read_begin, 0},

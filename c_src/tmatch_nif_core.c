@@ -97,7 +97,10 @@ int tmn_pack(tmn_set *s, tm_index *h, uint32_t n, const uint8_t *const *topics, 
 }
 
 int tmn_match(tmn_set *s, tm_index *h, uint32_t n, uint32_t order) {
-    uint32_t *hit = tmn_get(h, &s->hit, 4ull * (n + 1));
+    /* traversal order: (offset, count) pairs (tm_match_batch32_pairs), the
+       launches' blocks never wait for each other; sorted / unique: the CSR */
+    const int pairs = order == TM_ORDER_TRAVERSAL;
+    uint32_t *hit = tmn_get(h, &s->hit, pairs ? 4ull * (2ull * n + 1) : 4ull * (n + 1));
     uint8_t *err = tmn_get(h, &s->err, (uint64_t)n + 1);
     uint32_t *uniq = order == TM_ORDER_UNIQUE ? tmn_get(h, &s->uniq, 4ull * n + 4) : NULL;
     /* capacity: what the set already holds, at least TMN_IDS_PER_TOPIC ids per topic */
@@ -106,14 +109,16 @@ int tmn_match(tmn_set *s, tm_index *h, uint32_t n, uint32_t order) {
     uint32_t *vals = tmn_get(h, &s->vals, 4 * cap);
     if (!hit || !err || !vals || (order == TM_ORDER_UNIQUE && !uniq)) return TM_ENOMEM;
     cap = s->vals.cap / 4;
-    int rc = tm_match_batch32_ex(h, n, s->blob.p, s->offs.p, hit, vals, cap, err, order, uniq);
+    int rc = pairs ? tm_match_batch32_pairs(h, n, s->blob.p, s->offs.p, hit, vals, cap, err)
+                   : tm_match_batch32_ex(h, n, s->blob.p, s->offs.p, hit, vals, cap, err, order, uniq);
     /* TM_ECAP: the offsets are valid, so rerun with room for every id (again
        if concurrent inserts grew the total in between; a few times at most) */
     for (int tries = 0; rc == TM_ECAP && tries < 4; tries++) {
         s->reruns++;
-        vals = tmn_get(h, &s->vals, 4 * hit[n]);
-        rc = vals ? tm_match_batch32_ex(h, n, s->blob.p, s->offs.p, hit, vals, s->vals.cap / 4, err, order, uniq)
-                  : TM_ENOMEM;
+        vals = tmn_get(h, &s->vals, 4ull * (pairs ? hit[2ull * n] : hit[n]));
+        rc = !vals ? TM_ENOMEM
+             : pairs ? tm_match_batch32_pairs(h, n, s->blob.p, s->offs.p, hit, vals, s->vals.cap / 4, err)
+                     : tm_match_batch32_ex(h, n, s->blob.p, s->offs.p, hit, vals, s->vals.cap / 4, err, order, uniq);
     }
     /* err flag 4 (a batch the device failed; the library runs it again and
        returns TM_EDEVICE instead -- checked here all the same): the whole
@@ -141,6 +146,11 @@ int tmn_row(const tmn_set *s, uint32_t n, uint32_t order, uint32_t i, uint64_t *
     (void)n;
     *b = *e = 0;
     if (err[i]) return err[i] <= TMN_ERR_TOO_DEEP ? err[i] : TMN_ERR_DEVICE;
+    if (order == TM_ORDER_TRAVERSAL) {   /* (offset, count) pairs */
+        *b = hit[2ull * i];
+        *e = *b + hit[2ull * i + 1];
+        return 0;
+    }
     *b = hit[i];
     *e = order == TM_ORDER_UNIQUE ? hit[i] + ((const uint32_t *)s->uniq.p)[i] : hit[i + 1];
     return 0;

@@ -64,7 +64,9 @@ void *tmn_get_ex(tm_index *h, tmn_buf *b, uint64_t need, uint32_t flags);
  * the topics exceed 2^32 bytes: never for a broker micro-batch). */
 int tmn_pack(tmn_set *s, tm_index *h, uint32_t n, const uint8_t *const *topics, const uint64_t *lens);
 
-/* matches/3 for the packed batch in `order` (TM_ORDER_*) through
+/* matches/3 for the packed batch in `order` (TM_ORDER_*): traversal order
+ * through tm_match_batch32_pairs (per-topic (offset, count) pairs: the launch's
+ * blocks never wait for each other), sorted / unique through
  * tm_match_batch32_ex -- u32 offsets in and out, half the offset bytes of the
  * in-place batch over PCIe each way: sizes the value
  * buffer from what the set already holds (>= TMN_IDS_PER_TOPIC per topic), and

@@ -26,7 +26,8 @@ EXPORTS = ("tm_create", "tm_destroy", "tm_apply_deltas", "tm_sync", "tm_match_ba
            "tm_stream_release", "tm_match_batch_ex", "tm_match_batch_dev_ex", "tm_sort_segments",
            "tm_matches_filter", "tm_apply_deltas_ex", "tm_read_begin", "tm_read_end", "tm_epoch",
            "tm_create_replicas", "tm_replica_stats", "tm_debug_set", "tm_debug_get", "tm_match_batch32_ex",
-           "tm_match_batch32_dev", "tm_matches_filter_ex", "tm_host_alloc_ex", "tm_commit")
+           "tm_match_batch32_dev", "tm_matches_filter_ex", "tm_host_alloc_ex", "tm_commit",
+           "tm_match_batch32_pairs")
 TM_ALLOC_VRAM = 1
 TM_DEBUG_LB_SPINS, TM_DEBUG_LB_FAIL_BLOCK, TM_DEBUG_LB_LAUNCHES, TM_DEBUG_PHASES = 1, 2, 3, 4
 TM_DEBUG_FAILED_BATCHES, TM_DEBUG_RETRIED_BATCHES = 5, 6
@@ -38,6 +39,8 @@ TM_DEBUG_WIDE_NODES, TM_DEBUG_DENSE_WIDE = 15, 16
 TM_DEBUG_CMB_GATHER, TM_DEBUG_CMB_LAND = 17, 18
 TM_DEBUG_COMMITS, TM_DEBUG_COMMIT_WAITS, TM_DEBUG_COMMIT_FORCED = 19, 20, 21
 TM_DEBUG_SMALL_TICKET = 22
+TM_DEBUG_CMB_SPIN = 23
+TM_DEBUG_PATCH_ZC = 24
 
 
 class NativeUnavailable(RuntimeError):
@@ -114,11 +117,17 @@ def load_library(path: Path | None = None):
         "tm_replica_stats": (i32, [vp, u32, C.POINTER(u64), C.POINTER(C.c_int32)]),
         "tm_match_batch32_ex": (i32, [vp, u64, vp, vp, vp, vp, u64, vp, u32, vp]),
         "tm_match_batch32_dev": (i32, [vp, u64, vp, vp, vp, vp, u64, vp, vp]),
+        "tm_match_batch32_pairs": (i32, [vp, u64, vp, vp, vp, vp, u64, vp]),
         "tm_debug_set": (i32, [vp, u32, u64]),
         "tm_debug_get": (i32, [vp, u32, C.POINTER(u64)]),
     }
     for name, (res, args) in sig.items():
-        f = getattr(lib, name)
+        try:
+            f = getattr(lib, name)
+        except AttributeError:
+            if p == LIB_TMATCH:
+                raise
+            continue   # (an older TM_LIB study build: newer entry points absent)
         f.restype, f.argtypes = res, args
     if path is None:
         _lib = lib
@@ -308,6 +317,20 @@ class Index:
         self._check(self._lib.tm_match_batch32_ex(self._h, n, _ptr(blob), _ptr(offs), _ptr(hit), _ptr(vals), len(vals),
                                                   _ptr(err), order, _ptr(unique_counts)))
         return hit[: n + 1], vals[: int(hit[n])], err[:n]
+
+    def match_batch32_pairs(self, blob: np.ndarray, offs: np.ndarray, out):
+        """tm_match_batch32_pairs: u32 topic offsets in; out = (pairs u32[>= 2n+1],
+        values u32[cap], err u8[>= n]) -> (pairs[:2n+1], values, err[:n]);
+        topic i's values are values[pairs[2i] : pairs[2i] + pairs[2i+1]]
+        (disjoint spans, not in topic order).  In place, through the combiner,
+        when every buffer comes from host_array()."""
+        n = len(offs) - 1
+        pairs, vals, err = out
+        if offs.dtype != np.uint32 or pairs.dtype != np.uint32 or len(pairs) < 2 * n + 1 or len(err) < n:
+            raise ValueError("match_batch32_pairs: u32 offsets and large enough outputs expected")
+        self._check(self._lib.tm_match_batch32_pairs(self._h, n, _ptr(blob), _ptr(offs), _ptr(pairs), _ptr(vals),
+                                                     len(vals), _ptr(err)))
+        return pairs[: 2 * n + 1], vals, err[:n]
 
     def match_batch32_dev(self, n: int, d_blob: int, d_offs: int, d_hit: int, d_out: int, cap: int, d_err: int,
                           stream: int | None = None):

@@ -49,6 +49,8 @@ int (*apply_deltas)(tm_index *, uint64_t, const uint8_t *, const uint8_t *, cons
                     const uint8_t *);
 int (*commit)(tm_index *, uint64_t, const uint8_t *, const uint8_t *, const uint64_t *, const uint32_t *,
               const uint8_t *, uint64_t *);   // optional (ABI 1.10)
+int (*match_pairs)(tm_index *, uint64_t, const uint8_t *, const uint32_t *, uint32_t *, uint32_t *, uint64_t,
+                   uint8_t *);                 // optional (ABI 1.10)
 int (*stream_release)(tm_index *, void *);
 int (*match_batch32)(tm_index *, uint64_t, const uint8_t *, const uint32_t *, uint32_t *, uint32_t *, uint64_t,
                      uint8_t *, uint32_t, uint32_t *);
@@ -72,6 +74,7 @@ struct Caller {
     uint64_t n, cap;
     uint8_t *blob = nullptr; uint64_t *offs = nullptr, *hit = nullptr; uint32_t *vals = nullptr; uint8_t *err = nullptr;
     uint32_t *offs32 = nullptr, *hit32 = nullptr;   // mode 4: tm_match_batch32_ex (u32 offsets)
+    uint32_t *pairs32 = nullptr;                     // modes 6, 7: tm_match_batch32_pairs
     // mode 5: mode 4 with the inputs in TM_ALLOC_VRAM memory, written by the
     // caller before every batch (as a NIF packs each micro-batch)
     uint8_t *vblob = nullptr; uint32_t *voffs32 = nullptr; uint64_t nbytes = 0;
@@ -91,7 +94,8 @@ struct Caller {
         if ((rc = api::host_alloc(h, nb + 16, (void **)&blob)) || (rc = api::host_alloc(h, 8 * (nt + 1), (void **)&offs)) ||
             (rc = api::host_alloc(h, 8 * (nt + 1), (void **)&hit)) || (rc = api::host_alloc(h, 4 * cap, (void **)&vals)) ||
             (rc = api::host_alloc(h, nt + 1, (void **)&err)) || (rc = api::host_alloc(h, 4 * (nt + 1), (void **)&offs32)) ||
-            (rc = api::host_alloc(h, 4 * (nt + 1), (void **)&hit32)))
+            (rc = api::host_alloc(h, 4 * (nt + 1), (void **)&hit32)) ||
+            (rc = api::host_alloc(h, 4 * (2 * nt + 1), (void **)&pairs32)))
             return rc;
         memcpy(blob, tb + b0, nb);
         for (uint64_t i = 0; i <= nt; i++) offs[i] = to[first + i] - b0;
@@ -126,6 +130,15 @@ struct Caller {
             memcpy(voffs32, offs32, 4 * (n + 1));
             return api::match_batch32(h, n, vblob, voffs32, hit32, vals, cap, err, TM_ORDER_TRAVERSAL, nullptr);
         }
+        if (mode == 6 || mode == 7) {   // the NIF's pairs call; 6: inputs in TM_ALLOC_VRAM memory, 7: pinned
+            if (!api::match_pairs) return TM_EINVAL;
+            if (mode == 6) {
+                memcpy(vblob, blob, nbytes);
+                memcpy(voffs32, offs32, 4 * (n + 1));
+                return api::match_pairs(h, n, vblob, voffs32, pairs32, vals, cap, err);
+            }
+            return api::match_pairs(h, n, blob, offs32, pairs32, vals, cap, err);
+        }
         if (!s) return api::match_batch(h, n, blob, offs, hit, vals, cap, err);
         const bool hin = mode == 3, hout = mode == 2;
         int rc = api::match_batch_dev(h, n, hin ? mapped(blob) : dblob, hin ? mapped(offs) : doffs,
@@ -136,7 +149,7 @@ struct Caller {
     }
     void fini() {
         for (void *p : {(void *)blob, (void *)offs, (void *)hit, (void *)vals, (void *)err, (void *)offs32, (void *)hit32,
-                        (void *)vblob, (void *)voffs32})
+                        (void *)vblob, (void *)voffs32, (void *)pairs32})
             if (p) api::host_free(h, p);
         if (s) {
             for (void *p : {(void *)dblob, (void *)doffs, (void *)dhit, (void *)dvals, (void *)derr}) if (p) (void)hipFree(p);
@@ -159,6 +172,7 @@ int tmb_bind(void *lib) {
     api::match_batch_dev = reinterpret_cast<decltype(api::match_batch_dev)>(dlsym(lib, "tm_match_batch_dev"));
     api::apply_deltas = reinterpret_cast<decltype(api::apply_deltas)>(dlsym(lib, "tm_apply_deltas"));
     api::commit = reinterpret_cast<decltype(api::commit)>(dlsym(lib, "tm_commit"));
+    api::match_pairs = reinterpret_cast<decltype(api::match_pairs)>(dlsym(lib, "tm_match_batch32_pairs"));
     api::stream_release = reinterpret_cast<decltype(api::stream_release)>(dlsym(lib, "tm_stream_release"));
     api::match_batch32 = reinterpret_cast<decltype(api::match_batch32)>(dlsym(lib, "tm_match_batch32_ex"));
     api::match_batch32_dev = reinterpret_cast<decltype(api::match_batch32_dev)>(dlsym(lib, "tm_match_batch32_dev"));
@@ -174,7 +188,7 @@ int tmb_single_ex(tm_index *h, uint64_t n, const uint8_t *tb, const uint64_t *to
     Caller c;
     int rc = c.init(h, n, tb, to, 0, cap);
     if (rc) return rc;
-    if (mode == 5 && (rc = c.to_vram())) return rc;
+    if ((mode == 5 || mode == 6) && (rc = c.to_vram())) return rc;
     c.mode = mode ? mode : 1;
     std::vector<double> lat;
     for (int k = 0; k < iters + 3 && !rc; k++) {
@@ -204,7 +218,9 @@ int tmb_single(tm_index *h, uint64_t n, const uint8_t *tb, const uint64_t *to, u
 // 2: inputs in HBM, outputs written into the mapped host buffers; 3: inputs
 // read from the mapped host buffers, outputs in HBM; 4: in place with u32
 // offsets (tm_match_batch32_ex, what the NIF calls); 5: mode 4 with the inputs
-// in TM_ALLOC_VRAM memory the caller writes before every batch.
+// in TM_ALLOC_VRAM memory the caller writes before every batch; 6: mode 5
+// through tm_match_batch32_pairs ((offset, count) pairs: what the NIF binds);
+// 7: pairs with the inputs in pinned host memory.
 // out: [batches, topics_per_s, p50_ms, p99_ms, deltas_per_s, seconds]
 int tmb_callers_ex(tm_index *h, int nthreads, uint64_t n, const uint8_t *tb, const uint64_t *to, uint64_t cap,
                    double seconds, int churn_ops, int device_buffers, double *out) {
@@ -212,7 +228,7 @@ int tmb_callers_ex(tm_index *h, int nthreads, uint64_t n, const uint8_t *tb, con
     for (int k = 0; k < nthreads; k++) {
         int rc = cs[k].init(h, n, tb, to, (uint64_t)k * n, cap);
         if (rc) return rc;
-        if (device_buffers == 5 && (rc = cs[k].to_vram())) return rc;
+        if ((device_buffers == 5 || device_buffers == 6) && (rc = cs[k].to_vram())) return rc;
         if (device_buffers && device_buffers < 4 && (rc = cs[k].to_device())) return rc;
         cs[k].mode = device_buffers;
         if ((rc = cs[k].run())) return rc;   // warm: lane, workspace
@@ -313,8 +329,8 @@ int tmb_writers(tm_index *h, int nwriters, int nmatch, uint64_t n, const uint8_t
     for (int k = 0; k < nmatch; k++) {
         int rc = cs[k].init(h, n, tb, to, (uint64_t)k * n, cap);
         if (rc) return rc;
-        cs[k].mode = 4;
-        if (cs[k].to_vram() == TM_OK) cs[k].mode = 5;
+        cs[k].mode = api::match_pairs ? 7 : 4;   // the NIF's call: pairs, inputs in VRAM where it can
+        if (cs[k].to_vram() == TM_OK) cs[k].mode = api::match_pairs ? 6 : 5;
         if ((rc = cs[k].run())) return rc;
     }
     std::vector<std::vector<double>> mlat(nmatch), wlat(nwriters);
@@ -361,8 +377,11 @@ int tmb_writers(tm_index *h, int nwriters, int nmatch, uint64_t n, const uint8_t
         });
     for (int w = 0; w < nwriters; w++)
         th.emplace_back([&, w] {
-            // the one-topic batch a writer publishes after its subscribe (pinned: in place)
-            uint8_t *pb = nullptr; uint64_t *po = nullptr, *ph = nullptr; uint32_t *pv = nullptr; uint8_t *pe = nullptr;
+            // the one-topic batch a writer publishes after its subscribe: the
+            // NIF's call (u32 offsets, pinned buffers: in place, through the
+            // combiner -- it shares launches with the matchers' batches, as a
+            // publish goes through the broker's micro-batcher)
+            uint8_t *pb = nullptr; uint32_t *po = nullptr, *ph = nullptr; uint32_t *pv = nullptr; uint8_t *pe = nullptr;
             if (check && (api::host_alloc(h, 256, (void **)&pb) || api::host_alloc(h, 16, (void **)&po) ||
                           api::host_alloc(h, 16, (void **)&ph) || api::host_alloc(h, 4 * 4096, (void **)&pv) ||
                           api::host_alloc(h, 16, (void **)&pe))) { err = -2; return; }
@@ -386,8 +405,11 @@ int tmb_writers(tm_index *h, int nwriters, int nmatch, uint64_t n, const uint8_t
                     if (op == 1 && check) {
                         const std::string t = words ? topic + "/x" : topic;
                         memcpy(pb, t.data(), t.size());
-                        po[0] = 0; po[1] = t.size();
-                        if (api::match_batch(h, 1, pb, po, ph, pv, 4096, pe)) { err = -3; break; }
+                        po[0] = 0; po[1] = (uint32_t)t.size();
+                        if (api::match_batch32(h, 1, pb, po, ph, pv, 4096, pe, TM_ORDER_TRAVERSAL, nullptr)) {
+                            err = -3;
+                            break;
+                        }
                         bool seen = false;
                         for (uint64_t i = ph[0]; i < ph[1] && i < 4096; i++) seen |= pv[i] == r.val;
                         ryw_checks++;

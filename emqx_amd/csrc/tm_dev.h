@@ -88,6 +88,7 @@ struct Workspace {
     uint2 *deep_stk;      // [DEEP_LANES * (MAX_LEVELS + 1)]
     uint8_t *deep_plus;   // [DEEP_LANES * MAX_LEVELS] '+' levels of each deep lane's path
     uint64_t *look;       // [(n / SM_TOPICS + 4) * LB_STRIDE] one-launch kernels: per block, one look-back word (lb_word)
+    uint32_t *pairs;      // [2 * SMALL_SEGS] pairs launches: per segment, its values counter and block ticket (zero between launches)
     // list lengths of the last count-mode batch that finished here ([0, L_COUNT))
     // and its topic count ([L_COUNT]; 0: none yet), written by the device into
     // mapped host memory: the next batch sizes its tail grids from them;
@@ -147,7 +148,10 @@ struct SmallSeg {
     const uint8_t *blob; const void *offs; void *hit; uint8_t *err; uint32_t *out;
     uint64_t cap; uint32_t n, block0;
 };
-struct SmallSegs { uint32_t count, pad; SmallSeg s[SMALL_SEGS]; };
+// pairs: the launch writes per-topic (first position, count) pairs instead of
+// a CSR (hit[2 t], hit[2 t + 1]; hit[2 n] = the values' total; u32 offsets
+// only): tm_match_batch32_pairs
+struct SmallSegs { uint32_t count, pairs; SmallSeg s[SMALL_SEGS]; };
 hipError_t launch_small_segs(const DevIndex &ix, const Workspace &ws, const SmallSegs &sg, bool u32, uint32_t tag,
                              LbCtl lb, int small_kind, hipStream_t s, int *path = nullptr);
 // The combiner's results landed from HBM (TM_DEBUG_CMB_LAND): segment k's hit

@@ -127,8 +127,10 @@ struct Lane {
 // every replica has applied the patch it holds (a lagging replica is brought
 // up on its patch stream then).
 constexpr int PATCH_RING = 16;
+constexpr uint64_t PATCH_ZC_MAX = 64 << 10;   // patches up to this size are read in place by the patch kernel
 struct PatchSlot {
     uint8_t *pin = nullptr; uint64_t pin_cap = 0;
+    uint8_t *pin_dev = nullptr;               // its device address (mapped: small patches are read in place)
     uint64_t bytes = 0, nr = 0, seq = 0;      // the patch held: size, runs, number (0: none)
 };
 
@@ -266,6 +268,7 @@ struct tm_index {
     // large batches
     LbCtl dbg_lb{LB_SPINS, NONE, 0};
     uint32_t small_ticket = 0;      // TM_DEBUG_SMALL_TICKET: k_walk_small's blocks take start-order tickets
+    bool patch_zc = true;           // TM_DEBUG_PATCH_ZC: small patches read in place from pinned memory
     uint64_t dbg_lb_launches = 0;
     bool dbg_phases = false;        // TM_DEBUG_PHASES: small batches on the two-phase path too (tests)
     int small_kind = SMALL_AUTO;    // TM_DEBUG_SMALL_KERNEL: which one-launch kernel takes small batches
@@ -286,6 +289,7 @@ struct tm_index {
     std::atomic<int> cmb_leaders{CMB_LEADERS};
     std::atomic<int> cmb_gather_us{0};   // TM_DEBUG_CMB_GATHER
     std::atomic<int> cmb_land{0};        // TM_DEBUG_CMB_LAND
+    std::atomic<int> cmb_spin_us{0};     // TM_DEBUG_CMB_SPIN: a waiting caller spins this long before it sleeps
     std::atomic<uint64_t> cmb_launches{0}, cmb_batches{0};
 };
 
@@ -1398,9 +1402,18 @@ int apply_patch(tm_index *ix, int r, uint64_t q, hipStream_t st) {
     for (auto &l : ix->lanes)
         if (l->r == r && l->used && l->s != st) HIPCHK(ix, hipStreamWaitEvent(st, l->done, 0));
     if (R.last_patch) HIPCHK(ix, hipStreamWaitEvent(st, R.last_patch, 0));
-    HIPCHK(ix, hipMemcpyAsync(R.pdev[k], p.pin, p.bytes, hipMemcpyHostToDevice, st));
-    HIPCHK(ix, launch_patch(reinterpret_cast<const PatchRun *>(R.pdev[k]),
-                            reinterpret_cast<const uint32_t *>(R.pdev[k] + p.nr * sizeof(PatchRun)), p.nr,
+    // a small patch (a route write's few runs) is read by the patch kernel
+    // straight from the mapped pinned slot: one command on the stream instead
+    // of a DMA copy and the kernel behind it (the slot is reused only after
+    // pdone, recorded behind the kernel); larger ones are copied first
+    const uint8_t *src = R.pdev[k];
+    if (ix->patch_zc && p.pin_dev && p.bytes <= PATCH_ZC_MAX) {
+        src = p.pin_dev;
+    } else {
+        HIPCHK(ix, hipMemcpyAsync(R.pdev[k], p.pin, p.bytes, hipMemcpyHostToDevice, st));
+    }
+    HIPCHK(ix, launch_patch(reinterpret_cast<const PatchRun *>(src),
+                            reinterpret_cast<const uint32_t *>(src + p.nr * sizeof(PatchRun)), p.nr,
                             patch_bases(ix, r), st));
     HIPCHK(ix, hipEventRecord(R.pdone[k], st));
     R.ppending[k] = true;
@@ -1488,9 +1501,11 @@ int collect_patch_locked2(tm_index *ix) {
         p.pin_cap = 0;
         const uint64_t want = std::max<uint64_t>(bytes * 2, 1u << 20);
         uint8_t *np = nullptr;   // the capacity is recorded only once the buffer exists
-        HIPCHK(ix, hipHostMalloc(&np, want, hipHostMallocPortable));
+        HIPCHK(ix, hipHostMalloc(&np, want, hipHostMallocPortable | hipHostMallocMapped));
         p.pin = np;
         p.pin_cap = want;
+        void *dp = nullptr;
+        p.pin_dev = hipHostGetDevicePointer(&dp, np, 0) == hipSuccess ? static_cast<uint8_t *>(dp) : nullptr;
     }
     memcpy(p.pin, runs.data(), nr * sizeof(PatchRun));
     memcpy(p.pin + nr * sizeof(PatchRun), data.data(), nw * 4);
@@ -1587,7 +1602,7 @@ DevIndex dev_view_build(tm_index *ix, int r) {
 // ------------------------------------------------------------------ lanes
 
 void free_workspace(Workspace &w) {
-    void *wb[] = {w.cnt, w.nr, w.rng, w.lists, w.list_n, w.blk, w.deep_wid, w.deep_stk, w.deep_plus, w.look};
+    void *wb[] = {w.cnt, w.nr, w.rng, w.lists, w.list_n, w.blk, w.deep_wid, w.deep_stk, w.deep_plus, w.look, w.pairs};
     for (void *p : wb) if (p) (void)hipFree(p);
     if (w.hint_h) (void)hipHostFree(w.hint_h);
     w = Workspace{};
@@ -1723,6 +1738,8 @@ int ensure_ws(tm_index *ix, uint64_t n, Lane &ln) {
         HIPCHK(ix, hipMalloc(&w.deep_plus, (uint64_t)DEEP_LANES * MAX_LEVELS));
         HIPCHK(ix, hipMalloc(&w.list_n, LIST_SLOTS * 4));
         HIPCHK(ix, hipMemsetAsync(w.list_n, 0, LIST_SLOTS * 4, ln.s));
+        HIPCHK(ix, hipMalloc(&w.pairs, 2 * SMALL_SEGS * 4));
+        HIPCHK(ix, hipMemsetAsync(w.pairs, 0, 2 * SMALL_SEGS * 4, ln.s));
         HIPCHK(ix, hipHostMalloc(&w.hint_h, HINT_WORDS * 4, hipHostMallocMapped));
         std::memset(w.hint_h, 0, HINT_WORDS * 4);
         HIPCHK(ix, hipHostGetDevicePointer(reinterpret_cast<void **>(&w.hint_d), w.hint_h, 0));
@@ -2001,16 +2018,16 @@ int tm_commit(tm_index *ix, uint64_t n, const uint8_t *ops, const uint8_t *fb, c
     int left = ix->ngroups;
     for (;;) {
         const bool late = std::chrono::steady_clock::now() - t0 > COMMIT_WAIT;
+        bool busy[MAX_REPLICAS] = {};   // copies with a batch still reading them (one event query per lane)
+        for (auto &l : ix->lanes)
+            if (l->used && !busy[l->r] && hipEventQuery(l->done) == hipErrorNotReady) busy[l->r] = true;
         for (int gi = 0; gi < ix->ngroups; gi++) {
             if (done[gi]) continue;
             int pick = -1, copies = 0;
             for (int r = 0; r < ix->nrep; r++) {
                 if (ix->rep[r].group != gi) continue;
                 copies++;
-                bool idle = true;
-                for (auto &l : ix->lanes)
-                    if (l->r == r && l->used && hipEventQuery(l->done) == hipErrorNotReady) { idle = false; break; }
-                if (idle && (pick < 0 || ix->rep[r].applied > ix->rep[pick].applied)) pick = r;
+                if (!busy[r] && (pick < 0 || ix->rep[r].applied > ix->rep[pick].applied)) pick = r;
             }
             if (pick < 0 && copies > 1 && !late) continue;   // wait for a copy to drain
             if (pick >= 0) {
@@ -2369,9 +2386,11 @@ struct SmallReq {
     uint64_t n;
     const uint8_t *db; const uint8_t *dof; uint8_t *dh; uint8_t *de; uint8_t *dv;
     uint64_t cap;
+    bool pairs = false;         // (offset, count) pairs out (tm_match_batch32_pairs); a launch carries one kind
     int rc = TM_OK;
     bool done = false;
     std::condition_variable cv;
+    std::atomic<int> poke{0};   // done, or it may lead: a spinning waiter stops spinning
 };
 constexpr int CMB_LEGACY = 1;   // (not a TM_ code) the index no longer allows the one-launch path
 constexpr uint64_t CMB_HW_NS = 2000000;   // the high-water mark's memory (2 ms)
@@ -2402,6 +2421,8 @@ static int run_small_group(tm_index *ix, const std::vector<SmallReq *> &grp, uin
     SmallSegs sg{};
     LandSegs ls{};
     sg.count = ls.count = (uint32_t)grp.size();
+    sg.pairs = grp[0]->pairs ? 1u : 0u;
+    if (sg.pairs && land) return fail(ix, TM_EINVAL, "tm_match_batch32_pairs: TM_DEBUG_CMB_LAND takes CSR batches only");
     uint64_t at = 0;
     for (size_t k = 0; k < grp.size(); k++) {
         const SmallReq &r = *grp[k];
@@ -2482,11 +2503,12 @@ static int small_combined(tm_index *ix, SmallReq &rq) {
             }
             std::vector<SmallReq *> grp;
             uint64_t total = 0;
-            while (!ix->cmb_q.empty() && grp.size() < (size_t)SMALL_SEGS &&
-                   total + ix->cmb_q.front()->n <= ZC_TOPICS) {
-                total += ix->cmb_q.front()->n;
-                grp.push_back(ix->cmb_q.front());
-                ix->cmb_q.pop_front();
+            const bool pairs = ix->cmb_q.front()->pairs;   // a launch carries one output kind: the front's
+            for (auto it = ix->cmb_q.begin(); it != ix->cmb_q.end() && grp.size() < (size_t)SMALL_SEGS;) {
+                if ((*it)->pairs != pairs || total + (*it)->n > ZC_TOPICS) { ++it; continue; }
+                total += (*it)->n;
+                grp.push_back(*it);
+                it = ix->cmb_q.erase(it);
             }
             ix->cmb_inflight += (int)grp.size();
             if (!ix->cmb_q.empty() && ix->cmb_running < ix->cmb_leaders.load()) ix->cmb_q.front()->cv.notify_one();
@@ -2502,12 +2524,24 @@ static int small_combined(tm_index *ix, SmallReq &rq) {
             for (auto *r : grp) {
                 r->rc = rc;
                 r->done = true;
-                if (r != &rq) r->cv.notify_one();
+                if (r != &rq) { r->poke.store(1, std::memory_order_release); r->cv.notify_one(); }
             }
             ix->cmb_inflight -= (int)grp.size();
             ix->cmb_running--;
-            if (!ix->cmb_q.empty()) ix->cmb_q.front()->cv.notify_one();   // it may lead now
+            if (!ix->cmb_q.empty()) {   // it may lead now
+                ix->cmb_q.front()->poke.store(1, std::memory_order_release);
+                ix->cmb_q.front()->cv.notify_one();
+            }
             continue;
+        }
+        const int spin = ix->cmb_spin_us.load(std::memory_order_relaxed);
+        if (spin > 0) {   // TM_DEBUG_CMB_SPIN: spin a while before sleeping (no futex wake-up on the reply path)
+            rq.poke.store(0, std::memory_order_relaxed);
+            lk.unlock();
+            const uint64_t dl = ns_now() + (uint64_t)spin * 1000;
+            while (!rq.poke.load(std::memory_order_acquire) && ns_now() < dl) __builtin_ia32_pause();
+            lk.lock();
+            if (rq.done || rq.poke.load(std::memory_order_relaxed)) continue;
         }
         rq.cv.wait(lk);
     }
@@ -2760,6 +2794,51 @@ int tm_match_batch32_ex(tm_index *ix, uint64_t n, const uint8_t *tb, const uint3
     return rc;
 }
 
+// (offset, count) pairs (include/tmatch.h): an in-place batch the one-launch
+// kernel takes runs through the combiner as a pairs launch -- no look-back,
+// so no block waits for another; any other batch takes the CSR path and is
+// converted on the host.
+int tm_match_batch32_pairs(tm_index *ix, uint64_t n, const uint8_t *tb, const uint32_t *to, uint32_t *out_pairs,
+                           uint32_t *out_vals, uint64_t cap, uint8_t *out_err) {
+    if (!ix) return fail(nullptr, TM_EINVAL, "tm_match_batch32_pairs: null handle");
+    if (!to || !out_pairs || !out_err || (n && !tb && to[n] != to[0]))
+        return fail(ix, TM_EINVAL, "tm_match_batch32_pairs: null buffer");
+    if (n >= 0x7FFFFFFFull) return fail(ix, TM_EINVAL, "tm_match_batch32_pairs: batch too large");
+    if (cap > 0xFFFFFFFFull) cap = 0xFFFFFFFFull;
+    if (!n) { out_pairs[0] = 0; return TM_OK; }
+    if (n <= ZC_TOPICS && ((uintptr_t)tb & 15) == 0) {
+        const uint64_t nbytes = to[n];   // (before the lock: in TM_ALLOC_VRAM memory a host read is a PCIe round trip)
+        SmallReq rq;
+        {
+            std::lock_guard<std::mutex> g(ix->mu);
+            rq.db = nbytes ? pinned_dev(ix, tb, nbytes) : nullptr;
+            rq.dof = pinned_dev(ix, to, (n + 1) * 4);
+            rq.dh = pinned_dev(ix, out_pairs, (2 * n + 1) * 4);
+            rq.dv = out_vals ? pinned_dev(ix, out_vals, cap * 4) : nullptr;
+            rq.de = pinned_dev(ix, out_err, n);
+        }
+        if ((rq.db || !nbytes) && rq.dof && rq.dh && (rq.dv || !out_vals) && rq.de) {
+            rq.n = n; rq.cap = rq.dv ? cap : 0; rq.pairs = true;
+            const int rc = small_combined(ix, rq);
+            if (rc != CMB_LEGACY) {
+                if (rc) return rc;
+                return (out_vals && out_pairs[2 * n] > cap) ? TM_ECAP : TM_OK;
+            }
+        }
+    }
+    std::vector<uint32_t> h;
+    try {
+        h.resize(n + 1);
+    } catch (const std::bad_alloc &) {
+        return fail(ix, TM_ENOMEM, "tm_match_batch32_pairs: out of host memory");
+    }
+    const int rc = tm_match_batch32_ex(ix, n, tb, to, h.data(), out_vals, cap, out_err, TM_ORDER_TRAVERSAL, nullptr);
+    if (rc != TM_OK && rc != TM_ECAP) return rc;
+    for (uint64_t i = 0; i < n; i++) { out_pairs[2 * i] = h[i]; out_pairs[2 * i + 1] = h[i + 1] - h[i]; }
+    out_pairs[2 * n] = h[n];
+    return rc;
+}
+
 int tm_match_batch32_dev(tm_index *ix, uint64_t n, const uint8_t *bytes, const uint32_t *offs, uint32_t *hit_offs,
                          uint32_t *out, uint64_t cap, uint8_t *err, void *stream) {
     if (!ix) return fail(nullptr, TM_EINVAL, "tm_match_batch32_dev: null handle");
@@ -2899,7 +2978,9 @@ int tm_debug_set(tm_index *ix, uint32_t key, uint64_t value) {
     case TM_DEBUG_COMBINE: ix->cmb_leaders = value > 16 ? 16 : (int)value; break;
     case TM_DEBUG_CMB_GATHER: ix->cmb_gather_us = value > 1000 ? 1000 : (int)value; break;
     case TM_DEBUG_CMB_LAND: ix->cmb_land = value != 0; break;
+    case TM_DEBUG_CMB_SPIN: ix->cmb_spin_us = value > 1000 ? 1000 : (int)value; break;
     case TM_DEBUG_SMALL_TICKET: ix->small_ticket = value != 0; break;
+    case TM_DEBUG_PATCH_ZC: ix->patch_zc = value != 0; break;
     case TM_DEBUG_SMALL_KERNEL:
         if (value != SMALL_AUTO && value != SMALL_WAVE && value != SMALL_WAVE8)
             return fail(ix, TM_EINVAL, "tm_debug_set: TM_DEBUG_SMALL_KERNEL is 0, 1 or 3 (2, the lane kernel, was removed)");
@@ -2921,8 +3002,10 @@ int tm_debug_get(tm_index *ix, uint32_t key, uint64_t *value) {
     case TM_DEBUG_COMBINE: *value = (uint64_t)ix->cmb_leaders.load(); break;
     case TM_DEBUG_CMB_GATHER: *value = (uint64_t)ix->cmb_gather_us.load(); break;
     case TM_DEBUG_CMB_LAND: *value = (uint64_t)ix->cmb_land.load(); break;
+    case TM_DEBUG_CMB_SPIN: *value = (uint64_t)ix->cmb_spin_us.load(); break;
     case TM_DEBUG_COMMITS: *value = ix->commits.load(); break;
     case TM_DEBUG_SMALL_TICKET: *value = ix->small_ticket; break;
+    case TM_DEBUG_PATCH_ZC: *value = ix->patch_zc; break;
     case TM_DEBUG_COMMIT_WAITS: *value = ix->commit_waits.load(); break;
     case TM_DEBUG_COMMIT_FORCED: *value = ix->commit_forced.load(); break;
     case TM_DEBUG_COMBINED_LAUNCHES: *value = ix->cmb_launches.load(); break;

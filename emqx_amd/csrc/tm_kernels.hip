@@ -26,6 +26,19 @@
 // design goal is many independent loads in flight per CU, not MFMA.
 #include "tm_dev.h"
 
+// The tail kernels' last-block ticket (k_walk_tail, reset_lists_if_last) and
+// k_walk_small's look-back read totals other blocks published with relaxed
+// device-scope atomics, ordered only by s_waitcnt(0) before the ticket and
+// by agent-scope (sc1) loads in the reader -- no release/acquire fence, which
+// writes back and invalidates the whole L2 of the XCD (C3deep tail +68 us,
+// DESIGN.md 0 item 6).  That relies on the gfx94x/gfx95x memory system:
+// device-scope atomics are performed at the coherence point across the XCDs
+// and a completed s_waitcnt means they were.  Built for gfx950 only (ADVICE
+// r5): any other target must revisit it, so it does not compile.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "tm_kernels.hip: the tail tickets' ordering is argued for gfx950 only (see above)"
+#endif
+
 namespace tmx {
 
 // ----------------------------------------------------------------- helpers
@@ -1462,7 +1475,26 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_small(DevIndex ix, Workspace 
         s_fbk[gi] = live && fb;
     }
     __syncthreads();
-    if (wv == 0) {
+    if (wv == 0 && sg.pairs) {
+        // (offset, count) pairs (tm_match_batch32_pairs): the block reserves
+        // its values' span with ONE atomic on the segment's counter and never
+        // waits for another block -- no look-back, so a finished block frees
+        // its slot at once for the other callers' launches; the segment's
+        // last block (a ticket taken after its reservation returned) writes
+        // the total and resets both words for the next launch
+        if (threadIdx.x == 0) {
+            uint64_t sum = 0;
+            for (uint32_t i = 0; i < ST; i++) sum += s_cnt[i];
+            s_base = atomicAdd(&ws.pairs[2 * k], (uint32_t)sum);
+            s_sum = sum;
+            s_fail = 0;
+            if (atomicAdd(&ws.pairs[2 * k + 1], 1u) == nblk - 1) {
+                hit_offs[2 * n] = (OT)__hip_atomic_load(&ws.pairs[2 * k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                atomicExch(&ws.pairs[2 * k], 0u);
+                atomicExch(&ws.pairs[2 * k + 1], 0u);
+            }
+        }
+    } else if (wv == 0) {
         uint64_t sum = 0;
         for (uint32_t i = 0; i < ST; i++) sum += s_cnt[i];
         // one flag round trip per 64 predecessors (look_back); a failed wait
@@ -1479,12 +1511,19 @@ __global__ __launch_bounds__(WV_BLOCK) void k_walk_small(DevIndex ix, Workspace 
         }
     }
     __syncthreads();
-    // the block's hit offsets and flags: lanes 0..ST-1 of wave 0, one coalesced store each
+    // the block's hit offsets (pairs: first position and count) and flags:
+    // lanes 0..ST-1 of wave 0, one coalesced store each
     if (threadIdx.x < ST && (uint64_t)vb * ST + threadIdx.x < n) {
         uint64_t p = s_base;
         for (uint32_t i = 0; i < threadIdx.x; i++) p += s_cnt[i];
-        hit_offs[(uint64_t)vb * ST + threadIdx.x] = (OT)p;
-        o.err[(uint64_t)vb * ST + threadIdx.x] = s_fail ? 4 : s_err[threadIdx.x];
+        const uint64_t t_ = (uint64_t)vb * ST + threadIdx.x;
+        if (sg.pairs) {
+            hit_offs[2 * t_] = (OT)p;
+            hit_offs[2 * t_ + 1] = (OT)s_cnt[threadIdx.x];
+        } else {
+            hit_offs[t_] = (OT)p;
+        }
+        o.err[t_] = s_fail ? 4 : s_err[threadIdx.x];
     }
     if (s_fail) return;   // (block-uniform)
     // stage the block's values in LDS when they fit and no topic of the block

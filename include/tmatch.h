@@ -67,6 +67,24 @@
  * a batch again once and returns TM_EDEVICE if it fails again, so its callers
  * never see err 4; a device-API caller (tm_match_batch_dev*, asynchronous)
  * finds the flags in d_out_err and submits the batch again.
+ *
+ * Forward progress (k_walk_small's look-back).  A block of a
+ * one-launch batch waits only for blocks of its own launch (segment) that
+ * come before it.  In dispatch order (TM_DEBUG_SMALL_TICKET 0), "before" is
+ * blockIdx: the command processor hands a launch's workgroups to the 8 XCDs
+ * round robin and each XCD starts its share in index order, so within ONE
+ * launch the lowest unfinished block never waits for an unstarted one once
+ * the blocks below it have left their XCD -- but the XCDs start their shares
+ * independently, and with several look-back launches in flight (concurrent
+ * callers, the combiner's leaders) every slot of one XCD can be held by
+ * waiting blocks of one launch while the predecessor they wait for sits
+ * unstarted behind another launch's waiting blocks on another XCD.  So
+ * dispatch order alone does not guarantee progress on gfx950; the bounded
+ * wait turns such a stall into err 4 (a rerun, then TM_EDEVICE), never a
+ * wrong result.  With a start-order ticket (TM_DEBUG_SMALL_TICKET 1) a block
+ * takes its index from an atomic counter when it starts, so every block it
+ * waits for has started and runs to its publication without waiting for a
+ * later one: progress by construction.
  */
 #ifndef TMATCH_H
 #define TMATCH_H
@@ -232,6 +250,23 @@ int tm_match_batch32_ex(tm_index *h, uint64_t n, const uint8_t *topic_bytes, con
                         uint32_t *out_hit_offsets, uint32_t *out_values, uint64_t cap, uint8_t *out_err,
                         uint32_t order, uint32_t *out_unique);
 
+/* tm_match_batch32_ex in TM_ORDER_TRAVERSAL with the hit lists as per-topic
+ * (first position, count) pairs instead of a CSR: out_pairs[2 i] is topic i's
+ * first value in out_values, out_pairs[2 i + 1] its count, out_pairs[2 n] the
+ * values' total (TM_ECAP when it exceeds cap: the pairs are valid, values past
+ * cap dropped).  A topic's values are contiguous and in traversal order, as
+ * in the CSR; the topics' spans are disjoint but NOT in topic order.  What
+ * the NIF binds (c_src/tmatch_nif_core.c tmn_row): an in-place batch (every
+ * buffer from tm_host_alloc / TM_ALLOC_VRAM) of up to 65536 topics runs in
+ * one launch whose blocks each reserve their values' span with one atomic
+ * and never wait for another block (no cross-block scan: a finished block
+ * frees its slot at once for concurrent callers' launches, and forward
+ * progress needs no argument); any other batch takes tm_match_batch32_ex and
+ * is converted.  out_err is required (n entries).  (No reference counterpart:
+ * the NIF builds each topic's list from its span.) */
+int tm_match_batch32_pairs(tm_index *h, uint64_t n, const uint8_t *topic_bytes, const uint32_t *topic_offsets,
+                           uint32_t *out_pairs, uint32_t *out_values, uint64_t cap, uint8_t *out_err);
+
 /* tm_match_batch_dev with 32-bit offsets (traversal order): a batch of up to
  * 65536 topics reads and writes them as they are; a larger one is widened
  * into the stream's scratch, matched and narrowed on the device (two small
@@ -358,6 +393,11 @@ int tm_profile_read(tm_index *h, double *walk_ms, double *batch_ms, uint64_t *ba
  *                           theirs (0 = none, the default)
  *   TM_DEBUG_SMALL_TICKET   1: k_walk_small's blocks take a start-order
  *                           ticket (see "Forward progress"); 0: dispatch order
+ *   TM_DEBUG_PATCH_ZC       1 (default): patches up to 64 KiB are read by the
+ *                           patch kernel from mapped pinned memory; 0: copied
+ *                           to the device first
+ *   TM_DEBUG_CMB_SPIN       microseconds a caller waiting in the combiner spins
+ *                           before it sleeps (0: sleeps at once)
  *   TM_DEBUG_CMB_LAND       (study) 1: a combined launch writes its outputs to
  *                           HBM and one copy kernel lands them in the callers'
  *                           buffers (0 = the kernel writes them in place)
@@ -378,7 +418,8 @@ enum { TM_DEBUG_LB_SPINS = 1, TM_DEBUG_LB_FAIL_BLOCK = 2, TM_DEBUG_LB_LAUNCHES =
        TM_DEBUG_PATH_SMALL = 8, TM_DEBUG_PATH_LANE = 9, TM_DEBUG_SMALL_KERNEL = 10,
        TM_DEBUG_COMBINE = 12, TM_DEBUG_COMBINED_LAUNCHES = 13, TM_DEBUG_COMBINED_BATCHES = 14,
        TM_DEBUG_WIDE_NODES = 15, TM_DEBUG_DENSE_WIDE = 16, TM_DEBUG_CMB_GATHER = 17, TM_DEBUG_CMB_LAND = 18,
-       TM_DEBUG_COMMITS = 19, TM_DEBUG_COMMIT_WAITS = 20, TM_DEBUG_COMMIT_FORCED = 21, TM_DEBUG_SMALL_TICKET = 22 };
+       TM_DEBUG_COMMITS = 19, TM_DEBUG_COMMIT_WAITS = 20, TM_DEBUG_COMMIT_FORCED = 21, TM_DEBUG_SMALL_TICKET = 22,
+       TM_DEBUG_CMB_SPIN = 23, TM_DEBUG_PATCH_ZC = 24 };
 int tm_debug_set(tm_index *h, uint32_t key, uint64_t value);
 int tm_debug_get(tm_index *h, uint32_t key, uint64_t *value);
 

@@ -201,7 +201,7 @@ apply_batch(Ops, G = #gtab{tab = Tab}) ->
 %% stale event arriving after a later write harmless.
 -spec mirror_batch([emqx_trie_search:key(_)], gtab()) -> ok.
 mirror_batch(Keys, G) ->
-    flush(G, lists:foldl(fun(K, Acc) -> sync_delta(G, K, Acc) end, ?NOACC, Keys)).
+    commit(G, lists:foldl(fun(K, Acc) -> sync_delta(G, K, Acc) end, ?NOACC, Keys)).
 
 %% Replicated writes reach a core or replicant node as mnesia table events,
 %% bypassing emqx_router (SURVEY.md 3.2): emqx_router_gpu's event process
@@ -222,7 +222,7 @@ table_event(Event, G) ->
 -spec table_events([tuple()], gtab()) -> ok.
 table_events(Events, G = #gtab{tab = Tab}) ->
     Pos = key_pos(Tab),
-    flush(G, lists:foldl(
+    commit(G, lists:foldl(
         fun(E, Acc) ->
             case event_key(E, Pos) of
                 {ok, Key} -> sync_delta(G, Key, Acc);
@@ -385,10 +385,19 @@ escape_byte(C) -> <<C>>.
 %% Deltas were accumulated by prepending: ship them in the order they were
 %% made; the kids they release are quarantined under the epoch the batch made
 %% current (a reader that began earlier may still return them).
-flush(_G, {[], []}) ->
+flush(G, Acc) ->
+    ship(G, Acc, fun emqx_tmatch_nif:apply/2).
+
+%% The mirror's deltas (mirror_batch/2, table_events/2) go through the NIF's
+%% commit/2 (tm_commit): published on a table copy no publish batch is
+%% reading, so a route write never makes a publish batch wait on the GPU.
+commit(G, Acc) ->
+    ship(G, Acc, fun emqx_tmatch_nif:commit/2).
+
+ship(_G, {[], []}, _Call) ->
     ok;
-flush(#gtab{ref = Ref, quar = Quar}, {Deltas, Released}) ->
-    {ok, Epoch} = emqx_tmatch_nif:apply(Ref, lists:reverse(Deltas)),
+ship(#gtab{ref = Ref, quar = Quar}, {Deltas, Released}, Call) ->
+    {ok, Epoch} = Call(Ref, lists:reverse(Deltas)),
     true = ets:insert(Quar, [{{Epoch, Kid}} || Kid <- Released]),
     ok.
 

@@ -80,6 +80,29 @@ int tm_match_batch32_ex(tm_index *h, uint64_t n, const uint8_t *tb, const uint32
     return rc;
 }
 
+/* pairs: the CSR's rows laid out in REVERSE topic order (the library's
+   spans are disjoint but in no particular order) */
+int tm_match_batch32_pairs(tm_index *h, uint64_t n, const uint8_t *tb, const uint32_t *to, uint32_t *pairs,
+                           uint32_t *vals, uint64_t cap, uint8_t *err) {
+    uint32_t *hit = malloc(4 * (n + 1));
+    uint64_t total = 0;
+    for (uint64_t i = 0; i < n; i++) total += to[i + 1] > to[i] ? to[i + 1] - to[i] : 0;
+    uint32_t *tmp = malloc(4 * (total + 1));
+    int rc = tm_match_batch32_ex(h, n, tb, to, hit, tmp, total + 1, err, TM_ORDER_TRAVERSAL, NULL);
+    if (rc != TM_OK) { free(hit); free(tmp); return rc; }
+    uint64_t pos = 0;
+    for (uint64_t j = n; j-- > 0;) {
+        const uint32_t c = hit[j + 1] - hit[j];
+        pairs[2 * j] = (uint32_t)pos;
+        pairs[2 * j + 1] = c;
+        for (uint32_t k = 0; k < c; k++, pos++)
+            if (pos < cap) vals[pos] = tmp[hit[j] + k];
+    }
+    pairs[2 * n] = (uint32_t)pos;
+    free(hit); free(tmp);
+    return pos > cap ? TM_ECAP : TM_OK;
+}
+
 int tm_first_batch(tm_index *h, uint64_t n, const uint8_t *tb, const uint64_t *to, uint32_t *val, uint8_t *found) {
     (void)h;
     n_first++;

@@ -1240,11 +1240,12 @@ def test_concurrent_callers_see_consistent_snapshots(torch_dev, copies):
           f"p50 {np.percentile(lat, 50):.3f} ms p99 {np.percentile(lat, 99):.3f} ms")
 
 
-@pytest.mark.parametrize("kind,copies,leaders,gather,land,ticket", [
-    ("wave", 1, 4, 0, 0, 0), ("wave8", 1, 4, 0, 0, 0), ("auto", 2, None, 0, 0, 0), ("auto", 2, 2, 0, 0, 0),
-    ("auto", 1, 4, 30, 1, 0), ("auto", 2, 1, 30, 0, 0), ("auto", 2, 2, 0, 1, 0), ("auto", 2, 2, 0, 0, 1)])
+@pytest.mark.parametrize("kind,copies,leaders,gather,land,ticket,spin", [
+    ("wave", 1, 4, 0, 0, 0, 0), ("wave8", 1, 4, 0, 0, 0, 0), ("auto", 2, None, 0, 0, 0, 0), ("auto", 2, 2, 0, 0, 0, 0),
+    ("auto", 1, 4, 30, 1, 0, 0), ("auto", 2, 1, 30, 0, 0, 0), ("auto", 2, 2, 0, 1, 0, 0), ("auto", 2, 2, 0, 0, 1, 0),
+    ("auto", 2, 2, 0, 0, 1, 40)])
 def test_combined_callers_with_deltas_see_snapshots_and_never_fail(torch_dev, kind, copies, leaders, gather, land,
-                                                                   ticket):
+                                                                   ticket, spin):
     """The NIF's production path under load:
     16 host threads submit in-place 32-bit batches (tm_match_batch32_ex on
     host_array buffers, what the NIF's dirty schedulers do) through the
@@ -1270,6 +1271,7 @@ def test_combined_callers_with_deltas_see_snapshots_and_never_fail(torch_dev, ki
     ix.debug_set(_native.TM_DEBUG_CMB_GATHER, gather)
     ix.debug_set(_native.TM_DEBUG_CMB_LAND, land)
     ix.debug_set(_native.TM_DEBUG_SMALL_TICKET, ticket)
+    ix.debug_set(_native.TM_DEBUG_CMB_SPIN, spin)
     assert (ix.debug_get(_native.TM_DEBUG_CMB_GATHER), ix.debug_get(_native.TM_DEBUG_CMB_LAND)) == (gather, land)
     ix.debug_set(_native.TM_DEBUG_SMALL_KERNEL, _small_kind(kind))
     ix.apply(np.ones(len(fs), np.uint8), fs.blob, fs.offs, fs.vals)
@@ -2904,7 +2906,7 @@ def test_router_killed_mirror_never_serves_a_stale_handle(torch_dev):
     ts = wl.topics(3, 5_000, 1_000)
     topics = [ts.item(i) for i in range(len(ts))] + [b"down/x/y"]
     assert r.match_routes_batch(topics) == model.expected(topics)
-    old = r._mirror
+    old, n_before = r._mirror, len(model.wild)
     r.kill_mirror()
     for t, d in ((b"down/+/y", "n2"), (b"down/#", "n3")):
         r.add_route(t, d)
@@ -2915,9 +2917,111 @@ def test_router_killed_mirror_never_serves_a_stale_handle(torch_dev):
         r.match_routes(b"down/x/y")
     with pytest.raises(rt.MirrorDown):
         r.match_routes_batch(topics)
-    assert old.stats()["n_keys"] == sum(1 for i in range(len(fs)) if rt.tfilter(fs.item(i)) is not False)
+    assert old.stats()["n_keys"] == n_before          # the dead mirror took none of the writes
     r.restart_mirror(batch_size=1000)
     assert r._mirror is not old
     got = r.match_routes_batch(topics)
     assert got == model.expected(topics)
     assert {x.topic for x in got[-1]} >= {b"down/#", b"down/+/y"}
+
+
+def _pairs_as_csr(pairs, vals, n):
+    """(first, count) pairs -> CSR offsets and values in topic order; asserts
+    the spans are disjoint and cover [0, total) exactly"""
+    first, cnt = pairs[0:2 * n:2].astype(np.int64), pairs[1:2 * n:2].astype(np.int64)
+    total = int(pairs[2 * n])
+    assert int(cnt.sum()) == total
+    order = np.argsort(first, kind="stable")
+    ends = np.cumsum(cnt[order])
+    assert np.array_equal(first[order], ends - cnt[order])      # disjoint, back to back from 0
+    hit = np.zeros(n + 1, np.int64)
+    hit[1:] = np.cumsum(cnt)
+    out = np.concatenate([vals[f:f + c] for f, c in zip(first, cnt)]) if n else np.zeros(0, np.uint32)
+    return hit.astype(np.uint32), out.astype(np.uint32)
+
+
+@pytest.mark.parametrize("kind", ["auto", "wave"])
+def test_pairs_batches_equal_the_csr_path_and_the_oracle(torch_dev, kind):
+    """tm_match_batch32_pairs (what the NIF binds): per-topic (first, count)
+    pairs from launches whose blocks never wait for each other -- every
+    topic's values equal its CSR row (tm_match_batch32_ex) and the oracle's,
+    the spans are disjoint and cover the total, badarg stays in its own slot;
+    alone and from 10 concurrent callers sharing combined launches (with
+    deltas applied in between), inputs in host or TM_ALLOC_VRAM memory; a
+    batch above 65536 topics and an index too deep for the one-launch kernel
+    take the CSR path and are converted."""
+    import threading
+    fs = wl.filters(3, 200_000)
+    ix, o = gpu_index(fs), oracle_of(fs)
+    ix.debug_set(_native.TM_DEBUG_SMALL_KERNEL, _small_kind(kind))
+    sets = []
+    for k, nt in enumerate([1, 7, 100, 640, 3000, 4096, 9000, 20_000, 65_536, 70_000]):
+        ts = wl.topics(3, 200_000, nt, first=k * 80_000)
+        items = [ts.item(i) for i in range(nt)]
+        if nt >= 100:
+            items[nt // 2] = b"bad/#/topic"
+        blob, offs = _native.pack_strings(items)
+        vram = k % 2 == 1
+        pb = ix.host_array(len(blob) + 16, np.uint8, vram=vram)
+        pb[: len(blob)] = blob
+        po = ix.host_array(nt + 1, np.uint32, vram=vram)
+        po[:] = offs.astype(np.uint32)
+        cap = 64 * nt + 64
+        csr = (ix.host_array(nt + 1, np.uint32), ix.host_array(cap, np.uint32), ix.host_array(nt, np.uint8))
+        prs = [(ix.host_array(2 * nt + 1, np.uint32), ix.host_array(cap, np.uint32), ix.host_array(nt, np.uint8))
+               for _ in range(2)]
+        sets.append((pb, po, csr, prs, items, blob, offs))
+
+    def check(k, pairs, vals, err):
+        pb, po, csr, prs, items, blob, offs = sets[k]
+        h, v, e = ix.match_batch32(pb, po, csr)
+        hh, vv = _pairs_as_csr(pairs, vals, len(items))
+        return np.array_equal(hh, h) and np.array_equal(vv, v) and np.array_equal(err, e)
+
+    for k, (pb, po, csr, prs, items, blob, offs) in enumerate(sets):
+        pairs, vals, err = ix.match_batch32_pairs(pb, po, prs[0])
+        assert check(k, pairs, vals, err), k
+        oc, _, ohit, ovals = o.match_batch(blob, offs)
+        hh, vv = _pairs_as_csr(pairs, vals, len(items))
+        for i in range(len(items)):
+            if err[i]:
+                assert b"+" in items[i] or b"#" in items[i]
+                continue
+            assert np.array_equal(vv[hh[i]:hh[i + 1]], ovals[int(ohit[i]):int(ohit[i + 1])])
+    # concurrent callers through the combiner, deltas in between (each result
+    # equal to the CSR path run right after it: the deltas only add keys that
+    # no topic of these sets matches)
+    errors = []
+
+    def caller(k):
+        pb, po, csr, prs, items, _, _ = sets[k]
+        try:
+            for _ in range(15):
+                pairs, vals, err = ix.match_batch32_pairs(pb, po, prs[1])
+                hh, vv = _pairs_as_csr(pairs, vals, len(items))
+                hh0, vv0 = _pairs_as_csr(*ix.match_batch32_pairs(pb, po, prs[0])[:2], len(items))
+                if not (np.array_equal(hh, hh0) and np.array_equal(vv, vv0)):
+                    errors.append(k)
+                    return
+        except Exception as ex:   # noqa: BLE001 -- reported below
+            errors.append((k, repr(ex)))
+    l0 = ix.debug_get(_native.TM_DEBUG_COMBINED_LAUNCHES)
+    th = [threading.Thread(target=caller, args=(k,)) for k in range(len(sets) - 1)]
+    for t in th:
+        t.start()
+    for e in range(5):
+        d = items_of([b"zz/%d/+" % e], [9_000_000 + e])
+        ix.apply(np.ones(1, np.uint8), d.blob, d.offs, d.vals)
+    for t in th:
+        t.join()
+    assert not errors, errors
+    assert ix.debug_get(_native.TM_DEBUG_COMBINED_LAUNCHES) > l0
+    # an index the one-launch kernel cannot take: the CSR path, converted
+    deep = items_of([b"/".join([b"d"] * 34 + [b"+"])], [5_000_000])
+    ix.apply(np.ones(1, np.uint8), deep.blob, deep.offs, deep.vals)
+    p0 = ix.debug_get(_native.TM_DEBUG_PATH_PHASES)
+    for k in (3, 4):
+        pb, po, csr, prs, items, blob, offs = sets[k]
+        pairs, vals, err = ix.match_batch32_pairs(pb, po, prs[0])
+        assert check(k, pairs, vals, err)
+    assert ix.debug_get(_native.TM_DEBUG_PATH_PHASES) > p0

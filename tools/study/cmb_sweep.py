@@ -8,7 +8,7 @@ the route-writer leg (tmb_writers: one-key writes group-committed by a mirror
 thread while matcher threads run).  One JSON line per point.
 
 Lists take "," or "+" (tools/gpu.sh splits its step arguments on commas);
---combos is "leaders/gather/land" items.
+--combos is "leaders/gather/land[/spin_us]" items.
 """
 import argparse
 import ctypes
@@ -40,6 +40,9 @@ def main():
     p.add_argument("--writer-combos", default="4/0/0")
     p.add_argument("--writer-commit", default="1,0", help="1: the mirror ships with tm_commit, 0: tm_apply_deltas")
     p.add_argument("--tickets", default="0", help="TM_DEBUG_SMALL_TICKET values (k_walk_small start-order tickets)")
+    p.add_argument("--writer-check", default="1", help="1: each writer publishes its own topic after a subscribe")
+    p.add_argument("--patch-zc", default="1", help="TM_DEBUG_PATCH_ZC values")
+    p.add_argument("--writer-matchers", default="8")
     p.add_argument("--latency", default="", help="lone-batch sizes for a host-to-host latency leg per ticket value")
     p.add_argument("--writer-seconds", type=float, default=2.0)
     a = p.parse_args()
@@ -60,14 +63,18 @@ def main():
     hh, _, _ = ix.match_batch(ts.blob, ts.offs)
     cap = int(np.diff(hh.astype(np.int64)).reshape(max(thr), lb).sum(axis=1).max()) + 65536
 
+    spin = [0]
+
     def setk(combo):
-        lead, gat, land = (int(x) for x in combo.split("/"))
+        f = [int(x) for x in combo.split("/")] + [0]
+        lead, gat, land, spin[0] = f[0], f[1], f[2], f[3]
         ix.debug_set(_native.TM_DEBUG_COMBINE, lead)
         try:   # (an older library without these keys: only 0 is meaningful)
             ix.debug_set(_native.TM_DEBUG_CMB_GATHER, gat)
             ix.debug_set(_native.TM_DEBUG_CMB_LAND, land)
+            ix.debug_set(_native.TM_DEBUG_CMB_SPIN, spin[0])
         except _native.TmError:
-            assert gat == 0 and land == 0
+            assert gat == 0 and land == 0 and spin[0] == 0
         return lead, gat, land
 
     def set_ticket(tk):
@@ -106,6 +113,7 @@ def main():
                         launches = ix.debug_get(_native.TM_DEBUG_COMBINED_LAUNCHES) - l0
                         batches = ix.debug_get(_native.TM_DEBUG_COMBINED_BATCHES) - b0
                         print(json.dumps({"rep": rep, "threads": nth, "mode": mode, "leaders": lead, "ticket": tk,
+                                          "spin_us": spin[0],
                                           "gather_us": gat,
                                           "land": land, "churn": churn, "topics_per_s": round(out[1]),
                                           "p50_ms": round(out[2], 4), "p99_ms": round(out[3], 4),
@@ -115,21 +123,26 @@ def main():
     for nw in map(int, L(a.writers)):
         if nw <= 0:
             continue
-        for combo in L(a.writer_combos):
-          for cm in map(int, L(a.writer_commit)):
+        for combo, cm, ck, zc, nmt in [(c, m, k, z, t) for c in L(a.writer_combos) for m in map(int, L(a.writer_commit))
+                                      for k in map(int, L(a.writer_check)) for z in map(int, L(a.patch_zc))
+                                      for t in map(int, L(a.writer_matchers))]:
             lead, gat, land = setk(combo)
             set_ticket(0)
+            try:
+                ix.debug_set(_native.TM_DEBUG_PATCH_ZC, zc)
+            except _native.TmError:
+                assert zc == 1
             out = (ctypes.c_double * 10)()
             c0 = [ix.debug_get(k) for k in (_native.TM_DEBUG_COMMITS, _native.TM_DEBUG_COMMIT_WAITS,
                                             _native.TM_DEBUG_COMMIT_FORCED)] if cm else [0, 0, 0]
-            rc = hb.tmb_writers(ix._h, nw, 8, lb, _native._ptr(ts.blob), _native._ptr(ts.offs), cap,
-                                a.writer_seconds, 1, cm, out)
+            rc = hb.tmb_writers(ix._h, nw, nmt, lb, _native._ptr(ts.blob), _native._ptr(ts.offs), cap,
+                                a.writer_seconds, ck, cm, out)
             assert rc == 0, rc
             c1 = [ix.debug_get(k) for k in (_native.TM_DEBUG_COMMITS, _native.TM_DEBUG_COMMIT_WAITS,
                                             _native.TM_DEBUG_COMMIT_FORCED)] if cm else [0, 0, 0]
-            print(json.dumps({"leg": "writers", "commit": cm, "copies": a.copies,
+            print(json.dumps({"leg": "writers", "commit": cm, "copies": a.copies, "check": ck, "patch_zc": zc,
                               "commits": c1[0] - c0[0], "commit_waits": c1[1] - c0[1], "commit_forced": c1[2] - c0[2],
-                              "writers": nw, "matchers": 8, "leaders": lead, "gather_us": gat,
+                              "writers": nw, "matchers": nmt, "leaders": lead, "gather_us": gat,
                               "land": land, "writes_per_s": round(out[0]), "write_p50_ms": round(out[1], 4),
                               "write_p99_ms": round(out[2], 4), "commits_per_s": round(out[3]),
                               "topics_per_s": round(out[4]), "match_p50_ms": round(out[5], 4),
