@@ -447,6 +447,12 @@ def main():
         assert rc == 0, rc
         lat_native[f"{lb}_u32_vram_inputs"] = {"p50_ms": round(out[0], 4), "p99_ms": round(out[1], 4),
                                                "mean_ms": round(out[2], 4)}
+        out = (ctypes.c_double * 3)()   # the same through tm_match_batch32_pairs (the NIF's call)
+        rc = hb.tmb_single_ex(ix._h, lb, _native._ptr(sub.blob), _native._ptr(sub.offs), int(hh[-1]) + 4096,
+                              a.latency_batches * 5, 6, out)
+        assert rc == 0, rc
+        lat_native[f"{lb}_u32_vram_inputs_pairs"] = {"p50_ms": round(out[0], 4), "p99_ms": round(out[1], 4),
+                                                     "mean_ms": round(out[2], 4)}
         if a.concurrency > 0:
             conc = []
             if a.combine_leaders is not None:
@@ -455,9 +461,12 @@ def main():
             # u32-offset API the NIF calls (tm_match_batch32_ex), 0: the u64 one
             # mode 5: mode 4 with the inputs in TM_ALLOC_VRAM memory, written by each caller before
             # every batch (as a NIF packs its micro-batch): no PCIe read on the kernel's path
+            # mode 6: mode 5 through tm_match_batch32_pairs -- per-topic (offset, count) pairs, no
+            # cross-block look-back: what the NIF binds (c_src/tmatch_nif_core.c tmn_match)
             for nth, churn, mode in ((a.concurrency, 0, 0), (a.concurrency, 0, 4), (a.concurrency, 256, 4),
                                      (2 * a.concurrency, 256, 4), (a.concurrency, 0, 5), (a.concurrency, 256, 5),
-                                     (2 * a.concurrency, 256, 5)):
+                                     (2 * a.concurrency, 256, 5), (a.concurrency, 0, 6), (a.concurrency, 256, 6),
+                                     (2 * a.concurrency, 0, 6), (2 * a.concurrency, 256, 6)):
                 lb = min(4096, B)
                 sub = ts.slice(0, nth * lb)
                 hh, _, _ = ix.match_batch(sub.blob, sub.offs)
@@ -475,7 +484,8 @@ def main():
                              # again once, a second failure is TM_EDEVICE): forward progress under
                              # concurrent launches, measured
                              "failed_batches": fr1[0] - fr0[0], "retried_batches": fr1[1] - fr0[1],
-                             "inputs": "vram (written per batch)" if mode == 5 else "host",
+                             "inputs": "vram (written per batch)" if mode in (5, 6) else "host",
+                             "outputs": "pairs" if mode == 6 else "csr",
                              "combine_leaders": ix.debug_get(_native.TM_DEBUG_COMBINE) if mode >= 4 else None,
                              "callers": "native threads, tm_host_alloc buffers each (in place)"})
         if B >= 65536:

@@ -1247,7 +1247,7 @@ void word_key_op(tm_index *ix, bool ins, const std::vector<WordRef> &w, uint32_t
 
 constexpr uint64_t DEV_GUARD = 16;   // device elements kept allocated past the host size (see collect)
 
-int bring_up(tm_index *ix, int r, uint64_t upto, hipStream_t st);
+int bring_up(tm_index *ix, int r, uint64_t upto, hipStream_t st, bool idle = false);
 int collect_patch_locked(tm_index *ix);
 
 template <class T>
@@ -1381,7 +1381,7 @@ int batch_done(tm_index *ix, Lane &ln) {
 // later batch there waits for this one (`last_patch`, ensure_ws): a batch
 // sees exactly the deltas applied before it was queued (C5), whichever stream
 // either ran on.
-int apply_patch(tm_index *ix, int r, uint64_t q, hipStream_t st) {
+int apply_patch(tm_index *ix, int r, uint64_t q, hipStream_t st, bool wait_readers = true) {
     Replica &R = ix->rep[r];
     const uint32_t k = (uint32_t)((q - 1) % PATCH_RING);
     const PatchSlot &p = ix->patch[k];
@@ -1399,8 +1399,9 @@ int apply_patch(tm_index *ix, int r, uint64_t q, hipStream_t st) {
         R.pdev[k] = np;
         R.pdev_cap[k] = want;
     }
-    for (auto &l : ix->lanes)
-        if (l->r == r && l->used && l->s != st) HIPCHK(ix, hipStreamWaitEvent(st, l->done, 0));
+    if (wait_readers)   // (not for a copy known to be idle, nor again behind a patch just queued on st)
+        for (auto &l : ix->lanes)
+            if (l->r == r && l->used && l->s != st) HIPCHK(ix, hipStreamWaitEvent(st, l->done, 0));
     if (R.last_patch) HIPCHK(ix, hipStreamWaitEvent(st, R.last_patch, 0));
     // a small patch (a route write's few runs) is read by the patch kernel
     // straight from the mapped pinned slot: one command on the stream instead
@@ -1423,9 +1424,10 @@ int apply_patch(tm_index *ix, int r, uint64_t q, hipStream_t st) {
 }
 
 // replica r takes every logged patch up to `upto`, in order, on stream st
-int bring_up(tm_index *ix, int r, uint64_t upto, hipStream_t st) {
-    for (uint64_t q = ix->rep[r].applied + 1; q <= upto; q++)
-        if (int rc = apply_patch(ix, r, q, st)) return rc;
+int bring_up(tm_index *ix, int r, uint64_t upto, hipStream_t st, bool idle) {
+    const uint64_t first = ix->rep[r].applied + 1;   // (readers waited for once, before the first patch)
+    for (uint64_t q = first; q <= upto; q++)
+        if (int rc = apply_patch(ix, r, q, st, !idle && q == first)) return rc;
     return TM_OK;
 }
 
@@ -1901,6 +1903,11 @@ struct CmbTiming {
     std::atomic<uint64_t> lock_ns{0}, setup_ns{0}, launch_ns{0}, sync_ns{0}, release_ns{0}, done_ns{0}, req_ns{0};
 };
 static CmbTiming g_cmbt;
+// (TM_HOST_TIMING) where tm_commit's time goes
+struct CommitTiming {
+    std::atomic<uint64_t> n{0}, apply_ns{0}, lock_ns{0}, collect_ns{0}, idle_ns{0}, ship_ns{0};
+};
+static CommitTiming g_cmt;
 static const bool g_cmb_timing = getenv("TM_HOST_TIMING") != nullptr;
 static inline uint64_t ns_now() {
     return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
@@ -1917,6 +1924,12 @@ int tm_destroy(tm_index *ix) {
                 g_cmbt.lock_ns * us / g, g_cmbt.setup_ns * us / g, g_cmbt.launch_ns * us / g, g_cmbt.sync_ns * us / g,
                 g_cmbt.release_ns * us / g, g_cmbt.done_ns * us / g,
                 g_cmbt.req_ns * us / std::max<double>(1.0, (double)g_cmbt.reqs));
+    }
+    if (g_cmb_timing && g_cmt.n) {
+        const double c = (double)g_cmt.n, us = 1e-3;
+        fprintf(stderr, "tm commit: %lu commits; per commit us: image %.1f lock %.1f collect %.1f wait-idle %.1f "
+                        "ship %.1f\n", (unsigned long)g_cmt.n.load(), g_cmt.apply_ns * us / c, g_cmt.lock_ns * us / c,
+                g_cmt.collect_ns * us / c, g_cmt.idle_ns * us / c, g_cmt.ship_ns * us / c);
     }
     for (int r = 0; r < ix->nrep; r++) {
         (void)hipSetDevice(ix->rep[r].device);
@@ -2006,13 +2019,18 @@ int tm_commit(tm_index *ix, uint64_t n, const uint8_t *ops, const uint8_t *fb, c
         tm_index *ix;
         ~Unhold() { ix->img_hold.fetch_sub(1, std::memory_order_acq_rel); }
     } unhold{ix};
+    const uint64_t ta = g_cmb_timing ? ns_now() : 0;
     int rc = tm_apply_deltas_ex(ix, n, ops, fb, fo, values, key_flags, out_epoch);
     if (rc || !n) return rc;
+    const uint64_t tb = g_cmb_timing ? ns_now() : 0;
     std::unique_lock<std::mutex> g(ix->mu);
+    const uint64_t tc = g_cmb_timing ? ns_now() : 0;
     if ((rc = collect_patch(ix, true))) return rc;
     const uint64_t q = ix->patch_seq;
     if (ix->pub_seq >= q) return TM_OK;   // (nothing to ship: the deltas changed no device word)
     ix->commits++;
+    const uint64_t td = g_cmb_timing ? ns_now() : 0;
+    uint64_t t_idle = 0, t_ship = 0;
     const auto t0 = std::chrono::steady_clock::now();
     bool done[MAX_REPLICAS] = {}, waited = false;
     int left = ix->ngroups;
@@ -2031,7 +2049,9 @@ int tm_commit(tm_index *ix, uint64_t n, const uint8_t *ops, const uint8_t *fb, c
             }
             if (pick < 0 && copies > 1 && !late) continue;   // wait for a copy to drain
             if (pick >= 0) {
-                if ((rc = bring_up(ix, pick, q, ix->rep[pick].ps))) return rc;
+                const uint64_t t0s = g_cmb_timing ? ns_now() : 0;
+                if ((rc = bring_up(ix, pick, q, ix->rep[pick].ps, true))) return rc;
+                if (g_cmb_timing) t_ship += ns_now() - t0s;
                 ix->serving[gi] = pick;
             } else {
                 ix->commit_forced++;   // published below; the group's batches take the patch themselves
@@ -2041,12 +2061,19 @@ int tm_commit(tm_index *ix, uint64_t n, const uint8_t *ops, const uint8_t *fb, c
         }
         if (!left) break;
         waited = true;
+        const uint64_t tw = g_cmb_timing ? ns_now() : 0;
         g.unlock();
         std::this_thread::sleep_for(std::chrono::microseconds(2));
         g.lock();
+        if (g_cmb_timing) t_idle += ns_now() - tw;
     }
     if (waited) ix->commit_waits++;
     if (ix->pub_seq < q) ix->pub_seq = q;
+    if (g_cmb_timing) {
+        g_cmt.n++;
+        g_cmt.apply_ns += tb - ta; g_cmt.lock_ns += tc - tb; g_cmt.collect_ns += td - tc;
+        g_cmt.idle_ns += t_idle; g_cmt.ship_ns += t_ship;
+    }
     return TM_OK;
 }
 
@@ -2819,7 +2846,9 @@ int tm_match_batch32_pairs(tm_index *ix, uint64_t n, const uint8_t *tb, const ui
         }
         if ((rq.db || !nbytes) && rq.dof && rq.dh && (rq.dv || !out_vals) && rq.de) {
             rq.n = n; rq.cap = rq.dv ? cap : 0; rq.pairs = true;
-            const int rc = small_combined(ix, rq);
+            uint64_t t_end = 0;   // (TM_DEBUG_COMBINE 0: every batch its own launch)
+            const int rc = ix->cmb_leaders.load() > 0 ? small_combined(ix, rq)
+                                                      : run_small_group(ix, std::vector<SmallReq *>{&rq}, &t_end);
             if (rc != CMB_LEGACY) {
                 if (rc) return rc;
                 return (out_vals && out_pairs[2 * n] > cap) ? TM_ECAP : TM_OK;

@@ -44,6 +44,7 @@ def main():
     p.add_argument("--patch-zc", default="1", help="TM_DEBUG_PATCH_ZC values")
     p.add_argument("--writer-matchers", default="8")
     p.add_argument("--latency", default="", help="lone-batch sizes for a host-to-host latency leg per ticket value")
+    p.add_argument("--latency-modes", default="5", help="tmb_single_ex modes of the latency leg (5: CSR, 6: pairs)")
     p.add_argument("--writer-seconds", type=float, default=2.0)
     a = p.parse_args()
     from bench import CONFIGS, host_bench_lib
@@ -83,7 +84,7 @@ def main():
         except _native.TmError:
             assert tk == 0
 
-    for n in map(int, L(a.latency)):
+    for n, lm in [(x, m) for x in map(int, L(a.latency)) for m in map(int, L(a.latency_modes))]:
         for rep in range(a.repeat):
             for tk in map(int, L(a.tickets)):
                 set_ticket(tk)
@@ -91,9 +92,9 @@ def main():
                 hh2, _, _ = ix.match_batch(sub.blob, sub.offs)
                 out = (ctypes.c_double * 3)()
                 rc = hb.tmb_single_ex(ix._h, n, _native._ptr(sub.blob), _native._ptr(sub.offs), int(hh2[-1]) + 4096,
-                                      400, 5, out)
+                                      400, lm, out)
                 assert rc == 0, rc
-                print(json.dumps({"leg": "latency", "rep": rep, "topics": n, "ticket": tk, "inputs": "vram",
+                print(json.dumps({"leg": "latency", "rep": rep, "topics": n, "ticket": tk, "mode": lm,
                                   "p50_ms": round(out[0], 4), "p99_ms": round(out[1], 4),
                                   "mean_ms": round(out[2], 4)}), flush=True)
     for rep in range(a.repeat):
