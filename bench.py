@@ -123,6 +123,9 @@ def parse():
                         "device entries, native feeder threads submitting in-place host batches while a syncer thread "
                         "applies deltas (the NIF's deployment, INTEGRATION.md 5); with fewer GPUs than N the entries "
                         "repeat the local device -- a rehearsal, not scaling")
+    p.add_argument("--outputs", default="csr", choices=["csr", "pairs"],
+                   help="hit lists as a CSR (tm_match_batch_dev: walk, tails, scan + emit) or as per-topic "
+                        "(first position, count) pairs (tm_match_batch_dev_pairs: the walk writes its own values)")
     p.add_argument("--small-kernel", default="auto", choices=["auto", "wave", "wave8"],
                    help="the one-launch kernel of batches <= 65536 topics (latency and concurrent-caller legs): "
                         "the library's default, k_walk_small with 16 or 8 lanes per topic (TM_DEBUG_SMALL_KERNEL)")
@@ -275,6 +278,21 @@ def main():
     apply_s = [0.0]   # c5: host time inside tm_apply_deltas (the syncer's side of a churn step)
     xch = shard.Exchange(B, dev) if filter_sharded and world > 1 else None
 
+    pairs_out = a.outputs == "pairs"
+    assert not (pairs_out and (filter_sharded or level0 or a.split > 1)), "--outputs pairs: topic-sharded, no split"
+
+    def match(n, d_blob, d_offs, o, cap, sid):
+        if pairs_out:   # (the "hit" buffer holds the 2 n + 1 u32 pairs)
+            ix.match_batch_dev_pairs(n, d_blob.data_ptr(), d_offs.data_ptr(), o["hit"].data_ptr(), o["out"].data_ptr(),
+                                     cap, o["err"].data_ptr(), sid)
+        else:
+            ix.match_batch_dev(n, d_blob.data_ptr(), d_offs.data_ptr(), o["hit"].data_ptr(), o["out"].data_ptr(), cap,
+                               o["err"].data_ptr(), sid)
+
+    def total_of(o, n):
+        v = int(o["hit"][n].item())
+        return v & 0xFFFFFFFF if pairs_out else v
+
     def step(cap):
         k = kstep[0]
         kstep[0] += 1
@@ -293,8 +311,7 @@ def main():
             ta = time.perf_counter()
             ix.apply(d.flags, d.blob, d.offs, d.vals)
             apply_s[0] += time.perf_counter() - ta
-        ix.match_batch_dev(B, d_blob.data_ptr(), d_offs.data_ptr(), o["hit"].data_ptr(), o["out"].data_ptr(), cap,
-                           o["err"].data_ptr(), sid)
+        match(B, d_blob, d_offs, o, cap, sid)
         if filter_sharded:
             if world == 1:   # one shard: the merge alone (the exchange is the identity)
                 return shard.merge_local(o["hit"], o["out"], sid)
@@ -305,10 +322,9 @@ def main():
     total_hits = 0
     batch_hits = []
     for d_blob, d_offs in d_in:
-        ix.match_batch_dev(B, d_blob.data_ptr(), d_offs.data_ptr(), outs[0]["hit"].data_ptr(),
-                           outs[0]["out"].data_ptr(), 0, outs[0]["err"].data_ptr(), stream)
+        match(B, d_blob, d_offs, outs[0], 0, stream)
         torch.cuda.synchronize()
-        batch_hits.append(int(outs[0]["hit"][-1].item()))
+        batch_hits.append(total_of(outs[0], B))
         total_hits = max(total_hits, batch_hits[-1])
         if split > 1:   # each sub-batch's CSR is offset from 0: its own capacity is its own hits
             hv = outs[0]["hit"]
@@ -358,7 +374,7 @@ def main():
                   else [(0, B, outs[last_k % nstreams])])
     last_hits = 0
     for lo, n, o in last_parts:
-        h = int(o["hit"][n].item())
+        h = total_of(o, n)
         assert h <= cap
         last_hits += h
     merged_total = int(merged[0][-1].item()) if merged is not None else None
@@ -378,8 +394,7 @@ def main():
              "out": torch.zeros(max(cap, 1), dtype=torch.int32, device=dev)}   # the timed steps' outputs stay intact
 
     def iso_launch(d_blob, d_offs):
-        ix.match_batch_dev(B, d_blob.data_ptr(), d_offs.data_ptr(), spare["hit"].data_ptr(),
-                           spare["out"].data_ptr(), cap, spare["err"].data_ptr(), stream)
+        match(B, d_blob, d_offs, spare, cap, stream)
 
     ix.profile(False)
     torch.cuda.synchronize()
@@ -399,8 +414,8 @@ def main():
     paths1 = [ix.debug_get(k) for k in (_native.TM_DEBUG_PATH_PHASES, _native.TM_DEBUG_PATH_SMALL,
                                         _native.TM_DEBUG_PATH_LANE)]
     path = max(range(3), key=lambda i: paths1[i] - paths0[i])
-    kernel = ("k_walk_fast", "k_walk_small", "k_walk_small")[path]
-    one_launch = path != 0
+    kernel = "k_walk_pairs" if pairs_out else ("k_walk_fast", "k_walk_small", "k_walk_small")[path]
+    one_launch = path != 0 or pairs_out   # (the kernel writes the values too)
     el_t = torch.tensor([el], dtype=torch.float64, device=cdev)
     if world > 1:
         dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
@@ -575,6 +590,9 @@ def main():
         # the last timed step's output of this rank (its own shard's lists for c4)
         host_parts = [(lo, n, o["hit"][: n + 1].cpu().numpy().view(np.uint64), o["out"].cpu().numpy().view(np.uint32))
                       for lo, n, o in last_parts]
+        if pairs_out:   # (first position, count) per topic -> the same slicing as a CSR's [start, end)
+            host_parts = [(lo, n, hh.view(np.uint32)[: 2 * n].reshape(n, 2).astype(np.uint64), ho)
+                          for lo, n, hh, ho in host_parts]
         rng = np.random.default_rng(0x454D5158)
         idx = np.sort(rng.choice(B, ns, replace=False))
         lts = tsets[last_batch]
@@ -583,7 +601,11 @@ def main():
         mism = 0
         for j, i in enumerate(idx):
             lo, _, host_hit, host_out = next(p for p in host_parts if p[0] <= i < p[0] + p[1])
-            g = host_out[int(host_hit[i - lo]):int(host_hit[i - lo + 1])]
+            if pairs_out:
+                p0, c0 = int(host_hit[i - lo][0]), int(host_hit[i - lo][1])
+                g = host_out[p0:p0 + c0]
+            else:
+                g = host_out[int(host_hit[i - lo]):int(host_hit[i - lo + 1])]
             e = ovals[int(ohit[j]):int(ohit[j + 1])]
             mism += int(not np.array_equal(g, e))
         # algorithmic bytes per launch of the timed kernel (SURVEY.md 8d per
@@ -679,7 +701,7 @@ def main():
         "config": {"workload": f"{a.config}: {desc}", "filters": nf if (filter_sharded or level0) else len(fs),
                    "topics_per_gpu_step": B, "global_batch": topics_per_step, "parallelism": par,
                    "streams": nstreams, "sub_batches_per_step": split, "distinct_batches": R,
-                   "table_copies": copies},
+                   "table_copies": copies, "outputs": a.outputs},
         "roofline": {"bound": "hbm", "achieved": None if achieved is None else round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": None if achieved is None else round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,

@@ -27,7 +27,7 @@ EXPORTS = ("tm_create", "tm_destroy", "tm_apply_deltas", "tm_sync", "tm_match_ba
            "tm_matches_filter", "tm_apply_deltas_ex", "tm_read_begin", "tm_read_end", "tm_epoch",
            "tm_create_replicas", "tm_replica_stats", "tm_debug_set", "tm_debug_get", "tm_match_batch32_ex",
            "tm_match_batch32_dev", "tm_matches_filter_ex", "tm_host_alloc_ex", "tm_commit",
-           "tm_match_batch32_pairs")
+           "tm_match_batch32_pairs", "tm_match_batch_dev_pairs")
 TM_ALLOC_VRAM = 1
 TM_DEBUG_LB_SPINS, TM_DEBUG_LB_FAIL_BLOCK, TM_DEBUG_LB_LAUNCHES, TM_DEBUG_PHASES = 1, 2, 3, 4
 TM_DEBUG_FAILED_BATCHES, TM_DEBUG_RETRIED_BATCHES = 5, 6
@@ -107,6 +107,7 @@ def load_library(path: Path | None = None):
         "tm_stream_release": (i32, [vp, vp]),
         "tm_match_batch_ex": (i32, [vp, u64, vp, vp, vp, vp, u64, vp, u32, vp]),
         "tm_match_batch_dev_ex": (i32, [vp, u64, vp, vp, vp, vp, u64, vp, u32, vp, vp]),
+        "tm_match_batch_dev_pairs": (i32, [vp, u64, vp, vp, vp, vp, u64, vp, vp]),
         "tm_sort_segments": (i32, [vp, u64, vp, vp, u64, u32, vp, vp]),
         "tm_apply_deltas_ex": (i32, [vp, u64, vp, vp, vp, vp, vp, C.POINTER(u64)]),
         "tm_commit": (i32, [vp, u64, vp, vp, vp, vp, vp, C.POINTER(u64)]),
@@ -373,6 +374,11 @@ class Index:
                         stream: int | None = None, order: int = TM_ORDER_TRAVERSAL, d_unique: int | None = None):
         self._check(self._lib.tm_match_batch_dev_ex(self._h, n, d_blob, d_offs, d_hit, d_out, cap, d_err, order,
                                                     d_unique, stream))
+
+    def match_batch_dev_pairs(self, n: int, d_blob: int, d_offs: int, d_pairs: int, d_out: int, cap: int, d_err: int,
+                              stream: int | None = None):
+        """tm_match_batch_dev_pairs: per-topic (first position, count) u32 pairs, d_pairs[2 n] = total."""
+        self._check(self._lib.tm_match_batch_dev_pairs(self._h, n, d_blob, d_offs, d_pairs, d_out, cap, d_err, stream))
 
     def sort_segments(self, n: int, d_hit: int, d_vals: int, cap: int, order: int = TM_ORDER_SORTED,
                       d_unique: int | None = None, stream: int | None = None):

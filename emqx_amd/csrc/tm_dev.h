@@ -120,6 +120,13 @@ hipError_t launch_match_phase1(const DevIndex &ix, const Workspace &ws, uint64_t
 hipError_t launch_match_phase2(const DevIndex &ix, const Workspace &ws, uint64_t n, const uint8_t *bytes,
                                const uint64_t *offs, uint64_t *hit_offs, uint32_t *out, uint64_t cap,
                                hipStream_t s);
+// A batch with its hit lists as per-topic (first position, count) pairs
+// (pairs[2 t], pairs[2 t + 1]; pairs[2 n] = the values' total, saturated at
+// 2^32 - 1): k_walk_pairs writes every value itself, k_tail_pairs finishes the
+// deep and overflowed topics -- two launches, no scan and no k_emit
+hipError_t launch_match_pairs(const DevIndex &ix, const Workspace &ws, uint64_t n, const uint8_t *bytes,
+                              const uint64_t *offs, uint8_t *err, uint32_t *pairs, uint32_t *out, uint64_t cap,
+                              hipStream_t s, hipEvent_t ev_walk0 = nullptr, hipEvent_t ev_walk1 = nullptr);
 // The whole batch in ONE launch when the index allows it: up to SMALL_TOPICS
 // topics (small_path_ok: the fallback store of k_walk_small holds the index's
 // depth) on k_walk_small (16 or 8 lanes per topic); the two phases otherwise

@@ -2152,6 +2152,35 @@ int tm_match_batch_dev_ex(tm_index *ix, uint64_t n, const uint8_t *bytes, const 
     return prof_end(ix, ev, s);
 }
 
+int tm_match_batch_dev_pairs(tm_index *ix, uint64_t n, const uint8_t *bytes, const uint64_t *offs, uint32_t *pairs,
+                             uint32_t *out, uint64_t cap, uint8_t *err, void *stream) {
+    if (!ix) return fail(nullptr, TM_EINVAL, "tm_match_batch_dev_pairs: null handle");
+    if (!pairs || (n && (!offs || !bytes || !err))) return fail(ix, TM_EINVAL, "tm_match_batch_dev_pairs: null buffer");
+    if (reinterpret_cast<uintptr_t>(pairs) & 7) return fail(ix, TM_EINVAL, "tm_match_batch_dev_pairs: pairs not 8-byte aligned");
+    if (n >= 0xFFFFFFFFull) return fail(ix, TM_EINVAL, "tm_match_batch_dev_pairs: batch too large");
+    if (!out) cap = 0;
+    if (cap > 0xFFFFFFFFull) cap = 0xFFFFFFFFull;   // (32-bit positions)
+    std::lock_guard<std::mutex> g(ix->mu);
+    hipStream_t s = pick_stream(ix, stream);
+    int rc, grp = 0;
+    Lane *ln;
+    if ((rc = dev_group(ix, grp))) return rc;
+    if ((rc = collect_patch(ix))) return rc;
+    const int r = pick_copy(ix, grp, nullptr, s, true);
+    ix->rep[r].last_use = ++ix->tick;
+    ix->rep[r].batches++;
+    if ((rc = dev_lane(ix, s, r, ln))) return rc;
+    if ((rc = sync_locked(ix, ln->r, s))) return rc;
+    if ((rc = ensure_ws(ix, n, *ln))) return rc;
+    const DevIndex d = dev_view(ix, ln->r);
+    tm_index::ProfEv ev;
+    if ((rc = prof_begin(ix, ev, s))) return rc;
+    HIPCHK(ix, launch_match_pairs(d, ln->w, n, bytes, offs, err, pairs, out, cap, s, ev.w0, ev.w1));
+    ix->path_batches[PATH_PHASES]++;
+    if ((rc = batch_done(ix, *ln))) return rc;
+    return prof_end(ix, ev, s);
+}
+
 int tm_match_batch_dev(tm_index *ix, uint64_t n, const uint8_t *bytes, const uint64_t *offs, uint64_t *hit_offs,
                        uint32_t *out, uint64_t cap, uint8_t *err, void *stream) {
     return tm_match_batch_dev_ex(ix, n, bytes, offs, hit_offs, out, cap, err, TM_ORDER_TRAVERSAL, nullptr, stream);

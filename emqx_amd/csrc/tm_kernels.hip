@@ -1950,6 +1950,191 @@ __global__ __launch_bounds__(EMIT_BLOCK) void k_emit(DevIndex ix, Workspace ws, 
     wave_emit(ix, s_off[wv], s_rel[wv], s_flg[wv], R, base, endp, out, cap);
 }
 
+// ------------------------------------------------- one-pass batches as pairs
+//
+// tm_match_batch_dev_pairs: the hit lists as per-topic (first position, count)
+// pairs, so a walk block writes its own values -- no scan, no range lists, no
+// k_emit.  A block of 64 topics walks as k_walk_fast does (ranges in
+// registers), scans its counts in the wave, reserves its values' span with ONE
+// atomic on the batch's value counter (ws.blk[0], zero between batches), writes
+// its topics' pairs, then flattens its ranges into the (now dead) walk LDS and
+// writes the span as whole aligned quads (wave_emit, k_emit's copy).  Spans
+// are disjoint and in completion order, not topic order.  Deep topics (the
+// tail lists) and topics with more than RCAP ranges (span reserved here, values
+// re-walked) are finished by k_tail_pairs, whose last block writes the total.
+struct WalkLds {
+    uint32_t wid[FAST_L * WALK_BLOCK];
+    uint32_t pend[(FAST_L + 1) * WALK_BLOCK];
+    uint8_t len[FAST_L * WALK_BLOCK];
+};
+struct SpanLds {
+    uint32_t off[WR];
+    uint32_t rel[WR + 1];
+    uint8_t flg[WR];
+};
+static_assert(WALK_BLOCK == 64, "k_walk_pairs: one wave per block");
+
+__global__ __launch_bounds__(WALK_BLOCK, 8) void k_walk_pairs(DevIndex ix, Workspace ws, uint64_t n,
+                                                           const uint8_t *blob, const uint64_t *offs, uint8_t *err,
+                                                           uint32_t *pairs, uint32_t *out, uint64_t cap) {
+    __shared__ union { WalkLds w; SpanLds e; } s;
+    const uint32_t lane = threadIdx.x;
+    const uint64_t t = (uint64_t)blockIdx.x * WALK_BLOCK + lane;
+    RangeEmit em;
+    em.cnt = 0; em.nr = 0;
+    int deep = -1, ovf = -1;
+    if (t < n) {
+        LdsStore<FAST_L> st{s.w.wid + lane, s.w.pend + lane, s.w.len + lane, WALK_BLOCK, 0};
+        uint32_t levels;
+        const int rc = match_topic(ix, GlobalSrc{blob}, offs[t], offs[t + 1], st, em, &levels);
+        if (rc == RC_DEEP) {   // k_tail_pairs walks it (flag, pair and values)
+            deep = tail_list(ix, levels);
+            em.cnt = 0; em.nr = 0;
+        } else {
+            if (rc != RC_OK) { em.cnt = 0; em.nr = 0; }
+            __builtin_nontemporal_store((uint8_t)(rc == RC_BADARG ? 1 : 0), err + t);
+            if (em.nr > RCAP) ovf = L_OVF_MID;   // span reserved below, values re-walked by k_tail_pairs
+        }
+    }
+    list_push_wave(ws, n, deep, (uint32_t)t);
+    list_push_wave(ws, n, ovf, (uint32_t)t);
+    uint32_t tot;
+    const uint32_t ex = wave_excl_scan32(em.cnt, tot);
+    uint64_t base = 0;
+    if (lane == 0 && tot) base = atomicAdd((unsigned long long *)&ws.blk[0], (unsigned long long)tot);
+    base = ((uint64_t)(uint32_t)__shfl((int)(base >> 32), 0, 64) << 32) | (uint32_t)__shfl((int)(uint32_t)base, 0, 64);
+    if (t < n && deep < 0) {
+        const uint64_t pc = (uint64_t)(uint32_t)(base + ex) | ((uint64_t)em.cnt << 32);
+        __builtin_nontemporal_store(pc, reinterpret_cast<uint64_t *>(pairs) + t);
+    }
+    if (!tot) return;   // (wave-uniform)
+    // the span: one skip range for an overflowed topic, else its ranges
+    wave_sync();   // every lane is done with the walk's LDS
+    uint32_t R;
+    const bool skip = ovf >= 0;
+    const uint32_t r0 = wave_excl_scan32(skip ? (em.cnt ? 1u : 0u) : em.nr, R);
+    if (skip && em.cnt) {
+        s.e.off[r0] = 0;
+        s.e.rel[r0] = ex;
+        s.e.flg[r0] = RF_SKIP;
+    }
+    uint32_t acc = 0;
+#pragma unroll
+    for (int i = 0; i < RCAP; i++) {
+        if (skip || (uint32_t)i >= em.nr) break;
+        s.e.off[r0 + i] = em.r[i].x;   // RUN_INLINE: the value itself
+        s.e.rel[r0 + i] = ex + acc;
+        s.e.flg[r0 + i] = (em.r[i].y & RUN_INLINE) ? RF_INLINE : 0;
+        acc += em.r[i].y & RUN_CNT;
+    }
+    if (lane == 0) s.e.rel[R] = tot;
+    wave_sync();
+    wave_emit(ix, s.e.off, s.e.rel, s.e.flg, R, base, base + tot, out, cap);
+}
+
+// a tail topic's values at pos: from its ranges, or (more than RCAP) re-walked
+template <class S>
+__device__ __forceinline__ void tail_values(const DevIndex &ix, const uint8_t *blob, const uint64_t *offs, uint64_t t,
+                                            const RangeEmit &em, uint64_t pos, uint32_t *out, uint64_t cap, S &st) {
+    if (em.nr > RCAP) {
+        DirectEmit de{ix.vals, out, pos, cap};
+        match_topic(ix, GlobalSrc{blob}, offs[t], offs[t + 1], st, de);
+        return;
+    }
+#pragma unroll
+    for (int i = 0; i < RCAP; i++) {   // (static indices: the ranges stay in registers)
+        if ((uint32_t)i >= em.nr) break;
+        const uint2 r = em.r[i];
+        const uint32_t c = r.y & RUN_CNT;
+        for (uint32_t k = 0; k < c; k++, pos++)
+            if (pos < cap) out[pos] = (r.y & RUN_INLINE) ? r.x : ix.vals[r.x + k];
+    }
+}
+
+// one tail-list topic of a pairs batch (every lane of the wave calls it; live:
+// the lane has a topic): walk, reserve (one atomic per wave), pair, flag, values
+template <class S>
+__device__ void tail_pair(const DevIndex &ix, const Workspace &ws, uint64_t n, const uint8_t *blob,
+                          const uint64_t *offs, bool live, uint64_t t, uint8_t *err, uint32_t *pairs, uint32_t *out,
+                          uint64_t cap, S &st) {
+    RangeEmit em;
+    em.cnt = 0; em.nr = 0;
+    if (live) {
+        uint32_t levels;
+        const int rc = match_topic(ix, GlobalSrc{blob}, offs[t], offs[t + 1], st, em, &levels);
+        // (the lists' stores hold every level the walk can use; a deeper topic
+        // than the global scratch holds is flagged 2, no hits)
+        if (rc != RC_OK) { em.cnt = 0; em.nr = 0; }
+        err[t] = rc == RC_BADARG ? 1 : (rc == RC_DEEP ? 2 : 0);
+    }
+    uint32_t tot;
+    const uint32_t ex = wave_excl_scan32(em.cnt, tot);
+    const uint32_t lane = threadIdx.x & 63;
+    uint64_t base = 0;
+    if (lane == 0 && tot) base = atomicAdd((unsigned long long *)&ws.blk[0], (unsigned long long)tot);
+    base = ((uint64_t)(uint32_t)__shfl((int)(base >> 32), 0, 64) << 32) | (uint32_t)__shfl((int)(uint32_t)base, 0, 64);
+    if (!live) return;
+    const uint64_t pos = base + ex;
+    reinterpret_cast<uint64_t *>(pairs)[t] = (uint64_t)(uint32_t)pos | ((uint64_t)em.cnt << 32);
+    tail_values(ix, blob, offs, t, em, pos, out, cap, st);
+}
+
+// The second (last) launch of a pairs batch: the MID / DEEP lists (topics the
+// walk handed over, walked here from scratch) and the overflow list (span
+// reserved by the walk, values re-walked into it); the grid's last block
+// writes the total, zeroes the value counter and resets the lists
+__global__ __launch_bounds__(MID_BLOCK) void k_tail_pairs(DevIndex ix, Workspace ws, uint64_t n, const uint8_t *blob,
+                                                          const uint64_t *offs, uint8_t *err, uint32_t *pairs,
+                                                          uint32_t *out, uint64_t cap, uint32_t mid_grid) {
+    __shared__ uint32_t s_wid[MID_L * MID_BLOCK];
+    __shared__ uint32_t s_pend[(MID_L + 1) * MID_BLOCK];
+    __shared__ uint8_t s_len[MID_L * MID_BLOCK];
+    static_assert(MID_BLOCK == 64, "one wave per tail block");
+    if (blockIdx.x < mid_grid) {
+        LdsStore<MID_L> st{s_wid + threadIdx.x, s_pend + threadIdx.x, s_len + threadIdx.x, MID_BLOCK, 0};
+        const uint32_t cnt = ws.list_n[L_MID];
+        const uint32_t *lst = ws.lists + (uint64_t)L_MID * n;
+        for (uint32_t i0 = blockIdx.x * MID_BLOCK; i0 < cnt; i0 += mid_grid * MID_BLOCK) {
+            const uint32_t i = i0 + threadIdx.x;
+            tail_pair(ix, ws, n, blob, offs, i < cnt, i < cnt ? lst[i] : 0, err, pairs, out, cap, st);
+        }
+        const uint32_t co = ws.list_n[L_OVF_MID];
+        const uint32_t *lo = ws.lists + (uint64_t)L_OVF_MID * n;
+        for (uint32_t i = blockIdx.x * MID_BLOCK + threadIdx.x; i < co; i += mid_grid * MID_BLOCK) {
+            const uint64_t t = lo[i];
+            DirectEmit de{ix.vals, out, pairs[2 * t], cap};
+            match_topic(ix, GlobalSrc{blob}, offs[t], offs[t + 1], st, de);
+        }
+    } else {
+        const uint32_t lane = (blockIdx.x - mid_grid) * 64 + threadIdx.x;   // < DEEP_LANES
+        GlobalStore st{ws.deep_wid + (uint64_t)lane * MAX_LEVELS, ws.deep_stk + (uint64_t)lane * (MAX_LEVELS + 1),
+                       ws.deep_plus + (uint64_t)lane * MAX_LEVELS, 0};
+        const uint32_t cnt = ws.list_n[L_DEEP];
+        const uint32_t *lst = ws.lists + (uint64_t)L_DEEP * n;
+        for (uint32_t i0 = lane - threadIdx.x; i0 < cnt; i0 += DEEP_LANES) {
+            const uint32_t i = i0 + threadIdx.x;
+            tail_pair(ix, ws, n, blob, offs, i < cnt, i < cnt ? lst[i] : 0, err, pairs, out, cap, st);
+        }
+    }
+    // the grid's last block: every block's reservations have returned (their
+    // atomics drained before its ticket), so the counter is the total
+    __shared__ uint32_t s_last;
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    if (threadIdx.x == 0) s_last = atomicAdd(&ws.list_n[L_COUNT + 1], 1u) == gridDim.x - 1;
+    __syncthreads();
+    if (!s_last || threadIdx.x) return;
+    const uint64_t total = __hip_atomic_load(&ws.blk[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    pairs[2 * n] = total > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)total;
+    atomicExch((unsigned long long *)&ws.blk[0], 0ull);
+    for (int k = 0; k < L_COUNT; k++) {
+        const uint32_t len = atomicExch(&ws.list_n[k], 0u);
+        if (ws.hint_d) ws.hint_d[k] = len;
+    }
+    if (ws.hint_d) ws.hint_d[L_COUNT] = n < 0xFFFFFFFFull ? (uint32_t)n : 0xFFFFFFFFu;
+    atomicExch(&ws.list_n[L_COUNT + 1], 0u);
+}
+
 // The LITE fallback store of k_walk_small<8> (FAST_L levels resolving only
 // need_levels()) holds every topic of a shallow index without a
 // '#'-not-last key.  (Round 5's k_walk_lane, one lane per topic, ran on the same
@@ -2260,6 +2445,23 @@ hipError_t launch_match_phase2(const DevIndex &ix, const Workspace &ws, uint64_t
     const uint32_t mg = tail_blocks(ws, n, L_OVF_MID, MID_GRID);
     hipLaunchKernelGGL(k_rewalk_tail, dim3(mg + DEEP_LANES / 64), dim3(MID_BLOCK), 0, s, ix, ws, n, bytes, offs,
                        hit_offs, out, cap, mg);
+    return hipGetLastError();
+}
+
+// a pairs batch (tm_match_batch_dev_pairs): the walk writing its own values,
+// then the tail (deep and overflowed topics, the total): two launches
+hipError_t launch_match_pairs(const DevIndex &ix, const Workspace &ws, uint64_t n, const uint8_t *bytes,
+                              const uint64_t *offs, uint8_t *err, uint32_t *pairs, uint32_t *out, uint64_t cap,
+                              hipStream_t s, hipEvent_t ev_walk0, hipEvent_t ev_walk1) {
+    hipError_t e;
+    if (!n) return hipMemsetAsync(pairs, 0, sizeof(uint32_t), s);
+    if (ev_walk0 && (e = hipEventRecord(ev_walk0, s)) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_walk_pairs, dim3(blocks_for(n, WALK_BLOCK)), dim3(WALK_BLOCK), 0, s, ix, ws, n, bytes, offs, err,
+                       pairs, out, cap);
+    if (ev_walk1 && (e = hipEventRecord(ev_walk1, s)) != hipSuccess) return e;
+    const uint32_t mg = tail_blocks(ws, n, L_MID, MID_GRID_BIG);
+    hipLaunchKernelGGL(k_tail_pairs, dim3(mg + DEEP_LANES / 64), dim3(MID_BLOCK), 0, s, ix, ws, n, bytes, offs, err,
+                       pairs, out, cap, mg);
     return hipGetLastError();
 }
 

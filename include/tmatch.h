@@ -314,6 +314,23 @@ int tm_match_batch_dev_ex(tm_index *h, uint64_t n, const uint8_t *d_topic_bytes,
                           uint64_t *d_out_hit_offsets, uint32_t *d_out_values, uint64_t cap,
                           uint8_t *d_out_err, uint32_t order, uint32_t *d_out_unique, void *stream);
 
+/* tm_match_batch_dev (traversal order) with the hit lists as per-topic (first
+ * position, count) pairs, as tm_match_batch32_pairs gives them:
+ * d_out_pairs[2 i] / [2 i + 1] (u32; the array 8-byte aligned, 2 n + 1
+ * entries), d_out_pairs[2 n] the values' total (saturated at 2^32 - 1; values
+ * past cap, which is clamped to 2^32 - 1, are dropped).  Each topic's values
+ * are contiguous and in traversal order; the topics' spans are disjoint but NOT
+ * in topic order.  Two launches per batch: each walk block writes its own
+ * topics' values into a span it reserves with one atomic (no cross-block scan,
+ * no range lists, no emit kernel), then one small kernel finishes the topics
+ * deeper than the walk's level store and those with more than 8 value runs.
+ * For a consumer that builds one list per topic (the NIF, a fan-out stage):
+ * the same lists as tm_match_batch_dev, fewer passes over HBM.  (No reference
+ * counterpart: emqx_topic_index:matches/3 per topic, emqx_topic_index.erl:54-57.) */
+int tm_match_batch_dev_pairs(tm_index *h, uint64_t n, const uint8_t *d_topic_bytes, const uint64_t *d_topic_offsets,
+                             uint32_t *d_out_pairs, uint32_t *d_out_values, uint64_t cap, uint8_t *d_out_err,
+                             void *stream);
+
 /* Sort each segment of a device CSR (n segments, d_hit_offsets[n+1]) in
  * place in TM_ORDER_SORTED / TM_ORDER_UNIQUE order (d_out_unique as above),
  * asynchronously on `stream`: e.g. the merged lists of tm_merge_shards, which

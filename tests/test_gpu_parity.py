@@ -2556,10 +2556,12 @@ def test_combined_small_batches_equal_single_launches(torch_dev, kind, land, tic
     b0 = ix.debug_get(_native.TM_DEBUG_COMBINED_BATCHES)
     errors = []
 
-    def caller(k, rounds):
+    def caller(k, rounds, bar):
         pb, po, outs, _ = sets[k]
         try:
             for _ in range(rounds):
+                if bar is not None:
+                    bar.wait(timeout=30)
                 h, v, e = ix.match_batch32(pb, po, outs[1])
                 rh, rv, re_ = ref[k]
                 if not (np.array_equal(h, rh) and np.array_equal(v, rv) and np.array_equal(e, re_)):
@@ -2568,8 +2570,13 @@ def test_combined_small_batches_equal_single_launches(torch_dev, kind, land, tic
         except Exception as ex:   # noqa: BLE001 -- reported below
             errors.append((k, repr(ex)))
 
-    def run(rounds):
-        th = [threading.Thread(target=caller, args=(k, rounds)) for k in range(len(sets))]
+    def run(rounds, together=False):
+        # together: every round starts at a barrier, so the callers enter the
+        # library within a few us of each other (their Python result checks
+        # hold the GIL for far longer than a launch takes, so free-running
+        # callers seldom overlap in the library)
+        bar = threading.Barrier(len(sets)) if together else None
+        th = [threading.Thread(target=caller, args=(k, rounds, bar)) for k in range(len(sets))]
         for t in th:
             t.start()
         for t in th:
@@ -2577,7 +2584,7 @@ def test_combined_small_batches_equal_single_launches(torch_dev, kind, land, tic
 
     run(40)   # up to 3 leaders: whether callers queue depends on kernel speed
     ix.debug_set(_native.TM_DEBUG_COMBINE, 1)
-    run(20)   # one leader: 7 callers queue behind every launch
+    run(20, together=True)   # one leader: the other callers queue behind its launch
     ix.debug_set(_native.TM_DEBUG_COMBINE, 3)
     assert not errors, errors
     launches = ix.debug_get(_native.TM_DEBUG_COMBINED_LAUNCHES) - l0
@@ -3025,3 +3032,100 @@ def test_pairs_batches_equal_the_csr_path_and_the_oracle(torch_dev, kind):
         pairs, vals, err = ix.match_batch32_pairs(pb, po, prs[0])
         assert check(k, pairs, vals, err)
     assert ix.debug_get(_native.TM_DEBUG_PATH_PHASES) > p0
+
+
+# ------------------------------------------------- device batches as pairs
+
+def pairs_batch(torch, ix: _native.Index, ts: wl.ItemSet, cap=None, stream=None, reps=1):
+    """tm_match_batch_dev_pairs on device copies of ts: (pairs [n, 2], total,
+    values, err) on the host"""
+    dev = torch.device("cuda:0")
+    n = len(ts)
+    blob = torch.from_numpy(ts.blob.copy()).to(dev)
+    offs = torch.from_numpy(ts.offs.view(np.int64).copy()).to(dev)
+    pairs = torch.full((2 * n + 2,), -1, dtype=torch.int32, device=dev)
+    if cap is None:
+        h, _, _ = ix.match_batch(ts.blob, ts.offs)
+        cap = int(h[-1])
+    out = torch.full((max(cap, 1),), -1, dtype=torch.int32, device=dev)
+    err = torch.full((max(n, 1),), 7, dtype=torch.uint8, device=dev)
+    s = torch.cuda.current_stream().cuda_stream if stream is None else stream
+    for _ in range(reps):
+        ix.match_batch_dev_pairs(n, blob.data_ptr(), offs.data_ptr(), pairs.data_ptr(), out.data_ptr(), cap,
+                                 err.data_ptr(), s)
+    torch.cuda.synchronize()
+    p = pairs.cpu().numpy().view(np.uint32)
+    return p[:2 * n].reshape(n, 2).astype(np.int64), int(p[2 * n]), out.cpu().numpy().view(np.uint32)[:cap], \
+        err.cpu().numpy()[:n]
+
+
+def assert_pairs_same(torch, ix: _native.Index, o: Oracle, ts: wl.ItemSet, reps=1):
+    """the pairs equal the oracle's CSR topic by topic (values and order), the
+    spans are disjoint and tile [0, total), the flags equal the oracle's"""
+    cnt, _, ohit, ovals = o.match_batch(ts.blob, ts.offs)
+    pr, total, vals, err = pairs_batch(torch, ix, ts, reps=reps)
+    n = len(ts)
+    assert np.array_equal(err.astype(np.int64), np.where(cnt < 0, -cnt, 0)), "badarg / too-deep flags differ"
+    assert np.array_equal(pr[:, 1], np.maximum(cnt, 0)), "hit counts differ"
+    assert total == int(ohit[-1])
+    live = np.nonzero(pr[:, 1])[0]
+    order = live[np.argsort(pr[live, 0], kind="stable")]
+    ends = pr[order, 0] + pr[order, 1]
+    assert (len(order) == 0 and total == 0) or (pr[order[0], 0] == 0 and np.array_equal(pr[order[1:], 0], ends[:-1])
+                                                 and ends[-1] == total), "spans overlap or leave gaps"
+    for i in range(n):
+        c = int(pr[i, 1])
+        if c:
+            p = int(pr[i, 0])
+            assert np.array_equal(vals[p:p + c], ovals[int(ohit[i]):int(ohit[i + 1])]), \
+                f"topic {i} {ts.item(i)!r}: values differ"
+    return pr, total
+
+
+@pytest.mark.parametrize("cfg,nf,nt", [(3, 200_000, 120_000), (30, 200_000, 60_000), (1, 10_000, 50_000),
+                                      (2, 20_000, 40_000)])
+def test_pairs_device_batches_vs_oracle(torch_dev, cfg, nf, nt):
+    """tm_match_batch_dev_pairs (k_walk_pairs + k_tail_pairs): every topic's
+    values exact vs the oracle in traversal order; C3deep's tail lists (MID and
+    DEEP) and C2's overflowed topics (more than RCAP runs: span reserved by
+    the walk, values re-walked by the tail) included; run twice on the same
+    workspace (the value counter and the lists are reset between batches)"""
+    fs = wl.filters(2 if cfg == 2 else (3 if cfg == 30 else cfg), nf)
+    ts = wl.topics(cfg, nf, nt)
+    ix, o = gpu_index(fs), oracle_of(fs)
+    assert_pairs_same(torch_dev, ix, o, ts, reps=2)
+
+
+def test_pairs_device_edge_cases(torch_dev):
+    """deep topics (26 levels: MID list; 300 and 1000 levels: DEEP list),
+    overflowing runs, badarg topics, a '#'-not-last cut, an empty batch, and a
+    capacity smaller than the total (values past cap dropped, total reported)"""
+    letters = [chr(ord("a") + i).encode() for i in range(26)]
+    T = b"/".join(letters)
+    deep = b"/".join(b"l%d" % i for i in range(300))
+    filters = [b"#", T + b"/#", T + b"/+", b"+/" * 26 + b"#", b"a/+/c/+/e/+/g/+/i/+/k/+/m/+/o/+/q/+/s/+/u/+/w/+/y/+/#",
+               deep, deep + b"/#", b"l0/+/#", b"+/l1/#", deep.rsplit(b"/", 1)[0] + b"/+",
+               b"a/#", b"+/#", b"+/+/#", b"a/b/#", b"+/b/#", b"a/+/#", b"a/b/+", b"+/+", b"a/+", b"+/b",
+               b"a/b", b"#", b"+/+/+/#", b"x/#/y", b"x/#"]
+    topics = [T, T + b"/1", deep, deep + b"/x", b"a/b", b"a/b/c", b"l0/l1", b"/".join([b"w"] * 1000),
+              b"/".join([b"+"] * 40), T + b"/#", b"x", b"x/y", b"", b"q/+/r"]
+    r = random.Random(5)
+    topics = [r.choice(topics) for _ in range(3000)] + topics
+    fs = items_of(filters)
+    ix, o = gpu_index(fs), oracle_of(fs)
+    pr, total = assert_pairs_same(torch_dev, ix, o, items_of(topics), reps=2)
+    assert pr[:, 1].max() > 8   # 'a/b' overflows the RCAP ranges
+    # empty batch: the total alone
+    e = items_of([])
+    p0, t0, _, _ = pairs_batch(torch_dev, ix, e, cap=0)
+    assert t0 == 0 and len(p0) == 0
+    # capacity too small: total reported, every value below cap where the pairs say
+    ts = items_of(topics)
+    cnt, _, ohit, ovals = o.match_batch(ts.blob, ts.offs)
+    pr2, t2, v2, _ = pairs_batch(torch_dev, ix, ts, cap=100)
+    assert t2 == int(ohit[-1])
+    for i in range(len(ts)):
+        p, c = int(pr2[i, 0]), int(pr2[i, 1])
+        if p < 100 and c:
+            k = min(c, 100 - p)
+            assert np.array_equal(v2[p:p + k], ovals[int(ohit[i]):int(ohit[i]) + k])

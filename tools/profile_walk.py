@@ -24,6 +24,11 @@ def main():
                    help="topic order in the batch: generator stream, byte-sorted, bucketed "
                         "by the hash of the first two levels (locality study), or by predicted work "
                         "(level count, then hit count from a first device pass: divergence study)")
+    p.add_argument("--window", type=int, default=0,
+                   help="with --order sorted/bucket: order only inside consecutive windows of this many topics "
+                        "(the upper bound of a block-local grouping: its gain without its cost)")
+    p.add_argument("--outputs", default="csr", choices=["csr", "pairs"],
+                   help="tm_match_batch_dev (CSR) or tm_match_batch_dev_pairs ((first position, count) pairs)")
     p.add_argument("--filter-order", default="stream", choices=["stream", "sorted"],
                    help="insertion order of the filters (node ids follow it): generator stream or "
                         "byte-sorted, i.e. trie nodes numbered depth first (layout study)")
@@ -68,15 +73,17 @@ def main():
         ts = wl.topics(gen, nf, a.batch, first=k * a.batch)
         if a.order != "stream":
             items = ts.items()
+            W = a.window if a.window > 0 else len(items)
             if a.order == "sorted":
-                items = sorted(items)
+                items = [t for lo in range(0, len(items), W) for t in sorted(items[lo:lo + W])]
             elif a.order == "work":   # lanes of a wave get topics of similar work
                 hh, _, _ = ix.match_batch(ts.blob, ts.offs)
                 hits = np.diff(hh.astype(np.int64))
                 key = [(t.count(b"/"), int(h)) for t, h in zip(items, hits)]
                 items = [items[i] for i in sorted(range(len(items)), key=key.__getitem__)]
             else:
-                items = sorted(items, key=lambda t: hash(b"/".join(t.split(b"/")[:2])) & 0xFFFF)
+                items = [t for lo in range(0, len(items), W)
+                         for t in sorted(items[lo:lo + W], key=lambda t: hash(b"/".join(t.split(b"/")[:2])) & 0xFFFF)]
             blob, offs = _native.pack_strings(items)
             ts = wl.ItemSet(blob, offs, np.zeros(len(items), np.uint32), np.zeros(len(items), np.uint8))
         d_in.append((torch.from_numpy(ts.blob).to(dev), torch.from_numpy(ts.offs.view(np.int64)).to(dev)))
@@ -86,18 +93,27 @@ def main():
     S = max(1, a.streams)
     streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(S - 1)]
     tot = 0
+    pairs = a.outputs == "pairs"
+
+    def run(d_blob, d_offs, h_, o_, cap, e_, sid):
+        if pairs:   # (h_ holds the 2 n + 1 u32 pairs)
+            ix.match_batch_dev_pairs(a.batch, d_blob.data_ptr(), d_offs.data_ptr(), h_.data_ptr(), o_, cap,
+                                     e_.data_ptr(), sid)
+        else:
+            ix.match_batch_dev(a.batch, d_blob.data_ptr(), d_offs.data_ptr(), h_.data_ptr(), o_, cap, e_.data_ptr(),
+                               sid)
+
     for d_blob, d_offs in d_in:
-        ix.match_batch_dev(a.batch, d_blob.data_ptr(), d_offs.data_ptr(), d_hit.data_ptr(), 0, 0, d_err.data_ptr(), s)
+        run(d_blob, d_offs, d_hit, 0, 0, d_err, s)
         torch.cuda.synchronize()
-        tot = max(tot, int(d_hit[-1]))
+        tot = max(tot, int(d_hit[-1]) & (0xFFFFFFFF if pairs else ~0))
     outs = [(torch.zeros(a.batch + 1, dtype=torch.int64, device=dev), torch.zeros(a.batch, dtype=torch.uint8, device=dev),
              torch.zeros(max(tot, 1), dtype=torch.int32, device=dev)) for _ in range(S)]
 
     def launch(k):
         d_blob, d_offs = d_in[k % R]
         h_, e_, o_ = outs[k % S]
-        ix.match_batch_dev(a.batch, d_blob.data_ptr(), d_offs.data_ptr(), h_.data_ptr(), o_.data_ptr(), tot,
-                           e_.data_ptr(), streams[k % S].cuda_stream)
+        run(d_blob, d_offs, h_, o_.data_ptr(), tot, e_, streams[k % S].cuda_stream)
 
     for k in range(S):   # every stream's workspace exists before the timed launches
         launch(k)
@@ -143,7 +159,7 @@ def main():
     paths = [ix.debug_get(k) for k in (_native.TM_DEBUG_PATH_PHASES, _native.TM_DEBUG_PATH_SMALL,
                                        _native.TM_DEBUG_PATH_LANE)]
     assert not any(bool(e_.any().item()) for _, e_, _ in outs), "err flags set"
-    print(f"{a.config}/{a.order}/filters-{a.filter_order} streams={S} paths(phases,small,lane)={paths} filters={len(fs)} batch={a.batch} rotate={R} hits<={tot} "
+    print(f"{a.config}/{a.outputs}/{a.order}{'/w' + str(a.window) if a.window else ''}/filters-{a.filter_order} streams={S} paths(phases,small,lane)={paths} filters={len(fs)} batch={a.batch} rotate={R} hits<={tot} "
           f"wall/batch={el / a.batches * 1e3:.3f}ms walk={w / n:.4f}ms batch_dev={b / n:.4f}ms "
           f"rate={a.batch * a.batches / el / 1e9:.3f}G/s device_MiB={st['device_bytes'] / 2**20:.0f}", flush=True)
 

@@ -1,0 +1,3 @@
+set -e
+bash tools/gpu.sh r6c tests:pairs bench:bench_pairs:--steps,20,--warmup,5,--outputs,pairs,--latency-batches,0,--route-writers,0 \
+  walk:--outputs,pairs walk:--outputs,csr walk:--order,sorted,--window,4096 walk:--order,sorted,--window,65536 walk:--order,sorted
