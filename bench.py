@@ -281,17 +281,17 @@ def main():
     pairs_out = a.outputs == "pairs"
     assert not (pairs_out and (filter_sharded or level0 or a.split > 1)), "--outputs pairs: topic-sharded, no split"
 
-    def match(n, d_blob, d_offs, o, cap, sid):
-        if pairs_out:   # (the "hit" buffer holds the 2 n + 1 u32 pairs)
+    def match(n, d_blob, d_offs, o, cap, sid, pairs=None):
+        if pairs_out if pairs is None else pairs:   # (the "hit" buffer holds the 2 n + 1 u32 pairs)
             ix.match_batch_dev_pairs(n, d_blob.data_ptr(), d_offs.data_ptr(), o["hit"].data_ptr(), o["out"].data_ptr(),
                                      cap, o["err"].data_ptr(), sid)
         else:
             ix.match_batch_dev(n, d_blob.data_ptr(), d_offs.data_ptr(), o["hit"].data_ptr(), o["out"].data_ptr(), cap,
                                o["err"].data_ptr(), sid)
 
-    def total_of(o, n):
+    def total_of(o, n, pairs=None):
         v = int(o["hit"][n].item())
-        return v & 0xFFFFFFFF if pairs_out else v
+        return v & 0xFFFFFFFF if (pairs_out if pairs is None else pairs) else v
 
     def step(cap):
         k = kstep[0]
@@ -321,10 +321,22 @@ def main():
     # sizing pass (no values written) over every batch, then the output buffers
     total_hits = 0
     batch_hits = []
+    pairs_slack = [0]
     for d_blob, d_offs in d_in:
         match(B, d_blob, d_offs, outs[0], 0, stream)
         torch.cuda.synchronize()
         batch_hits.append(total_of(outs[0], B))
+        # pairs spans may leave gaps: + 64 x the most values of any 64 consecutive topics (tmatch.h)
+        if pairs_out:
+            c = outs[0]["hit"][:B].view(torch.int32).view(B, 2)[:, 1].to(torch.int64)
+            blk = torch.nn.functional.pad(c, (0, (-B) % 64)).view(-1, 64).sum(dim=1).max()
+        elif not (filter_sharded or split > 1):
+            hv = outs[0]["hit"]
+            idx = torch.arange(0, B + 64, 64, device=dev).clamp(max=B)
+            blk = (hv[idx[1:]] - hv[idx[:-1]]).max()
+        else:
+            blk = torch.zeros((), dtype=torch.int64)
+        pairs_slack[0] = max(pairs_slack[0], 64 * int(blk.item()))
         total_hits = max(total_hits, batch_hits[-1])
         if split > 1:   # each sub-batch's CSR is offset from 0: its own capacity is its own hits
             hv = outs[0]["hit"]
@@ -332,7 +344,8 @@ def main():
         if xch is not None:
             xch.size_from(outs[0]["hit"])   # per-peer exchange capacity: setup, not the data path
     slack = a.deltas * (a.steps + a.warmup) * 64 if dchunks else 0   # churn may add hits
-    cap = total_hits + slack
+    cap = total_hits + slack + (pairs_slack[0] if pairs_out else 0)
+    cap_pairs = total_hits + slack + pairs_slack[0]
     for o in outs:
         o["out"] = torch.zeros(max(cap, 1), dtype=torch.int32, device=dev)
     for _ in range(a.warmup):
@@ -376,6 +389,8 @@ def main():
     for lo, n, o in last_parts:
         h = total_of(o, n)
         assert h <= cap
+        if pairs_out:   # the extent: no value dropped
+            assert (int(o["hit"][n].item()) >> 32) <= cap
         last_hits += h
     merged_total = int(merged[0][-1].item()) if merged is not None else None
     merged_topics = merged[0].numel() - 1 if merged is not None else None
@@ -420,6 +435,39 @@ def main():
     if world > 1:
         dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
     el_max = float(el_t.item())
+
+    # The other output form over the same batches, streams and step count
+    # (rank 0 of a one-GPU topic-sharded run): the CSR next to the pairs
+    # headline, or the pairs next to a CSR one
+    alt = None
+    if world == 1 and not (filter_sharded or level0 or split > 1 or dchunks):
+        alt_pairs = not pairs_out
+        aouts = [{"hit": torch.zeros(B + 1, dtype=torch.int64, device=dev),
+                  "err": torch.zeros(B, dtype=torch.uint8, device=dev),
+                  "out": torch.zeros(max(cap_pairs, 1), dtype=torch.int32, device=dev)} for _ in range(nstreams)]
+
+        def alt_step(k):
+            match(B, *d_in[k % R], aouts[k % nstreams], cap_pairs, streams[k % nstreams].cuda_stream, pairs=alt_pairs)
+
+        for k in range(a.warmup):
+            alt_step(k)
+        torch.cuda.synchronize()
+        gc.collect()
+        gc.disable()
+        t1 = time.perf_counter()
+        for k in range(a.steps):
+            alt_step(a.warmup + k)
+        torch.cuda.synchronize()
+        el_alt = time.perf_counter() - t1
+        gc.enable()
+        assert all(total_of(o, B, pairs=alt_pairs) <= cap_pairs for o in aouts)
+        if alt_pairs:   # the extent (nothing dropped)
+            assert all((int(o["hit"][B].item()) >> 32) <= cap_pairs for o in aouts)
+        alt = {"outputs": "pairs" if alt_pairs else "csr", "value": round(B * a.steps / el_alt, 1),
+               "ms_per_step": round(el_alt / a.steps * 1e3, 4),
+               "api": "tm_match_batch_dev_pairs" if alt_pairs else "tm_match_batch_dev",
+               "note": "same batches, streams, warm-up and step count, timed after the headline region"}
+        del aouts
 
     # whole-job topics/s: topic-sharded = every rank's own batch; filter-sharded = the one shared batch
     topics_per_step = B if filter_sharded else world * B
@@ -468,6 +516,17 @@ def main():
         assert rc == 0, rc
         lat_native[f"{lb}_u32_vram_inputs_pairs"] = {"p50_ms": round(out[0], 4), "p99_ms": round(out[1], 4),
                                                      "mean_ms": round(out[2], 4)}
+        # the CSR call with k_walk_small's blocks taking a start-order ticket
+        # (TM_DEBUG_SMALL_TICKET: forward progress of the look-back by
+        # construction, include/tmatch.h) -- what the guarantee costs
+        ix.debug_set(_native.TM_DEBUG_SMALL_TICKET, 1)
+        out = (ctypes.c_double * 3)()
+        rc = hb.tmb_single_ex(ix._h, lb, _native._ptr(sub.blob), _native._ptr(sub.offs), int(hh[-1]) + 4096,
+                              a.latency_batches * 5, 5, out)
+        ix.debug_set(_native.TM_DEBUG_SMALL_TICKET, 0)
+        assert rc == 0, rc
+        lat_native[f"{lb}_u32_vram_inputs_ticket"] = {"p50_ms": round(out[0], 4), "p99_ms": round(out[1], 4),
+                                                      "mean_ms": round(out[2], 4)}
         if a.concurrency > 0:
             conc = []
             if a.combine_leaders is not None:
@@ -660,7 +719,8 @@ def main():
     if pmc.exists():
         try:
             pj = json.loads(pmc.read_text())
-            same = (pj.get("filters") == len(fs) and pj.get("batch") == B and pj.get("rotate") == R)
+            same = (pj.get("filters") == len(fs) and pj.get("batch") == B and pj.get("rotate") == R
+                    and kernel in (pj.get("walk_kernel") or ""))
             fresh = pj.get("source_hash") == source_hash()
             if same and fresh:
                 traffic = pj.get("walk_hbm_bytes_per_launch")
@@ -668,7 +728,7 @@ def main():
                 traffic_note = f"{pj.get('source')} (kernel sources {pj['source_hash']}, this tree)"
             else:
                 traffic_note = ("refused: " + ("stale (measured on other kernel sources)" if not fresh
-                                              else "different workload shape") + f" -- {pj.get('source')}")
+                                              else "different workload shape or kernel") + f" -- {pj.get('source')}")
         except (ValueError, KeyError, OSError) as e:
             traffic_note = f"unreadable: {e!r}"
     # practical roofline of a pointer-chasing walk: the measured memory-side
@@ -722,6 +782,7 @@ def main():
                                            f"overlapping the other {nstreams - 1} streams' kernels); "
                                            f"GBps_per_step = algorithmic bytes / ms_per_step"}},
         "checks": {"walk_isolated_le_ms_per_step": bool(iso_ms <= ms_per_step)},
+        "other_outputs": alt,
         "cpu_baseline": cpu,
         "matched_ids_per_s": round(last_hits * (1 if filter_sharded else world) * a.steps / el_max, 1),
         "hits_per_topic": round(merged_total / max(merged_topics, 1) if merged_total is not None else last_hits / B, 3),

@@ -89,6 +89,8 @@ struct Workspace {
     uint8_t *deep_plus;   // [DEEP_LANES * MAX_LEVELS] '+' levels of each deep lane's path
     uint64_t *look;       // [(n / SM_TOPICS + 4) * LB_STRIDE] one-launch kernels: per block, one look-back word (lb_word)
     uint32_t *pairs;      // [2 * SMALL_SEGS] pairs launches: per segment, its values counter and block ticket (zero between launches)
+    uint64_t *vres;       // [VRES_WORDS] a device pairs batch's value reservations (zero between batches):
+                          // region k's fill at [k * VRES_STRIDE], its failed attempts at [+1]; the pool at [VRES_POOL]
     // list lengths of the last count-mode batch that finished here ([0, L_COUNT))
     // and its topic count ([L_COUNT]; 0: none yet), written by the device into
     // mapped host memory: the next batch sizes its tail grids from them;
@@ -104,6 +106,15 @@ constexpr int SM_TICK = L_COUNT + 4;     // Workspace::list_n words: k_walk_smal
 constexpr int LIST_SLOTS = SM_TICK + SMALL_SEGS;   // Workspace::list_n entries
 constexpr int HINT_FAIL = L_COUNT + 1;    // Workspace::hint_* word of the fail flag
 constexpr int HINT_WORDS = L_COUNT + 2;
+// A device pairs batch reserves its values' spans in VRES_K regions of the
+// output (a walk block takes region blockIdx % VRES_K, each region's counter on
+// a line of its own) and, when its region is full, in the pool at the top: one
+// hot counter took 15.6k same-address device-scope atomics per 1M-topic batch,
+// +80 us on a 250 us walk
+constexpr int VRES_K = 64;
+constexpr int VRES_STRIDE = 16;                      // u64 words between counters (128 B)
+constexpr int VRES_POOL = VRES_K * VRES_STRIDE;
+constexpr int VRES_WORDS = VRES_POOL + VRES_STRIDE;
 constexpr int SM_TOPICS = 16;             // topics per block of the one-launch small-batch path
 constexpr int SM_TB = 256;                // topic bytes it stages in LDS (longer topics: the lane walk)
 constexpr int SM_VSTAGE = 1024;           // values of a block it stages in LDS before one contiguous write

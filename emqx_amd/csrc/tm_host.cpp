@@ -101,6 +101,7 @@ struct Lane {
     bool owned = false;       // stream created by the library (host-API lane)
     bool busy = false;        // checked out by a host-API caller
     bool used = false;        // `done` has been recorded
+    bool drained = false;     // `done` was seen complete since it was last recorded (no API call needed)
     hipEvent_t done = nullptr;   // after the lane's last batch: later patches wait for it
     uint64_t tick = 0;        // last use (LRU of device-API lanes)
     uint32_t tag = 0;         // launches on this workspace (the one-launch path's look-back tag)
@@ -1372,7 +1373,20 @@ bool batch_failed(tm_index *ix, Lane &ln) {
 int batch_done(tm_index *ix, Lane &ln) {
     HIPCHK(ix, hipEventRecord(ln.done, ln.s));
     ln.used = true;
+    ln.drained = false;
     return TM_OK;
+}
+
+// Is a batch of the lane still running?  (caller holds ix->mu)  A lane seen
+// drained stays so until its next batch: the copy pickers, the committer and
+// the patches ask about every lane under the index lock, and with concurrent
+// callers that was dozens of event queries (and stream waits) per launch and
+// per commit, while most lanes were long idle
+bool lane_busy(Lane &l) {
+    if (!l.used || l.drained) return false;
+    if (hipEventQuery(l.done) == hipErrorNotReady) return true;
+    l.drained = true;
+    return false;
 }
 
 // Apply logged patch q to replica r on stream st.  Patches rewrite the tables
@@ -1401,7 +1415,7 @@ int apply_patch(tm_index *ix, int r, uint64_t q, hipStream_t st, bool wait_reade
     }
     if (wait_readers)   // (not for a copy known to be idle, nor again behind a patch just queued on st)
         for (auto &l : ix->lanes)
-            if (l->r == r && l->used && l->s != st) HIPCHK(ix, hipStreamWaitEvent(st, l->done, 0));
+            if (l->r == r && l->s != st && lane_busy(*l)) HIPCHK(ix, hipStreamWaitEvent(st, l->done, 0));
     if (R.last_patch) HIPCHK(ix, hipStreamWaitEvent(st, R.last_patch, 0));
     // a small patch (a route write's few runs) is read by the patch kernel
     // straight from the mapped pinned slot: one command on the stream instead
@@ -1467,7 +1481,17 @@ int collect_patch_locked(tm_index *ix) {
     return rc;
 }
 
+// (TM_HOST_TIMING) collect_patch_locked2's parts: the tables' runs, the ring
+// slot's reuse (a lagging replica brought up and waited for), the pinned copy
+std::atomic<uint64_t> g_col_n{0}, g_col_runs_ns{0}, g_col_slot_ns{0}, g_col_copy_ns{0};
+const bool g_col_timing = getenv("TM_HOST_TIMING") != nullptr;
+uint64_t col_now() {
+    return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+        std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 int collect_patch_locked2(tm_index *ix) {
+    const uint64_t t0 = g_col_timing ? col_now() : 0;
     std::vector<PatchRun> runs;
     std::vector<uint32_t> data;
     int rc;
@@ -1482,6 +1506,7 @@ int collect_patch_locked2(tm_index *ix) {
     if ((rc = collect(ix, ix->wbits, 8, runs, data))) return rc;
     const uint64_t nr = runs.size(), nw = data.size();
     if (!nr) return TM_OK;
+    const uint64_t t1 = g_col_timing ? col_now() : 0;
     const uint64_t q = ix->patch_seq + 1;
     const uint32_t k = (uint32_t)((q - 1) % PATCH_RING);
     PatchSlot &p = ix->patch[k];
@@ -1496,6 +1521,7 @@ int collect_patch_locked2(tm_index *ix) {
             }
         }
     }
+    const uint64_t t2 = g_col_timing ? col_now() : 0;
     const uint64_t bytes = nr * sizeof(PatchRun) + nw * 4;
     if (bytes > p.pin_cap || !p.pin) {
         if (p.pin) HIPCHK(ix, hipHostFree(p.pin));
@@ -1512,6 +1538,10 @@ int collect_patch_locked2(tm_index *ix) {
     memcpy(p.pin, runs.data(), nr * sizeof(PatchRun));
     memcpy(p.pin + nr * sizeof(PatchRun), data.data(), nw * 4);
     p.bytes = bytes; p.nr = nr; p.seq = q;
+    if (g_col_timing) {
+        g_col_n++;
+        g_col_runs_ns += t1 - t0; g_col_slot_ns += t2 - t1; g_col_copy_ns += col_now() - t2;
+    }
     ix->patch_seq = q;
     ix->patch_bytes += nw * 4;
     ix->uploads++;
@@ -1554,7 +1584,7 @@ int pick_copy(tm_index *ix, int g, const int *busy, hipStream_t s = nullptr, boo
             for (auto &l : ix->lanes) {
                 if (l->r != r || !l->used) continue;
                 if (l->s == s) { mine = std::max<uint64_t>(mine, l->tick); continue; }
-                if (hipEventQuery(l->done) == hipErrorNotReady) { free_here = false; break; }
+                if (lane_busy(*l)) { free_here = false; break; }
             }
             if (free_here && (pick < 0 || mine > pick_tick)) { pick = r; pick_tick = mine; }
         }
@@ -1564,7 +1594,7 @@ int pick_copy(tm_index *ix, int g, const int *busy, hipStream_t s = nullptr, boo
         if (!ok(r)) continue;
         bool idle = true;
         for (auto &l : ix->lanes)
-            if (l->r == r && l->used && hipEventQuery(l->done) == hipErrorNotReady) { idle = false; break; }
+            if (l->r == r && lane_busy(*l)) { idle = false; break; }
         if (idle) return r;
     }
     int best = -1;
@@ -1604,7 +1634,8 @@ DevIndex dev_view_build(tm_index *ix, int r) {
 // ------------------------------------------------------------------ lanes
 
 void free_workspace(Workspace &w) {
-    void *wb[] = {w.cnt, w.nr, w.rng, w.lists, w.list_n, w.blk, w.deep_wid, w.deep_stk, w.deep_plus, w.look, w.pairs};
+    void *wb[] = {w.cnt, w.nr, w.rng, w.lists, w.list_n, w.blk, w.deep_wid, w.deep_stk, w.deep_plus, w.look, w.pairs,
+                  w.vres};
     for (void *p : wb) if (p) (void)hipFree(p);
     if (w.hint_h) (void)hipHostFree(w.hint_h);
     w = Workspace{};
@@ -1742,6 +1773,8 @@ int ensure_ws(tm_index *ix, uint64_t n, Lane &ln) {
         HIPCHK(ix, hipMemsetAsync(w.list_n, 0, LIST_SLOTS * 4, ln.s));
         HIPCHK(ix, hipMalloc(&w.pairs, 2 * SMALL_SEGS * 4));
         HIPCHK(ix, hipMemsetAsync(w.pairs, 0, 2 * SMALL_SEGS * 4, ln.s));
+        HIPCHK(ix, hipMalloc(&w.vres, VRES_WORDS * 8));
+        HIPCHK(ix, hipMemsetAsync(w.vres, 0, VRES_WORDS * 8, ln.s));
         HIPCHK(ix, hipHostMalloc(&w.hint_h, HINT_WORDS * 4, hipHostMallocMapped));
         std::memset(w.hint_h, 0, HINT_WORDS * 4);
         HIPCHK(ix, hipHostGetDevicePointer(reinterpret_cast<void **>(&w.hint_d), w.hint_h, 0));
@@ -1925,6 +1958,11 @@ int tm_destroy(tm_index *ix) {
                 g_cmbt.release_ns * us / g, g_cmbt.done_ns * us / g,
                 g_cmbt.req_ns * us / std::max<double>(1.0, (double)g_cmbt.reqs));
     }
+    if (g_cmb_timing && g_col_n) {
+        const double c = (double)g_col_n, us = 1e-3;
+        fprintf(stderr, "tm collect: %lu patches; per patch us: runs %.1f slot-reuse %.1f pinned-copy %.1f\n",
+                (unsigned long)g_col_n.load(), g_col_runs_ns * us / c, g_col_slot_ns * us / c, g_col_copy_ns * us / c);
+    }
     if (g_cmb_timing && g_cmt.n) {
         const double c = (double)g_cmt.n, us = 1e-3;
         fprintf(stderr, "tm commit: %lu commits; per commit us: image %.1f lock %.1f collect %.1f wait-idle %.1f "
@@ -2038,7 +2076,7 @@ int tm_commit(tm_index *ix, uint64_t n, const uint8_t *ops, const uint8_t *fb, c
         const bool late = std::chrono::steady_clock::now() - t0 > COMMIT_WAIT;
         bool busy[MAX_REPLICAS] = {};   // copies with a batch still reading them (one event query per lane)
         for (auto &l : ix->lanes)
-            if (l->used && !busy[l->r] && hipEventQuery(l->done) == hipErrorNotReady) busy[l->r] = true;
+            if (!busy[l->r] && lane_busy(*l)) busy[l->r] = true;
         for (int gi = 0; gi < ix->ngroups; gi++) {
             if (done[gi]) continue;
             int pick = -1, copies = 0;

@@ -1956,12 +1956,12 @@ __global__ __launch_bounds__(EMIT_BLOCK) void k_emit(DevIndex ix, Workspace ws, 
 // pairs, so a walk block writes its own values -- no scan, no range lists, no
 // k_emit.  A block of 64 topics walks as k_walk_fast does (ranges in
 // registers), scans its counts in the wave, reserves its values' span with ONE
-// atomic on the batch's value counter (ws.blk[0], zero between batches), writes
-// its topics' pairs, then flattens its ranges into the (now dead) walk LDS and
-// writes the span as whole aligned quads (wave_emit, k_emit's copy).  Spans
-// are disjoint and in completion order, not topic order.  Deep topics (the
-// tail lists) and topics with more than RCAP ranges (span reserved here, values
-// re-walked) are finished by k_tail_pairs, whose last block writes the total.
+// atomic on its region's counter (vres_reserve), writes its topics' pairs, then
+// flattens its ranges into the (now dead) walk LDS and writes the span as
+// whole aligned quads (wave_emit, k_emit's copy).  Spans are disjoint, in
+// completion order, and may leave gaps.  Deep topics (the tail lists) and
+// topics with more than RCAP ranges (span reserved here, values re-walked) are
+// finished by k_tail_pairs, whose last block writes the total and the extent.
 struct WalkLds {
     uint32_t wid[FAST_L * WALK_BLOCK];
     uint32_t pend[(FAST_L + 1) * WALK_BLOCK];
@@ -1973,6 +1973,27 @@ struct SpanLds {
     uint8_t flg[WR];
 };
 static_assert(WALK_BLOCK == 64, "k_walk_pairs: one wave per block");
+
+// A span of T values for region g of K (Workspace::vres): [g Rg, (g + 1) Rg)
+// while the region has room, else the pool [K Rg, cap); a position past cap
+// means the values were dropped (the caller's extent check).  The regions take
+// 7/8 of cap; a region's unused tail is a gap in the output.  K: one region per
+// 128 walk blocks, at most VRES_K (a batch of < 16k topics has one region and
+// fills it in order; a larger one spreads its blocks' atomics over K lines).
+__device__ __forceinline__ uint32_t vres_k(uint64_t n) {
+    const uint64_t k = (n + WALK_BLOCK - 1) / WALK_BLOCK / 128;
+    return k < 1 ? 1u : (k > VRES_K ? (uint32_t)VRES_K : (uint32_t)k);
+}
+__device__ __forceinline__ uint64_t vres_region(uint64_t cap, uint32_t K) { return (cap - cap / 8) / K; }
+__device__ __forceinline__ uint64_t vres_reserve(const Workspace &ws, uint64_t cap, uint32_t K, uint32_t g, uint32_t T) {
+    const uint64_t Rg = vres_region(cap, K);
+    if (g < K && Rg) {
+        const uint64_t old = atomicAdd((unsigned long long *)&ws.vres[g * VRES_STRIDE], (unsigned long long)T);
+        if (old + T <= Rg) return g * Rg + old;
+        atomicAdd((unsigned long long *)&ws.vres[g * VRES_STRIDE + 1], (unsigned long long)T);
+    }
+    return K * Rg + atomicAdd((unsigned long long *)&ws.vres[VRES_POOL], (unsigned long long)T);
+}
 
 __global__ __launch_bounds__(WALK_BLOCK, 8) void k_walk_pairs(DevIndex ix, Workspace ws, uint64_t n,
                                                            const uint8_t *blob, const uint64_t *offs, uint8_t *err,
@@ -2001,10 +2022,14 @@ __global__ __launch_bounds__(WALK_BLOCK, 8) void k_walk_pairs(DevIndex ix, Works
     uint32_t tot;
     const uint32_t ex = wave_excl_scan32(em.cnt, tot);
     uint64_t base = 0;
-    if (lane == 0 && tot) base = atomicAdd((unsigned long long *)&ws.blk[0], (unsigned long long)tot);
+    if (lane == 0 && tot) {
+        const uint32_t K = vres_k(n);
+        base = vres_reserve(ws, cap, K, blockIdx.x % K, tot);
+    }
     base = ((uint64_t)(uint32_t)__shfl((int)(base >> 32), 0, 64) << 32) | (uint32_t)__shfl((int)(uint32_t)base, 0, 64);
     if (t < n && deep < 0) {
-        const uint64_t pc = (uint64_t)(uint32_t)(base + ex) | ((uint64_t)em.cnt << 32);
+        const uint64_t p = base + ex < cap ? base + ex : cap;   // (past cap: dropped)
+        const uint64_t pc = (uint64_t)(uint32_t)p | ((uint64_t)em.cnt << 32);
         __builtin_nontemporal_store(pc, reinterpret_cast<uint64_t *>(pairs) + t);
     }
     if (!tot) return;   // (wave-uniform)
@@ -2071,11 +2096,11 @@ __device__ void tail_pair(const DevIndex &ix, const Workspace &ws, uint64_t n, c
     const uint32_t ex = wave_excl_scan32(em.cnt, tot);
     const uint32_t lane = threadIdx.x & 63;
     uint64_t base = 0;
-    if (lane == 0 && tot) base = atomicAdd((unsigned long long *)&ws.blk[0], (unsigned long long)tot);
+    if (lane == 0 && tot) base = vres_reserve(ws, cap, vres_k(n), VRES_K, tot);   // (the pool)
     base = ((uint64_t)(uint32_t)__shfl((int)(base >> 32), 0, 64) << 32) | (uint32_t)__shfl((int)(uint32_t)base, 0, 64);
     if (!live) return;
     const uint64_t pos = base + ex;
-    reinterpret_cast<uint64_t *>(pairs)[t] = (uint64_t)(uint32_t)pos | ((uint64_t)em.cnt << 32);
+    reinterpret_cast<uint64_t *>(pairs)[t] = (uint64_t)(uint32_t)(pos < cap ? pos : cap) | ((uint64_t)em.cnt << 32);
     tail_values(ix, blob, offs, t, em, pos, out, cap, st);
 }
 
@@ -2123,10 +2148,33 @@ __global__ __launch_bounds__(MID_BLOCK) void k_tail_pairs(DevIndex ix, Workspace
     __syncthreads();
     if (threadIdx.x == 0) s_last = atomicAdd(&ws.list_n[L_COUNT + 1], 1u) == gridDim.x - 1;
     __syncthreads();
-    if (!s_last || threadIdx.x) return;
-    const uint64_t total = __hip_atomic_load(&ws.blk[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!s_last) return;
+    // the total (every region's successful reservations and the pool's) and
+    // the extent (the end of the last value position used; past cap: values
+    // were dropped), then the counters zeroed for the next batch
+    const uint32_t K = vres_k(n);
+    const uint64_t Rg = vres_region(cap, K);
+    uint64_t total = 0, extent = 0;
+    for (uint32_t k = threadIdx.x; k <= VRES_K; k += MID_BLOCK) {
+        const uint64_t f = __hip_atomic_load(&ws.vres[k * VRES_STRIDE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (k < VRES_K) {
+            const uint64_t x = __hip_atomic_load(&ws.vres[k * VRES_STRIDE + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            total += f - x;
+            if (f - x) extent = max(extent, k * Rg + (f - x));
+        } else {
+            total += f;
+            if (f) extent = max(extent, K * Rg + f);
+        }
+        ws.vres[k * VRES_STRIDE] = 0;
+        ws.vres[k * VRES_STRIDE + 1] = 0;
+    }
+    for (int d = 32; d; d >>= 1) {
+        total += (uint64_t)__shfl_xor((long long)total, d, 64);
+        extent = max(extent, (uint64_t)__shfl_xor((long long)extent, d, 64));
+    }
+    if (threadIdx.x) return;
     pairs[2 * n] = total > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)total;
-    atomicExch((unsigned long long *)&ws.blk[0], 0ull);
+    pairs[2 * n + 1] = extent > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)extent;
     for (int k = 0; k < L_COUNT; k++) {
         const uint32_t len = atomicExch(&ws.list_n[k], 0u);
         if (ws.hint_d) ws.hint_d[k] = len;
@@ -2454,7 +2502,7 @@ hipError_t launch_match_pairs(const DevIndex &ix, const Workspace &ws, uint64_t 
                               const uint64_t *offs, uint8_t *err, uint32_t *pairs, uint32_t *out, uint64_t cap,
                               hipStream_t s, hipEvent_t ev_walk0, hipEvent_t ev_walk1) {
     hipError_t e;
-    if (!n) return hipMemsetAsync(pairs, 0, sizeof(uint32_t), s);
+    if (!n) return hipMemsetAsync(pairs, 0, 2 * sizeof(uint32_t), s);
     if (ev_walk0 && (e = hipEventRecord(ev_walk0, s)) != hipSuccess) return e;
     hipLaunchKernelGGL(k_walk_pairs, dim3(blocks_for(n, WALK_BLOCK)), dim3(WALK_BLOCK), 0, s, ix, ws, n, bytes, offs, err,
                        pairs, out, cap);

@@ -315,18 +315,30 @@ int tm_match_batch_dev_ex(tm_index *h, uint64_t n, const uint8_t *d_topic_bytes,
                           uint8_t *d_out_err, uint32_t order, uint32_t *d_out_unique, void *stream);
 
 /* tm_match_batch_dev (traversal order) with the hit lists as per-topic (first
- * position, count) pairs, as tm_match_batch32_pairs gives them:
- * d_out_pairs[2 i] / [2 i + 1] (u32; the array 8-byte aligned, 2 n + 1
- * entries), d_out_pairs[2 n] the values' total (saturated at 2^32 - 1; values
- * past cap, which is clamped to 2^32 - 1, are dropped).  Each topic's values
- * are contiguous and in traversal order; the topics' spans are disjoint but NOT
- * in topic order.  Two launches per batch: each walk block writes its own
- * topics' values into a span it reserves with one atomic (no cross-block scan,
- * no range lists, no emit kernel), then one small kernel finishes the topics
- * deeper than the walk's level store and those with more than 8 value runs.
- * For a consumer that builds one list per topic (the NIF, a fan-out stage):
- * the same lists as tm_match_batch_dev, fewer passes over HBM.  (No reference
- * counterpart: emqx_topic_index:matches/3 per topic, emqx_topic_index.erl:54-57.) */
+ * position, count) pairs: d_out_pairs[2 i] / [2 i + 1] (u32; the array 8-byte
+ * aligned, 2 n + 2 entries), d_out_pairs[2 n] the values' total and
+ * d_out_pairs[2 n + 1] the extent -- the end of the highest position used
+ * (both saturated at 2^32 - 1; cap is clamped to 2^32 - 1).  Each topic's
+ * values are contiguous and in traversal order; the topics' spans are disjoint,
+ * NOT in topic order, and may leave gaps: each walk block reserves its span
+ * with one atomic in one of up to 64 regions of the output (together 7/8 of
+ * cap; one region per 8192 topics) or, when its region is full, in the pool
+ * above them, so no counter is hot.  extent > cap means values were dropped (a
+ * topic whose first position + count exceeds cap lost those values: submit
+ * the batch again with a larger cap).  With one region (batches below 16k
+ * topics) none are when cap >= total + the most values of any 64 consecutive
+ * topics; a larger batch needs, besides that, every region to receive at
+ * least 7/8 of an even share of the values (its ~128+ walk blocks' topics are
+ * interleaved with the other regions' 64 apart, so a batch whose hits are not
+ * laid out in a period of 64 topics meets it); for any layout, cap >= 8 x
+ * (total + that most) is enough (the pool alone then holds every value).
+ * Two launches per batch: the walk writes its own topics' values (no
+ * cross-block scan, no range lists, no emit kernel), then one small kernel
+ * finishes the topics deeper than the walk's level store and those with more
+ * than 8 value runs.  For a consumer that builds one list per topic (the NIF, a
+ * fan-out stage): the same lists as tm_match_batch_dev, fewer passes over HBM.
+ * (No reference counterpart: emqx_topic_index:matches/3 per topic,
+ * emqx_topic_index.erl:54-57.) */
 int tm_match_batch_dev_pairs(tm_index *h, uint64_t n, const uint8_t *d_topic_bytes, const uint64_t *d_topic_offsets,
                              uint32_t *d_out_pairs, uint32_t *d_out_values, uint64_t cap, uint8_t *d_out_err,
                              void *stream);

@@ -3036,17 +3036,27 @@ def test_pairs_batches_equal_the_csr_path_and_the_oracle(torch_dev, kind):
 
 # ------------------------------------------------- device batches as pairs
 
+def pairs_cap(ix: _native.Index, ts: wl.ItemSet) -> int:
+    """a capacity with which no value is dropped: total + 64 x the most values
+    of any 64 consecutive topics (include/tmatch.h tm_match_batch_dev_pairs)"""
+    h, _, _ = ix.match_batch(ts.blob, ts.offs)
+    c = np.diff(h.astype(np.int64))
+    if len(c) == 0:
+        return 0
+    blk = np.add.reduceat(c, np.arange(0, len(c), 64))
+    return int(h[-1]) + 64 * int(blk.max())
+
+
 def pairs_batch(torch, ix: _native.Index, ts: wl.ItemSet, cap=None, stream=None, reps=1):
     """tm_match_batch_dev_pairs on device copies of ts: (pairs [n, 2], total,
-    values, err) on the host"""
+    extent, values, err) on the host"""
     dev = torch.device("cuda:0")
     n = len(ts)
     blob = torch.from_numpy(ts.blob.copy()).to(dev)
     offs = torch.from_numpy(ts.offs.view(np.int64).copy()).to(dev)
     pairs = torch.full((2 * n + 2,), -1, dtype=torch.int32, device=dev)
     if cap is None:
-        h, _, _ = ix.match_batch(ts.blob, ts.offs)
-        cap = int(h[-1])
+        cap = pairs_cap(ix, ts)
     out = torch.full((max(cap, 1),), -1, dtype=torch.int32, device=dev)
     err = torch.full((max(n, 1),), 7, dtype=torch.uint8, device=dev)
     s = torch.cuda.current_stream().cuda_stream if stream is None else stream
@@ -3055,15 +3065,16 @@ def pairs_batch(torch, ix: _native.Index, ts: wl.ItemSet, cap=None, stream=None,
                                  err.data_ptr(), s)
     torch.cuda.synchronize()
     p = pairs.cpu().numpy().view(np.uint32)
-    return p[:2 * n].reshape(n, 2).astype(np.int64), int(p[2 * n]), out.cpu().numpy().view(np.uint32)[:cap], \
-        err.cpu().numpy()[:n]
+    return p[:2 * n].reshape(n, 2).astype(np.int64), int(p[2 * n]), int(p[2 * n + 1]), \
+        out.cpu().numpy().view(np.uint32)[:cap], err.cpu().numpy()[:n]
 
 
 def assert_pairs_same(torch, ix: _native.Index, o: Oracle, ts: wl.ItemSet, reps=1):
     """the pairs equal the oracle's CSR topic by topic (values and order), the
-    spans are disjoint and tile [0, total), the flags equal the oracle's"""
+    spans are disjoint and end by the extent (<= cap: nothing dropped), the
+    flags equal the oracle's"""
     cnt, _, ohit, ovals = o.match_batch(ts.blob, ts.offs)
-    pr, total, vals, err = pairs_batch(torch, ix, ts, reps=reps)
+    pr, total, extent, vals, err = pairs_batch(torch, ix, ts, reps=reps)
     n = len(ts)
     assert np.array_equal(err.astype(np.int64), np.where(cnt < 0, -cnt, 0)), "badarg / too-deep flags differ"
     assert np.array_equal(pr[:, 1], np.maximum(cnt, 0)), "hit counts differ"
@@ -3071,15 +3082,15 @@ def assert_pairs_same(torch, ix: _native.Index, o: Oracle, ts: wl.ItemSet, reps=
     live = np.nonzero(pr[:, 1])[0]
     order = live[np.argsort(pr[live, 0], kind="stable")]
     ends = pr[order, 0] + pr[order, 1]
-    assert (len(order) == 0 and total == 0) or (pr[order[0], 0] == 0 and np.array_equal(pr[order[1:], 0], ends[:-1])
-                                                 and ends[-1] == total), "spans overlap or leave gaps"
+    assert len(order) == 0 or (np.all(pr[order[1:], 0] >= ends[:-1]) and ends.max() == extent), "spans overlap"
+    assert extent <= len(vals), "values dropped with a sufficient capacity"
     for i in range(n):
         c = int(pr[i, 1])
         if c:
             p = int(pr[i, 0])
             assert np.array_equal(vals[p:p + c], ovals[int(ohit[i]):int(ohit[i + 1])]), \
                 f"topic {i} {ts.item(i)!r}: values differ"
-    return pr, total
+    return pr, total, extent
 
 
 @pytest.mark.parametrize("cfg,nf,nt", [(3, 200_000, 120_000), (30, 200_000, 60_000), (1, 10_000, 50_000),
@@ -3113,19 +3124,22 @@ def test_pairs_device_edge_cases(torch_dev):
     topics = [r.choice(topics) for _ in range(3000)] + topics
     fs = items_of(filters)
     ix, o = gpu_index(fs), oracle_of(fs)
-    pr, total = assert_pairs_same(torch_dev, ix, o, items_of(topics), reps=2)
+    pr, total, _ = assert_pairs_same(torch_dev, ix, o, items_of(topics), reps=2)
     assert pr[:, 1].max() > 8   # 'a/b' overflows the RCAP ranges
-    # empty batch: the total alone
+    # empty batch: the total and extent alone
     e = items_of([])
-    p0, t0, _, _ = pairs_batch(torch_dev, ix, e, cap=0)
-    assert t0 == 0 and len(p0) == 0
-    # capacity too small: total reported, every value below cap where the pairs say
+    p0, t0, x0, _, _ = pairs_batch(torch_dev, ix, e, cap=0)
+    assert t0 == 0 and x0 == 0 and len(p0) == 0
+    # capacity too small: total reported, extent past cap, every value below
+    # cap where the pairs say, and the batch after it exact again
     ts = items_of(topics)
     cnt, _, ohit, ovals = o.match_batch(ts.blob, ts.offs)
-    pr2, t2, v2, _ = pairs_batch(torch_dev, ix, ts, cap=100)
-    assert t2 == int(ohit[-1])
-    for i in range(len(ts)):
-        p, c = int(pr2[i, 0]), int(pr2[i, 1])
-        if p < 100 and c:
-            k = min(c, 100 - p)
-            assert np.array_equal(v2[p:p + k], ovals[int(ohit[i]):int(ohit[i]) + k])
+    for cap in (100, total // 2, total):
+        pr2, t2, x2, v2, _ = pairs_batch(torch_dev, ix, ts, cap=cap)
+        assert t2 == int(ohit[-1]) and (x2 > cap or cap >= total)
+        for i in range(len(ts)):
+            p, c = int(pr2[i, 0]), int(pr2[i, 1])
+            if p < cap and c:
+                k = min(c, cap - p)
+                assert np.array_equal(v2[p:p + k], ovals[int(ohit[i]):int(ohit[i]) + k])
+    assert_pairs_same(torch_dev, ix, o, ts)

@@ -86,7 +86,8 @@ def pmc_values(prof, grid, last):
     return out
 
 
-MAIN_KERNELS = ("k_walk_small", "k_walk_fast")   # the timed kernel: a one-launch batch, else the two-phase walk
+# the timed kernel: a pairs batch's walk, a one-launch batch, else the two-phase walk
+MAIN_KERNELS = ("k_walk_pairs", "k_walk_small", "k_walk_fast")
 
 
 def main_kernel(names):
