@@ -123,7 +123,7 @@ def parse():
                         "device entries, native feeder threads submitting in-place host batches while a syncer thread "
                         "applies deltas (the NIF's deployment, INTEGRATION.md 5); with fewer GPUs than N the entries "
                         "repeat the local device -- a rehearsal, not scaling")
-    p.add_argument("--outputs", default="csr", choices=["csr", "pairs"],
+    p.add_argument("--outputs", default="pairs", choices=["csr", "pairs"],
                    help="hit lists as a CSR (tm_match_batch_dev: walk, tails, scan + emit) or as per-topic "
                         "(first position, count) pairs (tm_match_batch_dev_pairs: the walk writes its own values)")
     p.add_argument("--small-kernel", default="auto", choices=["auto", "wave", "wave8"],
@@ -293,10 +293,10 @@ def main():
         v = int(o["hit"][n].item())
         return v & 0xFFFFFFFF if (pairs_out if pairs is None else pairs) else v
 
-    def step(cap):
+    def step(cap, oset=None):
         k = kstep[0]
         kstep[0] += 1
-        o = outs[k % nstreams]
+        o = (oset or outs)[k % nstreams]
         d_blob, d_offs = d_in[k % R]
         if split > 1:   # sub-batch j on stream j, into its own CSR
             for j, (lo, n) in enumerate(parts):
@@ -326,17 +326,14 @@ def main():
         match(B, d_blob, d_offs, outs[0], 0, stream)
         torch.cuda.synchronize()
         batch_hits.append(total_of(outs[0], B))
-        # pairs spans may leave gaps: + 64 x the most values of any 64 consecutive topics (tmatch.h)
+        # pairs spans may leave gaps: + 4096 x the most hits of one topic (tmatch.h)
         if pairs_out:
-            c = outs[0]["hit"][:B].view(torch.int32).view(B, 2)[:, 1].to(torch.int64)
-            blk = torch.nn.functional.pad(c, (0, (-B) % 64)).view(-1, 64).sum(dim=1).max()
+            mx = outs[0]["hit"][:B].view(torch.int32).view(B, 2)[:, 1].max()
         elif not (filter_sharded or split > 1):
-            hv = outs[0]["hit"]
-            idx = torch.arange(0, B + 64, 64, device=dev).clamp(max=B)
-            blk = (hv[idx[1:]] - hv[idx[:-1]]).max()
+            mx = (outs[0]["hit"][1:B + 1] - outs[0]["hit"][:B]).max()
         else:
-            blk = torch.zeros((), dtype=torch.int64)
-        pairs_slack[0] = max(pairs_slack[0], 64 * int(blk.item()))
+            mx = torch.zeros((), dtype=torch.int64)
+        pairs_slack[0] = max(pairs_slack[0], 4096 * int(mx.item()))
         total_hits = max(total_hits, batch_hits[-1])
         if split > 1:   # each sub-batch's CSR is offset from 0: its own capacity is its own hits
             hv = outs[0]["hit"]
@@ -353,8 +350,11 @@ def main():
     torch.cuda.synchronize()
     assert not any(bool(o["err"].any().item()) for o in outs)
 
-    ix.profile(True)
-    ix.profile_read(reset=True)
+    # (no HIP timing events inside the timed region: the library's profiling
+    # events recorded around every walk cost the three-stream step 5-7 %,
+    # DESIGN.md 5 -- the per-kernel figures come from the profiled repeat and
+    # the isolated pass below)
+    ix.profile(False)
     apply_s[0] = 0.0
     # the host loop stands in for the NIF's C caller: keep Python's cyclic
     # collector out of the timed region (a full collection stalled the GPU
@@ -377,7 +377,25 @@ def main():
     gc.enable()
     if world > 1:
         dist.barrier()
+    # the profiled repeat: the same steps again with the library's events
+    # around each walk (the overlapped per-kernel figures), untimed
+    prof_steps = 0 if (filter_sharded or split > 1 or dchunks) else a.steps
+    kstep0 = kstep[0]
+    pouts = [{"hit": torch.zeros(B + 1, dtype=torch.int64, device=dev),
+              "err": torch.zeros(B, dtype=torch.uint8, device=dev),
+              "out": torch.zeros(max(cap, 1), dtype=torch.int32, device=dev)} for _ in range(nstreams)] \
+        if prof_steps else None   # (the timed steps' outputs stay intact for the parity sample)
+    ix.profile(True)
+    ix.profile_read(reset=True)
+    tp = time.perf_counter()
+    for _ in range(prof_steps):
+        step(cap, pouts)
+    torch.cuda.synchronize()
+    el_prof = time.perf_counter() - tp
     walk_ms, batch_ms, nb = ix.profile_read(reset=True)
+    ix.profile(False)
+    kstep[0] = kstep0
+    del pouts
     if xch is not None:   # the on-device high-water mark: did any timed batch overflow the capacity?
         assert xch.check(), "filter-sharded exchange capacity overflowed during the timed steps"
     last_k = kstep[0] - 1
@@ -775,18 +793,21 @@ def main():
                                      "the walk (8 L + 32 sum|F| + 4 B per topic; the values are k_emit's)"),
                      "algorithmic_bytes_per_launch": None if walk_bytes is None else int(walk_bytes),
                      "random_request_roofline": req_ceiling,
-                     "effective": {"kernel_avg_ms_overlapped": round(walk_avg_ms, 4),
+                     "effective": {"kernel_avg_ms_overlapped": round(walk_avg_ms, 4) if nb else None,
+                                   "profiled_repeat_ms_per_step": round(el_prof / prof_steps * 1e3, 4) if prof_steps
+                                   else None,
                                    "walk_GBps_per_step": None if walk_bytes is None
                                    else round(walk_bytes / (ms_per_step * 1e-3) / 1e9, 1),
-                                   "note": f"the timed region's walks ({'per sub-batch, ' if split > 1 else ''}"
-                                           f"overlapping the other {nstreams - 1} streams' kernels); "
+                                   "note": f"the walks of a profiled repeat of the timed steps (overlapping the other "
+                                           f"{nstreams - 1} streams' kernels; HIP timing events around each walk, "
+                                           f"which the timed region does not carry); "
                                            f"GBps_per_step = algorithmic bytes / ms_per_step"}},
         "checks": {"walk_isolated_le_ms_per_step": bool(iso_ms <= ms_per_step)},
         "other_outputs": alt,
         "cpu_baseline": cpu,
         "matched_ids_per_s": round(last_hits * (1 if filter_sharded else world) * a.steps / el_max, 1),
         "hits_per_topic": round(merged_total / max(merged_topics, 1) if merged_total is not None else last_hits / B, 3),
-        "batch_device_ms": round(batch_avg_ms, 4),
+        "batch_device_ms": round(batch_avg_ms, 4) if nb else None,
         "batch_device_isolated_ms": round(iso_batch, 4),
         "batch_latency_host_ms": lat_pinned,
         "concurrent_callers": conc,

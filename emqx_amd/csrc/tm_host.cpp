@@ -127,7 +127,11 @@ struct Lane {
 // still busy with theirs (tm_options.copies).  A slot is reused only once
 // every replica has applied the patch it holds (a lagging replica is brought
 // up on its patch stream then).
-constexpr int PATCH_RING = 16;
+// 128 slots: a slot is reused only once every copy has taken its patch, and a
+// copy no batch reads lags the others; with 16 slots and a route mirror's
+// group commits (~12k/s on 3 copies) the reuse brought a lagging copy up and
+// waited for it under the index lock, 25 us per commit (TM_HOST_TIMING)
+constexpr int PATCH_RING = 128;
 constexpr uint64_t PATCH_ZC_MAX = 64 << 10;   // patches up to this size are read in place by the patch kernel
 struct PatchSlot {
     uint8_t *pin = nullptr; uint64_t pin_cap = 0;
@@ -1400,7 +1404,13 @@ int apply_patch(tm_index *ix, int r, uint64_t q, hipStream_t st, bool wait_reade
     const uint32_t k = (uint32_t)((q - 1) % PATCH_RING);
     const PatchSlot &p = ix->patch[k];
     HIPCHK(ix, hipSetDevice(R.device));
-    if (p.bytes > R.pdev_cap[k] || !R.pdev[k]) {
+    // a small patch (a route write's few runs) is read by the patch kernel
+    // straight from the mapped pinned slot: one command on the stream instead
+    // of a DMA copy and the kernel behind it (the slot is reused only after
+    // pdone, recorded behind the kernel); larger ones are copied first, into a
+    // device buffer of the slot allocated on first use
+    const bool zc = ix->patch_zc && p.pin_dev && p.bytes <= PATCH_ZC_MAX;
+    if (!zc && (p.bytes > R.pdev_cap[k] || !R.pdev[k])) {
         if (R.ppending[k]) { HIPCHK(ix, hipEventSynchronize(R.pdone[k])); R.ppending[k] = false; }
         if (R.pdev[k]) HIPCHK(ix, hipFree(R.pdev[k]));
         R.pdev[k] = nullptr;
@@ -1417,12 +1427,8 @@ int apply_patch(tm_index *ix, int r, uint64_t q, hipStream_t st, bool wait_reade
         for (auto &l : ix->lanes)
             if (l->r == r && l->s != st && lane_busy(*l)) HIPCHK(ix, hipStreamWaitEvent(st, l->done, 0));
     if (R.last_patch) HIPCHK(ix, hipStreamWaitEvent(st, R.last_patch, 0));
-    // a small patch (a route write's few runs) is read by the patch kernel
-    // straight from the mapped pinned slot: one command on the stream instead
-    // of a DMA copy and the kernel behind it (the slot is reused only after
-    // pdone, recorded behind the kernel); larger ones are copied first
     const uint8_t *src = R.pdev[k];
-    if (ix->patch_zc && p.pin_dev && p.bytes <= PATCH_ZC_MAX) {
+    if (zc) {
         src = p.pin_dev;
     } else {
         HIPCHK(ix, hipMemcpyAsync(R.pdev[k], p.pin, p.bytes, hipMemcpyHostToDevice, st));
@@ -1527,7 +1533,7 @@ int collect_patch_locked2(tm_index *ix) {
         if (p.pin) HIPCHK(ix, hipHostFree(p.pin));
         p.pin = nullptr;
         p.pin_cap = 0;
-        const uint64_t want = std::max<uint64_t>(bytes * 2, 1u << 20);
+        const uint64_t want = std::max<uint64_t>(bytes * 2, 64u << 10);
         uint8_t *np = nullptr;   // the capacity is recorded only once the buffer exists
         HIPCHK(ix, hipHostMalloc(&np, want, hipHostMallocPortable | hipHostMallocMapped));
         p.pin = np;

@@ -2081,7 +2081,7 @@ __device__ __forceinline__ void tail_values(const DevIndex &ix, const uint8_t *b
 template <class S>
 __device__ void tail_pair(const DevIndex &ix, const Workspace &ws, uint64_t n, const uint8_t *blob,
                           const uint64_t *offs, bool live, uint64_t t, uint8_t *err, uint32_t *pairs, uint32_t *out,
-                          uint64_t cap, S &st) {
+                          uint64_t cap, uint32_t wave_no, S &st) {
     RangeEmit em;
     em.cnt = 0; em.nr = 0;
     if (live) {
@@ -2096,7 +2096,10 @@ __device__ void tail_pair(const DevIndex &ix, const Workspace &ws, uint64_t n, c
     const uint32_t ex = wave_excl_scan32(em.cnt, tot);
     const uint32_t lane = threadIdx.x & 63;
     uint64_t base = 0;
-    if (lane == 0 && tot) base = vres_reserve(ws, cap, vres_k(n), VRES_K, tot);   // (the pool)
+    if (lane == 0 && tot) {   // the waves of a list take the regions in turn, as the walk's blocks do
+        const uint32_t K = vres_k(n);
+        base = vres_reserve(ws, cap, K, wave_no % K, tot);
+    }
     base = ((uint64_t)(uint32_t)__shfl((int)(base >> 32), 0, 64) << 32) | (uint32_t)__shfl((int)(uint32_t)base, 0, 64);
     if (!live) return;
     const uint64_t pos = base + ex;
@@ -2121,7 +2124,7 @@ __global__ __launch_bounds__(MID_BLOCK) void k_tail_pairs(DevIndex ix, Workspace
         const uint32_t *lst = ws.lists + (uint64_t)L_MID * n;
         for (uint32_t i0 = blockIdx.x * MID_BLOCK; i0 < cnt; i0 += mid_grid * MID_BLOCK) {
             const uint32_t i = i0 + threadIdx.x;
-            tail_pair(ix, ws, n, blob, offs, i < cnt, i < cnt ? lst[i] : 0, err, pairs, out, cap, st);
+            tail_pair(ix, ws, n, blob, offs, i < cnt, i < cnt ? lst[i] : 0, err, pairs, out, cap, i0 / MID_BLOCK, st);
         }
         const uint32_t co = ws.list_n[L_OVF_MID];
         const uint32_t *lo = ws.lists + (uint64_t)L_OVF_MID * n;
@@ -2138,7 +2141,7 @@ __global__ __launch_bounds__(MID_BLOCK) void k_tail_pairs(DevIndex ix, Workspace
         const uint32_t *lst = ws.lists + (uint64_t)L_DEEP * n;
         for (uint32_t i0 = lane - threadIdx.x; i0 < cnt; i0 += DEEP_LANES) {
             const uint32_t i = i0 + threadIdx.x;
-            tail_pair(ix, ws, n, blob, offs, i < cnt, i < cnt ? lst[i] : 0, err, pairs, out, cap, st);
+            tail_pair(ix, ws, n, blob, offs, i < cnt, i < cnt ? lst[i] : 0, err, pairs, out, cap, i0 / 64 + 1, st);
         }
     }
     // the grid's last block: every block's reservations have returned (their

@@ -326,12 +326,14 @@ int tm_match_batch_dev_ex(tm_index *h, uint64_t n, const uint8_t *d_topic_bytes,
  * above them, so no counter is hot.  extent > cap means values were dropped (a
  * topic whose first position + count exceeds cap lost those values: submit
  * the batch again with a larger cap).  With one region (batches below 16k
- * topics) none are when cap >= total + the most values of any 64 consecutive
- * topics; a larger batch needs, besides that, every region to receive at
- * least 7/8 of an even share of the values (its ~128+ walk blocks' topics are
- * interleaved with the other regions' 64 apart, so a batch whose hits are not
- * laid out in a period of 64 topics meets it); for any layout, cap >= 8 x
- * (total + that most) is enough (the pool alone then holds every value).
+ * topics) none are when cap >= total + 64 x the most hits of one topic (a
+ * region's last reservation that did not fit wastes its tail); a larger
+ * batch needs cap >= total + 4096 x the most hits of one topic and every
+ * region to receive at least 7/8 of an even share of the values (its ~128+
+ * walk blocks' topics are interleaved with the other regions' 64 apart, so a
+ * batch whose hits are not laid out in a period of 64 topics meets it); for
+ * any layout, cap >= 8 x (total + 64 x the most hits of one topic) is enough
+ * (the pool alone then holds every value).
  * Two launches per batch: the walk writes its own topics' values (no
  * cross-block scan, no range lists, no emit kernel), then one small kernel
  * finishes the topics deeper than the walk's level store and those with more

@@ -3037,14 +3037,11 @@ def test_pairs_batches_equal_the_csr_path_and_the_oracle(torch_dev, kind):
 # ------------------------------------------------- device batches as pairs
 
 def pairs_cap(ix: _native.Index, ts: wl.ItemSet) -> int:
-    """a capacity with which no value is dropped: total + 64 x the most values
-    of any 64 consecutive topics (include/tmatch.h tm_match_batch_dev_pairs)"""
+    """a capacity with which no value is dropped: total + 4096 x the most hits
+    of one topic (include/tmatch.h tm_match_batch_dev_pairs)"""
     h, _, _ = ix.match_batch(ts.blob, ts.offs)
     c = np.diff(h.astype(np.int64))
-    if len(c) == 0:
-        return 0
-    blk = np.add.reduceat(c, np.arange(0, len(c), 64))
-    return int(h[-1]) + 64 * int(blk.max())
+    return int(h[-1]) + 4096 * int(c.max()) if len(c) else 0
 
 
 def pairs_batch(torch, ix: _native.Index, ts: wl.ItemSet, cap=None, stream=None, reps=1):

@@ -108,10 +108,8 @@ def main():
         run(d_blob, d_offs, d_hit, 0, 0, d_err, s)
         torch.cuda.synchronize()
         tot = max(tot, int(d_hit[-1]) & (0xFFFFFFFF if pairs else ~0))
-        if pairs:   # spans may leave gaps (tmatch.h): + 64 x the most values of any 64 consecutive topics
-            c = d_hit[:a.batch].view(torch.int32).view(a.batch, 2)[:, 1].to(torch.int64)
-            c = torch.nn.functional.pad(c, (0, (-a.batch) % 64)).view(-1, 64).sum(dim=1)
-            slack = max(slack, 64 * int(c.max().item()))
+        if pairs:   # spans may leave gaps (tmatch.h): + 4096 x the most hits of one topic
+            slack = max(slack, 4096 * int(d_hit[:a.batch].view(torch.int32).view(a.batch, 2)[:, 1].max().item()))
     tot += slack
     outs = [(torch.zeros(a.batch + 1, dtype=torch.int64, device=dev), torch.zeros(a.batch, dtype=torch.uint8, device=dev),
              torch.zeros(max(tot, 1), dtype=torch.int32, device=dev)) for _ in range(S)]
