@@ -788,7 +788,9 @@ def main():
                      "kernel_launches": int(iso_nb),
                      "kernel_timing": (f"HIP events on the launch stream around {kernel}, {iso_passes} passes over "
                                        f"the {R} batches back to back on one stream after the timed region"),
-                     "kernel_work": ("the whole batch: walk, look-back scan and CSR emission (8 L + 32 sum|F| + "
+                     "kernel_work": ("the walk writing every value into its block's reserved span, pairs out "
+                                     "(8 L + 32 sum|F| + 4 H + 4 B per topic)" if pairs_out else
+                                     "the whole batch: walk, look-back scan and CSR emission (8 L + 32 sum|F| + "
                                      "4 H + 4 B per topic)" if one_launch else
                                      "the walk (8 L + 32 sum|F| + 4 B per topic; the values are k_emit's)"),
                      "algorithmic_bytes_per_launch": None if walk_bytes is None else int(walk_bytes),

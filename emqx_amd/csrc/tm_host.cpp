@@ -2089,7 +2089,11 @@ int tm_commit(tm_index *ix, uint64_t n, const uint8_t *ops, const uint8_t *fb, c
             for (int r = 0; r < ix->nrep; r++) {
                 if (ix->rep[r].group != gi) continue;
                 copies++;
-                if (!busy[r] && (pick < 0 || ix->rep[r].applied > ix->rep[pick].applied)) pick = r;
+                // the idle copy that lags most: every copy takes every patch in
+                // turn, so none falls PATCH_RING behind (a ring slot's reuse
+                // would otherwise bring a lagging copy up and wait for it
+                // under the index lock)
+                if (!busy[r] && (pick < 0 || ix->rep[r].applied < ix->rep[pick].applied)) pick = r;
             }
             if (pick < 0 && copies > 1 && !late) continue;   // wait for a copy to drain
             if (pick >= 0) {
