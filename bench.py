@@ -123,9 +123,11 @@ def parse():
                         "device entries, native feeder threads submitting in-place host batches while a syncer thread "
                         "applies deltas (the NIF's deployment, INTEGRATION.md 5); with fewer GPUs than N the entries "
                         "repeat the local device -- a rehearsal, not scaling")
-    p.add_argument("--outputs", default="pairs", choices=["csr", "pairs"],
+    p.add_argument("--outputs", default=None, choices=["csr", "pairs"],
                    help="hit lists as a CSR (tm_match_batch_dev: walk, tails, scan + emit) or as per-topic "
-                        "(first position, count) pairs (tm_match_batch_dev_pairs: the walk writes its own values)")
+                        "(first position, count) pairs (tm_match_batch_dev_pairs: the walk writes its own values); "
+                        "default pairs, CSR for the filter-sharded configs and --split (their merge and sub-batches "
+                        "take CSRs)")
     p.add_argument("--small-kernel", default="auto", choices=["auto", "wave", "wave8"],
                    help="the one-launch kernel of batches <= 65536 topics (latency and concurrent-caller legs): "
                         "the library's default, k_walk_small with 16 or 8 lanes per topic (TM_DEBUG_SMALL_KERNEL)")
@@ -278,6 +280,8 @@ def main():
     apply_s = [0.0]   # c5: host time inside tm_apply_deltas (the syncer's side of a churn step)
     xch = shard.Exchange(B, dev) if filter_sharded and world > 1 else None
 
+    if a.outputs is None:
+        a.outputs = "csr" if (filter_sharded or level0 or a.split > 1) else "pairs"
     pairs_out = a.outputs == "pairs"
     assert not (pairs_out and (filter_sharded or level0 or a.split > 1)), "--outputs pairs: topic-sharded, no split"
 

@@ -2057,43 +2057,28 @@ __global__ __launch_bounds__(WALK_BLOCK, 8) void k_walk_pairs(DevIndex ix, Works
     wave_emit(ix, s.e.off, s.e.rel, s.e.flg, R, base, base + tot, out, cap);
 }
 
-// a tail topic's values at pos: from its ranges, or (more than RCAP) re-walked
-template <class S>
-__device__ __forceinline__ void tail_values(const DevIndex &ix, const uint8_t *blob, const uint64_t *offs, uint64_t t,
-                                            const RangeEmit &em, uint64_t pos, uint32_t *out, uint64_t cap, S &st) {
-    if (em.nr > RCAP) {
-        DirectEmit de{ix.vals, out, pos, cap};
-        match_topic(ix, GlobalSrc{blob}, offs[t], offs[t + 1], st, de);
-        return;
-    }
-#pragma unroll
-    for (int i = 0; i < RCAP; i++) {   // (static indices: the ranges stay in registers)
-        if ((uint32_t)i >= em.nr) break;
-        const uint2 r = em.r[i];
-        const uint32_t c = r.y & RUN_CNT;
-        for (uint32_t k = 0; k < c; k++, pos++)
-            if (pos < cap) out[pos] = (r.y & RUN_INLINE) ? r.x : ix.vals[r.x + k];
-    }
-}
-
 // one tail-list topic of a pairs batch (every lane of the wave calls it; live:
-// the lane has a topic): walk, reserve (one atomic per wave), pair, flag, values
-template <class S>
-__device__ void tail_pair(const DevIndex &ix, const Workspace &ws, uint64_t n, const uint8_t *blob,
+// the lane has a topic): walk, reserve (one atomic per wave), pair, flag; the
+// wave's values written as k_walk_pairs writes them (ranges flattened into
+// LDS, whole aligned quads); a topic with more than RCAP ranges is re-walked
+// into its span afterwards.  sp aliases the MID store's LDS: a wave's walks
+// are done before it is written (wave_sync), and read before the re-walk.
+template <class S>   // (inlined: a call would pass the kernel's DevIndex and Workspace through scratch)
+__device__ __forceinline__ void tail_pair(const DevIndex &ix, const Workspace &ws, uint64_t n, const uint8_t *blob,
                           const uint64_t *offs, bool live, uint64_t t, uint8_t *err, uint32_t *pairs, uint32_t *out,
-                          uint64_t cap, uint32_t wave_no, S &st) {
-    RangeEmit em;
-    em.cnt = 0; em.nr = 0;
+                          uint64_t cap, uint32_t wave_no, S &st, SpanLds &sp) {
+    // the walk is k_walk_tail's (run_topic: count, ranges and flag into the
+    // workspace at t -- its own register budget, no scratch); the ranges are
+    // read back below by the lane that wrote them
+    uint32_t c = 0;
     if (live) {
-        uint32_t levels;
-        const int rc = match_topic(ix, GlobalSrc{blob}, offs[t], offs[t + 1], st, em, &levels);
-        // (the lists' stores hold every level the walk can use; a deeper topic
-        // than the global scratch holds is flagged 2, no hits)
-        if (rc != RC_OK) { em.cnt = 0; em.nr = 0; }
-        err[t] = rc == RC_BADARG ? 1 : (rc == RC_DEEP ? 2 : 0);
+        int ovf = -1;   // (more than RCAP ranges: re-walked below, no list)
+        const Outs o{err, nullptr, nullptr};
+        const int rc = run_topic<MODE_COUNT>(ix, ws, n, blob, offs, t, st, o, &c, &ovf);
+        if (rc == RC_DEEP) c = 0;   // (not on the lists' stores: they hold every level a walk uses)
     }
     uint32_t tot;
-    const uint32_t ex = wave_excl_scan32(em.cnt, tot);
+    const uint32_t ex = wave_excl_scan32(c, tot);
     const uint32_t lane = threadIdx.x & 63;
     uint64_t base = 0;
     if (lane == 0 && tot) {   // the waves of a list take the regions in turn, as the walk's blocks do
@@ -2101,30 +2086,60 @@ __device__ void tail_pair(const DevIndex &ix, const Workspace &ws, uint64_t n, c
         base = vres_reserve(ws, cap, K, wave_no % K, tot);
     }
     base = ((uint64_t)(uint32_t)__shfl((int)(base >> 32), 0, 64) << 32) | (uint32_t)__shfl((int)(uint32_t)base, 0, 64);
-    if (!live) return;
     const uint64_t pos = base + ex;
-    reinterpret_cast<uint64_t *>(pairs)[t] = (uint64_t)(uint32_t)(pos < cap ? pos : cap) | ((uint64_t)em.cnt << 32);
-    tail_values(ix, blob, offs, t, em, pos, out, cap, st);
+    if (live)
+        reinterpret_cast<uint64_t *>(pairs)[t] = (uint64_t)(uint32_t)(pos < cap ? pos : cap) | ((uint64_t)c << 32);
+    if (!tot) return;   // (wave-uniform)
+    const uint32_t nr = live && c ? ws.nr[t] : 0;
+    const bool skip = nr > RCAP;
+    wave_sync();   // every lane is done with the store's LDS
+    uint32_t R;
+    const uint32_t r0 = wave_excl_scan32(skip ? 1u : nr, R);
+    if (skip) {
+        sp.off[r0] = 0;
+        sp.rel[r0] = ex;
+        sp.flg[r0] = RF_SKIP;
+    }
+    uint32_t acc = 0;
+    for (uint32_t i = 0; !skip && i < nr; i++) {
+        const uint64_t g = reinterpret_cast<const uint64_t *>(ws.rng)[(uint64_t)i * n + t];
+        sp.off[r0 + i] = (uint32_t)g;
+        sp.rel[r0 + i] = ex + acc;
+        sp.flg[r0 + i] = ((uint32_t)(g >> 32) & RUN_INLINE) ? RF_INLINE : 0;
+        acc += (uint32_t)(g >> 32) & RUN_CNT;
+    }
+    if (lane == 0) sp.rel[R] = tot;
+    wave_sync();
+    wave_emit(ix, sp.off, sp.rel, sp.flg, R, base, base + tot, out, cap);
+    wave_sync();   // the span table read before the store's LDS is walked again
+    if (skip) {   // (rare)
+        DirectEmit de{ix.vals, out, pos, cap};
+        match_topic(ix, GlobalSrc{blob}, offs[t], offs[t + 1], st, de);
+    }
 }
 
 // The second (last) launch of a pairs batch: the MID / DEEP lists (topics the
 // walk handed over, walked here from scratch) and the overflow list (span
 // reserved by the walk, values re-walked into it); the grid's last block
 // writes the total, zeroes the value counter and resets the lists
+struct MidLds {
+    uint32_t wid[MID_L * MID_BLOCK];
+    uint32_t pend[(MID_L + 1) * MID_BLOCK];
+    uint8_t len[MID_L * MID_BLOCK];
+};
 __global__ __launch_bounds__(MID_BLOCK) void k_tail_pairs(DevIndex ix, Workspace ws, uint64_t n, const uint8_t *blob,
                                                           const uint64_t *offs, uint8_t *err, uint32_t *pairs,
                                                           uint32_t *out, uint64_t cap, uint32_t mid_grid) {
-    __shared__ uint32_t s_wid[MID_L * MID_BLOCK];
-    __shared__ uint32_t s_pend[(MID_L + 1) * MID_BLOCK];
-    __shared__ uint8_t s_len[MID_L * MID_BLOCK];
+    __shared__ union { MidLds w; SpanLds e; } s;
     static_assert(MID_BLOCK == 64, "one wave per tail block");
     if (blockIdx.x < mid_grid) {
-        LdsStore<MID_L> st{s_wid + threadIdx.x, s_pend + threadIdx.x, s_len + threadIdx.x, MID_BLOCK, 0};
+        LdsStore<MID_L> st{s.w.wid + threadIdx.x, s.w.pend + threadIdx.x, s.w.len + threadIdx.x, MID_BLOCK, 0};
         const uint32_t cnt = ws.list_n[L_MID];
         const uint32_t *lst = ws.lists + (uint64_t)L_MID * n;
         for (uint32_t i0 = blockIdx.x * MID_BLOCK; i0 < cnt; i0 += mid_grid * MID_BLOCK) {
             const uint32_t i = i0 + threadIdx.x;
-            tail_pair(ix, ws, n, blob, offs, i < cnt, i < cnt ? lst[i] : 0, err, pairs, out, cap, i0 / MID_BLOCK, st);
+            tail_pair(ix, ws, n, blob, offs, i < cnt, i < cnt ? lst[i] : 0, err, pairs, out, cap, i0 / MID_BLOCK, st,
+                      s.e);
         }
         const uint32_t co = ws.list_n[L_OVF_MID];
         const uint32_t *lo = ws.lists + (uint64_t)L_OVF_MID * n;
@@ -2141,7 +2156,7 @@ __global__ __launch_bounds__(MID_BLOCK) void k_tail_pairs(DevIndex ix, Workspace
         const uint32_t *lst = ws.lists + (uint64_t)L_DEEP * n;
         for (uint32_t i0 = lane - threadIdx.x; i0 < cnt; i0 += DEEP_LANES) {
             const uint32_t i = i0 + threadIdx.x;
-            tail_pair(ix, ws, n, blob, offs, i < cnt, i < cnt ? lst[i] : 0, err, pairs, out, cap, i0 / 64 + 1, st);
+            tail_pair(ix, ws, n, blob, offs, i < cnt, i < cnt ? lst[i] : 0, err, pairs, out, cap, i0 / 64 + 1, st, s.e);
         }
     }
     // the grid's last block: every block's reservations have returned (their
