@@ -99,7 +99,7 @@ struct Lane {
     int r = 0;                // the replica whose tables this lane's batches read
     hipStream_t s = nullptr;
     bool owned = false;       // stream created by the library (host-API lane)
-    std::atomic<bool> busy{false};   // checked out by a host-API caller (set under ix->mu, cleared without it)
+    bool busy = false;        // checked out by a host-API caller
     bool used = false;        // `done` has been recorded
     bool drained = false;     // `done` was seen complete since it was last recorded (no API call needed)
     hipEvent_t done = nullptr;   // after the lane's last batch: later patches wait for it
@@ -174,7 +174,6 @@ struct tm_index {
     std::atomic<bool> img_dirty{true};
     bool view_ok = false;
     std::condition_variable cv;      // a host lane was released
-    std::atomic<int> lane_waiters{0};   // host_lane callers about to wait on cv (LaneLease)
     int nrep = 1, ngroups = 1;
     Replica rep[MAX_REPLICAS];
     uint64_t rr = 0;                 // round-robin among equally loaded replicas
@@ -1677,11 +1676,6 @@ int make_lane(tm_index *ix, int r, hipStream_t s, bool owned, Lane *&out) {
 // use.  Pending deltas are collected first (pick_copy must know which copies
 // are up to date).  Leaves the calling thread on the lane's device.
 int host_lane(tm_index *ix, std::unique_lock<std::mutex> &g, Lane *&out) {
-    struct Waiting {   // announced before the last look at the lanes (LaneLease)
-        tm_index *ix;
-        bool on = false;
-        ~Waiting() { if (on) ix->lane_waiters.fetch_sub(1); }
-    } waiting{ix};
     for (;;) {
         if (int rc = collect_patch(ix)) return rc;
         int busy[MAX_REPLICAS] = {}, gbusy[MAX_REPLICAS] = {};
@@ -1709,33 +1703,25 @@ int host_lane(tm_index *ix, std::unique_lock<std::mutex> &g, Lane *&out) {
             out->busy = true;
             return TM_OK;
         }
-        if (!waiting.on) {   // announce, then look once more before sleeping
-            waiting.on = true;
-            ix->lane_waiters.fetch_add(1);
-            continue;
-        }
         ix->cv.wait(g);
     }
 }
 
-// releases a checked-out host lane on every exit path.  Without the index
-// lock: a combined launch's leader used to wait 55-85 us for it after its GPU
-// wait just to clear this flag (TM_HOST_TIMING, with a route mirror
-// committing).  A host_lane caller that found no lane announces itself in
-// lane_waiters and looks once more before it sleeps, so either it sees the
-// cleared flag or the release sees it and wakes it under the lock (no lost
-// wake-up).
+// releases a checked-out host lane on every exit path (retaking the lock if
+// the caller dropped it to wait for the GPU).  Round 6 measured releasing it
+// without the lock (an atomic flag, waiters announced): the leader's 55-85 us
+// wait for the lock after its GPU wait went, and 16 concurrent callers lost
+// 10-15 % (4.0-4.1 vs 4.8-4.9e8 topics/s, profiles/r6/lane_release/) -- the
+// lock paces the leaders; kept.
 struct LaneLease {
     tm_index *ix;
     std::unique_lock<std::mutex> &g;
     Lane *ln = nullptr;
     ~LaneLease() {
         if (!ln) return;
-        ln->busy.store(false);
-        if (ix->lane_waiters.load() > 0) {
-            if (!g.owns_lock()) g.lock();
-            ix->cv.notify_all();
-        }
+        if (!g.owns_lock()) g.lock();
+        ln->busy = false;
+        ix->cv.notify_one();
     }
 };
 
