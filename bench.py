@@ -118,6 +118,9 @@ def parse():
                         "group-committing mirror thread (tm_commit) while --concurrency matcher threads run NIF-shaped "
                         "batches, on a second index of the same filters with --writes-copies table copies (0 = skip)")
     p.add_argument("--writes-copies", type=int, default=3)
+    p.add_argument("--small-ticket", type=int, default=1,
+                   help="k_walk_small's blocks take a start-order ticket (TM_DEBUG_SMALL_TICKET; 1 = the library's "
+                        "default, 0 = dispatch order)")
     p.add_argument("--replicas", type=int, default=0,
                    help="replica-topology leg: one process, one tm_create_replicas index (one host image) over N "
                         "device entries, native feeder threads submitting in-place host batches while a syncer thread "
@@ -219,6 +222,7 @@ def main():
     ix = _native.Index(device=local, hint_keys=len(fs), copies=copies)
     if a.small_kernel != "auto":
         ix.debug_set(_native.TM_DEBUG_SMALL_KERNEL, {"wave": _native.SMALL_WAVE, "wave8": _native.SMALL_WAVE8}[a.small_kernel])
+    ix.debug_set(_native.TM_DEBUG_SMALL_TICKET, a.small_ticket)
     chunk = 2_000_000
     for lo in range(0, len(fs), chunk):
         part = fs.slice(lo, min(lo + chunk, len(fs)))
@@ -538,17 +542,18 @@ def main():
         assert rc == 0, rc
         lat_native[f"{lb}_u32_vram_inputs_pairs"] = {"p50_ms": round(out[0], 4), "p99_ms": round(out[1], 4),
                                                      "mean_ms": round(out[2], 4)}
-        # the CSR call with k_walk_small's blocks taking a start-order ticket
-        # (TM_DEBUG_SMALL_TICKET: forward progress of the look-back by
-        # construction, include/tmatch.h) -- what the guarantee costs
-        ix.debug_set(_native.TM_DEBUG_SMALL_TICKET, 1)
+        # the CSR call with k_walk_small's blocks in dispatch order instead of
+        # the start-order ticket (TM_DEBUG_SMALL_TICKET, default 1: forward
+        # progress of the look-back by construction, include/tmatch.h) -- what
+        # the guarantee costs
+        ix.debug_set(_native.TM_DEBUG_SMALL_TICKET, 1 - a.small_ticket)
         out = (ctypes.c_double * 3)()
         rc = hb.tmb_single_ex(ix._h, lb, _native._ptr(sub.blob), _native._ptr(sub.offs), int(hh[-1]) + 4096,
                               a.latency_batches * 5, 5, out)
-        ix.debug_set(_native.TM_DEBUG_SMALL_TICKET, 0)
+        ix.debug_set(_native.TM_DEBUG_SMALL_TICKET, a.small_ticket)
         assert rc == 0, rc
-        lat_native[f"{lb}_u32_vram_inputs_ticket"] = {"p50_ms": round(out[0], 4), "p99_ms": round(out[1], 4),
-                                                      "mean_ms": round(out[2], 4)}
+        lat_native[f"{lb}_u32_vram_inputs_" + ("dispatch_order" if a.small_ticket else "ticket")] = {
+            "p50_ms": round(out[0], 4), "p99_ms": round(out[1], 4), "mean_ms": round(out[2], 4)}
         if a.concurrency > 0:
             conc = []
             if a.combine_leaders is not None:
@@ -925,6 +930,7 @@ def route_write_leg(a, fs, ts, local):
     from emqx_amd import _native
     t = time.time()
     wx = _native.Index(device=local, hint_keys=len(fs), copies=a.writes_copies)
+    wx.debug_set(_native.TM_DEBUG_SMALL_TICKET, a.small_ticket)
     for lo in range(0, len(fs), 2_000_000):
         part = fs.slice(lo, min(lo + 2_000_000, len(fs)))
         wx.apply(np.ones(len(part), np.uint8), part.blob, part.offs, part.vals)

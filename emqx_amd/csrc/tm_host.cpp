@@ -272,7 +272,11 @@ struct tm_index {
     // dbg_lb_launches one-launch batches, and the two-phase path forced for
     // large batches
     LbCtl dbg_lb{LB_SPINS, NONE, 0};
-    uint32_t small_ticket = 0;      // TM_DEBUG_SMALL_TICKET: k_walk_small's blocks take start-order tickets
+    // TM_DEBUG_SMALL_TICKET: k_walk_small's blocks take start-order tickets
+    // (the default since round 6: forward progress by construction, measured
+    // free -- a lone 4k batch 0.038 vs 0.040 ms, concurrent CSR callers
+    // 3.6-3.7 vs 3.3e8, profiles/r6/ticket/)
+    uint32_t small_ticket = 1;
     bool patch_zc = true;           // TM_DEBUG_PATCH_ZC: small patches read in place from pinned memory
     uint64_t dbg_lb_launches = 0;
     bool dbg_phases = false;        // TM_DEBUG_PHASES: small batches on the two-phase path too (tests)

@@ -81,7 +81,8 @@
  * unstarted behind another launch's waiting blocks on another XCD.  So
  * dispatch order alone does not guarantee progress on gfx950; the bounded
  * wait turns such a stall into err 4 (a rerun, then TM_EDEVICE), never a
- * wrong result.  With a start-order ticket (TM_DEBUG_SMALL_TICKET 1) a block
+ * wrong result.  With a start-order ticket (TM_DEBUG_SMALL_TICKET 1, the
+ * default since round 6: measured free) a block
  * takes its index from an atomic counter when it starts, so every block it
  * waits for has started and runs to its publication without waiting for a
  * later one: progress by construction.
@@ -422,8 +423,9 @@ int tm_profile_read(tm_index *h, double *walk_ms, double *batch_ms, uint64_t *ba
  *   TM_DEBUG_CMB_GATHER     (study) microseconds a new combined launch waits
  *                           for the callers between two batches to queue
  *                           theirs (0 = none, the default)
- *   TM_DEBUG_SMALL_TICKET   1: k_walk_small's blocks take a start-order
- *                           ticket (see "Forward progress"); 0: dispatch order
+ *   TM_DEBUG_SMALL_TICKET   1 (default): k_walk_small's blocks take a
+ *                           start-order ticket (see "Forward progress"); 0:
+ *                           dispatch order
  *   TM_DEBUG_PATCH_ZC       1 (default): patches up to 64 KiB are read by the
  *                           patch kernel from mapped pinned memory; 0: copied
  *                           to the device first
