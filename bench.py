@@ -118,6 +118,8 @@ def parse():
                         "group-committing mirror thread (tm_commit) while --concurrency matcher threads run NIF-shaped "
                         "batches, on a second index of the same filters with --writes-copies table copies (0 = skip)")
     p.add_argument("--writes-copies", type=int, default=3)
+    p.add_argument("--cmb-spin", type=int, default=0,
+                   help="microseconds a caller waiting in the combiner spins before it sleeps (TM_DEBUG_CMB_SPIN)")
     p.add_argument("--small-ticket", type=int, default=1,
                    help="k_walk_small's blocks take a start-order ticket (TM_DEBUG_SMALL_TICKET; 1 = the library's "
                         "default, 0 = dispatch order)")
@@ -223,6 +225,8 @@ def main():
     if a.small_kernel != "auto":
         ix.debug_set(_native.TM_DEBUG_SMALL_KERNEL, {"wave": _native.SMALL_WAVE, "wave8": _native.SMALL_WAVE8}[a.small_kernel])
     ix.debug_set(_native.TM_DEBUG_SMALL_TICKET, a.small_ticket)
+    if a.cmb_spin:
+        ix.debug_set(_native.TM_DEBUG_CMB_SPIN, a.cmb_spin)
     chunk = 2_000_000
     for lo in range(0, len(fs), chunk):
         part = fs.slice(lo, min(lo + chunk, len(fs)))
