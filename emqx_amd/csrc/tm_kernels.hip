@@ -2033,10 +2033,33 @@ __global__ __launch_bounds__(WALK_BLOCK, 8) void k_walk_pairs(DevIndex ix, Works
         __builtin_nontemporal_store(pc, reinterpret_cast<uint64_t *>(pairs) + t);
     }
     if (!tot) return;   // (wave-uniform)
-    // the span: one skip range for an overflowed topic, else its ranges
     wave_sync();   // every lane is done with the walk's LDS
-    uint32_t R;
     const bool skip = ovf >= 0;
+    constexpr uint32_t VST = sizeof(s) / 4;   // values the dead walk LDS holds (1,216)
+    if (tot <= VST) {
+        // Most spans (C3: ~540 values per wave, nearly all single-value runs
+        // kept inline): each lane stages its topic's values in LDS at its own
+        // offset, then the wave copies the span out in coalesced non-temporal
+        // dwords -- no range search per quad.  An overflowed topic's positions
+        // hold stale words until k_tail_pairs re-walks it (stream order).
+        uint32_t *sv = reinterpret_cast<uint32_t *>(&s);
+        uint32_t p = ex;
+#pragma unroll
+        for (int i = 0; i < RCAP; i++) {
+            if (skip || (uint32_t)i >= em.nr) break;
+            const uint2 r = em.r[i];
+            if (r.y & RUN_INLINE) { sv[p++] = r.x; continue; }
+#pragma unroll 2
+            for (uint32_t k = 0; k < (r.y & RUN_CNT); k++) sv[p++] = ix.vals[r.x + k];
+        }
+        wave_sync();
+        for (uint32_t i = lane; i < tot; i += 64)
+            if (base + i < cap) __builtin_nontemporal_store(sv[i], out + base + i);
+        return;
+    }
+    // a larger span: its ranges flattened (one skip range for an overflowed
+    // topic) and copied as whole aligned quads
+    uint32_t R;
     const uint32_t r0 = wave_excl_scan32(skip ? (em.cnt ? 1u : 0u) : em.nr, R);
     if (skip && em.cnt) {
         s.e.off[r0] = 0;
