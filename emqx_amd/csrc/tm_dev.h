@@ -172,18 +172,6 @@ struct SmallSeg {
 struct SmallSegs { uint32_t count, pairs; SmallSeg s[SMALL_SEGS]; };
 hipError_t launch_small_segs(const DevIndex &ix, const Workspace &ws, const SmallSegs &sg, bool u32, uint32_t tag,
                              LbCtl lb, int small_kind, hipStream_t s, int *path = nullptr);
-// The combiner's results landed from HBM (TM_DEBUG_CMB_LAND): segment k's hit
-// offsets (n + 1 u32), flags (n) and values (min(hit[n], cap) u32), written by
-// the launch into the lane's HBM arena, copied to the callers' buffers (mapped
-// pinned host memory) in ONE kernel -- 16 B per lane where both sides allow it,
-// whole lines per wave instead of the walk's scattered small PCIe writes.
-struct LandSeg {
-    const uint32_t *hit; const uint8_t *err; const uint32_t *vals;
-    uint32_t *dhit; uint8_t *derr; uint32_t *dvals;
-    uint64_t cap; uint32_t n, pad;
-};
-struct LandSegs { uint32_t count, pad; LandSeg s[SMALL_SEGS]; };
-hipError_t launch_land(const LandSegs &ls, hipStream_t s);
 // The one-launch small batch with 32-bit offsets in and out (hipErrorInvalidValue
 // if small_path_ok refuses the batch), and the 32 <-> 64-bit offset copies
 hipError_t launch_match32(const DevIndex &ix, const Workspace &ws, uint64_t n, const uint8_t *bytes,

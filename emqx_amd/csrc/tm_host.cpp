@@ -116,7 +116,6 @@ struct Lane {
     uint32_t *pin_vals = nullptr, *pin_vals_dev = nullptr; uint64_t pin_vals_cap = 0;
     uint32_t *d_vals = nullptr; uint64_t d_vals_cap = 0;   // sorted output: values sorted in HBM first
     uint64_t *d_o64 = nullptr, *d_h64 = nullptr; uint64_t d_o64_cap = 0, d_h64_cap = 0;   // 32-bit device API: widened offsets
-    uint8_t *d_land = nullptr; uint64_t d_land_cap = 0;   // combined launches' outputs in HBM (TM_DEBUG_CMB_LAND)
 };
 
 // Patch log: a ring of the last PATCH_RING patches (numbered 1, 2, ... in the
@@ -297,7 +296,6 @@ struct tm_index {
     uint64_t cmb_hw_ns = 0;           // when it was last reached
     std::atomic<int> cmb_leaders{CMB_LEADERS};
     std::atomic<int> cmb_gather_us{0};   // TM_DEBUG_CMB_GATHER
-    std::atomic<int> cmb_land{0};        // TM_DEBUG_CMB_LAND
     std::atomic<int> cmb_spin_us{0};     // TM_DEBUG_CMB_SPIN: a waiting caller spins this long before it sleeps
     std::atomic<uint64_t> cmb_launches{0}, cmb_batches{0};
 };
@@ -1653,7 +1651,7 @@ void free_workspace(Workspace &w) {
 
 void free_lane(Lane &l) {
     free_workspace(l.w);
-    void *dv[] = {l.d_in, l.d_res, l.d_vals, l.d_o64, l.d_h64, l.d_land};
+    void *dv[] = {l.d_in, l.d_res, l.d_vals, l.d_o64, l.d_h64};
     for (void *p : dv) if (p) (void)hipFree(p);
     void *pins[] = {l.pin_in, l.pin_out, l.pin_vals};
     for (void *p : pins) if (p) (void)hipHostFree(p);
@@ -2491,9 +2489,10 @@ static int retry_or_fail(tm_index *ix, std::unique_lock<std::mutex> &g, Lane &ln
 // TM_DEBUG_CMB_GATHER (us, study knob, 0 = off): a new leader first waits up to
 // that long while fewer batches are queued or in flight than the recent
 // high-water mark (callers between two batches are about to queue theirs), so
-// launches carry more batches.  TM_DEBUG_CMB_LAND: the launch writes its
-// outputs to the lane's HBM arena and one k_land launch copies them to the
-// callers' buffers (whole lines over PCIe instead of the walk's small writes).
+// launches carry more batches.  (Round 6 measured, and removed, a landing
+// variant: the launch writing its outputs to an HBM arena and one copy kernel
+// moving them to the callers' buffers -- slower than the walk's in-place
+// writes)
 struct SmallReq {
     uint64_t n;
     const uint8_t *db; const uint8_t *dof; uint8_t *dh; uint8_t *de; uint8_t *dv;
@@ -2506,8 +2505,6 @@ struct SmallReq {
 };
 constexpr int CMB_LEGACY = 1;   // (not a TM_ code) the index no longer allows the one-launch path
 constexpr uint64_t CMB_HW_NS = 2000000;   // the high-water mark's memory (2 ms)
-
-static uint64_t land_align(uint64_t b) { return (b + 255) & ~255ull; }
 
 static int run_small_group(tm_index *ix, const std::vector<SmallReq *> &grp, uint64_t *t_sync_end) {
     uint64_t total = 0;
@@ -2524,33 +2521,14 @@ static int run_small_group(tm_index *ix, const std::vector<SmallReq *> &grp, uin
     if ((rc = ensure_ws(ix, total + (uint64_t)SMALL_SEGS * SM_TOPICS, ln))) return rc;
     if (!small_path_ok(dev_view(ix, ln.r), total)) return CMB_LEGACY;
     ix->rep[ln.r].batches++;
-    const bool land = ix->cmb_land.load(std::memory_order_relaxed) != 0;
-    if (land) {   // the arena: each segment's offsets, flags, values (256-B aligned regions)
-        uint64_t need = 0;
-        for (auto *r : grp) need += land_align(4 * (r->n + 1)) + land_align(r->n) + land_align(4 * (r->dv ? r->cap : 0));
-        if ((rc = grow_dev(ix, s, ln.d_land, ln.d_land_cap, need))) return rc;
-    }
     SmallSegs sg{};
-    LandSegs ls{};
-    sg.count = ls.count = (uint32_t)grp.size();
+    sg.count = (uint32_t)grp.size();
     sg.pairs = grp[0]->pairs ? 1u : 0u;
-    if (sg.pairs && land) return fail(ix, TM_EINVAL, "tm_match_batch32_pairs: TM_DEBUG_CMB_LAND takes CSR batches only");
-    uint64_t at = 0;
     for (size_t k = 0; k < grp.size(); k++) {
         const SmallReq &r = *grp[k];
         const uint64_t vcap = r.dv ? r.cap : 0;
-        if (land) {
-            uint8_t *hh = ln.d_land + at, *he = hh + land_align(4 * (r.n + 1)), *hv = he + land_align(r.n);
-            at += land_align(4 * (r.n + 1)) + land_align(r.n) + land_align(4 * vcap);
-            sg.s[k] = SmallSeg{r.db ? r.db : r.dof, r.dof, hh, he, r.dv ? reinterpret_cast<uint32_t *>(hv) : nullptr,
-                               vcap, (uint32_t)r.n, 0};
-            ls.s[k] = LandSeg{reinterpret_cast<const uint32_t *>(hh), he, reinterpret_cast<const uint32_t *>(hv),
-                              reinterpret_cast<uint32_t *>(r.dh), r.de, reinterpret_cast<uint32_t *>(r.dv), vcap,
-                              (uint32_t)r.n, 0};
-        } else {
-            sg.s[k] = SmallSeg{r.db ? r.db : r.dof, r.dof, r.dh, r.de, reinterpret_cast<uint32_t *>(r.dv), vcap,
-                               (uint32_t)r.n, 0};
-        }
+        sg.s[k] = SmallSeg{r.db ? r.db : r.dof, r.dof, r.dh, r.de, reinterpret_cast<uint32_t *>(r.dv), vcap,
+                           (uint32_t)r.n, 0};
     }
     const uint64_t tc = g_cmb_timing ? ns_now() : 0;
     for (int tries = 0;; tries++) {
@@ -2559,7 +2537,6 @@ static int run_small_group(tm_index *ix, const std::vector<SmallReq *> &grp, uin
         if ((rc = next_tag(ix, ln, s, tag))) return rc;
         int path = PATH_SMALL;
         HIPCHK(ix, launch_small_segs(d, ln.w, sg, true, tag, next_lb(ix), ix->small_kind, s, &path));
-        if (land) HIPCHK(ix, launch_land(ls, s));
         ix->path_batches[path]++;
         ix->cmb_launches++;
         ix->cmb_batches += grp.size();
@@ -3091,7 +3068,7 @@ int tm_debug_set(tm_index *ix, uint32_t key, uint64_t value) {
     case TM_DEBUG_PHASES: ix->dbg_phases = value != 0; break;
     case TM_DEBUG_COMBINE: ix->cmb_leaders = value > 16 ? 16 : (int)value; break;
     case TM_DEBUG_CMB_GATHER: ix->cmb_gather_us = value > 1000 ? 1000 : (int)value; break;
-    case TM_DEBUG_CMB_LAND: ix->cmb_land = value != 0; break;
+    case TM_DEBUG_CMB_LAND: if (value) return fail(ix, TM_EINVAL, "tm_debug_set: TM_DEBUG_CMB_LAND was removed"); break;
     case TM_DEBUG_CMB_SPIN: ix->cmb_spin_us = value > 1000 ? 1000 : (int)value; break;
     case TM_DEBUG_SMALL_TICKET: ix->small_ticket = value != 0; break;
     case TM_DEBUG_PATCH_ZC: ix->patch_zc = value != 0; break;
@@ -3115,7 +3092,7 @@ int tm_debug_get(tm_index *ix, uint32_t key, uint64_t *value) {
     case TM_DEBUG_PATH_LANE: *value = ix->path_batches[PATH_LANE].load(); break;
     case TM_DEBUG_COMBINE: *value = (uint64_t)ix->cmb_leaders.load(); break;
     case TM_DEBUG_CMB_GATHER: *value = (uint64_t)ix->cmb_gather_us.load(); break;
-    case TM_DEBUG_CMB_LAND: *value = (uint64_t)ix->cmb_land.load(); break;
+    case TM_DEBUG_CMB_LAND: *value = 0; break;
     case TM_DEBUG_CMB_SPIN: *value = (uint64_t)ix->cmb_spin_us.load(); break;
     case TM_DEBUG_COMMITS: *value = ix->commits.load(); break;
     case TM_DEBUG_SMALL_TICKET: *value = ix->small_ticket; break;

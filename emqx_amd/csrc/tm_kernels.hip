@@ -2473,28 +2473,6 @@ __global__ __launch_bounds__(256) void k_copy_values(const uint64_t *hit, uint64
         dst[i] = src[i];
 }
 
-// The combiner's landing copy (launch_land): every lane moves 16 B per step
-// when source and destination are both 16-B aligned (the arena's regions are;
-// tm_host_alloc buffers are), else bytes.  Grid: x strides one segment, y = segment.
-__device__ __forceinline__ void land_copy(uint8_t *d, const uint8_t *s, uint64_t nb, uint64_t i0, uint64_t st) {
-    if ((((uintptr_t)d | (uintptr_t)s) & 15) == 0) {
-        const uint64_t q = nb >> 4;
-        for (uint64_t i = i0; i < q; i += st) reinterpret_cast<uint4 *>(d)[i] = ld4_once(s + 16 * i);
-        for (uint64_t i = (q << 4) + i0; i < nb; i += st) d[i] = s[i];
-    } else {
-        for (uint64_t i = i0; i < nb; i += st) d[i] = s[i];
-    }
-}
-
-__global__ __launch_bounds__(256) void k_land(LandSegs ls) {
-    const LandSeg &S = ls.s[blockIdx.y];
-    const uint64_t tot = S.hit[S.n], nv = tot < S.cap ? tot : S.cap;
-    const uint64_t i0 = (uint64_t)blockIdx.x * 256 + threadIdx.x, st = (uint64_t)gridDim.x * 256;
-    land_copy(reinterpret_cast<uint8_t *>(S.dhit), reinterpret_cast<const uint8_t *>(S.hit), 4ull * (S.n + 1), i0, st);
-    land_copy(S.derr, S.err, S.n, i0, st);
-    if (S.dvals) land_copy(reinterpret_cast<uint8_t *>(S.dvals), reinterpret_cast<const uint8_t *>(S.vals), 4 * nv, i0, st);
-}
-
 // ------------------------------------------------------------ launchers
 
 static inline uint32_t blocks_for(uint64_t n, uint32_t per) { return (uint32_t)((n + per - 1) / per); }
@@ -2636,12 +2614,6 @@ hipError_t launch_small_segs(const DevIndex &ix, const Workspace &ws, const Smal
     else
         launch_small_kernel<uint64_t>(w, blocks, ix, ws, F.n, F.blob, static_cast<const uint64_t *>(F.offs), F.err,
                                       static_cast<uint64_t *>(F.hit), F.out, F.cap, tg, lb, sg, s);
-    return hipGetLastError();
-}
-
-hipError_t launch_land(const LandSegs &ls, hipStream_t s) {
-    if (!ls.count || ls.count > (uint32_t)SMALL_SEGS) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_land, dim3(32, ls.count), dim3(256), 0, s, ls);
     return hipGetLastError();
 }
 

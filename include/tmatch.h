@@ -431,9 +431,9 @@ int tm_profile_read(tm_index *h, double *walk_ms, double *batch_ms, uint64_t *ba
  *                           to the device first
  *   TM_DEBUG_CMB_SPIN       microseconds a caller waiting in the combiner spins
  *                           before it sleeps (0: sleeps at once)
- *   TM_DEBUG_CMB_LAND       (study) 1: a combined launch writes its outputs to
- *                           HBM and one copy kernel lands them in the callers'
- *                           buffers (0 = the kernel writes them in place)
+ *   TM_DEBUG_CMB_LAND       retired (round 6: the combined launch's outputs
+ *                           landed from HBM by a copy kernel, measured slower
+ *                           and removed): 0 only, TM_EINVAL otherwise
  * tm_debug_get: those settings; TM_DEBUG_COMMITS / _COMMIT_WAITS / _COMMIT_FORCED:
  * tm_commit patches, those that waited for a copy to drain, and those
  * published without an idle copy; TM_DEBUG_FAILED_BATCHES (one-launch batches whose look-back

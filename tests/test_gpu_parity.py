@@ -1242,7 +1242,7 @@ def test_concurrent_callers_see_consistent_snapshots(torch_dev, copies):
 
 @pytest.mark.parametrize("kind,copies,leaders,gather,land,ticket,spin", [
     ("wave", 1, 4, 0, 0, 0, 0), ("wave8", 1, 4, 0, 0, 0, 0), ("auto", 2, None, 0, 0, 0, 0), ("auto", 2, 2, 0, 0, 0, 0),
-    ("auto", 1, 4, 30, 1, 0, 0), ("auto", 2, 1, 30, 0, 0, 0), ("auto", 2, 2, 0, 1, 0, 0), ("auto", 2, 2, 0, 0, 1, 0),
+    ("auto", 1, 4, 30, 0, 0, 0), ("auto", 2, 1, 30, 0, 0, 0), ("auto", 2, 2, 0, 0, 0, 200), ("auto", 2, 2, 0, 0, 1, 0),
     ("auto", 2, 2, 0, 0, 1, 40)])
 def test_combined_callers_with_deltas_see_snapshots_and_never_fail(torch_dev, kind, copies, leaders, gather, land,
                                                                    ticket, spin):
@@ -1251,8 +1251,10 @@ def test_combined_callers_with_deltas_see_snapshots_and_never_fail(torch_dev, ki
     host_array buffers, what the NIF's dirty schedulers do) through the
     host-batch combiner at 4 leaders (the default; and at 2 and 1) -- shared
     k_walk_small launches with a segment table; with a gather window
-    (TM_DEBUG_CMB_GATHER) and with the outputs landed from HBM by k_land
-    (TM_DEBUG_CMB_LAND) -- while the main thread applies 16 delta
+    (TM_DEBUG_CMB_GATHER), with the start-order ticket and with waiting
+    callers spinning (TM_DEBUG_CMB_SPIN; the round-5 landing variant,
+    TM_DEBUG_CMB_LAND, was removed in round 6: land is 0) -- while the main
+    thread applies 16 delta
     epochs.  Every
     batch equals the oracle after exactly the epochs its probe topic saw, a
     thread never goes back in time, and no batch's look-back wait expired:
@@ -2507,12 +2509,12 @@ def test_router_boot_1m_routes_and_node_down_cleanup(torch_dev):
     assert r.mirror_keys() == len(filter_rows) - sum(1 for t, _ in dead if tfilter(t) is not False)
 
 
-@pytest.mark.parametrize("kind,land,ticket", [("wave", 0, 0), ("wave8", 0, 0), ("auto", 1, 0), ("auto", 0, 1)])
+@pytest.mark.parametrize("kind,land,ticket", [("wave", 0, 0), ("wave8", 0, 0), ("auto", 0, 0), ("auto", 0, 1)])
 def test_combined_small_batches_equal_single_launches(torch_dev, kind, land, ticket):
     """The host-batch combiner (tm_host.cpp small_combined): concurrent callers'
     in-place 32-bit batches of 1 to 20k topics run as shared k_walk_small
-    launches with a segment table (land: outputs written to HBM, then landed
-    by k_land) -- each caller's hit offsets,
+    launches with a segment table (land: 0 -- the landing variant was removed
+    in round 6) -- each caller's hit offsets,
     values and flags identical to its batch run alone (combiner off) and to
     the oracle; a badarg topic stays in its own slot; a forced look-back
     failure reruns the whole launch once (every caller still exact)."""

@@ -1,5 +1,7 @@
 #!/usr/bin/env python3
-"""Combiner sweep (study, round 6; not product code): native caller threads of
+"""(Round 6 close: the library's TM_DEBUG_CMB_LAND variant was removed after this sweep measured it slower;
+land=1 passes now fail with TM_EINVAL -- run them on the commit that had it, a5371f1.)
+Combiner sweep (study, round 6; not product code): native caller threads of
 4k-topic C3 batches through tm_match_batch32_ex (the NIF's call; mode 5 =
 inputs in TM_ALLOC_VRAM memory, mode 4 = pinned host memory) over combiner
 leaders x gather window (TM_DEBUG_CMB_GATHER, us) x landing from HBM
