@@ -3142,3 +3142,48 @@ def test_pairs_device_edge_cases(torch_dev):
                 k = min(c, cap - p)
                 assert np.array_equal(v2[p:p + k], ovals[int(ohit[i]):int(ohit[i]) + k])
     assert_pairs_same(torch_dev, ix, o, ts)
+
+
+@pytest.mark.parametrize("copies,nstreams", [(1, 2), (2, 2), (3, 3)])
+def test_pairs_batches_on_streams_see_patches_in_order(torch_dev, copies, nstreams):
+    """The headline's form under churn: device pairs batches on several
+    streams, deltas applied between them (with 1-3 copies of the tables), each
+    batch's lists exact against the oracle after exactly the deltas applied
+    before it was queued -- the region counters and tail lists of every
+    stream's workspace reset between its batches."""
+    torch = torch_dev
+    nf = 30_000
+    fs = wl.filters(5, nf)
+    ix = _native.Index(copies=copies)
+    ix.apply(np.ones(len(fs), np.uint8), fs.blob, fs.offs, fs.vals)
+    o = oracle_of(fs)
+    ts = wl.topics(5, nf, 40_000)
+    dev = torch.device("cuda:0")
+    d_blob = torch.from_numpy(ts.blob.copy()).to(dev)
+    d_offs = torch.from_numpy(ts.offs.view(np.int64).copy()).to(dev)
+    streams = [torch.cuda.Stream() for _ in range(nstreams)]
+    n = len(ts)
+    results = []
+    for k in range(4 if copies == 1 else 9):
+        d = wl.deltas(nf, k * 3_000, 3_000 if k % 3 else 40)
+        ix.apply(d.flags, d.blob, d.offs, d.vals)
+        o.apply(d.flags, d.blob, d.offs, d.vals)
+        o.prepare()
+        cnt, _, ohit, ovals = o.match_batch(ts.blob, ts.offs)
+        cap = int(ohit[-1]) + 4096 * int(max(int(np.max(cnt)), 1))
+        pairs = torch.zeros(2 * n + 2, dtype=torch.int32, device=dev)
+        err = torch.zeros(n, dtype=torch.uint8, device=dev)
+        out = torch.zeros(cap, dtype=torch.int32, device=dev)
+        ix.match_batch_dev_pairs(n, d_blob.data_ptr(), d_offs.data_ptr(), pairs.data_ptr(), out.data_ptr(), cap,
+                                 err.data_ptr(), streams[k % nstreams].cuda_stream)
+        results.append((pairs, out, err, cnt, ohit, ovals, cap))
+    torch.cuda.synchronize()
+    for pairs, out, err, cnt, ohit, ovals, cap in results:
+        p = pairs.cpu().numpy().view(np.uint32)
+        v = out.cpu().numpy().view(np.uint32)
+        assert int(p[2 * n]) == int(ohit[-1]) and int(p[2 * n + 1]) <= cap
+        assert not err.cpu().numpy().any()
+        pr = p[:2 * n].reshape(n, 2).astype(np.int64)
+        assert np.array_equal(pr[:, 1], np.maximum(cnt, 0))
+        for i in range(0, n, 7):   # (a sample of the topics per batch: 9 batches x 40k topics)
+            assert np.array_equal(v[pr[i, 0]:pr[i, 0] + pr[i, 1]], ovals[int(ohit[i]):int(ohit[i + 1])]), i
