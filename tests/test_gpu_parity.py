@@ -3187,3 +3187,27 @@ def test_pairs_batches_on_streams_see_patches_in_order(torch_dev, copies, nstrea
         assert np.array_equal(pr[:, 1], np.maximum(cnt, 0))
         for i in range(0, n, 7):   # (a sample of the topics per batch: 9 batches x 40k topics)
             assert np.array_equal(v[pr[i, 0]:pr[i, 0] + pr[i, 1]], ovals[int(ohit[i]):int(ohit[i + 1])]), i
+
+
+def test_pairs_regions_under_a_tight_capacity(torch_dev):
+    """A batch large enough for several regions (120k topics: 14) with cap =
+    the exact total: spans may not all fit (regions leave gaps), and the
+    library says so -- the extent exceeds cap exactly when some topic's span
+    does; every value that landed below cap is the oracle's, and the next
+    batch on the workspace (ample cap) is exact again (counters reset)."""
+    torch = torch_dev
+    nf = 200_000
+    fs = wl.filters(3, nf)
+    ix, o = gpu_index(fs), oracle_of(fs)
+    ts = wl.topics(3, nf, 120_000)
+    cnt, _, ohit, ovals = o.match_batch(ts.blob, ts.offs)
+    total = int(ohit[-1])
+    pr, t2, x2, v2, _ = pairs_batch(torch, ix, ts, cap=total)
+    assert t2 == total
+    ends = pr[:, 0] + pr[:, 1]
+    assert (x2 > total) == bool((ends > total).any())
+    for i in range(0, len(ts), 5):
+        p, c = int(pr[i, 0]), int(pr[i, 1])
+        k = max(0, min(c, total - p))
+        assert np.array_equal(v2[p:p + k], ovals[int(ohit[i]):int(ohit[i]) + k]), i
+    assert_pairs_same(torch, ix, o, ts)
