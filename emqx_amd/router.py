@@ -185,20 +185,13 @@ class Router:
         each key reconciled against the table, all of them shipped as ONE
         device call before returning (commit: tm_commit, the hook's group
         commit -- published on a table copy no publish batch is reading)."""
-        n = 0
         with self._tables:   # the table's state at reconcile time
             present = [k in self._filters for k in keys]
-        for k, here in zip(keys, present):
-            if here:
-                self._mirror.insert_key(k, [])
-            else:
-                self._mirror.delete_key(k)
-            n += 1
-        if n:
-            if commit:
-                self._mirror.flush(commit=True)
-            else:
-                self._mirror.flush()
+        if keys:
+            # queued and shipped under one hold of the mirror's lock: a publish
+            # batch's flush cannot ship them as a plain delta in between
+            # (Tab.sync_keys -- the read-your-writes race of round 6)
+            self._mirror.sync_keys(keys, present, commit=commit)
             self.mirror_calls += 1
 
     def _hook(self, keys):

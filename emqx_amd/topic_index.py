@@ -80,20 +80,39 @@ class Tab:
         """Ship the queued deltas as ONE call (commit: tm_commit -- the route
         mirror's group commit, which no batch waits for on the GPU)."""
         with self._lock:
-            if not self._ops:
-                return
-            ops = np.array([o[0] for o in self._ops], dtype=np.uint8)
-            blob, offs = _native.pack_strings([o[1] for o in self._ops])
-            vals = np.array([o[2] for o in self._ops], dtype=np.uint32)
-            flags = np.array([o[3] for o in self._ops], dtype=np.uint8)
-            self._ops = []
-            epoch = (self._index.apply(ops, blob, offs, vals, flags, commit=True) if commit
-                     else self._index.apply(ops, blob, offs, vals, flags))
-            # the deletes just shipped are visible from `epoch` on: their u32s
-            # wait until no reader that began earlier is running
-            for kid in self._released:
-                self._quarantine.append((epoch, kid))
-            self._released = []
+            self._flush_locked(commit)
+
+    def sync_keys(self, keys, present, commit: bool = False):
+        """Reconcile `keys` (present[i]: the key is in the table) and ship the
+        delta in ONE call, the queueing and the shipping under one hold of the
+        lock: a reader's flush (match_kids) cannot take these ops in between
+        and ship them as a plain tm_apply_deltas, which a tm_commit running
+        meanwhile would publish only with itself (include/tmatch.h) -- the
+        writer's commit would then find nothing to ship and return before its
+        keys were readable (the router's read-your-writes)."""
+        with self._lock:
+            for k, here in zip(keys, present):
+                if here:
+                    self._insert_locked(k, [])
+                else:
+                    self._delete_locked(k)
+            self._flush_locked(commit)
+
+    def _flush_locked(self, commit: bool):
+        if not self._ops:
+            return
+        ops = np.array([o[0] for o in self._ops], dtype=np.uint8)
+        blob, offs = _native.pack_strings([o[1] for o in self._ops])
+        vals = np.array([o[2] for o in self._ops], dtype=np.uint32)
+        flags = np.array([o[3] for o in self._ops], dtype=np.uint8)
+        self._ops = []
+        epoch = (self._index.apply(ops, blob, offs, vals, flags, commit=True) if commit
+                 else self._index.apply(ops, blob, offs, vals, flags))
+        # the deletes just shipped are visible from `epoch` on: their u32s
+        # wait until no reader that began earlier is running
+        for kid in self._released:
+            self._quarantine.append((epoch, kid))
+        self._released = []
 
     def _take_kid(self) -> int:
         if not self._free and self._quarantine:
@@ -108,23 +127,29 @@ class Tab:
     # -- table operations (one writer at a time, as the reference's callers)
     def insert_key(self, key, record):
         with self._lock:
-            if key not in self._records:
-                self._sorted = None
-                kid = self._take_kid()
-                self._keys[kid] = key
-                self._kid[key] = kid
-                self._queue(_native.TM_OP_INSERT, key, kid)
-            self._records[key] = record
+            self._insert_locked(key, record)
 
     def delete_key(self, key):
         with self._lock:
-            if key in self._records:
-                self._sorted = None
-                kid = self._kid.pop(key)
-                del self._records[key]
-                self._queue(_native.TM_OP_DELETE, key, kid)
-                self._keys[kid] = None
-                self._released.append(kid)
+            self._delete_locked(key)
+
+    def _insert_locked(self, key, record):
+        if key not in self._records:
+            self._sorted = None
+            kid = self._take_kid()
+            self._keys[kid] = key
+            self._kid[key] = kid
+            self._queue(_native.TM_OP_INSERT, key, kid)
+        self._records[key] = record
+
+    def _delete_locked(self, key):
+        if key in self._records:
+            self._sorted = None
+            kid = self._kid.pop(key)
+            del self._records[key]
+            self._queue(_native.TM_OP_DELETE, key, kid)
+            self._keys[kid] = None
+            self._released.append(kid)
 
     def attach(self, rows, batch_size: int = 1000) -> int:
         """Boot the device mirror from an existing table (emqx_topic_index_gpu:

@@ -30,6 +30,14 @@ class FakeMirror:
         self.flushes += 1
         self.pending = []
 
+    def sync_keys(self, keys, present, commit=False):
+        for k, here in zip(keys, present):
+            if here:
+                self.insert_key(k, [])
+            else:
+                self.delete_key(k)
+        self.flush(commit)
+
     def attach(self, rows, batch_size):
         calls, n = 0, 0
         for key, rec in rows:
@@ -193,3 +201,50 @@ def test_killed_mirror_is_never_served_and_reboots_from_the_tables():
     assert mirrors[0].keys == set(r._filters) == {make_key(b"b/#", "n2"), make_key(b"c/+", "n1"),
                                                   make_key(b"d/+/#", "n3")}
     assert r.pending_events() == 0
+
+
+class _RecordingIndex:
+    """_native.Index's write side, recording which call shipped each key."""
+
+    def __init__(self):
+        import threading
+        self.calls, self._e, self._mu = [], 0, threading.Lock()
+
+    def apply(self, ops, blob, offs, vals, flags, commit=False):
+        with self._mu:
+            self._e += 1
+            self.calls.append((commit, [bytes(blob[offs[i]:offs[i + 1]]) for i in range(len(ops))]))
+            return self._e
+
+    def epoch(self):
+        return self._e, self._e
+
+
+def test_commit_sync_is_not_shipped_by_a_readers_flush():
+    """Round-6 read-your-writes race: the group commit queued its keys, a
+    publish batch's flush (match_kids) shipped them as a plain delta, and the
+    commit found nothing to ship -- its writers read before the patch was
+    published.  Tab.sync_keys queues and ships under one lock hold, so every
+    key a commit reconciles goes out in a commit call."""
+    import threading
+    from emqx_amd import topic_index as ti
+    ix = _RecordingIndex()
+    tab = ti.Tab(index=ix)
+    stop = threading.Event()
+
+    def reader():
+        while not stop.is_set():
+            tab.flush()
+
+    th = [threading.Thread(target=reader) for _ in range(2)]
+    for t in th:
+        t.start()
+    try:
+        for i in range(2000):
+            tab.sync_keys([make_key(f"wr/{i}/+".encode(), "n1")], [True], commit=True)
+    finally:
+        stop.set()
+        for t in th:
+            t.join()
+    shipped = [(c, k) for c, ks in ix.calls for k in ks]
+    assert len(shipped) == 2000 and all(c for c, _ in shipped)
